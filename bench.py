@@ -1,0 +1,219 @@
+#!/usr/bin/env python
+"""Throughput of the batch candidate-scoring hot path on MI355X.
+
+Workload (BASELINE.json configs[1], "C2" in SURVEY.md §8(d)):
+  Rosenbrock-64 space: 64 FloatParameters named 0..63 in [-1000, 1000]
+  DE-Alt proposal (cr = 0.2, n_cross = 1, F = U/2 + 0.5) over a population of
+  m candidates per GPU, hash_config + dedup against the history,
+  GP surrogate n = 1024 (SE-ARD, ell = 0.2, sf2 = 1, sn2 = 1e-6) refit every
+  round, EI (xi = 0) + top-k (k = 256), fp64.
+One step = one round: GP fit + propose + hash + dedup + encode + GP score +
+top-k (+ all-gather merge of the local top-k over RCCL when N > 1).
+
+    python bench.py [--gpus N --steps K --warmup W]
+
+N > 1 is launched by torch.distributed.run (one rank per GPU, backend nccl =
+RCCL); each rank scores its own shard of global candidate indices (weak
+scaling: m per GPU is fixed) and the local top-k lists are all-gathered and
+merged.  Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+# MI355X peaks (MI355X_MICROARCH.md chip table; FP64 matrix = FP64 vector
+# spec 78.6 TF -- SURVEY.md §8(d))
+PEAK_FP64_TFLOPS = 78.6
+PEAK_HBM_GBS = 8000.0
+
+
+def rosenbrock_decoded(X01):
+    xs = X01 * 2000.0 - 1000.0
+    return np.sum(100.0 * (xs[:, 1:] - xs[:, :-1] ** 2) ** 2 + (xs[:, :-1] - 1.0) ** 2, axis=1)
+
+
+def training_set(n, d, seed):
+    rng = np.random.default_rng(seed)
+    X = rng.uniform(size=(n, d))
+    return X, rosenbrock_decoded(X)
+
+
+def cpu_baseline(m_sample, n, d, k, seed=1):
+    """The oracle (CPU restatement of the reference path) on a bounded sample,
+    single-threaded like the reference search loop (api.py:428-446)."""
+    try:
+        from threadpoolctl import threadpool_limits
+    except Exception:  # pragma: no cover
+        threadpool_limits = None
+    from oracle import de as ode
+    from oracle import gp as ogp
+    from oracle import hashing as oh
+    from oracle import select as osel
+    from oracle.space import FLOAT, Param, features
+
+    space = [Param(i, FLOAT, -1000.0, 1000.0) for i in range(d)]
+    X, y = training_set(n, d, seed + 100)
+    ctx = threadpool_limits(limits=1) if threadpool_limits else None
+    if ctx:
+        ctx.__enter__()
+    try:
+        pop = ode.population_init(space, m_sample, seed)
+        t0 = time.perf_counter()
+        g = ogp.GP(X, y, lengthscale=0.2, sigma_f2=1.0, sigma_n2=1e-6)
+        trial = ode.propose_de_vec(space, pop, seed, 0, 0, m_sample, 0.2, 1)
+        hx = [oh.hash_config(space, list(trial[:, j])) for j in range(m_sample)]
+        dup = osel.dedup(hx, set())
+        mu, var = g.posterior(features(space, trial).T)
+        ei = ogp.acquisition(mu, var, g.f_best)
+        osel.topk(list(ei), k, dup=dup)
+        dt = time.perf_counter() - t0
+    finally:
+        if ctx:
+            ctx.__exit__(None, None, None)
+    return {"value": m_sample / dt, "unit": "candidates/s", "cores": 1, "kind": "port",
+            "sample": f"oracle/ (NumPy+hashlib restatement), {m_sample} R64 candidates, n={n} GP fit + DE + "
+                      f"hash_config + dedup + posterior + EI + top-{k}, 1 thread, {dt:.2f} s"}
+
+
+def load_traffic(kernel_key):
+    path = os.path.join(ROOT, "profiles", "pmc_summary.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        return d.get(kernel_key, {}).get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--m", type=int, default=1 << 20, help="candidates per GPU per round")
+    ap.add_argument("--n", type=int, default=1024, help="GP training points")
+    ap.add_argument("--d", type=int, default=64)
+    ap.add_argument("--k", type=int, default=256)
+    ap.add_argument("--cpu-sample", type=int, default=8192)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    from uptune_amd.engine import BatchEngine
+    from uptune_amd.manipulator import ConfigurationManipulator, FloatParameter
+
+    m, n, d, k = args.m, args.n, args.d, args.k
+    manip = ConfigurationManipulator([FloatParameter(i, -1000.0, 1000.0) for i in range(d)])
+    eng = BatchEngine(manip, device=local, seed=1)
+    npop = m * world                       # replicated population, deterministic init on every rank
+    eng.population_init(npop)
+    eng.history_reset(0)
+    X, y = training_set(n, d, 101)
+    cand_base = rank * m
+    acq = eng.acq("ei", xi=0.0)
+
+    def step(r):
+        eng.gp_fit(X, y, lengthscale=0.2, sigma_f2=1.0, sigma_n2=1e-6)
+        idx, top, dig, _ = eng.score_round_de(m, k, round_=r, cand_base=cand_base, cr=0.2, n_cross=1, acq=acq,
+                                              want_values=False)
+        if world > 1:
+            gi = [torch.empty_like(idx) for _ in range(world)]
+            gs = [torch.empty_like(top) for _ in range(world)]
+            gd = [torch.empty_like(dig) for _ in range(world)]
+            dist.all_gather(gi, idx)
+            dist.all_gather(gs, top)
+            dist.all_gather(gd, dig)
+            ai, asc, ad = torch.cat(gi), torch.cat(gs), torch.cat(gd).contiguous()
+            dup = eng.dedup(ad)                       # cross-shard duplicates: first (smallest index) wins
+            dup = torch.where(ai < 0, torch.ones_like(dup), dup)
+            pos, top = eng.topk(asc, k, dup=dup)
+            idx = torch.where(pos >= 0, ai[pos.clamp(min=0)], pos)
+        return idx, top
+
+    for w in range(args.warmup):
+        step(w)
+    torch.cuda.synchronize()
+
+    eng.set_timing(True)
+    stage_ms = {}
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for s in range(args.steps):
+        idx, top = step(args.warmup + s)
+        for st in ("propose", "hash", "dedup", "encode", "kstar", "var", "finalize", "topk"):
+            try:
+                stage_ms.setdefault(st, []).append(eng.stage_time(st))
+            except Exception:
+                pass
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    eng.set_timing(False)
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    ms_per_step = elapsed * 1000.0 / args.steps
+    value = world * m / (elapsed / args.steps)
+    stages = {st: float(np.mean(v)) for st, v in stage_ms.items()}
+    # dominant kernel: the variance GEMM  V = L^-1 K*^T  (fp64 MFMA)
+    var_ms = stages.get("var")
+    flops_var = float(m) * n * (n + 1)       # algorithmic: lower-triangular n x n times k* per candidate
+    achieved = flops_var / (var_ms * 1e-3) / 1e12 if var_ms else None
+    traffic = load_traffic("var")
+    result = {
+        "metric": "candidate configs scored/sec (GP-EI + top-k)",
+        "value": value,
+        "unit": "candidates/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (Rosenbrock-64 objective on uniform training points; DE population random-init)",
+        "config": {"workload": "C2 R64: DE-Alt + hash_config + dedup + GP-EI n=1024 + top-256",
+                   "candidates_per_gpu": m, "gp_n": n, "dims": d, "k": k, "parallelism": f"dp{world}"},
+        "stage_ms": stages,
+        "roofline": {"bound": "mfma", "kernel": "k_gp_gemm<1> (var: L^-1 K*^T, fp64 MFMA 16x16x4)",
+                     "achieved": achieved, "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
+                     "frac": (achieved / PEAK_FP64_TFLOPS) if achieved else None, "traffic": traffic},
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        try:
+            result["cpu_baseline"] = cpu_baseline(args.cpu_sample, n, d, k)
+        except Exception as ex:  # keep the GPU number even if the baseline fails
+            result["cpu_baseline"] = {"error": repr(ex)}
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,192 @@
+/*
+ * uthot.h -- C ABI of libuthot.so, the gfx950 (MI355X) batch candidate
+ * proposal + scoring library behind uptune_amd.
+ *
+ * Drop-in boundary.  The reference runs this path one configuration at a
+ * time inside the Python search loop:
+ *   SearchTechnique.desired_configuration()   opentuner/search/technique.py:113-121
+ *   DifferentialEvolution.create_new_configuration
+ *                                             opentuner/search/differentialevolution.py:105-129
+ *   HybridParticle.move / op3_swarm           opentuner/search/pso.py:70-77
+ *   EvolutionaryTechnique.mutation            opentuner/search/evolutionarytechniques.py:51-61
+ *   ConfigurationManipulator.hash_config      opentuner/search/manipulator.py:233-243
+ *   SearchDriver.get_configuration/has_results opentuner/search/driver.py:157-158,253-258
+ *   ParallelTuning.unique / hash_cfg          python/uptune/api.py:254-288
+ * Each entry point below replaces one of those per-candidate Python calls
+ * with one batched, stream-ordered call over m candidates.
+ *
+ * Conventions
+ *   - every function returns 0 on success or a negative UT_E* code; the
+ *     message is available from ut_last_error(ctx);
+ *   - pointer arguments are DEVICE pointers unless the name ends in _host;
+ *   - work is enqueued on the context's HIP stream (ut_set_stream); results
+ *     are valid once that stream is synchronised;
+ *   - SoA value arrays are column-per-parameter: value of param p for
+ *     candidate i lives at values[p * ld + i] (f64 for every kind: FLOAT raw
+ *     value, INT/LOGINT raw integer, POW2 raw power of two, BOOL 0/1,
+ *     ENUM option index);
+ *   - digests are 8 big-endian uint32 words (= sha256().digest()) per
+ *     candidate, candidate-major ([m][8]);
+ *   - candidate indices are GLOBAL (cand_base + i), so random streams and
+ *     tie-breaks do not depend on how a pool is sharded over GPUs.
+ *   - one context per host thread.
+ */
+#ifndef UTHOT_H
+#define UTHOT_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct ut_ctx ut_ctx;
+
+enum {
+  UT_OK = 0,
+  UT_EINVAL = -1,      /* bad argument */
+  UT_EHIP = -2,        /* HIP runtime error */
+  UT_ENOSPACE = -3,    /* ut_space_define not called */
+  UT_EUNSUPPORTED = -4,
+  UT_ENOTPD = -5,      /* GP kernel matrix not positive definite */
+  UT_ENOMEM = -6
+};
+
+/* parameter kinds: manipulator.py:651-1356 (the kinds create_params builds,
+ * python/uptune/api.py:179-199) */
+enum {
+  UT_FLOAT = 0,  /* FloatParameter        manipulator.py:703-744 */
+  UT_INT = 1,    /* IntegerParameter      manipulator.py:651-700 */
+  UT_LOGINT = 2, /* LogIntegerParameter   manipulator.py:781-797 */
+  UT_POW2 = 3,   /* PowerOfTwoParameter   manipulator.py:813-836 */
+  UT_BOOL = 4,   /* BooleanParameter      manipulator.py:930-996 */
+  UT_ENUM = 5,   /* EnumParameter         manipulator.py:1024-1045 */
+  UT_PERM = 6    /* PermutationParameter  manipulator.py:1048-1356 (not yet) */
+};
+
+typedef struct ut_param_desc {
+  int32_t kind;        /* UT_* kind */
+  int32_t sort_rank;   /* position in sorted(params, key=name)  (manipulator.py:237) */
+  double lo, hi;       /* legal_range of the stored value (min_value, max_value) */
+  double u_lo, u_hi;   /* unit-encoding bounds as Python computes them
+                          (ints widened by 0.4999, manipulator.py:476-479) */
+  double u_span;       /* float(u_hi - u_lo) as Python computes it */
+  int64_t n_options;   /* ENUM option count (BOOL: 2) */
+  const char* name;    /* str(p.name) bytes, not NUL-terminated */
+  int32_t name_len;
+  int32_t lut_count;   /* >0: inner digests of repr(value_i) supplied in lut */
+  const uint8_t* lut_host; /* lut_count * 32 bytes: sha256(repr(value)).digest(),
+                              indexed by (value - lo) for INT, option index for
+                              ENUM, 0=False/1=True for BOOL */
+} ut_param_desc;
+
+typedef struct ut_de_params {   /* differentialevolution.py:34-40,142-151 */
+  double cr;                    /* crossover rate (0.9 DE, 0.2 DE-Alt) */
+  int32_t n_cross;              /* forced crossovers (1), <= 4 */
+  int32_t pad;
+} ut_de_params;
+
+typedef struct ut_gp_hyper {
+  double sigma_f2;    /* signal variance */
+  double sigma_n2;    /* noise variance added to the diagonal */
+  double jitter;      /* extra diagonal jitter */
+  const double* lengthscale_host; /* d entries (ARD) */
+} ut_gp_hyper;
+
+enum { UT_ACQ_EI = 0, UT_ACQ_UCB = 1 };
+
+typedef struct ut_acq {
+  int32_t kind;       /* UT_ACQ_EI or UT_ACQ_UCB */
+  int32_t pad;
+  double xi;          /* EI exploration offset */
+  double kappa;       /* UCB: score = kappa*sigma - mu */
+} ut_acq;
+
+/* ---- context ------------------------------------------------------------ */
+int ut_ctx_create(int device, uint64_t seed, ut_ctx** out);
+int ut_ctx_destroy(ut_ctx* ctx);
+const char* ut_last_error(ut_ctx* ctx);
+int ut_set_stream(ut_ctx* ctx, void* hip_stream);   /* hipStream_t; NULL = library stream */
+int ut_sync(ut_ctx* ctx);
+int ut_version(void);
+
+/* ---- search space (ConfigurationManipulator, manipulator.py:129-272) ---- */
+/* py2_layout: 1 = OpenTuner/Python-2 hash layout (no b'' around primitive
+ * inner digests; pins samples/tutorials/tuneup.opentuner.db), 0 = uptune's
+ * Python-3 port (manipulator.py:240 str() of a bytes object). */
+int ut_space_define(ut_ctx* ctx, int32_t n_params, const ut_param_desc* params, int32_t py2_layout);
+/* outer hash message length in bytes, SHA-256 block count, GP feature width */
+int ut_space_info(ut_ctx* ctx, int64_t* outer_len, int64_t* outer_blocks, int32_t* n_features);
+
+/* ---- population (DifferentialEvolution.population, PSO particles) ------- */
+/* op1_randomize every member on the device (manipulator.py:171-176,596-606) */
+int ut_population_init(ut_ctx* ctx, int64_t npop, uint32_t round_);
+int ut_population_set(ut_ctx* ctx, int64_t npop, const double* values, int64_t ld);
+int ut_population_get(ut_ctx* ctx, double* values, int64_t ld);
+/* copy trial rows back into the population: pop[:, idx[j]] = trial[:, j] */
+int ut_population_replace(ut_ctx* ctx, const double* trial, int64_t ld, const int64_t* idx, int64_t n);
+
+/* ---- proposal ----------------------------------------------------------- */
+/* DE/rand/1/bin: one trial per candidate; candidate g targets population
+ * member g % npop (differentialevolution.py:105-129). */
+int ut_propose_de(ut_ctx* ctx, const ut_de_params* p, uint32_t round_, int64_t cand_base, int64_t m,
+                  double* out_values, int64_t ld);
+
+/* GP features of configurations: unit values (get_unit_value), BOOL 0/1,
+ * ENUM one-hot.  out_features[f * ld_out + i]. */
+int ut_encode_features(ut_ctx* ctx, const double* values, int64_t ld, int64_t m, double* out_features,
+                       int64_t ld_out);
+
+/* ---- identity + dedup (hash_config, driver.get_configuration) ----------- */
+int ut_hash(ut_ctx* ctx, const double* values, int64_t ld, int64_t m, uint32_t* out_digest);
+int ut_history_reset(ut_ctx* ctx, int64_t capacity);
+int ut_history_add(ut_ctx* ctx, const uint32_t* digests, int64_t n);   /* device [n][8] */
+int ut_history_add_host(ut_ctx* ctx, const uint32_t* digests_host, int64_t n);
+/* out_dup[i] = 1 if digest i is in the history or repeats an earlier
+ * (smaller index) candidate of the same batch. */
+int ut_dedup(ut_ctx* ctx, const uint32_t* digests, int64_t m, uint8_t* out_dup);
+
+/* ---- GP surrogate ------------------------------------------------------- */
+/* X_host: [n][d] features, y_host: [n] objective (minimised).  Fits
+ * L = chol(K + (sigma_n2 + jitter) I), L^-1, alpha on the device. */
+int ut_gp_fit(ut_ctx* ctx, const double* X_host, const double* y_host, int32_t n, int32_t d,
+              const ut_gp_hyper* hyper);
+/* posterior of standardised y and the acquisition score for m candidates
+ * (features [d][ld]).  mu/var/score may be NULL.  dup (may be NULL) marks
+ * candidates excluded from selection (score forced to -inf). */
+int ut_gp_score(ut_ctx* ctx, const double* features, int64_t ld, int64_t m, const ut_acq* acq,
+                const uint8_t* dup, double* mu, double* var, double* score);
+/* f_best (min standardised y), y mean/std used for standardisation */
+int ut_gp_stats(ut_ctx* ctx, double* f_best, double* y_mean, double* y_std);
+
+/* ---- selection ---------------------------------------------------------- */
+/* k largest scores, ties -> smallest global index; entries with dup[i]!=0 or
+ * NaN score are never selected; missing slots get index -1. */
+int ut_topk(ut_ctx* ctx, const double* score, const uint8_t* dup, int64_t m, int64_t cand_base, int32_t k,
+            int64_t* out_idx, double* out_score);
+
+/* ---- one whole round: propose(DE) -> hash -> dedup -> encode -> GP score
+ *      -> top-k.  Buffers are owned by the context; results copied to the
+ *      given device pointers (any may be NULL). ------------------------- */
+typedef struct ut_round_out {
+  int64_t* topk_idx;      /* [k] global candidate index */
+  double* topk_score;     /* [k] */
+  uint32_t* topk_digest;  /* [k][8] */
+  double* topk_values;    /* [P][k] */
+} ut_round_out;
+int ut_score_round_de(ut_ctx* ctx, const ut_de_params* de, const ut_acq* acq, uint32_t round_, int64_t cand_base,
+                      int64_t m, int32_t k, const ut_round_out* out);
+/* device pointers to the last round's internal buffers (for tests/bench) */
+int ut_round_buffers(ut_ctx* ctx, double** values, double** features, uint32_t** digests, uint8_t** dup,
+                     double** mu, double** var, double** score, int64_t* ld);
+
+/* per-kernel device time of the last ut_score_round_* call (ms), when
+ * timing is enabled with ut_set_timing(ctx, 1).  names: "propose", "hash",
+ * "dedup", "encode", "gp_fit", "kstar", "var", "finalize", "topk" */
+int ut_set_timing(ut_ctx* ctx, int32_t on);
+int ut_stage_time(ut_ctx* ctx, const char* stage, double* ms);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* UTHOT_H */

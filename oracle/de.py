@@ -1,0 +1,125 @@
+"""Batched DE/rand/1/bin restated from
+python/uptune/opentuner/search/differentialevolution.py:105-129.
+
+Batch semantics (the build's): candidate g (global index)
+targets population member g % npop and produces one trial.  The reference's
+random draws are replaced by Philox draws keyed by (seed, g, stream, round):
+
+  donors  x1,x2,x3 : 3 distinct members != target      (:109-118, shuffle(set(pop)-{target}))
+  use_f   = random()/2.0 + 0.5                          (:120)
+  forced  = first n_cross names of a shuffled name list (:122-125)
+            == the n_cross params with the smallest per-param keys
+  cross   = forced or random() < cr                     (:125)
+  primitive: op4_set_linear(x1, x2, x3, 1.0, F, -F)     (manipulator.py:523-542)
+  complex:   copy x1; randomize iff x2 != x3            (manipulator.py:866-914)
+  otherwise the target's value is kept (cfg = copy(parent))  (:106)
+"""
+import numpy as np
+
+from . import philox as ph
+from .space import get_unit_value_vec, op4_set_linear_primitive, randomize, set_unit_value_vec
+
+
+def donors(g, npop, seed, round_):
+    """3 distinct members != t = g % npop (vectorised)"""
+    g = np.asarray(g, dtype=np.uint64)
+    t = (g % np.uint64(npop)).astype(np.int64)
+    x, y, z, _ = ph.draw(seed, g, ph.STREAM_CAND | 0, round_, ph.OP_DE)
+    a = ph.umulhi32(x, npop - 1).astype(np.int64)
+    d1 = a + (a >= t)
+    e0, e1 = np.minimum(t, d1), np.maximum(t, d1)
+    b = ph.umulhi32(y, npop - 2).astype(np.int64)
+    b = b + (b >= e0)
+    b = b + (b >= e1)
+    d2 = b
+    s = np.sort(np.stack([t, d1, d2]), axis=0)
+    c = ph.umulhi32(z, npop - 3).astype(np.int64)
+    c = c + (c >= s[0])
+    c = c + (c >= s[1])
+    c = c + (c >= s[2])
+    return t, d1, d2, c
+
+
+def use_f(g, seed, round_):
+    x, y, _, _ = ph.draw(seed, g, ph.STREAM_CAND | 1, round_, ph.OP_DE)
+    return ph.u01(x, y) / 2.0 + 0.5
+
+
+def forced_mask(g, P, n_cross, seed, round_):
+    """bool [P][m]: param p is among the n_cross smallest (key, p)"""
+    g = np.asarray(g, dtype=np.uint64)
+    if n_cross <= 0:
+        return np.zeros((P, g.size), dtype=bool)
+    keys = np.stack([(ph.draw(seed, g, p, round_, ph.OP_DE)[2].astype(np.uint64) << np.uint64(32)) | np.uint64(p)
+                     for p in range(P)])
+    kth = np.sort(keys, axis=0)[min(n_cross, P) - 1]
+    return keys <= kth
+
+
+def propose_de_vec(space, pop, seed, round_, cand_base, m, cr, n_cross=1):
+    """pop: SoA [P][npop] float64 -> trial SoA [P][m]"""
+    P, npop = pop.shape
+    g = np.arange(cand_base, cand_base + m, dtype=np.uint64)
+    t, d1, d2, d3 = donors(g, npop, seed, round_)
+    F = use_f(g, seed, round_)
+    forced = forced_mask(g, P, n_cross, seed, round_)
+    out = np.empty((P, m), dtype=np.float64)
+    for p, prm in enumerate(space):
+        x, y, _, _ = ph.draw(seed, g, p, round_, ph.OP_DE)
+        cross = forced[p] | (ph.u01(x, y) < cr)
+        col = pop[p]
+        vt = col[t]
+        x1, x2, x3 = col[d1], col[d2], col[d3]
+        if prm.is_primitive():
+            va, vb, vc = get_unit_value_vec(prm, x1), get_unit_value_vec(prm, x2), get_unit_value_vec(prm, x3)
+            u = (1.0 * va + F * vb) + (-F) * vc
+            u = np.where(1.0 < u, 1.0, u)
+            u = np.where(u > 0.0, u, 0.0)
+            nv = set_unit_value_vec(prm, u, vt)
+        else:
+            nv = x1.copy()
+            diff = x2 != x3
+            if diff.any():
+                gi = g[diff]
+                rx, ry, rz, rw = ph.draw(seed, gi, p | (1 << ph.STREAM_SUB_SHIFT), round_, ph.OP_DE)
+                from .space import to_f64
+                nv[diff] = [to_f64(prm, randomize(prm, int(a), int(b), int(c), int(d)))
+                            for a, b, c, d in zip(rx, ry, rz, rw)]
+        out[p] = np.where(cross, nv, vt)
+    return out
+
+
+def propose_de_scalar(space, pop_cfgs, seed, round_, g, cr, n_cross=1):
+    """One trial, written like create_new_configuration (:105-129) over
+    Python values.  pop_cfgs: list of configs (lists of stored values)."""
+    npop = len(pop_cfgs)
+    t, d1, d2, d3 = (int(v[0]) for v in donors(np.array([g]), npop, seed, round_))
+    cfg = list(pop_cfgs[t])                         # manipulator.copy(parent.config.data)
+    x1, x2, x3 = pop_cfgs[d1], pop_cfgs[d2], pop_cfgs[d3]
+    F = float(use_f(np.array([g]), seed, round_)[0])
+    forced = forced_mask(np.array([g]), len(space), n_cross, seed, round_)[:, 0]
+    for p, prm in enumerate(space):
+        x, y, _, _ = ph.draw(seed, np.array([g]), p, round_, ph.OP_DE)
+        if forced[p] or float(ph.u01(x, y)[0]) < cr:
+            if prm.is_primitive():
+                cfg[p] = op4_set_linear_primitive(prm, x1[p], x2[p], x3[p], 1.0, F, -F, cfg[p])
+            else:
+                cfg[p] = x1[p]                      # copy_value(cfg_a, cfg)
+                if x2[p] != x3[p]:                  # add_difference: not same_value -> randomize
+                    rx, ry, rz, rw = ph.draw(seed, np.array([g]), p | (1 << ph.STREAM_SUB_SHIFT), round_, ph.OP_DE)
+                    cfg[p] = randomize(prm, int(rx[0]), int(ry[0]), int(rz[0]), int(rw[0]))
+    return cfg
+
+
+def population_init(space, npop, seed, round_=0):
+    """op1_randomize every member (manipulator.py:171-176) -> SoA [P][npop]"""
+    from .space import to_f64
+    g = np.arange(npop, dtype=np.uint64)
+    out = np.empty((len(space), npop), dtype=np.float64)
+    for p, prm in enumerate(space):
+        x, y, z, w = ph.draw(seed, g, p, round_, ph.OP_INIT)
+        if prm.kind == 0:  # FLOAT, vectorised: lo + (hi - lo) * u
+            out[p] = prm.lo + (prm.hi - prm.lo) * ph.u01(x, y)
+        else:
+            out[p] = [to_f64(prm, randomize(prm, int(a), int(b), int(c), int(d))) for a, b, c, d in zip(x, y, z, w)]
+    return out

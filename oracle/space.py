@@ -1,0 +1,164 @@
+"""Parameter kinds and their value arithmetic, restated from
+python/uptune/opentuner/search/manipulator.py.
+
+A space is a list of `Param`; a configuration row is a list of stored
+values (FLOAT float, INT int, BOOL bool, ENUM the option object).  Scalar
+functions follow the reference line by line (Python floats, Python
+round/min/max); the *_vec versions are the same arithmetic over numpy
+float64 columns (elementwise IEEE ops, np.rint == Python round half-even),
+checked equal to the scalar versions in tests/test_oracle.py.
+"""
+from dataclasses import dataclass, field
+from typing import Any, List
+
+import numpy as np
+
+FLOAT, INT, LOGINT, POW2, BOOL, ENUM, PERM = range(7)
+
+
+@dataclass
+class Param:
+    name: Any
+    kind: int
+    lo: Any = 0
+    hi: Any = 0
+    options: List[Any] = field(default_factory=list)
+
+    def is_primitive(self):
+        return self.kind in (FLOAT, INT, LOGINT, POW2)
+
+    def legal_range(self):
+        # NumericParameter.legal_range  manipulator.py:593-594
+        return self.lo, self.hi
+
+    def is_integer_type(self):
+        # manipulator.py:469-471
+        return self.kind == INT
+
+
+def unit_range(p):
+    """low/high used by get/set_unit_value (manipulator.py:475-479)"""
+    low, high = p.legal_range()
+    if p.is_integer_type():
+        low -= 0.4999
+        high += 0.4999
+    return low, high
+
+
+def get_unit_value(p, val):
+    """manipulator.py:473-488"""
+    low, high = unit_range(p)
+    if low < high:
+        return float(val - low) / float(high - low)
+    return 0.0
+
+
+def set_unit_value(p, unit_value, current):
+    """manipulator.py:490-503 -> new stored value (current if unchanged)"""
+    assert 0.0 <= unit_value <= 1.0
+    low, high = unit_range(p)
+    if low < high:
+        val = unit_value * float(high - low) + low
+        if p.is_integer_type():
+            val = round(val)
+        val = max(low, min(val, high))
+        return int(val) if p.kind == INT else float(val)
+    return current
+
+
+def op4_set_linear_primitive(p, va_raw, vb_raw, vc_raw, a, b, c, current):
+    """PrimitiveParameter.op4_set_linear  manipulator.py:523-542"""
+    va = get_unit_value(p, va_raw)
+    vb = get_unit_value(p, vb_raw)
+    vc = get_unit_value(p, vc_raw)
+    v = a * va + b * vb + c * vc
+    v = max(0.0, min(v, 1.0))
+    return set_unit_value(p, v, current)
+
+
+def randomize(p, x, y, z, w):
+    """op1_randomize given one Philox block (x, y, z, w) as Python ints.
+    FLOAT: random.uniform(lo, hi) = lo + (hi-lo)*random()   manipulator.py:606
+    INT:   random.randint(lo, hi)                            manipulator.py:604
+    BOOL:  random.choice((True, False))                      manipulator.py:946-949
+    ENUM:  random.choice(options)                            manipulator.py:1039
+    """
+    from . import philox as ph
+    if p.kind == FLOAT:
+        u = float(ph.u01(x, y))
+        return p.lo + (p.hi - p.lo) * u
+    r64 = int(ph.u64(z, w))
+    if p.kind == INT:
+        return p.lo + (r64 * (p.hi - p.lo + 1) >> 64)
+    if p.kind == BOOL:
+        return (True, False)[(r64 * 2) >> 64]
+    if p.kind == ENUM:
+        return p.options[(r64 * len(p.options)) >> 64]
+    raise NotImplementedError(p.kind)
+
+
+# ---- value <-> f64 column codec (the device's SoA representation) --------
+def to_f64(p, v):
+    if p.kind == FLOAT:
+        return float(v)
+    if p.kind == INT:
+        return float(int(v))
+    if p.kind == BOOL:
+        return 1.0 if v else 0.0
+    if p.kind == ENUM:
+        return float(p.options.index(v))
+    raise NotImplementedError(p.kind)
+
+
+def from_f64(p, x):
+    if p.kind == FLOAT:
+        return float(x)
+    if p.kind == INT:
+        return int(x)
+    if p.kind == BOOL:
+        return bool(x != 0.0)
+    if p.kind == ENUM:
+        return p.options[int(x)]
+    raise NotImplementedError(p.kind)
+
+
+# ---- vectorised forms over f64 columns -----------------------------------
+def unit_consts(p):
+    low, high = unit_range(p)
+    return float(low), float(high), float(high - low)
+
+
+def get_unit_value_vec(p, col):
+    low, high, span = unit_consts(p)
+    if low < high:
+        return (col - low) / span
+    return np.zeros_like(col)
+
+
+def set_unit_value_vec(p, u, current):
+    low, high, span = unit_consts(p)
+    if not (low < high):
+        return current.copy()
+    val = u * span + low
+    if p.is_integer_type():
+        val = np.rint(val)
+    val = np.where(high < val, high, val)   # min(val, high)
+    val = np.where(val > low, val, low)     # max(low, .)
+    if p.kind == INT:
+        val = np.trunc(val)
+    return val
+
+
+def features(space, rows_f64):
+    """GP features of SoA rows [P][n]: unit values, BOOL 0/1, ENUM one-hot
+    (the build's encoding, SURVEY.md §8(a) GP spec)."""
+    cols = []
+    for p, col in zip(space, rows_f64):
+        if p.is_primitive():
+            cols.append(get_unit_value_vec(p, col))
+        elif p.kind == BOOL:
+            cols.append(col.copy())
+        elif p.kind == ENUM:
+            for k in range(len(p.options)):
+                cols.append((col == k).astype(np.float64))
+    return np.stack(cols)

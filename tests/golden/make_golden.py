@@ -1,0 +1,141 @@
+"""Generate the committed golden fixtures under tests/golden/.
+
+Run in the build container (needs /root/reference for the two data files it
+reads; never imports or executes reference code):
+
+    python tests/golden/make_golden.py
+
+Inputs read as DATA from the reference:
+  * samples/tutorials/tuneup.opentuner.db  -- sqlite; only the `hash` column
+    of table `configuration` is read (the pickled `data` column is never
+    loaded).  The tutorial space is IntegerParameter('BLOCK_SIZE', 1, 10)
+    (samples/tutorials/mmm_tuner.py:20-21); each stored hash is matched to
+    the BLOCK_SIZE whose Python-2-layout hash_config reproduces it.
+  * samples/gcc-options/matmul-record.csv  -- recorded gcc-flag configs
+    (enum codes 1..3 decoded with the sorted mapping of api.py:296-300).
+
+Everything else is produced by the oracle (oracle/*) from fixed seeds.
+"""
+import csv
+import json
+import os
+import sqlite3
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+
+from oracle import de as ode  # noqa: E402
+from oracle import gp as ogp  # noqa: E402
+from oracle import hashing as oh  # noqa: E402
+from oracle.space import BOOL, ENUM, FLOAT, INT, Param, features  # noqa: E402
+
+REF = os.environ.get("UT_REFERENCE", "/root/reference")
+
+
+def tutorial_db():
+    db = os.path.join(REF, "samples/tutorials/tuneup.opentuner.db/zhang-x1.ece.cornell.edu.db")
+    con = sqlite3.connect(f"file:{db}?mode=ro", uri=True)
+    rows = con.execute("select id, hash from configuration order by id").fetchall()
+    con.close()
+    space = [Param("BLOCK_SIZE", INT, 1, 10)]
+    table = {oh.hash_config(space, [k], py2=True): k for k in range(1, 11)}
+    out = []
+    for cid, h in rows:
+        out.append({"id": cid, "hash": h, "BLOCK_SIZE": table.get(h)})
+    assert all(r["BLOCK_SIZE"] is not None for r in out), out
+    with open(os.path.join(HERE, "tutorial_db_hashes.json"), "w") as f:
+        json.dump({"space": [["IntegerParameter", "BLOCK_SIZE", [1, 10]]], "layout": "py2", "rows": out}, f,
+                  indent=1)
+
+
+def gcc_space_and_rows(nrows=512, nhash=64):
+    path = os.path.join(REF, "samples/gcc-options/matmul-record.csv")
+    with open(path) as f:
+        r = csv.reader(f)
+        header = next(r)
+        rows = [row for row in r]
+    cols = [c for c in header if c not in ("time", "build_time", "qor", "is_best")]
+    idx = [header.index(c) for c in cols]
+    data = np.array([[int(float(row[i])) for i in idx] for row in rows], dtype=np.int64)
+    opts = ["on", "off", "default"]                 # tune_gcc.py:262 option order
+    code = {x + 1: y for x, y in enumerate(sorted(set(opts)))}   # api.py:296-300
+    params = []
+    spec = []
+    for j, c in enumerate(cols):
+        if c == "-O":
+            params.append(Param(c, INT, 0, 3))
+            spec.append(["IntegerParameter", c, [0, 3]])
+        elif c.startswith("-f"):
+            params.append(Param(c, ENUM, options=list(opts)))
+            spec.append(["EnumParameter", c, list(opts)])
+        else:
+            lo, hi = int(data[:, j].min()), int(data[:, j].max())
+            params.append(Param(c, INT, lo, hi))
+            spec.append(["IntegerParameter", c, [lo, hi]])
+    cfgs = []
+    for row in data[:nrows]:
+        cfg = []
+        for p, v in zip(params, row):
+            cfg.append(code[int(v)] if p.kind == ENUM else int(v))
+        cfgs.append(cfg)
+    hashes = [oh.hash_config(params, cfgs[i]) for i in range(nhash)]
+    # SoA f64 values (enum -> option index)
+    vals = np.array([[float(opts.index(v)) if p.kind == ENUM else float(v) for p, v in zip(params, cfg)]
+                     for cfg in cfgs]).T
+    np.savez_compressed(os.path.join(HERE, "gcc_rows.npz"), values=vals.astype(np.float64))
+    with open(os.path.join(HERE, "gcc_space.json"), "w") as f:
+        json.dump({"params": spec, "enum_code": {str(k): v for k, v in code.items()},
+                   "source": "samples/gcc-options/matmul-record.csv (int ranges = recorded min..max)",
+                   "hashes_py3": hashes}, f)
+
+
+def r64():
+    rng = np.random.default_rng(7)
+    space = [Param(d, FLOAT, -1000.0, 1000.0) for d in range(64)]
+    vals = rng.uniform(-1000, 1000, size=(64, 24))
+    # add representational edge cases: integers, tiny, exponent-form values
+    vals[:, 0] = 0.0
+    vals[:, 1] = np.round(vals[:, 1])
+    vals[:5, 2] = [1e-5, -2.5e-7, 1000.0, -1000.0, 0.1]
+    hashes = [oh.hash_config(space, list(vals[:, j])) for j in range(vals.shape[1])]
+    np.savez_compressed(os.path.join(HERE, "r64_hashes.npz"), values=vals, hashes=np.array(hashes))
+
+
+def mixed_space():
+    return [Param("x", FLOAT, -5.0, 5.0), Param("n", INT, 1, 64), Param("flag", BOOL),
+            Param("mode", ENUM, options=["a", "b", "c", 4]), Param("y", FLOAT, 0.0, 1.0),
+            Param("big", INT, -100000, 2000000)]
+
+
+def de_golden():
+    space = mixed_space()
+    pop = ode.population_init(space, 16, seed=11, round_=0)
+    trial = ode.propose_de_vec(space, pop, seed=11, round_=3, cand_base=5, m=48, cr=0.5, n_cross=1)
+    np.savez_compressed(os.path.join(HERE, "de_mixed.npz"), pop=pop, trial=trial)
+
+
+def gp_golden():
+    rng = np.random.default_rng(3)
+    n, d, m = 96, 5, 300
+    X = rng.uniform(size=(n, d))
+    y = np.sum((X - 0.3) ** 2, axis=1) + 0.05 * rng.standard_normal(n)
+    U = rng.uniform(size=(m, d))
+    U[:4] = X[:4]  # candidates on training points (sigma ~ 0 branch)
+    g = ogp.GP(X, y, lengthscale=0.3, sigma_f2=1.0, sigma_n2=1e-6, jitter=1e-8)
+    mu, var = g.posterior(U)
+    ei = ogp.acquisition(mu, var, g.f_best, "ei", 0.0)
+    ucb = ogp.acquisition(mu, var, g.f_best, "ucb", kappa=2.0)
+    np.savez_compressed(os.path.join(HERE, "gp_small.npz"), X=X, y=y, U=U, mu=mu, var=var, ei=ei, ucb=ucb,
+                        f_best=g.f_best)
+
+
+if __name__ == "__main__":
+    tutorial_db()
+    gcc_space_and_rows()
+    r64()
+    de_golden()
+    gp_golden()
+    print("golden fixtures written to", HERE)

@@ -1,0 +1,98 @@
+"""The shared device arithmetic (uptune_amd/csrc/ut_core.h), compiled for the
+host with g++, against CPython's repr / hashlib and the oracle's Philox.
+This exercises the exact source the gfx950 kernels compile (CPU, no GPU)."""
+import ctypes
+import hashlib
+import math
+import os
+import random
+import struct
+import subprocess
+
+import numpy as np
+import pytest
+
+from oracle import philox as ph
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HOSTLIB = os.path.join(ROOT, "uptune_amd", "libuthot_hostcheck.so")
+
+
+@pytest.fixture(scope="module")
+def hc():
+    src = os.path.join(ROOT, "uptune_amd", "csrc", "hostcheck.cpp")
+    if not os.path.exists(HOSTLIB) or os.path.getmtime(HOSTLIB) < os.path.getmtime(src):
+        subprocess.check_call(["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-ffp-contract=off", src, "-o",
+                               HOSTLIB])
+    lib = ctypes.CDLL(HOSTLIB)
+    lib.uthc_repr_double.argtypes = [ctypes.c_double, ctypes.c_char_p]
+    lib.uthc_repr_int64.argtypes = [ctypes.c_longlong, ctypes.c_char_p]
+    lib.uthc_sha256.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p]
+    lib.uthc_philox.argtypes = [ctypes.c_ulonglong, ctypes.c_ulonglong, ctypes.c_uint, ctypes.c_uint, ctypes.c_uint,
+                                ctypes.POINTER(ctypes.c_uint)]
+    return lib
+
+
+def _repr(lib, x):
+    buf = ctypes.create_string_buffer(64)
+    n = lib.uthc_repr_double(x, buf)
+    return buf.raw[:n].decode()
+
+
+SPECIAL = [0.0, -0.0, 1.0, -1.0, 0.1, 0.2, 0.3, 1e16, 1e15, 9999999999999998.0, 1e-4, 1e-5, 0.00012345,
+           123.456, 5e-324, -5e-324, 2.2250738585072014e-308, 2.225073858507201e-308, 1.7976931348623157e308,
+           float("inf"), float("-inf"), 9007199254740993.0, 1e22, 1e23, 2.0 ** 63, 2.0 ** -1074 * 3, 1 / 3,
+           -1000.0, 1000.0, 999.9999999999999, 4.35, 2.675, 1e300, 1e-300, 100.0, 12345678901234567890.0]
+
+
+def test_repr_special(hc):
+    for x in SPECIAL:
+        assert _repr(hc, x) == repr(x), x
+    assert _repr(hc, float("nan")) == "nan"
+
+
+def test_repr_random_bits(hc):
+    rng = random.Random(12345)
+    for _ in range(200000):
+        x = struct.unpack("<d", struct.pack("<Q", rng.getrandbits(64)))[0]
+        if math.isnan(x):
+            continue
+        assert _repr(hc, x) == repr(x)
+
+
+def test_repr_search_ranges(hc):
+    rng = random.Random(99)
+    for lo, hi in [(-1000.0, 1000.0), (0.0, 1.0), (-1e-3, 1e-3), (1e10, 1e18)]:
+        for _ in range(50000):
+            x = rng.uniform(lo, hi)
+            assert _repr(hc, x) == repr(x)
+    # values produced by set_unit_value arithmetic: u * span + lo
+    for _ in range(50000):
+        u = rng.random()
+        x = u * 2000.0 + -1000.0
+        assert _repr(hc, x) == repr(x)
+
+
+def test_repr_int(hc):
+    buf = ctypes.create_string_buffer(32)
+    for v in [0, 1, -1, 9, 10, 99, 100, 2**31, -2**31, 2**53 + 1, 2**63 - 1, -2**63, 107572959]:
+        n = hc.uthc_repr_int64(v, buf)
+        assert buf.raw[:n].decode() == repr(v)
+
+
+def test_sha256(hc):
+    rng = random.Random(3)
+    out = ctypes.create_string_buffer(32)
+    for L in [0, 1, 3, 55, 56, 63, 64, 65, 119, 120, 127, 128, 4588, 30178]:
+        m = bytes(rng.getrandbits(8) for _ in range(L))
+        hc.uthc_sha256(m, L, out)
+        assert out.raw == hashlib.sha256(m).digest()
+
+
+def test_philox_matches_oracle(hc):
+    out = (ctypes.c_uint * 4)()
+    for seed, cand, stream, rnd, op in [(0, 0, 0, 0, 1), (2**40 + 7, 123456789, 5, 17, 2),
+                                        (1, 2**33 + 5, 0xFFFF0001, 300, 4)]:
+        hc.uthc_philox(seed, cand, stream, rnd, op, out)
+        want = ph.draw(seed, np.array([cand], dtype=np.uint64), stream, rnd, op)
+        assert list(out) == [int(w[0]) for w in want]

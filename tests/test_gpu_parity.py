@@ -1,0 +1,348 @@
+"""Device path (libuthot.so through the C ABI) vs the oracle.  Needs a GPU.
+
+Tolerances: bit-exact for values, digests, dedup masks and selected
+indices; GP mu / var / EI within 1e-5 relative (fp64 path, BASELINE.json
+north_star) with an absolute floor of 1e-9 for quantities that are ~0.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+from oracle import de as ode  # noqa: E402
+from oracle import gp as ogp  # noqa: E402
+from oracle import hashing as oh  # noqa: E402
+from oracle import select as osel  # noqa: E402
+from oracle.space import BOOL, ENUM, FLOAT, INT, Param, features, from_f64  # noqa: E402
+
+RTOL = 1e-5
+ATOL = 1e-9
+
+
+def _require_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def to_manip(space):
+    from uptune_amd.manipulator import (BooleanParameter, ConfigurationManipulator, EnumParameter, FloatParameter,
+                                        IntegerParameter)
+    m = ConfigurationManipulator()
+    for p in space:
+        if p.kind == FLOAT:
+            m.add_parameter(FloatParameter(p.name, p.lo, p.hi))
+        elif p.kind == INT:
+            m.add_parameter(IntegerParameter(p.name, p.lo, p.hi))
+        elif p.kind == BOOL:
+            m.add_parameter(BooleanParameter(p.name))
+        elif p.kind == ENUM:
+            m.add_parameter(EnumParameter(p.name, p.options))
+    return m
+
+
+def engine(space, seed=0, py2=False):
+    _require_gpu()
+    from uptune_amd.engine import BatchEngine
+    return BatchEngine(to_manip(space), device=0, seed=seed, py2_layout=py2)
+
+
+def dev(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+def hexes(d):
+    from uptune_amd.engine import digests_to_hex
+    return digests_to_hex(d)
+
+
+def mixed_space():
+    return [Param("x", FLOAT, -5.0, 5.0), Param("n", INT, 1, 64), Param("flag", BOOL),
+            Param("mode", ENUM, options=["a", "b", "c", 4]), Param("y", FLOAT, 0.0, 1.0),
+            Param("big", INT, -100000, 2000000)]
+
+
+def r64_space():
+    return [Param(d, FLOAT, -1000.0, 1000.0) for d in range(64)]
+
+
+def oracle_hashes(space, vals):
+    return [oh.hash_config(space, [from_f64(p, vals[i, j]) for i, p in enumerate(space)])
+            for j in range(vals.shape[1])]
+
+
+# --------------------------------------------------------------------------- hash
+def test_hash_tutorial_db_py2(golden_dir):
+    d = json.load(open(os.path.join(golden_dir, "tutorial_db_hashes.json")))
+    space = [Param("BLOCK_SIZE", INT, 1, 10)]
+    e = engine(space, py2=True)
+    vals = np.array([[float(r["BLOCK_SIZE"]) for r in d["rows"]]])
+    got = hexes(e.hash(dev(vals)))
+    assert got == [r["hash"] for r in d["rows"]]
+
+
+def test_hash_r64_golden_and_random(golden_dir):
+    z = np.load(os.path.join(golden_dir, "r64_hashes.npz"))
+    e = engine(r64_space())
+    assert e.space_info()[:2] == (4588, 72)
+    assert hexes(e.hash(dev(z["values"]))) == list(z["hashes"])
+    rng = np.random.default_rng(5)
+    vals = rng.uniform(-1000, 1000, size=(64, 2000))
+    vals[:, :50] = np.round(vals[:, :50], rng.integers(0, 6))  # short reprs
+    vals[3, 60:80] = rng.uniform(-1e-4, 1e-4, 20)               # exponent form
+    assert hexes(e.hash(dev(vals))) == oracle_hashes(r64_space(), vals)
+
+
+def test_hash_gcc_space(golden_dir):
+    d = json.load(open(os.path.join(golden_dir, "gcc_space.json")))
+    vals = np.load(os.path.join(golden_dir, "gcc_rows.npz"))["values"]
+    space = []
+    for ptype, name, rng in d["params"]:
+        space.append(Param(name, ENUM, options=list(rng)) if ptype == "EnumParameter" else
+                     Param(name, INT, rng[0], rng[1]))
+    e = engine(space)
+    assert e.space_info()[:2] == (30178, 472)
+    got = hexes(e.hash(dev(vals)))
+    assert got[:64] == d["hashes_py3"]
+    assert got == oracle_hashes(space, vals)
+
+
+def test_hash_mixed_and_py2():
+    space = mixed_space()
+    pop = ode.population_init(space, 3000, seed=3)
+    for py2 in (False, True):
+        e = engine(space, py2=py2)
+        got = hexes(e.hash(dev(pop)))
+        want = [oh.hash_config(space, [from_f64(p, pop[i, j]) for i, p in enumerate(space)], py2=py2)
+                for j in range(pop.shape[1])]
+        assert got == want
+
+
+# --------------------------------------------------------------------------- proposal
+def test_population_init_matches_oracle():
+    space = mixed_space()
+    e = engine(space, seed=11)
+    e.population_init(1000, round_=2)
+    got = e.population_get().cpu().numpy()
+    np.testing.assert_array_equal(got, ode.population_init(space, 1000, seed=11, round_=2))
+
+
+@pytest.mark.parametrize("cr,n_cross", [(0.5, 1), (0.2, 1), (0.9, 2), (0.0, 0)])
+def test_de_matches_oracle(cr, n_cross):
+    space = mixed_space()
+    e = engine(space, seed=21)
+    pop = ode.population_init(space, 257, seed=4)
+    e.population_set(dev(pop))
+    got = e.propose_de(4000, round_=7, cand_base=123, cr=cr, n_cross=n_cross).cpu().numpy()
+    want = ode.propose_de_vec(space, pop, seed=21, round_=7, cand_base=123, m=4000, cr=cr, n_cross=n_cross)
+    np.testing.assert_array_equal(got, want)
+
+
+def test_de_golden(golden_dir):
+    z = np.load(os.path.join(golden_dir, "de_mixed.npz"))
+    e = engine(mixed_space(), seed=11)
+    e.population_set(dev(z["pop"]))
+    got = e.propose_de(48, round_=3, cand_base=5, cr=0.5, n_cross=1).cpu().numpy()
+    np.testing.assert_array_equal(got, z["trial"])
+
+
+def test_de_r64_large():
+    space = r64_space()
+    e = engine(space, seed=1)
+    e.population_init(1 << 16)
+    pop = e.population_get().cpu().numpy()
+    np.testing.assert_array_equal(pop, ode.population_init(space, 1 << 16, seed=1))
+    got = e.propose_de(1 << 16, round_=1, cr=0.2).cpu().numpy()
+    np.testing.assert_array_equal(got, ode.propose_de_vec(space, pop, 1, 1, 0, 1 << 16, 0.2, 1))
+
+
+def test_encode_features():
+    space = mixed_space()
+    e = engine(space)
+    pop = ode.population_init(space, 500, seed=8)
+    got = e.encode(dev(pop)).cpu().numpy()
+    np.testing.assert_array_equal(got, features(space, pop))
+
+
+# --------------------------------------------------------------------------- dedup
+def test_dedup_matches_oracle():
+    space = [Param("a", INT, 0, 20), Param("b", ENUM, options=["x", "y"]), Param("c", BOOL)]
+    e = engine(space, seed=2)
+    pop = ode.population_init(space, 5000, seed=2)  # 84 distinct configs -> many in-batch dups
+    d = e.hash(dev(pop))
+    hx = hexes(d)
+    hist = hx[3000:3010]
+    e.history_reset(16)
+    e.history_add(hist)
+    got = e.dedup(d).cpu().numpy().tolist()
+    assert got == osel.dedup(hx, set(hist))
+    # growth path of the history table keeps earlier entries
+    e.history_add(hexes(e.hash(dev(ode.population_init(space, 3000, seed=99)))))
+    got2 = e.dedup(d).cpu().numpy()
+    assert got2.sum() >= sum(got)
+
+
+def test_dedup_unique_large():
+    space = r64_space()
+    e = engine(space, seed=3)
+    e.population_init(1 << 15)
+    vals = e.population_get()
+    vals = torch.cat([vals, vals[:, :100]], dim=1).contiguous()
+    d = e.hash(vals)
+    e.history_reset(0)
+    dup = e.dedup(d).cpu().numpy()
+    assert dup[: 1 << 15].sum() == 0 and dup[1 << 15:].sum() == 100
+
+
+# --------------------------------------------------------------------------- GP
+def _close(got, want, rtol=RTOL, atol=ATOL):
+    np.testing.assert_allclose(got, want, rtol=rtol, atol=atol)
+
+
+def test_gp_small_golden(golden_dir):
+    z = np.load(os.path.join(golden_dir, "gp_small.npz"))
+    space = [Param(f"u{k}", FLOAT, 0.0, 1.0) for k in range(5)]
+    e = engine(space)
+    e.gp_fit(z["X"], z["y"], lengthscale=0.3, sigma_f2=1.0, sigma_n2=1e-6, jitter=1e-8)
+    fb, mean, sd = e.gp_stats()
+    assert abs(fb - float(z["f_best"])) < 1e-12
+    U = dev(z["U"].T)
+    mu, var, ei = e.gp_score(U, acq=e.acq("ei"))
+    _close(mu.cpu().numpy(), z["mu"])
+    _close(var.cpu().numpy(), z["var"])
+    _close(ei.cpu().numpy(), z["ei"])
+    _, _, ucb = e.gp_score(U, acq=e.acq("ucb", kappa=2.0))
+    _close(ucb.cpu().numpy(), z["ucb"])
+
+
+@pytest.mark.parametrize("n,d,ell", [(1024, 64, 0.2), (200, 8, 0.5), (77, 3, 0.25)])
+def test_gp_vs_oracle(n, d, ell):
+    rng = np.random.default_rng(n + d)
+    X = rng.uniform(size=(n, d))
+    y = np.sum((X - 0.4) ** 2, axis=1) + 0.01 * rng.standard_normal(n)
+    U = rng.uniform(size=(3000, d))
+    U[:10] = X[:10] + 1e-3
+    space = [Param(f"u{k}", FLOAT, 0.0, 1.0) for k in range(d)]
+    e = engine(space)
+    e.gp_fit(X, y, lengthscale=ell, sigma_f2=1.0, sigma_n2=1e-6, jitter=1e-8)
+    g = ogp.GP(X, y, lengthscale=ell, sigma_f2=1.0, sigma_n2=1e-6, jitter=1e-8)
+    mu_o, var_o = g.posterior(U)
+    ei_o = ogp.acquisition(mu_o, var_o, g.f_best)
+    mu, var, ei = e.gp_score(dev(U.T))
+    _close(mu.cpu().numpy(), mu_o)
+    _close(var.cpu().numpy(), var_o, atol=1e-8)
+    _close(ei.cpu().numpy(), ei_o, atol=1e-8)
+
+
+# --------------------------------------------------------------------------- top-k
+def test_topk_matches_oracle():
+    e = engine([Param("x", FLOAT, 0.0, 1.0)])
+    rng = np.random.default_rng(0)
+    for m, k in [(10, 4), (5000, 256), (100000, 1000), (2048 * 3 + 7, 17)]:
+        s = np.round(rng.standard_normal(m), 2)  # many ties
+        s[::97] = np.nan
+        dup = (rng.uniform(size=m) < 0.1).astype(np.uint8)
+        idx, top = e.topk(dev(s), k, dup=dev(dup), cand_base=1000)
+        want = osel.topk(list(s), k, dup=list(dup), cand_base=1000)
+        assert idx.cpu().numpy().tolist() == want
+
+
+# --------------------------------------------------------------------------- round
+def _round_oracle(space, pop, seed, round_, cand_base, m, cr, X, y, ell, hist, k):
+    trial = ode.propose_de_vec(space, pop, seed, round_, cand_base, m, cr, 1)
+    hx = oracle_hashes(space, trial)
+    dup = osel.dedup(hx, set(hist))
+    g = ogp.GP(X, y, lengthscale=ell, sigma_f2=1.0, sigma_n2=1e-6, jitter=1e-8)
+    mu, var = g.posterior(features(space, trial).T)
+    ei = ogp.acquisition(mu, var, g.f_best)
+    return trial, hx, dup, ei
+
+
+def test_score_round_de_small():
+    space = mixed_space()
+    seed, m, k = 5, 6000, 64
+    e = engine(space, seed=seed)
+    pop = ode.population_init(space, 512, seed=seed)
+    e.population_set(dev(pop))
+    rng = np.random.default_rng(1)
+    X = features(space, pop[:, :100]).T
+    y = rng.standard_normal(100)
+    e.gp_fit(X, y, lengthscale=0.7, sigma_f2=1.0, sigma_n2=1e-6, jitter=1e-8)
+    hist = oracle_hashes(space, pop[:, :300])
+    e.history_reset(300)
+    e.history_add(hist)
+    idx, top, dig, vals = e.score_round_de(m, k, round_=2, cand_base=0, cr=0.2)
+    trial, hx, dup, ei = _round_oracle(space, pop, seed, 2, 0, m, 0.2, X, y, 0.7, hist, k)
+    (pv, pf, pd, pdup, pmu, pvar, psc), ld = e.round_buffers()
+    assert ld >= m and psc
+    e.sync()
+    idx_l = idx.cpu().numpy().tolist()
+    # selected rows: values and digests are bit-exact with the oracle
+    for j, g in enumerate(idx_l):
+        assert g >= 0 and not dup[g]
+        np.testing.assert_array_equal(vals[:, j].cpu().numpy(), trial[:, g])
+        assert hexes(dig[j:j + 1])[0] == hx[g]
+    # selection = oracle top-k of the oracle scores wherever scores are distinct
+    want = osel.topk(list(ei), k, dup=dup)
+    top_o = np.asarray([ei[g] for g in want])
+    _close(top.cpu().numpy(), top_o, atol=1e-8)
+    gaps = np.abs(np.diff(np.sort(np.asarray(ei)[np.asarray(dup) == 0])[::-1][: k + 1]))
+    if gaps.min() > 1e-6:
+        assert idx_l == want
+
+
+def test_sharding_invariance():
+    """top-k over a pool split into shards (global candidate indices) and
+    merged equals the single-shot top-k -- the multi-GPU contract."""
+    space = r64_space()
+    e = engine(space, seed=9)
+    e.population_init(4096)
+    rng = np.random.default_rng(2)
+    X = rng.uniform(size=(256, 64))
+    y = rng.standard_normal(256)
+    e.gp_fit(X, y, lengthscale=2.0)
+    k, m = 32, 8192
+    i_full, s_full, _, _ = e.score_round_de(m, k, round_=1, cand_base=0)
+    parts = []
+    for base in (0, 3000, 6000):
+        mm = min(3000, m - base)
+        i_p, s_p, _, _ = e.score_round_de(mm, k, round_=1, cand_base=base)
+        parts += list(zip(s_p.cpu().numpy().tolist(), i_p.cpu().numpy().tolist()))
+    parts = [p for p in parts if p[1] >= 0]
+    parts.sort(key=lambda t: (-t[0], t[1]))
+    assert [p[1] for p in parts[:k]] == i_full.cpu().numpy().tolist()
+
+
+def test_full_size_round_properties():
+    """C2 at full size (m = 2^20, n = 1024, d = 64): size-independent checks."""
+    space = r64_space()
+    m, n, k = 1 << 20, 1024, 256
+    e = engine(space, seed=1)
+    e.population_init(m)
+    rng = np.random.default_rng(0)
+    X = rng.uniform(size=(n, 64))
+    xs = X * 2000.0 - 1000.0
+    y = np.sum(100.0 * (xs[:, 1:] - xs[:, :-1] ** 2) ** 2 + (xs[:, :-1] - 1.0) ** 2, axis=1)
+    e.gp_fit(X, y, lengthscale=0.2, sigma_f2=1.0, sigma_n2=1e-6)
+    e.history_reset(0)
+    idx, top, dig, vals = e.score_round_de(m, k, round_=0, cand_base=0, cr=0.2)
+    idx = idx.cpu().numpy()
+    top = top.cpu().numpy()
+    assert np.all(idx >= 0) and len(set(idx.tolist())) == k
+    assert np.all(np.diff(top) <= 0)
+    v = vals.cpu().numpy()
+    # digests of the selected rows recomputed by the oracle
+    assert hexes(dig) == oracle_hashes(space, v)
+    # their scores recomputed by the oracle GP
+    g = ogp.GP(X, y, lengthscale=0.2, sigma_f2=1.0, sigma_n2=1e-6)
+    mu, var = g.posterior(features(space, v).T)
+    ei = ogp.acquisition(mu, var, g.f_best)
+    _close(top, ei, atol=1e-8)
+    # and the rows are exactly the DE trials the oracle proposes for those indices
+    pop = e.population_get().cpu().numpy()
+    sub = ode.propose_de_vec(space, pop, 1, 0, 0, m, 0.2, 1)[:, idx]
+    np.testing.assert_array_equal(v, sub)

@@ -1,0 +1,165 @@
+"""The oracle against the reference's own data and standard KATs (CPU)."""
+import hashlib
+import json
+import os
+import random
+
+import numpy as np
+
+from oracle import de as ode
+from oracle import gp as ogp
+from oracle import hashing as oh
+from oracle import philox as ph
+from oracle import select as osel
+from oracle.space import BOOL, ENUM, FLOAT, INT, Param, from_f64, get_unit_value, set_unit_value
+
+
+def test_tutorial_db_hashes_pin_layout(golden_dir):
+    """9 Configuration.hash values stored by the reference's tutorial run
+    (samples/tutorials/tuneup.opentuner.db) are reproduced exactly by the
+    Python-2 outer-message layout."""
+    d = json.load(open(os.path.join(golden_dir, "tutorial_db_hashes.json")))
+    space = [Param("BLOCK_SIZE", INT, 1, 10)]
+    assert len(d["rows"]) == 9
+    for r in d["rows"]:
+        assert oh.hash_config(space, [r["BLOCK_SIZE"]], py2=True) == r["hash"]
+    # and the py3 layout (uptune's port) differs only by the b'' wrapper
+    msg = oh.outer_message(space, [3])
+    assert msg.startswith(b"BLOCK_SIZEb'") and msg.endswith(b"'0|")
+
+
+def test_py3_layout_matches_reference_expression():
+    """str(bytes) wrapper of manipulator.py:240/459 under Python 3"""
+    inner = hashlib.sha256(repr(2.5).encode("utf-8")).hexdigest().encode()
+    m = hashlib.sha256()
+    m.update(str("x").encode())
+    m.update(str(inner).encode())
+    m.update(str(0).encode())
+    m.update(b"|")
+    assert oh.hash_config([Param("x", FLOAT, 0.0, 5.0)], [2.5]) == m.hexdigest()
+
+
+def test_sha256_fips_vectors():
+    assert hashlib.sha256(b"abc").hexdigest() == "ba7816bf8f01cfea414140de5dae2223b00361a396177a9cb410ff61f20015ad"
+    assert hashlib.sha256(b"").hexdigest() == "e3b0c44298fc1c149afbf4c8996fb92427ae41e4649b934ca495991b7852b855"
+
+
+def test_philox_random123_kats():
+    cases = [((0, 0, 0, 0), (0, 0), (0x6627e8d5, 0xe169c58d, 0xbc57ac4c, 0x9b00dbd8)),
+             ((0xffffffff,) * 4, (0xffffffff,) * 2, (0x408f276d, 0x41c83b0e, 0xa20bc7c6, 0x6d5451fd)),
+             ((0x243f6a88, 0x85a308d3, 0x13198a2e, 0x03707344), (0xa4093822, 0x299f31d0),
+              (0xd16cfe09, 0x94fdcceb, 0x5001e420, 0x24126ea1))]
+    for c, k, want in cases:
+        got = ph.philox4x32_10(*c, *k)
+        assert tuple(int(x) for x in got) == want
+
+
+def test_mulhi64():
+    rng = random.Random(0)
+    a = [rng.getrandbits(64) for _ in range(200)]
+    b = [rng.getrandbits(63) + 1 for _ in range(200)]
+    got = ph.mulhi64(np.array(a, dtype=np.uint64), np.array(b, dtype=np.uint64))
+    assert [int(x) for x in got] == [(x * y) >> 64 for x, y in zip(a, b)]
+
+
+def test_unit_value_roundtrip_int():
+    p = Param("n", INT, 1, 10)
+    for v in range(1, 11):
+        u = get_unit_value(p, v)
+        assert set_unit_value(p, u, None) == v
+
+
+def _space():
+    return [Param("x", FLOAT, -5.0, 5.0), Param("n", INT, 1, 64), Param("flag", BOOL),
+            Param("mode", ENUM, options=["a", "b", "c", 4]), Param("y", FLOAT, 0.0, 1.0),
+            Param("big", INT, -100000, 2000000)]
+
+
+def test_de_scalar_equals_vectorised():
+    space = _space()
+    pop = ode.population_init(space, 16, seed=11)
+    trial = ode.propose_de_vec(space, pop, seed=11, round_=3, cand_base=5, m=48, cr=0.5, n_cross=1)
+    pop_cfgs = [[from_f64(p, pop[j, i]) for j, p in enumerate(space)] for i in range(16)]
+    for i in range(48):
+        cfg = ode.propose_de_scalar(space, pop_cfgs, 11, 3, 5 + i, 0.5, 1)
+        assert [from_f64(p, trial[j, i]) for j, p in enumerate(space)] == cfg
+
+
+def test_de_golden(golden_dir):
+    z = np.load(os.path.join(golden_dir, "de_mixed.npz"))
+    space = _space()
+    pop = ode.population_init(space, 16, seed=11)
+    np.testing.assert_array_equal(pop, z["pop"])
+    trial = ode.propose_de_vec(space, pop, seed=11, round_=3, cand_base=5, m=48, cr=0.5, n_cross=1)
+    np.testing.assert_array_equal(trial, z["trial"])
+
+
+def test_de_invariants():
+    space = _space()
+    pop = ode.population_init(space, 64, seed=1)
+    trial = ode.propose_de_vec(space, pop, seed=1, round_=0, cand_base=0, m=256, cr=0.2, n_cross=1)
+    assert np.all((trial[0] >= -5.0) & (trial[0] <= 5.0))
+    assert np.all(trial[1] == np.round(trial[1])) and np.all((trial[1] >= 1) & (trial[1] <= 64))
+    assert set(np.unique(trial[2])) <= {0.0, 1.0}
+    assert set(np.unique(trial[3])) <= {0.0, 1.0, 2.0, 3.0}
+    # donors are distinct and differ from the target
+    t, d1, d2, d3 = ode.donors(np.arange(4096, dtype=np.uint64), 7, seed=9, round_=2)
+    st = np.stack([t, d1, d2, d3])
+    assert all(len(set(st[:, i])) == 4 for i in range(st.shape[1]))
+    assert st.min() >= 0 and st.max() < 7
+    # at least one param changes per trial (n_cross=1) unless the forced op is a no-op
+    forced = ode.forced_mask(np.arange(256, dtype=np.uint64), len(space), 1, 1, 0)
+    assert np.all(forced.sum(axis=0) == 1)
+
+
+def test_r64_hash_golden(golden_dir):
+    z = np.load(os.path.join(golden_dir, "r64_hashes.npz"))
+    space = [Param(d, FLOAT, -1000.0, 1000.0) for d in range(64)]
+    vals = z["values"]
+    for j in range(vals.shape[1]):
+        assert oh.hash_config(space, list(vals[:, j])) == z["hashes"][j]
+    # outer message length is constant: 4588 bytes for R64
+    assert len(oh.outer_message(space, list(vals[:, 0]))) == 4588
+
+
+def test_gcc_hash_golden(golden_dir):
+    d = json.load(open(os.path.join(golden_dir, "gcc_space.json")))
+    vals = np.load(os.path.join(golden_dir, "gcc_rows.npz"))["values"]
+    space = []
+    for ptype, name, rng in d["params"]:
+        if ptype == "EnumParameter":
+            space.append(Param(name, ENUM, options=list(rng)))
+        else:
+            space.append(Param(name, INT, rng[0], rng[1]))
+    assert len(space) == 339
+    for j, h in enumerate(d["hashes_py3"][:16]):
+        cfg = [from_f64(p, vals[i, j]) for i, p in enumerate(space)]
+        assert oh.hash_config(space, cfg) == h
+    assert len(oh.outer_message(space, cfg)) == 30178
+
+
+def test_gp_golden(golden_dir):
+    z = np.load(os.path.join(golden_dir, "gp_small.npz"))
+    g = ogp.GP(z["X"], z["y"], lengthscale=0.3, sigma_f2=1.0, sigma_n2=1e-6, jitter=1e-8)
+    mu, var = g.posterior(z["U"])
+    np.testing.assert_allclose(mu, z["mu"], rtol=1e-12, atol=1e-12)
+    np.testing.assert_allclose(var, z["var"], rtol=1e-9, atol=1e-12)
+    # posterior at training points: small variance, mean ~ ys
+    assert np.all(var[:4] < 1e-4)
+    np.testing.assert_allclose(mu[:4], g.ys[:4], atol=1e-3)
+
+
+def test_ei_properties():
+    mu = np.array([0.0, -1.0, 1.0, 0.0])
+    var = np.array([1.0, 1.0, 1.0, 0.0])
+    ei = ogp.acquisition(mu, var, f_best=0.0)
+    assert ei[1] > ei[0] > ei[2] > 0
+    assert ei[3] == 0.0
+
+
+def test_topk_and_dedup_semantics():
+    s = [0.5, 0.9, 0.9, float("nan"), 0.1, 0.9]
+    assert osel.topk(s, 3) == [1, 2, 5]
+    assert osel.topk(s, 3, dup=[0, 1, 0, 0, 0, 0]) == [2, 5, 0]
+    assert osel.topk(s, 8, cand_base=10)[-2:] == [-1, -1]
+    assert osel.dedup(["a", "b", "a", "c"], history={"c"}) == [0, 0, 1, 1]

@@ -1,0 +1,118 @@
+"""ctypes binding of libuthot.so (include/uthot.h).
+
+The product path has no CPU fallback: if the shared library is missing or
+cannot be loaded, importing this module's `lib()` raises.  Structures mirror
+the C header field for field.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("UTHOT_LIB", os.path.join(_HERE, "libuthot.so"))
+
+UT_FLOAT, UT_INT, UT_LOGINT, UT_POW2, UT_BOOL, UT_ENUM, UT_PERM = range(7)
+UT_ACQ_EI, UT_ACQ_UCB = 0, 1
+
+ERRORS = {
+    -1: "UT_EINVAL", -2: "UT_EHIP", -3: "UT_ENOSPACE", -4: "UT_EUNSUPPORTED", -5: "UT_ENOTPD", -6: "UT_ENOMEM",
+}
+
+
+class ParamDesc(C.Structure):
+    _fields_ = [
+        ("kind", C.c_int32), ("sort_rank", C.c_int32),
+        ("lo", C.c_double), ("hi", C.c_double),
+        ("u_lo", C.c_double), ("u_hi", C.c_double), ("u_span", C.c_double),
+        ("n_options", C.c_int64),
+        ("name", C.c_char_p), ("name_len", C.c_int32),
+        ("lut_count", C.c_int32), ("lut_host", C.c_void_p),
+    ]
+
+
+class DeParams(C.Structure):
+    _fields_ = [("cr", C.c_double), ("n_cross", C.c_int32), ("pad", C.c_int32)]
+
+
+class GpHyper(C.Structure):
+    _fields_ = [("sigma_f2", C.c_double), ("sigma_n2", C.c_double), ("jitter", C.c_double),
+                ("lengthscale_host", C.c_void_p)]
+
+
+class Acq(C.Structure):
+    _fields_ = [("kind", C.c_int32), ("pad", C.c_int32), ("xi", C.c_double), ("kappa", C.c_double)]
+
+
+class RoundOut(C.Structure):
+    _fields_ = [("topk_idx", C.c_void_p), ("topk_score", C.c_void_p), ("topk_digest", C.c_void_p),
+                ("topk_values", C.c_void_p)]
+
+
+P = C.c_void_p
+I32, I64, U32, U64, D = C.c_int32, C.c_int64, C.c_uint32, C.c_uint64, C.c_double
+
+# name -> (restype, argtypes); every symbol declared in include/uthot.h
+SIGNATURES = {
+    "ut_version": (C.c_int, []),
+    "ut_ctx_create": (C.c_int, [C.c_int, U64, C.POINTER(P)]),
+    "ut_ctx_destroy": (C.c_int, [P]),
+    "ut_last_error": (C.c_char_p, [P]),
+    "ut_set_stream": (C.c_int, [P, P]),
+    "ut_sync": (C.c_int, [P]),
+    "ut_space_define": (C.c_int, [P, I32, C.POINTER(ParamDesc), I32]),
+    "ut_space_info": (C.c_int, [P, C.POINTER(I64), C.POINTER(I64), C.POINTER(I32)]),
+    "ut_population_init": (C.c_int, [P, I64, U32]),
+    "ut_population_set": (C.c_int, [P, I64, P, I64]),
+    "ut_population_get": (C.c_int, [P, P, I64]),
+    "ut_population_replace": (C.c_int, [P, P, I64, P, I64]),
+    "ut_propose_de": (C.c_int, [P, C.POINTER(DeParams), U32, I64, I64, P, I64]),
+    "ut_encode_features": (C.c_int, [P, P, I64, I64, P, I64]),
+    "ut_hash": (C.c_int, [P, P, I64, I64, P]),
+    "ut_history_reset": (C.c_int, [P, I64]),
+    "ut_history_add": (C.c_int, [P, P, I64]),
+    "ut_history_add_host": (C.c_int, [P, P, I64]),
+    "ut_dedup": (C.c_int, [P, P, I64, P]),
+    "ut_gp_fit": (C.c_int, [P, P, P, I32, I32, C.POINTER(GpHyper)]),
+    "ut_gp_score": (C.c_int, [P, P, I64, I64, C.POINTER(Acq), P, P, P, P]),
+    "ut_gp_stats": (C.c_int, [P, C.POINTER(D), C.POINTER(D), C.POINTER(D)]),
+    "ut_topk": (C.c_int, [P, P, P, I64, I64, I32, P, P]),
+    "ut_score_round_de": (C.c_int, [P, C.POINTER(DeParams), C.POINTER(Acq), U32, I64, I64, I32,
+                                    C.POINTER(RoundOut)]),
+    "ut_round_buffers": (C.c_int, [P, C.POINTER(P), C.POINTER(P), C.POINTER(P), C.POINTER(P), C.POINTER(P),
+                                   C.POINTER(P), C.POINTER(P), C.POINTER(I64)]),
+    "ut_set_timing": (C.c_int, [P, I32]),
+    "ut_stage_time": (C.c_int, [P, C.c_char_p, C.POINTER(D)]),
+}
+
+_lock = threading.Lock()
+_lib = None
+
+
+class UthotError(RuntimeError):
+    pass
+
+
+def lib() -> C.CDLL:
+    """Load libuthot.so once; raise (never fall back) when it is unavailable."""
+    global _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise UthotError(
+                    f"{LIB_PATH} not found: build it with `python -m uptune_amd.build` "
+                    "(the uptune_amd device path has no CPU fallback)")
+            handle = C.CDLL(LIB_PATH)
+            for name, (res, args) in SIGNATURES.items():
+                fn = getattr(handle, name)
+                fn.restype = res
+                fn.argtypes = args
+            _lib = handle
+        return _lib
+
+
+def check(ctx, rc: int, what: str) -> None:
+    if rc != 0:
+        msg = lib().ut_last_error(ctx).decode(errors="replace") if ctx else ""
+        raise UthotError(f"{what} failed: {ERRORS.get(rc, rc)}: {msg}")

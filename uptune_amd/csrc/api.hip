@@ -1,0 +1,534 @@
+// api.hip -- C ABI entry points (include/uthot.h) and the host-side space
+// compiler.
+#include <algorithm>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "ut_internal.h"
+
+namespace ut {
+
+int set_err(ut_ctx* c, int code, const std::string& msg) {
+  if (c) c->err = msg;
+  return code;
+}
+
+void mark(ut_ctx* c, const char* name) {
+  if (!c->timing.on) return;
+  hipEvent_t e;
+  if (hipEventCreate(&e) != hipSuccess) return;
+  hipEventRecord(e, c->stream);
+  c->timing.marks.emplace_back(name, e);
+}
+
+static void timing_begin(ut_ctx* c) {
+  if (!c->timing.on) return;
+  for (auto& m : c->timing.marks) hipEventDestroy(m.second);
+  c->timing.marks.clear();
+  mark(c, "begin");
+}
+
+static int timing_end(ut_ctx* c) {
+  if (!c->timing.on) return 0;
+  UT_HIP(c, hipStreamSynchronize(c->stream));
+  c->timing.last.clear();
+  for (size_t i = 1; i < c->timing.marks.size(); ++i) {
+    float ms = 0.f;
+    hipEventElapsedTime(&ms, c->timing.marks[i - 1].second, c->timing.marks[i].second);
+    c->timing.last.emplace_back(c->timing.marks[i].first, (double)ms);
+  }
+  for (auto& m : c->timing.marks) hipEventDestroy(m.second);
+  c->timing.marks.clear();
+  return 0;
+}
+
+static void free_space(Space& s) {
+  if (s.d_params) hipFree(s.d_params);
+  if (s.d_order) hipFree(s.d_order);
+  if (s.d_words) hipFree(s.d_words);
+  if (s.d_block_last) hipFree(s.d_block_last);
+  if (s.d_lut) hipFree(s.d_lut);
+  s = Space();
+}
+
+// Build the fixed outer message of hash_config (manipulator.py:233-243):
+//   for i, p in enumerate(sorted params): name ++ hash_value ++ str(i) ++ "|"
+// with hash_value = "b'" hex "'" (py3, primitive) or hex.
+static int compile_hash_layout(ut_ctx* c, const std::vector<std::string>& names,
+                               const std::vector<bool>& primitive) {
+  Space& s = c->space;
+  const int32_t P = s.P;
+  std::vector<uint8_t> msg;
+  std::vector<int64_t> hole_start(P);
+  for (int32_t j = 0; j < P; ++j) {
+    const int32_t p = s.host_order[j];
+    msg.insert(msg.end(), names[p].begin(), names[p].end());
+    const bool wrap = primitive[p] && !s.py2;
+    if (wrap) { msg.push_back('b'); msg.push_back('\''); }
+    hole_start[j] = (int64_t)msg.size();
+    for (int q = 0; q < 64; ++q) msg.push_back(0);
+    if (wrap) msg.push_back('\'');
+    const std::string idx = std::to_string(j);
+    msg.insert(msg.end(), idx.begin(), idx.end());
+    msg.push_back('|');
+  }
+  const int64_t L = (int64_t)msg.size();
+  msg.push_back(0x80);
+  while (msg.size() % 64 != 56) msg.push_back(0);
+  const uint64_t bits = (uint64_t)L * 8;
+  for (int q = 7; q >= 0; --q) msg.push_back((uint8_t)(bits >> (8 * q)));
+  const int64_t NBLK = (int64_t)msg.size() / 64;
+  std::vector<HashWord> words(NBLK * 16);
+  std::vector<int16_t> block_last(NBLK);
+  int32_t j = 0;  // first hole that may overlap the current word
+  int16_t running = -1;
+  for (int64_t w = 0; w < NBLK * 16; ++w) {
+    HashWord hw;
+    hw.tmpl = ((uint32_t)msg[4 * w] << 24) | ((uint32_t)msg[4 * w + 1] << 16) | ((uint32_t)msg[4 * w + 2] << 8) |
+              (uint32_t)msg[4 * w + 3];
+    hw.hole = -1;
+    hw.q1 = 0;
+    hw.shift = 0;
+    while (j < P && hole_start[j] + 64 <= 4 * w) ++j;
+    if (j < P && hole_start[j] < 4 * w + 4 && hole_start[j] + 64 > 4 * w) {
+      const int64_t d = 4 * w - hole_start[j];           // -3 .. 63
+      const int64_t q = (d >= 0) ? d / 4 : -1;           // floor(d / 4)
+      hw.hole = (int16_t)j;
+      hw.q1 = (uint8_t)(q + 1);
+      hw.shift = (uint8_t)(d - 4 * q);
+      if (j > running) running = (int16_t)j;
+    }
+    words[w] = hw;
+    if (w % 16 == 15) block_last[w / 16] = running;
+  }
+  UT_CHECK(c, P < 32767, UT_EINVAL, "too many parameters");
+  s.outer_len = L;
+  s.outer_blocks = NBLK;
+  UT_HIP(c, hipMalloc((void**)&s.d_words, sizeof(HashWord) * words.size()));
+  UT_HIP(c, hipMemcpy(s.d_words, words.data(), sizeof(HashWord) * words.size(), hipMemcpyHostToDevice));
+  UT_HIP(c, hipMalloc((void**)&s.d_block_last, sizeof(int16_t) * block_last.size()));
+  UT_HIP(c, hipMemcpy(s.d_block_last, block_last.data(), sizeof(int16_t) * block_last.size(), hipMemcpyHostToDevice));
+  return 0;
+}
+
+static int history_alloc(ut_ctx* c, int64_t cap) {
+  int64_t p2 = 1024;
+  while (p2 < cap) p2 <<= 1;
+  if (c->hist_keys) {
+    UT_HIP(c, hipStreamSynchronize(c->stream));
+    hipFree(c->hist_keys);
+    hipFree(c->hist_state);
+  }
+  UT_HIP(c, hipMalloc((void**)&c->hist_keys, sizeof(uint32_t) * 8 * p2));
+  UT_HIP(c, hipMalloc((void**)&c->hist_state, sizeof(uint32_t) * p2));
+  UT_HIP(c, hipMemsetAsync(c->hist_state, 0, sizeof(uint32_t) * p2, c->stream));
+  c->hist_cap = p2;
+  c->hist_count = 0;
+  return 0;
+}
+
+}  // namespace ut
+
+using namespace ut;
+
+extern "C" {
+
+int ut_version(void) { return 1; }
+
+int ut_ctx_create(int device, uint64_t seed, ut_ctx** out) {
+  if (!out) return UT_EINVAL;
+  *out = nullptr;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= device || device < 0) return UT_EHIP;
+  if (hipSetDevice(device) != hipSuccess) return UT_EHIP;
+  ut_ctx* c = new ut_ctx();
+  c->device = device;
+  c->seed = seed;
+  if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return UT_EHIP;
+  }
+  c->stream = c->own_stream;
+  *out = c;
+  return 0;
+}
+
+int ut_ctx_destroy(ut_ctx* c) {
+  if (!c) return UT_EINVAL;
+  hipSetDevice(c->device);
+  hipStreamSynchronize(c->stream);
+  free_space(c->space);
+  auto fr = [](void* p) { if (p) hipFree(p); };
+  fr(c->pop); fr(c->hist_keys); fr(c->hist_state); fr(c->batch_slots);
+  fr(c->gp_Xs); fr(c->gp_xnorm); fr(c->gp_K); fr(c->gp_Linv); fr(c->gp_y); fr(c->gp_tmp);
+  fr(c->gp_alpha); fr(c->gp_inv_ell); fr(c->gp_stats); fr(c->gp_flag);
+  fr(c->kst.p); fr(c->mu_part.p); fr(c->var_part.p); fr(c->cnorm.p);
+  fr(c->r_values.p); fr(c->r_feat.p); fr(c->r_mu.p); fr(c->r_var.p); fr(c->r_score.p); fr(c->r_digest.p);
+  fr(c->r_dup.p); fr(c->tk_score[0].p); fr(c->tk_score[1].p); fr(c->tk_idx[0].p); fr(c->tk_idx[1].p);
+  fr(c->r_topk_idx.p); fr(c->r_topk_score.p);
+  for (auto& m : c->timing.marks) hipEventDestroy(m.second);
+  if (c->own_stream) hipStreamDestroy(c->own_stream);
+  delete c;
+  return 0;
+}
+
+const char* ut_last_error(ut_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+int ut_set_stream(ut_ctx* c, void* s) {
+  if (!c) return UT_EINVAL;
+  c->stream = s ? (hipStream_t)s : c->own_stream;
+  return 0;
+}
+
+int ut_sync(ut_ctx* c) {
+  if (!c) return UT_EINVAL;
+  UT_HIP(c, hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+int ut_space_define(ut_ctx* c, int32_t P, const ut_param_desc* params, int32_t py2_layout) {
+  if (!c) return UT_EINVAL;
+  UT_CHECK(c, P >= 1 && params, UT_EINVAL, "space: need at least one parameter");
+  UT_HIP(c, hipSetDevice(c->device));
+  UT_HIP(c, hipStreamSynchronize(c->stream));
+  free_space(c->space);
+  c->has_space = false;
+  Space& s = c->space;
+  s.P = P;
+  s.py2 = py2_layout ? 1 : 0;
+  s.host_params.resize(P);
+  s.host_order.assign(P, -1);
+  std::vector<std::string> names(P);
+  std::vector<bool> primitive(P);
+  std::vector<uint32_t> lut;
+  int32_t feat = 0;
+  for (int32_t p = 0; p < P; ++p) {
+    const ut_param_desc& d = params[p];
+    DevParam& q = s.host_params[p];
+    q.kind = d.kind;
+    q.lo = d.lo; q.hi = d.hi;
+    q.u_lo = d.u_lo; q.u_hi = d.u_hi; q.u_span = d.u_span;
+    q.n_opt = d.n_options;
+    q.feat_col = feat;
+    UT_CHECK(c, d.sort_rank >= 0 && d.sort_rank < P && s.host_order[d.sort_rank] == -1, UT_EINVAL,
+             "space: sort_rank must be a permutation of 0..P-1");
+    s.host_order[d.sort_rank] = p;
+    names[p] = std::string(d.name ? d.name : "", d.name ? (size_t)d.name_len : 0);
+    switch (d.kind) {
+      case UT_FLOAT: case UT_INT:
+        q.n_feat = 1; primitive[p] = true; break;
+      case UT_BOOL:
+        q.n_feat = 1; primitive[p] = false; q.n_opt = 2; break;
+      case UT_ENUM:
+        UT_CHECK(c, d.n_options >= 1, UT_EINVAL, "space: enum needs options");
+        q.n_feat = (int32_t)d.n_options; primitive[p] = false; break;
+      default:
+        return set_err(c, UT_EUNSUPPORTED, "space: parameter kind " + std::to_string(d.kind) +
+                                               " is not supported on the device path yet");
+    }
+    feat += q.n_feat;
+    if (d.lut_count > 0) {
+      UT_CHECK(c, d.lut_host != nullptr, UT_EINVAL, "space: lut_count > 0 but lut_host is NULL");
+      q.hash_mode = HM_LUT;
+      q.lut_base = (int64_t)(lut.size() / 8);
+      q.lut_n = d.lut_count;
+      for (int32_t v = 0; v < d.lut_count; ++v)
+        for (int w = 0; w < 8; ++w) {
+          const uint8_t* b = d.lut_host + (size_t)v * 32 + 4 * w;
+          lut.push_back(((uint32_t)b[0] << 24) | ((uint32_t)b[1] << 16) | ((uint32_t)b[2] << 8) | b[3]);
+        }
+    } else {
+      q.lut_base = 0;
+      q.lut_n = 0;
+      if (d.kind == UT_FLOAT) q.hash_mode = HM_FLOAT;
+      else if (d.kind == UT_INT) q.hash_mode = HM_INT;
+      else return set_err(c, UT_EINVAL, "space: BOOL/ENUM parameters need an inner-digest LUT");
+    }
+  }
+  s.n_feat = feat;
+  UT_HIP(c, hipMalloc((void**)&s.d_params, sizeof(DevParam) * P));
+  UT_HIP(c, hipMemcpy(s.d_params, s.host_params.data(), sizeof(DevParam) * P, hipMemcpyHostToDevice));
+  UT_HIP(c, hipMalloc((void**)&s.d_order, sizeof(int32_t) * P));
+  UT_HIP(c, hipMemcpy(s.d_order, s.host_order.data(), sizeof(int32_t) * P, hipMemcpyHostToDevice));
+  if (lut.empty()) lut.resize(8, 0u);
+  UT_HIP(c, hipMalloc((void**)&s.d_lut, sizeof(uint32_t) * lut.size()));
+  UT_HIP(c, hipMemcpy(s.d_lut, lut.data(), sizeof(uint32_t) * lut.size(), hipMemcpyHostToDevice));
+  int rc = compile_hash_layout(c, names, primitive);
+  if (rc) return rc;
+  c->has_space = true;
+  // a new space invalidates the population
+  if (c->pop) {
+    hipFree(c->pop);
+    c->pop = nullptr;
+    c->npop = 0;
+    c->pop_cap = 0;
+  }
+  return 0;
+}
+
+int ut_space_info(ut_ctx* c, int64_t* outer_len, int64_t* outer_blocks, int32_t* n_features) {
+  if (!c) return UT_EINVAL;
+  UT_CHECK(c, c->has_space, UT_ENOSPACE, "space not defined");
+  if (outer_len) *outer_len = c->space.outer_len;
+  if (outer_blocks) *outer_blocks = c->space.outer_blocks;
+  if (n_features) *n_features = c->space.n_feat;
+  return 0;
+}
+
+static int pop_alloc(ut_ctx* c, int64_t npop) {
+  const int64_t need = npop * c->space.P;
+  if (c->pop && c->pop_cap >= need) {
+    c->npop = npop;
+    return 0;
+  }
+  if (c->pop) {
+    UT_HIP(c, hipStreamSynchronize(c->stream));
+    hipFree(c->pop);
+  }
+  UT_HIP(c, hipMalloc((void**)&c->pop, sizeof(double) * need));
+  c->pop_cap = need;
+  c->npop = npop;
+  return 0;
+}
+
+int ut_population_init(ut_ctx* c, int64_t npop, uint32_t round_) {
+  if (!c) return UT_EINVAL;
+  UT_CHECK(c, c->has_space, UT_ENOSPACE, "space not defined");
+  UT_CHECK(c, npop >= 4 && npop < (int64_t)0xFFFFFFFF, UT_EINVAL, "population size must be in [4, 2^32)");
+  int rc = pop_alloc(c, npop);
+  if (rc) return rc;
+  return launch_population_init(c, round_);
+}
+
+int ut_population_set(ut_ctx* c, int64_t npop, const double* values, int64_t ld) {
+  if (!c) return UT_EINVAL;
+  UT_CHECK(c, c->has_space, UT_ENOSPACE, "space not defined");
+  UT_CHECK(c, npop >= 4 && npop < (int64_t)0xFFFFFFFF && values && ld >= npop, UT_EINVAL,
+           "population_set: bad arguments");
+  int rc = pop_alloc(c, npop);
+  if (rc) return rc;
+  UT_HIP(c, hipMemcpy2DAsync(c->pop, sizeof(double) * npop, values, sizeof(double) * ld, sizeof(double) * npop,
+                             c->space.P, hipMemcpyDeviceToDevice, c->stream));
+  return 0;
+}
+
+int ut_population_get(ut_ctx* c, double* values, int64_t ld) {
+  if (!c) return UT_EINVAL;
+  UT_CHECK(c, c->pop != nullptr && values && ld >= c->npop, UT_EINVAL, "population_get: bad arguments");
+  UT_HIP(c, hipMemcpy2DAsync(values, sizeof(double) * ld, c->pop, sizeof(double) * c->npop,
+                             sizeof(double) * c->npop, c->space.P, hipMemcpyDeviceToDevice, c->stream));
+  return 0;
+}
+
+int ut_propose_de(ut_ctx* c, const ut_de_params* p, uint32_t round_, int64_t cand_base, int64_t m,
+                  double* out_values, int64_t ld) {
+  if (!c) return UT_EINVAL;
+  UT_CHECK(c, c->has_space, UT_ENOSPACE, "space not defined");
+  UT_CHECK(c, c->pop != nullptr, UT_EINVAL, "propose_de: population not initialised");
+  UT_CHECK(c, p && p->n_cross >= 0 && p->n_cross <= 4, UT_EINVAL, "propose_de: n_cross must be in [0, 4]");
+  UT_CHECK(c, m >= 0 && cand_base >= 0 && out_values && ld >= m, UT_EINVAL, "propose_de: bad arguments");
+  if (m == 0) return 0;
+  return launch_de(c, p, round_, cand_base, m, out_values, ld);
+}
+
+int ut_encode_features(ut_ctx* c, const double* values, int64_t ld, int64_t m, double* feat, int64_t ldf) {
+  if (!c) return UT_EINVAL;
+  UT_CHECK(c, c->has_space, UT_ENOSPACE, "space not defined");
+  UT_CHECK(c, values && feat && ld >= m && ldf >= m, UT_EINVAL, "encode: bad arguments");
+  if (m == 0) return 0;
+  return launch_encode(c, values, ld, m, feat, ldf);
+}
+
+int ut_hash(ut_ctx* c, const double* values, int64_t ld, int64_t m, uint32_t* out) {
+  if (!c) return UT_EINVAL;
+  UT_CHECK(c, c->has_space, UT_ENOSPACE, "space not defined");
+  UT_CHECK(c, values && out && ld >= m && m >= 0, UT_EINVAL, "hash: bad arguments");
+  return launch_hash(c, values, ld, m, out);
+}
+
+int ut_history_reset(ut_ctx* c, int64_t capacity) {
+  if (!c) return UT_EINVAL;
+  UT_CHECK(c, capacity >= 0, UT_EINVAL, "history capacity < 0");
+  return history_alloc(c, capacity * 2 > 1024 ? capacity * 2 : 1024);
+}
+
+int ut_history_add(ut_ctx* c, const uint32_t* dig, int64_t n) {
+  if (!c) return UT_EINVAL;
+  if (n <= 0) return 0;
+  UT_CHECK(c, dig != nullptr, UT_EINVAL, "history_add: NULL digests");
+  if (!c->hist_keys || (c->hist_count + n) * 2 > c->hist_cap) {
+    // grow: rebuild is not needed for correctness of membership if we keep
+    // the old entries, so re-insert by copying old keys
+    const int64_t old_cap = c->hist_cap;
+    uint32_t* old_keys = c->hist_keys;
+    uint32_t* old_state = c->hist_state;
+    const int64_t old_count = c->hist_count;
+    c->hist_keys = nullptr;
+    c->hist_state = nullptr;
+    int64_t want = (old_count + n) * 4;
+    int64_t p2 = 1024;
+    while (p2 < want) p2 <<= 1;
+    UT_HIP(c, hipMalloc((void**)&c->hist_keys, sizeof(uint32_t) * 8 * p2));
+    UT_HIP(c, hipMalloc((void**)&c->hist_state, sizeof(uint32_t) * p2));
+    UT_HIP(c, hipMemsetAsync(c->hist_state, 0, sizeof(uint32_t) * p2, c->stream));
+    c->hist_cap = p2;
+    c->hist_count = 0;
+    if (old_keys) {
+      int rc = launch_hist_rehash(c, old_keys, old_state, old_cap);
+      UT_HIP(c, hipStreamSynchronize(c->stream));
+      hipFree(old_keys);
+      hipFree(old_state);
+      if (rc) return rc;
+      c->hist_count = old_count;
+    }
+  }
+  int rc = launch_hist_insert(c, dig, n);
+  if (rc) return rc;
+  c->hist_count += n;
+  return 0;
+}
+
+int ut_history_add_host(ut_ctx* c, const uint32_t* dig, int64_t n) {
+  if (!c) return UT_EINVAL;
+  if (n <= 0) return 0;
+  UT_CHECK(c, dig != nullptr, UT_EINVAL, "history_add_host: NULL digests");
+  uint32_t* tmp = nullptr;
+  UT_HIP(c, hipMalloc((void**)&tmp, sizeof(uint32_t) * 8 * n));
+  UT_HIP(c, hipMemcpyAsync(tmp, dig, sizeof(uint32_t) * 8 * n, hipMemcpyHostToDevice, c->stream));
+  int rc = ut_history_add(c, tmp, n);
+  UT_HIP(c, hipStreamSynchronize(c->stream));
+  hipFree(tmp);
+  return rc;
+}
+
+int ut_dedup(ut_ctx* c, const uint32_t* dig, int64_t m, uint8_t* dup) {
+  if (!c) return UT_EINVAL;
+  UT_CHECK(c, dig && dup && m >= 0, UT_EINVAL, "dedup: bad arguments");
+  return launch_dedup(c, dig, m, dup);
+}
+
+int ut_gp_fit(ut_ctx* c, const double* X, const double* y, int32_t n, int32_t d, const ut_gp_hyper* h) {
+  if (!c) return UT_EINVAL;
+  UT_HIP(c, hipSetDevice(c->device));
+  return gp_fit_impl(c, X, y, n, d, h);
+}
+
+int ut_gp_score(ut_ctx* c, const double* feat, int64_t ld, int64_t m, const ut_acq* acq, const uint8_t* dup,
+                double* mu, double* var, double* score) {
+  if (!c) return UT_EINVAL;
+  UT_CHECK(c, feat && ld >= m && m >= 0, UT_EINVAL, "gp_score: bad arguments");
+  return gp_score_impl(c, feat, ld, m, acq, dup, mu, var, score);
+}
+
+int ut_gp_stats(ut_ctx* c, double* f_best, double* y_mean, double* y_std) {
+  if (!c) return UT_EINVAL;
+  UT_CHECK(c, c->gp_ready, UT_EINVAL, "gp_stats: no fitted GP");
+  double st[4];
+  UT_HIP(c, hipMemcpyAsync(st, c->gp_stats, sizeof(double) * 3, hipMemcpyDeviceToHost, c->stream));
+  UT_HIP(c, hipStreamSynchronize(c->stream));
+  if (f_best) *f_best = st[0];
+  if (y_mean) *y_mean = st[1];
+  if (y_std) *y_std = st[2];
+  return 0;
+}
+
+int ut_topk(ut_ctx* c, const double* score, const uint8_t* dup, int64_t m, int64_t cand_base, int32_t k,
+            int64_t* out_idx, double* out_score) {
+  if (!c) return UT_EINVAL;
+  UT_CHECK(c, score || m == 0, UT_EINVAL, "topk: NULL score");
+  return topk_impl(c, score, dup, m, cand_base, k, out_idx, out_score);
+}
+
+int ut_score_round_de(ut_ctx* c, const ut_de_params* de, const ut_acq* acq, uint32_t round_, int64_t cand_base,
+                      int64_t m, int32_t k, const ut_round_out* out) {
+  if (!c) return UT_EINVAL;
+  UT_CHECK(c, c->has_space, UT_ENOSPACE, "space not defined");
+  UT_CHECK(c, c->pop != nullptr, UT_EINVAL, "score_round: population not initialised");
+  UT_CHECK(c, c->gp_ready, UT_EINVAL, "score_round: call ut_gp_fit first");
+  UT_CHECK(c, c->gp_d == c->space.n_feat, UT_EINVAL, "score_round: GP feature width != space feature width");
+  UT_CHECK(c, m >= 1 && de && acq, UT_EINVAL, "score_round: bad arguments");
+  const int64_t ld = ((m + 127) / 128) * 128;
+  const int32_t P = c->space.P, F = c->space.n_feat;
+  int rc;
+  if ((rc = ensure(c, c->r_values, (size_t)P * ld))) return rc;
+  if ((rc = ensure(c, c->r_feat, (size_t)F * ld))) return rc;
+  if ((rc = ensure(c, c->r_digest, (size_t)8 * ld))) return rc;
+  if ((rc = ensure(c, c->r_dup, (size_t)ld))) return rc;
+  if ((rc = ensure(c, c->r_mu, (size_t)ld))) return rc;
+  if ((rc = ensure(c, c->r_var, (size_t)ld))) return rc;
+  if ((rc = ensure(c, c->r_score, (size_t)ld))) return rc;
+  if ((rc = ensure(c, c->r_topk_idx, (size_t)k))) return rc;
+  if ((rc = ensure(c, c->r_topk_score, (size_t)k))) return rc;
+  c->r_ld = ld;
+  c->r_m = m;
+  timing_begin(c);
+  if ((rc = ut_propose_de(c, de, round_, cand_base, m, c->r_values.p, ld))) return rc;
+  mark(c, "propose");
+  if ((rc = launch_hash(c, c->r_values.p, ld, m, c->r_digest.p))) return rc;
+  mark(c, "hash");
+  if ((rc = launch_dedup(c, c->r_digest.p, m, c->r_dup.p))) return rc;
+  mark(c, "dedup");
+  if ((rc = launch_encode(c, c->r_values.p, ld, m, c->r_feat.p, ld))) return rc;
+  mark(c, "encode");
+  if ((rc = gp_score_impl(c, c->r_feat.p, ld, m, acq, c->r_dup.p, c->r_mu.p, c->r_var.p, c->r_score.p))) return rc;
+  if ((rc = topk_impl(c, c->r_score.p, c->r_dup.p, m, cand_base, k, c->r_topk_idx.p, c->r_topk_score.p)))
+    return rc;
+  mark(c, "topk");
+  if (out) {
+    if (out->topk_idx)
+      UT_HIP(c, hipMemcpyAsync(out->topk_idx, c->r_topk_idx.p, sizeof(int64_t) * k, hipMemcpyDeviceToDevice,
+                               c->stream));
+    if (out->topk_score)
+      UT_HIP(c, hipMemcpyAsync(out->topk_score, c->r_topk_score.p, sizeof(double) * k, hipMemcpyDeviceToDevice,
+                               c->stream));
+    if (out->topk_values || out->topk_digest) {
+      double* vals = out->topk_values;
+      ut::DevBuf<double> tmp;
+      if (!vals) {
+        if ((rc = ensure(c, tmp, (size_t)P * k))) return rc;
+        vals = tmp.p;
+      }
+      rc = launch_gather_rows(c, c->r_values.p, ld, c->r_topk_idx.p, cand_base, k, vals, k, c->r_digest.p,
+                              out->topk_digest);
+      if (tmp.p) {
+        UT_HIP(c, hipStreamSynchronize(c->stream));
+        hipFree(tmp.p);
+      }
+      if (rc) return rc;
+    }
+  }
+  return timing_end(c);
+}
+
+int ut_round_buffers(ut_ctx* c, double** values, double** features, uint32_t** digests, uint8_t** dup,
+                     double** mu, double** var, double** score, int64_t* ld) {
+  if (!c) return UT_EINVAL;
+  if (values) *values = c->r_values.p;
+  if (features) *features = c->r_feat.p;
+  if (digests) *digests = c->r_digest.p;
+  if (dup) *dup = c->r_dup.p;
+  if (mu) *mu = c->r_mu.p;
+  if (var) *var = c->r_var.p;
+  if (score) *score = c->r_score.p;
+  if (ld) *ld = c->r_ld;
+  return 0;
+}
+
+int ut_set_timing(ut_ctx* c, int32_t on) {
+  if (!c) return UT_EINVAL;
+  c->timing.on = on != 0;
+  return 0;
+}
+
+int ut_stage_time(ut_ctx* c, const char* stage, double* ms) {
+  if (!c || !stage || !ms) return UT_EINVAL;
+  for (auto& e : c->timing.last)
+    if (e.first == stage) {
+      *ms = e.second;
+      return 0;
+    }
+  return set_err(c, UT_EINVAL, std::string("no timing for stage ") + stage);
+}
+
+}  // extern "C"

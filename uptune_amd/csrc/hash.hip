@@ -1,0 +1,138 @@
+// hash.hip -- batched ConfigurationManipulator.hash_config on gfx950.
+//
+// Reference (manipulator.py:233-243, :456-459, :855-858):
+//   m = sha256()
+//   for i, p in enumerate(sorted(params, key=name)):
+//     m.update(str(p.name)); m.update(str(p.hash_value(cfg))); m.update(str(i)); m.update(b"|")
+// where hash_value is sha256(repr(value)).hexdigest() -- wrapped as "b'...'"
+// for primitive params by uptune's Python-3 port (str() of a bytes object).
+//
+// For a given space the outer message has a FIXED length: only the 64 hex
+// characters of each inner digest vary.  The host therefore compiles the
+// message into a table of 32-bit words (constant template bits + which hex
+// "hole" overlaps the word and at what byte shift); the kernel streams the
+// outer SHA-256 blocks word by word, producing each parameter's inner digest
+// just before its hole is first needed.
+//
+// Inner digests: discrete values (ENUM, BOOL, small-range INT) come from a
+// host-built LUT; FLOAT values are formatted on the device with Python's
+// shortest round-trip repr (ut_core.h) and hashed (one SHA-256 block);
+// large-range INT values use repr(int).
+//
+// One lane = one candidate.  Per-lane byte strings and hex words live in LDS
+// in [word][lane] layout (bank-conflict-free, no cross-lane traffic, so no
+// barriers).  Bound: integer VALU (~1.4k ops per SHA-256 compression).
+#include "ut_internal.h"
+
+namespace ut {
+
+constexpr int HASH_NT = 128;
+constexpr int SCR_WORDS = 7;                       // inner message bytes 0..27
+constexpr int HEX_WORDS = 18;                      // [0]=0, [1..16]=hex, [17]=0
+constexpr int LDS_WORDS = SCR_WORDS + 2 * HEX_WORDS;
+
+struct LdsEmit {
+  uint8_t* base;  // &lds[0] as bytes
+  int lane;
+  __device__ __forceinline__ void put(int pos, uint8_t ch) {
+    base[(((pos >> 2) * HASH_NT + lane) << 2) + (pos & 3)] = ch;
+  }
+};
+
+__device__ __forceinline__ void inner_digest(const DevParam& pr, double v, const uint32_t* __restrict__ lut,
+                                             uint32_t* lds, int lane, uint32_t D[8]) {
+  if (pr.hash_mode == HM_LUT) {
+    int64_t idx;
+    if (pr.kind == UT_ENUM || pr.kind == UT_BOOL) idx = (int64_t)v;
+    else idx = (int64_t)(v - pr.lo);
+    idx = idx < 0 ? 0 : (idx >= pr.lut_n ? pr.lut_n - 1 : idx);  // never fault on garbage input
+    const uint4* src = reinterpret_cast<const uint4*>(lut + (pr.lut_base + idx) * 8);
+    const uint4 a = src[0], b = src[1];
+    D[0] = a.x; D[1] = a.y; D[2] = a.z; D[3] = a.w;
+    D[4] = b.x; D[5] = b.y; D[6] = b.z; D[7] = b.w;
+    return;
+  }
+#pragma unroll
+  for (int w = 0; w < SCR_WORDS; ++w) lds[w * HASH_NT + lane] = 0u;
+  LdsEmit e{reinterpret_cast<uint8_t*>(lds), lane};
+  int len;
+  if (pr.hash_mode == HM_FLOAT) len = repr_double(v, e);
+  else len = repr_int64((int64_t)v, e);
+  e.put(len, 0x80);
+  uint32_t W[16];
+#pragma unroll
+  for (int w = 0; w < SCR_WORDS; ++w) W[w] = __builtin_bswap32(lds[w * HASH_NT + lane]);
+#pragma unroll
+  for (int w = SCR_WORDS; w < 15; ++w) W[w] = 0u;
+  W[15] = (uint32_t)len * 8u;
+  sha256_init(D);
+  sha256_compress(D, W);
+}
+
+__global__ __launch_bounds__(HASH_NT) void k_hash(const DevParam* __restrict__ params,
+                                                  const int32_t* __restrict__ order,
+                                                  const HashWord* __restrict__ words,
+                                                  const int16_t* __restrict__ block_last, int32_t nblocks,
+                                                  const uint32_t* __restrict__ lut, const double* __restrict__ values,
+                                                  int64_t ld, int64_t m, uint32_t* __restrict__ out) {
+  __shared__ uint32_t lds[LDS_WORDS * HASH_NT];
+  const int lane = threadIdx.x;
+  const int64_t i0 = (int64_t)blockIdx.x * HASH_NT + lane;
+  const bool valid = i0 < m;
+  const int64_t i = valid ? i0 : (m - 1);
+  uint32_t* hexs = lds + SCR_WORDS * HASH_NT;
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    hexs[(s * HEX_WORDS + 0) * HASH_NT + lane] = 0u;
+    hexs[(s * HEX_WORDS + 17) * HASH_NT + lane] = 0u;
+  }
+  uint32_t H[8];
+  sha256_init(H);
+  int32_t next = 0;
+  for (int32_t b = 0; b < nblocks; ++b) {
+    const int32_t last = block_last[b];
+    while (next <= last) {
+      const int32_t p = order[next];
+      const DevParam pr = params[p];
+      const double v = values[(int64_t)p * ld + i];
+      uint32_t D[8];
+      inner_digest(pr, v, lut, lds, lane, D);
+      uint32_t HX[16];
+      digest_hex(D, HX);
+      uint32_t* slot = hexs + (next & 1) * HEX_WORDS * HASH_NT;
+#pragma unroll
+      for (int w = 0; w < 16; ++w) slot[(w + 1) * HASH_NT + lane] = HX[w];
+      ++next;
+    }
+    uint32_t W[16];
+    const HashWord* hw = words + (int64_t)b * 16;
+#pragma unroll
+    for (int w = 0; w < 16; ++w) {
+      const HashWord e = hw[w];
+      uint32_t x = e.tmpl;
+      if (e.hole >= 0) {
+        const uint32_t* slot = hexs + (e.hole & 1) * HEX_WORDS * HASH_NT;
+        const uint64_t cat = ((uint64_t)slot[e.q1 * HASH_NT + lane] << 32) | slot[(e.q1 + 1) * HASH_NT + lane];
+        x |= (uint32_t)((cat << (8 * e.shift)) >> 32);
+      }
+      W[w] = x;
+    }
+    sha256_compress(H, W);
+  }
+  if (valid) {
+    uint4* dst = reinterpret_cast<uint4*>(out + i * 8);
+    dst[0] = make_uint4(H[0], H[1], H[2], H[3]);
+    dst[1] = make_uint4(H[4], H[5], H[6], H[7]);
+  }
+}
+
+int launch_hash(ut_ctx* c, const double* values, int64_t ld, int64_t m, uint32_t* out) {
+  if (m <= 0) return 0;
+  const Space& s = c->space;
+  hipLaunchKernelGGL(k_hash, dim3(grid1(m, HASH_NT)), dim3(HASH_NT), 0, c->stream, s.d_params, s.d_order,
+                     s.d_words, s.d_block_last, (int32_t)s.outer_blocks, s.d_lut, values, ld, m, out);
+  UT_LAUNCH_CHECK(c);
+  return 0;
+}
+
+}  // namespace ut

@@ -1,0 +1,59 @@
+// Host (g++) build of ut_core.h, used ONLY by tests/test_core_host.py to
+// check the shared arithmetic against CPython (repr, hashlib) without a GPU.
+// Nothing in the product path loads this library.
+#include <stddef.h>
+#include <string.h>
+#include "ut_core.h"
+
+namespace {
+struct BufEmit {
+  char* p;
+  void put(int pos, uint8_t c) { p[pos] = (char)c; }
+};
+}  // namespace
+
+extern "C" {
+int uthc_repr_double(double x, char* out) {
+  BufEmit e{out};
+  return ut::repr_double(x, e);
+}
+int uthc_repr_int64(long long v, char* out) {
+  BufEmit e{out};
+  return ut::repr_int64((int64_t)v, e);
+}
+void uthc_sha256(const unsigned char* msg, size_t len, unsigned char* out32) {
+  uint32_t H[8];
+  ut::sha256_init(H);
+  size_t total = len + 9;
+  size_t nblk = (total + 63) / 64;
+  for (size_t b = 0; b < nblk; ++b) {
+    uint32_t W[16];
+    for (int w = 0; w < 16; ++w) {
+      uint32_t v = 0;
+      for (int t = 0; t < 4; ++t) {
+        size_t pos = b * 64 + w * 4 + t;
+        uint32_t byte;
+        if (pos < len) byte = msg[pos];
+        else if (pos == len) byte = 0x80;
+        else if (pos >= nblk * 64 - 8) byte = (uint32_t)(((unsigned long long)len * 8) >> (8 * (nblk * 64 - 1 - pos))) & 0xFF;
+        else byte = 0;
+        v = (v << 8) | byte;
+      }
+      W[w] = v;
+    }
+    ut::sha256_compress(H, W);
+  }
+  for (int i = 0; i < 8; ++i)
+    for (int t = 0; t < 4; ++t) out32[i * 4 + t] = (unsigned char)(H[i] >> (24 - 8 * t));
+}
+void uthc_philox(unsigned long long seed, unsigned long long cand, unsigned stream, unsigned round_, unsigned op,
+                 unsigned* out4) {
+  ut::u32x4 r = ut::draw(seed, cand, stream, round_, op);
+  out4[0] = r.x; out4[1] = r.y; out4[2] = r.z; out4[3] = r.w;
+}
+void uthc_philox_raw(const unsigned* ctr4, const unsigned* key2, unsigned* out4) {
+  ut::u32x4 c{ctr4[0], ctr4[1], ctr4[2], ctr4[3]};
+  ut::u32x4 r = ut::philox4x32_10(c, key2[0], key2[1]);
+  out4[0] = r.x; out4[1] = r.y; out4[2] = r.z; out4[3] = r.w;
+}
+}

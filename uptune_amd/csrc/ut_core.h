@@ -1,0 +1,485 @@
+// ut_core.h -- arithmetic shared by the gfx950 kernels and the host-side
+// self-check build: Philox4x32-10 counter RNG, SHA-256, and Python's
+// shortest-round-trip repr(float) (Ryu-style digit generation + CPython's
+// 'r' formatting rules).
+//
+// Everything here is written for 64-wide CDNA4 wavefronts first (no
+// dynamic register indexing, branch-light integer code) and also compiles
+// as plain C++ with g++ so the same code can be checked against CPython on
+// the host (tests/test_core_host.py).
+//
+// Reference semantics restated here:
+//   * hash_value / hash_config string layout:
+//       python/uptune/opentuner/search/manipulator.py:233-243 (outer message)
+//       python/uptune/opentuner/search/manipulator.py:456-459 (primitive inner)
+//       python/uptune/opentuner/search/manipulator.py:855-858 (complex inner)
+//   * repr(float) = CPython Python/pystrtod.c format_float_short, mode 'r'
+//     (exponent form iff decpt <= -4 or decpt > 16, ".0" added to integral
+//     values, "%+.02d" exponent).
+#pragma once
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#define UT_HD __host__ __device__ __forceinline__
+#define UT_CONST_TABLE static constexpr
+#else
+#define UT_HD static inline
+#define UT_CONST_TABLE static constexpr
+#endif
+
+#include "ryu_tables.h"
+
+namespace ut {
+
+// ---------------------------------------------------------------------------
+// 64x64 -> 128 helpers
+// ---------------------------------------------------------------------------
+UT_HD uint64_t umulhi64(uint64_t a, uint64_t b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __umul64hi(a, b);
+#else
+  return (uint64_t)(((unsigned __int128)a * b) >> 64);
+#endif
+}
+
+UT_HD uint32_t umulhi32(uint32_t a, uint32_t b) {
+  return (uint32_t)(((uint64_t)a * b) >> 32);
+}
+
+// ---------------------------------------------------------------------------
+// Philox4x32-10 (Salmon et al., SC'11).  Key = 2x32, counter = 4x32.
+// ---------------------------------------------------------------------------
+struct u32x4 {
+  uint32_t x, y, z, w;
+};
+
+UT_HD u32x4 philox4x32_10(u32x4 c, uint32_t k0, uint32_t k1) {
+  const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u;
+  const uint32_t W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint64_t p0 = (uint64_t)M0 * c.x;
+    const uint64_t p1 = (uint64_t)M1 * c.z;
+    const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+    const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+    u32x4 n;
+    n.x = hi1 ^ c.y ^ k0;
+    n.y = lo1;
+    n.z = hi0 ^ c.w ^ k1;
+    n.w = lo0;
+    c = n;
+    k0 += W0;
+    k1 += W1;
+  }
+  return c;
+}
+
+// uniform double in [0,1) with 53 random bits from two 32-bit words
+UT_HD double u01_from(uint32_t lo, uint32_t hi) {
+  const uint64_t v = (((uint64_t)hi << 32) | lo) >> 11;
+  return (double)v * (1.0 / 9007199254740992.0);
+}
+UT_HD uint64_t u64_from(uint32_t lo, uint32_t hi) { return ((uint64_t)hi << 32) | lo; }
+// floor(x * n / 2^64): an integer in [0, n)
+UT_HD uint64_t below64(uint64_t x, uint64_t n) { return umulhi64(x, n); }
+
+// Counter layout shared by every kernel and by oracle/philox.py:
+//   c.x, c.y = global candidate index (lo, hi)
+//   c.z      = stream (param index p, or STREAM_* | sub)
+//   c.w      = (round << 8) | op
+enum : uint32_t {
+  OP_INIT = 1, OP_DE = 2, OP_PSO = 3, OP_GA = 4, OP_GGA = 5,
+};
+enum : uint32_t {
+  STREAM_CAND = 0xFFFF0000u,   // per-candidate draws: STREAM_CAND | k
+  STREAM_RETRY_SHIFT = 20,     // per-param draws at GA retry r: p | (r << 20)
+  STREAM_SUB_SHIFT = 28,       // second block of per-param draws: p | (s << 28)
+};
+
+UT_HD u32x4 draw(uint64_t seed, uint64_t cand, uint32_t stream, uint32_t round_, uint32_t op) {
+  u32x4 c;
+  c.x = (uint32_t)cand;
+  c.y = (uint32_t)(cand >> 32);
+  c.z = stream;
+  c.w = (round_ << 8) | (op & 0xFFu);
+  return philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+}
+
+// ---------------------------------------------------------------------------
+// SHA-256 (FIPS 180-4)
+// ---------------------------------------------------------------------------
+UT_CONST_TABLE uint32_t SHA256_K[64] = {
+    0x428a2f98u, 0x71374491u, 0xb5c0fbcfu, 0xe9b5dba5u, 0x3956c25bu, 0x59f111f1u, 0x923f82a4u, 0xab1c5ed5u,
+    0xd807aa98u, 0x12835b01u, 0x243185beu, 0x550c7dc3u, 0x72be5d74u, 0x80deb1feu, 0x9bdc06a7u, 0xc19bf174u,
+    0xe49b69c1u, 0xefbe4786u, 0x0fc19dc6u, 0x240ca1ccu, 0x2de92c6fu, 0x4a7484aau, 0x5cb0a9dcu, 0x76f988dau,
+    0x983e5152u, 0xa831c66du, 0xb00327c8u, 0xbf597fc7u, 0xc6e00bf3u, 0xd5a79147u, 0x06ca6351u, 0x14292967u,
+    0x27b70a85u, 0x2e1b2138u, 0x4d2c6dfcu, 0x53380d13u, 0x650a7354u, 0x766a0abbu, 0x81c2c92eu, 0x92722c85u,
+    0xa2bfe8a1u, 0xa81a664bu, 0xc24b8b70u, 0xc76c51a3u, 0xd192e819u, 0xd6990624u, 0xf40e3585u, 0x106aa070u,
+    0x19a4c116u, 0x1e376c08u, 0x2748774cu, 0x34b0bcb5u, 0x391c0cb3u, 0x4ed8aa4au, 0x5b9cca4fu, 0x682e6ff3u,
+    0x748f82eeu, 0x78a5636fu, 0x84c87814u, 0x8cc70208u, 0x90befffau, 0xa4506cebu, 0xbef9a3f7u, 0xc67178f2u};
+
+UT_HD uint32_t rotr32(uint32_t x, int n) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_alignbit(x, x, n);
+#else
+  return (x >> n) | (x << (32 - n));
+#endif
+}
+
+UT_HD void sha256_init(uint32_t H[8]) {
+  H[0] = 0x6a09e667u; H[1] = 0xbb67ae85u; H[2] = 0x3c6ef372u; H[3] = 0xa54ff53au;
+  H[4] = 0x510e527fu; H[5] = 0x9b05688cu; H[6] = 0x1f83d9abu; H[7] = 0x5be0cd19u;
+}
+
+// One compression.  W holds the 16 big-endian message words and is consumed
+// (used as the rolling schedule), so callers pass a scratch copy.
+UT_HD void sha256_compress(uint32_t H[8], uint32_t W[16]) {
+  uint32_t a = H[0], b = H[1], c = H[2], d = H[3], e = H[4], f = H[5], g = H[6], h = H[7];
+#pragma unroll
+  for (int t = 0; t < 64; ++t) {
+    uint32_t w;
+    if (t < 16) {
+      w = W[t];
+    } else {
+      const uint32_t w15 = W[(t - 15) & 15], w2 = W[(t - 2) & 15];
+      const uint32_t s0 = rotr32(w15, 7) ^ rotr32(w15, 18) ^ (w15 >> 3);
+      const uint32_t s1 = rotr32(w2, 17) ^ rotr32(w2, 19) ^ (w2 >> 10);
+      w = W[t & 15] + s0 + W[(t - 7) & 15] + s1;
+      W[t & 15] = w;
+    }
+    const uint32_t S1 = rotr32(e, 6) ^ rotr32(e, 11) ^ rotr32(e, 25);
+    const uint32_t ch = (e & f) ^ (~e & g);
+    const uint32_t t1 = h + S1 + ch + SHA256_K[t] + w;
+    const uint32_t S0 = rotr32(a, 2) ^ rotr32(a, 13) ^ rotr32(a, 22);
+    const uint32_t mj = (a & b) ^ (a & c) ^ (b & c);
+    const uint32_t t2 = S0 + mj;
+    h = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
+  }
+  H[0] += a; H[1] += b; H[2] += c; H[3] += d; H[4] += e; H[5] += f; H[6] += g; H[7] += h;
+}
+
+// Two message words of lowercase hex for the 16-bit value v (big-endian chars).
+UT_HD uint32_t hex4(uint32_t v16) {
+  uint32_t x = ((v16 & 0xF000u) << 12) | ((v16 & 0x0F00u) << 8) | ((v16 & 0x00F0u) << 4) | (v16 & 0x000Fu);
+  const uint32_t ge10 = ((x + 0x06060606u) >> 4) & 0x01010101u;
+  return x + 0x30303030u + ge10 * 39u;
+}
+
+// digest (8 big-endian words) -> 16 big-endian words of 64 hex chars
+UT_HD void digest_hex(const uint32_t D[8], uint32_t HX[16]) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    HX[2 * i] = hex4(D[i] >> 16);
+    HX[2 * i + 1] = hex4(D[i] & 0xFFFFu);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Shortest round-trip decimal digits of a double (Ryu d2d).
+// ---------------------------------------------------------------------------
+UT_HD uint32_t pow5bits(int32_t e) { return (uint32_t)(((uint32_t)e * 1217359u) >> 19) + 1u; }
+UT_HD uint32_t log10Pow2(int32_t e) { return ((uint32_t)e * 78913u) >> 18; }
+UT_HD uint32_t log10Pow5(int32_t e) { return ((uint32_t)e * 732923u) >> 20; }
+
+UT_HD uint32_t pow5Factor(uint64_t v) {
+  uint32_t count = 0;
+  for (;;) {
+    const uint64_t q = v / 5;
+    const uint32_t r = (uint32_t)(v - 5 * q);
+    if (r != 0) break;
+    v = q;
+    ++count;
+  }
+  return count;
+}
+UT_HD bool multipleOfPowerOf5(uint64_t v, uint32_t p) { return pow5Factor(v) >= p; }
+UT_HD bool multipleOfPowerOf2(uint64_t v, uint32_t p) { return (v & ((1ull << p) - 1)) == 0; }
+
+// (m * (mulHi*2^64 + mulLo)) >> j, j >= 64
+UT_HD uint64_t mulShift64(uint64_t m, uint64_t mulLo, uint64_t mulHi, int32_t j) {
+  const uint64_t b0hi = umulhi64(m, mulLo);
+  const uint64_t b2lo = m * mulHi;
+  const uint64_t b2hi = umulhi64(m, mulHi);
+  // (b0hi + b2) as 128 bits
+  const uint64_t lo = b0hi + b2lo;
+  const uint64_t hi = b2hi + (lo < b0hi ? 1u : 0u);
+  const int32_t s = j - 64;  // 0 < s < 64 for all reachable inputs
+  return (lo >> s) | (hi << (64 - s));
+}
+
+struct Dec64 {
+  uint64_t mantissa;  // decimal digits as an integer
+  int32_t exponent;   // value = mantissa * 10^exponent
+};
+
+UT_HD uint32_t decimal_length17(uint64_t v) {
+  uint32_t n = 1;
+  uint64_t p = 10;
+  for (int i = 0; i < 16; ++i) {
+    n += (v >= p) ? 1u : 0u;
+    p *= 10;
+  }
+  return n;
+}
+
+// ieee mantissa/exponent -> shortest decimal (value must be finite, non-zero)
+UT_HD Dec64 d2d(uint64_t ieeeMantissa, uint32_t ieeeExponent) {
+  int32_t e2;
+  uint64_t m2;
+  if (ieeeExponent == 0) {
+    e2 = 1 - 1023 - 52 - 2;
+    m2 = ieeeMantissa;
+  } else {
+    e2 = (int32_t)ieeeExponent - 1023 - 52 - 2;
+    m2 = (1ull << 52) | ieeeMantissa;
+  }
+  const bool even = (m2 & 1) == 0;
+  const bool acceptBounds = even;
+  const uint64_t mv = 4 * m2;
+  const uint32_t mmShift = (ieeeMantissa != 0 || ieeeExponent <= 1) ? 1u : 0u;
+
+  uint64_t vr, vp, vm;
+  int32_t e10;
+  bool vmIsTrailingZeros = false;
+  bool vrIsTrailingZeros = false;
+  if (e2 >= 0) {
+    const uint32_t q = log10Pow2(e2) - (e2 > 3 ? 1u : 0u);
+    e10 = (int32_t)q;
+    const int32_t k = 125 + (int32_t)pow5bits((int32_t)q) - 1;
+    const int32_t i = -e2 + (int32_t)q + k;
+    const uint64_t lo = UT_POW5_INV_SPLIT[q][0], hi = UT_POW5_INV_SPLIT[q][1];
+    vr = mulShift64(mv, lo, hi, i);
+    vp = mulShift64(mv + 2, lo, hi, i);
+    vm = mulShift64(mv - 1 - mmShift, lo, hi, i);
+    if (q <= 21) {
+      const uint32_t mvMod5 = (uint32_t)(mv - 5 * (mv / 5));
+      if (mvMod5 == 0) {
+        vrIsTrailingZeros = multipleOfPowerOf5(mv, q);
+      } else if (acceptBounds) {
+        vmIsTrailingZeros = multipleOfPowerOf5(mv - 1 - mmShift, q);
+      } else {
+        vp -= multipleOfPowerOf5(mv + 2, q) ? 1u : 0u;
+      }
+    }
+  } else {
+    const uint32_t q = log10Pow5(-e2) - (-e2 > 1 ? 1u : 0u);
+    e10 = (int32_t)q + e2;
+    const int32_t i = -e2 - (int32_t)q;
+    const int32_t k = (int32_t)pow5bits(i) - 125;
+    const int32_t j = (int32_t)q - k;
+    const uint64_t lo = UT_POW5_SPLIT[i][0], hi = UT_POW5_SPLIT[i][1];
+    vr = mulShift64(mv, lo, hi, j);
+    vp = mulShift64(mv + 2, lo, hi, j);
+    vm = mulShift64(mv - 1 - mmShift, lo, hi, j);
+    if (q <= 1) {
+      vrIsTrailingZeros = true;
+      if (acceptBounds) {
+        vmIsTrailingZeros = mmShift == 1;
+      } else {
+        --vp;
+      }
+    } else if (q < 63) {
+      vrIsTrailingZeros = multipleOfPowerOf2(mv, q);
+    }
+  }
+
+  int32_t removed = 0;
+  uint32_t lastRemovedDigit = 0;
+  uint64_t output;
+  if (vmIsTrailingZeros || vrIsTrailingZeros) {
+    for (;;) {
+      const uint64_t vpDiv10 = vp / 10;
+      const uint64_t vmDiv10 = vm / 10;
+      if (vpDiv10 <= vmDiv10) break;
+      const uint32_t vmMod10 = (uint32_t)(vm - 10 * vmDiv10);
+      const uint64_t vrDiv10 = vr / 10;
+      const uint32_t vrMod10 = (uint32_t)(vr - 10 * vrDiv10);
+      vmIsTrailingZeros &= vmMod10 == 0;
+      vrIsTrailingZeros &= lastRemovedDigit == 0;
+      lastRemovedDigit = vrMod10;
+      vr = vrDiv10; vp = vpDiv10; vm = vmDiv10;
+      ++removed;
+    }
+    if (vmIsTrailingZeros) {
+      for (;;) {
+        const uint64_t vmDiv10 = vm / 10;
+        const uint32_t vmMod10 = (uint32_t)(vm - 10 * vmDiv10);
+        if (vmMod10 != 0) break;
+        const uint64_t vpDiv10 = vp / 10;
+        const uint64_t vrDiv10 = vr / 10;
+        const uint32_t vrMod10 = (uint32_t)(vr - 10 * vrDiv10);
+        vrIsTrailingZeros &= lastRemovedDigit == 0;
+        lastRemovedDigit = vrMod10;
+        vr = vrDiv10; vp = vpDiv10; vm = vmDiv10;
+        ++removed;
+      }
+    }
+    if (vrIsTrailingZeros && lastRemovedDigit == 5 && (vr % 2) == 0) lastRemovedDigit = 4;
+    output = vr + (((vr == vm && (!acceptBounds || !vmIsTrailingZeros)) || lastRemovedDigit >= 5) ? 1u : 0u);
+  } else {
+    bool roundUp = false;
+    const uint64_t vpDiv100 = vp / 100;
+    const uint64_t vmDiv100 = vm / 100;
+    if (vpDiv100 > vmDiv100) {
+      const uint64_t vrDiv100 = vr / 100;
+      const uint32_t vrMod100 = (uint32_t)(vr - 100 * vrDiv100);
+      roundUp = vrMod100 >= 50;
+      vr = vrDiv100; vp = vpDiv100; vm = vmDiv100;
+      removed += 2;
+    }
+    for (;;) {
+      const uint64_t vpDiv10 = vp / 10;
+      const uint64_t vmDiv10 = vm / 10;
+      if (vpDiv10 <= vmDiv10) break;
+      const uint64_t vrDiv10 = vr / 10;
+      const uint32_t vrMod10 = (uint32_t)(vr - 10 * vrDiv10);
+      roundUp = vrMod10 >= 5;
+      vr = vrDiv10; vp = vpDiv10; vm = vmDiv10;
+      ++removed;
+    }
+    output = vr + ((vr == vm || roundUp) ? 1u : 0u);
+  }
+  Dec64 fd;
+  fd.exponent = e10 + removed;
+  fd.mantissa = output;
+  return fd;
+}
+
+// ---------------------------------------------------------------------------
+// repr(float) / repr(int) emitters.  Emit::put(pos, byte) writes one byte at
+// string position pos; the function returns the string length.  Positions
+// are computed in closed form so digits can be produced least-significant
+// first without any dynamic register indexing.
+// ---------------------------------------------------------------------------
+template <class Emit>
+UT_HD int repr_double(double x, Emit& out) {
+  uint64_t bits;
+#if defined(__HIP_DEVICE_COMPILE__)
+  bits = (uint64_t)__double_as_longlong(x);
+#else
+  __builtin_memcpy(&bits, &x, 8);
+#endif
+  const bool neg = (bits >> 63) != 0;
+  const uint64_t mant = bits & ((1ull << 52) - 1);
+  const uint32_t expo = (uint32_t)((bits >> 52) & 0x7FFu);
+  if (expo == 0x7FFu) {
+    if (mant != 0) {
+      out.put(0, 'n'); out.put(1, 'a'); out.put(2, 'n');
+      return 3;
+    }
+    int s = 0;
+    if (neg) out.put(s++, '-');
+    out.put(s, 'i'); out.put(s + 1, 'n'); out.put(s + 2, 'f');
+    return s + 3;
+  }
+  uint64_t digits;
+  int32_t n, decpt;
+  if (expo == 0 && mant == 0) {
+    digits = 0;
+    n = 1;
+    decpt = 1;
+  } else {
+    const Dec64 d = d2d(mant, expo);
+    digits = d.mantissa;
+    n = (int32_t)decimal_length17(digits);
+    decpt = n + d.exponent;
+  }
+  const int s = neg ? 1 : 0;
+  if (neg) out.put(0, '-');
+  const bool use_exp = (decpt <= -4) || (decpt > 16);
+  if (use_exp) {
+    // d[.ddd]e(+|-)XX
+    int pos = s + n + (n > 1 ? 1 : 0);
+    for (int i = n - 1; i >= 0; --i) {
+      const uint64_t q = digits / 10;
+      const uint32_t dg = (uint32_t)(digits - 10 * q);
+      digits = q;
+      out.put(s + i + (i >= 1 ? 1 : 0), (uint8_t)('0' + dg));
+    }
+    if (n > 1) out.put(s + 1, '.');
+    int e = decpt - 1;
+    out.put(pos++, 'e');
+    out.put(pos++, e < 0 ? '-' : '+');
+    if (e < 0) e = -e;
+    if (e >= 100) {
+      out.put(pos++, (uint8_t)('0' + e / 100));
+      e %= 100;
+    }
+    out.put(pos++, (uint8_t)('0' + e / 10));
+    out.put(pos++, (uint8_t)('0' + e % 10));
+    return pos;
+  }
+  if (decpt <= 0) {
+    // 0.000ddd
+    out.put(s, '0');
+    out.put(s + 1, '.');
+    for (int z = 0; z < -decpt; ++z) out.put(s + 2 + z, '0');
+    const int base = s + 2 - decpt;
+    for (int i = n - 1; i >= 0; --i) {
+      const uint64_t q = digits / 10;
+      const uint32_t dg = (uint32_t)(digits - 10 * q);
+      digits = q;
+      out.put(base + i, (uint8_t)('0' + dg));
+    }
+    return base + n;
+  }
+  if (decpt < n) {
+    // ddd.ddd
+    for (int i = n - 1; i >= 0; --i) {
+      const uint64_t q = digits / 10;
+      const uint32_t dg = (uint32_t)(digits - 10 * q);
+      digits = q;
+      out.put(s + i + (i >= decpt ? 1 : 0), (uint8_t)('0' + dg));
+    }
+    out.put(s + decpt, '.');
+    return s + n + 1;
+  }
+  // ddd000.0
+  for (int i = n - 1; i >= 0; --i) {
+    const uint64_t q = digits / 10;
+    const uint32_t dg = (uint32_t)(digits - 10 * q);
+    digits = q;
+    out.put(s + i, (uint8_t)('0' + dg));
+  }
+  for (int z = n; z < decpt; ++z) out.put(s + z, '0');
+  out.put(s + decpt, '.');
+  out.put(s + decpt + 1, '0');
+  return s + decpt + 2;
+}
+
+template <class Emit>
+UT_HD int repr_int64(int64_t v, Emit& out) {
+  const bool neg = v < 0;
+  uint64_t u = neg ? (uint64_t)0 - (uint64_t)v : (uint64_t)v;
+  const int s = neg ? 1 : 0;
+  if (neg) out.put(0, '-');
+  uint32_t n = 1;
+  {
+    uint64_t p = 10;
+    for (int i = 0; i < 19; ++i) {
+      n += (u >= p) ? 1u : 0u;
+      if (p > UINT64_C(1844674407370955161)) break;
+      p *= 10;
+    }
+  }
+  for (int i = (int)n - 1; i >= 0; --i) {
+    const uint64_t q = u / 10;
+    out.put(s + i, (uint8_t)('0' + (uint32_t)(u - 10 * q)));
+    u = q;
+  }
+  return s + (int)n;
+}
+
+// ---------------------------------------------------------------------------
+// Parameter value arithmetic (unit encoding) -- bit-exact restatement of
+//   get_unit_value  manipulator.py:473-488
+//   set_unit_value  manipulator.py:490-503
+//   op4_set_linear  manipulator.py:523-542
+// Compiled with -ffp-contract=off: every multiply and add rounds separately
+// and in Python's left-to-right order.
+// ---------------------------------------------------------------------------
+UT_HD double py_min(double a, double b) { return (b < a) ? b : a; }  // Python min(a, b)
+UT_HD double py_max(double a, double b) { return (b > a) ? b : a; }  // Python max(a, b)
+
+}  // namespace ut

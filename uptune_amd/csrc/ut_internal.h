@@ -1,0 +1,189 @@
+// ut_internal.h -- context, device-side space description and launch
+// helpers shared by the libuthot translation units.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string>
+#include <vector>
+
+#include "../../include/uthot.h"
+#include "ut_core.h"
+
+namespace ut {
+
+// Per-parameter record in device memory (uniform across a wave: every lane of
+// a candidate-parallel kernel reads the same record, so these become scalar
+// loads).
+struct DevParam {
+  int32_t kind;
+  int32_t hash_mode;   // HM_LUT / HM_FLOAT / HM_INT
+  int64_t lut_base;    // first digest of this param in the LUT buffer
+  int64_t lut_n;       // LUT entries (indices are clamped to [0, lut_n))
+  double lo, hi;       // legal range of the stored value
+  double u_lo, u_hi;   // unit-encoding range (widened for integer types)
+  double u_span;       // u_hi - u_lo, rounded as Python rounds it
+  int64_t n_opt;       // ENUM/BOOL option count
+  int32_t feat_col;    // first GP feature column
+  int32_t n_feat;      // GP feature columns of this param
+};
+
+enum : int32_t { HM_LUT = 0, HM_FLOAT = 1, HM_INT = 2 };
+
+// One 32-bit word of the fixed-layout outer hash message.
+struct HashWord {
+  uint32_t tmpl;   // constant bytes (zero where hex characters go)
+  int16_t hole;    // sorted-parameter position whose 64 hex chars overlap, -1 none
+  uint8_t q1;      // hex word index + 1 (0..16) of the first overlapping word
+  uint8_t shift;   // byte shift 0..3
+};
+
+struct Space {
+  int32_t P = 0;
+  int32_t n_feat = 0;
+  int32_t py2 = 0;
+  std::vector<DevParam> host_params;
+  std::vector<int32_t> host_order;        // sorted position -> param index
+  int64_t outer_len = 0;
+  int64_t outer_blocks = 0;
+  DevParam* d_params = nullptr;
+  int32_t* d_order = nullptr;             // sorted position -> param index
+  HashWord* d_words = nullptr;            // outer_blocks * 16
+  int16_t* d_block_last = nullptr;        // last sorted position needed by each block
+  uint32_t* d_lut = nullptr;              // digests [*][8]
+};
+
+template <class T>
+struct DevBuf {
+  T* p = nullptr;
+  size_t n = 0;
+};
+
+struct Timing {
+  bool on = false;
+  std::vector<std::pair<std::string, hipEvent_t>> marks;
+  std::vector<std::pair<std::string, double>> last;
+};
+
+}  // namespace ut
+
+struct ut_ctx {
+  int device = 0;
+  uint64_t seed = 0;
+  hipStream_t stream = nullptr;
+  hipStream_t own_stream = nullptr;
+  std::string err;
+  ut::Space space;
+  bool has_space = false;
+
+  // population
+  double* pop = nullptr;
+  int64_t npop = 0;
+  int64_t pop_cap = 0;
+
+  // history set
+  uint32_t* hist_keys = nullptr;   // [cap][8]
+  uint32_t* hist_state = nullptr;  // [cap] 0 empty / 1 full
+  int64_t hist_cap = 0;
+  int64_t hist_count = 0;
+
+  // batch dedup table
+  int32_t* batch_slots = nullptr;
+  int64_t batch_cap = 0;
+
+  // GP state
+  int32_t gp_n = 0, gp_d = 0;
+  bool gp_ready = false;
+  double* gp_Xs = nullptr;     // [n][d] scaled features
+  double* gp_xnorm = nullptr;  // [n]
+  double* gp_K = nullptr;      // [n][n] work / L
+  double* gp_Linv = nullptr;   // [n][n]
+  double* gp_y = nullptr;      // [n] standardised
+  double* gp_tmp = nullptr;    // [n]
+  double* gp_alpha = nullptr;  // [n]
+  double* gp_inv_ell = nullptr;// [d]
+  double* gp_stats = nullptr;  // [4]: f_best, mean, std, flag
+  int32_t* gp_flag = nullptr;
+  double gp_sf2 = 1.0;
+  int64_t gp_cap_n = 0;
+
+  // scratch for GP scoring / round pipeline
+  ut::DevBuf<double> kst;        // [n][ld]
+  ut::DevBuf<double> mu_part;    // [RT][ld]
+  ut::DevBuf<double> var_part;   // [RT][ld]
+  ut::DevBuf<double> cnorm;      // [ld]
+  ut::DevBuf<double> r_values, r_feat, r_mu, r_var, r_score;
+  ut::DevBuf<uint32_t> r_digest;
+  ut::DevBuf<uint8_t> r_dup;
+  ut::DevBuf<double> tk_score[2];
+  ut::DevBuf<int64_t> tk_idx[2];
+  ut::DevBuf<int64_t> r_topk_idx;
+  ut::DevBuf<double> r_topk_score;
+  int64_t r_ld = 0;
+  int64_t r_m = 0;
+
+  ut::Timing timing;
+};
+
+namespace ut {
+
+int set_err(ut_ctx* c, int code, const std::string& msg);
+
+#define UT_HIP(ctx, call)                                                                 \
+  do {                                                                                    \
+    hipError_t e_ = (call);                                                               \
+    if (e_ != hipSuccess)                                                                 \
+      return ::ut::set_err((ctx), UT_EHIP, std::string(#call) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+#define UT_CHECK(ctx, cond, code, msg)                    \
+  do {                                                    \
+    if (!(cond)) return ::ut::set_err((ctx), (code), (msg)); \
+  } while (0)
+
+#define UT_LAUNCH_CHECK(ctx)                                                       \
+  do {                                                                             \
+    hipError_t e_ = hipGetLastError();                                             \
+    if (e_ != hipSuccess)                                                          \
+      return ::ut::set_err((ctx), UT_EHIP, std::string("launch: ") + hipGetErrorString(e_)); \
+  } while (0)
+
+template <class T>
+int ensure(ut_ctx* c, DevBuf<T>& b, size_t n) {
+  if (b.n >= n && b.p) return 0;
+  if (b.p) {
+    hipError_t e = hipStreamSynchronize(c->stream);
+    (void)e;
+    (void)hipFree(b.p);
+    b.p = nullptr;
+    b.n = 0;
+  }
+  size_t bytes = n * sizeof(T);
+  if (bytes == 0) bytes = sizeof(T);
+  hipError_t e = hipMalloc((void**)&b.p, bytes);
+  if (e != hipSuccess) return set_err(c, UT_ENOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
+  b.n = n;
+  return 0;
+}
+
+void mark(ut_ctx* c, const char* name);
+
+// kernel launchers implemented in the .hip translation units
+int launch_population_init(ut_ctx* c, uint32_t round_);
+int launch_de(ut_ctx* c, const ut_de_params* p, uint32_t round_, int64_t cand_base, int64_t m, double* out,
+              int64_t ld);
+int launch_encode(ut_ctx* c, const double* values, int64_t ld, int64_t m, double* feat, int64_t ldf);
+int launch_hash(ut_ctx* c, const double* values, int64_t ld, int64_t m, uint32_t* out);
+int launch_hist_insert(ut_ctx* c, const uint32_t* dig, int64_t n);
+int launch_hist_rehash(ut_ctx* c, const uint32_t* okeys, const uint32_t* ostate, int64_t ocap);
+int launch_dedup(ut_ctx* c, const uint32_t* dig, int64_t m, uint8_t* dup);
+int gp_fit_impl(ut_ctx* c, const double* X, const double* y, int32_t n, int32_t d, const ut_gp_hyper* h);
+int gp_score_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, const ut_acq* acq, const uint8_t* dup,
+                  double* mu, double* var, double* score);
+int topk_impl(ut_ctx* c, const double* score, const uint8_t* dup, int64_t m, int64_t cand_base, int32_t k,
+              int64_t* out_idx, double* out_score);
+int launch_gather_rows(ut_ctx* c, const double* values, int64_t ld, const int64_t* idx, int64_t cand_base,
+                       int32_t k, double* out, int64_t ldo, const uint32_t* dig, uint32_t* out_dig);
+
+inline unsigned grid1(int64_t n, int bs) { return (unsigned)((n + bs - 1) / bs); }
+
+}  // namespace ut

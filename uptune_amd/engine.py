@@ -1,0 +1,243 @@
+"""BatchEngine: the Python face of libuthot.so.
+
+Owns one ut_ctx (one GPU, one HIP stream = torch's current stream on that
+device, so library kernels and torch.distributed collectives are ordered on
+the same queue).  All large arrays are torch tensors resident in HBM; only
+their data pointers cross the C ABI.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Any, Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from . import _lib as L
+from .manipulator import SpaceSpec, compile_space, to_descs
+
+
+def _ptr(t: Optional[torch.Tensor]):
+    return None if t is None else C.c_void_p(t.data_ptr())
+
+
+def digests_to_hex(d: torch.Tensor | np.ndarray) -> List[str]:
+    """[n][8] big-endian uint32 words (as int32/uint32) -> hexdigest strings"""
+    a = d.cpu().numpy() if isinstance(d, torch.Tensor) else np.asarray(d)
+    a = a.view(np.uint32).astype(">u4")
+    return [row.tobytes().hex() for row in a]
+
+
+def hex_to_digests(hexes: Sequence[str]) -> np.ndarray:
+    """hexdigest strings -> [n][8] uint32 (big-endian word values)"""
+    if not hexes:
+        return np.zeros((0, 8), dtype=np.uint32)
+    raw = np.frombuffer(b"".join(bytes.fromhex(h) for h in hexes), dtype=">u4").reshape(-1, 8)
+    return raw.astype(np.uint32)
+
+
+class BatchEngine:
+    """One device context over one search space."""
+
+    def __init__(self, space, device: int = 0, seed: int = 0, py2_layout: bool = False):
+        self.lib = L.lib()
+        if not torch.cuda.is_available():
+            raise L.UthotError("uptune_amd.BatchEngine needs a ROCm GPU (torch.cuda.is_available() is False)")
+        self.device = torch.device("cuda", device)
+        self.seed = int(seed)
+        self.spec: SpaceSpec = space if isinstance(space, SpaceSpec) else compile_space(space)
+        ctx = C.c_void_p()
+        torch.cuda.set_device(self.device)
+        L.check(None, self.lib.ut_ctx_create(device, self.seed, C.byref(ctx)), "ut_ctx_create")
+        self.ctx = ctx
+        self._bind_stream()
+        descs, keep = to_descs(self.spec)
+        L.check(self.ctx, self.lib.ut_space_define(self.ctx, self.spec.P, descs, 1 if py2_layout else 0),
+                "ut_space_define")
+        del keep
+        self.npop = 0
+
+    # -- plumbing ----------------------------------------------------------
+    def _bind_stream(self):
+        s = torch.cuda.current_stream(self.device)
+        L.check(self.ctx, self.lib.ut_set_stream(self.ctx, C.c_void_p(s.cuda_stream)), "ut_set_stream")
+
+    def close(self):
+        if getattr(self, "ctx", None):
+            self.lib.ut_ctx_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __deepcopy__(self, memo):
+        # techniques are deepcopied per SearchDriver (driver.py:75); a device
+        # context is never copied -- the copy re-creates it lazily
+        return None
+
+    def sync(self):
+        L.check(self.ctx, self.lib.ut_sync(self.ctx), "ut_sync")
+
+    def space_info(self) -> Tuple[int, int, int]:
+        a, b, c = C.c_int64(), C.c_int64(), C.c_int32()
+        L.check(self.ctx, self.lib.ut_space_info(self.ctx, C.byref(a), C.byref(b), C.byref(c)), "ut_space_info")
+        return a.value, b.value, c.value
+
+    def _empty(self, *shape, dtype=torch.float64) -> torch.Tensor:
+        return torch.empty(*shape, dtype=dtype, device=self.device)
+
+    # -- population --------------------------------------------------------
+    def population_init(self, npop: int, round_: int = 0):
+        L.check(self.ctx, self.lib.ut_population_init(self.ctx, int(npop), int(round_)), "ut_population_init")
+        self.npop = int(npop)
+
+    def population_set(self, values: torch.Tensor):
+        values = values.to(self.device, torch.float64).contiguous()
+        n = values.shape[1]
+        L.check(self.ctx, self.lib.ut_population_set(self.ctx, n, _ptr(values), n), "ut_population_set")
+        self.npop = n
+
+    def population_get(self) -> torch.Tensor:
+        out = self._empty(self.spec.P, self.npop)
+        L.check(self.ctx, self.lib.ut_population_get(self.ctx, _ptr(out), self.npop), "ut_population_get")
+        return out
+
+    def population_replace(self, trial: torch.Tensor, idx: torch.Tensor):
+        trial = trial.contiguous()
+        idx = idx.to(self.device, torch.int64).contiguous()
+        L.check(self.ctx, self.lib.ut_population_replace(self.ctx, _ptr(trial), trial.shape[1], _ptr(idx),
+                                                         idx.numel()), "ut_population_replace")
+
+    # -- proposal ----------------------------------------------------------
+    def propose_de(self, m: int, round_: int = 0, cand_base: int = 0, cr: float = 0.2, n_cross: int = 1,
+                   out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        if out is None:
+            out = self._empty(self.spec.P, m)
+        p = L.DeParams(cr=float(cr), n_cross=int(n_cross))
+        L.check(self.ctx, self.lib.ut_propose_de(self.ctx, C.byref(p), int(round_), int(cand_base), int(m),
+                                                 _ptr(out), out.stride(0)), "ut_propose_de")
+        return out
+
+    def encode(self, values: torch.Tensor, m: Optional[int] = None) -> torch.Tensor:
+        m = values.shape[1] if m is None else m
+        feat = self._empty(self.spec.n_features, m)
+        L.check(self.ctx, self.lib.ut_encode_features(self.ctx, _ptr(values), values.stride(0), m, _ptr(feat), m),
+                "ut_encode_features")
+        return feat
+
+    # -- identity / dedup --------------------------------------------------
+    def hash(self, values: torch.Tensor, m: Optional[int] = None) -> torch.Tensor:
+        m = values.shape[1] if m is None else m
+        out = self._empty(m, 8, dtype=torch.int32)
+        L.check(self.ctx, self.lib.ut_hash(self.ctx, _ptr(values), values.stride(0), m, _ptr(out)), "ut_hash")
+        return out
+
+    def hash_configs(self, cfgs: Sequence[Dict[Any, Any]]) -> List[str]:
+        vals = torch.from_numpy(self.spec.encode_configs(cfgs)).to(self.device)
+        d = self.hash(vals)
+        return digests_to_hex(d)
+
+    def history_reset(self, capacity: int = 0):
+        L.check(self.ctx, self.lib.ut_history_reset(self.ctx, int(capacity)), "ut_history_reset")
+
+    def history_add(self, digests):
+        if isinstance(digests, torch.Tensor):
+            d = digests.to(self.device, torch.int32).contiguous()
+            L.check(self.ctx, self.lib.ut_history_add(self.ctx, _ptr(d), d.shape[0]), "ut_history_add")
+        else:
+            arr = np.ascontiguousarray(hex_to_digests(digests) if len(digests) and isinstance(digests[0], str)
+                                       else np.asarray(digests, dtype=np.uint32).reshape(-1, 8))
+            L.check(self.ctx, self.lib.ut_history_add_host(self.ctx, arr.ctypes.data, arr.shape[0]),
+                    "ut_history_add_host")
+
+    def dedup(self, digests: torch.Tensor) -> torch.Tensor:
+        m = digests.shape[0]
+        out = self._empty(m, dtype=torch.uint8)
+        L.check(self.ctx, self.lib.ut_dedup(self.ctx, _ptr(digests), m, _ptr(out)), "ut_dedup")
+        return out
+
+    # -- GP ----------------------------------------------------------------
+    def gp_fit(self, X: np.ndarray, y: np.ndarray, lengthscale, sigma_f2: float = 1.0, sigma_n2: float = 1e-6,
+               jitter: float = 0.0):
+        X = np.ascontiguousarray(X, dtype=np.float64)
+        y = np.ascontiguousarray(y, dtype=np.float64)
+        n, d = X.shape
+        ell = np.ascontiguousarray(np.broadcast_to(np.asarray(lengthscale, dtype=np.float64), (d,)))
+        h = L.GpHyper(sigma_f2=float(sigma_f2), sigma_n2=float(sigma_n2), jitter=float(jitter),
+                      lengthscale_host=ell.ctypes.data)
+        L.check(self.ctx, self.lib.ut_gp_fit(self.ctx, X.ctypes.data, y.ctypes.data, n, d, C.byref(h)), "ut_gp_fit")
+
+    def gp_stats(self) -> Tuple[float, float, float]:
+        a, b, c = C.c_double(), C.c_double(), C.c_double()
+        L.check(self.ctx, self.lib.ut_gp_stats(self.ctx, C.byref(a), C.byref(b), C.byref(c)), "ut_gp_stats")
+        return a.value, b.value, c.value
+
+    @staticmethod
+    def acq(kind: str = "ei", xi: float = 0.0, kappa: float = 2.0) -> L.Acq:
+        return L.Acq(kind=L.UT_ACQ_EI if kind == "ei" else L.UT_ACQ_UCB, xi=float(xi), kappa=float(kappa))
+
+    def gp_score(self, feat: torch.Tensor, m: Optional[int] = None, acq: Optional[L.Acq] = None,
+                 dup: Optional[torch.Tensor] = None):
+        m = feat.shape[1] if m is None else m
+        acq = acq or self.acq()
+        mu, var, score = self._empty(m), self._empty(m), self._empty(m)
+        L.check(self.ctx, self.lib.ut_gp_score(self.ctx, _ptr(feat), feat.stride(0), m, C.byref(acq), _ptr(dup),
+                                               _ptr(mu), _ptr(var), _ptr(score)), "ut_gp_score")
+        return mu, var, score
+
+    # -- selection ---------------------------------------------------------
+    def topk(self, score: torch.Tensor, k: int, dup: Optional[torch.Tensor] = None, cand_base: int = 0):
+        idx = self._empty(k, dtype=torch.int64)
+        top = self._empty(k)
+        L.check(self.ctx, self.lib.ut_topk(self.ctx, _ptr(score), _ptr(dup), score.numel(), int(cand_base), int(k),
+                                           _ptr(idx), _ptr(top)), "ut_topk")
+        return idx, top
+
+    # -- whole round -------------------------------------------------------
+    def score_round_de(self, m: int, k: int, round_: int = 0, cand_base: int = 0, cr: float = 0.2,
+                       n_cross: int = 1, acq: Optional[L.Acq] = None, want_values: bool = True):
+        de = L.DeParams(cr=float(cr), n_cross=int(n_cross))
+        acq = acq or self.acq()
+        idx = self._empty(k, dtype=torch.int64)
+        top = self._empty(k)
+        dig = self._empty(k, 8, dtype=torch.int32)
+        vals = self._empty(self.spec.P, k) if want_values else None
+        out = L.RoundOut(topk_idx=idx.data_ptr(), topk_score=top.data_ptr(), topk_digest=dig.data_ptr(),
+                         topk_values=vals.data_ptr() if vals is not None else None)
+        L.check(self.ctx, self.lib.ut_score_round_de(self.ctx, C.byref(de), C.byref(acq), int(round_),
+                                                     int(cand_base), int(m), int(k), C.byref(out)),
+                "ut_score_round_de")
+        return idx, top, dig, vals
+
+    def round_buffers(self):
+        ptrs = [C.c_void_p() for _ in range(7)]
+        ld = C.c_int64()
+        L.check(self.ctx, self.lib.ut_round_buffers(self.ctx, *[C.byref(p) for p in ptrs], C.byref(ld)),
+                "ut_round_buffers")
+        return [p.value for p in ptrs], ld.value
+
+    def set_timing(self, on: bool):
+        L.check(self.ctx, self.lib.ut_set_timing(self.ctx, 1 if on else 0), "ut_set_timing")
+
+    def stage_time(self, stage: str) -> float:
+        v = C.c_double()
+        L.check(self.ctx, self.lib.ut_stage_time(self.ctx, stage.encode(), C.byref(v)), "ut_stage_time")
+        return v.value
+
+    def decode(self, values: torch.Tensor) -> List[Dict[Any, Any]]:
+        return self.spec.decode_values(values.detach().cpu().numpy())
+
+
+_DEFAULT: Dict[int, BatchEngine] = {}
+
+
+def default_engine(manipulator) -> BatchEngine:
+    key = id(manipulator)
+    eng = _DEFAULT.get(key)
+    if eng is None:
+        eng = BatchEngine(manipulator)
+        _DEFAULT[key] = eng
+    return eng

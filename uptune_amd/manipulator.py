@@ -1,0 +1,319 @@
+"""Host-side mirror of the reference's search-space API.
+
+Same class names, constructor arguments and value semantics as
+python/uptune/opentuner/search/manipulator.py (the parameter kinds that
+uptune's create_params builds, python/uptune/api.py:179-199):
+
+    IntegerParameter(name, min, max)          manipulator.py:651
+    FloatParameter(name, min, max)            manipulator.py:703
+    LogIntegerParameter(name, min, max)       manipulator.py:781
+    PowerOfTwoParameter(name, min, max)       manipulator.py:813
+    BooleanParameter(name)                    manipulator.py:930
+    EnumParameter(name, options)              manipulator.py:1024
+    PermutationParameter(name, items)         manipulator.py:1048
+    ConfigurationManipulator(params)          manipulator.py:129
+
+A configuration is a plain dict name -> value, exactly as in the reference.
+The batch work (proposal, hash_config, dedup, scoring) runs on the GPU via
+uptune_amd.engine.BatchEngine; this module only describes the space and
+converts between config dicts and the device's structure-of-arrays rows.
+
+`compile_space` also accepts a reference ConfigurationManipulator (duck
+typed on class names and min_value/max_value/options attributes), which is
+what makes the GPU techniques a drop-in for an existing OpenTuner/uptune
+search driver.
+"""
+from __future__ import annotations
+
+import hashlib
+import math
+from dataclasses import dataclass, field
+from typing import Any, Dict, List, Sequence
+
+import numpy as np
+
+from . import _lib as L
+
+# discrete INT ranges up to this many values get an inner-digest LUT
+INT_LUT_MAX = 4096
+
+
+class Parameter:
+    """Base of the mirrored parameter kinds (manipulator.py:275)."""
+
+    def __init__(self, name):
+        self.name = name
+        self.parent = None
+
+    def is_primitive(self, ignored=None) -> bool:
+        return isinstance(self, PrimitiveParameter)
+
+    def is_permutation(self, ignored=None) -> bool:
+        return isinstance(self, PermutationParameter)
+
+
+class PrimitiveParameter(Parameter):
+    value_type: type = float
+
+    def is_integer_type(self) -> bool:
+        return self.value_type(0) == self.value_type(0.1)
+
+
+class NumericParameter(PrimitiveParameter):
+    def __init__(self, name, min_value, max_value):
+        assert min_value <= max_value
+        super().__init__(name)
+        self.min_value = self.value_type(min_value)
+        self.max_value = self.value_type(max_value)
+
+    def legal_range(self, config=None):
+        return self.min_value, self.max_value
+
+
+class IntegerParameter(NumericParameter):
+    value_type = int
+
+
+class FloatParameter(NumericParameter):
+    value_type = float
+
+
+class LogIntegerParameter(FloatParameter):
+    """integer searched on a log scale (manipulator.py:781-797); host API only
+    in this round -- the device path rejects it with UT_EUNSUPPORTED."""
+
+    def __init__(self, name, min_value, max_value):
+        Parameter.__init__(self, name)
+        self.min_value = float(min_value)
+        self.max_value = float(max_value)
+
+
+class PowerOfTwoParameter(IntegerParameter):
+    """power of two searched by exponent (manipulator.py:813-836); host API only
+    in this round."""
+
+    def __init__(self, name, min_value, max_value):
+        assert min_value >= 1
+        assert math.log(min_value, 2) % 1 == 0
+        assert math.log(max_value, 2) % 1 == 0
+        super().__init__(name, min_value, max_value)
+
+
+class ComplexParameter(Parameter):
+    pass
+
+
+class BooleanParameter(ComplexParameter):
+    pass
+
+
+class EnumParameter(ComplexParameter):
+    def __init__(self, name, options):
+        super().__init__(name)
+        self.options = list(options)
+
+
+class PermutationParameter(ComplexParameter):
+    """host API only in this round (device path: UT_EUNSUPPORTED)."""
+
+    def __init__(self, name, items):
+        super().__init__(name)
+        self._items = list(items)
+        self.size = len(items)
+
+
+class ConfigurationManipulator:
+    """Fixed list of parameters; configs are dicts (manipulator.py:129-272)."""
+
+    def __init__(self, params=None, config_type=dict, seed_config=None):
+        self.params = list(params or [])
+        self.config_type = config_type
+        self._seed_config = seed_config
+        for p in self.params:
+            p.parent = self
+
+    def add_parameter(self, p):
+        p.parent = self
+        self.params.append(p)
+
+    def parameters(self, config=None):
+        return self.params
+
+    def param_names(self, *args):
+        return sorted(p.name for p in self.params)
+
+    def copy(self, config):
+        import copy
+        return copy.deepcopy(config)
+
+    def hash_config(self, config) -> str:
+        """sha256 hex identity of a config (manipulator.py:233-243), computed on
+        the GPU (batch of one)."""
+        from .engine import default_engine
+        return default_engine(self).hash_configs([config])[0]
+
+
+# ---------------------------------------------------------------------------
+# space compilation: parameters -> ut_param_desc[] + value codecs
+# ---------------------------------------------------------------------------
+def _kind_of(p) -> int:
+    cls = type(p).__name__
+    names = {c.__name__ for c in type(p).__mro__}
+    if "PermutationParameter" in names:
+        return L.UT_PERM
+    if "PowerOfTwoParameter" in names:
+        return L.UT_POW2
+    if "LogIntegerParameter" in names:
+        return L.UT_LOGINT
+    if "BooleanParameter" in names:
+        return L.UT_BOOL
+    if "EnumParameter" in names:
+        return L.UT_ENUM
+    if "IntegerParameter" in names:
+        return L.UT_INT
+    if "FloatParameter" in names:
+        return L.UT_FLOAT
+    raise TypeError(f"unsupported parameter class {cls} for {getattr(p, 'name', '?')!r}")
+
+
+def _digest(s: str) -> bytes:
+    return hashlib.sha256(s.encode("utf-8")).digest()
+
+
+@dataclass
+class ParamSpec:
+    name: Any
+    kind: int
+    lo: float = 0.0
+    hi: float = 0.0
+    u_lo: float = 0.0
+    u_hi: float = 0.0
+    u_span: float = 0.0
+    options: List[Any] = field(default_factory=list)
+    feat_col: int = 0
+    n_feat: int = 1
+    lut: bytes = b""
+
+    def to_value(self, v) -> float:
+        if self.kind == L.UT_FLOAT:
+            return float(v)
+        if self.kind == L.UT_INT:
+            return float(int(v))
+        if self.kind == L.UT_BOOL:
+            return 1.0 if v else 0.0
+        if self.kind == L.UT_ENUM:
+            return float(self.options.index(v))
+        raise TypeError("unsupported kind")
+
+    def from_value(self, x: float):
+        if self.kind == L.UT_FLOAT:
+            return float(x)
+        if self.kind == L.UT_INT:
+            return int(x)
+        if self.kind == L.UT_BOOL:
+            return bool(x != 0.0)
+        if self.kind == L.UT_ENUM:
+            return self.options[int(x)]
+        raise TypeError("unsupported kind")
+
+
+@dataclass
+class SpaceSpec:
+    params: List[ParamSpec]
+    order: List[int]           # sorted position -> param index
+    n_features: int
+
+    @property
+    def P(self) -> int:
+        return len(self.params)
+
+    def names(self) -> List[Any]:
+        return [p.name for p in self.params]
+
+    def encode_configs(self, cfgs: Sequence[Dict[Any, Any]]) -> np.ndarray:
+        """configs -> SoA [P][n] float64"""
+        out = np.empty((self.P, len(cfgs)), dtype=np.float64)
+        for j, cfg in enumerate(cfgs):
+            for p, ps in enumerate(self.params):
+                out[p, j] = ps.to_value(cfg[ps.name])
+        return out
+
+    def decode_values(self, values: np.ndarray) -> List[Dict[Any, Any]]:
+        """SoA [P][n] -> configs"""
+        n = values.shape[1]
+        return [{ps.name: ps.from_value(values[p, j]) for p, ps in enumerate(self.params)} for j in range(n)]
+
+
+def unit_bounds(kind: int, lo, hi):
+    """legal range for get/set_unit_value exactly as Python computes it
+    (manipulator.py:475-479, 493-497)."""
+    low, high = lo, hi
+    if kind == L.UT_INT:
+        low -= 0.4999
+        high += 0.4999
+    return float(low), float(high), float(high - low)
+
+
+def compile_space(params) -> SpaceSpec:
+    """Build the device description of a parameter list (our mirror classes or
+    the reference's own Parameter objects)."""
+    if hasattr(params, "params"):
+        params = params.params
+    specs: List[ParamSpec] = []
+    feat = 0
+    for p in params:
+        kind = _kind_of(p)
+        ps = ParamSpec(name=p.name, kind=kind)
+        if kind in (L.UT_FLOAT, L.UT_INT):
+            lo, hi = p.min_value, p.max_value
+            ps.lo, ps.hi = float(lo), float(hi)
+            ps.u_lo, ps.u_hi, ps.u_span = unit_bounds(kind, lo, hi)
+            ps.n_feat = 1
+            if kind == L.UT_INT and (hi - lo + 1) <= INT_LUT_MAX:
+                ps.lut = b"".join(_digest(repr(int(v))) for v in range(int(lo), int(hi) + 1))
+        elif kind == L.UT_BOOL:
+            ps.options = [True, False]
+            ps.n_feat = 1
+            ps.lut = _digest(repr(False)) + _digest(repr(True))
+        elif kind == L.UT_ENUM:
+            ps.options = list(p.options)
+            ps.n_feat = len(ps.options)
+            ps.lut = b"".join(_digest(repr(o)) for o in ps.options)
+        else:
+            # still compiled so the host API can describe it; the device
+            # rejects these kinds in ut_space_define
+            ps.n_feat = 1
+        ps.feat_col = feat
+        feat += ps.n_feat
+        specs.append(ps)
+    order = sorted(range(len(specs)), key=lambda i: specs[i].name)
+    return SpaceSpec(params=specs, order=order, n_features=feat)
+
+
+def to_descs(spec: SpaceSpec):
+    """SpaceSpec -> (ctypes ParamDesc array, keepalive list)"""
+    keep = []
+    arr = (L.ParamDesc * spec.P)()
+    rank = [0] * spec.P
+    for r, i in enumerate(spec.order):
+        rank[i] = r
+    for i, ps in enumerate(spec.params):
+        d = arr[i]
+        d.kind = ps.kind
+        d.sort_rank = rank[i]
+        d.lo, d.hi = ps.lo, ps.hi
+        d.u_lo, d.u_hi, d.u_span = ps.u_lo, ps.u_hi, ps.u_span
+        d.n_options = len(ps.options)
+        nb = str(ps.name).encode("utf-8")
+        keep.append(nb)
+        d.name = nb
+        d.name_len = len(nb)
+        if ps.lut:
+            buf = (np.frombuffer(ps.lut, dtype=np.uint8)).copy()
+            keep.append(buf)
+            d.lut_count = len(ps.lut) // 32
+            d.lut_host = buf.ctypes.data
+        else:
+            d.lut_count = 0
+            d.lut_host = None
+    return arr, keep
