@@ -106,7 +106,9 @@ typedef struct ut_acq {
 int ut_ctx_create(int device, uint64_t seed, ut_ctx** out);
 int ut_ctx_destroy(ut_ctx* ctx);
 const char* ut_last_error(ut_ctx* ctx);
-int ut_set_stream(ut_ctx* ctx, void* hip_stream);   /* hipStream_t; NULL = library stream */
+/* hipStream_t to enqueue on; NULL = the device's default (null) stream.  A new
+ * context starts on its own non-blocking stream. */
+int ut_set_stream(ut_ctx* ctx, void* hip_stream);
 int ut_sync(ut_ctx* ctx);
 int ut_version(void);
 

@@ -177,7 +177,7 @@ const char* ut_last_error(ut_ctx* c) { return c ? c->err.c_str() : "null context
 
 int ut_set_stream(ut_ctx* c, void* s) {
   if (!c) return UT_EINVAL;
-  c->stream = s ? (hipStream_t)s : c->own_stream;
+  c->stream = (hipStream_t)s;  // NULL = the device's default (null) stream
   return 0;
 }
 
