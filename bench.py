@@ -117,6 +117,7 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
+    from uptune_amd.dist import allgather_topk
     from uptune_amd.engine import BatchEngine
     from uptune_amd.manipulator import ConfigurationManipulator, FloatParameter
 
@@ -135,17 +136,7 @@ def main():
         idx, top, dig, _ = eng.score_round_de(m, k, round_=r, cand_base=cand_base, cr=0.2, n_cross=1, acq=acq,
                                               want_values=False)
         if world > 1:
-            gi = [torch.empty_like(idx) for _ in range(world)]
-            gs = [torch.empty_like(top) for _ in range(world)]
-            gd = [torch.empty_like(dig) for _ in range(world)]
-            dist.all_gather(gi, idx)
-            dist.all_gather(gs, top)
-            dist.all_gather(gd, dig)
-            ai, asc, ad = torch.cat(gi), torch.cat(gs), torch.cat(gd).contiguous()
-            dup = eng.dedup(ad)                       # cross-shard duplicates: first (smallest index) wins
-            dup = torch.where(ai < 0, torch.ones_like(dup), dup)
-            pos, top = eng.topk(asc, k, dup=dup)
-            idx = torch.where(pos >= 0, ai[pos.clamp(min=0)], pos)
+            idx, top = allgather_topk(idx, top, dig, k)   # RCCL all_gather + deterministic merge
         return idx, top
 
     for w in range(args.warmup):

@@ -1,0 +1,101 @@
+"""Batched GA-family proposal restated from
+python/uptune/opentuner/search/evolutionarytechniques.py:29-134 and
+globalGA.py:187-243.
+
+Per candidate (one `desired_configuration` call):
+  parents   = [select(), select()] if random() < crossover_rate else [select()]   (:72-78)
+              select() = the global best config (GreedySelectionMixin, :90-96),
+              or manipulator.random() when there is none (parent1 is None)
+  crossover = GGA only (crossover_strength > 0): copy the first
+              int(crossover_strength * P) params of a shuffle from parent 2
+              (globalGA.py:227-235); GA's permutation crossover is a no-op for
+              spaces without permutations (:123-134)
+  retry <= max_retries (:45-49):
+      mutation: shuffle(params); mutate the first must_mutate_count; each other
+                param with probability mutation_rate (:51-61)
+        uniform: op1_randomize                                    (:63-67)
+        normal (NormalMutationMixin, :107-114): primitive ->
+                op1_normal_mutation(sigma) (manipulator.py:505-521); Bool -> op1_flip,
+                Enum -> op1_randomize (random.choice(manipulators))
+      accept when hash_config(cfg) is not a parent hash  == the values differ
+      bitwise from every parent
+  after max_retries failures the technique returns None (candidate invalid).
+Draws (op = OP_GA or OP_GGA): CAND|0 -> parents; p|2<<28 / p|3<<28 random
+parent values; p|4<<28 crossover keys; p|r<<20 per-retry keys + mutation
+coins; p|r<<20|1<<28 randomize values; p|r<<20|2<<28 normal draws.
+"""
+import numpy as np
+
+from . import philox as ph
+from .mathx import normal_draw
+from .space import BOOL, ENUM, get_unit_value_vec, randomize, set_unit_value_vec, to_f64
+
+
+def _rand_col(prm, seed, g, stream, round_, op):
+    x, y, z, w = ph.draw(seed, g, stream, round_, op)
+    return np.array([to_f64(prm, randomize(prm, int(a), int(b), int(c), int(d))) for a, b, c, d in zip(x, y, z, w)])
+
+
+def _smallest(keys, n):
+    """bool [P][m]: rank (by key) < n"""
+    if n <= 0:
+        return np.zeros(keys.shape, dtype=bool)
+    rank = np.argsort(np.argsort(keys, axis=0, kind="stable"), axis=0, kind="stable")
+    return rank < n
+
+
+def _keys(seed, g, P, stream_of, round_, op):
+    return np.stack([(ph.draw(seed, g, stream_of(p), round_, op)[2].astype(np.uint64) << np.uint64(32)) |
+                     np.uint64(p) for p in range(P)])
+
+
+def propose_ga_vec(space, parent1, parent2, seed, round_, cand_base, m, mutation_rate=0.1, must_mutate_count=1,
+                   normal=False, sigma=0.1, crossover_rate=0.0, crossover_strength=0.0, max_retries=10,
+                   op=ph.OP_GA):
+    P = len(space)
+    g = np.arange(cand_base, cand_base + m, dtype=np.uint64)
+    x, y, _, _ = ph.draw(seed, g, ph.STREAM_CAND | 0, round_, op)
+    two = ph.u01(x, y) < crossover_rate
+    P1 = np.empty((P, m))
+    P2 = np.empty((P, m))
+    for p, prm in enumerate(space):
+        P1[p] = parent1[p] if parent1 is not None else _rand_col(prm, seed, g, p | (2 << 28), round_, op)
+        if parent2 is not None:
+            P2[p] = parent2[p]
+        elif parent1 is not None:
+            P2[p] = parent1[p]
+        else:
+            P2[p] = _rand_col(prm, seed, g, p | (3 << 28), round_, op)
+    cfg = P1.copy()
+    if crossover_strength > 0:
+        d = int(crossover_strength * P)
+        sel = _smallest(_keys(seed, g, P, lambda p: p | (4 << 28), round_, op), d) & two[None, :]
+        cfg = np.where(sel, P2, cfg)
+    accepted = np.zeros(m, dtype=bool)
+    for r in range(max_retries):
+        active = ~accepted
+        forced = _smallest(_keys(seed, g, P, lambda p: p | (r << 20), round_, op), must_mutate_count)
+        for p, prm in enumerate(space):
+            xx, yy, _, _ = ph.draw(seed, g, p | (r << 20), round_, op)
+            mut = active & (forced[p] | (ph.u01(xx, yy) < mutation_rate))
+            if not mut.any():
+                continue
+            gi = g[mut]
+            cur = cfg[p, mut]
+            if normal and prm.is_primitive():
+                v = get_unit_value_vec(prm, cur)
+                z = normal_draw(seed, gi, p | (r << 20) | (2 << 28), round_, op)
+                v = v + (0.0 + z * sigma)
+                v = np.where(v < 0.0, v * -1.0, v)
+                v = np.where(v > 1.0, 1.0 - np.fmod(v, 1.0), v)
+                new = set_unit_value_vec(prm, v, cur)
+            elif normal and prm.kind == BOOL:
+                new = 1.0 - cur
+            else:
+                new = _rand_col(prm, seed, gi, p | (r << 20) | (1 << 28), round_, op)
+            cfg[p, mut] = new
+        b = cfg.view(np.uint64)
+        diff1 = np.any(b != P1.view(np.uint64), axis=0)
+        diff2 = np.any(b != P2.view(np.uint64), axis=0)
+        accepted |= active & diff1 & (~two | diff2)
+    return cfg, ~accepted

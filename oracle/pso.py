@@ -1,0 +1,77 @@
+"""Batched PSO move restated from python/uptune/opentuner/search/pso.py:23-77
+and the per-kind op3_swarm (manipulator.py:660-700 Int, :709-744 Float,
+:962-996 Bool, :409-443 default/Enum).
+
+HybridParticle.move calls, for every param,
+    op3_swarm(position, global_best, self.best, c=omega, c1=phi_g, c2=phi_l, velocity=v)
+so with cfg = x, cfg1 = g, cfg2 = l:
+    v' = v*c + (g - x)*c1*r1 + (l - x)*c2*r2            (draw order r1, r2)
+  Float:  x' = min(vmax, max(x + v', vmin))
+  Int:    s = k / (1 + exp(-v')) + vmin,  p ~ N(s, (sigma k)^2),  x' = int(min(vmax, max(round(p), vmin)))
+  Bool:   s = 1 / (1 + exp(-v')),  x' = (s - U) > 0
+  Enum:   opn_stochastic_mix(cfg, [cfg, g, l], [c, c1, c2]) copies FROM the particle
+          INTO the drawn parent (manipulator.py:442) -> the particle's
+          value never changes (enum_mode=0, reference); enum_mode=1 copies from
+          the drawn parent instead (corrected).
+Reference quirk kept by default: `self.best = self.position` aliases the same
+dict (pso.py:212-213, :199), so l == x and the local term is 0 -- pass
+pbest = pos to reproduce it.
+
+Draws: Philox (seed, g, p, round, OP_PSO): (x,y)->r1, (z,w)->r2; block
+p|1<<28: (x,y) -> U (Bool) / r (Enum); normal draws (Int) from
+mathx.normal_draw(stream p|2<<28); exp is mathx.ut_exp.
+"""
+import numpy as np
+
+from . import philox as ph
+from .mathx import normal_draw, ut_exp
+from .space import BOOL, ENUM, FLOAT, INT
+
+
+def propose_pso_vec(space, pos, vel, pbest, gbest, seed, round_, cand_base, m, omega=0.5, phi_l=0.5, phi_g=0.5,
+                    sigma=0.2, enum_mode=0):
+    P, npop = pos.shape
+    g = np.arange(cand_base, cand_base + m, dtype=np.uint64)
+    t = (g % np.uint64(npop)).astype(np.int64)
+    out_x = np.empty((P, m))
+    out_v = np.empty((P, m))
+    c, c1, c2 = omega, phi_g, phi_l
+    for p, prm in enumerate(space):
+        x = pos[p, t]
+        v = vel[p, t]
+        lb = pbest[p, t]
+        gb = gbest[p]
+        r = ph.draw(seed, g, p, round_, ph.OP_PSO)
+        r1, r2 = ph.u01(r[0], r[1]), ph.u01(r[2], r[3])
+        if prm.kind == ENUM:
+            nv = v
+            if enum_mode == 1:
+                q = ph.draw(seed, g, p | (1 << ph.STREAM_SUB_SHIFT), round_, ph.OP_PSO)
+                rr = ph.u01(q[0], q[1])
+                tot = c + c1 + c2
+                w0, w1 = c / tot, c1 / tot
+                nx = np.where(rr < w0, x, np.where(rr < w0 + w1, gb, lb))
+            else:
+                nx = x
+        else:
+            nv = ((v * c) + (((gb - x) * c1) * r1)) + (((lb - x) * c2) * r2)
+            if prm.kind == FLOAT:
+                y = x + nv
+                y = np.where(prm.lo > y, prm.lo, y)       # max(p, vmin)
+                nx = np.where(y < prm.hi, y, prm.hi)      # min(vmax, .)
+            elif prm.kind == INT:
+                k = float(prm.hi - prm.lo)
+                s = k / (1.0 + ut_exp(-nv)) + prm.lo
+                z = normal_draw(seed, g, p | (2 << ph.STREAM_SUB_SHIFT), round_, ph.OP_PSO)
+                pp = np.rint(s + z * (sigma * k))
+                pp = np.where(prm.lo > pp, float(prm.lo), pp)
+                nx = np.where(pp < prm.hi, pp, float(prm.hi))
+            elif prm.kind == BOOL:
+                s = 1.0 / (1.0 + ut_exp(-nv))
+                q = ph.draw(seed, g, p | (1 << ph.STREAM_SUB_SHIFT), round_, ph.OP_PSO)
+                nx = ((s - ph.u01(q[0], q[1])) > 0).astype(np.float64)
+            else:
+                raise NotImplementedError(prm.kind)
+        out_x[p] = nx
+        out_v[p] = nv
+    return out_x, out_v

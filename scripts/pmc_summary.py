@@ -1,0 +1,71 @@
+"""Summarise rocprofv3 output into profiles/:
+
+  python scripts/pmc_summary.py gpurun_out/prof rNN
+
+* kernel_stats (from --kernel-trace --stats) -> profiles/<tag>_kernel_stats.csv
+* FETCH_SIZE / WRITE_SIZE passes (separate --pmc runs) -> per-kernel mean per
+  launch, converted to bytes (x1024) with the gfx950 correction of
+  MI355X_MICROARCH.md §HBM: FETCH_SIZE reports half the bytes of a wide
+  coalesced read, so read bytes = 2 x FETCH_SIZE x 1024 (raw values are kept
+  alongside).  Written to profiles/pmc_summary.json keyed by stage name.
+"""
+import csv
+import json
+import os
+import shutil
+import sys
+from collections import defaultdict
+
+STAGES = {  # stage key -> kernel-name prefix
+    "var": "void ut::k_gp_gemm<1>", "kstar": "void ut::k_gp_gemm<0>", "hash": "ut::k_hash",
+    "propose": "ut::k_de", "encode": "ut::k_encode", "finalize": "ut::k_gp_finalize",
+    "dedup_insert": "ut::k_batch_insert", "dedup_mark": "ut::k_dedup_mark",
+    "topk0": "void ut::k_topk_chunk<0>", "pso": "ut::k_pso", "ga": "ut::k_ga",
+}
+
+
+def per_kernel(path, counter):
+    acc = defaultdict(list)
+    with open(path) as f:
+        for row in csv.DictReader(f):
+            if row["Counter_Name"] == counter:
+                acc[row["Kernel_Name"]].append(float(row["Counter_Value"]))
+    return {k: sum(v) / len(v) for k, v in acc.items()}
+
+
+def main(prof, tag):
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out_dir = os.path.join(root, "profiles")
+    os.makedirs(out_dir, exist_ok=True)
+    shutil.copy(os.path.join(prof, "trace", "run_kernel_stats.csv"), os.path.join(out_dir, f"{tag}_kernel_stats.csv"))
+    fetch = per_kernel(os.path.join(prof, "pmc_fetch", "run_counter_collection.csv"), "FETCH_SIZE")
+    write = per_kernel(os.path.join(prof, "pmc_write", "run_counter_collection.csv"), "WRITE_SIZE")
+    stats = {}
+    with open(os.path.join(prof, "trace", "run_kernel_stats.csv")) as f:
+        for row in csv.DictReader(f):
+            stats[row["Name"]] = row
+    summary = {"_note": "bytes per launch; read = 2 x FETCH_SIZE x 1024 (gfx950 correction, MI355X_MICROARCH.md "
+                        "§HBM), write = WRITE_SIZE x 1024; raw counters kept. source: " + tag}
+    for key, prefix in STAGES.items():
+        kf = [k for k in fetch if k.startswith(prefix)]
+        kw = [k for k in write if k.startswith(prefix)]
+        ks = [k for k in stats if k.startswith(prefix)]
+        if not (kf and kw):
+            continue
+        fr, wr = fetch[kf[0]], write[kw[0]]
+        summary[key] = {
+            "kernel": kf[0][:120],
+            "fetch_size_kb_raw": fr, "write_size_kb_raw": wr,
+            "read_bytes_per_launch": 2.0 * fr * 1024.0, "write_bytes_per_launch": wr * 1024.0,
+            "hbm_bytes_per_launch": 2.0 * fr * 1024.0 + wr * 1024.0,
+            "avg_ns": float(stats[ks[0]]["AverageNs"]) if ks else None,
+        }
+    with open(os.path.join(out_dir, "pmc_summary.json"), "w") as f:
+        json.dump(summary, f, indent=1)
+    with open(os.path.join(out_dir, f"{tag}_pmc_summary.json"), "w") as f:
+        json.dump(summary, f, indent=1)
+    print(json.dumps(summary, indent=1))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2])

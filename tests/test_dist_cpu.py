@@ -1,0 +1,92 @@
+"""World-size-2 gloo run of the multi-GPU exchange (uptune_amd/dist.py):
+sharded local top-k -> all_gather -> merge equals the single-pool top-k,
+including cross-shard duplicate digests and score ties; history broadcast."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from oracle import select as osel
+
+
+def _pool(m=4000, seed=0):
+    rng = np.random.default_rng(seed)
+    scores = np.round(rng.standard_normal(m), 1)          # heavy ties
+    dig = rng.integers(0, 2**31, size=(m, 8), dtype=np.int64).astype(np.int32)
+    # plant duplicates: later candidates repeat earlier configs (same digest, same score)
+    for a, b in [(5, 3100), (17, 2500), (2600, 3999), (100, 101)]:
+        dig[b] = dig[a]
+        scores[b] = scores[a]
+    scores[::53] = np.nan
+    return scores, dig
+
+
+def _global_ref(scores, dig, k):
+    hexes = [row.tobytes() for row in dig]
+    dup = osel.dedup(hexes, set())
+    return osel.topk(list(scores), k, dup=dup)
+
+
+def _worker(rank, world, port, k, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from uptune_amd.dist import allgather_topk, broadcast_history
+    scores, dig = _pool()
+    m = len(scores)
+    lo, hi = rank * m // world, (rank + 1) * m // world
+    # local shard: in-shard dedup + local top-k (what ut_score_round_* returns)
+    hexes = [row.tobytes() for row in dig[lo:hi]]
+    dup = osel.dedup(hexes, set())
+    loc = osel.topk(list(scores[lo:hi]), k, dup=dup, cand_base=lo)
+    li = torch.tensor(loc, dtype=torch.int64)
+    ls = torch.tensor([scores[g] if g >= 0 else float("-inf") for g in loc], dtype=torch.float64)
+    ld = torch.tensor(np.stack([dig[g] if g >= 0 else np.zeros(8, np.int32) for g in loc]), dtype=torch.int32)
+    gi, gs = allgather_topk(li, ls, ld, k)
+    X = torch.arange(12, dtype=torch.float64).reshape(3, 4) if rank == 0 else None
+    y = torch.tensor([1.0, 2.0, 3.0]) if rank == 0 else None
+    dd = torch.arange(24, dtype=torch.int32).reshape(3, 8) if rank == 0 else None
+    X, y, dd = broadcast_history(X, y, dd, 3, 4, "cpu")
+    q.put((rank, gi.tolist(), float(X.sum()), float(y.sum()), int(dd.sum())))
+    dist.destroy_process_group()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.parametrize("world,k", [(2, 64), (2, 7), (4, 32)])
+def test_sharded_topk_equals_global(world, k):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, k, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    scores, dig = _pool()
+    want = _global_ref(scores, dig, k)
+    for rank, got, xs, ys, ds in res:
+        assert got == want
+        assert (xs, ys, ds) == (66.0, 6.0, 276)
+
+
+def test_merge_topk_unit():
+    from uptune_amd.dist import merge_topk
+    s = torch.tensor([0.9, 0.5, 0.9, 0.7, float("-inf")], dtype=torch.float64)
+    i = torch.tensor([7, 3, 2, 9, -1])
+    d = torch.tensor([[1] * 8, [2] * 8, [3] * 8, [1] * 8, [0] * 8], dtype=torch.int32)
+    gi, gs = merge_topk(s, i, d, 4)
+    # digest [1]*8 appears as idx 7 and 9 -> 7 survives
+    assert gi.tolist() == [2, 7, 3, -1]

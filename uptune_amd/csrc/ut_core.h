@@ -24,6 +24,7 @@
 #define UT_HD __host__ __device__ __forceinline__
 #define UT_CONST_TABLE static constexpr
 #else
+#include <math.h>
 #define UT_HD static inline
 #define UT_CONST_TABLE static constexpr
 #endif
@@ -469,6 +470,119 @@ UT_HD int repr_int64(int64_t v, Emit& out) {
     u = q;
   }
   return s + (int)n;
+}
+
+// ---------------------------------------------------------------------------
+// Deterministic exp / log / normal draws.  Built only from IEEE +,-,*,/,
+// sqrt and exponent-field manipulation, evaluated in a fixed order (the
+// kernels are compiled with -ffp-contract=off), so the device and the numpy
+// oracle (oracle/mathx.py) produce identical bits -- libm/ocml results may
+// differ by an ulp and would otherwise leak into discrete PSO/GA outcomes.
+// Accuracy ~1 ulp over the ranges used.
+// ---------------------------------------------------------------------------
+UT_HD double bits_to_d(uint64_t b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __longlong_as_double((long long)b);
+#else
+  double d;
+  __builtin_memcpy(&d, &b, 8);
+  return d;
+#endif
+}
+UT_HD uint64_t d_to_bits(double d) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return (uint64_t)__double_as_longlong(d);
+#else
+  uint64_t b;
+  __builtin_memcpy(&b, &d, 8);
+  return b;
+#endif
+}
+UT_HD double dsqrt(double x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __dsqrt_rn(x);
+#else
+  return __builtin_sqrt(x);
+#endif
+}
+
+constexpr double UT_LN2_HI = 6.93147180369123816490e-01;  // ln2 with 32 trailing zero bits
+constexpr double UT_LN2_LO = 1.90821492927058770002e-10;
+constexpr double UT_INV_LN2 = 1.44269504088896338700e+00;
+constexpr double UT_SQRT2 = 1.41421356237309514547e+00;
+
+// natural log for positive normal x
+UT_HD double ut_log(double x) {
+  const uint64_t b = d_to_bits(x);
+  int32_t e = (int32_t)((b >> 52) & 0x7FF) - 1023;
+  double m = bits_to_d((b & 0x000FFFFFFFFFFFFFull) | 0x3FF0000000000000ull);  // [1, 2)
+  if (m > UT_SQRT2) {
+    m = bits_to_d((b & 0x000FFFFFFFFFFFFFull) | 0x3FE0000000000000ull);        // [0.5, 1)
+    e += 1;
+  }
+  const double s = (m - 1.0) / (m + 1.0);
+  const double s2 = s * s;
+  double p = 1.0 / 23.0;
+  p = p * s2 + 1.0 / 21.0;
+  p = p * s2 + 1.0 / 19.0;
+  p = p * s2 + 1.0 / 17.0;
+  p = p * s2 + 1.0 / 15.0;
+  p = p * s2 + 1.0 / 13.0;
+  p = p * s2 + 1.0 / 11.0;
+  p = p * s2 + 1.0 / 9.0;
+  p = p * s2 + 1.0 / 7.0;
+  p = p * s2 + 1.0 / 5.0;
+  p = p * s2 + 1.0 / 3.0;
+  const double lm = (2.0 * s) + ((2.0 * s) * (s2 * p));
+  const double fe = (double)e;
+  return (fe * UT_LN2_HI) + ((fe * UT_LN2_LO) + lm);
+}
+
+// exp(x); 0 for x < -745.2, +inf for x > 709.78
+UT_HD double ut_exp(double x) {
+  if (x != x) return x;
+  if (x > 709.782712893384) return bits_to_d(0x7FF0000000000000ull);
+  if (x < -745.2) return 0.0;
+  const double kd = rint(x * UT_INV_LN2);
+  const double r = (x - kd * UT_LN2_HI) - kd * UT_LN2_LO;
+  double p = 1.0 / 6227020800.0;        // 1/13!
+  p = p * r + 1.0 / 479001600.0;
+  p = p * r + 1.0 / 39916800.0;
+  p = p * r + 1.0 / 3628800.0;
+  p = p * r + 1.0 / 362880.0;
+  p = p * r + 1.0 / 40320.0;
+  p = p * r + 1.0 / 5040.0;
+  p = p * r + 1.0 / 720.0;
+  p = p * r + 1.0 / 120.0;
+  p = p * r + 1.0 / 24.0;
+  p = p * r + 1.0 / 6.0;
+  p = p * r + 0.5;
+  p = p * r + 1.0;
+  p = p * r + 1.0;
+  int32_t k = (int32_t)kd;
+  if (k > 1023) {  // x just below the overflow threshold: 2^k in two steps
+    p = p * 2.0;
+    k -= 1;
+  }
+  if (k < -1021) {
+    p = p * bits_to_d((uint64_t)(k + 1000 + 1023) << 52);
+    return p * bits_to_d((uint64_t)(-1000 + 1023) << 52);
+  }
+  return p * bits_to_d((uint64_t)(k + 1023) << 52);
+}
+
+// standard normal by Marsaglia's polar method over counter draws; attempt a
+// uses stream (stream | a << 24).  16 attempts (P(all rejected) ~ 2e-11,
+// then 0.0).
+UT_HD double normal_draw(uint64_t seed, uint64_t cand, uint32_t stream, uint32_t round_, uint32_t op) {
+  for (uint32_t a = 0; a < 16; ++a) {
+    const u32x4 r = draw(seed, cand, stream | (a << 24), round_, op);
+    const double u = 2.0 * u01_from(r.x, r.y) - 1.0;
+    const double v = 2.0 * u01_from(r.z, r.w) - 1.0;
+    const double s = u * u + v * v;
+    if (s > 0.0 && s < 1.0) return u * dsqrt((-2.0 * ut_log(s)) / s);
+  }
+  return 0.0;
 }
 
 // ---------------------------------------------------------------------------

@@ -1,0 +1,90 @@
+"""Multi-GPU exchange for the scoring round (one process per GPU).
+
+SURVEY.md §8(e): the candidate pool is sharded by GLOBAL candidate index
+(rank r owns [r*m, (r+1)*m)); population, training set, GP factor and history
+are replicated.  Two real exchanges exist per round:
+
+  * all_gather of every rank's local top-k records (score, index, digest) and a
+    deterministic merge -- cross-shard duplicates (equal digests) keep the
+    smallest global index, ties on score break by the smallest index, so the
+    merged top-k is identical to the single-GPU result for the same pool;
+  * broadcast from rank 0 of the per-round history delta (new evaluated rows,
+    their objective values and digests) -- the analog of the reference's
+    per-round api.sync result injection (python/uptune/api.py:547-553,
+    opentuner/api.py:87-104).
+
+Backend "nccl" is RCCL over xGMI on ROCm; the same code runs with "gloo" on
+CPU tensors (tests/test_dist_cpu.py).  Payloads are a few KB (latency
+bound), so there is no bucketing.
+"""
+from __future__ import annotations
+
+from typing import Optional, Tuple
+
+import torch
+import torch.distributed as dist
+
+
+def merge_topk(scores: torch.Tensor, idx: torch.Tensor, digests: torch.Tensor, k: int
+               ) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Merge gathered local top-k lists.
+
+    scores [R*k] f64, idx [R*k] i64 (-1 = empty slot), digests [R*k][8] i32.
+    Returns (idx [k], score [k]) sorted by (-score, idx), empty slots -1.
+    """
+    valid = idx >= 0
+    s = scores[valid]
+    i = idx[valid]
+    d = digests[valid]
+    if i.numel():
+        # first (smallest global index) occurrence of each digest survives
+        _, inv = torch.unique(d, dim=0, return_inverse=True)
+        big = torch.iinfo(torch.int64).max
+        first = torch.full((int(inv.max().item()) + 1,), big, dtype=torch.int64, device=i.device)
+        first = first.scatter_reduce(0, inv, i, reduce="amin")
+        keep = i == first[inv]
+        s, i = s[keep], i[keep]
+        # sort by index, then stable by descending score -> (-score, idx) order
+        o = torch.argsort(i, stable=True)
+        s, i = s[o], i[o]
+        o = torch.argsort(-s, stable=True)
+        s, i = s[o], i[o]
+    out_i = torch.full((k,), -1, dtype=torch.int64, device=idx.device)
+    out_s = torch.full((k,), float("-inf"), dtype=scores.dtype, device=idx.device)
+    n = min(k, i.numel())
+    out_i[:n] = i[:n]
+    out_s[:n] = s[:n]
+    return out_i, out_s
+
+
+def allgather_topk(idx: torch.Tensor, score: torch.Tensor, digest: torch.Tensor, k: int,
+                   group: Optional[dist.ProcessGroup] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+    """all_gather the local (idx, score, digest) top-k of every rank and merge."""
+    world = dist.get_world_size(group)
+    gi = [torch.empty_like(idx) for _ in range(world)]
+    gs = [torch.empty_like(score) for _ in range(world)]
+    gd = [torch.empty_like(digest) for _ in range(world)]
+    dist.all_gather(gi, idx.contiguous(), group=group)
+    dist.all_gather(gs, score.contiguous(), group=group)
+    dist.all_gather(gd, digest.contiguous(), group=group)
+    return merge_topk(torch.cat(gs), torch.cat(gi), torch.cat(gd), k)
+
+
+def broadcast_history(X: Optional[torch.Tensor], y: Optional[torch.Tensor], digests: Optional[torch.Tensor],
+                      n: int, d: int, device, src: int = 0, group: Optional[dist.ProcessGroup] = None
+                      ) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+    """Broadcast a history delta of n rows (features [n][d] f64, y [n] f64,
+    digests [n][8] i32) from `src` to every rank; non-src ranks pass None."""
+    rank = dist.get_rank(group)
+    if rank == src:
+        X = X.to(device, torch.float64).contiguous()
+        y = y.to(device, torch.float64).contiguous()
+        digests = digests.to(device, torch.int32).contiguous()
+    else:
+        X = torch.empty((n, d), dtype=torch.float64, device=device)
+        y = torch.empty((n,), dtype=torch.float64, device=device)
+        digests = torch.empty((n, 8), dtype=torch.int32, device=device)
+    dist.broadcast(X, src, group=group)
+    dist.broadcast(y, src, group=group)
+    dist.broadcast(digests, src, group=group)
+    return X, y, digests
