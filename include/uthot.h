@@ -134,6 +134,42 @@ int ut_population_replace(ut_ctx* ctx, const double* trial, int64_t ld, const in
 int ut_propose_de(ut_ctx* ctx, const ut_de_params* p, uint32_t round_, int64_t cand_base, int64_t m,
                   double* out_values, int64_t ld);
 
+/* PSO (pso.py:11-77, HybridParticle + op3_swarm per kind).  Candidate g
+ * moves particle g % npop towards gbest (device row [P]) and its own best. */
+typedef struct ut_pso_params {
+  double omega, phi_l, phi_g;   /* 0.5, 0.5, 0.5 (pso.py:202) */
+  double sigma;                 /* Int/Pow2 gaussian noise, unit scale 0.2 (manipulator.py:661) */
+  int32_t alias_pbest;          /* 1 = reference: particle.best IS the position (pso.py:212-213) */
+  int32_t enum_mode;            /* 0 = reference: enum never moves (manipulator.py:442); 1 = corrected */
+} ut_pso_params;
+/* velocities := 0 and particle bests := positions (pso.py:218-221) */
+int ut_pso_reset(ut_ctx* ctx);
+int ut_propose_pso(ut_ctx* ctx, const ut_pso_params* p, const double* gbest, uint32_t round_, int64_t cand_base,
+                   int64_t m, double* out_values, double* out_velocity, int64_t ld);
+/* particles [cand_base, cand_base+m) take the moved positions / velocities */
+int ut_pso_commit(ut_ctx* ctx, const double* values, const double* velocity, int64_t ld, int64_t cand_base,
+                  int64_t m);
+/* particle bests for selected particles: best[:, idx[j]] = values[:, j] */
+int ut_pso_update_best(ut_ctx* ctx, const double* values, int64_t ld, const int64_t* idx, int64_t n);
+
+/* GA family (evolutionarytechniques.py:13-158, globalGA.py:11-129). */
+typedef struct ut_ga_params {
+  double mutation_rate;       /* per-param mutation probability */
+  double sigma;               /* NormalMutationMixin sigma (0.1) */
+  double crossover_rate;      /* probability of selecting two parents */
+  double crossover_strength;  /* GGA: fraction of params copied from parent 2 (0.2); 0 = GA family */
+  int32_t must_mutate_count;  /* 1; <= P */
+  int32_t normal;             /* 1 = NormalGreedyMutation / GGA, 0 = UniformGreedyMutation / GA */
+  int32_t max_retries;        /* 10 (hash equal to a parent -> mutate again); <= 15 */
+  int32_t op;                 /* RNG stream family: 4 = GA, 5 = GGA */
+} ut_ga_params;
+/* parent1/parent2: device rows [P] (the global best), NULL = random parent
+ * (select() without a best result).  out_invalid[i] = 1 when all retries
+ * reproduced a parent (the reference returns None). */
+int ut_propose_ga(ut_ctx* ctx, const ut_ga_params* p, const double* parent1, const double* parent2,
+                  uint32_t round_, int64_t cand_base, int64_t m, double* out_values, int64_t ld,
+                  uint8_t* out_invalid);
+
 /* GP features of configurations: unit values (get_unit_value), BOOL 0/1,
  * ENUM one-hot.  out_features[f * ld_out + i]. */
 int ut_encode_features(ut_ctx* ctx, const double* values, int64_t ld, int64_t m, double* out_features,

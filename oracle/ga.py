@@ -20,9 +20,14 @@ Per candidate (one `desired_configuration` call):
       accept when hash_config(cfg) is not a parent hash  == the values differ
       bitwise from every parent
   after max_retries failures the technique returns None (candidate invalid).
+"The first d params of a shuffle" is a uniformly random d-subset; the batch
+form draws it with Knuth's selection sampling (Algorithm S: param p joins
+with probability (d - chosen) / (P - p), exactly d chosen), one uniform per
+param.
 Draws (op = OP_GA or OP_GGA): CAND|0 -> parents; p|2<<28 / p|3<<28 random
-parent values; p|4<<28 crossover keys; p|r<<20 per-retry keys + mutation
-coins; p|r<<20|1<<28 randomize values; p|r<<20|2<<28 normal draws.
+parent values; p|4<<28 crossover subset; p|r<<20: (x,y) must-mutate subset,
+(z,w) mutation coin; p|r<<20|1<<28 randomize values; p|r<<20|2<<28 normal
+draws.
 """
 import numpy as np
 
@@ -36,17 +41,25 @@ def _rand_col(prm, seed, g, stream, round_, op):
     return np.array([to_f64(prm, randomize(prm, int(a), int(b), int(c), int(d))) for a, b, c, d in zip(x, y, z, w)])
 
 
-def _smallest(keys, n):
-    """bool [P][m]: rank (by key) < n"""
-    if n <= 0:
-        return np.zeros(keys.shape, dtype=bool)
-    rank = np.argsort(np.argsort(keys, axis=0, kind="stable"), axis=0, kind="stable")
-    return rank < n
+def select_subset(u, d):
+    """Algorithm S over params in order: u [P][m] uniforms -> bool [P][m] with
+    exactly d True per column"""
+    P, m = u.shape
+    chosen = np.zeros(m, dtype=np.float64)
+    out = np.zeros((P, m), dtype=bool)
+    for p in range(P):
+        take = (float(P - p) * u[p]) < (float(d) - chosen)
+        out[p] = take
+        chosen = chosen + take
+    return out
 
 
-def _keys(seed, g, P, stream_of, round_, op):
-    return np.stack([(ph.draw(seed, g, stream_of(p), round_, op)[2].astype(np.uint64) << np.uint64(32)) |
-                     np.uint64(p) for p in range(P)])
+def _uniforms(seed, g, P, stream_of, round_, op, hi=False):
+    rows = []
+    for p in range(P):
+        x, y, z, w = ph.draw(seed, g, stream_of(p), round_, op)
+        rows.append(ph.u01(z, w) if hi else ph.u01(x, y))
+    return np.stack(rows)
 
 
 def propose_ga_vec(space, parent1, parent2, seed, round_, cand_base, m, mutation_rate=0.1, must_mutate_count=1,
@@ -69,15 +82,15 @@ def propose_ga_vec(space, parent1, parent2, seed, round_, cand_base, m, mutation
     cfg = P1.copy()
     if crossover_strength > 0:
         d = int(crossover_strength * P)
-        sel = _smallest(_keys(seed, g, P, lambda p: p | (4 << 28), round_, op), d) & two[None, :]
+        sel = select_subset(_uniforms(seed, g, P, lambda p: p | (4 << 28), round_, op), d) & two[None, :]
         cfg = np.where(sel, P2, cfg)
     accepted = np.zeros(m, dtype=bool)
     for r in range(max_retries):
         active = ~accepted
-        forced = _smallest(_keys(seed, g, P, lambda p: p | (r << 20), round_, op), must_mutate_count)
+        forced = select_subset(_uniforms(seed, g, P, lambda p: p | (r << 20), round_, op), must_mutate_count)
         for p, prm in enumerate(space):
-            xx, yy, _, _ = ph.draw(seed, g, p | (r << 20), round_, op)
-            mut = active & (forced[p] | (ph.u01(xx, yy) < mutation_rate))
+            _, _, zz, ww = ph.draw(seed, g, p | (r << 20), round_, op)
+            mut = active & (forced[p] | (ph.u01(zz, ww) < mutation_rate))
             if not mut.any():
                 continue
             gi = g[mut]

@@ -346,3 +346,58 @@ def test_full_size_round_properties():
     pop = e.population_get().cpu().numpy()
     sub = ode.propose_de_vec(space, pop, 1, 0, 0, m, 0.2, 1)[:, idx]
     np.testing.assert_array_equal(v, sub)
+
+
+# --------------------------------------------------------------------------- PSO / GA
+@pytest.mark.parametrize("alias,enum_mode", [(True, 0), (False, 1)])
+def test_pso_matches_oracle(alias, enum_mode):
+    from oracle import pso as opso
+    space = mixed_space()
+    e = engine(space, seed=31)
+    pop = ode.population_init(space, 700, seed=6)
+    e.population_set(dev(pop))
+    e.pso_reset()
+    vel = np.zeros_like(pop)
+    gbest = pop[:, 17].copy()
+    x, v = e.propose_pso(gbest, 700, round_=4, alias_pbest=alias, enum_mode=enum_mode)
+    wx, wv = opso.propose_pso_vec(space, pop, vel, pop, gbest, 31, 4, 0, 700, enum_mode=enum_mode)
+    np.testing.assert_array_equal(x.cpu().numpy(), wx)
+    np.testing.assert_array_equal(v.cpu().numpy(), wv)
+    # second generation from committed state (non-zero velocities)
+    e.pso_commit(x, v)
+    x2, v2 = e.propose_pso(gbest, 1400, round_=5, cand_base=0, alias_pbest=alias, enum_mode=enum_mode)
+    pb = wx if alias else pop
+    wx2, wv2 = opso.propose_pso_vec(space, wx, wv, pb, gbest, 31, 5, 0, 1400, enum_mode=enum_mode)
+    np.testing.assert_array_equal(x2.cpu().numpy(), wx2)
+    np.testing.assert_array_equal(v2.cpu().numpy(), wv2)
+
+
+@pytest.mark.parametrize("kw", [
+    dict(mutation_rate=0.1),                                             # UniformGreedyMutation / ga-base
+    dict(mutation_rate=0.3, normal=True, sigma=0.1),                     # NormalGreedyMutation(0.3)
+    dict(mutation_rate=0.1, normal=True, crossover_rate=0.5, crossover_strength=0.2, op=5),   # GGA
+    dict(mutation_rate=0.01, crossover_rate=0.8),                        # GA(crossover=...)
+])
+def test_ga_matches_oracle(kw):
+    from oracle import ga as oga
+    space = mixed_space() + [Param("z%d" % i, INT, 0, 3) for i in range(8)]
+    e = engine(space, seed=41)
+    pop = ode.population_init(space, 8, seed=9)
+    best = pop[:, 0].copy()
+    for p1, p2 in [(best, None), (None, None), (best, pop[:, 1].copy())]:
+        got, inv = e.propose_ga(3000, parent1=p1, parent2=p2, round_=2, cand_base=11, **kw)
+        want, winv = oga.propose_ga_vec(space, p1, p2, 41, 2, 11, 3000, **kw)
+        np.testing.assert_array_equal(got.cpu().numpy(), want)
+        np.testing.assert_array_equal(inv.cpu().numpy().astype(bool), winv)
+
+
+def test_ga_retry_gives_up_on_tiny_space():
+    """A 1-value space can never differ from its parent: every candidate is
+    invalid after max_retries (the reference returns None, :45-49)."""
+    from oracle import ga as oga
+    space = [Param("only", INT, 5, 5), Param("b", ENUM, options=["x"])]
+    e = engine(space, seed=1)
+    got, inv = e.propose_ga(100, parent1=np.array([5.0, 0.0]), mutation_rate=0.5)
+    assert inv.cpu().numpy().all()
+    _, winv = oga.propose_ga_vec(space, np.array([5.0, 0.0]), None, 1, 0, 0, 100, mutation_rate=0.5)
+    assert winv.all()

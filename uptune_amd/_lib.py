@@ -36,6 +36,17 @@ class DeParams(C.Structure):
     _fields_ = [("cr", C.c_double), ("n_cross", C.c_int32), ("pad", C.c_int32)]
 
 
+class PsoParams(C.Structure):
+    _fields_ = [("omega", C.c_double), ("phi_l", C.c_double), ("phi_g", C.c_double), ("sigma", C.c_double),
+                ("alias_pbest", C.c_int32), ("enum_mode", C.c_int32)]
+
+
+class GaParams(C.Structure):
+    _fields_ = [("mutation_rate", C.c_double), ("sigma", C.c_double), ("crossover_rate", C.c_double),
+                ("crossover_strength", C.c_double), ("must_mutate_count", C.c_int32), ("normal", C.c_int32),
+                ("max_retries", C.c_int32), ("op", C.c_int32)]
+
+
 class GpHyper(C.Structure):
     _fields_ = [("sigma_f2", C.c_double), ("sigma_n2", C.c_double), ("jitter", C.c_double),
                 ("lengthscale_host", C.c_void_p)]
@@ -68,6 +79,11 @@ SIGNATURES = {
     "ut_population_get": (C.c_int, [P, P, I64]),
     "ut_population_replace": (C.c_int, [P, P, I64, P, I64]),
     "ut_propose_de": (C.c_int, [P, C.POINTER(DeParams), U32, I64, I64, P, I64]),
+    "ut_pso_reset": (C.c_int, [P]),
+    "ut_propose_pso": (C.c_int, [P, C.POINTER(PsoParams), P, U32, I64, I64, P, P, I64]),
+    "ut_pso_commit": (C.c_int, [P, P, P, I64, I64, I64]),
+    "ut_pso_update_best": (C.c_int, [P, P, I64, P, I64]),
+    "ut_propose_ga": (C.c_int, [P, C.POINTER(GaParams), P, P, U32, I64, I64, P, I64, P]),
     "ut_encode_features": (C.c_int, [P, P, I64, I64, P, I64]),
     "ut_hash": (C.c_int, [P, P, I64, I64, P]),
     "ut_history_reset": (C.c_int, [P, I64]),

@@ -160,7 +160,7 @@ int ut_ctx_destroy(ut_ctx* c) {
   hipStreamSynchronize(c->stream);
   free_space(c->space);
   auto fr = [](void* p) { if (p) hipFree(p); };
-  fr(c->pop); fr(c->hist_keys); fr(c->hist_state); fr(c->batch_slots);
+  fr(c->pop); fr(c->pso_vel); fr(c->pso_best); fr(c->hist_keys); fr(c->hist_state); fr(c->batch_slots);
   fr(c->gp_Xs); fr(c->gp_xnorm); fr(c->gp_K); fr(c->gp_Linv); fr(c->gp_y); fr(c->gp_tmp);
   fr(c->gp_alpha); fr(c->gp_inv_ell); fr(c->gp_stats); fr(c->gp_flag);
   fr(c->kst.p); fr(c->mu_part.p); fr(c->var_part.p); fr(c->cnorm.p);

@@ -207,6 +207,144 @@ __global__ void k_pop_replace(int32_t P, double* __restrict__ pop, int64_t ldp, 
   for (int32_t p = 0; p < P; ++p) pop[(int64_t)p * ldp + dst] = trial[(int64_t)p * ld + j];
 }
 
+// ---------------------------------------------------------------------------
+// PSO: HybridParticle.move (pso.py:70-77) with the per-kind op3_swarm
+// (manipulator.py:660-700 Int, :709-744 Float, :962-996 Bool, :409-443 Enum).
+// Candidate g moves particle g % npop:  cfg = x, cfg1 = gbest, cfg2 = pbest,
+// c = omega, c1 = phi_g, c2 = phi_l.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_pso(const DevParam* __restrict__ params, int32_t P,
+                                             const double* __restrict__ pos, const double* __restrict__ vel,
+                                             const double* __restrict__ pbest, int64_t ldp, int64_t npop,
+                                             const double* __restrict__ gbest, double c, double c1, double c2,
+                                             double sigma, int32_t enum_mode, uint64_t seed, uint32_t round_,
+                                             int64_t cand_base, int64_t m, double* __restrict__ out_x,
+                                             double* __restrict__ out_v, int64_t ldo) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= m) return;
+  const uint64_t g = (uint64_t)(cand_base + i);
+  const int64_t t = (int64_t)(g % (uint64_t)npop);
+  for (int32_t p = 0; p < P; ++p) {
+    const DevParam pr = params[p];
+    const int64_t o = (int64_t)p * ldp + t;
+    const double x = pos[o], v = vel[o], l = pbest[o], gb = gbest[p];
+    const u32x4 r = draw(seed, g, (uint32_t)p, round_, OP_PSO);
+    const double r1 = u01_from(r.x, r.y), r2 = u01_from(r.z, r.w);
+    double nx, nv;
+    if (pr.kind == UT_ENUM) {
+      nv = v;
+      nx = x;  // reference: opn_stochastic_mix copies the particle INTO the parent (manipulator.py:442)
+      if (enum_mode == 1) {
+        const u32x4 q = draw(seed, g, (uint32_t)p | (1u << STREAM_SUB_SHIFT), round_, OP_PSO);
+        const double rr = u01_from(q.x, q.y);
+        const double tot = (c + c1) + c2;
+        const double w0 = c / tot, w1 = c1 / tot;
+        nx = rr < w0 ? x : (rr < w0 + w1 ? gb : l);
+      }
+    } else {
+      nv = ((v * c) + (((gb - x) * c1) * r1)) + (((l - x) * c2) * r2);
+      if (pr.kind == UT_FLOAT) {
+        double y = x + nv;
+        y = (pr.lo > y) ? pr.lo : y;   // max(p, vmin)
+        nx = (y < pr.hi) ? y : pr.hi;  // min(vmax, .)
+      } else if (pr.kind == UT_INT) {
+        const double k = pr.hi - pr.lo;
+        const double s = k / (1.0 + ut_exp(-nv)) + pr.lo;
+        const double z = normal_draw(seed, g, (uint32_t)p | (2u << STREAM_SUB_SHIFT), round_, OP_PSO);
+        double pp = rint(s + z * (sigma * k));
+        pp = (pr.lo > pp) ? pr.lo : pp;
+        nx = (pp < pr.hi) ? pp : pr.hi;
+      } else {  // BOOL
+        const double s = 1.0 / (1.0 + ut_exp(-nv));
+        const u32x4 q = draw(seed, g, (uint32_t)p | (1u << STREAM_SUB_SHIFT), round_, OP_PSO);
+        nx = ((s - u01_from(q.x, q.y)) > 0.0) ? 1.0 : 0.0;
+      }
+    }
+    out_x[(int64_t)p * ldo + i] = nx;
+    if (out_v) out_v[(int64_t)p * ldo + i] = nv;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// GA family: EvolutionaryTechnique.desired_configuration
+// (evolutionarytechniques.py:29-61), NormalMutationMixin (:98-114), GGA
+// crossover (globalGA.py:227-235).  Random d-subsets ("first d of a shuffle")
+// by selection sampling, one uniform per parameter (oracle/ga.py).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ double parent_value(const DevParam& pr, const double* parent, int32_t p, uint32_t sub,
+                                               uint64_t seed, uint64_t g, uint32_t round_, uint32_t op) {
+  if (parent) return parent[p];
+  return randomize(pr, draw(seed, g, (uint32_t)p | (sub << STREAM_SUB_SHIFT), round_, op));
+}
+
+__global__ __launch_bounds__(256) void k_ga(const DevParam* __restrict__ params, int32_t P,
+                                            const double* __restrict__ parent1, const double* __restrict__ parent2,
+                                            double mutation_rate, double sigma, double crossover_rate, int32_t d_cross,
+                                            int32_t must, int32_t normal, int32_t max_retries, uint32_t op,
+                                            uint64_t seed, uint32_t round_, int64_t cand_base, int64_t m,
+                                            double* __restrict__ out, int64_t ldo, uint8_t* __restrict__ invalid) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= m) return;
+  const uint64_t g = (uint64_t)(cand_base + i);
+  const u32x4 rc = draw(seed, g, STREAM_CAND | 0u, round_, op);
+  const bool two = u01_from(rc.x, rc.y) < crossover_rate;
+  const double* p2row = parent2 ? parent2 : parent1;  // select() twice returns the same best config
+  // parent 1 (and the GGA crossover from parent 2)
+  double chosen = 0.0;
+  for (int32_t p = 0; p < P; ++p) {
+    const DevParam pr = params[p];
+    double v = parent_value(pr, parent1, p, 2u, seed, g, round_, op);
+    if (d_cross > 0 && two) {
+      const u32x4 q = draw(seed, g, (uint32_t)p | (4u << STREAM_SUB_SHIFT), round_, op);
+      if ((double)(P - p) * u01_from(q.x, q.y) < (double)d_cross - chosen) {
+        chosen += 1.0;
+        v = parent_value(pr, p2row, p, 3u, seed, g, round_, op);
+      }
+    }
+    out[(int64_t)p * ldo + i] = v;
+  }
+  bool accepted = false;
+  for (int32_t r = 0; r < max_retries && !accepted; ++r) {
+    bool diff1 = false, diff2 = false;
+    double sel = 0.0;
+    for (int32_t p = 0; p < P; ++p) {
+      const DevParam pr = params[p];
+      const uint32_t sp = (uint32_t)p | ((uint32_t)r << STREAM_RETRY_SHIFT);
+      const u32x4 q = draw(seed, g, sp, round_, op);
+      bool mut = false;
+      if ((double)(P - p) * u01_from(q.x, q.y) < (double)must - sel) {
+        sel += 1.0;
+        mut = true;
+      }
+      mut = mut || (u01_from(q.z, q.w) < mutation_rate);
+      const int64_t o = (int64_t)p * ldo + i;
+      double v = out[o];
+      if (mut) {
+        if (normal && is_primitive(pr.kind)) {
+          // op1_normal_mutation (manipulator.py:505-521)
+          double u = unit_of(pr, v);
+          const double z = normal_draw(seed, g, sp | (2u << STREAM_SUB_SHIFT), round_, op);
+          u = u + (0.0 + z * sigma);
+          if (u < 0.0) u = u * -1.0;
+          if (u > 1.0) u = 1.0 - fmod(u, 1.0);
+          v = from_unit(pr, u, v);
+        } else if (normal && pr.kind == UT_BOOL) {
+          v = 1.0 - v;  // op1_flip
+        } else {
+          v = randomize(pr, draw(seed, g, sp | (1u << STREAM_SUB_SHIFT), round_, op));
+        }
+        out[o] = v;
+      }
+      const double a = parent_value(pr, parent1, p, 2u, seed, g, round_, op);
+      const double b = parent_value(pr, p2row, p, 3u, seed, g, round_, op);
+      diff1 |= d_to_bits(v) != d_to_bits(a);
+      diff2 |= d_to_bits(v) != d_to_bits(b);
+    }
+    accepted = diff1 && (!two || diff2);
+  }
+  if (invalid) invalid[i] = accepted ? 0 : 1;
+}
+
 int launch_population_init(ut_ctx* c, uint32_t round_) {
   hipLaunchKernelGGL(k_population_init, dim3(grid1(c->npop, 256)), dim3(256), 0, c->stream, c->space.d_params,
                      c->space.P, c->pop, c->npop, c->npop, c->seed, round_);
@@ -218,6 +356,26 @@ int launch_de(ut_ctx* c, const ut_de_params* p, uint32_t round_, int64_t cand_ba
               int64_t ld) {
   hipLaunchKernelGGL(k_de, dim3(grid1(m, 256)), dim3(256), 0, c->stream, c->space.d_params, c->space.P, c->pop,
                      c->npop, c->npop, p->cr, p->n_cross, c->seed, round_, cand_base, m, out, ld);
+  UT_LAUNCH_CHECK(c);
+  return 0;
+}
+
+int launch_pso(ut_ctx* c, const ut_pso_params* a, const double* gbest, uint32_t round_, int64_t cand_base,
+               int64_t m, double* out_x, double* out_v, int64_t ld) {
+  const double* pb = a->alias_pbest ? c->pop : c->pso_best;
+  hipLaunchKernelGGL(k_pso, dim3(grid1(m, 256)), dim3(256), 0, c->stream, c->space.d_params, c->space.P, c->pop,
+                     c->pso_vel, pb, c->npop, c->npop, gbest, a->omega, a->phi_g, a->phi_l, a->sigma, a->enum_mode,
+                     c->seed, round_, cand_base, m, out_x, out_v, ld);
+  UT_LAUNCH_CHECK(c);
+  return 0;
+}
+
+int launch_ga(ut_ctx* c, const ut_ga_params* a, const double* parent1, const double* parent2, uint32_t round_,
+              int64_t cand_base, int64_t m, double* out, int64_t ld, uint8_t* invalid) {
+  const int32_t d = (int32_t)(a->crossover_strength * (double)c->space.P);  // int(strength * len(params))
+  hipLaunchKernelGGL(k_ga, dim3(grid1(m, 256)), dim3(256), 0, c->stream, c->space.d_params, c->space.P, parent1,
+                     parent2, a->mutation_rate, a->sigma, a->crossover_rate, d, a->must_mutate_count, a->normal,
+                     a->max_retries, (uint32_t)a->op, c->seed, round_, cand_base, m, out, ld, invalid);
   UT_LAUNCH_CHECK(c);
   return 0;
 }
@@ -248,4 +406,77 @@ extern "C" int ut_population_replace(ut_ctx* c, const double* trial, int64_t ld,
                      c->npop, trial, ld, idx, n);
   UT_LAUNCH_CHECK(c);
   return 0;
+}
+
+extern "C" int ut_pso_reset(ut_ctx* c) {
+  if (!c) return UT_EINVAL;
+  UT_CHECK(c, c->has_space && c->pop != nullptr, UT_EINVAL, "pso_reset: population not initialised");
+  const int64_t need = c->npop * c->space.P;
+  if (c->pso_cap < need) {
+    if (c->pso_vel) {
+      UT_HIP(c, hipStreamSynchronize(c->stream));
+      hipFree(c->pso_vel);
+      hipFree(c->pso_best);
+    }
+    UT_HIP(c, hipMalloc((void**)&c->pso_vel, sizeof(double) * need));
+    UT_HIP(c, hipMalloc((void**)&c->pso_best, sizeof(double) * need));
+    c->pso_cap = need;
+  }
+  UT_HIP(c, hipMemsetAsync(c->pso_vel, 0, sizeof(double) * need, c->stream));
+  UT_HIP(c, hipMemcpyAsync(c->pso_best, c->pop, sizeof(double) * need, hipMemcpyDeviceToDevice, c->stream));
+  return 0;
+}
+
+extern "C" int ut_propose_pso(ut_ctx* c, const ut_pso_params* a, const double* gbest, uint32_t round_,
+                              int64_t cand_base, int64_t m, double* out_values, double* out_vel, int64_t ld) {
+  if (!c) return UT_EINVAL;
+  UT_CHECK(c, c->has_space && c->pop != nullptr, UT_EINVAL, "propose_pso: population not initialised");
+  UT_CHECK(c, c->pso_vel != nullptr && c->pso_cap >= c->npop * c->space.P, UT_EINVAL,
+           "propose_pso: call ut_pso_reset after (re)initialising the population");
+  UT_CHECK(c, a && gbest && out_values && m >= 0 && cand_base >= 0 && ld >= m, UT_EINVAL,
+           "propose_pso: bad arguments");
+  for (int32_t p = 0; p < c->space.P; ++p)
+    UT_CHECK(c, c->space.host_params[p].kind != UT_PERM, UT_EUNSUPPORTED, "propose_pso: permutation params");
+  if (m == 0) return 0;
+  return ut::launch_pso(c, a, gbest, round_, cand_base, m, out_values, out_vel, ld);
+}
+
+extern "C" int ut_pso_commit(ut_ctx* c, const double* values, const double* vel, int64_t ld, int64_t cand_base,
+                             int64_t m) {
+  if (!c) return UT_EINVAL;
+  UT_CHECK(c, c->pso_vel != nullptr && values && cand_base >= 0 && m >= 0 && cand_base + m <= c->npop && ld >= m,
+           UT_EINVAL, "pso_commit: bad arguments");
+  if (m == 0) return 0;
+  UT_HIP(c, hipMemcpy2DAsync(c->pop + cand_base, sizeof(double) * c->npop, values, sizeof(double) * ld,
+                             sizeof(double) * m, c->space.P, hipMemcpyDeviceToDevice, c->stream));
+  if (vel)
+    UT_HIP(c, hipMemcpy2DAsync(c->pso_vel + cand_base, sizeof(double) * c->npop, vel, sizeof(double) * ld,
+                               sizeof(double) * m, c->space.P, hipMemcpyDeviceToDevice, c->stream));
+  return 0;
+}
+
+extern "C" int ut_pso_update_best(ut_ctx* c, const double* values, int64_t ld, const int64_t* idx, int64_t n) {
+  if (!c) return UT_EINVAL;
+  UT_CHECK(c, c->pso_best != nullptr && values && idx && n >= 0, UT_EINVAL, "pso_update_best: bad arguments");
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(ut::k_pop_replace, dim3(ut::grid1(n, 64)), dim3(64), 0, c->stream, c->space.P, c->pso_best,
+                     c->npop, values, ld, idx, n);
+  UT_LAUNCH_CHECK(c);
+  return 0;
+}
+
+extern "C" int ut_propose_ga(ut_ctx* c, const ut_ga_params* a, const double* parent1, const double* parent2,
+                             uint32_t round_, int64_t cand_base, int64_t m, double* out_values, int64_t ld,
+                             uint8_t* out_invalid) {
+  if (!c) return UT_EINVAL;
+  UT_CHECK(c, c->has_space, UT_ENOSPACE, "space not defined");
+  UT_CHECK(c, a && out_values && m >= 0 && cand_base >= 0 && ld >= m, UT_EINVAL, "propose_ga: bad arguments");
+  UT_CHECK(c, a->max_retries >= 1 && a->max_retries <= 15, UT_EINVAL, "propose_ga: max_retries must be in [1, 15]");
+  UT_CHECK(c, a->must_mutate_count >= 0 && a->must_mutate_count <= c->space.P, UT_EINVAL,
+           "propose_ga: must_mutate_count out of range");
+  UT_CHECK(c, a->op >= 0 && a->op < 256, UT_EINVAL, "propose_ga: op must fit 8 bits");
+  for (int32_t p = 0; p < c->space.P; ++p)
+    UT_CHECK(c, c->space.host_params[p].kind != UT_PERM, UT_EUNSUPPORTED, "propose_ga: permutation params");
+  if (m == 0) return 0;
+  return ut::launch_ga(c, a, parent1, parent2, round_, cand_base, m, out_values, ld, out_invalid);
 }

@@ -80,6 +80,11 @@ struct ut_ctx {
   int64_t npop = 0;
   int64_t pop_cap = 0;
 
+  // PSO state
+  double* pso_vel = nullptr;    // [P][npop]
+  double* pso_best = nullptr;   // [P][npop]
+  int64_t pso_cap = 0;
+
   // history set
   uint32_t* hist_keys = nullptr;   // [cap][8]
   uint32_t* hist_state = nullptr;  // [cap] 0 empty / 1 full
@@ -171,6 +176,10 @@ void mark(ut_ctx* c, const char* name);
 int launch_population_init(ut_ctx* c, uint32_t round_);
 int launch_de(ut_ctx* c, const ut_de_params* p, uint32_t round_, int64_t cand_base, int64_t m, double* out,
               int64_t ld);
+int launch_pso(ut_ctx* c, const ut_pso_params* a, const double* gbest, uint32_t round_, int64_t cand_base,
+               int64_t m, double* out_x, double* out_v, int64_t ld);
+int launch_ga(ut_ctx* c, const ut_ga_params* a, const double* parent1, const double* parent2, uint32_t round_,
+              int64_t cand_base, int64_t m, double* out, int64_t ld, uint8_t* invalid);
 int launch_encode(ut_ctx* c, const double* values, int64_t ld, int64_t m, double* feat, int64_t ldf);
 int launch_hash(ut_ctx* c, const double* values, int64_t ld, int64_t m, uint32_t* out);
 int launch_hist_insert(ut_ctx* c, const uint32_t* dig, int64_t n);

@@ -121,6 +121,49 @@ class BatchEngine:
                                                  _ptr(out), out.stride(0)), "ut_propose_de")
         return out
 
+    def pso_reset(self):
+        L.check(self.ctx, self.lib.ut_pso_reset(self.ctx), "ut_pso_reset")
+
+    def _row(self, r):
+        if r is None:
+            return None
+        if isinstance(r, torch.Tensor):
+            return r.to(self.device, torch.float64).contiguous()
+        return torch.as_tensor(np.asarray(r, dtype=np.float64), device=self.device)
+
+    def propose_pso(self, gbest, m: int, round_: int = 0, cand_base: int = 0, omega: float = 0.5,
+                    phi_l: float = 0.5, phi_g: float = 0.5, sigma: float = 0.2, alias_pbest: bool = True,
+                    enum_mode: int = 0):
+        """HybridParticle.move for particles (cand_base + i) % npop (pso.py:70-77)."""
+        gb = self._row(gbest)
+        x = self._empty(self.spec.P, m)
+        v = self._empty(self.spec.P, m)
+        a = L.PsoParams(omega=omega, phi_l=phi_l, phi_g=phi_g, sigma=sigma, alias_pbest=1 if alias_pbest else 0,
+                        enum_mode=int(enum_mode))
+        L.check(self.ctx, self.lib.ut_propose_pso(self.ctx, C.byref(a), _ptr(gb), int(round_), int(cand_base), int(m),
+                                                  _ptr(x), _ptr(v), m), "ut_propose_pso")
+        return x, v
+
+    def pso_commit(self, values: torch.Tensor, vel: Optional[torch.Tensor], cand_base: int = 0):
+        L.check(self.ctx, self.lib.ut_pso_commit(self.ctx, _ptr(values), _ptr(vel), values.stride(0), int(cand_base),
+                                                 values.shape[1]), "ut_pso_commit")
+
+    def propose_ga(self, m: int, parent1=None, parent2=None, round_: int = 0, cand_base: int = 0,
+                   mutation_rate: float = 0.1, sigma: float = 0.1, crossover_rate: float = 0.0,
+                   crossover_strength: float = 0.0, must_mutate_count: int = 1, normal: bool = False,
+                   max_retries: int = 10, op: int = 4):
+        """EvolutionaryTechnique / GGA proposals (evolutionarytechniques.py:29-61,
+        globalGA.py:187-235); returns (values [P][m], invalid [m])."""
+        p1, p2 = self._row(parent1), self._row(parent2)
+        out = self._empty(self.spec.P, m)
+        inv = self._empty(m, dtype=torch.uint8)
+        a = L.GaParams(mutation_rate=mutation_rate, sigma=sigma, crossover_rate=crossover_rate,
+                       crossover_strength=crossover_strength, must_mutate_count=must_mutate_count,
+                       normal=1 if normal else 0, max_retries=max_retries, op=op)
+        L.check(self.ctx, self.lib.ut_propose_ga(self.ctx, C.byref(a), _ptr(p1), _ptr(p2), int(round_),
+                                                 int(cand_base), int(m), _ptr(out), m, _ptr(inv)), "ut_propose_ga")
+        return out, inv
+
     def encode(self, values: torch.Tensor, m: Optional[int] = None) -> torch.Tensor:
         m = values.shape[1] if m is None else m
         feat = self._empty(self.spec.n_features, m)
