@@ -33,6 +33,7 @@ sys.path.insert(0, ROOT)
 # MI355X peaks (MI355X_MICROARCH.md chip table; FP64 matrix = FP64 vector
 # spec 78.6 TF -- SURVEY.md §8(d))
 PEAK_FP64_TFLOPS = 78.6
+PEAK_FP32_TFLOPS = 157.3
 PEAK_HBM_GBS = 8000.0
 
 
@@ -105,6 +106,8 @@ def main():
     ap.add_argument("--k", type=int, default=256)
     ap.add_argument("--cpu-sample", type=int, default=8192)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--precision", type=int, default=64, choices=(64, 32),
+                    help="GP contractions on fp64 MFMA (1e-5 parity) or fp32 MFMA (1e-3 parity)")
     args = ap.parse_args()
 
     import torch
@@ -125,6 +128,7 @@ def main():
     manip = ConfigurationManipulator([FloatParameter(i, -1000.0, 1000.0) for i in range(d)])
     eng = BatchEngine(manip, device=local, seed=1)
     npop = m * world                       # replicated population, deterministic init on every rank
+    eng.gp_set_precision(args.precision)
     eng.population_init(npop)
     eng.history_reset(0)
     X, y = training_set(n, d, 101)
@@ -173,7 +177,8 @@ def main():
     var_ms = stages.get("var")
     flops_var = float(m) * n * (n + 1)       # algorithmic: lower-triangular n x n times k* per candidate
     achieved = flops_var / (var_ms * 1e-3) / 1e12 if var_ms else None
-    traffic = load_traffic("var")
+    peak = PEAK_FP64_TFLOPS if args.precision == 64 else PEAK_FP32_TFLOPS
+    traffic = load_traffic("var" if args.precision == 64 else "var32")
     result = {
         "metric": "candidate configs scored/sec (GP-EI + top-k)",
         "value": value,
@@ -185,14 +190,18 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f64",
+        "dtype": "f64" if args.precision == 64 else "f32 (K*, L^-1 K* MFMA; fit/EI f64)",
         "data": "synthetic (Rosenbrock-64 objective on uniform training points; DE population random-init)",
         "config": {"workload": "C2 R64: DE-Alt + hash_config + dedup + GP-EI n=1024 + top-256",
                    "candidates_per_gpu": m, "gp_n": n, "dims": d, "k": k, "parallelism": f"dp{world}"},
         "stage_ms": stages,
-        "roofline": {"bound": "mfma", "kernel": "k_gp_gemm<1> (var: L^-1 K*^T, fp64 MFMA 16x16x4)",
-                     "achieved": achieved, "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
-                     "frac": (achieved / PEAK_FP64_TFLOPS) if achieved else None, "traffic": traffic},
+        "roofline": {"bound": "mfma",
+                     "kernel": "k_gp_gemm2<%s,1> (var: L^-1 K*^T, %s)" % (
+                         ("double", "v_mfma_f64_16x16x4_f64") if args.precision == 64 else
+                         ("float", "v_mfma_f32_32x32x2_f32")),
+                     "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
+                     "frac": (achieved / peak) if achieved else None, "traffic": traffic,
+                     "flops_per_launch": flops_var},
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -194,6 +194,10 @@ int ut_gp_fit(ut_ctx* ctx, const double* X_host, const double* y_host, int32_t n
  * candidates excluded from selection (score forced to -inf). */
 int ut_gp_score(ut_ctx* ctx, const double* features, int64_t ld, int64_t m, const ut_acq* acq,
                 const uint8_t* dup, double* mu, double* var, double* score);
+/* arithmetic of the two scoring contractions (K* and L^-1 K*^T) for fits made
+ * after this call: 64 = fp64 MFMA (default; 1e-5 parity), 32 = fp32 MFMA
+ * (1e-3 parity).  The fit itself is always fp64. */
+int ut_gp_set_precision(ut_ctx* ctx, int32_t bits);
 /* f_best (min standardised y), y mean/std used for standardisation */
 int ut_gp_stats(ut_ctx* ctx, double* f_best, double* y_mean, double* y_std);
 

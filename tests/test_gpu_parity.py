@@ -219,8 +219,11 @@ def test_gp_small_golden(golden_dir):
     _close(ucb.cpu().numpy(), z["ucb"])
 
 
-@pytest.mark.parametrize("n,d,ell", [(1024, 64, 0.2), (200, 8, 0.5), (77, 3, 0.25)])
-def test_gp_vs_oracle(n, d, ell):
+@pytest.mark.parametrize("prec", [64, 32])
+@pytest.mark.parametrize("n,d,ell", [(1024, 64, 0.2), (200, 8, 0.5), (77, 3, 0.25), (300, 16, 1.5)])
+def test_gp_vs_oracle(n, d, ell, prec):
+    """fp64: 1e-5 relative; fp32 MFMA contractions: 1e-3 relative (north star),
+    absolute floor 1e-4 (variance near training points is a cancellation)."""
     rng = np.random.default_rng(n + d)
     X = rng.uniform(size=(n, d))
     y = np.sum((X - 0.4) ** 2, axis=1) + 0.01 * rng.standard_normal(n)
@@ -228,14 +231,22 @@ def test_gp_vs_oracle(n, d, ell):
     U[:10] = X[:10] + 1e-3
     space = [Param(f"u{k}", FLOAT, 0.0, 1.0) for k in range(d)]
     e = engine(space)
+    e.gp_set_precision(prec)
     e.gp_fit(X, y, lengthscale=ell, sigma_f2=1.0, sigma_n2=1e-6, jitter=1e-8)
     g = ogp.GP(X, y, lengthscale=ell, sigma_f2=1.0, sigma_n2=1e-6, jitter=1e-8)
     mu_o, var_o = g.posterior(U)
     ei_o = ogp.acquisition(mu_o, var_o, g.f_best)
     mu, var, ei = e.gp_score(dev(U.T))
-    _close(mu.cpu().numpy(), mu_o)
-    _close(var.cpu().numpy(), var_o, atol=1e-8)
-    _close(ei.cpu().numpy(), ei_o, atol=1e-8)
+    if prec == 64:
+        _close(mu.cpu().numpy(), mu_o)
+        _close(var.cpu().numpy(), var_o, atol=1e-8)
+        _close(ei.cpu().numpy(), ei_o, atol=1e-8)
+    else:
+        # fp32 var contraction: 1e-3 relative, absolute floor 1e-5 (var near
+        # training points is sf2 - |L^-1 k*|^2, a cancellation in fp32)
+        _close(mu.cpu().numpy(), mu_o)                     # K* and mu stay fp64
+        _close(var.cpu().numpy(), var_o, rtol=1e-3, atol=1e-5)
+        _close(ei.cpu().numpy(), ei_o, rtol=1e-3, atol=1e-5)
 
 
 # --------------------------------------------------------------------------- top-k

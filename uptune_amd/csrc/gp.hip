@@ -21,17 +21,14 @@
 //   GEMM1: A = Xs [n x d],    B = U^T (features, [d][m]) -> K*^T  [n][m] + mu partials
 //   GEMM2: A = L^-1 [n x n],  B = K*^T [n][m]  (lower-triangular A: K loop stops
 //          at the tile's diagonal)  -> |L^-1 k*|^2 partials
-// Both use v_mfma_f64_16x16x4_f64 (fp64 in / fp64 accumulate), a 64x128
-// output tile per 256-thread workgroup and an XCD-aware block order that
-// keeps the n/64 row tiles of one candidate column tile on one XCD (shared
-// L2 for the B stream).
+// Both run in gp_gemm.hip (fp64 MFMA by default, fp32 MFMA when
+// ut_gp_set_precision(ctx, 32)).
 #include "ut_internal.h"
 
 namespace ut {
 
-typedef double d4v __attribute__((ext_vector_type(4)));
-
-constexpr int NB = 64;  // Cholesky / inverse block
+constexpr int NB = 64;     // Cholesky / inverse block
+constexpr int NPAD = 128;  // training set padded to the GEMM row tile
 
 // ---------------------------------------------------------------------------
 // fit
@@ -315,110 +312,6 @@ __global__ void k_lower_tmv(const double* __restrict__ Li, int32_t npad, const d
 // ---------------------------------------------------------------------------
 // score
 // ---------------------------------------------------------------------------
-constexpr int BM = 64, BN = 128, BK = 16;
-constexpr int AS_LD = BM + 16, BS_LD = BN + 16;  // +16 doubles: conflict-free b64 fragment reads
-
-template <int MODE>
-__global__ __launch_bounds__(256) void k_gp_gemm(const double* __restrict__ A, int64_t lda,
-                                                 const double* __restrict__ B, int64_t ldb, int32_t K,
-                                                 int32_t RT, int32_t CT, int64_t m,
-                                                 // MODE 0
-                                                 const double* __restrict__ inv_ell,
-                                                 const double* __restrict__ xnorm,
-                                                 const double* __restrict__ cnorm,
-                                                 const double* __restrict__ alpha, double sf2, int32_t n,
-                                                 double* __restrict__ kst, int64_t ldk,
-                                                 // both: column partials [RT][ldp]
-                                                 double* __restrict__ part, int64_t ldp) {
-  __shared__ double As[BK * AS_LD];
-  __shared__ double Bs[BK * BS_LD];
-  // XCD-aware order: blocks b, b+8, ... share an XCD; walk all RT row tiles
-  // of a column tile consecutively inside one XCD group.
-  const int32_t b = blockIdx.x;
-  const int32_t xcd = b & 7, jj = b >> 3;
-  const int32_t rt = jj % RT;
-  const int32_t ct = (jj / RT) * 8 + xcd;
-  if (ct >= CT) return;
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  const int64_t col0 = (int64_t)ct * BN;
-  const int32_t row0 = rt * BM;
-  const int32_t kmax = (MODE == 1) ? ((row0 + BM) < K ? (row0 + BM) : K) : K;
-
-  d4v acc[4][2];
-#pragma unroll
-  for (int a = 0; a < 4; ++a)
-#pragma unroll
-    for (int c = 0; c < 2; ++c) acc[a][c] = (d4v){0.0, 0.0, 0.0, 0.0};
-
-  const int ar = t >> 2, akq = (t & 3) * 4;   // A loader: row, k quad
-  const int bk = t >> 4, bc = (t & 15) * 8;   // B loader: k row, 8 columns
-  for (int32_t k0 = 0; k0 < kmax; k0 += BK) {
-    // A tile (transposed into As[k][row])
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int32_t kk = k0 + akq + u;
-      As[(akq + u) * AS_LD + ar] = (kk < K) ? A[(int64_t)(row0 + ar) * lda + kk] : 0.0;
-    }
-    // B tile
-    {
-      const int32_t kk = k0 + bk;
-      const double sc = (MODE == 0 && kk < K) ? inv_ell[kk] : 1.0;
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int64_t col = col0 + bc + u;
-        double v = 0.0;
-        if (kk < K && col < m) v = B[(int64_t)kk * ldb + col];
-        Bs[bk * BS_LD + bc + u] = (MODE == 0) ? v * sc : v;
-      }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int ks = 0; ks < BK / 4; ++ks) {
-      const int kr = ks * 4 + (lane >> 4);
-      double af[4], bf[2];
-#pragma unroll
-      for (int a = 0; a < 4; ++a) af[a] = As[kr * AS_LD + a * 16 + (lane & 15)];
-#pragma unroll
-      for (int c = 0; c < 2; ++c) bf[c] = Bs[kr * BS_LD + w * 32 + c * 16 + (lane & 15)];
-#pragma unroll
-      for (int a = 0; a < 4; ++a)
-#pragma unroll
-        for (int c = 0; c < 2; ++c) acc[a][c] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[a], bf[c], acc[a][c], 0, 0, 0);
-    }
-    __syncthreads();
-  }
-
-  // epilogue: C/D map of v_mfma_f64_16x16x4: col = lane & 15, row = (lane >> 4) + 4 * r
-#pragma unroll
-  for (int c = 0; c < 2; ++c) {
-    const int64_t col = col0 + w * 32 + c * 16 + (lane & 15);
-    double colsum = 0.0;
-#pragma unroll
-    for (int a = 0; a < 4; ++a) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int32_t row = row0 + a * 16 + (lane >> 4) + 4 * r;
-        const double x = acc[a][c][r];
-        if (MODE == 0) {
-          double ks = 0.0;
-          if (row < n && col < m) {
-            double d2 = xnorm[row] + cnorm[col] - 2.0 * x;
-            d2 = d2 > 0.0 ? d2 : 0.0;
-            ks = sf2 * exp(-0.5 * d2);
-          }
-          if (col < ldk) kst[(int64_t)row * ldk + col] = ks;
-          colsum += alpha[row] * ks;
-        } else {
-          colsum += x * x;
-        }
-      }
-    }
-    colsum += __shfl_xor(colsum, 16);
-    colsum += __shfl_xor(colsum, 32);
-    if ((lane >> 4) == 0 && col < m) part[(int64_t)rt * ldp + col] = colsum;
-  }
-}
-
 // scaled candidate norms |u / ell|^2
 __global__ void k_gp_cnorm(const double* __restrict__ feat, int64_t ld, int64_t m, int32_t d,
                            const double* __restrict__ inv_ell, double* __restrict__ cn) {
@@ -468,6 +361,11 @@ __global__ void k_gp_finalize(int64_t m, int32_t RT1, int32_t RT2, const double*
 // ---------------------------------------------------------------------------
 static int gp_alloc(ut_ctx* c, int32_t npad, int32_t d) {
   if (c->gp_cap_n >= npad && c->gp_d == d && c->gp_Xs) return 0;
+  if (c->gp_Xs_f) {
+    UT_HIP(c, hipStreamSynchronize(c->stream));
+    hipFree(c->gp_Xs_f); hipFree(c->gp_Linv_f);
+    c->gp_Xs_f = nullptr; c->gp_Linv_f = nullptr;
+  }
   if (c->gp_Xs) {
     UT_HIP(c, hipStreamSynchronize(c->stream));
     hipFree(c->gp_Xs); hipFree(c->gp_xnorm); hipFree(c->gp_K); hipFree(c->gp_Linv);
@@ -484,6 +382,8 @@ static int gp_alloc(ut_ctx* c, int32_t npad, int32_t d) {
   UT_HIP(c, hipMalloc((void**)&c->gp_inv_ell, sizeof(double) * d));
   UT_HIP(c, hipMalloc((void**)&c->gp_stats, sizeof(double) * 4));
   UT_HIP(c, hipMalloc((void**)&c->gp_flag, sizeof(int32_t)));
+  UT_HIP(c, hipMalloc((void**)&c->gp_Xs_f, sizeof(float) * npad * d));
+  UT_HIP(c, hipMalloc((void**)&c->gp_Linv_f, sizeof(float) * npad * npad));
   c->gp_cap_n = npad;
   c->gp_d = d;
   return 0;
@@ -491,7 +391,7 @@ static int gp_alloc(ut_ctx* c, int32_t npad, int32_t d) {
 
 int gp_fit_impl(ut_ctx* c, const double* X, const double* y, int32_t n, int32_t d, const ut_gp_hyper* h) {
   UT_CHECK(c, n >= 1 && d >= 1 && X && y && h && h->lengthscale_host, UT_EINVAL, "gp_fit: bad arguments");
-  const int32_t npad = ((n + NB - 1) / NB) * NB;
+  const int32_t npad = ((n + NPAD - 1) / NPAD) * NPAD;
   int rc = gp_alloc(c, npad, d);
   if (rc) return rc;
   c->gp_n = n;
@@ -526,6 +426,11 @@ int gp_fit_impl(ut_ctx* c, const double* X, const double* y, int32_t n, int32_t 
   hipLaunchKernelGGL(k_lower_tmv, dim3(grid1(npad, 256)), dim3(256), 0, c->stream, c->gp_Linv, npad, c->gp_tmp,
                      c->gp_alpha);
   UT_LAUNCH_CHECK(c);
+  if (c->gp_prec == 32) {
+    if ((rc = launch_to_f32(c, c->gp_Xs, c->gp_Xs_f, (int64_t)npad * d))) return rc;
+    if ((rc = launch_to_f32(c, c->gp_Linv, c->gp_Linv_f, (int64_t)npad * npad))) return rc;
+  }
+  c->gp_fit_prec = c->gp_prec;
   int32_t flag = 0;
   UT_HIP(c, hipMemcpyAsync(&flag, c->gp_flag, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
   UT_HIP(c, hipStreamSynchronize(c->stream));
@@ -540,11 +445,11 @@ int gp_score_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, const ut
   UT_CHECK(c, acq != nullptr, UT_EINVAL, "gp_score: acq is NULL");
   if (m <= 0) return 0;
   const int32_t n = c->gp_n, d = c->gp_d;
-  const int32_t npad = ((n + NB - 1) / NB) * NB;
-  const int32_t RT = npad / BM;
-  const int32_t CT = (int32_t)((m + BN - 1) / BN);
-  const int32_t CT8 = ((CT + 7) / 8) * 8;
-  const int64_t ldk = (int64_t)CT * BN;
+  const int32_t npad = ((n + NPAD - 1) / NPAD) * NPAD;
+  const int32_t RT = npad / NPAD;
+  const int32_t CT = (int32_t)((m + NPAD - 1) / NPAD);
+  const int64_t ldk = (int64_t)CT * NPAD;
+  const bool fp32 = c->gp_fit_prec == 32;
   int rc;
   if ((rc = ensure(c, c->kst, (size_t)npad * ldk))) return rc;
   if ((rc = ensure(c, c->mu_part, (size_t)RT * ldk))) return rc;
@@ -553,15 +458,13 @@ int gp_score_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, const ut
   hipLaunchKernelGGL(k_gp_cnorm, dim3(grid1(m, 256)), dim3(256), 0, c->stream, feat, ld, m, d, c->gp_inv_ell,
                      c->cnorm.p);
   mark(c, "cnorm");
-  hipLaunchKernelGGL(k_gp_gemm<0>, dim3(RT * CT8), dim3(256), 0, c->stream, c->gp_Xs, (int64_t)d, feat, ld, d, RT,
-                     CT, m, c->gp_inv_ell, c->gp_xnorm, c->cnorm.p, c->gp_alpha, c->gp_sf2, n, c->kst.p, ldk,
-                     c->mu_part.p, ldk);
-  UT_LAUNCH_CHECK(c);
+  if ((rc = launch_gemm_kstar(c, fp32, (const void*)c->gp_Xs, d, feat, ld, d, RT,
+                              CT, m, c->kst.p, ldk, c->mu_part.p)))
+    return rc;
   mark(c, "kstar");
-  hipLaunchKernelGGL(k_gp_gemm<1>, dim3(RT * CT8), dim3(256), 0, c->stream, c->gp_Linv, (int64_t)npad, c->kst.p,
-                     ldk, npad, RT, CT, m, nullptr, nullptr, nullptr, nullptr, 0.0, n, nullptr, (int64_t)0,
-                     c->var_part.p, ldk);
-  UT_LAUNCH_CHECK(c);
+  if ((rc = launch_gemm_var(c, fp32, fp32 ? (const void*)c->gp_Linv_f : (const void*)c->gp_Linv, npad, c->kst.p,
+                            ldk, npad, RT, CT, m, c->var_part.p)))
+    return rc;
   mark(c, "var");
   hipLaunchKernelGGL(k_gp_finalize, dim3(grid1(m, 256)), dim3(256), 0, c->stream, m, RT, RT, c->mu_part.p,
                      c->var_part.p, ldk, c->gp_sf2, c->gp_stats, acq->kind, acq->xi, acq->kappa, dup, mu, var,

@@ -109,6 +109,10 @@ struct ut_ctx {
   double* gp_stats = nullptr;  // [4]: f_best, mean, std, flag
   int32_t* gp_flag = nullptr;
   double gp_sf2 = 1.0;
+  int32_t gp_prec = 64;        // precision requested for the next fit
+  int32_t gp_fit_prec = 64;    // precision of the fitted factors used by scoring
+  float* gp_Xs_f = nullptr;    // fp32 copies for the fp32 MFMA path
+  float* gp_Linv_f = nullptr;
   int64_t gp_cap_n = 0;
 
   // scratch for GP scoring / round pipeline
@@ -190,6 +194,11 @@ int gp_score_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, const ut
                   double* mu, double* var, double* score);
 int topk_impl(ut_ctx* c, const double* score, const uint8_t* dup, int64_t m, int64_t cand_base, int32_t k,
               int64_t* out_idx, double* out_score);
+int launch_gemm_kstar(ut_ctx* c, bool fp32, const void* A, int64_t lda, const double* feat, int64_t ldf, int32_t d,
+                      int32_t RT, int32_t CT, int64_t m, void* kst, int64_t ldk, double* part);
+int launch_gemm_var(ut_ctx* c, bool fp32, const void* Linv, int64_t lda, const void* kst, int64_t ldk, int32_t npad,
+                    int32_t RT, int32_t CT, int64_t m, double* part);
+int launch_to_f32(ut_ctx* c, const double* src, float* dst, int64_t n);
 int launch_gather_rows(ut_ctx* c, const double* values, int64_t ld, const int64_t* idx, int64_t cand_base,
                        int32_t k, double* out, int64_t ldo, const uint32_t* dig, uint32_t* out_dig);
 

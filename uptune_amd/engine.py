@@ -203,6 +203,9 @@ class BatchEngine:
         return out
 
     # -- GP ----------------------------------------------------------------
+    def gp_set_precision(self, bits: int):
+        L.check(self.ctx, self.lib.ut_gp_set_precision(self.ctx, int(bits)), "ut_gp_set_precision")
+
     def gp_fit(self, X: np.ndarray, y: np.ndarray, lengthscale, sigma_f2: float = 1.0, sigma_n2: float = 1e-6,
                jitter: float = 0.0):
         X = np.ascontiguousarray(X, dtype=np.float64)
