@@ -19,17 +19,20 @@
 // shortest round-trip repr (ut_core.h) and hashed (one SHA-256 block);
 // large-range INT values use repr(int).
 //
-// One lane = one candidate.  Per-lane byte strings and hex words live in LDS
-// in [word][lane] layout (bank-conflict-free, no cross-lane traffic, so no
-// barriers).  Bound: integer VALU (~1.4k ops per SHA-256 compression).
+// One lane = one candidate.  The repr byte string is assembled in LDS in
+// [word][lane] layout (bank-conflict-free, no cross-lane traffic, so no
+// barriers); the two live 64-char hex "holes" stay in VGPRs and are indexed
+// with the wave-uniform word-table entry (s_set_gpr_idx / v_movrels, no
+// scratch).  Bound: integer VALU (~1.4k ops per SHA-256 compression, with
+// Sigma/Ch/Maj as single v_bitop3_b32).
 #include "ut_internal.h"
 
 namespace ut {
 
 constexpr int HASH_NT = 128;
 constexpr int SCR_WORDS = 7;                       // inner message bytes 0..27
-constexpr int HEX_WORDS = 18;                      // [0]=0, [1..16]=hex, [17]=0
-constexpr int LDS_WORDS = SCR_WORDS + 2 * HEX_WORDS;
+
+typedef uint32_t hexv __attribute__((ext_vector_type(16)));
 
 struct LdsEmit {
   uint8_t* base;  // &lds[0] as bytes
@@ -69,23 +72,24 @@ __device__ __forceinline__ void inner_digest(const DevParam& pr, double v, const
   sha256_compress(D, W);
 }
 
+__device__ __forceinline__ uint32_t hex_at(const hexv& X, int32_t q) {
+  // wave-uniform q in [-1, 16]; words outside the hole read as zero bytes
+  const uint32_t v = X[q & 15];
+  return (q >= 0 && q < 16) ? v : 0u;
+}
+
 __global__ __launch_bounds__(HASH_NT) void k_hash(const DevParam* __restrict__ params,
                                                   const int32_t* __restrict__ order,
                                                   const HashWord* __restrict__ words,
                                                   const int16_t* __restrict__ block_last, int32_t nblocks,
                                                   const uint32_t* __restrict__ lut, const double* __restrict__ values,
                                                   int64_t ld, int64_t m, uint32_t* __restrict__ out) {
-  __shared__ uint32_t lds[LDS_WORDS * HASH_NT];
+  __shared__ uint32_t lds[SCR_WORDS * HASH_NT];
   const int lane = threadIdx.x;
   const int64_t i0 = (int64_t)blockIdx.x * HASH_NT + lane;
   const bool valid = i0 < m;
   const int64_t i = valid ? i0 : (m - 1);
-  uint32_t* hexs = lds + SCR_WORDS * HASH_NT;
-#pragma unroll
-  for (int s = 0; s < 2; ++s) {
-    hexs[(s * HEX_WORDS + 0) * HASH_NT + lane] = 0u;
-    hexs[(s * HEX_WORDS + 17) * HASH_NT + lane] = 0u;
-  }
+  hexv hx0 = {}, hx1 = {};
   uint32_t H[8];
   sha256_init(H);
   int32_t next = 0;
@@ -97,11 +101,14 @@ __global__ __launch_bounds__(HASH_NT) void k_hash(const DevParam* __restrict__ p
       const double v = values[(int64_t)p * ld + i];
       uint32_t D[8];
       inner_digest(pr, v, lut, lds, lane, D);
-      uint32_t HX[16];
-      digest_hex(D, HX);
-      uint32_t* slot = hexs + (next & 1) * HEX_WORDS * HASH_NT;
+      hexv h;
 #pragma unroll
-      for (int w = 0; w < 16; ++w) slot[(w + 1) * HASH_NT + lane] = HX[w];
+      for (int k = 0; k < 8; ++k) {
+        h[2 * k] = hex4(D[k] >> 16);
+        h[2 * k + 1] = hex4(D[k] & 0xFFFFu);
+      }
+      if (next & 1) hx1 = h;
+      else hx0 = h;
       ++next;
     }
     uint32_t W[16];
@@ -111,8 +118,16 @@ __global__ __launch_bounds__(HASH_NT) void k_hash(const DevParam* __restrict__ p
       const HashWord e = hw[w];
       uint32_t x = e.tmpl;
       if (e.hole >= 0) {
-        const uint32_t* slot = hexs + (e.hole & 1) * HEX_WORDS * HASH_NT;
-        const uint64_t cat = ((uint64_t)slot[e.q1 * HASH_NT + lane] << 32) | slot[(e.q1 + 1) * HASH_NT + lane];
+        const int32_t q = (int32_t)e.q1 - 1;
+        uint32_t lo, hi;
+        if (e.hole & 1) {
+          lo = hex_at(hx1, q);
+          hi = hex_at(hx1, q + 1);
+        } else {
+          lo = hex_at(hx0, q);
+          hi = hex_at(hx0, q + 1);
+        }
+        const uint64_t cat = ((uint64_t)lo << 32) | hi;
         x |= (uint32_t)((cat << (8 * e.shift)) >> 32);
       }
       W[w] = x;

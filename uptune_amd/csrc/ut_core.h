@@ -128,6 +128,30 @@ UT_HD uint32_t rotr32(uint32_t x, int n) {
 #endif
 }
 
+// 3-input bitwise ops: one v_bitop3_b32 on gfx950 (truth table over
+// a=0xF0, b=0xCC, c=0xAA)
+UT_HD uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+#else
+  return a ^ b ^ c;
+#endif
+}
+UT_HD uint32_t sha_ch(uint32_t e, uint32_t f, uint32_t g) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_bitop3_b32(e, f, g, 0xCA);
+#else
+  return (e & f) ^ (~e & g);
+#endif
+}
+UT_HD uint32_t sha_maj(uint32_t a, uint32_t b, uint32_t c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0xE8);
+#else
+  return (a & b) ^ (a & c) ^ (b & c);
+#endif
+}
+
 UT_HD void sha256_init(uint32_t H[8]) {
   H[0] = 0x6a09e667u; H[1] = 0xbb67ae85u; H[2] = 0x3c6ef372u; H[3] = 0xa54ff53au;
   H[4] = 0x510e527fu; H[5] = 0x9b05688cu; H[6] = 0x1f83d9abu; H[7] = 0x5be0cd19u;
@@ -144,18 +168,16 @@ UT_HD void sha256_compress(uint32_t H[8], uint32_t W[16]) {
       w = W[t];
     } else {
       const uint32_t w15 = W[(t - 15) & 15], w2 = W[(t - 2) & 15];
-      const uint32_t s0 = rotr32(w15, 7) ^ rotr32(w15, 18) ^ (w15 >> 3);
-      const uint32_t s1 = rotr32(w2, 17) ^ rotr32(w2, 19) ^ (w2 >> 10);
+      const uint32_t s0 = xor3(rotr32(w15, 7), rotr32(w15, 18), w15 >> 3);
+      const uint32_t s1 = xor3(rotr32(w2, 17), rotr32(w2, 19), w2 >> 10);
       w = W[t & 15] + s0 + W[(t - 7) & 15] + s1;
       W[t & 15] = w;
     }
-    const uint32_t S1 = rotr32(e, 6) ^ rotr32(e, 11) ^ rotr32(e, 25);
-    const uint32_t ch = (e & f) ^ (~e & g);
-    const uint32_t t1 = h + S1 + ch + SHA256_K[t] + w;
-    const uint32_t S0 = rotr32(a, 2) ^ rotr32(a, 13) ^ rotr32(a, 22);
-    const uint32_t mj = (a & b) ^ (a & c) ^ (b & c);
-    const uint32_t t2 = S0 + mj;
-    h = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
+    const uint32_t S1 = xor3(rotr32(e, 6), rotr32(e, 11), rotr32(e, 25));
+    const uint32_t t1 = (h + S1 + sha_ch(e, f, g)) + (SHA256_K[t] + w);
+    const uint32_t S0 = xor3(rotr32(a, 2), rotr32(a, 13), rotr32(a, 22));
+    const uint32_t mj = sha_maj(a, b, c);
+    h = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + S0 + mj;
   }
   H[0] += a; H[1] += b; H[2] += c; H[3] += d; H[4] += e; H[5] += f; H[6] += g; H[7] += h;
 }
