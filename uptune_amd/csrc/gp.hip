@@ -47,25 +47,6 @@ __global__ void k_gp_prep_train(const double* __restrict__ X, int32_t n, int32_t
   xnorm[j] = s;
 }
 
-__global__ void k_gp_kmat(const double* __restrict__ Xs, const double* __restrict__ xnorm, int32_t n, int32_t npad,
-                          int32_t d, double sf2, double diag, double* __restrict__ K) {
-  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= (int64_t)npad * npad) return;
-  const int32_t i = (int32_t)(e / npad), j = (int32_t)(e % npad);
-  double v;
-  if (i >= n || j >= n) {
-    v = (i == j) ? 1.0 : 0.0;  // identity padding keeps the factorisation exact
-  } else {
-    double dot = 0.0;
-    for (int32_t k = 0; k < d; ++k) dot += Xs[(int64_t)i * d + k] * Xs[(int64_t)j * d + k];
-    double d2 = xnorm[i] + xnorm[j] - 2.0 * dot;
-    d2 = d2 > 0.0 ? d2 : 0.0;
-    v = sf2 * exp(-0.5 * d2);
-    if (i == j) v += diag;
-  }
-  K[e] = v;
-}
-
 // mean / std (ddof=0) / standardise / f_best = min(ys); one workgroup
 __global__ __launch_bounds__(256) void k_gp_ystats(const double* __restrict__ y, int32_t n, int32_t npad,
                                                    double* __restrict__ ys, double* __restrict__ stats) {
@@ -114,177 +95,281 @@ __global__ __launch_bounds__(256) void k_gp_ystats(const double* __restrict__ y,
   }
 }
 
-// unblocked Cholesky of a NB x NB block held in LDS (row-major, stride NB+1)
+// unblocked Cholesky of a NB x NB block held in LDS (row-major, stride NB+1).
+// 256 threads as 16 x 16, each owning a 4 x 4 patch.  Per column every
+// thread computes the pivot itself (no serial step), reads the column,
+// barrier, applies the rank-1 update and writes the scaled column, barrier.
 __device__ void lds_chol(double* A, int32_t* flag) {
   const int t = threadIdx.x;
+  const int r0 = (t >> 4) * 4, s0 = (t & 15) * 4;
   for (int c = 0; c < NB; ++c) {
-    if (t == 0) {
-      const double dv = A[c * (NB + 1) + c];
-      if (!(dv > 0.0)) atomicOr(flag, 1);
-      A[c * (NB + 1) + c] = sqrt(dv > 0.0 ? dv : 1e-300);
+    const double dv = A[c * (NB + 1) + c];
+    const double piv = sqrt(dv > 0.0 ? dv : 1e-300);
+    const double inv = 1.0 / piv;
+    double lr[4], ls[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      lr[i] = A[(r0 + i) * (NB + 1) + c] * inv;
+      ls[i] = A[(s0 + i) * (NB + 1) + c] * inv;
     }
-    __syncthreads();
-    const double piv = A[c * (NB + 1) + c];
-    for (int r = c + 1 + t; r < NB; r += blockDim.x) A[r * (NB + 1) + c] /= piv;
-    __syncthreads();
-    const int rem = NB - c - 1;
-    for (int e = t; e < rem * rem; e += blockDim.x) {
-      const int r = c + 1 + e / rem, s = c + 1 + e % rem;
-      if (s <= r) A[r * (NB + 1) + s] -= A[r * (NB + 1) + c] * A[s * (NB + 1) + c];
+    __syncthreads();  // every read of column c (and of the pivot) done before writes
+    if (t == 0) {
+      if (!(dv > 0.0)) atomicOr(flag, 1);
+      A[c * (NB + 1) + c] = piv;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = r0 + i;
+      if (r > c) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int s2 = s0 + j;
+          if (s2 > c && s2 <= r) A[r * (NB + 1) + s2] -= lr[i] * ls[j];
+        }
+        if (s0 == 0) A[r * (NB + 1) + c] = lr[i];  // scaled column, one writer per row
+      }
     }
     __syncthreads();
   }
 }
 
-// Panel kb: every workgroup factors the diagonal block; workgroup 0 writes
-// it back, workgroup w >= 1 solves row block kb + w:  X L_kk^T = A.
-__global__ __launch_bounds__(256) void k_chol_panel(double* __restrict__ K, int32_t npad, int32_t kb,
-                                                    int32_t* flag) {
+// X = inv(S) for the lower-triangular NB x NB block S (stride NB+1), row by
+// row: X[r][:] = (e_r - S[r][0:r] X[0:r][:]) / S[r][r]; thread (q, c) sums
+// the terms s = q (mod 4) of column c with a fixed, fully unrolled trip count.
+__device__ void lds_trinv(const double* S, double* X, double* red /* [4][NB] */) {
+  const int t = threadIdx.x, c = t & 63, q = t >> 6;
+  for (int e = t; e < NB * (NB + 1); e += blockDim.x) X[e] = 0.0;  // rows not yet solved multiply as 0
+  __syncthreads();
+  for (int r = 0; r < NB; ++r) {
+    double p = 0.0;
+#pragma unroll
+    for (int u = 0; u < NB / 4; ++u) {
+      const int s2 = q + 4 * u;
+      const double a = (s2 < r) ? S[r * (NB + 1) + s2] : 0.0;
+      p += a * X[s2 * (NB + 1) + c];
+    }
+    red[q * NB + c] = p;
+    __syncthreads();
+    if (q == 0) {
+      const double sum = (red[c] + red[NB + c]) + (red[2 * NB + c] + red[3 * NB + c]);
+      X[r * (NB + 1) + c] = (c > r) ? 0.0 : (((r == c) ? 1.0 : 0.0) - sum) / S[r * (NB + 1) + r];
+    }
+    __syncthreads();
+  }
+}
+
+// 64 x 64 tile  acc = A[64 x K] * B[64 x K]^T  (both row-major in global,
+// leading dims lda / ldb) on v_mfma_f64_16x16x4; each wave 32 x 32.
+typedef double fd4 __attribute__((ext_vector_type(4)));
+__device__ void tile64_nt(const double* __restrict__ A, int64_t lda, const double* __restrict__ B, int64_t ldb,
+                          int32_t K, double* As, double* Bs, fd4 (&acc)[2][2]) {
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int wr = w >> 1, wc = w & 1;
+  for (int32_t k0 = 0; k0 < K; k0 += 16) {
+    for (int e = t; e < 64 * 16; e += 256) {
+      const int r = e >> 4, kk = e & 15;
+      const bool in = (k0 + kk) < K;
+      As[kk * 80 + r] = in ? A[(int64_t)r * lda + k0 + kk] : 0.0;
+      Bs[kk * 80 + r] = in ? B[(int64_t)r * ldb + k0 + kk] : 0.0;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const int kr = ks * 4 + (lane >> 4);
+      double af[2], bf[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) af[i] = As[kr * 80 + wr * 32 + i * 16 + (lane & 15)];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) bf[j] = Bs[kr * 80 + wc * 32 + j * 16 + (lane & 15)];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[i], bf[j], acc[i][j], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+}
+
+// acc element (i, j, r) -> tile row / column
+__device__ __forceinline__ int tile_row(int i, int r) { return ((threadIdx.x >> 6) >> 1) * 32 + i * 16 + ((threadIdx.x & 63) >> 4) + 4 * r; }
+__device__ __forceinline__ int tile_col(int j) { return ((threadIdx.x >> 6) & 1) * 32 + j * 16 + (threadIdx.x & 15); }
+
+// Panel kb, step 1 (one workgroup): L_kk = chol(A_kk) written to K, and
+// inv(L_kk) written as the diagonal block of L^-1.
+__global__ __launch_bounds__(256) void k_chol_diag(double* __restrict__ K, double* __restrict__ Li, int32_t npad,
+                                                   int32_t kb, int32_t* flag) {
   __shared__ double Lkk[NB * (NB + 1)];
-  __shared__ double Ab[NB * (NB + 1)];
+  __shared__ double Xi[NB * (NB + 1)];
+  __shared__ double red[4 * NB];
   const int t = threadIdx.x;
   const int64_t base = (int64_t)kb * NB;
   for (int e = t; e < NB * NB; e += blockDim.x) {
-    const int r = e / NB, s = e % NB;
-    Lkk[r * (NB + 1) + s] = K[(base + r) * npad + base + s];
+    const int r = e >> 6, s2 = e & 63;
+    Lkk[r * (NB + 1) + s2] = K[(base + r) * npad + base + s2];
   }
   __syncthreads();
   lds_chol(Lkk, flag);
-  if (blockIdx.x == 0) {
-    for (int e = t; e < NB * NB; e += blockDim.x) {
-      const int r = e / NB, s = e % NB;
-      K[(base + r) * npad + base + s] = (s <= r) ? Lkk[r * (NB + 1) + s] : 0.0;
-    }
-    return;
-  }
-  const int64_t rb = (int64_t)(kb + blockIdx.x) * NB;
+  lds_trinv(Lkk, Xi, red);
   for (int e = t; e < NB * NB; e += blockDim.x) {
-    const int r = e / NB, s = e % NB;
-    Ab[r * (NB + 1) + s] = K[(rb + r) * npad + base + s];
+    const int r = e >> 6, s2 = e & 63;
+    K[(base + r) * npad + base + s2] = (s2 <= r) ? Lkk[r * (NB + 1) + s2] : 0.0;
+    Li[(base + r) * npad + base + s2] = Xi[r * (NB + 1) + s2];
   }
-  __syncthreads();
-  if (t < NB) {
-    double* row = Ab + t * (NB + 1);
-    for (int c = 0; c < NB; ++c) {
-      double v = row[c];
-      for (int s = 0; s < c; ++s) v -= row[s] * Lkk[c * (NB + 1) + s];
-      row[c] = v / Lkk[c * (NB + 1) + c];
-    }
-  }
-  __syncthreads();
-  for (int e = t; e < NB * NB; e += blockDim.x) {
-    const int r = e / NB, s = e % NB;
-    K[(rb + r) * npad + base + s] = Ab[r * (NB + 1) + s];
-  }
+}
+
+// Panel kb, step 2: row block i > kb:  L_ik = A_ik * inv(L_kk)^T  (NT product)
+__global__ __launch_bounds__(256) void k_chol_rows(double* __restrict__ K, const double* __restrict__ Li,
+                                                   int32_t npad, int32_t kb) {
+  __shared__ double As[16 * 80];
+  __shared__ double Bs[16 * 80];
+  const int64_t base = (int64_t)kb * NB, rb = (int64_t)(kb + 1 + blockIdx.x) * NB;
+  fd4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = (fd4){0.0, 0.0, 0.0, 0.0};
+  tile64_nt(K + rb * npad + base, npad, Li + base * npad + base, npad, NB, As, Bs, acc);
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) K[(rb + tile_row(i, r)) * npad + base + tile_col(j)] = acc[i][j][r];
 }
 
 // Trailing update A_ij -= L_i,kb L_j,kb^T for kb < j <= i < nb.
 __global__ __launch_bounds__(256) void k_chol_update(double* __restrict__ K, int32_t npad, int32_t kb) {
-  __shared__ double Li[NB * (NB + 1)];
-  __shared__ double Lj[NB * (NB + 1)];
-  // linear tile id -> (i, j), j <= i, both in (kb, nb)
+  __shared__ double As[16 * 80];
+  __shared__ double Bs[16 * 80];
   int32_t tid = blockIdx.x;
   int32_t i = 0;
   while ((i + 1) * (i + 2) / 2 <= tid) ++i;
   const int32_t j = tid - i * (i + 1) / 2;
   const int64_t ib = (int64_t)(kb + 1 + i) * NB, jb = (int64_t)(kb + 1 + j) * NB, cb = (int64_t)kb * NB;
-  const int t = threadIdx.x;
-  for (int e = t; e < NB * NB; e += blockDim.x) {
-    const int r = e / NB, s = e % NB;
-    Li[r * (NB + 1) + s] = K[(ib + r) * npad + cb + s];
-    Lj[r * (NB + 1) + s] = K[(jb + r) * npad + cb + s];
-  }
-  __syncthreads();
-  for (int e = t; e < NB * NB; e += blockDim.x) {
-    const int r = e / NB, s = e % NB;
-    double acc = 0.0;
-    for (int q = 0; q < NB; ++q) acc += Li[r * (NB + 1) + q] * Lj[s * (NB + 1) + q];
-    K[(ib + r) * npad + jb + s] -= acc;
-  }
+  fd4 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) acc[a][b] = (fd4){0.0, 0.0, 0.0, 0.0};
+  tile64_nt(K + ib * npad + cb, npad, K + jb * npad + cb, npad, NB, As, Bs, acc);
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) K[(ib + tile_row(a, r)) * npad + jb + tile_col(b)] -= acc[a][b][r];
 }
 
-// invert the lower-triangular NB x NB block in S (stride NB+1) into X
-__device__ void lds_trinv(const double* S, double* X) {
-  const int t = threadIdx.x;
-  if (t < NB) {
-    const int c = t;
-    for (int r = 0; r < NB; ++r) {
-      double v;
-      if (r < c) {
-        v = 0.0;
-      } else {
-        v = (r == c) ? 1.0 : 0.0;
-        for (int s = c; s < r; ++s) v -= S[r * (NB + 1) + s] * X[s * (NB + 1) + c];
-        v /= S[r * (NB + 1) + r];
+// K = sf2 exp(-0.5 |xs_i - xs_j|^2) + diag I, 64 x 64 tiles on fp64 MFMA;
+// padded rows/columns (>= n) form an identity block
+__global__ __launch_bounds__(256) void k_gp_kmat(const double* __restrict__ Xs, const double* __restrict__ xnorm,
+                                                 int32_t n, int32_t npad, int32_t d, double sf2, double diag,
+                                                 double* __restrict__ K) {
+  __shared__ double As[16 * 80];
+  __shared__ double Bs[16 * 80];
+  const int64_t ib = (int64_t)blockIdx.y * 64, jb = (int64_t)blockIdx.x * 64;
+  fd4 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) acc[a][b] = (fd4){0.0, 0.0, 0.0, 0.0};
+  tile64_nt(Xs + ib * d, d, Xs + jb * d, d, d, As, Bs, acc);
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t i = ib + tile_row(a, r), j = jb + tile_col(b);
+        double v;
+        if (i >= n || j >= n) {
+          v = (i == j) ? 1.0 : 0.0;
+        } else {
+          double d2 = xnorm[i] + xnorm[j] - 2.0 * acc[a][b][r];
+          d2 = d2 > 0.0 ? d2 : 0.0;
+          v = sf2 * exp(-0.5 * d2);
+          if (i == j) v += diag;
+        }
+        K[i * npad + j] = v;
       }
-      X[r * (NB + 1) + c] = v;
-    }
-  }
-  __syncthreads();
 }
 
-// Block row I of L^-1:  Linv_IJ = -inv(L_II) * sum_{K=J}^{I-1} L_IK Linv_KJ
-__global__ __launch_bounds__(256) void k_trinv_row(const double* __restrict__ L, double* __restrict__ Li,
-                                                   int32_t npad, int32_t I) {
-  __shared__ double S[NB * (NB + 1)];
-  __shared__ double X[NB * (NB + 1)];
-  __shared__ double T[NB * (NB + 1)];
-  const int t = threadIdx.x;
-  const int32_t J = blockIdx.x;
-  const int64_t Ib = (int64_t)I * NB, Jb = (int64_t)J * NB;
-  for (int e = t; e < NB * NB; e += blockDim.x) {
-    const int r = e / NB, s = e % NB;
-    S[r * (NB + 1) + s] = L[(Ib + r) * npad + Ib + s];
+// Batched fp64 GEMM for the recursive triangular inverse.  Pair z at level
+// size s (offset o = z * 2s):
+//   phase 0:  T_z = B * Ai     B = L[o+s:o+2s, o:o+s],  Ai = Li[o:o+s, o:o+s]  (lower)
+//   phase 1:  Li[o+s:o+2s, o:o+s] = -Ci * T_z            Ci = Li[o+s:o+2s, o+s:o+2s]  (lower)
+// 64 x 64 output tile per 256-thread workgroup, v_mfma_f64_16x16x4 (each
+// wave 32 x 32 = 2 x 2 MFMA tiles), K step 16; the triangular operand limits
+// the K range of each tile.
+__global__ __launch_bounds__(256) void k_trinv_level(const double* __restrict__ L, double* __restrict__ Li,
+                                                     double* __restrict__ T, int32_t npad, int32_t s, int32_t phase) {
+  __shared__ double As[16 * 80];
+  __shared__ double Bs[16 * 80];
+  const int32_t z = blockIdx.z;
+  const int64_t o = (int64_t)z * 2 * s;
+  const int32_t s2 = (int32_t)min((int64_t)s, (int64_t)npad - o - s);  // ragged last pair (multiple of 64)
+  const int32_t tr = blockIdx.y * 64, tc = blockIdx.x * 64;  // output tile inside the s2 x s block
+  if (s2 <= 0 || tr >= s2) return;
+  const double* A;
+  const double* B;
+  int64_t lda, ldb;
+  int32_t k_lo, k_hi;
+  double* C;
+  int64_t ldc;
+  double sign;
+  if (phase == 0) {
+    A = L + (o + s) * npad + o; lda = npad;                       // B (dense)
+    B = Li + o * npad + o; ldb = npad;                            // Ai (lower): rows k >= tc contribute
+    k_lo = tc; k_hi = s;
+    C = T + (int64_t)z * s * s; ldc = s; sign = 1.0;
+  } else {
+    A = Li + (o + s) * npad + (o + s); lda = npad;                // Ci (lower): k <= tr + 63
+    B = T + (int64_t)z * s * s; ldb = s;
+    k_lo = 0; k_hi = min(tr + 64, s2);
+    C = Li + (o + s) * npad + o; ldc = npad; sign = -1.0;
   }
-  __syncthreads();
-  lds_trinv(S, X);
-  if (J == I) {
-    for (int e = t; e < NB * NB; e += blockDim.x) {
-      const int r = e / NB, s = e % NB;
-      Li[(Ib + r) * npad + Ib + s] = X[r * (NB + 1) + s];
-    }
-    // zero the upper blocks of this block row
-    for (int64_t e = t; e < (int64_t)NB * (npad - Ib - NB); e += blockDim.x) {
-      const int64_t r = e / (npad - Ib - NB), s = e % (npad - Ib - NB);
-      Li[(Ib + r) * npad + Ib + NB + s] = 0.0;
-    }
-    return;
-  }
-  double acc[16];
+  typedef double d4 __attribute__((ext_vector_type(4)));
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int wr = w >> 1, wc = w & 1;
+  d4 acc[2][2];
 #pragma unroll
-  for (int q = 0; q < 16; ++q) acc[q] = 0.0;
-  for (int32_t Kb = J; Kb < I; ++Kb) {
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = (d4){0.0, 0.0, 0.0, 0.0};
+  for (int32_t k0 = k_lo; k0 < k_hi; k0 += 16) {
+    // A tile 64 x 16 -> As[k][row]; B tile 16 x 64 -> Bs[k][col]
+    for (int e = t; e < 64 * 16; e += 256) {
+      const int r = e >> 4, kk = e & 15;
+      As[kk * 80 + r] = A[(int64_t)(tr + r) * lda + k0 + kk];
+      const int kb = e >> 6, c = e & 63;
+      Bs[kb * 80 + c] = B[(int64_t)(k0 + kb) * ldb + tc + c];
+    }
     __syncthreads();
-    for (int e = t; e < NB * NB; e += blockDim.x) {
-      const int r = e / NB, s = e % NB;
-      S[r * (NB + 1) + s] = L[(Ib + r) * npad + (int64_t)Kb * NB + s];
-      T[r * (NB + 1) + s] = Li[((int64_t)Kb * NB + r) * npad + Jb + s];
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const int kr = ks * 4 + (lane >> 4);
+      double af[2], bf[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) af[i] = As[kr * 80 + wr * 32 + i * 16 + (lane & 15)];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) bf[j] = Bs[kr * 80 + wc * 32 + j * 16 + (lane & 15)];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[i], bf[j], acc[i][j], 0, 0, 0);
     }
     __syncthreads();
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const int e = t + q * 256;
-      const int r = e / NB, s = e % NB;
-      double v = 0.0;
-      for (int w = 0; w < NB; ++w) v += S[r * (NB + 1) + w] * T[w * (NB + 1) + s];
-      acc[q] += v;
-    }
   }
-  __syncthreads();
 #pragma unroll
-  for (int q = 0; q < 16; ++q) {
-    const int e = t + q * 256;
-    T[(e / NB) * (NB + 1) + e % NB] = acc[q];
-  }
-  __syncthreads();
+  for (int i = 0; i < 2; ++i)
 #pragma unroll
-  for (int q = 0; q < 16; ++q) {
-    const int e = t + q * 256;
-    const int r = e / NB, s = e % NB;
-    double v = 0.0;
-    for (int w = 0; w <= r; ++w) v += X[r * (NB + 1) + w] * T[w * (NB + 1) + s];
-    Li[(Ib + r) * npad + Jb + s] = -v;
-  }
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = tr + wr * 32 + i * 16 + (lane >> 4) + 4 * r;
+        const int col = tc + wc * 32 + j * 16 + (lane & 15);
+        C[(int64_t)row * ldc + col] = sign * acc[i][j][r];
+      }
 }
 
 // out = Linv * v  (one wave per row)
@@ -299,14 +384,18 @@ __global__ __launch_bounds__(256) void k_lower_mv(const double* __restrict__ Li,
   if (lane == 0) out[r] = s;
 }
 
-// out = Linv^T * v  (one thread per column)
-__global__ void k_lower_tmv(const double* __restrict__ Li, int32_t npad, const double* __restrict__ v,
-                            double* __restrict__ out) {
-  const int32_t c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= npad) return;
+// out = Linv^T * v: 64 columns per workgroup, 4 row phases reduced in LDS
+__global__ __launch_bounds__(256) void k_lower_tmv(const double* __restrict__ Li, int32_t npad,
+                                                   const double* __restrict__ v, double* __restrict__ out) {
+  __shared__ double red[4][64];
+  const int t = threadIdx.x, cl = t & 63, ph = t >> 6;
+  const int32_t c = blockIdx.x * 64 + cl;
   double s = 0.0;
-  for (int32_t r = c; r < npad; ++r) s += Li[(int64_t)r * npad + c] * v[r];
-  out[c] = s;
+  if (c < npad)
+    for (int32_t r = c + ph; r < npad; r += 4) s += Li[(int64_t)r * npad + c] * v[r];
+  red[ph][cl] = s;
+  __syncthreads();
+  if (ph == 0 && c < npad) out[c] = (red[0][cl] + red[1][cl]) + (red[2][cl] + red[3][cl]);
 }
 
 // ---------------------------------------------------------------------------
@@ -363,8 +452,8 @@ static int gp_alloc(ut_ctx* c, int32_t npad, int32_t d) {
   if (c->gp_cap_n >= npad && c->gp_d == d && c->gp_Xs) return 0;
   if (c->gp_Xs_f) {
     UT_HIP(c, hipStreamSynchronize(c->stream));
-    hipFree(c->gp_Xs_f); hipFree(c->gp_Linv_f);
-    c->gp_Xs_f = nullptr; c->gp_Linv_f = nullptr;
+    hipFree(c->gp_Xs_f); hipFree(c->gp_Linv_f); hipFree(c->gp_T);
+    c->gp_Xs_f = nullptr; c->gp_Linv_f = nullptr; c->gp_T = nullptr;
   }
   if (c->gp_Xs) {
     UT_HIP(c, hipStreamSynchronize(c->stream));
@@ -382,6 +471,7 @@ static int gp_alloc(ut_ctx* c, int32_t npad, int32_t d) {
   UT_HIP(c, hipMalloc((void**)&c->gp_inv_ell, sizeof(double) * d));
   UT_HIP(c, hipMalloc((void**)&c->gp_stats, sizeof(double) * 4));
   UT_HIP(c, hipMalloc((void**)&c->gp_flag, sizeof(int32_t)));
+  UT_HIP(c, hipMalloc((void**)&c->gp_T, sizeof(double) * npad * npad));
   UT_HIP(c, hipMalloc((void**)&c->gp_Xs_f, sizeof(float) * npad * d));
   UT_HIP(c, hipMalloc((void**)&c->gp_Linv_f, sizeof(float) * npad * npad));
   c->gp_cap_n = npad;
@@ -406,24 +496,32 @@ int gp_fit_impl(ut_ctx* c, const double* X, const double* y, int32_t n, int32_t 
   UT_HIP(c, hipMemsetAsync(c->gp_flag, 0, sizeof(int32_t), c->stream));
   hipLaunchKernelGGL(k_gp_prep_train, dim3(grid1(npad, 256)), dim3(256), 0, c->stream, dX, n, npad, d,
                      c->gp_inv_ell, c->gp_Xs, c->gp_xnorm);
-  hipLaunchKernelGGL(k_gp_kmat, dim3(grid1((int64_t)npad * npad, 256)), dim3(256), 0, c->stream, c->gp_Xs,
+  hipLaunchKernelGGL(k_gp_kmat, dim3(npad / 64, npad / 64), dim3(256), 0, c->stream, c->gp_Xs,
                      c->gp_xnorm, n, npad, d, h->sigma_f2, h->sigma_n2 + h->jitter, c->gp_K);
   hipLaunchKernelGGL(k_gp_ystats, dim3(1), dim3(256), 0, c->stream, dy, n, npad, c->gp_y, c->gp_stats);
   UT_LAUNCH_CHECK(c);
   const int32_t nb = npad / NB;
+  UT_HIP(c, hipMemsetAsync(c->gp_Linv, 0, sizeof(double) * npad * npad, c->stream));
   for (int32_t kb = 0; kb < nb; ++kb) {
-    hipLaunchKernelGGL(k_chol_panel, dim3(nb - kb), dim3(256), 0, c->stream, c->gp_K, npad, kb, c->gp_flag);
+    hipLaunchKernelGGL(k_chol_diag, dim3(1), dim3(256), 0, c->stream, c->gp_K, c->gp_Linv, npad, kb, c->gp_flag);
     const int32_t T = nb - kb - 1;
-    if (T > 0)
+    if (T > 0) {
+      hipLaunchKernelGGL(k_chol_rows, dim3(T), dim3(256), 0, c->stream, c->gp_K, c->gp_Linv, npad, kb);
       hipLaunchKernelGGL(k_chol_update, dim3(T * (T + 1) / 2), dim3(256), 0, c->stream, c->gp_K, npad, kb);
+    }
   }
   UT_LAUNCH_CHECK(c);
-  for (int32_t I = 0; I < nb; ++I)
-    hipLaunchKernelGGL(k_trinv_row, dim3(I + 1), dim3(256), 0, c->stream, c->gp_K, c->gp_Linv, npad, I);
+  // off-diagonal blocks of L^-1 by recursive doubling (diagonal blocks came from k_chol_diag)
+  for (int32_t lv = NB; lv < npad; lv *= 2) {
+    const int32_t pairs = (int32_t)((npad - lv + 2 * lv - 1) / (2 * lv));
+    const dim3 grid(lv / 64, lv / 64, pairs);
+    hipLaunchKernelGGL(k_trinv_level, grid, dim3(256), 0, c->stream, c->gp_K, c->gp_Linv, c->gp_T, npad, lv, 0);
+    hipLaunchKernelGGL(k_trinv_level, grid, dim3(256), 0, c->stream, c->gp_K, c->gp_Linv, c->gp_T, npad, lv, 1);
+  }
   UT_LAUNCH_CHECK(c);
   hipLaunchKernelGGL(k_lower_mv, dim3(grid1(npad, 4)), dim3(256), 0, c->stream, c->gp_Linv, npad, c->gp_y,
                      c->gp_tmp);
-  hipLaunchKernelGGL(k_lower_tmv, dim3(grid1(npad, 256)), dim3(256), 0, c->stream, c->gp_Linv, npad, c->gp_tmp,
+  hipLaunchKernelGGL(k_lower_tmv, dim3(grid1(npad, 64)), dim3(256), 0, c->stream, c->gp_Linv, npad, c->gp_tmp,
                      c->gp_alpha);
   UT_LAUNCH_CHECK(c);
   if (c->gp_prec == 32) {

@@ -102,6 +102,7 @@ struct ut_ctx {
   double* gp_xnorm = nullptr;  // [n]
   double* gp_K = nullptr;      // [n][n] work / L
   double* gp_Linv = nullptr;   // [n][n]
+  double* gp_T = nullptr;      // [n][n] scratch of the recursive inverse
   double* gp_y = nullptr;      // [n] standardised
   double* gp_tmp = nullptr;    // [n]
   double* gp_alpha = nullptr;  // [n]
