@@ -196,7 +196,7 @@ def main():
                    "candidates_per_gpu": m, "gp_n": n, "dims": d, "k": k, "parallelism": f"dp{world}"},
         "stage_ms": stages,
         "roofline": {"bound": "mfma",
-                     "kernel": "k_gp_gemm2<%s,1> (var: L^-1 K*^T, %s)" % (
+                     "kernel": "k_gp_var<%s> (persistent var contraction L^-1 K*^T, %s)" % (
                          ("double", "v_mfma_f64_16x16x4_f64") if args.precision == 64 else
                          ("float", "v_mfma_f32_32x32x2_f32")),
                      "achieved": achieved, "peak": peak, "unit": "TFLOP/s",

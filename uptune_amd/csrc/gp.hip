@@ -452,8 +452,8 @@ static int gp_alloc(ut_ctx* c, int32_t npad, int32_t d) {
   if (c->gp_cap_n >= npad && c->gp_d == d && c->gp_Xs) return 0;
   if (c->gp_Xs_f) {
     UT_HIP(c, hipStreamSynchronize(c->stream));
-    hipFree(c->gp_Xs_f); hipFree(c->gp_Linv_f); hipFree(c->gp_T);
-    c->gp_Xs_f = nullptr; c->gp_Linv_f = nullptr; c->gp_T = nullptr;
+    hipFree(c->gp_Xs_f); hipFree(c->gp_LinvT); hipFree(c->gp_LinvT_f); hipFree(c->gp_T); hipFree(c->gp_ctr);
+    c->gp_Xs_f = nullptr; c->gp_LinvT = nullptr; c->gp_LinvT_f = nullptr; c->gp_T = nullptr; c->gp_ctr = nullptr;
   }
   if (c->gp_Xs) {
     UT_HIP(c, hipStreamSynchronize(c->stream));
@@ -473,7 +473,9 @@ static int gp_alloc(ut_ctx* c, int32_t npad, int32_t d) {
   UT_HIP(c, hipMalloc((void**)&c->gp_flag, sizeof(int32_t)));
   UT_HIP(c, hipMalloc((void**)&c->gp_T, sizeof(double) * npad * npad));
   UT_HIP(c, hipMalloc((void**)&c->gp_Xs_f, sizeof(float) * npad * d));
-  UT_HIP(c, hipMalloc((void**)&c->gp_Linv_f, sizeof(float) * npad * npad));
+  UT_HIP(c, hipMalloc((void**)&c->gp_LinvT, sizeof(double) * npad * npad));
+  UT_HIP(c, hipMalloc((void**)&c->gp_LinvT_f, sizeof(float) * npad * npad));
+  UT_HIP(c, hipMalloc((void**)&c->gp_ctr, sizeof(int32_t) * 8));
   c->gp_cap_n = npad;
   c->gp_d = d;
   return 0;
@@ -524,10 +526,8 @@ int gp_fit_impl(ut_ctx* c, const double* X, const double* y, int32_t n, int32_t 
   hipLaunchKernelGGL(k_lower_tmv, dim3(grid1(npad, 64)), dim3(256), 0, c->stream, c->gp_Linv, npad, c->gp_tmp,
                      c->gp_alpha);
   UT_LAUNCH_CHECK(c);
-  if (c->gp_prec == 32) {
-    if ((rc = launch_to_f32(c, c->gp_Xs, c->gp_Xs_f, (int64_t)npad * d))) return rc;
-    if ((rc = launch_to_f32(c, c->gp_Linv, c->gp_Linv_f, (int64_t)npad * npad))) return rc;
-  }
+  if (c->gp_prec == 32 && (rc = launch_to_f32(c, c->gp_Xs, c->gp_Xs_f, (int64_t)npad * d))) return rc;
+  if ((rc = launch_transpose(c, c->gp_Linv, npad, c->gp_LinvT, c->gp_prec == 32 ? c->gp_LinvT_f : nullptr))) return rc;
   c->gp_fit_prec = c->gp_prec;
   int32_t flag = 0;
   UT_HIP(c, hipMemcpyAsync(&flag, c->gp_flag, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
@@ -546,7 +546,9 @@ int gp_score_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, const ut
   const int32_t npad = ((n + NPAD - 1) / NPAD) * NPAD;
   const int32_t RT = npad / NPAD;
   const int32_t CT = (int32_t)((m + NPAD - 1) / NPAD);
-  const int64_t ldk = (int64_t)CT * NPAD;
+  // K* rows padded to whole variance column tiles: the variance kernel reads
+  // full 256-candidate strips; columns >= m only feed outputs that are dropped
+  const int64_t ldk = ((m + VAR_BN - 1) / VAR_BN) * VAR_BN;
   const bool fp32 = c->gp_fit_prec == 32;
   int rc;
   if ((rc = ensure(c, c->kst, (size_t)npad * ldk))) return rc;
@@ -560,8 +562,8 @@ int gp_score_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, const ut
                               CT, m, c->kst.p, ldk, c->mu_part.p)))
     return rc;
   mark(c, "kstar");
-  if ((rc = launch_gemm_var(c, fp32, fp32 ? (const void*)c->gp_Linv_f : (const void*)c->gp_Linv, npad, c->kst.p,
-                            ldk, npad, RT, CT, m, c->var_part.p)))
+  if ((rc = launch_gemm_var(c, fp32, fp32 ? (const void*)c->gp_LinvT_f : (const void*)c->gp_LinvT, npad, c->kst.p,
+                            ldk, npad, m, c->var_part.p)))
     return rc;
   mark(c, "var");
   hipLaunchKernelGGL(k_gp_finalize, dim3(grid1(m, 256)), dim3(256), 0, c->stream, m, RT, RT, c->mu_part.p,

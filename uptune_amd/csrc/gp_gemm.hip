@@ -7,6 +7,8 @@
 //   MODE 1 (var):  C[n x m] = L^-1[n x n] * K*^T[n x m]   (lower triangular:
 //                  the K loop of row tile rt stops at (rt+1)*128)
 //                  epilogue: column partial  sum_c C[c][i]^2
+//                  (the library launches the persistent k_gp_var below for
+//                  this; MODE 1 of k_gp_gemm2 stays as its reference form)
 //
 // Tile 128 x 128 per 256-thread workgroup (2 x 2 waves of 64 x 64), K step 32,
 // global -> register prefetch of step t+1 while step t computes out of the
@@ -268,17 +270,223 @@ int launch_gemm_kstar(ut_ctx* c, bool fp32, const void* A, int64_t lda, const do
   return 0;
 }
 
-int launch_gemm_var(ut_ctx* c, bool fp32, const void* Linv, int64_t lda, const void* kst, int64_t ldk, int32_t npad,
-                    int32_t RT, int32_t CT, int64_t m, double* part) {
-  const int32_t CT8 = ((CT + 7) / 8) * 8;
+// ---------------------------------------------------------------------------
+// Variance contraction, persistent:  part[rt][col] = sum_{r in tile rt} (L^-1 K*^T)[r][col]^2
+//
+// One 512-thread workgroup per CU (8 waves as 2 x 4 of 64 x 64 outputs) walks
+// (column strip, row tile) work items: 128 rows of L^-1 x 256 candidates, K
+// loop over [0, (rt+1)*128) (L^-1 is lower triangular).  Work items of XCD
+// group x (blocks b = x mod 8) are the column strips ct = x mod 8, handed out
+// by a per-group atomic ticket, the longest row tile of a strip first; the 8
+// row tiles of a strip therefore run side by side on one XCD and share the
+// strip through its L2.  Tiles are staged by global_load_lds_dwordx4 (1 KiB
+// per wave-instruction, lane-linear LDS image) into a 3-deep ring: step kt+1
+// stays in flight across the barrier of step kt (counted vmcnt, raw barrier).
+// A non-persistent grid of these tiles left CUs idle ~30% of the time: the
+// in-order workgroup dispatcher stalls behind long (late row) tiles.
+//   A = (L^-1)^T [k][row] (ld npad), B = K*^T [k][col] (ld ldk, ldk % 256 == 0)
+//   fp64: v_mfma_f64_16x16x4_f64, BK 16;  fp32: v_mfma_f32_32x32x2_f32, BK 32
+// ---------------------------------------------------------------------------
+constexpr int V_NT = 512, V_ST = 3;
+
+template <typename T>
+struct VCfg {
+  static constexpr int BK = 64 / (int)sizeof(T) * 2;  // 16 (f64), 32 (f32): 16 KiB A + 32 KiB B per stage
+  static constexpr int SA = BK * VAR_BM, SB = BK * VAR_BN, STAGE = SA + SB;
+  static constexpr int PER_INSTR = 1024 / (int)sizeof(T);  // elements one glds wave-instruction moves
+};
+
+template <typename T>
+__device__ __forceinline__ void var_issue(const T* __restrict__ AT, int64_t lda, const T* __restrict__ B, int64_t ldb,
+                                          int32_t row0, int64_t col0, int32_t k0, T* st, int w, int lane) {
+  using C = VCfg<T>;
+  constexpr int EPL = 16 / (int)sizeof(T);  // elements per lane
+  // wave w: A instructions 2w, 2w+1 (16 in all), B instructions 4w .. 4w+3 (32 in all)
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int q = 2 * w + u;
+    const int e = q * C::PER_INSTR + lane * EPL;  // linear index in the [BK][BM] tile
+    const T* src = AT + (int64_t)(k0 + e / VAR_BM) * lda + row0 + (e % VAR_BM);
+    __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(st + q * C::PER_INSTR), 16, 0, 0);
+  }
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int q = 4 * w + u;
+    const int e = q * C::PER_INSTR + lane * EPL;  // linear index in the [BK][BN] tile
+    const T* src = B + (int64_t)(k0 + e / VAR_BN) * ldb + col0 + (e % VAR_BN);
+    __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(st + C::SA + q * C::PER_INSTR), 16,
+                                     0, 0);
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(V_NT, 1) void k_gp_var(const T* __restrict__ AT, int64_t lda, const T* __restrict__ B,
+                                                     int64_t ldb, int32_t K, int32_t RT, int32_t CT, int64_t m,
+                                                     int32_t* __restrict__ ticket, double* __restrict__ part,
+                                                     int64_t ldp) {
+  using C = VCfg<T>;
+  constexpr int BK = C::BK;
+  // ALL LDS in one object: a second __shared__ beside the glds ring makes
+  // hipcc wait vmcnt(0) before every step's first ds_read (drains the ring)
+  __shared__ __attribute__((aligned(16))) T lds[V_ST * C::STAGE + 16 / sizeof(T)];
+  int32_t& s_item = *reinterpret_cast<int32_t*>(lds + V_ST * C::STAGE);
+  const int t = threadIdx.x, lane = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wm = w >> 2, wn = w & 3;
+  const int32_t xcd = blockIdx.x & 7;
+
+  for (;;) {
+    if (t == 0) s_item = atomicAdd(&ticket[xcd], 1);
+    __syncthreads();  // also: the previous item's epilogue is done with the LDS
+    const int32_t j = s_item;
+    const int32_t ct = (j / RT) * 8 + xcd;
+    if (ct >= CT) break;  // uniform: every wave of the block leaves together
+    const int32_t rt = RT - 1 - (j % RT);
+    const int64_t col0 = (int64_t)ct * VAR_BN;
+    const int32_t row0 = rt * VAR_BM;
+    const int32_t nk = min(K, row0 + VAR_BM) / BK;
+
+    typedef double d4 __attribute__((ext_vector_type(4)));
+    typedef float f16 __attribute__((ext_vector_type(16)));
+    d4 accd[4][4];
+    f16 accf[2][2];
+    if constexpr (sizeof(T) == 8) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) accd[i][jj] = (d4){0.0, 0.0, 0.0, 0.0};
+    } else {
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) accf[i][jj][r] = 0.0f;
+    }
+
+    var_issue<T>(AT, lda, B, ldb, row0, col0, 0, lds, w, lane);
+    if (nk > 1) var_issue<T>(AT, lda, B, ldb, row0, col0, BK, lds + C::STAGE, w, lane);
+    for (int32_t kt = 0; kt < nk; ++kt) {
+      // 6 glds per wave per stage: leave stage kt+1 in flight, retire stage kt
+      if (kt + 1 < nk)
+        asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();  // all waves' stage kt landed; all reads of stage kt-1 done
+      asm volatile("" ::: "memory");
+      if (kt + 2 < nk)
+        var_issue<T>(AT, lda, B, ldb, row0, col0, (kt + 2) * BK, lds + ((kt + 2) % V_ST) * C::STAGE, w, lane);
+      const T* as = lds + (kt % V_ST) * C::STAGE;
+      const T* bs = as + C::SA;
+      if constexpr (sizeof(T) == 8) {
+#pragma unroll
+        for (int ks = 0; ks < BK / 4; ++ks) {
+          const int kr = ks * 4 + (lane >> 4);
+          double af[4], bf[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) af[i] = as[kr * VAR_BM + wm * 64 + i * 16 + (lane & 15)];
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj) bf[jj] = bs[kr * VAR_BN + wn * 64 + jj * 16 + (lane & 15)];
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj)
+              accd[i][jj] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[i], bf[jj], accd[i][jj], 0, 0, 0);
+        }
+      } else {
+#pragma unroll
+        for (int ks = 0; ks < BK / 2; ++ks) {
+          const int kr = ks * 2 + (lane >> 5);
+          float af[2], bf[2];
+#pragma unroll
+          for (int i = 0; i < 2; ++i) af[i] = as[kr * VAR_BM + wm * 64 + i * 32 + (lane & 31)];
+#pragma unroll
+          for (int jj = 0; jj < 2; ++jj) bf[jj] = bs[kr * VAR_BN + wn * 64 + jj * 32 + (lane & 31)];
+#pragma unroll
+          for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int jj = 0; jj < 2; ++jj)
+              accf[i][jj] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i], bf[jj], accf[i][jj], 0, 0, 0);
+        }
+      }
+    }
+
+    // epilogue: column sums of squares over this tile's 128 rows
+    __syncthreads();
+    double* red = reinterpret_cast<double*>(lds);  // [2][256]
+    if constexpr (sizeof(T) == 8) {
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        const int cl = wn * 64 + jj * 16 + (lane & 15);
+        double s = 0.0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) s += accd[i][jj][r] * accd[i][jj][r];
+        s += __shfl_xor(s, 16);
+        s += __shfl_xor(s, 32);
+        if ((lane >> 4) == 0) red[wm * VAR_BN + cl] = s;
+      }
+    } else {
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) {
+        const int cl = wn * 64 + jj * 32 + (lane & 31);
+        double s = 0.0;
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) s += (double)accf[i][jj][r] * (double)accf[i][jj][r];
+        s += __shfl_xor(s, 32);
+        if ((lane >> 5) == 0) red[wm * VAR_BN + cl] = s;
+      }
+    }
+    __syncthreads();
+    if (t < VAR_BN) {
+      const int64_t col = col0 + t;
+      if (col < m) part[(int64_t)rt * ldp + col] = red[t] + red[VAR_BN + t];
+    }
+  }
+}
+
+int launch_gemm_var(ut_ctx* c, bool fp32, const void* LinvT, int64_t lda, const void* kst, int64_t ldk, int32_t npad,
+                    int64_t m, double* part) {
+  UT_CHECK(c, npad % VAR_BM == 0 && ldk % VAR_BN == 0 && ldk >= m, UT_EINVAL, "gemm_var: bad padding");
+  const int32_t RT = npad / VAR_BM;
+  const int32_t CT = (int32_t)((m + VAR_BN - 1) / VAR_BN);
+  const int64_t items = (int64_t)RT * CT;
+  // one block per CU (the 144 KiB LDS ring allows no more), a multiple of 8 so
+  // every XCD group has workers; never more blocks than work items
+  int32_t nb = (c->n_cu / 8) * 8;
+  if (items < nb) nb = (int32_t)(((items + 7) / 8) * 8);
+  UT_HIP(c, hipMemsetAsync(c->gp_ctr, 0, sizeof(int32_t) * 8, c->stream));
   if (fp32)
-    hipLaunchKernelGGL((k_gp_gemm2<float, 1>), dim3(RT * CT8), dim3(G_NT), 0, c->stream, (const float*)Linv, lda,
-                       kst, ldk, npad, RT, CT, m, nullptr, nullptr, nullptr, nullptr, 0.0, 0, (float*)nullptr,
-                       (int64_t)0, part, ldk);
+    hipLaunchKernelGGL(k_gp_var<float>, dim3(nb), dim3(V_NT), 0, c->stream, (const float*)LinvT, lda,
+                       (const float*)kst, ldk, npad, RT, CT, m, c->gp_ctr, part, ldk);
   else
-    hipLaunchKernelGGL((k_gp_gemm2<double, 1>), dim3(RT * CT8), dim3(G_NT), 0, c->stream, (const double*)Linv, lda,
-                       kst, ldk, npad, RT, CT, m, nullptr, nullptr, nullptr, nullptr, 0.0, 0, (double*)nullptr,
-                       (int64_t)0, part, ldk);
+    hipLaunchKernelGGL(k_gp_var<double>, dim3(nb), dim3(V_NT), 0, c->stream, (const double*)LinvT, lda,
+                       (const double*)kst, ldk, npad, RT, CT, m, c->gp_ctr, part, ldk);
+  UT_LAUNCH_CHECK(c);
+  return 0;
+}
+
+// dst[c][r] = src[r][c] (n x n, n % 64 == 0), optionally also as fp32
+__global__ __launch_bounds__(256) void k_transpose(const double* __restrict__ src, int32_t n, double* __restrict__ dst,
+                                                   float* __restrict__ dst_f) {
+  __shared__ double tile[64][65];
+  const int32_t r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  for (int r = ty; r < 64; r += 4) tile[r][tx] = src[(int64_t)(r0 + r) * n + c0 + tx];
+  __syncthreads();
+  for (int r = ty; r < 64; r += 4) {
+    const double v = tile[tx][r];
+    dst[(int64_t)(c0 + r) * n + r0 + tx] = v;
+    if (dst_f) dst_f[(int64_t)(c0 + r) * n + r0 + tx] = (float)v;
+  }
+}
+
+int launch_transpose(ut_ctx* c, const double* src, int32_t n, double* dst, float* dst_f) {
+  UT_CHECK(c, n % 64 == 0, UT_EINVAL, "transpose: n % 64 != 0");
+  hipLaunchKernelGGL(k_transpose, dim3(n / 64, n / 64), dim3(256), 0, c->stream, src, n, dst, dst_f);
   UT_LAUNCH_CHECK(c);
   return 0;
 }

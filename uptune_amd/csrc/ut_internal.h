@@ -113,7 +113,10 @@ struct ut_ctx {
   int32_t gp_prec = 64;        // precision requested for the next fit
   int32_t gp_fit_prec = 64;    // precision of the fitted factors used by scoring
   float* gp_Xs_f = nullptr;    // fp32 copies for the fp32 MFMA path
-  float* gp_Linv_f = nullptr;
+  double* gp_LinvT = nullptr;  // (L^-1)^T [k][row]: the A operand of the variance contraction
+  float* gp_LinvT_f = nullptr;
+  int32_t* gp_ctr = nullptr;   // [8] per-XCD tile tickets of the persistent variance kernel
+  int32_t n_cu = 256;
   int64_t gp_cap_n = 0;
 
   // scratch for GP scoring / round pipeline
@@ -197,8 +200,10 @@ int topk_impl(ut_ctx* c, const double* score, const uint8_t* dup, int64_t m, int
               int64_t* out_idx, double* out_score);
 int launch_gemm_kstar(ut_ctx* c, bool fp32, const void* A, int64_t lda, const double* feat, int64_t ldf, int32_t d,
                       int32_t RT, int32_t CT, int64_t m, void* kst, int64_t ldk, double* part);
-int launch_gemm_var(ut_ctx* c, bool fp32, const void* Linv, int64_t lda, const void* kst, int64_t ldk, int32_t npad,
-                    int32_t RT, int32_t CT, int64_t m, double* part);
+int launch_gemm_var(ut_ctx* c, bool fp32, const void* LinvT, int64_t lda, const void* kst, int64_t ldk, int32_t npad,
+                    int64_t m, double* part);
+int launch_transpose(ut_ctx* c, const double* src, int32_t n, double* dst, float* dst_f);
+constexpr int VAR_BM = 128, VAR_BN = 256;  // variance-contraction tile (rows of L^-1 x candidates)
 int launch_to_f32(ut_ctx* c, const double* src, float* dst, int64_t n);
 int launch_gather_rows(ut_ctx* c, const double* values, int64_t ld, const int64_t* idx, int64_t cand_base,
                        int32_t k, double* out, int64_t ldo, const uint32_t* dig, uint32_t* out_dig);
