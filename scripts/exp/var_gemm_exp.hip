@@ -1,6 +1,9 @@
 // Standalone experiment: GP variance contraction  part[rt][col] = sum_rows (L^-1 K*^T)^2
-// on the C2 shape (npad = 1024, m = 1M, fp64), current library kernel vs a
-// global_load_lds pipelined variant.  Not part of the library.
+// on the C2 shape (npad = 1024, m = 1M, fp64): a non-persistent
+// global_load_lds grid (one workgroup per tile) vs the library's persistent
+// k_gp_var.  The per-block stamps of the non-persistent grid are what showed
+// CUs idling between tiles (in-order dispatch behind long tiles).  Not part
+// of the library.
 //
 //   hipcc -O3 -std=c++17 --offload-arch=gfx950 -ffp-contract=off -I uptune_amd/csrc \
 //     scripts/exp/var_gemm_exp.hip -L uptune_amd -luthot -Wl,-rpath,$PWD/uptune_amd -o scripts/exp/var_gemm_exp
@@ -181,13 +184,14 @@ int main(int argc, char** argv) {
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
   const double flops = (double)m * npad * (npad + 1);
-  const int CT = (int)((m + 127) / 128), CT8 = ((CT + 7) / 8) * 8;
   const int CTx = (int)((m + 255) / 256), CTx8 = ((CTx + 7) / 8) * 8;
 
+  int32_t* ticket;
+  CK(hipMalloc(&ticket, sizeof(int32_t) * 8));
   auto run0 = [&]() {
-    hipLaunchKernelGGL((k_gp_gemm2<double, 1>), dim3(RT * CT8), dim3(G_NT), 0, 0, (const double*)L, (int64_t)npad,
-                       (const void*)Kst, ldk, npad, RT, CT, m, nullptr, nullptr, nullptr, nullptr, 0.0, 0,
-                       (double*)nullptr, (int64_t)0, p0, ldk);
+    CK(hipMemsetAsync(ticket, 0, sizeof(int32_t) * 8, 0));
+    hipLaunchKernelGGL(k_gp_var<double>, dim3(256), dim3(V_NT), 0, 0, (const double*)LT, (int64_t)npad,
+                       (const double*)Kst, ldk, npad, RT, CTx, m, ticket, p0, ldk);
   };
   auto run1 = [&](int prio) {
     if (prio)
@@ -211,7 +215,7 @@ int main(int argc, char** argv) {
     printf("%-28s %9.3f ms  %7.2f TF/s  (%.1f%% of 78.6)\n", name, ms, flops / ms * 1e-9, flops / ms * 1e-9 / 78.6 * 100);
     fflush(stdout);
   };
-  timeit("lib k_gp_gemm2<double,1>", run0);
+  timeit("lib k_gp_var<double> (persistent)", run0);
   timeit("glds 128x256 3-stage", [&] { run1(0); });
   std::vector<double> h0((size_t)RT * ldk), h1((size_t)RT * ldk);
   CK(hipMemcpy(h0.data(), p0, sizeof(double) * h0.size(), hipMemcpyDeviceToHost));
@@ -222,7 +226,7 @@ int main(int argc, char** argv) {
       double a = h0[(size_t)r * ldk + c], b = h1[(size_t)r * ldk + c];
       if (a != b) ++bad;
     }
-  printf("glds vs lib: %lld mismatching partials of %lld\n", (long long)bad, (long long)(RT * m));
+  printf("grid vs persistent: %lld mismatching partials of %lld\n", (long long)bad, (long long)(RT * m));
   timeit("glds 128x256 3-stage prio", [&] { run1(1); });
   timeit("glds fixed B tile (L2)", [&] {
     hipLaunchKernelGGL((k_var_glds<0, 1>), dim3(RT * CTx8), dim3(X_NT), 0, 0, LT, (int64_t)npad, Kst, ldk, npad, RT, CTx,

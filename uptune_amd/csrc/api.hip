@@ -166,7 +166,7 @@ int ut_ctx_destroy(ut_ctx* c) {
   fr(c->pop); fr(c->pso_vel); fr(c->pso_best); fr(c->hist_keys); fr(c->hist_state); fr(c->batch_slots);
   fr(c->gp_Xs); fr(c->gp_xnorm); fr(c->gp_K); fr(c->gp_Linv); fr(c->gp_y); fr(c->gp_tmp);
   fr(c->gp_alpha); fr(c->gp_inv_ell); fr(c->gp_stats); fr(c->gp_flag); fr(c->gp_Xs_f); fr(c->gp_T);
-  fr(c->gp_LinvT); fr(c->gp_LinvT_f); fr(c->gp_ctr);
+  fr(c->gp_LinvT); fr(c->gp_LinvT_f); fr(c->gp_ctr); fr(c->gp_XsT); fr(c->ucand.p);
   fr(c->kst.p); fr(c->mu_part.p); fr(c->var_part.p); fr(c->cnorm.p);
   fr(c->r_values.p); fr(c->r_feat.p); fr(c->r_mu.p); fr(c->r_var.p); fr(c->r_score.p); fr(c->r_digest.p);
   fr(c->r_dup.p); fr(c->tk_score[0].p); fr(c->tk_score[1].p); fr(c->tk_idx[0].p); fr(c->tk_idx[1].p);

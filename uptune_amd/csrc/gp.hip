@@ -453,7 +453,9 @@ static int gp_alloc(ut_ctx* c, int32_t npad, int32_t d) {
   if (c->gp_Xs_f) {
     UT_HIP(c, hipStreamSynchronize(c->stream));
     hipFree(c->gp_Xs_f); hipFree(c->gp_LinvT); hipFree(c->gp_LinvT_f); hipFree(c->gp_T); hipFree(c->gp_ctr);
+    hipFree(c->gp_XsT);
     c->gp_Xs_f = nullptr; c->gp_LinvT = nullptr; c->gp_LinvT_f = nullptr; c->gp_T = nullptr; c->gp_ctr = nullptr;
+    c->gp_XsT = nullptr;
   }
   if (c->gp_Xs) {
     UT_HIP(c, hipStreamSynchronize(c->stream));
@@ -475,7 +477,8 @@ static int gp_alloc(ut_ctx* c, int32_t npad, int32_t d) {
   UT_HIP(c, hipMalloc((void**)&c->gp_Xs_f, sizeof(float) * npad * d));
   UT_HIP(c, hipMalloc((void**)&c->gp_LinvT, sizeof(double) * npad * npad));
   UT_HIP(c, hipMalloc((void**)&c->gp_LinvT_f, sizeof(float) * npad * npad));
-  UT_HIP(c, hipMalloc((void**)&c->gp_ctr, sizeof(int32_t) * 8));
+  UT_HIP(c, hipMalloc((void**)&c->gp_ctr, sizeof(int32_t) * 16));
+  UT_HIP(c, hipMalloc((void**)&c->gp_XsT, sizeof(double) * npad * (((d + 15) / 16) * 16)));
   c->gp_cap_n = npad;
   c->gp_d = d;
   return 0;
@@ -527,6 +530,7 @@ int gp_fit_impl(ut_ctx* c, const double* X, const double* y, int32_t n, int32_t 
                      c->gp_alpha);
   UT_LAUNCH_CHECK(c);
   if (c->gp_prec == 32 && (rc = launch_to_f32(c, c->gp_Xs, c->gp_Xs_f, (int64_t)npad * d))) return rc;
+  if ((rc = launch_xs_t(c, c->gp_Xs, npad, d, ((d + 15) / 16) * 16, c->gp_XsT))) return rc;
   if ((rc = launch_transpose(c, c->gp_Linv, npad, c->gp_LinvT, c->gp_prec == 32 ? c->gp_LinvT_f : nullptr))) return rc;
   c->gp_fit_prec = c->gp_prec;
   int32_t flag = 0;
@@ -544,22 +548,21 @@ int gp_score_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, const ut
   if (m <= 0) return 0;
   const int32_t n = c->gp_n, d = c->gp_d;
   const int32_t npad = ((n + NPAD - 1) / NPAD) * NPAD;
-  const int32_t RT = npad / NPAD;
-  const int32_t CT = (int32_t)((m + NPAD - 1) / NPAD);
+  const int32_t dpad = ((d + 15) / 16) * 16;
   // K* rows padded to whole variance column tiles: the variance kernel reads
-  // full 256-candidate strips; columns >= m only feed outputs that are dropped
+  // full 256-candidate strips (the K* kernel writes zeros past m)
   const int64_t ldk = ((m + VAR_BN - 1) / VAR_BN) * VAR_BN;
   const bool fp32 = c->gp_fit_prec == 32;
+  const int32_t RT = npad / NPAD;
   int rc;
   if ((rc = ensure(c, c->kst, (size_t)npad * ldk))) return rc;
   if ((rc = ensure(c, c->mu_part, (size_t)RT * ldk))) return rc;
   if ((rc = ensure(c, c->var_part, (size_t)RT * ldk))) return rc;
   if ((rc = ensure(c, c->cnorm, (size_t)ldk))) return rc;
-  hipLaunchKernelGGL(k_gp_cnorm, dim3(grid1(m, 256)), dim3(256), 0, c->stream, feat, ld, m, d, c->gp_inv_ell,
-                     c->cnorm.p);
+  if ((rc = ensure(c, c->ucand, (size_t)dpad * ldk))) return rc;
+  if ((rc = launch_prep_cand(c, feat, ld, m, d, dpad, c->ucand.p, ldk, c->cnorm.p))) return rc;
   mark(c, "cnorm");
-  if ((rc = launch_gemm_kstar(c, fp32, (const void*)c->gp_Xs, d, feat, ld, d, RT,
-                              CT, m, c->kst.p, ldk, c->mu_part.p)))
+  if ((rc = launch_gemm_kstar(c, fp32, c->gp_XsT, npad, c->ucand.p, dpad, m, c->kst.p, ldk, c->mu_part.p)))
     return rc;
   mark(c, "kstar");
   if ((rc = launch_gemm_var(c, fp32, fp32 ? (const void*)c->gp_LinvT_f : (const void*)c->gp_LinvT, npad, c->kst.p,

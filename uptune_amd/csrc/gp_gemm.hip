@@ -1,22 +1,11 @@
 // gp_gemm.hip -- the two dense contractions of GP scoring (the MFMA-bound
-// stage of the path):
+// stage of the path), both persistent (one or two workgroups per CU pulling
+// work items from per-XCD tickets) and staged by global_load_lds:
 //
-//   MODE 0 (K*):   C[n x m] = Xs[n x d] * (U/ell)[d x m]
-//                  epilogue: k* = sf2 exp(-0.5 max(|xs|^2 + |us|^2 - 2C, 0)),
-//                  store K*^T [n][ld] and the column partial  sum_j alpha_j k*_j
-//   MODE 1 (var):  C[n x m] = L^-1[n x n] * K*^T[n x m]   (lower triangular:
-//                  the K loop of row tile rt stops at (rt+1)*128)
-//                  epilogue: column partial  sum_c C[c][i]^2
-//                  (the library launches the persistent k_gp_var below for
-//                  this; MODE 1 of k_gp_gemm2 stays as its reference form)
-//
-// Tile 128 x 128 per 256-thread workgroup (2 x 2 waves of 64 x 64), K step 32,
-// global -> register prefetch of step t+1 while step t computes out of the
-// other LDS buffer (one barrier per step).  A (Xs / L^-1) is small and
-// L2/MALL resident; B (the candidate stream) is read along m with 16-byte
-// loads.  Row tiles of one candidate column tile are dispatched
-// consecutively inside one XCD group (blocks b, b+8, ... share an XCD) so the
-// B column tile is fetched from HBM once and re-read from that XCD's L2.
+//   k_gp_kstar:  C = (X/ell) (U/ell)^T, epilogue k* = sf2 exp(-0.5 max(|x|^2+|u|^2-2C, 0)),
+//                stores K*^T [n][ldk] and the column partial  sum_r alpha_r k*_r   (mean)
+//   k_gp_var:    V = L^-1 K*^T (L^-1 lower triangular: row tile rt stops its K
+//                loop at (rt+1)*128), epilogue column partial  sum_r V[r][c]^2   (variance)
 //
 //   fp64: v_mfma_f64_16x16x4_f64   (C/D: col = lane&15, row = (lane>>4) + 4r)
 //   fp32: v_mfma_f32_32x32x2_f32   (C/D: col = lane&31, row = (r&3) + 8(r>>2) + 4(lane>>5))
@@ -24,248 +13,206 @@
 
 namespace ut {
 
-typedef double gd4 __attribute__((ext_vector_type(4)));
-typedef float gf16 __attribute__((ext_vector_type(16)));
-
-constexpr int G_BM = 128, G_BN = 128, G_NT = 256;
-
-template <typename T>
-struct GCfg;
-template <>
-struct GCfg<double> {
-  static constexpr int BK = 16;          // 2 x 36 KB LDS buffers and ~200 VGPRs: 2 waves / SIMD
-  static constexpr int LDA = G_BM + 16;  // row stride (elements) of As[k][row]: 288 dwords = 32 mod 64 banks
-  static constexpr int LDB = G_BN + 16;
-};
-template <>
-struct GCfg<float> {
-  static constexpr int BK = 32;
-  static constexpr int LDA = G_BM + 4;
-  static constexpr int LDB = G_BN + 4;
-};
-
-template <typename T>
-__device__ __forceinline__ T to_t(double v) {
-  return (T)v;
+__global__ void k_to_f32(const double* __restrict__ src, float* __restrict__ dst, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) dst[i] = (float)src[i];
 }
 
-// T: MFMA operand/accumulate type; TS: type K* is stored in (MODE 0).
-template <typename T, int MODE, typename TS = T>
-__global__ __launch_bounds__(G_NT, 2) void k_gp_gemm2(
-    const T* __restrict__ A, int64_t lda, const void* __restrict__ Bv, int64_t ldb, int32_t K, int32_t RT,
-    int32_t CT, int64_t m,
-    // MODE 0
-    const double* __restrict__ inv_ell, const double* __restrict__ xnorm, const double* __restrict__ cnorm,
-    const double* __restrict__ alpha, double sf2, int32_t n, TS* __restrict__ kst, int64_t ldk,
-    // column partials [RT][ldp]
-    double* __restrict__ part, int64_t ldp) {
-  constexpr int G_BK = GCfg<T>::BK, LDA = GCfg<T>::LDA, LDB = GCfg<T>::LDB;
-  constexpr int PT = G_BK / 2;               // staged elements per thread for A and for B
-  __shared__ __attribute__((aligned(16))) T As[2][G_BK * LDA];
-  __shared__ __attribute__((aligned(16))) T Bs[2][G_BK * LDB];
+// ---------------------------------------------------------------------------
+// K* contraction, persistent:  C = Xs U'  (Xs = X/ell [n][d], U' = U/ell [d][m])
+//   k*[r][c] = sf2 exp(-0.5 max(|xs_r|^2 + |u'_c|^2 - 2 C[r][c], 0))  (0 outside n x m)
+//   stored as K*^T [r][ldk] (TS), plus the column partial sum_r alpha_r k*[r][c]
+// 256-thread workgroups (2 x 2 waves of 64 x 64) on 128 x 128 tiles, K = dpad
+// in steps of 16, a 2-stage glds ring (64 KiB) so TWO workgroups share a CU
+// and one's exp/store epilogue overlaps the other's MFMAs.  Work items are
+// handed out per XCD group like k_gp_var's.
+//   A = Xs^T [dpad][npad] (rows >= d zero), B = U' [dpad][ldk] (rows >= d and
+//   columns >= m zero; written by k_gp_prep_cand)
+// ---------------------------------------------------------------------------
+constexpr int K_NT = 256, K_BM = 128, K_BN = 128, K_BK = 16;
+constexpr int K_SA = K_BK * K_BM, K_SB = K_BK * K_BN, K_STAGE = K_SA + K_SB;
 
-  const int32_t b = blockIdx.x;
-  const int32_t xcd = b & 7, jj = b >> 3;
-  const int32_t rt = jj % RT;
-  const int32_t ct = (jj / RT) * 8 + xcd;
-  if (ct >= CT) return;
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+__device__ __forceinline__ void kstar_issue(const double* __restrict__ AT, int64_t lda, const double* __restrict__ B,
+                                            int64_t ldb, int32_t row0, int64_t col0, int32_t k0, double* st, int w,
+                                            int lane) {
+  // 16 KiB of A and 16 KiB of B per stage = 32 wave-instructions, 8 per wave
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int q = 4 * w + u;  // 0..15: A tile row k = q (128 doubles = 1 KiB)
+    const double* src = AT + (int64_t)(k0 + q) * lda + row0 + lane * 2;
+    __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(st + q * 128), 16, 0, 0);
+  }
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int q = 4 * w + u;
+    const double* src = B + (int64_t)(k0 + q) * ldb + col0 + lane * 2;
+    __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(st + K_SA + q * 128), 16, 0, 0);
+  }
+}
+
+template <typename TS>
+__global__ __launch_bounds__(K_NT, 2) void k_gp_kstar(const double* __restrict__ AT, int64_t lda,
+                                                      const double* __restrict__ B, int64_t ldb, int32_t dpad,
+                                                      int32_t RT, int32_t CT, const double* __restrict__ xnorm,
+                                                      const double* __restrict__ cnorm,
+                                                      const double* __restrict__ alpha, double sf2, int32_t n,
+                                                      int64_t m, int32_t* __restrict__ ticket, TS* __restrict__ kst,
+                                                      int64_t ldk, double* __restrict__ part) {
+  // one __shared__ object (see k_gp_var): the 2-stage ring, then the ticket slot
+  __shared__ __attribute__((aligned(16))) double lds[2 * K_STAGE + 2];
+  int32_t& s_item = *reinterpret_cast<int32_t*>(lds + 2 * K_STAGE);
+  const int t = threadIdx.x, lane = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
   const int wm = w >> 1, wn = w & 1;
-  const int64_t col0 = (int64_t)ct * G_BN;
-  const int32_t row0 = rt * G_BM;
-  const int32_t kmax = (MODE == 1) ? min(K, row0 + G_BM) : K;
-  const int32_t nk = (kmax + G_BK - 1) / G_BK;
+  const int32_t xcd = blockIdx.x & 7;
+  const int32_t nk = dpad / K_BK;
+  typedef double d4 __attribute__((ext_vector_type(4)));
 
-  // staging maps
-  const int ar = t >> 1, ak = (t & 1) * PT;   // A: row, first of PT k (2 threads per row)
-  constexpr int TPK = G_BN / PT;              // B: threads per k row
-  const int bk = t / TPK, bc = (t % TPK) * PT;
-  const bool bfull = (col0 + G_BN) <= m;      // MODE 0: whole column tile in range
+  for (;;) {
+    if (t == 0) s_item = atomicAdd(&ticket[xcd], 1);
+    __syncthreads();
+    const int32_t j = s_item;
+    const int32_t ct = (j / RT) * 8 + xcd;
+    if (ct >= CT) break;
+    const int32_t rt = j % RT;
+    const int64_t col0 = (int64_t)ct * K_BN;
+    const int32_t row0 = rt * K_BM;
 
-  T ra[PT], rb[PT];
-  auto load = [&](int32_t k0) {
-    // A
-    if (MODE == 1) {
-      const T* src = A + (int64_t)(row0 + ar) * lda + k0 + ak;
-#pragma unroll
-      for (int u = 0; u < PT; ++u) ra[u] = src[u];
-    } else {
-#pragma unroll
-      for (int u = 0; u < PT; ++u) {
-        const int32_t kk = k0 + ak + u;
-        ra[u] = (kk < K) ? A[(int64_t)(row0 + ar) * lda + kk] : (T)0;
-      }
-    }
-    // B
-    const int32_t kk = k0 + bk;
-    if (MODE == 1) {
-      const T* src = reinterpret_cast<const T*>(Bv) + (int64_t)kk * ldb + col0 + bc;
-#pragma unroll
-      for (int u = 0; u < PT; ++u) rb[u] = src[u];
-    } else {
-      const double* src = reinterpret_cast<const double*>(Bv) + (int64_t)kk * ldb + col0 + bc;
-      const double sc = (kk < K) ? inv_ell[kk] : 0.0;
-      if (kk < K && bfull) {
-#pragma unroll
-        for (int u = 0; u < PT; ++u) rb[u] = to_t<T>(src[u] * sc);
-      } else {
-#pragma unroll
-        for (int u = 0; u < PT; ++u) rb[u] = (kk < K && col0 + bc + u < m) ? to_t<T>(src[u] * sc) : (T)0;
-      }
-    }
-  };
-  auto store = [&](int buf) {
-#pragma unroll
-    for (int u = 0; u < PT; ++u) As[buf][(ak + u) * LDA + ar] = ra[u];
-#pragma unroll
-    for (int u = 0; u < PT; ++u) Bs[buf][bk * LDB + bc + u] = rb[u];
-  };
-
-  // accumulators: fp64 4x4 tiles of 16x16 (4 doubles), fp32 2x2 tiles of 32x32 (16 floats)
-  gd4 accd[4][4];
-  gf16 accf[2][2];
-  if constexpr (sizeof(T) == 8) {
+    d4 acc[4][4];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) accd[i][j] = (gd4){0.0, 0.0, 0.0, 0.0};
-  } else {
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) accf[i][j][r] = 0.0f;
-  }
+      for (int jj = 0; jj < 4; ++jj) acc[i][jj] = (d4){0.0, 0.0, 0.0, 0.0};
 
-  load(0);
-  store(0);
-  __syncthreads();
-  for (int32_t kt = 0; kt < nk; ++kt) {
-    const int buf = kt & 1;
-    if (kt + 1 < nk) load((kt + 1) * G_BK);
-    const T* as = As[buf];
-    const T* bs = Bs[buf];
-    if constexpr (sizeof(T) == 8) {
+    kstar_issue(AT, lda, B, ldb, row0, col0, 0, lds, w, lane);
+    for (int32_t kt = 0; kt < nk; ++kt) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();  // stage kt landed everywhere; stage kt-1 fully read
+      asm volatile("" ::: "memory");
+      if (kt + 1 < nk) kstar_issue(AT, lda, B, ldb, row0, col0, (kt + 1) * K_BK, lds + ((kt + 1) & 1) * K_STAGE, w, lane);
+      const double* as = lds + (kt & 1) * K_STAGE;
+      const double* bs = as + K_SA;
 #pragma unroll
-      for (int ks = 0; ks < G_BK / 4; ++ks) {
+      for (int ks = 0; ks < K_BK / 4; ++ks) {
         const int kr = ks * 4 + (lane >> 4);
         double af[4], bf[4];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) af[i] = as[kr * LDA + wm * 64 + i * 16 + (lane & 15)];
+        for (int i = 0; i < 4; ++i) af[i] = as[kr * K_BM + wm * 64 + i * 16 + (lane & 15)];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) bf[j] = bs[kr * LDB + wn * 64 + j * 16 + (lane & 15)];
+        for (int jj = 0; jj < 4; ++jj) bf[jj] = bs[kr * K_BN + wn * 64 + jj * 16 + (lane & 15)];
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
-          for (int j = 0; j < 4; ++j) accd[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[i], bf[j], accd[i][j], 0, 0, 0);
-      }
-    } else {
-#pragma unroll
-      for (int ks = 0; ks < G_BK / 2; ++ks) {
-        const int kr = ks * 2 + (lane >> 5);
-        float af[2], bf[2];
-#pragma unroll
-        for (int i = 0; i < 2; ++i) af[i] = as[kr * LDA + wm * 64 + i * 32 + (lane & 31)];
-#pragma unroll
-        for (int j = 0; j < 2; ++j) bf[j] = bs[kr * LDB + wn * 64 + j * 32 + (lane & 31)];
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-          for (int j = 0; j < 2; ++j) accf[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i], bf[j], accf[i][j], 0, 0, 0);
+          for (int jj = 0; jj < 4; ++jj)
+            acc[i][jj] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[i], bf[jj], acc[i][jj], 0, 0, 0);
       }
     }
-    if (kt + 1 < nk) store(buf ^ 1);
-    __syncthreads();
-  }
 
-  // ---- epilogue: per-column partial over this tile's 128 rows ----------------
-  double* red = reinterpret_cast<double*>(&As[0][0]);  // [2][128], reused after the final barrier
-  if constexpr (sizeof(T) == 8) {
+    __syncthreads();  // ring free: reuse as the column reduction buffer
+    double* red = lds;  // [2][128]
+    // operands of the epilogue loaded up front and unconditionally (rows < npad,
+    // columns < ldk are always in range): a load under a per-element condition
+    // makes hipcc wait vmcnt(0) per element
+    double xn[4][4], al[4][4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int cl = wn * 64 + j * 16 + (lane & 15);
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int32_t row = row0 + wm * 64 + i * 16 + (lane >> 4) + 4 * r;
+        xn[i][r] = xnorm[row];
+        al[i][r] = alpha[row];
+      }
+    double cn[4];
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) cn[jj] = cnorm[col0 + wn * 64 + jj * 16 + (lane & 15)];
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+      const int cl = wn * 64 + jj * 16 + (lane & 15);
       const int64_t col = col0 + cl;
+      const bool cin = col < m;
       double s = 0.0;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int32_t row = row0 + wm * 64 + i * 16 + (lane >> 4) + 4 * r;
-          const double x = accd[i][j][r];
-          if (MODE == 0) {
-            double ks = 0.0;
-            if (row < n && col < m) {
-              double d2 = xnorm[row] + cnorm[col] - 2.0 * x;
-              d2 = d2 > 0.0 ? d2 : 0.0;
-              ks = sf2 * exp(-0.5 * d2);
-            }
-            kst[(int64_t)row * ldk + col] = (TS)ks;
-            s += alpha[row] * ks;
-          } else {
-            s += x * x;
-          }
+          double d2 = xn[i][r] + cn[jj] - 2.0 * acc[i][jj][r];
+          d2 = d2 > 0.0 ? d2 : 0.0;
+          const double e = sf2 * exp(-0.5 * d2);
+          const double ks = (row < n && cin) ? e : 0.0;
+          kst[(int64_t)row * ldk + col] = (TS)ks;
+          s += al[i][r] * ks;
         }
       }
       s += __shfl_xor(s, 16);
       s += __shfl_xor(s, 32);
-      if ((lane >> 4) == 0) red[wm * G_BN + cl] = s;
+      if ((lane >> 4) == 0) red[wm * K_BN + cl] = s;
     }
-  } else {
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int cl = wn * 64 + j * 32 + (lane & 31);
-      const int64_t col = col0 + cl;
-      double s = 0.0;
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int32_t row = row0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-          const float x = accf[i][j][r];
-          if (MODE == 0) {
-            float ks = 0.0f;
-            if (row < n && col < m) {
-              double d2 = xnorm[row] + cnorm[col] - 2.0 * (double)x;
-              d2 = d2 > 0.0 ? d2 : 0.0;
-              ks = (float)sf2 * __expf(-0.5f * (float)d2);
-            }
-            kst[(int64_t)row * ldk + col] = (TS)ks;
-            s += alpha[row] * (double)ks;
-          } else {
-            s += (double)x * (double)x;
-          }
-        }
-      }
-      s += __shfl_xor(s, 32);
-      if ((lane >> 5) == 0) red[wm * G_BN + cl] = s;
+    __syncthreads();
+    if (t < K_BN) {
+      const int64_t col = col0 + t;
+      if (col < m) part[(int64_t)rt * ldk + col] = red[t] + red[K_BN + t];
     }
-  }
-  __syncthreads();
-  if (t < G_BN) {
-    const int64_t col = col0 + t;
-    if (col < m) part[(int64_t)rt * ldp + col] = red[t] + red[G_BN + t];
   }
 }
 
-__global__ void k_to_f32(const double* __restrict__ src, float* __restrict__ dst, int64_t n) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) dst[i] = (float)src[i];
-}
-
-int launch_gemm_kstar(ut_ctx* c, bool fp32, const void* A, int64_t lda, const double* feat, int64_t ldf, int32_t d,
-                      int32_t RT, int32_t CT, int64_t m, void* kst, int64_t ldk, double* part) {
-  const int32_t CT8 = ((CT + 7) / 8) * 8;
-  // fp32 mode: the small K* contraction stays fp64 (the |a|^2+|b|^2-2ab form
-  // cancels), only its output is stored as fp32 for the large var contraction
+int launch_gemm_kstar(ut_ctx* c, bool fp32, const double* XsT, int32_t npad, const double* ucand, int32_t dpad,
+                      int64_t m, void* kst, int64_t ldk, double* part) {
+  UT_CHECK(c, npad % K_BM == 0 && dpad % K_BK == 0 && ldk % K_BN == 0 && ldk >= m, UT_EINVAL,
+           "gemm_kstar: bad padding");
+  const int32_t RT = npad / K_BM;
+  const int32_t CT = (int32_t)(ldk / K_BN);  // every column of K* (zeros past m) is written
+  const int64_t items = (int64_t)RT * CT;
+  int32_t nb = 2 * (c->n_cu / 8) * 8;
+  if (items < nb) nb = (int32_t)(((items + 7) / 8) * 8);
+  UT_HIP(c, hipMemsetAsync(c->gp_ctr + 8, 0, sizeof(int32_t) * 8, c->stream));
   if (fp32)
-    hipLaunchKernelGGL((k_gp_gemm2<double, 0, float>), dim3(RT * CT8), dim3(G_NT), 0, c->stream, (const double*)A,
-                       lda, (const void*)feat, ldf, d, RT, CT, m, c->gp_inv_ell, c->gp_xnorm, c->cnorm.p, c->gp_alpha,
-                       c->gp_sf2, c->gp_n, (float*)kst, ldk, part, ldk);
+    hipLaunchKernelGGL(k_gp_kstar<float>, dim3(nb), dim3(K_NT), 0, c->stream, XsT, (int64_t)npad, ucand, ldk, dpad,
+                       RT, CT, c->gp_xnorm, c->cnorm.p, c->gp_alpha, c->gp_sf2, c->gp_n, m, c->gp_ctr + 8,
+                       (float*)kst, ldk, part);
   else
-    hipLaunchKernelGGL((k_gp_gemm2<double, 0>), dim3(RT * CT8), dim3(G_NT), 0, c->stream, (const double*)A, lda,
-                       (const void*)feat, ldf, d, RT, CT, m, c->gp_inv_ell, c->gp_xnorm, c->cnorm.p, c->gp_alpha,
-                       c->gp_sf2, c->gp_n, (double*)kst, ldk, part, ldk);
+    hipLaunchKernelGGL(k_gp_kstar<double>, dim3(nb), dim3(K_NT), 0, c->stream, XsT, (int64_t)npad, ucand, ldk, dpad,
+                       RT, CT, c->gp_xnorm, c->cnorm.p, c->gp_alpha, c->gp_sf2, c->gp_n, m, c->gp_ctr + 8,
+                       (double*)kst, ldk, part);
+  UT_LAUNCH_CHECK(c);
+  return 0;
+}
+
+// U'[k][i] = feat[k][i] / ell_k (0 for k >= d or i >= m), cnorm[i] = |u'_i|^2
+__global__ void k_gp_prep_cand(const double* __restrict__ feat, int64_t ld, int64_t m, int32_t d, int32_t dpad,
+                               const double* __restrict__ inv_ell, double* __restrict__ u, int64_t ldu,
+                               double* __restrict__ cn) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= ldu) return;
+  double s = 0.0;
+  for (int32_t k = 0; k < dpad; ++k) {
+    const double v = (k < d && i < m) ? feat[(int64_t)k * ld + i] * inv_ell[k] : 0.0;
+    u[(int64_t)k * ldu + i] = v;
+    s += v * v;
+  }
+  cn[i] = s;
+}
+
+int launch_prep_cand(ut_ctx* c, const double* feat, int64_t ld, int64_t m, int32_t d, int32_t dpad, double* u,
+                     int64_t ldu, double* cn) {
+  hipLaunchKernelGGL(k_gp_prep_cand, dim3(grid1(ldu, 256)), dim3(256), 0, c->stream, feat, ld, m, d, dpad,
+                     c->gp_inv_ell, u, ldu, cn);
+  UT_LAUNCH_CHECK(c);
+  return 0;
+}
+
+// Xs^T [dpad][npad] from Xs [npad][d] (rows >= d zero)
+__global__ void k_gp_xs_t(const double* __restrict__ Xs, int32_t npad, int32_t d, int32_t dpad,
+                          double* __restrict__ XsT) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (int64_t)dpad * npad) return;
+  const int32_t k = (int32_t)(e / npad), r = (int32_t)(e % npad);
+  XsT[e] = (k < d) ? Xs[(int64_t)r * d + k] : 0.0;
+}
+
+int launch_xs_t(ut_ctx* c, const double* Xs, int32_t npad, int32_t d, int32_t dpad, double* XsT) {
+  hipLaunchKernelGGL(k_gp_xs_t, dim3(grid1((int64_t)dpad * npad, 256)), dim3(256), 0, c->stream, Xs, npad, d, dpad,
+                     XsT);
   UT_LAUNCH_CHECK(c);
   return 0;
 }

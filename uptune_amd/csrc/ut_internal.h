@@ -114,8 +114,9 @@ struct ut_ctx {
   int32_t gp_fit_prec = 64;    // precision of the fitted factors used by scoring
   float* gp_Xs_f = nullptr;    // fp32 copies for the fp32 MFMA path
   double* gp_LinvT = nullptr;  // (L^-1)^T [k][row]: the A operand of the variance contraction
+  double* gp_XsT = nullptr;    // (X/ell)^T [dpad][npad]: the A operand of the K* contraction
   float* gp_LinvT_f = nullptr;
-  int32_t* gp_ctr = nullptr;   // [8] per-XCD tile tickets of the persistent variance kernel
+  int32_t* gp_ctr = nullptr;   // [16] per-XCD work tickets: [0,8) variance, [8,16) K*
   int32_t n_cu = 256;
   int64_t gp_cap_n = 0;
 
@@ -124,6 +125,7 @@ struct ut_ctx {
   ut::DevBuf<double> mu_part;    // [RT][ld]
   ut::DevBuf<double> var_part;   // [RT][ld]
   ut::DevBuf<double> cnorm;      // [ld]
+  ut::DevBuf<double> ucand;      // [dpad][ld] candidate features / ell (the K* B operand)
   ut::DevBuf<double> r_values, r_feat, r_mu, r_var, r_score;
   ut::DevBuf<uint32_t> r_digest;
   ut::DevBuf<uint8_t> r_dup;
@@ -198,8 +200,11 @@ int gp_score_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, const ut
                   double* mu, double* var, double* score);
 int topk_impl(ut_ctx* c, const double* score, const uint8_t* dup, int64_t m, int64_t cand_base, int32_t k,
               int64_t* out_idx, double* out_score);
-int launch_gemm_kstar(ut_ctx* c, bool fp32, const void* A, int64_t lda, const double* feat, int64_t ldf, int32_t d,
-                      int32_t RT, int32_t CT, int64_t m, void* kst, int64_t ldk, double* part);
+int launch_gemm_kstar(ut_ctx* c, bool fp32, const double* XsT, int32_t npad, const double* ucand, int32_t dpad,
+                      int64_t m, void* kst, int64_t ldk, double* part);
+int launch_prep_cand(ut_ctx* c, const double* feat, int64_t ld, int64_t m, int32_t d, int32_t dpad, double* u,
+                     int64_t ldu, double* cn);
+int launch_xs_t(ut_ctx* c, const double* Xs, int32_t npad, int32_t d, int32_t dpad, double* XsT);
 int launch_gemm_var(ut_ctx* c, bool fp32, const void* LinvT, int64_t lda, const void* kst, int64_t ldk, int32_t npad,
                     int64_t m, double* part);
 int launch_transpose(ut_ctx* c, const double* src, int32_t n, double* dst, float* dst_f);
