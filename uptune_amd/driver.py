@@ -115,29 +115,12 @@ class SearchDriver:
     def best_configuration(self):
         return None if self.best_result is None else self.best_result.configuration
 
-    def training_set(self, spec):
-        """(X unit-space features [n][d], y standardised-ready times) of every result"""
+    def training_configs(self):
+        """(configurations, times) of every result, in arrival order"""
         keys = list(self.results)
-        if not keys:
-            return np.zeros((0, spec.n_features)), np.zeros(0)
         cfgs = [self.results[k].configuration for k in keys]
         y = np.array([self.results[k].time for k in keys], dtype=np.float64)
-        return self._features(spec, cfgs), y
-
-    def _features(self, spec, cfgs):
-        tech = self._any_engine()
-        import torch
-        vals = torch.from_numpy(spec.encode_configs(cfgs)).to(tech.device)
-        return tech.encode(vals).T.contiguous().cpu().numpy()
-
-    def _any_engine(self):
-        stack = [self.root_technique]
-        while stack:
-            t = stack.pop()
-            if getattr(t, "engine", None) is not None:
-                return t.engine
-            stack.extend(getattr(t, "techniques", []))
-        raise RuntimeError("no device engine available for feature encoding")
+        return cfgs, y
 
     def population_result(self, tech, idx) -> Optional[Result]:
         return self._pop_results.get((tech.name, idx))

@@ -171,6 +171,13 @@ class BatchEngine:
                 "ut_encode_features")
         return feat
 
+    def features_host(self, cfgs: Sequence[Dict[Any, Any]]) -> np.ndarray:
+        """configs -> GP features [n][F] (host f64), encoded on the device"""
+        if not len(cfgs):
+            return np.zeros((0, self.spec.n_features))
+        vals = torch.from_numpy(self.spec.encode_configs(cfgs)).to(self.device)
+        return self.encode(vals).T.contiguous().cpu().numpy()
+
     # -- identity / dedup --------------------------------------------------
     def hash(self, values: torch.Tensor, m: Optional[int] = None) -> torch.Tensor:
         m = values.shape[1] if m is None else m

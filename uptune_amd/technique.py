@@ -317,9 +317,10 @@ class GpuBatchTechnique(SearchTechnique):
             self._hist_seen = len(seen)
 
     def _fit(self) -> bool:
-        X, y = self.driver.training_set(self.engine.spec)
+        cfgs, y = self.driver.training_configs()
         if len(y) < self.min_train:
             return False
+        X = self.engine.features_host(cfgs)
         self.engine.gp_fit(X, y, lengthscale=self.lengthscale, sigma_f2=1.0, sigma_n2=1e-6, jitter=1e-8)
         return True
 
