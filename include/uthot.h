@@ -57,8 +57,8 @@ enum {
 enum {
   UT_FLOAT = 0,  /* FloatParameter        manipulator.py:703-744 */
   UT_INT = 1,    /* IntegerParameter      manipulator.py:651-700 */
-  UT_LOGINT = 2, /* LogIntegerParameter   manipulator.py:781-797 */
-  UT_POW2 = 3,   /* PowerOfTwoParameter   manipulator.py:813-836 */
+  UT_LOGINT = 2, /* LogIntegerParameter   manipulator.py:778-797 (stored int, searched log2) */
+  UT_POW2 = 3,   /* PowerOfTwoParameter   manipulator.py:811-836 (stored 2^e, searched e) */
   UT_BOOL = 4,   /* BooleanParameter      manipulator.py:930-996 */
   UT_ENUM = 5,   /* EnumParameter         manipulator.py:1024-1045 */
   UT_PERM = 6    /* PermutationParameter  manipulator.py:1048-1356 (not yet) */
@@ -67,17 +67,24 @@ enum {
 typedef struct ut_param_desc {
   int32_t kind;        /* UT_* kind */
   int32_t sort_rank;   /* position in sorted(params, key=name)  (manipulator.py:237) */
-  double lo, hi;       /* legal_range of the stored value (min_value, max_value) */
-  double u_lo, u_hi;   /* unit-encoding bounds as Python computes them
-                          (ints widened by 0.4999, manipulator.py:476-479) */
+  double lo, hi;       /* min_value, max_value of the STORED value (POW2: powers of two) */
+  double u_lo, u_hi;   /* unit-encoding bounds of the SEARCHED value (get_value) as Python
+                          computes them: ints widened by 0.4999 (manipulator.py:476-479);
+                          LOGINT: its scaled legal_range (:792-795); POW2: exponents -+0.4999 */
   double u_span;       /* float(u_hi - u_lo) as Python computes it */
   int64_t n_options;   /* ENUM option count (BOOL: 2) */
   const char* name;    /* str(p.name) bytes, not NUL-terminated */
   int32_t name_len;
-  int32_t lut_count;   /* >0: inner digests of repr(value_i) supplied in lut */
-  const uint8_t* lut_host; /* lut_count * 32 bytes: sha256(repr(value)).digest(),
-                              indexed by (value - lo) for INT, option index for
+  int32_t lut_count;   /* >0: inner digests of repr(get_value) supplied in lut */
+  const uint8_t* lut_host; /* lut_count * 32 bytes: sha256(repr(get_value)).digest(),
+                              indexed by (value - lo) for INT and LOGINT, by
+                              (exponent - log2 lo) for POW2, by option index for
                               ENUM, 0=False/1=True for BOOL */
+  int32_t vtab_count;  /* LOGINT: >0 = get_value(v) = math.log(v + 1.0 - min, 2.0) for
+                          v = lo .. lo+vtab_count-1, computed by the host's CPython;
+                          0 = computed on the device (correctly rounded log) */
+  int32_t pad;
+  const double* vtab_host;
 } ut_param_desc;
 
 typedef struct ut_de_params {   /* differentialevolution.py:34-40,142-151 */

@@ -17,12 +17,14 @@ which both are plain hex (pinned by samples/tutorials/tuneup.opentuner.db).
 """
 import hashlib
 
-from .space import BOOL, ENUM, FLOAT, INT
+from .space import BOOL, ENUM, FLOAT, scale
 
 
 def hash_value(p, v, py2=False):
     if p.is_primitive():
-        gv = float(v) if p.kind == FLOAT else int(v)
+        # repr(self.get_value(config)): LOGINT hashes its log-scale float,
+        # POW2 its integer exponent (ScaledNumericParameter.get_value :769-770)
+        gv = scale(p, float(v) if p.kind == FLOAT else int(v))
         inner = hashlib.sha256(repr(gv).encode("utf-8")).hexdigest().encode()
         return inner.decode() if py2 else str(inner)
     if p.kind == BOOL:

@@ -6,8 +6,9 @@ HybridParticle.move calls, for every param,
     op3_swarm(position, global_best, self.best, c=omega, c1=phi_g, c2=phi_l, velocity=v)
 so with cfg = x, cfg1 = g, cfg2 = l:
     v' = v*c + (g - x)*c1*r1 + (l - x)*c2*r2            (draw order r1, r2)
-  Float:  x' = min(vmax, max(x + v', vmin))
+  Float:  x' = min(vmax, max(x + v', vmin))          (LogInt: on log values, then _unscale)
   Int:    s = k / (1 + exp(-v')) + vmin,  p ~ N(s, (sigma k)^2),  x' = int(min(vmax, max(round(p), vmin)))
+          (PowerOfTwo: on exponents, then 2 ** x')
   Bool:   s = 1 / (1 + exp(-v')),  x' = (s - U) > 0
   Enum:   opn_stochastic_mix(cfg, [cfg, g, l], [c, c1, c2]) copies FROM the particle
           INTO the drawn parent (manipulator.py:442) -> the particle's
@@ -25,7 +26,7 @@ import numpy as np
 
 from . import philox as ph
 from .mathx import normal_draw, ut_exp
-from .space import BOOL, ENUM, FLOAT, INT
+from .space import BOOL, ENUM, FLOAT, INT, LOGINT, POW2, scale_vec, unscale_vec
 
 
 def propose_pso_vec(space, pos, vel, pbest, gbest, seed, round_, cand_base, m, omega=0.5, phi_l=0.5, phi_g=0.5,
@@ -37,10 +38,13 @@ def propose_pso_vec(space, pos, vel, pbest, gbest, seed, round_, cand_base, m, o
     out_v = np.empty((P, m))
     c, c1, c2 = omega, phi_g, phi_l
     for p, prm in enumerate(space):
-        x = pos[p, t]
+        # scaled kinds move in their search scale (get_value/set_value):
+        # LOGINT by the Float rule on log values, POW2 by the Int rule on exponents
+        x = scale_vec(prm, pos[p, t])
         v = vel[p, t]
-        lb = pbest[p, t]
-        gb = gbest[p]
+        lb = scale_vec(prm, pbest[p, t])
+        gb = float(scale_vec(prm, np.array([gbest[p]]))[0])
+        vmin, vmax = (float(b) for b in prm.legal_range()) if prm.is_primitive() else (0.0, 0.0)
         r = ph.draw(seed, g, p, round_, ph.OP_PSO)
         r1, r2 = ph.u01(r[0], r[1]), ph.u01(r[2], r[3])
         if prm.kind == ENUM:
@@ -55,17 +59,17 @@ def propose_pso_vec(space, pos, vel, pbest, gbest, seed, round_, cand_base, m, o
                 nx = x
         else:
             nv = ((v * c) + (((gb - x) * c1) * r1)) + (((lb - x) * c2) * r2)
-            if prm.kind == FLOAT:
+            if prm.kind in (FLOAT, LOGINT):
                 y = x + nv
-                y = np.where(prm.lo > y, prm.lo, y)       # max(p, vmin)
-                nx = np.where(y < prm.hi, y, prm.hi)      # min(vmax, .)
-            elif prm.kind == INT:
-                k = float(prm.hi - prm.lo)
-                s = k / (1.0 + ut_exp(-nv)) + prm.lo
+                y = np.where(vmin > y, vmin, y)           # max(p, vmin)
+                nx = unscale_vec(prm, np.where(y < vmax, y, vmax))   # min(vmax, .); set_value
+            elif prm.kind in (INT, POW2):
+                k = vmax - vmin
+                s = k / (1.0 + ut_exp(-nv)) + vmin
                 z = normal_draw(seed, g, p | (2 << ph.STREAM_SUB_SHIFT), round_, ph.OP_PSO)
                 pp = np.rint(s + z * (sigma * k))
-                pp = np.where(prm.lo > pp, float(prm.lo), pp)
-                nx = np.where(pp < prm.hi, pp, float(prm.hi))
+                pp = np.where(vmin > pp, vmin, pp)
+                nx = unscale_vec(prm, np.where(pp < vmax, pp, vmax))
             elif prm.kind == BOOL:
                 s = 1.0 / (1.0 + ut_exp(-nv))
                 q = ph.draw(seed, g, p | (1 << ph.STREAM_SUB_SHIFT), round_, ph.OP_PSO)

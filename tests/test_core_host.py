@@ -96,3 +96,54 @@ def test_philox_matches_oracle(hc):
         hc.uthc_philox(seed, cand, stream, rnd, op, out)
         want = ph.draw(seed, np.array([cand], dtype=np.uint64), stream, rnd, op)
         assert list(out) == [int(w[0]) for w in want]
+
+
+def _batch(lib, name, xs):
+    fn = getattr(lib, name)
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_longlong]
+    x = np.ascontiguousarray(xs, dtype=np.float64)
+    out = np.empty_like(x)
+    fn(x.ctypes.data, out.ctypes.data, x.size)
+    return out
+
+
+def test_py_log2_correctly_rounded(hc):
+    """log_cr / py_log2 (math.log(x, 2.0) = log(x) / log(2.0)) are correctly
+    rounded: checked against 80-digit Decimal on integer and random arguments.
+    (CPython's libm log is not: it differs from the correctly rounded value on
+    ~2e-5 of integer arguments on this host, which is why LogInteger digests
+    and log values come from host tables computed by CPython itself -- see
+    uptune_amd/manipulator.py LOGINT_TABLE_MAX.)"""
+    from decimal import Decimal, getcontext
+    getcontext().prec = 80
+    rng = random.Random(7)
+    xs = [0.5001, 1.4999, 2.4999, 1e6 + 0.4999, 2.0 ** 40 + 3, 2.0 ** 52 - 1, 9170.0, 136837.0, 277862.0] + \
+         [float(rng.randrange(1, 1 << 24)) for _ in range(5000)] + [rng.uniform(0.5, 1e12) for _ in range(5000)]
+    got = _batch(hc, "uthc_py_log2", xs)
+    ln2 = math.log(2.0)
+    for x, g in zip(xs, got):
+        want = float(Decimal(x).ln()) / ln2
+        assert g == want, (x, g, want)
+
+
+def test_logint_unscale_matches_cpython(hc):
+    """LogIntegerParameter._unscale int(round(2.0 ** v - 1.0 + min))
+    (manipulator.py:787-790): the device's correctly rounded 2^v gives the same
+    stored integer as CPython's pow on every argument tried"""
+    rng = random.Random(8)
+    for mn, mx in ((1.0, 1024.0), (0.0, 1e6), (5.0, 3e9), (1.0, 2.0 ** 40)):
+        lo = math.log(mn - 0.4999 + 1.0 - mn, 2.0)
+        hi = math.log(mx + 0.4999 + 1.0 - mn, 2.0)
+        xs = np.array([rng.uniform(lo, hi) for _ in range(100000)] + [lo, hi])
+        got = _batch_unscale(hc, xs, mn)
+        want = np.array([float(int(round(2.0 ** float(x) - 1.0 + mn))) for x in xs])
+        assert np.array_equal(got, want)
+
+
+def _batch_unscale(lib, xs, mn):
+    fn = lib.uthc_logint_unscale
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_double, ctypes.c_void_p, ctypes.c_longlong]
+    x = np.ascontiguousarray(xs, dtype=np.float64)
+    out = np.empty_like(x)
+    fn(x.ctypes.data, mn, out.ctypes.data, x.size)
+    return out

@@ -29,20 +29,7 @@ def _require_gpu():
         pytest.skip("no GPU")
 
 
-def to_manip(space):
-    from uptune_amd.manipulator import (BooleanParameter, ConfigurationManipulator, EnumParameter, FloatParameter,
-                                        IntegerParameter)
-    m = ConfigurationManipulator()
-    for p in space:
-        if p.kind == FLOAT:
-            m.add_parameter(FloatParameter(p.name, p.lo, p.hi))
-        elif p.kind == INT:
-            m.add_parameter(IntegerParameter(p.name, p.lo, p.hi))
-        elif p.kind == BOOL:
-            m.add_parameter(BooleanParameter(p.name))
-        elif p.kind == ENUM:
-            m.add_parameter(EnumParameter(p.name, p.options))
-    return m
+from _spaces import oracle_space, to_manip  # noqa: E402
 
 
 def engine(space, seed=0, py2=False):
@@ -412,3 +399,74 @@ def test_ga_retry_gives_up_on_tiny_space():
     assert inv.cpu().numpy().all()
     _, winv = oga.propose_ga_vec(space, np.array([5.0, 0.0]), None, 1, 0, 0, 100, mutation_rate=0.5)
     assert winv.all()
+
+
+# --------------------------------------------------------------------------- scaled kinds (C3 HPL-64)
+def hpl_space():
+    from uptune_amd import spaces
+    return oracle_space(spaces.hpl64())
+
+
+def _libm_log_is_cr(x):
+    """True when CPython's math.log(x) is the correctly rounded log (the
+    device's LogInteger log is; glibc's is not on ~2e-5 of arguments)"""
+    import math
+    from decimal import Decimal, getcontext
+    getcontext().prec = 60
+    return math.log(x) == float(Decimal(x).ln())
+
+
+def test_hpl_population_de_encode_hash():
+    space = hpl_space()
+    e = engine(space, seed=13)
+    e.population_init(4000, round_=1)
+    pop = e.population_get().cpu().numpy()
+    np.testing.assert_array_equal(pop, ode.population_init(space, 4000, seed=13, round_=1))
+    got = e.propose_de(6000, round_=3, cand_base=77, cr=0.5, n_cross=2).cpu().numpy()
+    want = ode.propose_de_vec(space, pop, 13, 3, 77, 6000, 0.5, 2)
+    np.testing.assert_array_equal(got, want)
+    np.testing.assert_array_equal(e.encode(dev(got)).cpu().numpy(), features(space, got))
+    # hashes: bit-exact, except where the large-range LogInteger (device log)
+    # meets one of libm's non-correctly-rounded logs
+    li3 = [i for i, p in enumerate(space) if p.name == "logint_3"][0]
+    hx = hexes(e.hash(dev(got)))
+    want_h = oracle_hashes(space, got)
+    bad = [j for j in range(got.shape[1]) if hx[j] != want_h[j]]
+    for j in bad:
+        assert not _libm_log_is_cr(got[li3, j] + 1.0 - 0.0), j
+    assert len(bad) <= 2
+
+
+@pytest.mark.parametrize("alias,enum_mode", [(True, 0), (False, 1)])
+def test_hpl_pso_matches_oracle(alias, enum_mode):
+    from oracle import pso as opso
+    space = hpl_space()
+    e = engine(space, seed=17)
+    pop = ode.population_init(space, 900, seed=3)
+    e.population_set(dev(pop))
+    e.pso_reset()
+    gbest = pop[:, 5].copy()
+    x, v = e.propose_pso(gbest, 900, round_=2, alias_pbest=alias, enum_mode=enum_mode)
+    wx, wv = opso.propose_pso_vec(space, pop, np.zeros_like(pop), pop, gbest, 17, 2, 0, 900, enum_mode=enum_mode)
+    np.testing.assert_array_equal(x.cpu().numpy(), wx)
+    np.testing.assert_array_equal(v.cpu().numpy(), wv)
+    e.pso_commit(x, v)
+    x2, v2 = e.propose_pso(gbest, 900, round_=3, alias_pbest=alias, enum_mode=enum_mode)
+    wx2, wv2 = opso.propose_pso_vec(space, wx, wv, wx if alias else pop, gbest, 17, 3, 0, 900, enum_mode=enum_mode)
+    np.testing.assert_array_equal(x2.cpu().numpy(), wx2)
+    np.testing.assert_array_equal(v2.cpu().numpy(), wv2)
+
+
+@pytest.mark.parametrize("kw", [dict(mutation_rate=0.2), dict(mutation_rate=0.3, normal=True, sigma=0.1),
+                                dict(mutation_rate=0.1, normal=True, crossover_rate=0.5, crossover_strength=0.2,
+                                     op=5)])
+def test_hpl_ga_matches_oracle(kw):
+    from oracle import ga as oga
+    space = hpl_space()
+    e = engine(space, seed=19)
+    pop = ode.population_init(space, 4, seed=2)
+    for p1, p2 in [(pop[:, 0].copy(), None), (None, None), (pop[:, 0].copy(), pop[:, 1].copy())]:
+        got, inv = e.propose_ga(2000, parent1=p1, parent2=p2, round_=1, cand_base=3, **kw)
+        want, winv = oga.propose_ga_vec(space, p1, p2, 19, 1, 3, 2000, **kw)
+        np.testing.assert_array_equal(got.cpu().numpy(), want)
+        np.testing.assert_array_equal(inv.cpu().numpy().astype(bool), winv)

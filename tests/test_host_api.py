@@ -41,10 +41,13 @@ def test_ctx_create_fails_loudly_without_gpu():
 
 
 def test_struct_layouts():
-    assert ctypes.sizeof(L.ParamDesc) == 80
-    assert ctypes.sizeof(L.GpHyper) == 32 and ctypes.sizeof(L.RoundOut) == 32
-    assert ctypes.sizeof(L.DeParams) == 16
-    assert ctypes.sizeof(L.Acq) == 24
+    """ctypes mirrors == the C compiler's layout of include/uthot.h (host build)"""
+    import os
+    hc = ctypes.CDLL(os.path.join(os.path.dirname(L.LIB_PATH), "libuthot_hostcheck.so"))
+    hc.uthc_sizeof.restype = ctypes.c_longlong
+    for i, st in enumerate([L.ParamDesc, L.GpHyper, L.RoundOut, L.DeParams, L.Acq, L.PsoParams, L.GaParams]):
+        assert ctypes.sizeof(st) == hc.uthc_sizeof(i), st.__name__
+    assert ctypes.sizeof(L.ParamDesc) == 96
 
 
 def test_compile_space_mixed():
@@ -87,3 +90,28 @@ def test_duck_typed_reference_like_params():
 
     spec = compile_space([IntegerParameter("BLOCK_SIZE", 1, 10)])
     assert spec.params[0].kind == L.UT_INT and spec.params[0].lo == 1.0
+
+
+def test_compile_space_scaled_kinds():
+    """LogInteger / PowerOfTwo descriptors carry the reference's legal ranges
+    (manipulator.py:792-795, :829-830) and host-computed CPython tables"""
+    import math
+    from uptune_amd import spaces
+    from uptune_amd import _lib as L
+    from uptune_amd.manipulator import LOGINT_TABLE_MAX, compile_space, to_descs
+    spec = compile_space(spaces.hpl64())
+    assert spec.P == 64
+    by = {ps.name: ps for ps in spec.params}
+    li = by["logint_2"]
+    assert li.kind == L.UT_LOGINT and (li.lo, li.hi) == (16.0, 65536.0)
+    assert li.u_lo == math.log(16.0 - 0.4999 + 1.0 - 16.0, 2.0)
+    assert li.u_hi == math.log(65536.0 + 0.4999 + 1.0 - 16.0, 2.0)
+    assert li.vtab.size == 65536 - 16 + 1 and li.vtab[5] == math.log(21 + 1.0 - 16.0, 2.0)
+    assert len(li.lut) == 32 * li.vtab.size
+    assert by["logint_3"].vtab is None and (1 << 30) + 1 > LOGINT_TABLE_MAX    # device log
+    p2 = by["pow2_1"]
+    assert p2.kind == L.UT_POW2 and (p2.u_lo, p2.u_hi) == (4 - 0.4999, 20 + 0.4999) and len(p2.lut) == 32 * 17
+    arr, keep = to_descs(spec)
+    assert arr[[i for i, ps in enumerate(spec.params) if ps.name == "logint_2"][0]].vtab_count == 65521
+    cfg = {"pow2_1": 1 << 9, "logint_2": 300}
+    assert by["pow2_1"].to_value(cfg["pow2_1"]) == 512.0 and by["logint_2"].from_value(300.0) == 300

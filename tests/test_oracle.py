@@ -163,3 +163,59 @@ def test_topk_and_dedup_semantics():
     assert osel.topk(s, 3, dup=[0, 1, 0, 0, 0, 0]) == [2, 5, 0]
     assert osel.topk(s, 8, cand_base=10)[-2:] == [-1, -1]
     assert osel.dedup(["a", "b", "a", "c"], history={"c"}) == [0, 0, 1, 1]
+
+
+# ---------------------------------------------------------------- scaled kinds
+def _scaled_space():
+    from oracle.space import LOGINT, POW2
+    return [Param("li", LOGINT, 1, 1000), Param("li0", LOGINT, 0, 1 << 30), Param("p2", POW2, 1, 1 << 20),
+            Param("x", FLOAT, -5.0, 5.0), Param("p2s", POW2, 256, 256), Param("n", INT, -3, 40)]
+
+
+def test_logint_pow2_reference_semantics():
+    """get_value / legal_range / unit round trip of LogIntegerParameter and
+    PowerOfTwoParameter (manipulator.py:778-836), written out from the source"""
+    import math
+    from oracle.space import LOGINT, POW2, scale
+    li = Param("li", LOGINT, 1, 1000)
+    lo, hi = li.legal_range()
+    assert lo == math.log(1.0 - 0.4999 + 1.0 - 1.0, 2.0) and hi == math.log(1000.0 + 0.4999 + 1.0 - 1.0, 2.0)
+    for v in range(1, 1001):
+        assert scale(li, v) == math.log(v + 1.0 - 1.0, 2.0)
+        assert set_unit_value(li, get_unit_value(li, v), None) == v
+    p2 = Param("p2", POW2, 1, 1 << 20)
+    assert p2.legal_range() == (0, 20)
+    for e in range(21):
+        assert scale(p2, 1 << e) == e
+        assert set_unit_value(p2, get_unit_value(p2, 1 << e), None) == 1 << e
+    # hash_value = sha256(repr(get_value)): a float for LogInteger, the exponent for PowerOfTwo
+    h = hashlib.sha256(repr(math.log(7 + 1.0 - 1.0, 2.0)).encode()).hexdigest().encode()
+    assert oh.hash_value(li, 7, py2=True) == h.decode()
+    assert oh.hash_value(p2, 1 << 13, py2=True) == hashlib.sha256(b"13").hexdigest()
+
+
+def test_scaled_kinds_de_scalar_equals_vectorised():
+    space = _scaled_space()
+    pop = ode.population_init(space, 32, seed=5)
+    trial = ode.propose_de_vec(space, pop, seed=5, round_=2, cand_base=9, m=64, cr=0.7, n_cross=1)
+    pop_cfgs = [[from_f64(p, pop[j, i]) for j, p in enumerate(space)] for i in range(32)]
+    for i in range(64):
+        cfg = ode.propose_de_scalar(space, pop_cfgs, 5, 2, 9 + i, 0.7, 1)
+        assert [from_f64(p, trial[j, i]) for j, p in enumerate(space)] == cfg
+    # stored values stay legal: ints in range, powers of two
+    assert np.all((trial[0] >= 1) & (trial[0] <= 1000)) and np.all(trial[0] == np.round(trial[0]))
+    assert np.all(np.frexp(trial[2])[0] == 0.5) and np.all(trial[4] == 256.0)
+
+
+def test_scaled_kinds_pso_ga_legal():
+    from oracle import ga as oga
+    from oracle import pso as opso
+    space = _scaled_space()
+    pop = ode.population_init(space, 64, seed=6)
+    x, v = opso.propose_pso_vec(space, pop, np.zeros_like(pop), pop, pop[:, 3], seed=6, round_=1, cand_base=0, m=64)
+    y, inv = oga.propose_ga_vec(space, pop[:, 0], None, seed=6, round_=1, cand_base=0, m=64, mutation_rate=0.3,
+                                normal=True)
+    for out in (x, y):
+        assert np.all((out[0] >= 1) & (out[0] <= 1000)) and np.all(out[0] == np.round(out[0]))
+        assert np.all((out[1] >= 0) & (out[1] <= 1 << 30))
+        assert np.all(np.frexp(out[2])[0] == 0.5) and np.all((out[2] >= 1) & (out[2] <= 1 << 20))

@@ -29,6 +29,7 @@ class ParamDesc(C.Structure):
         ("n_options", C.c_int64),
         ("name", C.c_char_p), ("name_len", C.c_int32),
         ("lut_count", C.c_int32), ("lut_host", C.c_void_p),
+        ("vtab_count", C.c_int32), ("pad", C.c_int32), ("vtab_host", C.c_void_p),
     ]
 
 

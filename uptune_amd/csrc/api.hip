@@ -1,6 +1,7 @@
 // api.hip -- C ABI entry points (include/uthot.h) and the host-side space
 // compiler.
 #include <algorithm>
+#include <cmath>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -49,6 +50,7 @@ static void free_space(Space& s) {
   if (s.d_words) hipFree(s.d_words);
   if (s.d_block_last) hipFree(s.d_block_last);
   if (s.d_lut) hipFree(s.d_lut);
+  if (s.d_vtab) hipFree(s.d_vtab);
   s = Space();
 }
 
@@ -206,6 +208,7 @@ int ut_space_define(ut_ctx* c, int32_t P, const ut_param_desc* params, int32_t p
   std::vector<std::string> names(P);
   std::vector<bool> primitive(P);
   std::vector<uint32_t> lut;
+  std::vector<double> vtab;
   int32_t feat = 0;
   for (int32_t p = 0; p < P; ++p) {
     const ut_param_desc& d = params[p];
@@ -215,13 +218,25 @@ int ut_space_define(ut_ctx* c, int32_t P, const ut_param_desc* params, int32_t p
     q.u_lo = d.u_lo; q.u_hi = d.u_hi; q.u_span = d.u_span;
     q.n_opt = d.n_options;
     q.feat_col = feat;
+    q.vtab_base = 0;
+    q.vtab_n = 0;
     UT_CHECK(c, d.sort_rank >= 0 && d.sort_rank < P && s.host_order[d.sort_rank] == -1, UT_EINVAL,
              "space: sort_rank must be a permutation of 0..P-1");
     s.host_order[d.sort_rank] = p;
     names[p] = std::string(d.name ? d.name : "", d.name ? (size_t)d.name_len : 0);
     switch (d.kind) {
-      case UT_FLOAT: case UT_INT:
+      case UT_FLOAT: case UT_INT: case UT_LOGINT:
         q.n_feat = 1; primitive[p] = true; break;
+      case UT_POW2: {
+        // searched by exponent: legal_range = (log2 min, log2 max)  (manipulator.py:829-830)
+        UT_CHECK(c, d.lo >= 1.0 && d.hi >= d.lo && d.hi <= 0x1p1023, UT_EINVAL, "space: bad PowerOfTwo range");
+        int elo = 0, ehi = 0;
+        UT_CHECK(c, frexp(d.lo, &elo) == 0.5 && frexp(d.hi, &ehi) == 0.5, UT_EINVAL,
+                 "space: PowerOfTwo bounds must be powers of two");
+        q.lo = (double)(elo - 1);
+        q.hi = (double)(ehi - 1);
+        q.n_feat = 1; primitive[p] = true; break;
+      }
       case UT_BOOL:
         q.n_feat = 1; primitive[p] = false; q.n_opt = 2; break;
       case UT_ENUM:
@@ -232,6 +247,12 @@ int ut_space_define(ut_ctx* c, int32_t P, const ut_param_desc* params, int32_t p
                                                " is not supported on the device path yet");
     }
     feat += q.n_feat;
+    if (d.kind == UT_LOGINT && d.vtab_count > 0) {
+      UT_CHECK(c, d.vtab_host != nullptr, UT_EINVAL, "space: vtab_count > 0 but vtab_host is NULL");
+      q.vtab_base = (int64_t)vtab.size();
+      q.vtab_n = d.vtab_count;
+      vtab.insert(vtab.end(), d.vtab_host, d.vtab_host + d.vtab_count);
+    }
     if (d.lut_count > 0) {
       UT_CHECK(c, d.lut_host != nullptr, UT_EINVAL, "space: lut_count > 0 but lut_host is NULL");
       q.hash_mode = HM_LUT;
@@ -247,7 +268,8 @@ int ut_space_define(ut_ctx* c, int32_t P, const ut_param_desc* params, int32_t p
       q.lut_n = 0;
       if (d.kind == UT_FLOAT) q.hash_mode = HM_FLOAT;
       else if (d.kind == UT_INT) q.hash_mode = HM_INT;
-      else return set_err(c, UT_EINVAL, "space: BOOL/ENUM parameters need an inner-digest LUT");
+      else if (d.kind == UT_LOGINT) q.hash_mode = HM_LOGINT;
+      else return set_err(c, UT_EINVAL, "space: BOOL/ENUM/POW2 parameters need an inner-digest LUT");
     }
   }
   s.n_feat = feat;
@@ -258,6 +280,9 @@ int ut_space_define(ut_ctx* c, int32_t P, const ut_param_desc* params, int32_t p
   if (lut.empty()) lut.resize(8, 0u);
   UT_HIP(c, hipMalloc((void**)&s.d_lut, sizeof(uint32_t) * lut.size()));
   UT_HIP(c, hipMemcpy(s.d_lut, lut.data(), sizeof(uint32_t) * lut.size(), hipMemcpyHostToDevice));
+  if (vtab.empty()) vtab.resize(1, 0.0);
+  UT_HIP(c, hipMalloc((void**)&s.d_vtab, sizeof(double) * vtab.size()));
+  UT_HIP(c, hipMemcpy(s.d_vtab, vtab.data(), sizeof(double) * vtab.size(), hipMemcpyHostToDevice));
   int rc = compile_hash_layout(c, names, primitive);
   if (rc) return rc;
   c->has_space = true;

@@ -14,10 +14,11 @@
 // outer SHA-256 blocks word by word, producing each parameter's inner digest
 // just before its hole is first needed.
 //
-// Inner digests: discrete values (ENUM, BOOL, small-range INT) come from a
-// host-built LUT; FLOAT values are formatted on the device with Python's
-// shortest round-trip repr (ut_core.h) and hashed (one SHA-256 block);
-// large-range INT values use repr(int).
+// Inner digests: discrete values (ENUM, BOOL, POW2 exponents, small-range
+// INT and LOGINT) come from a host-built LUT; FLOAT values are formatted on
+// the device with Python's shortest round-trip repr (ut_core.h) and hashed
+// (one SHA-256 block); large-range INT values use repr(int), large-range
+// LOGINT values repr of the device's correctly rounded log2.
 //
 // One lane = one candidate.  The repr byte string is assembled in LDS in
 // [word][lane] layout (bank-conflict-free, no cross-lane traffic, so no
@@ -25,7 +26,7 @@
 // with the wave-uniform word-table entry (s_set_gpr_idx / v_movrels, no
 // scratch).  Bound: integer VALU (~1.4k ops per SHA-256 compression, with
 // Sigma/Ch/Maj as single v_bitop3_b32).
-#include "ut_internal.h"
+#include "ut_param.h"
 
 namespace ut {
 
@@ -47,7 +48,8 @@ __device__ __forceinline__ void inner_digest(const DevParam& pr, double v, const
   if (pr.hash_mode == HM_LUT) {
     int64_t idx;
     if (pr.kind == UT_ENUM || pr.kind == UT_BOOL) idx = (int64_t)v;
-    else idx = (int64_t)(v - pr.lo);
+    else if (pr.kind == UT_POW2) idx = (int64_t)(pow2_exponent(v) - pr.lo);  // repr(exponent)
+    else idx = (int64_t)(v - pr.lo);                                       // INT, LOGINT
     idx = idx < 0 ? 0 : (idx >= pr.lut_n ? pr.lut_n - 1 : idx);  // never fault on garbage input
     const uint4* src = reinterpret_cast<const uint4*>(lut + (pr.lut_base + idx) * 8);
     const uint4 a = src[0], b = src[1];
@@ -60,6 +62,7 @@ __device__ __forceinline__ void inner_digest(const DevParam& pr, double v, const
   LdsEmit e{reinterpret_cast<uint8_t*>(lds), lane};
   int len;
   if (pr.hash_mode == HM_FLOAT) len = repr_double(v, e);
+  else if (pr.hash_mode == HM_LOGINT) len = repr_double(py_log2(__dsub_rn(__dadd_rn(v, 1.0), pr.lo)), e);
   else len = repr_int64((int64_t)v, e);
   e.put(len, 0x80);
   uint32_t W[16];

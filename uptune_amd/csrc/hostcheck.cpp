@@ -4,6 +4,7 @@
 #include <stddef.h>
 #include <string.h>
 #include "ut_core.h"
+#include "../../include/uthot.h"
 
 namespace {
 struct BufEmit {
@@ -13,6 +14,20 @@ struct BufEmit {
 }  // namespace
 
 extern "C" {
+// C-ABI struct sizes as the C compiler lays them out (checked against the
+// ctypes mirrors in uptune_amd/_lib.py)
+long long uthc_sizeof(int which) {
+  switch (which) {
+    case 0: return (long long)sizeof(ut_param_desc);
+    case 1: return (long long)sizeof(ut_gp_hyper);
+    case 2: return (long long)sizeof(ut_round_out);
+    case 3: return (long long)sizeof(ut_de_params);
+    case 4: return (long long)sizeof(ut_acq);
+    case 5: return (long long)sizeof(ut_pso_params);
+    case 6: return (long long)sizeof(ut_ga_params);
+    default: return -1;
+  }
+}
 int uthc_repr_double(double x, char* out) {
   BufEmit e{out};
   return ut::repr_double(x, e);
@@ -50,6 +65,15 @@ void uthc_philox(unsigned long long seed, unsigned long long cand, unsigned stre
                  unsigned* out4) {
   ut::u32x4 r = ut::draw(seed, cand, stream, round_, op);
   out4[0] = r.x; out4[1] = r.y; out4[2] = r.z; out4[3] = r.w;
+}
+void uthc_py_log2(const double* x, double* out, long long n) {
+  for (long long i = 0; i < n; ++i) out[i] = ut::py_log2(x[i]);
+}
+void uthc_exp2(const double* x, double* out, long long n) {
+  for (long long i = 0; i < n; ++i) out[i] = ut::exp2_cr(x[i]);
+}
+void uthc_logint_unscale(const double* s, double mn, double* out, long long n) {
+  for (long long i = 0; i < n; ++i) out[i] = rint((ut::exp2_cr(s[i]) - 1.0) + mn);
 }
 void uthc_philox_raw(const unsigned* ctr4, const unsigned* key2, unsigned* out4) {
   ut::u32x4 c{ctr4[0], ctr4[1], ctr4[2], ctr4[3]};

@@ -14,52 +14,9 @@
 //   set_unit_value      manipulator.py:490-503
 //   op4_set_linear      manipulator.py:523-542 (primitive), :866-914 (complex)
 //   DE trial            differentialevolution.py:105-129
-#include "ut_internal.h"
+#include "ut_param.h"
 
 namespace ut {
-
-__device__ __forceinline__ bool is_primitive(int kind) { return kind <= UT_POW2; }
-
-// get_unit_value (manipulator.py:473-488)
-__device__ __forceinline__ double unit_of(const DevParam& pr, double v) {
-  if (pr.u_lo < pr.u_hi) return __ddiv_rn(__dsub_rn(v, pr.u_lo), pr.u_span);
-  return 0.0;
-}
-
-// set_unit_value (manipulator.py:490-503); returns the new stored value, or
-// `keep` when the range is a single point (the reference leaves it alone).
-__device__ __forceinline__ double from_unit(const DevParam& pr, double u, double keep) {
-  if (!(pr.u_lo < pr.u_hi)) return keep;
-  double val = __dadd_rn(__dmul_rn(u, pr.u_span), pr.u_lo);
-  if (pr.kind == UT_INT) val = rint(val);  // Python round(): half-to-even
-  val = py_max(pr.u_lo, py_min(val, pr.u_hi));
-  if (pr.kind == UT_INT) val = trunc(val);  // int(val)
-  return val;
-}
-
-// op1_randomize for one parameter from one 4x32 draw
-__device__ __forceinline__ double randomize(const DevParam& pr, u32x4 r) {
-  switch (pr.kind) {
-    case UT_FLOAT: {
-      // random.uniform(a, b) = a + (b - a) * random()
-      const double u = u01_from(r.x, r.y);
-      return __dadd_rn(pr.lo, __dmul_rn(__dsub_rn(pr.hi, pr.lo), u));
-    }
-    case UT_INT: {
-      // random.randint(lo, hi)
-      const int64_t lo = (int64_t)pr.lo, hi = (int64_t)pr.hi;
-      return (double)(lo + (int64_t)below64(u64_from(r.z, r.w), (uint64_t)(hi - lo + 1)));
-    }
-    case UT_BOOL:
-      // random.choice((True, False))
-      return below64(u64_from(r.z, r.w), 2) == 0 ? 1.0 : 0.0;
-    case UT_ENUM:
-      // random.choice(self.options) -> option index
-      return (double)below64(u64_from(r.z, r.w), (uint64_t)pr.n_opt);
-    default:
-      return 0.0;
-  }
-}
 
 __global__ __launch_bounds__(256) void k_population_init(const DevParam* __restrict__ params, int32_t P,
                                                          double* __restrict__ pop, int64_t ld, int64_t npop,
@@ -101,7 +58,7 @@ __device__ __forceinline__ void pick_donors(uint32_t w0, uint32_t w1, uint32_t w
 // random keys (= the first n_cross names of a uniform shuffle,
 // differentialevolution.py:122-125).
 __global__ __launch_bounds__(256) void k_de(const DevParam* __restrict__ params, int32_t P,
-                                            const double* __restrict__ pop, int64_t ldp, int64_t npop,
+                                            const double* __restrict__ vtab, const double* __restrict__ pop, int64_t ldp, int64_t npop,
                                             double cr, int32_t n_cross, uint64_t seed, uint32_t round_,
                                             int64_t cand_base, int64_t m, double* __restrict__ out,
                                             int64_t ldo) {
@@ -146,7 +103,7 @@ __global__ __launch_bounds__(256) void k_de(const DevParam* __restrict__ params,
     if (forced || u01_from(r.x, r.y) < cr) {
       const double x1 = col[d1], x2 = col[d2], x3 = col[d3];
       if (is_primitive(pr.kind)) {
-        const double va = unit_of(pr, x1), vb = unit_of(pr, x2), vc = unit_of(pr, x3);
+        const double va = unit_of(pr, x1, vtab), vb = unit_of(pr, x2, vtab), vc = unit_of(pr, x3, vtab);
         // v = a*va + b*vb + c*vc with a = 1.0, b = F, c = -F
         double u = __dadd_rn(__dadd_rn(__dmul_rn(1.0, va), __dmul_rn(F, vb)), __dmul_rn(nF, vc));
         u = py_max(0.0, py_min(u, 1.0));
@@ -167,7 +124,7 @@ __global__ __launch_bounds__(256) void k_de(const DevParam* __restrict__ params,
 
 // GP features of a configuration.
 __global__ __launch_bounds__(256) void k_encode(const DevParam* __restrict__ params, int32_t P,
-                                                const double* __restrict__ values, int64_t ld, int64_t m,
+                                                const double* __restrict__ vtab, const double* __restrict__ values, int64_t ld, int64_t m,
                                                 double* __restrict__ feat, int64_t ldf) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= m) return;
@@ -175,7 +132,7 @@ __global__ __launch_bounds__(256) void k_encode(const DevParam* __restrict__ par
     const DevParam pr = params[p];
     const double v = values[(int64_t)p * ld + i];
     if (is_primitive(pr.kind)) {
-      feat[(int64_t)pr.feat_col * ldf + i] = unit_of(pr, v);
+      feat[(int64_t)pr.feat_col * ldf + i] = unit_of(pr, v, vtab);
     } else if (pr.kind == UT_BOOL) {
       feat[(int64_t)pr.feat_col * ldf + i] = v;
     } else {
@@ -214,7 +171,7 @@ __global__ void k_pop_replace(int32_t P, double* __restrict__ pop, int64_t ldp, 
 // c = omega, c1 = phi_g, c2 = phi_l.
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_pso(const DevParam* __restrict__ params, int32_t P,
-                                             const double* __restrict__ pos, const double* __restrict__ vel,
+                                             const double* __restrict__ vtab, const double* __restrict__ pos, const double* __restrict__ vel,
                                              const double* __restrict__ pbest, int64_t ldp, int64_t npop,
                                              const double* __restrict__ gbest, double c, double c1, double c2,
                                              double sigma, int32_t enum_mode, uint64_t seed, uint32_t round_,
@@ -227,33 +184,38 @@ __global__ __launch_bounds__(256) void k_pso(const DevParam* __restrict__ params
   for (int32_t p = 0; p < P; ++p) {
     const DevParam pr = params[p];
     const int64_t o = (int64_t)p * ldp + t;
-    const double x = pos[o], v = vel[o], l = pbest[o], gb = gbest[p];
+    // scaled kinds move in their search scale (get_value / set_value):
+    // LOGINT by the Float rule on log values, POW2 by the Int rule on exponents
+    const double xr = pos[o], v = vel[o];
+    const double x = scaled_of(pr, xr, vtab), l = scaled_of(pr, pbest[o], vtab), gb = scaled_of(pr, gbest[p], vtab);
     const u32x4 r = draw(seed, g, (uint32_t)p, round_, OP_PSO);
     const double r1 = u01_from(r.x, r.y), r2 = u01_from(r.z, r.w);
     double nx, nv;
     if (pr.kind == UT_ENUM) {
       nv = v;
-      nx = x;  // reference: opn_stochastic_mix copies the particle INTO the parent (manipulator.py:442)
+      nx = xr;  // reference: opn_stochastic_mix copies the particle INTO the parent (manipulator.py:442)
       if (enum_mode == 1) {
         const u32x4 q = draw(seed, g, (uint32_t)p | (1u << STREAM_SUB_SHIFT), round_, OP_PSO);
         const double rr = u01_from(q.x, q.y);
         const double tot = (c + c1) + c2;
         const double w0 = c / tot, w1 = c1 / tot;
-        nx = rr < w0 ? x : (rr < w0 + w1 ? gb : l);
+        nx = rr < w0 ? xr : (rr < w0 + w1 ? gbest[p] : pbest[o]);
       }
     } else {
       nv = ((v * c) + (((gb - x) * c1) * r1)) + (((l - x) * c2) * r2);
-      if (pr.kind == UT_FLOAT) {
+      if (pr.kind == UT_FLOAT || pr.kind == UT_LOGINT) {
+        // legal_range: FLOAT (lo, hi); LOGINT its scaled range (u_lo, u_hi)
+        const double vmin = pr.kind == UT_FLOAT ? pr.lo : pr.u_lo, vmax = pr.kind == UT_FLOAT ? pr.hi : pr.u_hi;
         double y = x + nv;
-        y = (pr.lo > y) ? pr.lo : y;   // max(p, vmin)
-        nx = (y < pr.hi) ? y : pr.hi;  // min(vmax, .)
-      } else if (pr.kind == UT_INT) {
+        y = (vmin > y) ? vmin : y;              // max(p, vmin)
+        nx = unscale(pr, (y < vmax) ? y : vmax);  // min(vmax, .); set_value
+      } else if (pr.kind == UT_INT || pr.kind == UT_POW2) {
         const double k = pr.hi - pr.lo;
         const double s = k / (1.0 + ut_exp(-nv)) + pr.lo;
         const double z = normal_draw(seed, g, (uint32_t)p | (2u << STREAM_SUB_SHIFT), round_, OP_PSO);
         double pp = rint(s + z * (sigma * k));
         pp = (pr.lo > pp) ? pr.lo : pp;
-        nx = (pp < pr.hi) ? pp : pr.hi;
+        nx = unscale(pr, (pp < pr.hi) ? pp : pr.hi);
       } else {  // BOOL
         const double s = 1.0 / (1.0 + ut_exp(-nv));
         const u32x4 q = draw(seed, g, (uint32_t)p | (1u << STREAM_SUB_SHIFT), round_, OP_PSO);
@@ -278,7 +240,7 @@ __device__ __forceinline__ double parent_value(const DevParam& pr, const double*
 }
 
 __global__ __launch_bounds__(256) void k_ga(const DevParam* __restrict__ params, int32_t P,
-                                            const double* __restrict__ parent1, const double* __restrict__ parent2,
+                                            const double* __restrict__ vtab, const double* __restrict__ parent1, const double* __restrict__ parent2,
                                             double mutation_rate, double sigma, double crossover_rate, int32_t d_cross,
                                             int32_t must, int32_t normal, int32_t max_retries, uint32_t op,
                                             uint64_t seed, uint32_t round_, int64_t cand_base, int64_t m,
@@ -322,7 +284,7 @@ __global__ __launch_bounds__(256) void k_ga(const DevParam* __restrict__ params,
       if (mut) {
         if (normal && is_primitive(pr.kind)) {
           // op1_normal_mutation (manipulator.py:505-521)
-          double u = unit_of(pr, v);
+          double u = unit_of(pr, v, vtab);
           const double z = normal_draw(seed, g, sp | (2u << STREAM_SUB_SHIFT), round_, op);
           u = u + (0.0 + z * sigma);
           if (u < 0.0) u = u * -1.0;
@@ -354,7 +316,8 @@ int launch_population_init(ut_ctx* c, uint32_t round_) {
 
 int launch_de(ut_ctx* c, const ut_de_params* p, uint32_t round_, int64_t cand_base, int64_t m, double* out,
               int64_t ld) {
-  hipLaunchKernelGGL(k_de, dim3(grid1(m, 256)), dim3(256), 0, c->stream, c->space.d_params, c->space.P, c->pop,
+  hipLaunchKernelGGL(k_de, dim3(grid1(m, 256)), dim3(256), 0, c->stream, c->space.d_params, c->space.P,
+                     c->space.d_vtab, c->pop,
                      c->npop, c->npop, p->cr, p->n_cross, c->seed, round_, cand_base, m, out, ld);
   UT_LAUNCH_CHECK(c);
   return 0;
@@ -363,7 +326,8 @@ int launch_de(ut_ctx* c, const ut_de_params* p, uint32_t round_, int64_t cand_ba
 int launch_pso(ut_ctx* c, const ut_pso_params* a, const double* gbest, uint32_t round_, int64_t cand_base,
                int64_t m, double* out_x, double* out_v, int64_t ld) {
   const double* pb = a->alias_pbest ? c->pop : c->pso_best;
-  hipLaunchKernelGGL(k_pso, dim3(grid1(m, 256)), dim3(256), 0, c->stream, c->space.d_params, c->space.P, c->pop,
+  hipLaunchKernelGGL(k_pso, dim3(grid1(m, 256)), dim3(256), 0, c->stream, c->space.d_params, c->space.P,
+                     c->space.d_vtab, c->pop,
                      c->pso_vel, pb, c->npop, c->npop, gbest, a->omega, a->phi_g, a->phi_l, a->sigma, a->enum_mode,
                      c->seed, round_, cand_base, m, out_x, out_v, ld);
   UT_LAUNCH_CHECK(c);
@@ -373,7 +337,8 @@ int launch_pso(ut_ctx* c, const ut_pso_params* a, const double* gbest, uint32_t 
 int launch_ga(ut_ctx* c, const ut_ga_params* a, const double* parent1, const double* parent2, uint32_t round_,
               int64_t cand_base, int64_t m, double* out, int64_t ld, uint8_t* invalid) {
   const int32_t d = (int32_t)(a->crossover_strength * (double)c->space.P);  // int(strength * len(params))
-  hipLaunchKernelGGL(k_ga, dim3(grid1(m, 256)), dim3(256), 0, c->stream, c->space.d_params, c->space.P, parent1,
+  hipLaunchKernelGGL(k_ga, dim3(grid1(m, 256)), dim3(256), 0, c->stream, c->space.d_params, c->space.P,
+                     c->space.d_vtab, parent1,
                      parent2, a->mutation_rate, a->sigma, a->crossover_rate, d, a->must_mutate_count, a->normal,
                      a->max_retries, (uint32_t)a->op, c->seed, round_, cand_base, m, out, ld, invalid);
   UT_LAUNCH_CHECK(c);
@@ -382,7 +347,7 @@ int launch_ga(ut_ctx* c, const ut_ga_params* a, const double* parent1, const dou
 
 int launch_encode(ut_ctx* c, const double* values, int64_t ld, int64_t m, double* feat, int64_t ldf) {
   hipLaunchKernelGGL(k_encode, dim3(grid1(m, 256)), dim3(256), 0, c->stream, c->space.d_params, c->space.P,
-                     values, ld, m, feat, ldf);
+                     c->space.d_vtab, values, ld, m, feat, ldf);
   UT_LAUNCH_CHECK(c);
   return 0;
 }

@@ -608,6 +608,105 @@ UT_HD double normal_draw(uint64_t seed, uint64_t cand, uint32_t stream, uint32_t
 }
 
 // ---------------------------------------------------------------------------
+// Double-double natural log and 2^x for the scaled parameter kinds
+// (manipulator.py:778-797):
+//   LogIntegerParameter._scale   = math.log(v + 1.0 - min, 2.0)   (CPython: log(x) / log(2.0))
+//   LogIntegerParameter._unscale = int(round(2.0 ** v - 1.0 + min))
+// CPython calls libm log() and pow(); glibc's are correctly rounded except in
+// rare hard cases (<= 0.52 ulp).  These evaluate to ~2^-100 relative before
+// the one final rounding, i.e. they are correctly rounded except within
+// 2^-100 of a rounding boundary, so they agree with the reference bit for
+// bit wherever libm rounds correctly (tests/test_core_host.py: every
+// integer argument up to 2^20 plus random ones against CPython).
+// ---------------------------------------------------------------------------
+struct dd {
+  double hi, lo;
+};
+UT_HD double fma_rn(double a, double b, double c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __fma_rn(a, b, c);
+#else
+  return __builtin_fma(a, b, c);
+#endif
+}
+UT_HD dd two_sum(double a, double b) {
+  const double s = a + b, bb = s - a;
+  return dd{s, (a - (s - bb)) + (b - bb)};
+}
+UT_HD dd fast_two_sum(double a, double b) {  // |a| >= |b|
+  const double s = a + b;
+  return dd{s, b - (s - a)};
+}
+UT_HD dd two_prod(double a, double b) {
+  const double p = a * b;
+  return dd{p, fma_rn(a, b, -p)};
+}
+UT_HD dd dd_add(dd a, dd b) {
+  dd s = two_sum(a.hi, b.hi);
+  const dd t = two_sum(a.lo, b.lo);
+  s.lo += t.hi;
+  s = fast_two_sum(s.hi, s.lo);
+  s.lo += t.lo;
+  return fast_two_sum(s.hi, s.lo);
+}
+UT_HD dd dd_mul(dd a, dd b) {
+  dd p = two_prod(a.hi, b.hi);
+  p.lo += a.hi * b.lo + a.lo * b.hi;
+  return fast_two_sum(p.hi, p.lo);
+}
+UT_HD dd dd_mul_d(dd a, double b) {
+  dd p = two_prod(a.hi, b);
+  p.lo += a.lo * b;
+  return fast_two_sum(p.hi, p.lo);
+}
+UT_HD dd dd_div_d(dd a, double b) {
+  const double q1 = a.hi / b;
+  const dd p = two_prod(q1, b);
+  const double r = ((a.hi - p.hi) - p.lo) + a.lo;
+  return fast_two_sum(q1, r / b);
+}
+UT_HD dd dd_ldexp(dd a, int32_t k) {  // exact scaling by 2^k (|k| <= 1000, normal results)
+  const double s = bits_to_d((uint64_t)(k + 1023) << 52);
+  return dd{a.hi * s, a.lo * s};
+}
+
+constexpr double UT_LN2_DD_HI = 0x1.62e42fefa39efp-1;   // log(2.0) rounded = 6.93147180559945286e-01
+constexpr double UT_LN2_DD_LO = 0x1.abc9e3b39803fp-56;  // ln 2 - UT_LN2_DD_HI
+
+// exp of a double-double argument, |x| < 700
+UT_HD dd dd_exp(dd x) {
+  const double kd = rint(x.hi * UT_INV_LN2);
+  dd r = dd_add(x, dd_mul_d(dd{UT_LN2_DD_HI, UT_LN2_DD_LO}, -kd));  // |r| <= 0.35
+  r = dd_ldexp(r, -8);                                                  // |r| <= 1.4e-3
+  // expm1(r) = r (1 + r/2 (1 + r/3 (1 + ... r/10)))
+  dd p{1.0, 0.0};
+  for (int k = 10; k >= 2; --k) p = dd_add(dd{1.0, 0.0}, dd_div_d(dd_mul(r, p), (double)k));
+  dd a = dd_mul(r, p);
+  for (int i = 0; i < 8; ++i) a = dd_add(dd{2.0 * a.hi, 2.0 * a.lo}, dd_mul(a, a));  // (1+a)^2 - 1
+  return dd_ldexp(dd_add(dd{1.0, 0.0}, a), (int32_t)kd);
+}
+
+// natural log of a positive normal double, one Newton step in double-double
+// from ut_log: y1 = y0 + x e^-y0 - 1
+UT_HD double log_cr(double x) {
+  const double y0 = ut_log(x);
+  const dd t = dd_mul_d(dd_exp(dd{-y0, 0.0}), x);
+  const dd y1 = dd_add(dd{y0, 0.0}, dd_add(t, dd{-1.0, 0.0}));
+  return y1.hi;
+}
+
+// math.log(x, 2.0) as CPython evaluates it: log(x) / log(2.0)
+UT_HD double py_log2(double x) { return log_cr(x) / UT_LN2_DD_HI; }
+
+// 2.0 ** s, |s| < 1000
+UT_HD double exp2_cr(double s) {
+  dd t = two_prod(s, UT_LN2_DD_HI);
+  t.lo += s * UT_LN2_DD_LO;
+  t = fast_two_sum(t.hi, t.lo);
+  return dd_exp(t).hi;
+}
+
+// ---------------------------------------------------------------------------
 // Parameter value arithmetic (unit encoding) -- bit-exact restatement of
 //   get_unit_value  manipulator.py:473-488
 //   set_unit_value  manipulator.py:490-503

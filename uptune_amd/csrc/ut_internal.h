@@ -16,18 +16,22 @@ namespace ut {
 // loads).
 struct DevParam {
   int32_t kind;
-  int32_t hash_mode;   // HM_LUT / HM_FLOAT / HM_INT
+  int32_t hash_mode;   // HM_LUT / HM_FLOAT / HM_INT / HM_LOGINT
   int64_t lut_base;    // first digest of this param in the LUT buffer
   int64_t lut_n;       // LUT entries (indices are clamped to [0, lut_n))
-  double lo, hi;       // legal range of the stored value
-  double u_lo, u_hi;   // unit-encoding range (widened for integer types)
+  double lo, hi;       // FLOAT/INT/LOGINT: stored-value bounds (min_value, max_value);
+                       // POW2: exponent bounds (its legal_range, manipulator.py:829-830)
+  double u_lo, u_hi;   // unit-encoding range of the searched value (get_value):
+                       // widened for integer types; LOGINT: the scaled legal_range
   double u_span;       // u_hi - u_lo, rounded as Python rounds it
   int64_t n_opt;       // ENUM/BOOL option count
   int32_t feat_col;    // first GP feature column
   int32_t n_feat;      // GP feature columns of this param
+  int64_t vtab_base;   // LOGINT: first entry of get_value(v) for v = lo.. in the value table
+  int64_t vtab_n;      // LOGINT: table entries; 0 = compute the log on the device
 };
 
-enum : int32_t { HM_LUT = 0, HM_FLOAT = 1, HM_INT = 2 };
+enum : int32_t { HM_LUT = 0, HM_FLOAT = 1, HM_INT = 2, HM_LOGINT = 3 };
 
 // One 32-bit word of the fixed-layout outer hash message.
 struct HashWord {
@@ -50,6 +54,7 @@ struct Space {
   HashWord* d_words = nullptr;            // outer_blocks * 16
   int16_t* d_block_last = nullptr;        // last sorted position needed by each block
   uint32_t* d_lut = nullptr;              // digests [*][8]
+  double* d_vtab = nullptr;               // LOGINT get_value tables (host-computed by CPython)
 };
 
 template <class T>

@@ -36,6 +36,13 @@ from . import _lib as L
 
 # discrete INT ranges up to this many values get an inner-digest LUT
 INT_LUT_MAX = 4096
+# LogInteger ranges up to this many values get host tables (get_value and the
+# inner digest), computed by this host's CPython math.log -- i.e. exactly the
+# reference's values.  libm log is not correctly rounded everywhere (it
+# differs from the correctly rounded log on ~2e-5 of integer arguments here),
+# so larger ranges, which fall back to the device's correctly rounded log,
+# can differ from the reference in that fraction of LogInteger values.
+LOGINT_TABLE_MAX = 1 << 22
 
 
 class Parameter:
@@ -79,18 +86,29 @@ class FloatParameter(NumericParameter):
 
 
 class LogIntegerParameter(FloatParameter):
-    """integer searched on a log scale (manipulator.py:781-797); host API only
-    in this round -- the device path rejects it with UT_EUNSUPPORTED."""
+    """integer searched on a log scale (manipulator.py:778-797): stored as an
+    int, get_value = math.log(v + 1.0 - min, 2.0)."""
 
     def __init__(self, name, min_value, max_value):
         Parameter.__init__(self, name)
         self.min_value = float(min_value)
         self.max_value = float(max_value)
 
+    def _scale(self, v):
+        return math.log(v + 1.0 - self.min_value, 2.0)
+
+    def _unscale(self, v):
+        return int(round(2.0 ** v - 1.0 + self.min_value))
+
+    def legal_range(self, config=None):
+        return self._scale(self.min_value - 0.4999), self._scale(self.max_value + 0.4999)
+
 
 class PowerOfTwoParameter(IntegerParameter):
-    """power of two searched by exponent (manipulator.py:813-836); host API only
-    in this round."""
+    """power of two searched by exponent (manipulator.py:811-836)."""
+
+    def legal_range(self, config=None):
+        return int(math.log(self.min_value, 2)), int(math.log(self.max_value, 2))
 
     def __init__(self, name, min_value, max_value):
         assert min_value >= 1
@@ -193,11 +211,12 @@ class ParamSpec:
     feat_col: int = 0
     n_feat: int = 1
     lut: bytes = b""
+    vtab: Any = None      # LOGINT: float64 get_value table
 
     def to_value(self, v) -> float:
         if self.kind == L.UT_FLOAT:
             return float(v)
-        if self.kind == L.UT_INT:
+        if self.kind in (L.UT_INT, L.UT_LOGINT, L.UT_POW2):
             return float(int(v))
         if self.kind == L.UT_BOOL:
             return 1.0 if v else 0.0
@@ -208,7 +227,7 @@ class ParamSpec:
     def from_value(self, x: float):
         if self.kind == L.UT_FLOAT:
             return float(x)
-        if self.kind == L.UT_INT:
+        if self.kind in (L.UT_INT, L.UT_LOGINT, L.UT_POW2):
             return int(x)
         if self.kind == L.UT_BOOL:
             return bool(x != 0.0)
@@ -271,6 +290,25 @@ def compile_space(params) -> SpaceSpec:
             ps.n_feat = 1
             if kind == L.UT_INT and (hi - lo + 1) <= INT_LUT_MAX:
                 ps.lut = b"".join(_digest(repr(int(v))) for v in range(int(lo), int(hi) + 1))
+        elif kind == L.UT_LOGINT:
+            # LogIntegerParameter (manipulator.py:778-797): stored int bounds,
+            # searched on log2 values over the widened legal_range
+            mn, mx = float(p.min_value), float(p.max_value)
+            ps.lo, ps.hi = mn, mx
+            scale = lambda v: math.log(v + 1.0 - mn, 2.0)  # noqa: E731  (_scale :784-785)
+            ps.u_lo, ps.u_hi = scale(mn - 0.4999), scale(mx + 0.4999)
+            ps.u_span = float(ps.u_hi - ps.u_lo)
+            n = int(mx) - int(mn) + 1
+            if n <= LOGINT_TABLE_MAX:
+                vals = [scale(float(v)) for v in range(int(mn), int(mx) + 1)]
+                ps.vtab = np.array(vals, dtype=np.float64)
+                ps.lut = b"".join(_digest(repr(x)) for x in vals)
+        elif kind == L.UT_POW2:
+            # PowerOfTwoParameter (manipulator.py:811-836): searched by the exponent
+            ps.lo, ps.hi = float(p.min_value), float(p.max_value)
+            elo, ehi = int(math.log(p.min_value, 2)), int(math.log(p.max_value, 2))
+            ps.u_lo, ps.u_hi, ps.u_span = unit_bounds(L.UT_INT, elo, ehi)
+            ps.lut = b"".join(_digest(repr(e)) for e in range(elo, ehi + 1))
         elif kind == L.UT_BOOL:
             ps.options = [True, False]
             ps.n_feat = 1
@@ -316,4 +354,12 @@ def to_descs(spec: SpaceSpec):
         else:
             d.lut_count = 0
             d.lut_host = None
+        if ps.vtab is not None:
+            vt = np.ascontiguousarray(ps.vtab, dtype=np.float64)
+            keep.append(vt)
+            d.vtab_count = vt.size
+            d.vtab_host = vt.ctypes.data
+        else:
+            d.vtab_count = 0
+            d.vtab_host = None
     return arr, keep
