@@ -136,7 +136,7 @@ def main():
     acq = eng.acq("ei", xi=0.0)
 
     def step(r):
-        eng.gp_fit(X, y, lengthscale=0.2, sigma_f2=1.0, sigma_n2=1e-6)
+        eng.gp_fit(X, y, lengthscale=0.2, sigma_f2=1.0, sigma_n2=1e-6, wait=False)   # overlaps propose + hash
         idx, top, dig, _ = eng.score_round_de(m, k, round_=r, cand_base=cand_base, cr=0.2, n_cross=1, acq=acq,
                                               want_values=False)
         if world > 1:

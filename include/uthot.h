@@ -196,6 +196,14 @@ int ut_dedup(ut_ctx* ctx, const uint32_t* digests, int64_t m, uint8_t* out_dup);
  * L = chol(K + (sigma_n2 + jitter) I), L^-1, alpha on the device. */
 int ut_gp_fit(ut_ctx* ctx, const double* X_host, const double* y_host, int32_t n, int32_t d,
               const ut_gp_hyper* hyper);
+/* The same fit, enqueued on the context's internal fit stream without a host
+ * wait: it runs beside whatever is enqueued next (e.g. the proposal and hash
+ * stages of the next round), and every later scoring call waits for it on the
+ * device.  X_host / y_host may be reused on return.  A failed fit (not
+ * positive definite) is reported by ut_gp_stats / ut_gp_fit, and makes every
+ * score NaN (nothing is selected). */
+int ut_gp_fit_async(ut_ctx* ctx, const double* X_host, const double* y_host, int32_t n, int32_t d,
+                    const ut_gp_hyper* hyper);
 /* posterior of standardised y and the acquisition score for m candidates
  * (features [d][ld]).  mu/var/score may be NULL.  dup (may be NULL) marks
  * candidates excluded from selection (score forced to -inf). */

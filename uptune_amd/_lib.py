@@ -92,6 +92,7 @@ SIGNATURES = {
     "ut_history_add_host": (C.c_int, [P, P, I64]),
     "ut_dedup": (C.c_int, [P, P, I64, P]),
     "ut_gp_fit": (C.c_int, [P, P, P, I32, I32, C.POINTER(GpHyper)]),
+    "ut_gp_fit_async": (C.c_int, [P, P, P, I32, I32, C.POINTER(GpHyper)]),
     "ut_gp_score": (C.c_int, [P, P, I64, I64, C.POINTER(Acq), P, P, P, P]),
     "ut_gp_set_precision": (C.c_int, [P, I32]),
     "ut_gp_stats": (C.c_int, [P, C.POINTER(D), C.POINTER(D), C.POINTER(D)]),

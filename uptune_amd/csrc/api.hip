@@ -20,26 +20,32 @@ void mark(ut_ctx* c, const char* name) {
   hipEvent_t e;
   if (hipEventCreate(&e) != hipSuccess) return;
   hipEventRecord(e, c->stream);
-  c->timing.marks.emplace_back(name, e);
+  c->timing.marks.push_back({name, c->stream, e});
 }
 
 static void timing_begin(ut_ctx* c) {
   if (!c->timing.on) return;
-  for (auto& m : c->timing.marks) hipEventDestroy(m.second);
+  for (auto& m : c->timing.marks) hipEventDestroy(m.ev);
   c->timing.marks.clear();
-  mark(c, "begin");
+  mark(c, "");
 }
 
 static int timing_end(ut_ctx* c) {
   if (!c->timing.on) return 0;
-  UT_HIP(c, hipStreamSynchronize(c->stream));
+  UT_HIP(c, ut::sync_all(c));
   c->timing.last.clear();
-  for (size_t i = 1; i < c->timing.marks.size(); ++i) {
-    float ms = 0.f;
-    hipEventElapsedTime(&ms, c->timing.marks[i - 1].second, c->timing.marks[i].second);
-    c->timing.last.emplace_back(c->timing.marks[i].first, (double)ms);
+  for (size_t i = 0; i < c->timing.marks.size(); ++i) {
+    const auto& m = c->timing.marks[i];
+    if (m.name.empty()) continue;
+    for (size_t j = i; j-- > 0;) {  // the previous mark on the same stream
+      if (c->timing.marks[j].stream != m.stream) continue;
+      float ms = 0.f;
+      hipEventElapsedTime(&ms, c->timing.marks[j].ev, m.ev);
+      c->timing.last.emplace_back(m.name, (double)ms);
+      break;
+    }
   }
-  for (auto& m : c->timing.marks) hipEventDestroy(m.second);
+  for (auto& m : c->timing.marks) hipEventDestroy(m.ev);
   c->timing.marks.clear();
   return 0;
 }
@@ -81,36 +87,39 @@ static int compile_hash_layout(ut_ctx* c, const std::vector<std::string>& names,
   const uint64_t bits = (uint64_t)L * 8;
   for (int q = 7; q >= 0; --q) msg.push_back((uint8_t)(bits >> (8 * q)));
   const int64_t NBLK = (int64_t)msg.size() / 64;
+  // a 4-byte word must never touch two holes (the kernel fetches one hole per word)
+  for (int32_t q = 0; q + 1 < P; ++q)
+    UT_CHECK(c, hole_start[q + 1] - (hole_start[q] + 64) >= 3, UT_EUNSUPPORTED,
+             "hash layout: parameter names too short to separate the digest holes");
   std::vector<HashWord> words(NBLK * 16);
-  std::vector<int16_t> block_last(NBLK);
+  std::vector<int32_t> block_last(NBLK);
   int32_t j = 0;  // first hole that may overlap the current word
-  int16_t running = -1;
+  int32_t running = -1;
   for (int64_t w = 0; w < NBLK * 16; ++w) {
     HashWord hw;
     hw.tmpl = ((uint32_t)msg[4 * w] << 24) | ((uint32_t)msg[4 * w + 1] << 16) | ((uint32_t)msg[4 * w + 2] << 8) |
               (uint32_t)msg[4 * w + 3];
-    hw.hole = -1;
-    hw.q1 = 0;
-    hw.shift = 0;
+    hw.info = 0;
     while (j < P && hole_start[j] + 64 <= 4 * w) ++j;
     if (j < P && hole_start[j] < 4 * w + 4 && hole_start[j] + 64 > 4 * w) {
       const int64_t d = 4 * w - hole_start[j];           // -3 .. 63
-      const int64_t q = (d >= 0) ? d / 4 : -1;           // floor(d / 4)
-      hw.hole = (int16_t)j;
-      hw.q1 = (uint8_t)(q + 1);
-      hw.shift = (uint8_t)(d - 4 * q);
-      if (j > running) running = (int16_t)j;
+      const int64_t q = (d >= 0) ? d / 4 : -1;           // floor(d / 4): hex word holding byte d
+      const uint32_t slot = (uint32_t)(j & 1) * 16;      // hole j lives in hex slot j % 2
+      uint32_t info = HW_HOLE | ((uint32_t)(d - 4 * q) * 8) << HW_SHIFT_POS;
+      if (q >= 0) info |= HW_LO_VALID | (slot + (uint32_t)q);
+      if (q + 1 < 16) info |= HW_HI_VALID | ((slot + (uint32_t)(q + 1)) << HW_HI_POS);
+      hw.info = info;
+      if (j > running) running = j;
     }
     words[w] = hw;
     if (w % 16 == 15) block_last[w / 16] = running;
   }
-  UT_CHECK(c, P < 32767, UT_EINVAL, "too many parameters");
   s.outer_len = L;
   s.outer_blocks = NBLK;
   UT_HIP(c, hipMalloc((void**)&s.d_words, sizeof(HashWord) * words.size()));
   UT_HIP(c, hipMemcpy(s.d_words, words.data(), sizeof(HashWord) * words.size(), hipMemcpyHostToDevice));
-  UT_HIP(c, hipMalloc((void**)&s.d_block_last, sizeof(int16_t) * block_last.size()));
-  UT_HIP(c, hipMemcpy(s.d_block_last, block_last.data(), sizeof(int16_t) * block_last.size(), hipMemcpyHostToDevice));
+  UT_HIP(c, hipMalloc((void**)&s.d_block_last, sizeof(int32_t) * block_last.size()));
+  UT_HIP(c, hipMemcpy(s.d_block_last, block_last.data(), sizeof(int32_t) * block_last.size(), hipMemcpyHostToDevice));
   return 0;
 }
 
@@ -118,7 +127,7 @@ static int history_alloc(ut_ctx* c, int64_t cap) {
   int64_t p2 = 1024;
   while (p2 < cap) p2 <<= 1;
   if (c->hist_keys) {
-    UT_HIP(c, hipStreamSynchronize(c->stream));
+    UT_HIP(c, ut::sync_all(c));
     hipFree(c->hist_keys);
     hipFree(c->hist_state);
   }
@@ -150,8 +159,14 @@ int ut_ctx_create(int device, uint64_t seed, ut_ctx** out) {
   int ncu = 0;
   if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && ncu >= 8)
     c->n_cu = ncu;
-  if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess) {
-    delete c;
+  if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->fit_stream, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_fit, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_prefit, hipEventDisableTiming) != hipSuccess) {
+    ut_ctx_destroy(c);
     return UT_EHIP;
   }
   c->stream = c->own_stream;
@@ -162,7 +177,7 @@ int ut_ctx_create(int device, uint64_t seed, ut_ctx** out) {
 int ut_ctx_destroy(ut_ctx* c) {
   if (!c) return UT_EINVAL;
   hipSetDevice(c->device);
-  hipStreamSynchronize(c->stream);
+  if (c->stream) ut::sync_all(c);
   free_space(c->space);
   auto fr = [](void* p) { if (p) hipFree(p); };
   fr(c->pop); fr(c->pso_vel); fr(c->pso_best); fr(c->hist_keys); fr(c->hist_state); fr(c->batch_slots);
@@ -173,8 +188,12 @@ int ut_ctx_destroy(ut_ctx* c) {
   fr(c->r_values.p); fr(c->r_feat.p); fr(c->r_mu.p); fr(c->r_var.p); fr(c->r_score.p); fr(c->r_digest.p);
   fr(c->r_dup.p); fr(c->tk_score[0].p); fr(c->tk_score[1].p); fr(c->tk_idx[0].p); fr(c->tk_idx[1].p);
   fr(c->r_topk_idx.p); fr(c->r_topk_score.p);
-  for (auto& m : c->timing.marks) hipEventDestroy(m.second);
-  if (c->own_stream) hipStreamDestroy(c->own_stream);
+  for (auto& m : c->timing.marks) hipEventDestroy(m.ev);
+  for (hipEvent_t e : {c->ev_fork, c->ev_join, c->ev_fit, c->ev_prefit})
+    if (e) hipEventDestroy(e);
+  if (c->fit_host) hipHostFree(c->fit_host);
+  for (hipStream_t st : {c->own_stream, c->side, c->fit_stream})
+    if (st) hipStreamDestroy(st);
   delete c;
   return 0;
 }
@@ -189,7 +208,7 @@ int ut_set_stream(ut_ctx* c, void* s) {
 
 int ut_sync(ut_ctx* c) {
   if (!c) return UT_EINVAL;
-  UT_HIP(c, hipStreamSynchronize(c->stream));
+  UT_HIP(c, ut::sync_all(c));
   return 0;
 }
 
@@ -197,7 +216,7 @@ int ut_space_define(ut_ctx* c, int32_t P, const ut_param_desc* params, int32_t p
   if (!c) return UT_EINVAL;
   UT_CHECK(c, P >= 1 && params, UT_EINVAL, "space: need at least one parameter");
   UT_HIP(c, hipSetDevice(c->device));
-  UT_HIP(c, hipStreamSynchronize(c->stream));
+  UT_HIP(c, ut::sync_all(c));
   free_space(c->space);
   c->has_space = false;
   Space& s = c->space;
@@ -312,7 +331,7 @@ static int pop_alloc(ut_ctx* c, int64_t npop) {
     return 0;
   }
   if (c->pop) {
-    UT_HIP(c, hipStreamSynchronize(c->stream));
+    UT_HIP(c, ut::sync_all(c));
     hipFree(c->pop);
   }
   UT_HIP(c, hipMalloc((void**)&c->pop, sizeof(double) * need));
@@ -405,7 +424,7 @@ int ut_history_add(ut_ctx* c, const uint32_t* dig, int64_t n) {
     c->hist_count = 0;
     if (old_keys) {
       int rc = launch_hist_rehash(c, old_keys, old_state, old_cap);
-      UT_HIP(c, hipStreamSynchronize(c->stream));
+      UT_HIP(c, ut::sync_all(c));
       hipFree(old_keys);
       hipFree(old_state);
       if (rc) return rc;
@@ -426,7 +445,7 @@ int ut_history_add_host(ut_ctx* c, const uint32_t* dig, int64_t n) {
   UT_HIP(c, hipMalloc((void**)&tmp, sizeof(uint32_t) * 8 * n));
   UT_HIP(c, hipMemcpyAsync(tmp, dig, sizeof(uint32_t) * 8 * n, hipMemcpyHostToDevice, c->stream));
   int rc = ut_history_add(c, tmp, n);
-  UT_HIP(c, hipStreamSynchronize(c->stream));
+  UT_HIP(c, ut::sync_all(c));
   hipFree(tmp);
   return rc;
 }
@@ -440,7 +459,15 @@ int ut_dedup(ut_ctx* c, const uint32_t* dig, int64_t m, uint8_t* dup) {
 int ut_gp_fit(ut_ctx* c, const double* X, const double* y, int32_t n, int32_t d, const ut_gp_hyper* h) {
   if (!c) return UT_EINVAL;
   UT_HIP(c, hipSetDevice(c->device));
-  return gp_fit_impl(c, X, y, n, d, h);
+  int rc = gp_fit_enqueue(c, X, y, n, d, h);
+  if (rc) return rc;
+  return gp_wait_fit(c);
+}
+
+int ut_gp_fit_async(ut_ctx* c, const double* X, const double* y, int32_t n, int32_t d, const ut_gp_hyper* h) {
+  if (!c) return UT_EINVAL;
+  UT_HIP(c, hipSetDevice(c->device));
+  return gp_fit_enqueue(c, X, y, n, d, h);
 }
 
 int ut_gp_score(ut_ctx* c, const double* feat, int64_t ld, int64_t m, const ut_acq* acq, const uint8_t* dup,
@@ -460,9 +487,11 @@ int ut_gp_set_precision(ut_ctx* c, int32_t bits) {
 int ut_gp_stats(ut_ctx* c, double* f_best, double* y_mean, double* y_std) {
   if (!c) return UT_EINVAL;
   UT_CHECK(c, c->gp_ready, UT_EINVAL, "gp_stats: no fitted GP");
+  int rc = gp_wait_fit(c);
+  if (rc) return rc;
   double st[4];
   UT_HIP(c, hipMemcpyAsync(st, c->gp_stats, sizeof(double) * 3, hipMemcpyDeviceToHost, c->stream));
-  UT_HIP(c, hipStreamSynchronize(c->stream));
+  UT_HIP(c, ut::sync_all(c));
   if (f_best) *f_best = st[0];
   if (y_mean) *y_mean = st[1];
   if (y_std) *y_std = st[2];
@@ -501,13 +530,24 @@ int ut_score_round_de(ut_ctx* c, const ut_de_params* de, const ut_acq* acq, uint
   timing_begin(c);
   if ((rc = ut_propose_de(c, de, round_, cand_base, m, c->r_values.p, ld))) return rc;
   mark(c, "propose");
-  if ((rc = launch_hash(c, c->r_values.p, ld, m, c->r_digest.p))) return rc;
-  mark(c, "hash");
-  if ((rc = launch_dedup(c, c->r_digest.p, m, c->r_dup.p))) return rc;
-  mark(c, "dedup");
+  // fork: hash_config + dedup on the side stream, beside encode + GP scoring
+  UT_HIP(c, hipEventRecord(c->ev_fork, c->stream));
+  UT_HIP(c, hipStreamWaitEvent(c->side, c->ev_fork, 0));
+  {
+    StreamScope on_side(c, c->side);
+    mark(c, "");
+    if ((rc = launch_hash(c, c->r_values.p, ld, m, c->r_digest.p))) return rc;
+    mark(c, "hash");
+    if ((rc = launch_dedup(c, c->r_digest.p, m, c->r_dup.p))) return rc;
+    mark(c, "dedup");
+    UT_HIP(c, hipEventRecord(c->ev_join, c->side));
+  }
   if ((rc = launch_encode(c, c->r_values.p, ld, m, c->r_feat.p, ld))) return rc;
   mark(c, "encode");
-  if ((rc = gp_score_impl(c, c->r_feat.p, ld, m, acq, c->r_dup.p, c->r_mu.p, c->r_var.p, c->r_score.p))) return rc;
+  // join before the finalize kernel, which masks duplicates
+  if ((rc = gp_score_impl(c, c->r_feat.p, ld, m, acq, c->r_dup.p, c->r_mu.p, c->r_var.p, c->r_score.p,
+                          c->ev_join)))
+    return rc;
   if ((rc = topk_impl(c, c->r_score.p, c->r_dup.p, m, cand_base, k, c->r_topk_idx.p, c->r_topk_score.p)))
     return rc;
   mark(c, "topk");
@@ -528,7 +568,7 @@ int ut_score_round_de(ut_ctx* c, const ut_de_params* de, const ut_acq* acq, uint
       rc = launch_gather_rows(c, c->r_values.p, ld, c->r_topk_idx.p, cand_base, k, vals, k, c->r_digest.p,
                               out->topk_digest);
       if (tmp.p) {
-        UT_HIP(c, hipStreamSynchronize(c->stream));
+        UT_HIP(c, ut::sync_all(c));
         hipFree(tmp.p);
       }
       if (rc) return rc;

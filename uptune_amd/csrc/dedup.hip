@@ -129,7 +129,7 @@ int launch_dedup(ut_ctx* c, const uint32_t* dig, int64_t m, uint8_t* dup) {
   UT_CHECK(c, m < (int64_t)0x7FFFFFFF, UT_EINVAL, "dedup batch must be < 2^31 candidates");
   if (c->batch_cap < cap) {
     if (c->batch_slots) {
-      UT_HIP(c, hipStreamSynchronize(c->stream));
+      UT_HIP(c, ut::sync_all(c));
       UT_HIP(c, hipFree(c->batch_slots));
     }
     UT_HIP(c, hipMalloc((void**)&c->batch_slots, cap * sizeof(int32_t)));

@@ -23,6 +23,8 @@
 //          at the tile's diagonal)  -> |L^-1 k*|^2 partials
 // Both run in gp_gemm.hip (fp64 MFMA by default, fp32 MFMA when
 // ut_gp_set_precision(ctx, 32)).
+#include <cstring>
+
 #include "ut_internal.h"
 
 namespace ut {
@@ -428,8 +430,8 @@ __device__ __forceinline__ double acq_score(int kind, double mu, double var, dou
 
 __global__ void k_gp_finalize(int64_t m, int32_t RT1, int32_t RT2, const double* __restrict__ mu_part,
                               const double* __restrict__ var_part, int64_t ldp, double sf2,
-                              const double* __restrict__ stats, int32_t kind, double xi, double kappa,
-                              const uint8_t* __restrict__ dup, double* __restrict__ mu_out,
+                              const double* __restrict__ stats, const int32_t* __restrict__ fit_flag, int32_t kind,
+                              double xi, double kappa, const uint8_t* __restrict__ dup, double* __restrict__ mu_out,
                               double* __restrict__ var_out, double* __restrict__ score_out) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= m) return;
@@ -439,6 +441,9 @@ __global__ void k_gp_finalize(int64_t m, int32_t RT1, int32_t RT2, const double*
   double var = sf2 - vs;
   var = var > 0.0 ? var : 0.0;
   double sc = acq_score(kind, mu, var, stats[0], xi, kappa);
+  if (*fit_flag != 0) {  // failed (asynchronous) fit: nothing is selectable
+    mu = var = sc = __builtin_nan("");
+  }
   if (dup && dup[i]) sc = -1.0 / 0.0;
   if (mu_out) mu_out[i] = mu;
   if (var_out) var_out[i] = var;
@@ -451,14 +456,14 @@ __global__ void k_gp_finalize(int64_t m, int32_t RT1, int32_t RT2, const double*
 static int gp_alloc(ut_ctx* c, int32_t npad, int32_t d) {
   if (c->gp_cap_n >= npad && c->gp_d == d && c->gp_Xs) return 0;
   if (c->gp_Xs_f) {
-    UT_HIP(c, hipStreamSynchronize(c->stream));
+    UT_HIP(c, ut::sync_all(c));
     hipFree(c->gp_Xs_f); hipFree(c->gp_LinvT); hipFree(c->gp_LinvT_f); hipFree(c->gp_T); hipFree(c->gp_ctr);
     hipFree(c->gp_XsT);
     c->gp_Xs_f = nullptr; c->gp_LinvT = nullptr; c->gp_LinvT_f = nullptr; c->gp_T = nullptr; c->gp_ctr = nullptr;
     c->gp_XsT = nullptr;
   }
   if (c->gp_Xs) {
-    UT_HIP(c, hipStreamSynchronize(c->stream));
+    UT_HIP(c, ut::sync_all(c));
     hipFree(c->gp_Xs); hipFree(c->gp_xnorm); hipFree(c->gp_K); hipFree(c->gp_Linv);
     hipFree(c->gp_y); hipFree(c->gp_tmp); hipFree(c->gp_alpha); hipFree(c->gp_inv_ell);
     hipFree(c->gp_stats); hipFree(c->gp_flag);
@@ -484,20 +489,41 @@ static int gp_alloc(ut_ctx* c, int32_t npad, int32_t d) {
   return 0;
 }
 
-int gp_fit_impl(ut_ctx* c, const double* X, const double* y, int32_t n, int32_t d, const ut_gp_hyper* h) {
+// Enqueue a fit on the fit stream, ordered after everything already enqueued
+// on the caller's stream (earlier rounds read the GP state being replaced).
+// Scoring waits on ev_fit; failure (not positive definite) is reported by
+// gp_wait_fit and, on the device, by NaN scores from k_gp_finalize.
+int gp_fit_enqueue(ut_ctx* c, const double* X, const double* y, int32_t n, int32_t d, const ut_gp_hyper* h) {
   UT_CHECK(c, n >= 1 && d >= 1 && X && y && h && h->lengthscale_host, UT_EINVAL, "gp_fit: bad arguments");
   const int32_t npad = ((n + NPAD - 1) / NPAD) * NPAD;
   int rc = gp_alloc(c, npad, d);
   if (rc) return rc;
+  // pinned staging (the previous fit's copies out of it are complete once ev_fit is)
+  const size_t need = (size_t)n * d + n + d;
+  if (c->fit_pending) UT_HIP(c, hipEventSynchronize(c->ev_fit));
+  if (c->fit_host_n < need) {
+    if (c->fit_host) hipHostFree(c->fit_host);
+    c->fit_host = nullptr;
+    c->fit_host_n = 0;
+    UT_HIP(c, hipHostMalloc((void**)&c->fit_host, sizeof(double) * need, hipHostMallocDefault));
+    c->fit_host_n = need;
+  }
+  double* hX = c->fit_host;
+  double* hy = hX + (size_t)n * d;
+  double* hinv = hy + n;
+  std::memcpy(hX, X, sizeof(double) * n * d);
+  std::memcpy(hy, y, sizeof(double) * n);
+  for (int32_t k = 0; k < d; ++k) hinv[k] = 1.0 / h->lengthscale_host[k];
+  UT_HIP(c, hipEventRecord(c->ev_prefit, c->stream));
+  UT_HIP(c, hipStreamWaitEvent(c->fit_stream, c->ev_prefit, 0));
+  StreamScope on_fit(c, c->fit_stream);
   c->gp_n = n;
   c->gp_sf2 = h->sigma_f2;
-  std::vector<double> inv(d);
-  for (int32_t k = 0; k < d; ++k) inv[k] = 1.0 / h->lengthscale_host[k];
   double* dX = c->gp_tmp;           // [n][d] staging (gp_tmp holds npad*(d+1))
   double* dy = c->gp_tmp + (int64_t)npad * d;
-  UT_HIP(c, hipMemcpyAsync(c->gp_inv_ell, inv.data(), sizeof(double) * d, hipMemcpyHostToDevice, c->stream));
-  UT_HIP(c, hipMemcpyAsync(dX, X, sizeof(double) * n * d, hipMemcpyHostToDevice, c->stream));
-  UT_HIP(c, hipMemcpyAsync(dy, y, sizeof(double) * n, hipMemcpyHostToDevice, c->stream));
+  UT_HIP(c, hipMemcpyAsync(c->gp_inv_ell, hinv, sizeof(double) * d, hipMemcpyHostToDevice, c->stream));
+  UT_HIP(c, hipMemcpyAsync(dX, hX, sizeof(double) * n * d, hipMemcpyHostToDevice, c->stream));
+  UT_HIP(c, hipMemcpyAsync(dy, hy, sizeof(double) * n, hipMemcpyHostToDevice, c->stream));
   UT_HIP(c, hipMemsetAsync(c->gp_flag, 0, sizeof(int32_t), c->stream));
   hipLaunchKernelGGL(k_gp_prep_train, dim3(grid1(npad, 256)), dim3(256), 0, c->stream, dX, n, npad, d,
                      c->gp_inv_ell, c->gp_Xs, c->gp_xnorm);
@@ -533,19 +559,31 @@ int gp_fit_impl(ut_ctx* c, const double* X, const double* y, int32_t n, int32_t 
   if ((rc = launch_xs_t(c, c->gp_Xs, npad, d, ((d + 15) / 16) * 16, c->gp_XsT))) return rc;
   if ((rc = launch_transpose(c, c->gp_Linv, npad, c->gp_LinvT, c->gp_prec == 32 ? c->gp_LinvT_f : nullptr))) return rc;
   c->gp_fit_prec = c->gp_prec;
+  UT_HIP(c, hipEventRecord(c->ev_fit, c->stream));
+  c->fit_pending = true;
+  c->gp_ready = true;
+  return 0;
+}
+
+// Wait for the enqueued fit and check it (positive definite).
+int gp_wait_fit(ut_ctx* c) {
+  if (!c->fit_pending) return 0;
   int32_t flag = 0;
-  UT_HIP(c, hipMemcpyAsync(&flag, c->gp_flag, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
-  UT_HIP(c, hipStreamSynchronize(c->stream));
-  c->gp_ready = (flag == 0);
-  UT_CHECK(c, flag == 0, UT_ENOTPD, "gp_fit: kernel matrix is not positive definite (raise jitter)");
+  UT_HIP(c, hipEventSynchronize(c->ev_fit));
+  UT_HIP(c, hipMemcpy(&flag, c->gp_flag, sizeof(int32_t), hipMemcpyDeviceToHost));
+  if (flag != 0) {
+    c->gp_ready = false;
+    return set_err(c, UT_ENOTPD, "gp_fit: kernel matrix is not positive definite (raise jitter)");
+  }
   return 0;
 }
 
 int gp_score_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, const ut_acq* acq, const uint8_t* dup,
-                  double* mu, double* var, double* score) {
+                  double* mu, double* var, double* score, hipEvent_t dup_ready) {
   UT_CHECK(c, c->gp_ready, UT_EINVAL, "gp_score: call ut_gp_fit first");
   UT_CHECK(c, acq != nullptr, UT_EINVAL, "gp_score: acq is NULL");
   if (m <= 0) return 0;
+  if (c->fit_pending) UT_HIP(c, hipStreamWaitEvent(c->stream, c->ev_fit, 0));  // GP state is written by the fit
   const int32_t n = c->gp_n, d = c->gp_d;
   const int32_t npad = ((n + NPAD - 1) / NPAD) * NPAD;
   const int32_t dpad = ((d + 15) / 16) * 16;
@@ -569,9 +607,10 @@ int gp_score_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, const ut
                             ldk, npad, m, c->var_part.p)))
     return rc;
   mark(c, "var");
+  if (dup_ready) UT_HIP(c, hipStreamWaitEvent(c->stream, dup_ready, 0));
   hipLaunchKernelGGL(k_gp_finalize, dim3(grid1(m, 256)), dim3(256), 0, c->stream, m, RT, RT, c->mu_part.p,
-                     c->var_part.p, ldk, c->gp_sf2, c->gp_stats, acq->kind, acq->xi, acq->kappa, dup, mu, var,
-                     score);
+                     c->var_part.p, ldk, c->gp_sf2, c->gp_stats, c->gp_flag, acq->kind, acq->xi, acq->kappa, dup,
+                     mu, var, score);
   UT_LAUNCH_CHECK(c);
   mark(c, "finalize");
   return 0;

@@ -22,10 +22,13 @@
 //
 // One lane = one candidate.  The repr byte string is assembled in LDS in
 // [word][lane] layout (bank-conflict-free, no cross-lane traffic, so no
-// barriers); the two live 64-char hex "holes" stay in VGPRs and are indexed
-// with the wave-uniform word-table entry (s_set_gpr_idx / v_movrels, no
-// scratch).  Bound: integer VALU (~1.4k ops per SHA-256 compression, with
-// Sigma/Ch/Maj as single v_bitop3_b32).
+// barriers); the two live 64-char hex "holes" stay in one 32-register array
+// indexed by the wave-uniform word-table entry (s_set_gpr_idx / v_movrels, no
+// scratch, no per-word selects).  The word table is read with scalar loads;
+// parameter values are prefetched one parameter ahead.  Bound: integer VALU
+// (~1.45k ops per SHA-256 compression, Sigma/Ch/Maj as single v_bitop3_b32;
+// the 3-source ops issue at half rate, so ~28.5 G compressions/s is the
+// measured chip ceiling, scripts/exp/sha_rate.hip).
 #include "ut_param.h"
 
 namespace ut {
@@ -33,7 +36,7 @@ namespace ut {
 constexpr int HASH_NT = 128;
 constexpr int SCR_WORDS = 7;                       // inner message bytes 0..27
 
-typedef uint32_t hexv __attribute__((ext_vector_type(16)));
+typedef uint32_t hex32 __attribute__((ext_vector_type(32)));
 
 struct LdsEmit {
   uint8_t* base;  // &lds[0] as bytes
@@ -43,20 +46,9 @@ struct LdsEmit {
   }
 };
 
-__device__ __forceinline__ void inner_digest(const DevParam& pr, double v, const uint32_t* __restrict__ lut,
-                                             uint32_t* lds, int lane, uint32_t D[8]) {
-  if (pr.hash_mode == HM_LUT) {
-    int64_t idx;
-    if (pr.kind == UT_ENUM || pr.kind == UT_BOOL) idx = (int64_t)v;
-    else if (pr.kind == UT_POW2) idx = (int64_t)(pow2_exponent(v) - pr.lo);  // repr(exponent)
-    else idx = (int64_t)(v - pr.lo);                                       // INT, LOGINT
-    idx = idx < 0 ? 0 : (idx >= pr.lut_n ? pr.lut_n - 1 : idx);  // never fault on garbage input
-    const uint4* src = reinterpret_cast<const uint4*>(lut + (pr.lut_base + idx) * 8);
-    const uint4 a = src[0], b = src[1];
-    D[0] = a.x; D[1] = a.y; D[2] = a.z; D[3] = a.w;
-    D[4] = b.x; D[5] = b.y; D[6] = b.z; D[7] = b.w;
-    return;
-  }
+// sha256(repr(value)) for the non-LUT modes: the repr bytes are assembled in
+// this lane's LDS column, then one SHA-256 block
+__device__ __forceinline__ void repr_digest(const DevParam& pr, double v, uint32_t* lds, int lane, uint32_t D[8]) {
 #pragma unroll
   for (int w = 0; w < SCR_WORDS; ++w) lds[w * HASH_NT + lane] = 0u;
   LdsEmit e{reinterpret_cast<uint8_t*>(lds), lane};
@@ -75,63 +67,78 @@ __device__ __forceinline__ void inner_digest(const DevParam& pr, double v, const
   sha256_compress(D, W);
 }
 
-__device__ __forceinline__ uint32_t hex_at(const hexv& X, int32_t q) {
-  // wave-uniform q in [-1, 16]; words outside the hole read as zero bytes
-  const uint32_t v = X[q & 15];
-  return (q >= 0 && q < 16) ? v : 0u;
+// LUT row of a discrete value (the host hashed repr(get_value) of every value)
+__device__ __forceinline__ int64_t lut_row(const DevParam& pr, double v) {
+  int64_t idx;
+  if (pr.kind == UT_ENUM || pr.kind == UT_BOOL) idx = (int64_t)v;
+  else if (pr.kind == UT_POW2) idx = (int64_t)(pow2_exponent(v) - pr.lo);  // repr(exponent)
+  else idx = (int64_t)(v - pr.lo);                                       // INT, LOGINT
+  idx = idx < 0 ? 0 : (idx >= pr.lut_n ? pr.lut_n - 1 : idx);  // never fault on garbage input
+  return pr.lut_base + idx;
 }
 
 __global__ __launch_bounds__(HASH_NT) void k_hash(const DevParam* __restrict__ params,
                                                   const int32_t* __restrict__ order,
-                                                  const HashWord* __restrict__ words,
-                                                  const int16_t* __restrict__ block_last, int32_t nblocks,
-                                                  const uint32_t* __restrict__ lut, const double* __restrict__ values,
-                                                  int64_t ld, int64_t m, uint32_t* __restrict__ out) {
+                                                  const uint2* __restrict__ words,
+                                                  const int32_t* __restrict__ block_last, int32_t nblocks,
+                                                  int32_t P, const uint4* __restrict__ lut,
+                                                  const double* __restrict__ values, int64_t ld, int64_t m,
+                                                  uint32_t* __restrict__ out) {
   __shared__ uint32_t lds[SCR_WORDS * HASH_NT];
   const int lane = threadIdx.x;
   const int64_t i0 = (int64_t)blockIdx.x * HASH_NT + lane;
   const bool valid = i0 < m;
   const int64_t i = valid ? i0 : (m - 1);
-  hexv hx0 = {}, hx1 = {};
+  hex32 HX = {};  // two 16-word hex slots: hole j in HX[16 (j % 2) .. 16 (j % 2) + 15]
   uint32_t H[8];
   sha256_init(H);
   int32_t next = 0;
+  // the value of the next parameter to digest is loaded one parameter ahead
+  double vnext = values[(int64_t)order[0] * ld + i];
   for (int32_t b = 0; b < nblocks; ++b) {
     const int32_t last = block_last[b];
     while (next <= last) {
       const int32_t p = order[next];
       const DevParam pr = params[p];
-      const double v = values[(int64_t)p * ld + i];
+      const double v = vnext;
       uint32_t D[8];
-      inner_digest(pr, v, lut, lds, lane, D);
-      hexv h;
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        h[2 * k] = hex4(D[k] >> 16);
-        h[2 * k + 1] = hex4(D[k] & 0xFFFFu);
+      if (pr.hash_mode == HM_LUT) {
+        const uint4* src = lut + 2 * lut_row(pr, v);
+        const uint4 a = src[0], c = src[1];  // issued before the prefetch: waits leave it in flight
+        if (next + 1 < P) vnext = values[(int64_t)order[next + 1] * ld + i];
+        D[0] = a.x; D[1] = a.y; D[2] = a.z; D[3] = a.w;
+        D[4] = c.x; D[5] = c.y; D[6] = c.z; D[7] = c.w;
+      } else {
+        if (next + 1 < P) vnext = values[(int64_t)order[next + 1] * ld + i];
+        repr_digest(pr, v, lds, lane, D);
       }
-      if (next & 1) hx1 = h;
-      else hx0 = h;
+      // 64 hex characters as 16 big-endian words into slot next % 2
+      if (next & 1) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          HX[16 + 2 * k] = hex4(D[k] >> 16);
+          HX[16 + 2 * k + 1] = hex4(D[k] & 0xFFFFu);
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          HX[2 * k] = hex4(D[k] >> 16);
+          HX[2 * k + 1] = hex4(D[k] & 0xFFFFu);
+        }
+      }
       ++next;
     }
     uint32_t W[16];
-    const HashWord* hw = words + (int64_t)b * 16;
+    const uint2* hw = words + (int64_t)b * 16;
 #pragma unroll
     for (int w = 0; w < 16; ++w) {
-      const HashWord e = hw[w];
-      uint32_t x = e.tmpl;
-      if (e.hole >= 0) {
-        const int32_t q = (int32_t)e.q1 - 1;
-        uint32_t lo, hi;
-        if (e.hole & 1) {
-          lo = hex_at(hx1, q);
-          hi = hex_at(hx1, q + 1);
-        } else {
-          lo = hex_at(hx0, q);
-          hi = hex_at(hx0, q + 1);
-        }
+      const uint2 e = hw[w];  // scalar load: the same word for every lane
+      uint32_t x = e.x;
+      if (e.y) {
+        const uint32_t lo = (e.y & HW_LO_VALID) ? HX[e.y & 31u] : 0u;
+        const uint32_t hi = (e.y & HW_HI_VALID) ? HX[(e.y >> HW_HI_POS) & 31u] : 0u;
         const uint64_t cat = ((uint64_t)lo << 32) | hi;
-        x |= (uint32_t)((cat << (8 * e.shift)) >> 32);
+        x |= (uint32_t)((cat << ((e.y >> HW_SHIFT_POS) & 31u)) >> 32);
       }
       W[w] = x;
     }
@@ -148,7 +155,8 @@ int launch_hash(ut_ctx* c, const double* values, int64_t ld, int64_t m, uint32_t
   if (m <= 0) return 0;
   const Space& s = c->space;
   hipLaunchKernelGGL(k_hash, dim3(grid1(m, HASH_NT)), dim3(HASH_NT), 0, c->stream, s.d_params, s.d_order,
-                     s.d_words, s.d_block_last, (int32_t)s.outer_blocks, s.d_lut, values, ld, m, out);
+                     reinterpret_cast<const uint2*>(s.d_words), s.d_block_last, (int32_t)s.outer_blocks, s.P,
+                     reinterpret_cast<const uint4*>(s.d_lut), values, ld, m, out);
   UT_LAUNCH_CHECK(c);
   return 0;
 }

@@ -379,7 +379,7 @@ extern "C" int ut_pso_reset(ut_ctx* c) {
   const int64_t need = c->npop * c->space.P;
   if (c->pso_cap < need) {
     if (c->pso_vel) {
-      UT_HIP(c, hipStreamSynchronize(c->stream));
+      UT_HIP(c, ut::sync_all(c));
       hipFree(c->pso_vel);
       hipFree(c->pso_best);
     }

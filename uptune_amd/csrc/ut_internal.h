@@ -3,6 +3,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <initializer_list>
 #include <string>
 #include <vector>
 
@@ -33,12 +34,20 @@ struct DevParam {
 
 enum : int32_t { HM_LUT = 0, HM_FLOAT = 1, HM_INT = 2, HM_LOGINT = 3 };
 
-// One 32-bit word of the fixed-layout outer hash message.
+// One 32-bit word of the fixed-layout outer hash message: the constant bytes
+// plus, when the word overlaps a digest "hole", where its hex bytes come from
+// in the kernel's 32-register hex array (hole j lives in slot j % 2).  8 bytes,
+// read with scalar loads (every lane of a wave uses the same word).
 struct HashWord {
   uint32_t tmpl;   // constant bytes (zero where hex characters go)
-  int16_t hole;    // sorted-parameter position whose 64 hex chars overlap, -1 none
-  uint8_t q1;      // hex word index + 1 (0..16) of the first overlapping word
-  uint8_t shift;   // byte shift 0..3
+  uint32_t info;   // 0 = no hole; else HW_* fields
+};
+enum : uint32_t {
+  HW_LO_VALID = 1u << 6,   // bits 0..4: hex register of the word's first bytes
+  HW_HI_POS = 8,           // bits 8..12: hex register of its last bytes
+  HW_HI_VALID = 1u << 14,
+  HW_SHIFT_POS = 16,       // bits 16..20: left shift of the 64-bit concatenation, in bits
+  HW_HOLE = 1u << 31,
 };
 
 struct Space {
@@ -52,7 +61,7 @@ struct Space {
   DevParam* d_params = nullptr;
   int32_t* d_order = nullptr;             // sorted position -> param index
   HashWord* d_words = nullptr;            // outer_blocks * 16
-  int16_t* d_block_last = nullptr;        // last sorted position needed by each block
+  int32_t* d_block_last = nullptr;        // last sorted position needed by each block
   uint32_t* d_lut = nullptr;              // digests [*][8]
   double* d_vtab = nullptr;               // LOGINT get_value tables (host-computed by CPython)
 };
@@ -64,8 +73,13 @@ struct DevBuf {
 };
 
 struct Timing {
+  struct Mark {
+    std::string name;   // "" = a stream's start point, not reported
+    hipStream_t stream;
+    hipEvent_t ev;
+  };
   bool on = false;
-  std::vector<std::pair<std::string, hipEvent_t>> marks;
+  std::vector<Mark> marks;  // a stage's time = its mark - the previous mark on the same stream
   std::vector<std::pair<std::string, double>> last;
 };
 
@@ -74,8 +88,17 @@ struct Timing {
 struct ut_ctx {
   int device = 0;
   uint64_t seed = 0;
-  hipStream_t stream = nullptr;
+  hipStream_t stream = nullptr;      // the caller-visible stream (ut_set_stream)
   hipStream_t own_stream = nullptr;
+  // internal streams: a round's hash + dedup run on `side` beside the GP
+  // contractions on `stream`; an asynchronous GP fit runs on `fit_stream`
+  // beside the round's proposal / hash (joined by events, never by host waits)
+  hipStream_t side = nullptr;
+  hipStream_t fit_stream = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_fit = nullptr, ev_prefit = nullptr;
+  bool fit_pending = false;          // scoring waits on ev_fit before touching GP state
+  double* fit_host = nullptr;        // pinned staging of X, y, 1/ell for the asynchronous fit
+  size_t fit_host_n = 0;
   std::string err;
   ut::Space space;
   bool has_space = false;
@@ -148,6 +171,25 @@ namespace ut {
 
 int set_err(ut_ctx* c, int code, const std::string& msg);
 
+// wait for every stream of the context (before freeing or reusing buffers)
+inline hipError_t sync_all(ut_ctx* c) {
+  hipError_t e = hipStreamSynchronize(c->stream);
+  for (hipStream_t s : {c->side, c->fit_stream}) {
+    if (!s) continue;
+    const hipError_t e2 = hipStreamSynchronize(s);
+    if (e == hipSuccess) e = e2;
+  }
+  return e;
+}
+
+// launches inside the scope go to stream s (the launch helpers all use c->stream)
+struct StreamScope {
+  ut_ctx* c;
+  hipStream_t saved;
+  StreamScope(ut_ctx* ctx, hipStream_t s) : c(ctx), saved(ctx->stream) { ctx->stream = s; }
+  ~StreamScope() { c->stream = saved; }
+};
+
 #define UT_HIP(ctx, call)                                                                 \
   do {                                                                                    \
     hipError_t e_ = (call);                                                               \
@@ -171,7 +213,7 @@ template <class T>
 int ensure(ut_ctx* c, DevBuf<T>& b, size_t n) {
   if (b.n >= n && b.p) return 0;
   if (b.p) {
-    hipError_t e = hipStreamSynchronize(c->stream);
+    hipError_t e = ut::sync_all(c);
     (void)e;
     (void)hipFree(b.p);
     b.p = nullptr;
@@ -186,6 +228,8 @@ int ensure(ut_ctx* c, DevBuf<T>& b, size_t n) {
 }
 
 void mark(ut_ctx* c, const char* name);
+int gp_fit_enqueue(ut_ctx* c, const double* X, const double* y, int32_t n, int32_t d, const ut_gp_hyper* h);
+int gp_wait_fit(ut_ctx* c);
 
 // kernel launchers implemented in the .hip translation units
 int launch_population_init(ut_ctx* c, uint32_t round_);
@@ -200,9 +244,8 @@ int launch_hash(ut_ctx* c, const double* values, int64_t ld, int64_t m, uint32_t
 int launch_hist_insert(ut_ctx* c, const uint32_t* dig, int64_t n);
 int launch_hist_rehash(ut_ctx* c, const uint32_t* okeys, const uint32_t* ostate, int64_t ocap);
 int launch_dedup(ut_ctx* c, const uint32_t* dig, int64_t m, uint8_t* dup);
-int gp_fit_impl(ut_ctx* c, const double* X, const double* y, int32_t n, int32_t d, const ut_gp_hyper* h);
 int gp_score_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, const ut_acq* acq, const uint8_t* dup,
-                  double* mu, double* var, double* score);
+                  double* mu, double* var, double* score, hipEvent_t dup_ready = nullptr);
 int topk_impl(ut_ctx* c, const double* score, const uint8_t* dup, int64_t m, int64_t cand_base, int32_t k,
               int64_t* out_idx, double* out_score);
 int launch_gemm_kstar(ut_ctx* c, bool fp32, const double* XsT, int32_t npad, const double* ucand, int32_t dpad,

@@ -214,14 +214,17 @@ class BatchEngine:
         L.check(self.ctx, self.lib.ut_gp_set_precision(self.ctx, int(bits)), "ut_gp_set_precision")
 
     def gp_fit(self, X: np.ndarray, y: np.ndarray, lengthscale, sigma_f2: float = 1.0, sigma_n2: float = 1e-6,
-               jitter: float = 0.0):
+               jitter: float = 0.0, wait: bool = True):
+        """ut_gp_fit (wait=True) or ut_gp_fit_async (wait=False: the fit runs on the
+        device beside the next round's proposal/hash stages)"""
         X = np.ascontiguousarray(X, dtype=np.float64)
         y = np.ascontiguousarray(y, dtype=np.float64)
         n, d = X.shape
         ell = np.ascontiguousarray(np.broadcast_to(np.asarray(lengthscale, dtype=np.float64), (d,)))
         h = L.GpHyper(sigma_f2=float(sigma_f2), sigma_n2=float(sigma_n2), jitter=float(jitter),
                       lengthscale_host=ell.ctypes.data)
-        L.check(self.ctx, self.lib.ut_gp_fit(self.ctx, X.ctypes.data, y.ctypes.data, n, d, C.byref(h)), "ut_gp_fit")
+        fn = self.lib.ut_gp_fit if wait else self.lib.ut_gp_fit_async
+        L.check(self.ctx, fn(self.ctx, X.ctypes.data, y.ctypes.data, n, d, C.byref(h)), "ut_gp_fit")
 
     def gp_stats(self) -> Tuple[float, float, float]:
         a, b, c = C.c_double(), C.c_double(), C.c_double()
