@@ -22,9 +22,11 @@
  *   - work is enqueued on the context's HIP stream (ut_set_stream); results
  *     are valid once that stream is synchronised;
  *   - SoA value arrays are column-per-parameter: value of param p for
- *     candidate i lives at values[p * ld + i] (f64 for every kind: FLOAT raw
- *     value, INT/LOGINT raw integer, POW2 raw power of two, BOOL 0/1,
- *     ENUM option index);
+ *     candidate i lives at values[col(p) * ld + i] (f64 for every kind: FLOAT
+ *     raw value, INT/LOGINT raw integer, POW2 raw power of two, BOOL 0/1,
+ *     ENUM option index); a PERM of size S takes S consecutive columns
+ *     holding its item indices in order.  col(p) = p + the sum of (size - 1)
+ *     over the PERM params before p (ut_space_columns);
  *   - digests are 8 big-endian uint32 words (= sha256().digest()) per
  *     candidate, candidate-major ([m][8]);
  *   - candidate indices are GLOBAL (cand_base + i), so random streams and
@@ -61,7 +63,7 @@ enum {
   UT_POW2 = 3,   /* PowerOfTwoParameter   manipulator.py:811-836 (stored 2^e, searched e) */
   UT_BOOL = 4,   /* BooleanParameter      manipulator.py:930-996 */
   UT_ENUM = 5,   /* EnumParameter         manipulator.py:1024-1045 */
-  UT_PERM = 6    /* PermutationParameter  manipulator.py:1048-1356 (not yet) */
+  UT_PERM = 6    /* PermutationParameter  manipulator.py:1048-1356 (n_options = size) */
 };
 
 typedef struct ut_param_desc {
@@ -85,7 +87,15 @@ typedef struct ut_param_desc {
                           0 = computed on the device (correctly rounded log) */
   int32_t pad;
   const double* vtab_host;
+  /* PERM: repr(item) bytes of the n_options items, concatenated, and their
+   * n_options + 1 offsets; the inner digest is sha256(repr(list of items)),
+   * "[" + ", ".join(repr(item)) + "]" (ComplexParameter.hash_value :855-858) */
+  const uint8_t* perm_repr_host;
+  const int32_t* perm_repr_off_host;
 } ut_param_desc;
+
+/* permutation crossover operators (op3_cross_*, manipulator.py:1179-1353) */
+enum { UT_X_NONE = 0, UT_X_OX1 = 1, UT_X_OX3 = 2, UT_X_PX = 3, UT_X_CX = 4, UT_X_PMX = 5 };
 
 typedef struct ut_de_params {   /* differentialevolution.py:34-40,142-151 */
   double cr;                    /* crossover rate (0.9 DE, 0.2 DE-Alt) */
@@ -126,6 +136,8 @@ int ut_version(void);
 int ut_space_define(ut_ctx* ctx, int32_t n_params, const ut_param_desc* params, int32_t py2_layout);
 /* outer hash message length in bytes, SHA-256 block count, GP feature width */
 int ut_space_info(ut_ctx* ctx, int64_t* outer_len, int64_t* outer_blocks, int32_t* n_features);
+/* number of SoA value columns (= n_params unless the space has PERMs) */
+int ut_space_columns(ut_ctx* ctx, int32_t* n_columns);
 
 /* ---- population (DifferentialEvolution.population, PSO particles) ------- */
 /* op1_randomize every member on the device (manipulator.py:171-176,596-606) */
@@ -148,6 +160,8 @@ typedef struct ut_pso_params {
   double sigma;                 /* Int/Pow2 gaussian noise, unit scale 0.2 (manipulator.py:661) */
   int32_t alias_pbest;          /* 1 = reference: particle.best IS the position (pso.py:212-213) */
   int32_t enum_mode;            /* 0 = reference: enum never moves (manipulator.py:442); 1 = corrected */
+  int32_t crossover;            /* PERM: UT_X_* of PSO(crossover=...) (pso.py:80-84; op3_swarm :1115-1140) */
+  int32_t pad;
 } ut_pso_params;
 /* velocities := 0 and particle bests := positions (pso.py:218-221) */
 int ut_pso_reset(ut_ctx* ctx);
@@ -169,6 +183,9 @@ typedef struct ut_ga_params {
   int32_t normal;             /* 1 = NormalGreedyMutation / GGA, 0 = UniformGreedyMutation / GA */
   int32_t max_retries;        /* 10 (hash equal to a parent -> mutate again); <= 15 */
   int32_t op;                 /* RNG stream family: 4 = GA, 5 = GGA */
+  int32_t crossover;          /* GA(crossover=...): UT_X_* applied to PERM params of size > 6 when two
+                                 parents are selected (CrossoverMixin.crossover :123-134); UT_X_NONE else */
+  int32_t pad;
 } ut_ga_params;
 /* parent1/parent2: device rows [P] (the global best), NULL = random parent
  * (select() without a best result).  out_invalid[i] = 1 when all retries
@@ -178,7 +195,7 @@ int ut_propose_ga(ut_ctx* ctx, const ut_ga_params* p, const double* parent1, con
                   uint8_t* out_invalid);
 
 /* GP features of configurations: unit values (get_unit_value), BOOL 0/1,
- * ENUM one-hot.  out_features[f * ld_out + i]. */
+ * ENUM one-hot, PERM position of each item / (size - 1).  out_features[f * ld_out + i]. */
 int ut_encode_features(ut_ctx* ctx, const double* values, int64_t ld, int64_t m, double* out_features,
                        int64_t ld_out);
 

@@ -12,12 +12,15 @@ random draws are replaced by Philox draws keyed by (seed, g, stream, round):
   cross   = forced or random() < cr                     (:125)
   primitive: op4_set_linear(x1, x2, x3, 1.0, F, -F)     (manipulator.py:523-542)
   complex:   copy x1; randomize iff x2 != x3            (manipulator.py:866-914)
+             (PERM: randomize = shuffle of the x1 copy, oracle/perm.py)
   otherwise the target's value is kept (cfg = copy(parent))  (:106)
 """
 import numpy as np
 
+from . import perm as pm
 from . import philox as ph
-from .space import get_unit_value_vec, op4_set_linear_primitive, randomize, set_unit_value_vec
+from .space import (PERM, columns, get_unit_value_vec, op4_set_linear_primitive, randomize, set_unit_value_vec,
+                    width)
 
 
 def donors(g, npop, seed, round_):
@@ -57,17 +60,32 @@ def forced_mask(g, P, n_cross, seed, round_):
 
 
 def propose_de_vec(space, pop, seed, round_, cand_base, m, cr, n_cross=1):
-    """pop: SoA [P][npop] float64 -> trial SoA [P][m]"""
-    P, npop = pop.shape
+    """pop: SoA [ncols][npop] float64 -> trial SoA [ncols][m]"""
+    ncols, npop = pop.shape
+    P = len(space)
+    starts, _ = columns(space)
     g = np.arange(cand_base, cand_base + m, dtype=np.uint64)
     t, d1, d2, d3 = donors(g, npop, seed, round_)
     F = use_f(g, seed, round_)
     forced = forced_mask(g, P, n_cross, seed, round_)
-    out = np.empty((P, m), dtype=np.float64)
+    out = np.empty((ncols, m), dtype=np.float64)
     for p, prm in enumerate(space):
         x, y, _, _ = ph.draw(seed, g, p, round_, ph.OP_DE)
         cross = forced[p] | (ph.u01(x, y) < cr)
-        col = pop[p]
+        c0 = starts[p]
+        if prm.kind == PERM:
+            S = width(prm)
+            blk = pop[c0:c0 + S]
+            for j in range(m):
+                if cross[j]:
+                    v = [int(a) for a in blk[:, d1[j]]]                 # copy_value(x1)
+                    if list(blk[:, d2[j]]) != list(blk[:, d3[j]]):     # add_difference -> op1_randomize
+                        pm.shuffle(v, pm.Words(seed, g[j], p | (1 << ph.STREAM_SUB_SHIFT), round_, ph.OP_DE))
+                    out[c0:c0 + S, j] = v
+                else:
+                    out[c0:c0 + S, j] = blk[:, t[j]]
+            continue
+        col = pop[c0]
         vt = col[t]
         x1, x2, x3 = col[d1], col[d2], col[d3]
         if prm.is_primitive():
@@ -85,7 +103,7 @@ def propose_de_vec(space, pop, seed, round_, cand_base, m, cr, n_cross=1):
                 from .space import to_f64
                 nv[diff] = [to_f64(prm, randomize(prm, int(a), int(b), int(c), int(d)))
                             for a, b, c, d in zip(rx, ry, rz, rw)]
-        out[p] = np.where(cross, nv, vt)
+        out[c0] = np.where(cross, nv, vt)
     return out
 
 
@@ -103,6 +121,10 @@ def propose_de_scalar(space, pop_cfgs, seed, round_, g, cr, n_cross=1):
         if forced[p] or float(ph.u01(x, y)[0]) < cr:
             if prm.is_primitive():
                 cfg[p] = op4_set_linear_primitive(prm, x1[p], x2[p], x3[p], 1.0, F, -F, cfg[p])
+            elif prm.kind == PERM:
+                cfg[p] = list(x1[p])                # copy_value: deepcopy of the list
+                if x2[p] != x3[p]:                  # add_difference -> op1_randomize = shuffle
+                    pm.shuffle(cfg[p], pm.Words(seed, g, p | (1 << ph.STREAM_SUB_SHIFT), round_, ph.OP_DE))
             else:
                 cfg[p] = x1[p]                      # copy_value(cfg_a, cfg)
                 if x2[p] != x3[p]:                  # add_difference: not same_value -> randomize
@@ -112,14 +134,21 @@ def propose_de_scalar(space, pop_cfgs, seed, round_, g, cr, n_cross=1):
 
 
 def population_init(space, npop, seed, round_=0):
-    """op1_randomize every member (manipulator.py:171-176) -> SoA [P][npop]"""
+    """op1_randomize every member (manipulator.py:171-176) -> SoA [ncols][npop]"""
     from .space import to_f64
     g = np.arange(npop, dtype=np.uint64)
-    out = np.empty((len(space), npop), dtype=np.float64)
+    starts, nc = columns(space)
+    out = np.empty((nc, npop), dtype=np.float64)
     for p, prm in enumerate(space):
+        c0 = starts[p]
+        if prm.kind == PERM:   # seed_value() = list(items), then shuffle
+            S = width(prm)
+            for j in range(npop):
+                out[c0:c0 + S, j] = pm.randomized(pm.identity(S), pm.Words(seed, j, p, round_, ph.OP_INIT))
+            continue
         x, y, z, w = ph.draw(seed, g, p, round_, ph.OP_INIT)
         if prm.kind == 0:  # FLOAT, vectorised: lo + (hi - lo) * u
-            out[p] = prm.lo + (prm.hi - prm.lo) * ph.u01(x, y)
+            out[c0] = prm.lo + (prm.hi - prm.lo) * ph.u01(x, y)
         else:
-            out[p] = [to_f64(prm, randomize(prm, int(a), int(b), int(c), int(d))) for a, b, c, d in zip(x, y, z, w)]
+            out[c0] = [to_f64(prm, randomize(prm, int(a), int(b), int(c), int(d))) for a, b, c, d in zip(x, y, z, w)]
     return out

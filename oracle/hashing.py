@@ -17,7 +17,7 @@ which both are plain hex (pinned by samples/tutorials/tuneup.opentuner.db).
 """
 import hashlib
 
-from .space import BOOL, ENUM, FLOAT, scale
+from .space import BOOL, ENUM, FLOAT, PERM, scale
 
 
 def hash_value(p, v, py2=False):
@@ -29,7 +29,7 @@ def hash_value(p, v, py2=False):
         return inner.decode() if py2 else str(inner)
     if p.kind == BOOL:
         return hashlib.sha256(repr(bool(v)).encode()).hexdigest()
-    if p.kind == ENUM:
+    if p.kind in (ENUM, PERM):   # PERM: v is the list of items, repr(list)
         return hashlib.sha256(repr(v).encode()).hexdigest()
     raise NotImplementedError(p.kind)
 

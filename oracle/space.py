@@ -140,6 +140,46 @@ def randomize(p, x, y, z, w):
     raise NotImplementedError(p.kind)
 
 
+# ---- SoA column layout: a PERM of size S owns S columns of item indices ----
+def width(p):
+    return len(p.options) if p.kind == PERM else 1
+
+
+def columns(space):
+    """first SoA column of every param, and the column count"""
+    cols, c = [], 0
+    for p in space:
+        cols.append(c)
+        c += width(p)
+    return cols, c
+
+
+def row_values(space, soa, j):
+    """stored values of candidate j (PERM: the list of items)"""
+    cols, _ = columns(space)
+    out = []
+    for p, c in zip(space, cols):
+        if p.kind == PERM:
+            out.append([p.options[int(x)] for x in soa[c:c + width(p), j]])
+        else:
+            out.append(from_f64(p, soa[c, j]))
+    return out
+
+
+def soa_from_rows(space, rows):
+    """list of stored-value rows -> SoA [ncols][n]"""
+    cols, nc = columns(space)
+    out = np.empty((nc, len(rows)))
+    for j, row in enumerate(rows):
+        for p, c, v in zip(space, cols, row):
+            if p.kind == PERM:
+                idx = {repr(it): k for k, it in enumerate(p.options)}
+                out[c:c + width(p), j] = [idx[repr(it)] for it in v]
+            else:
+                out[c, j] = to_f64(p, v)
+    return out
+
+
 # ---- value <-> f64 column codec (the device's SoA representation) --------
 def to_f64(p, v):
     if p.kind == FLOAT:
@@ -210,10 +250,21 @@ def set_unit_value_vec(p, u, current):
 
 
 def features(space, rows_f64):
-    """GP features of SoA rows [P][n]: unit values, BOOL 0/1, ENUM one-hot
-    (the build's encoding, SURVEY.md §8(a) GP spec)."""
+    """GP features of SoA rows [ncols][n]: unit values, BOOL 0/1, ENUM one-hot,
+    PERM position of each item / (S - 1) (the build's encoding, SURVEY.md
+    §8(a) GP spec: "Perm ... position-normalised")."""
     cols = []
-    for p, col in zip(space, rows_f64):
+    starts, _ = columns(space)
+    for p, c0 in zip(space, starts):
+        col = rows_f64[c0]
+        if p.kind == PERM:
+            S = width(p)
+            pos = np.zeros((S, rows_f64.shape[1]))
+            for k in range(S):
+                items = rows_f64[c0 + k].astype(np.int64)
+                pos[items, np.arange(rows_f64.shape[1])] = (k / (S - 1)) if S > 1 else 0.0
+            cols.extend(list(pos))
+            continue
         if p.is_primitive():
             cols.append(get_unit_value_vec(p, col))
         elif p.kind == BOOL:

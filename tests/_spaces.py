@@ -1,6 +1,6 @@
 """Test helper: mirror parameter objects (uptune_amd.manipulator) -> oracle
 Param lists, and back."""
-from oracle.space import BOOL, ENUM, FLOAT, INT, LOGINT, POW2, Param
+from oracle.space import BOOL, ENUM, FLOAT, INT, LOGINT, PERM, POW2, Param
 
 
 def oracle_space(manip):
@@ -19,6 +19,8 @@ def oracle_space(manip):
             out.append(Param(p.name, BOOL))
         elif cls == "EnumParameter":
             out.append(Param(p.name, ENUM, options=list(p.options)))
+        elif cls == "PermutationParameter":
+            out.append(Param(p.name, PERM, options=list(p._items)))
         else:
             raise TypeError(cls)
     return out
@@ -26,7 +28,8 @@ def oracle_space(manip):
 
 def to_manip(space):
     from uptune_amd.manipulator import (BooleanParameter, ConfigurationManipulator, EnumParameter, FloatParameter,
-                                        IntegerParameter, LogIntegerParameter, PowerOfTwoParameter)
+                                        IntegerParameter, LogIntegerParameter, PermutationParameter,
+                                        PowerOfTwoParameter)
     m = ConfigurationManipulator()
     for p in space:
         if p.kind == FLOAT:
@@ -41,4 +44,6 @@ def to_manip(space):
             m.add_parameter(BooleanParameter(p.name))
         elif p.kind == ENUM:
             m.add_parameter(EnumParameter(p.name, p.options))
+        elif p.kind == PERM:
+            m.add_parameter(PermutationParameter(p.name, p.options))
     return m

@@ -470,3 +470,111 @@ def test_hpl_ga_matches_oracle(kw):
         want, winv = oga.propose_ga_vec(space, p1, p2, 19, 1, 3, 2000, **kw)
         np.testing.assert_array_equal(got.cpu().numpy(), want)
         np.testing.assert_array_equal(inv.cpu().numpy().astype(bool), winv)
+
+
+# --------------------------------------------------------------------------- permutations
+def perm_space():
+    from uptune_amd import spaces
+    return oracle_space(spaces.perm_mixed())
+
+
+def _row_hashes(space, vals):
+    from oracle.space import row_values
+    return [oh.hash_config(space, row_values(space, vals, j)) for j in range(vals.shape[1])]
+
+
+def test_perm_population_de_encode_hash():
+    space = perm_space()
+    e = engine(space, seed=23)
+    e.population_init(3000, round_=1)
+    pop = e.population_get().cpu().numpy()
+    np.testing.assert_array_equal(pop, ode.population_init(space, 3000, seed=23, round_=1))
+    got = e.propose_de(2500, round_=4, cand_base=11, cr=0.5, n_cross=2).cpu().numpy()
+    np.testing.assert_array_equal(got, ode.propose_de_vec(space, pop, 23, 4, 11, 2500, 0.5, 2))
+    np.testing.assert_array_equal(e.encode(dev(got)).cpu().numpy(), features(space, got))
+    assert hexes(e.hash(dev(got))) == _row_hashes(space, got)
+    # config dicts round trip through the host codec, and hash the same on the host path
+    cfgs = e.decode(dev(got[:, :20]))
+    assert isinstance(cfgs[0]["tour"], list) and sorted(cfgs[0]["tour"]) == [100 + 7 * k for k in range(40)]
+    assert e.hash_configs(cfgs) == _row_hashes(space, got[:, :20])
+
+
+@pytest.mark.parametrize("xop", ["op3_cross_OX1", "op3_cross_OX3", "op3_cross_PX", "op3_cross_CX",
+                                 "op3_cross_PMX"])
+def test_perm_pso_matches_oracle(xop):
+    from oracle import perm as opm
+    from oracle import pso as opso
+    space = perm_space()
+    e = engine(space, seed=29)
+    pop = ode.population_init(space, 600, seed=8)
+    e.population_set(dev(pop))
+    e.pso_reset()
+    gbest = pop[:, 7].copy()
+    x, v = e.propose_pso(gbest, 600, round_=2, alias_pbest=True, crossover=xop)
+    wx, wv = opso.propose_pso_vec(space, pop, np.zeros_like(pop), pop, gbest, 29, 2, 0, 600,
+                                  crossover=opm.XNAMES[xop])
+    np.testing.assert_array_equal(x.cpu().numpy(), wx)
+    np.testing.assert_array_equal(v.cpu().numpy(), wv)
+    # non-aliased bests: pso_best holds the reset positions while the positions move
+    e.pso_commit(x, v)
+    x2, v2 = e.propose_pso(gbest, 600, round_=3, alias_pbest=False, crossover=xop)
+    wx2, wv2 = opso.propose_pso_vec(space, wx, wv, pop, gbest, 29, 3, 0, 600, crossover=opm.XNAMES[xop])
+    np.testing.assert_array_equal(x2.cpu().numpy(), wx2)
+    np.testing.assert_array_equal(v2.cpu().numpy(), wv2)
+
+
+@pytest.mark.parametrize("xop", ["op3_cross_OX1", "op3_cross_OX3", "op3_cross_PX", "op3_cross_CX",
+                                 "op3_cross_PMX"])
+@pytest.mark.parametrize("normal", [False, True])
+def test_perm_ga_matches_oracle(xop, normal):
+    from oracle import ga as oga
+    from oracle import perm as opm
+    space = perm_space()
+    e = engine(space, seed=31)
+    pop = ode.population_init(space, 4, seed=6)
+    kw = dict(mutation_rate=0.2, crossover_rate=0.8, normal=normal)
+    for p1, p2 in [(pop[:, 0].copy(), pop[:, 1].copy()), (None, None), (pop[:, 2].copy(), None)]:
+        got, inv = e.propose_ga(1500, parent1=p1, parent2=p2, round_=2, cand_base=5, crossover=xop, **kw)
+        want, winv = oga.propose_ga_vec(space, p1, p2, 31, 2, 5, 1500, crossover=opm.XNAMES[xop], **kw)
+        np.testing.assert_array_equal(got.cpu().numpy(), want)
+        np.testing.assert_array_equal(inv.cpu().numpy().astype(bool), winv)
+
+
+def test_perm_gga_matches_oracle():
+    from oracle import ga as oga
+    space = perm_space()
+    e = engine(space, seed=37)
+    pop = ode.population_init(space, 4, seed=7)
+    kw = dict(mutation_rate=0.1, normal=True, crossover_rate=0.5, crossover_strength=0.2, op=5)
+    got, inv = e.propose_ga(1500, parent1=pop[:, 0].copy(), parent2=pop[:, 3].copy(), round_=1, **kw)
+    want, winv = oga.propose_ga_vec(space, pop[:, 0].copy(), pop[:, 3].copy(), 37, 1, 0, 1500, **kw)
+    np.testing.assert_array_equal(got.cpu().numpy(), want)
+    np.testing.assert_array_equal(inv.cpu().numpy().astype(bool), winv)
+
+
+def test_perm_score_round():
+    """whole DE round on a permutation space: selection == oracle's"""
+    from oracle.space import features as ofeat
+    space = perm_space()
+    e = engine(space, seed=41)
+    e.population_init(4096)
+    pop = e.population_get().cpu().numpy()
+    rng = np.random.default_rng(3)
+    Xv = ode.population_init(space, 200, seed=77)
+    X = ofeat(space, Xv).T
+    y = rng.normal(size=200)
+    e.gp_fit(X, y, lengthscale=0.7, sigma_f2=1.0, sigma_n2=1e-4, jitter=1e-8)
+    e.history_reset(0)
+    idx, top, dig, vals = e.score_round_de(4096, 32, round_=1, cr=0.3)
+    trial = ode.propose_de_vec(space, pop, 41, 1, 0, 4096, 0.3, 1)
+    g = ogp.GP(X, y, lengthscale=0.7, sigma_f2=1.0, sigma_n2=1e-4, jitter=1e-8)
+    mu, var = g.posterior(ofeat(space, trial).T)
+    ei = ogp.acquisition(mu, var, g.f_best)
+    dup = osel.dedup(_row_hashes(space, trial), set())
+    want = osel.topk(list(ei), 32, dup=dup)
+    idx_l = idx.cpu().numpy().tolist()
+    _close(top.cpu().numpy(), np.asarray([ei[g] for g in want]), atol=1e-8)
+    np.testing.assert_array_equal(vals.cpu().numpy(), trial[:, idx_l])
+    gaps = np.abs(np.diff(np.sort(np.asarray(ei)[np.asarray(dup) == 0])[::-1][:33]))
+    if gaps.min() > 1e-6:
+        assert idx_l == want

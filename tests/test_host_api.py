@@ -47,7 +47,7 @@ def test_struct_layouts():
     hc.uthc_sizeof.restype = ctypes.c_longlong
     for i, st in enumerate([L.ParamDesc, L.GpHyper, L.RoundOut, L.DeParams, L.Acq, L.PsoParams, L.GaParams]):
         assert ctypes.sizeof(st) == hc.uthc_sizeof(i), st.__name__
-    assert ctypes.sizeof(L.ParamDesc) == 96
+    assert ctypes.sizeof(L.ParamDesc) == 112
 
 
 def test_compile_space_mixed():

@@ -15,6 +15,10 @@ LIB_PATH = os.environ.get("UTHOT_LIB", os.path.join(_HERE, "libuthot.so"))
 
 UT_FLOAT, UT_INT, UT_LOGINT, UT_POW2, UT_BOOL, UT_ENUM, UT_PERM = range(7)
 UT_ACQ_EI, UT_ACQ_UCB = 0, 1
+# permutation crossover operators (op3_cross_*, manipulator.py:1179-1353)
+UT_X_NONE, UT_X_OX1, UT_X_OX3, UT_X_PX, UT_X_CX, UT_X_PMX = range(6)
+CROSSOVERS = {"op3_cross_OX1": UT_X_OX1, "op3_cross_OX3": UT_X_OX3, "op3_cross_PX": UT_X_PX,
+              "op3_cross_CX": UT_X_CX, "op3_cross_PMX": UT_X_PMX}
 
 ERRORS = {
     -1: "UT_EINVAL", -2: "UT_EHIP", -3: "UT_ENOSPACE", -4: "UT_EUNSUPPORTED", -5: "UT_ENOTPD", -6: "UT_ENOMEM",
@@ -30,6 +34,7 @@ class ParamDesc(C.Structure):
         ("name", C.c_char_p), ("name_len", C.c_int32),
         ("lut_count", C.c_int32), ("lut_host", C.c_void_p),
         ("vtab_count", C.c_int32), ("pad", C.c_int32), ("vtab_host", C.c_void_p),
+        ("perm_repr_host", C.c_void_p), ("perm_repr_off_host", C.c_void_p),
     ]
 
 
@@ -39,13 +44,14 @@ class DeParams(C.Structure):
 
 class PsoParams(C.Structure):
     _fields_ = [("omega", C.c_double), ("phi_l", C.c_double), ("phi_g", C.c_double), ("sigma", C.c_double),
-                ("alias_pbest", C.c_int32), ("enum_mode", C.c_int32)]
+                ("alias_pbest", C.c_int32), ("enum_mode", C.c_int32), ("crossover", C.c_int32),
+                ("pad", C.c_int32)]
 
 
 class GaParams(C.Structure):
     _fields_ = [("mutation_rate", C.c_double), ("sigma", C.c_double), ("crossover_rate", C.c_double),
                 ("crossover_strength", C.c_double), ("must_mutate_count", C.c_int32), ("normal", C.c_int32),
-                ("max_retries", C.c_int32), ("op", C.c_int32)]
+                ("max_retries", C.c_int32), ("op", C.c_int32), ("crossover", C.c_int32), ("pad", C.c_int32)]
 
 
 class GpHyper(C.Structure):
@@ -75,6 +81,7 @@ SIGNATURES = {
     "ut_sync": (C.c_int, [P]),
     "ut_space_define": (C.c_int, [P, I32, C.POINTER(ParamDesc), I32]),
     "ut_space_info": (C.c_int, [P, C.POINTER(I64), C.POINTER(I64), C.POINTER(I32)]),
+    "ut_space_columns": (C.c_int, [P, C.POINTER(I32)]),
     "ut_population_init": (C.c_int, [P, I64, U32]),
     "ut_population_set": (C.c_int, [P, I64, P, I64]),
     "ut_population_get": (C.c_int, [P, P, I64]),

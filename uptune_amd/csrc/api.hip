@@ -57,6 +57,9 @@ static void free_space(Space& s) {
   if (s.d_block_last) hipFree(s.d_block_last);
   if (s.d_lut) hipFree(s.d_lut);
   if (s.d_vtab) hipFree(s.d_vtab);
+  for (void* q : {(void*)s.d_order_col, (void*)s.d_perm_params, (void*)s.d_perm_bytes, (void*)s.d_perm_off,
+                  (void*)s.d_perm_offbase, (void*)s.d_perm_len})
+    if (q) hipFree(q);
   s = Space();
 }
 
@@ -228,11 +231,17 @@ int ut_space_define(ut_ctx* c, int32_t P, const ut_param_desc* params, int32_t p
   std::vector<bool> primitive(P);
   std::vector<uint32_t> lut;
   std::vector<double> vtab;
-  int32_t feat = 0;
+  std::vector<int32_t> perm_params, perm_off, perm_offbase, perm_len;
+  std::vector<uint8_t> perm_bytes;
+  int32_t feat = 0, col = 0;
   for (int32_t p = 0; p < P; ++p) {
     const ut_param_desc& d = params[p];
     DevParam& q = s.host_params[p];
     q.kind = d.kind;
+    q.col = col;
+    q.psize = 1;
+    q.wcol = 0;
+    q.pslot = -1;
     q.lo = d.lo; q.hi = d.hi;
     q.u_lo = d.u_lo; q.u_hi = d.u_hi; q.u_span = d.u_span;
     q.n_opt = d.n_options;
@@ -261,11 +270,42 @@ int ut_space_define(ut_ctx* c, int32_t P, const ut_param_desc* params, int32_t p
       case UT_ENUM:
         UT_CHECK(c, d.n_options >= 1, UT_EINVAL, "space: enum needs options");
         q.n_feat = (int32_t)d.n_options; primitive[p] = false; break;
+      case UT_PERM: {
+        // PermutationParameter(name, items): S columns of item indices,
+        // inner digest sha256(repr(list)) computed on the device from the
+        // items' repr bytes (a fixed-length message per space)
+        UT_CHECK(c, d.n_options >= 1 && d.n_options <= 65536, UT_EINVAL, "space: permutation size must be in [1, 65536]");
+        UT_CHECK(c, d.perm_repr_host && d.perm_repr_off_host, UT_EINVAL, "space: permutation needs item reprs");
+        const int32_t S = (int32_t)d.n_options;
+        q.psize = S;
+        q.n_opt = S;
+        q.n_feat = S;
+        q.wcol = s.perm_cols;
+        q.pslot = s.n_perm;
+        q.hash_mode = HM_PERM;
+        primitive[p] = false;
+        perm_params.push_back(p);
+        perm_offbase.push_back((int32_t)perm_off.size());
+        const int32_t base = (int32_t)perm_bytes.size();
+        const int32_t* off = d.perm_repr_off_host;
+        UT_CHECK(c, off[0] == 0, UT_EINVAL, "space: permutation repr offsets must start at 0");
+        for (int32_t k = 0; k < S; ++k)
+          UT_CHECK(c, off[k + 1] > off[k], UT_EINVAL, "space: empty item repr");
+        perm_bytes.insert(perm_bytes.end(), d.perm_repr_host, d.perm_repr_host + off[S]);
+        for (int32_t k = 0; k <= S; ++k) perm_off.push_back(base + off[k]);
+        perm_len.push_back(2 + off[S] + 2 * (S - 1));  // "[" items joined by ", " "]"
+        s.n_perm += 1;
+        s.perm_cols += S;
+        if (S > s.perm_smax) s.perm_smax = S;
+        break;
+      }
       default:
         return set_err(c, UT_EUNSUPPORTED, "space: parameter kind " + std::to_string(d.kind) +
                                                " is not supported on the device path yet");
     }
     feat += q.n_feat;
+    col += q.psize;
+    if (d.kind == UT_PERM) continue;
     if (d.kind == UT_LOGINT && d.vtab_count > 0) {
       UT_CHECK(c, d.vtab_host != nullptr, UT_EINVAL, "space: vtab_count > 0 but vtab_host is NULL");
       q.vtab_base = (int64_t)vtab.size();
@@ -292,6 +332,7 @@ int ut_space_define(ut_ctx* c, int32_t P, const ut_param_desc* params, int32_t p
     }
   }
   s.n_feat = feat;
+  s.ncols = col;
   UT_HIP(c, hipMalloc((void**)&s.d_params, sizeof(DevParam) * P));
   UT_HIP(c, hipMemcpy(s.d_params, s.host_params.data(), sizeof(DevParam) * P, hipMemcpyHostToDevice));
   UT_HIP(c, hipMalloc((void**)&s.d_order, sizeof(int32_t) * P));
@@ -302,6 +343,24 @@ int ut_space_define(ut_ctx* c, int32_t P, const ut_param_desc* params, int32_t p
   if (vtab.empty()) vtab.resize(1, 0.0);
   UT_HIP(c, hipMalloc((void**)&s.d_vtab, sizeof(double) * vtab.size()));
   UT_HIP(c, hipMemcpy(s.d_vtab, vtab.data(), sizeof(double) * vtab.size(), hipMemcpyHostToDevice));
+  {
+    std::vector<int32_t> order_col(P);
+    for (int32_t j = 0; j < P; ++j) order_col[j] = s.host_params[s.host_order[j]].col;
+    UT_HIP(c, hipMalloc((void**)&s.d_order_col, sizeof(int32_t) * P));
+    UT_HIP(c, hipMemcpy(s.d_order_col, order_col.data(), sizeof(int32_t) * P, hipMemcpyHostToDevice));
+  }
+  if (s.n_perm > 0) {
+    auto up = [&](auto*& dst, const auto& v) -> hipError_t {
+      hipError_t e = hipMalloc((void**)&dst, sizeof(v[0]) * v.size());
+      if (e != hipSuccess) return e;
+      return hipMemcpy(dst, v.data(), sizeof(v[0]) * v.size(), hipMemcpyHostToDevice);
+    };
+    UT_HIP(c, up(s.d_perm_params, perm_params));
+    UT_HIP(c, up(s.d_perm_bytes, perm_bytes));
+    UT_HIP(c, up(s.d_perm_off, perm_off));
+    UT_HIP(c, up(s.d_perm_offbase, perm_offbase));
+    UT_HIP(c, up(s.d_perm_len, perm_len));
+  }
   int rc = compile_hash_layout(c, names, primitive);
   if (rc) return rc;
   c->has_space = true;
@@ -324,8 +383,15 @@ int ut_space_info(ut_ctx* c, int64_t* outer_len, int64_t* outer_blocks, int32_t*
   return 0;
 }
 
+int ut_space_columns(ut_ctx* c, int32_t* n_columns) {
+  if (!c) return UT_EINVAL;
+  UT_CHECK(c, c->has_space, UT_ENOSPACE, "space not defined");
+  if (n_columns) *n_columns = c->space.ncols;
+  return 0;
+}
+
 static int pop_alloc(ut_ctx* c, int64_t npop) {
-  const int64_t need = npop * c->space.P;
+  const int64_t need = npop * c->space.ncols;
   if (c->pop && c->pop_cap >= need) {
     c->npop = npop;
     return 0;
@@ -357,7 +423,7 @@ int ut_population_set(ut_ctx* c, int64_t npop, const double* values, int64_t ld)
   int rc = pop_alloc(c, npop);
   if (rc) return rc;
   UT_HIP(c, hipMemcpy2DAsync(c->pop, sizeof(double) * npop, values, sizeof(double) * ld, sizeof(double) * npop,
-                             c->space.P, hipMemcpyDeviceToDevice, c->stream));
+                             c->space.ncols, hipMemcpyDeviceToDevice, c->stream));
   return 0;
 }
 
@@ -365,7 +431,7 @@ int ut_population_get(ut_ctx* c, double* values, int64_t ld) {
   if (!c) return UT_EINVAL;
   UT_CHECK(c, c->pop != nullptr && values && ld >= c->npop, UT_EINVAL, "population_get: bad arguments");
   UT_HIP(c, hipMemcpy2DAsync(values, sizeof(double) * ld, c->pop, sizeof(double) * c->npop,
-                             sizeof(double) * c->npop, c->space.P, hipMemcpyDeviceToDevice, c->stream));
+                             sizeof(double) * c->npop, c->space.ncols, hipMemcpyDeviceToDevice, c->stream));
   return 0;
 }
 
@@ -514,9 +580,9 @@ int ut_score_round_de(ut_ctx* c, const ut_de_params* de, const ut_acq* acq, uint
   UT_CHECK(c, c->gp_d == c->space.n_feat, UT_EINVAL, "score_round: GP feature width != space feature width");
   UT_CHECK(c, m >= 1 && de && acq, UT_EINVAL, "score_round: bad arguments");
   const int64_t ld = ((m + 127) / 128) * 128;
-  const int32_t P = c->space.P, F = c->space.n_feat;
+  const int32_t NC = c->space.ncols, F = c->space.n_feat;
   int rc;
-  if ((rc = ensure(c, c->r_values, (size_t)P * ld))) return rc;
+  if ((rc = ensure(c, c->r_values, (size_t)NC * ld))) return rc;
   if ((rc = ensure(c, c->r_feat, (size_t)F * ld))) return rc;
   if ((rc = ensure(c, c->r_digest, (size_t)8 * ld))) return rc;
   if ((rc = ensure(c, c->r_dup, (size_t)ld))) return rc;
@@ -562,7 +628,7 @@ int ut_score_round_de(ut_ctx* c, const ut_de_params* de, const ut_acq* acq, uint
       double* vals = out->topk_values;
       ut::DevBuf<double> tmp;
       if (!vals) {
-        if ((rc = ensure(c, tmp, (size_t)P * k))) return rc;
+        if ((rc = ensure(c, tmp, (size_t)NC * k))) return rc;
         vals = tmp.p;
       }
       rc = launch_gather_rows(c, c->r_values.p, ld, c->r_topk_idx.p, cand_base, k, vals, k, c->r_digest.p,

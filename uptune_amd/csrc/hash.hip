@@ -38,13 +38,15 @@ constexpr int SCR_WORDS = 7;                       // inner message bytes 0..27
 
 typedef uint32_t hex32 __attribute__((ext_vector_type(32)));
 
-struct LdsEmit {
+template <int NT>
+struct LdsEmitN {
   uint8_t* base;  // &lds[0] as bytes
   int lane;
   __device__ __forceinline__ void put(int pos, uint8_t ch) {
-    base[(((pos >> 2) * HASH_NT + lane) << 2) + (pos & 3)] = ch;
+    base[(((pos >> 2) * NT + lane) << 2) + (pos & 3)] = ch;
   }
 };
+using LdsEmit = LdsEmitN<HASH_NT>;
 
 // sha256(repr(value)) for the non-LUT modes: the repr bytes are assembled in
 // this lane's LDS column, then one SHA-256 block
@@ -77,12 +79,76 @@ __device__ __forceinline__ int64_t lut_row(const DevParam& pr, double v) {
   return pr.lut_base + idx;
 }
 
+// sha256(repr(list of items)) of every PERM param: "[" + ", ".join(repr(item))
+// + "]" streamed through a 64-byte block in this lane's LDS column.  The
+// message length is constant per param (a permutation of fixed items).
+constexpr int PD_NT = 128;
+
+__global__ __launch_bounds__(PD_NT) void k_perm_digest(const DevParam* __restrict__ params,
+                                                       const int32_t* __restrict__ perm_params, int32_t n_perm,
+                                                       const uint8_t* __restrict__ bytes,
+                                                       const int32_t* __restrict__ off,
+                                                       const int32_t* __restrict__ offbase,
+                                                       const int32_t* __restrict__ msg_len,
+                                                       const double* __restrict__ values, int64_t ld, int64_t m,
+                                                       uint32_t* __restrict__ out) {
+  __shared__ uint32_t lds[16 * PD_NT];
+  const int lane = threadIdx.x;
+  const int64_t i = (int64_t)blockIdx.x * PD_NT + lane;
+  if (i >= m) return;  // no barriers below: every lane owns its LDS column
+  LdsEmitN<PD_NT> e{reinterpret_cast<uint8_t*>(lds), lane};
+  for (int32_t q = 0; q < n_perm; ++q) {
+    const DevParam pr = params[perm_params[q]];
+    const int32_t S = pr.psize;
+    const int32_t* o = off + offbase[q];
+    uint32_t H[8];
+    sha256_init(H);
+#pragma unroll
+    for (int w = 0; w < 16; ++w) lds[w * PD_NT + lane] = 0u;
+    int32_t fill = 0;
+    auto flush = [&]() {
+      uint32_t W[16];
+#pragma unroll
+      for (int w = 0; w < 16; ++w) {
+        W[w] = __builtin_bswap32(lds[w * PD_NT + lane]);
+        lds[w * PD_NT + lane] = 0u;
+      }
+      sha256_compress(H, W);
+      fill = 0;
+    };
+    auto emit = [&](uint8_t ch) {
+      e.put(fill, ch);
+      if (++fill == 64) flush();
+    };
+    emit('[');
+    for (int32_t k = 0; k < S; ++k) {
+      if (k > 0) { emit(','); emit(' '); }
+      int32_t item = (int32_t)values[(int64_t)(pr.col + k) * ld + i];
+      item = item < 0 ? 0 : (item >= S ? S - 1 : item);  // never fault on garbage input
+      for (int32_t b = o[item]; b < o[item + 1]; ++b) emit(bytes[b]);
+    }
+    emit(']');
+    emit(0x80);
+    if (fill > 56) {
+      while (fill != 0) emit(0);
+    }
+    while (fill < 56) emit(0);
+    const uint64_t bits = (uint64_t)msg_len[q] * 8u;
+    for (int b = 7; b >= 0; --b) emit((uint8_t)(bits >> (8 * b)));  // completes (and flushes) the block
+    uint4* dst = reinterpret_cast<uint4*>(out + ((int64_t)q * m + i) * 8);
+    dst[0] = make_uint4(H[0], H[1], H[2], H[3]);
+    dst[1] = make_uint4(H[4], H[5], H[6], H[7]);
+  }
+}
+
 __global__ __launch_bounds__(HASH_NT) void k_hash(const DevParam* __restrict__ params,
                                                   const int32_t* __restrict__ order,
+                                                  const int32_t* __restrict__ order_col,
                                                   const uint2* __restrict__ words,
                                                   const int32_t* __restrict__ block_last, int32_t nblocks,
                                                   int32_t P, const uint4* __restrict__ lut,
                                                   const double* __restrict__ values, int64_t ld, int64_t m,
+                                                  const uint4* __restrict__ perm_dig,
                                                   uint32_t* __restrict__ out) {
   __shared__ uint32_t lds[SCR_WORDS * HASH_NT];
   const int lane = threadIdx.x;
@@ -94,7 +160,7 @@ __global__ __launch_bounds__(HASH_NT) void k_hash(const DevParam* __restrict__ p
   sha256_init(H);
   int32_t next = 0;
   // the value of the next parameter to digest is loaded one parameter ahead
-  double vnext = values[(int64_t)order[0] * ld + i];
+  double vnext = values[(int64_t)order_col[0] * ld + i];
   for (int32_t b = 0; b < nblocks; ++b) {
     const int32_t last = block_last[b];
     while (next <= last) {
@@ -105,11 +171,17 @@ __global__ __launch_bounds__(HASH_NT) void k_hash(const DevParam* __restrict__ p
       if (pr.hash_mode == HM_LUT) {
         const uint4* src = lut + 2 * lut_row(pr, v);
         const uint4 a = src[0], c = src[1];  // issued before the prefetch: waits leave it in flight
-        if (next + 1 < P) vnext = values[(int64_t)order[next + 1] * ld + i];
+        if (next + 1 < P) vnext = values[(int64_t)order_col[next + 1] * ld + i];
+        D[0] = a.x; D[1] = a.y; D[2] = a.z; D[3] = a.w;
+        D[4] = c.x; D[5] = c.y; D[6] = c.z; D[7] = c.w;
+      } else if (pr.hash_mode == HM_PERM) {
+        const uint4* src = perm_dig + 2 * ((int64_t)pr.pslot * m + i);
+        const uint4 a = src[0], c = src[1];
+        if (next + 1 < P) vnext = values[(int64_t)order_col[next + 1] * ld + i];
         D[0] = a.x; D[1] = a.y; D[2] = a.z; D[3] = a.w;
         D[4] = c.x; D[5] = c.y; D[6] = c.z; D[7] = c.w;
       } else {
-        if (next + 1 < P) vnext = values[(int64_t)order[next + 1] * ld + i];
+        if (next + 1 < P) vnext = values[(int64_t)order_col[next + 1] * ld + i];
         repr_digest(pr, v, lds, lane, D);
       }
       // 64 hex characters as 16 big-endian words into slot next % 2
@@ -154,9 +226,20 @@ __global__ __launch_bounds__(HASH_NT) void k_hash(const DevParam* __restrict__ p
 int launch_hash(ut_ctx* c, const double* values, int64_t ld, int64_t m, uint32_t* out) {
   if (m <= 0) return 0;
   const Space& s = c->space;
+  const uint32_t* pd = nullptr;
+  if (s.n_perm > 0) {
+    int rc = ensure(c, c->perm_dig, (size_t)s.n_perm * (size_t)m * 8);
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_perm_digest, dim3(grid1(m, PD_NT)), dim3(PD_NT), 0, c->stream, s.d_params, s.d_perm_params,
+                       s.n_perm, s.d_perm_bytes, s.d_perm_off, s.d_perm_offbase, s.d_perm_len, values, ld, m,
+                       c->perm_dig.p);
+    UT_LAUNCH_CHECK(c);
+    pd = c->perm_dig.p;
+  }
   hipLaunchKernelGGL(k_hash, dim3(grid1(m, HASH_NT)), dim3(HASH_NT), 0, c->stream, s.d_params, s.d_order,
-                     reinterpret_cast<const uint2*>(s.d_words), s.d_block_last, (int32_t)s.outer_blocks, s.P,
-                     reinterpret_cast<const uint4*>(s.d_lut), values, ld, m, out);
+                     s.d_order_col, reinterpret_cast<const uint2*>(s.d_words), s.d_block_last,
+                     (int32_t)s.outer_blocks, s.P, reinterpret_cast<const uint4*>(s.d_lut), values, ld, m,
+                     reinterpret_cast<const uint4*>(pd), out);
   UT_LAUNCH_CHECK(c);
   return 0;
 }

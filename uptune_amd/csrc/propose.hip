@@ -14,7 +14,13 @@
 //   set_unit_value      manipulator.py:490-503
 //   op4_set_linear      manipulator.py:523-542 (primitive), :866-914 (complex)
 //   DE trial            differentialevolution.py:105-129
+//   PERM operators      manipulator.py:1048-1356 (ut_perm.h)
+//
+// Column model: param p's values start at SoA column params[p].col; a PERM
+// of size S owns S columns (item indices).  Per-param random draws are keyed
+// by the PARAM index, so spaces without PERMs (col == p) are unchanged.
 #include "ut_param.h"
+#include "ut_perm.h"
 
 namespace ut {
 
@@ -25,8 +31,16 @@ __global__ __launch_bounds__(256) void k_population_init(const DevParam* __restr
   if (i >= npop) return;
   for (int32_t p = 0; p < P; ++p) {
     const DevParam pr = params[p];
+    if (pr.kind == UT_PERM) {
+      // seed_value() = list(items), then op1_randomize = shuffle
+      WRow x{pop + (int64_t)pr.col * ld + i, ld};
+      perm_identity(x, pr.psize);
+      PermRng R(seed, (uint64_t)i, (uint32_t)p, round_, OP_INIT);
+      perm_shuffle(x, pr.psize, R);
+      continue;
+    }
     const u32x4 r = draw(seed, (uint64_t)i, (uint32_t)p, round_, OP_INIT);
-    pop[(int64_t)p * ld + i] = randomize(pr, r);
+    pop[(int64_t)pr.col * ld + i] = randomize(pr, r);
   }
 }
 
@@ -95,12 +109,28 @@ __global__ __launch_bounds__(256) void k_de(const DevParam* __restrict__ params,
     bool forced = false;
 #pragma unroll
     for (int s = 0; s < 4; ++s) forced |= (s < n_cross) && ((uint32_t)fk[s] == (uint32_t)p) && (fk[s] != ~0ull);
-    const double* col = pop + (int64_t)p * ldp;
-    const double vt = col[t];
-    double v = vt;
+    const double* col = pop + (int64_t)pr.col * ldp;
     // `i < n_cross or random() < cr` (short-circuit: the draw is only
     // consulted for non-forced params, which is what selecting on it does)
-    if (forced || u01_from(r.x, r.y) < cr) {
+    const bool cross = forced || u01_from(r.x, r.y) < cr;
+    if (pr.kind == UT_PERM) {
+      // ComplexParameter.op4_set_linear: copy x1, shuffle it iff x2 != x3
+      const int32_t S = pr.psize;
+      WRow o{out + (int64_t)pr.col * ldo + i, ldo};
+      if (cross) {
+        perm_copy(o, PRow{col + d1, ldp}, S);
+        if (!perm_equal(PRow{col + d2, ldp}, PRow{col + d3, ldp}, S)) {
+          PermRng R(seed, g, (uint32_t)p | (1u << STREAM_SUB_SHIFT), round_, OP_DE);
+          perm_shuffle(o, S, R);
+        }
+      } else {
+        perm_copy(o, PRow{col + t, ldp}, S);
+      }
+      continue;
+    }
+    const double vt = col[t];
+    double v = vt;
+    if (cross) {
       const double x1 = col[d1], x2 = col[d2], x3 = col[d3];
       if (is_primitive(pr.kind)) {
         const double va = unit_of(pr, x1, vtab), vb = unit_of(pr, x2, vtab), vc = unit_of(pr, x3, vtab);
@@ -118,7 +148,7 @@ __global__ __launch_bounds__(256) void k_de(const DevParam* __restrict__ params,
         }
       }
     }
-    out[(int64_t)p * ldo + i] = v;
+    out[(int64_t)pr.col * ldo + i] = v;
   }
 }
 
@@ -130,11 +160,19 @@ __global__ __launch_bounds__(256) void k_encode(const DevParam* __restrict__ par
   if (i >= m) return;
   for (int32_t p = 0; p < P; ++p) {
     const DevParam pr = params[p];
-    const double v = values[(int64_t)p * ld + i];
+    const double v = values[(int64_t)pr.col * ld + i];
     if (is_primitive(pr.kind)) {
       feat[(int64_t)pr.feat_col * ldf + i] = unit_of(pr, v, vtab);
     } else if (pr.kind == UT_BOOL) {
       feat[(int64_t)pr.feat_col * ldf + i] = v;
+    } else if (pr.kind == UT_PERM) {
+      // position of each item, normalised: feature[item] = k / (S - 1)
+      const int32_t S = pr.psize;
+      for (int32_t k = 0; k < S; ++k) {
+        int32_t item = (int32_t)values[(int64_t)(pr.col + k) * ld + i];
+        item = item < 0 ? 0 : (item >= S ? S - 1 : item);  // never fault on garbage input
+        feat[(int64_t)(pr.feat_col + item) * ldf + i] = S > 1 ? (double)k / (double)(S - 1) : 0.0;
+      }
     } else {
       const int64_t o = (int64_t)v;
       for (int64_t k = 0; k < pr.n_opt; ++k) feat[(int64_t)(pr.feat_col + k) * ldf + i] = (k == o) ? 1.0 : 0.0;
@@ -142,7 +180,7 @@ __global__ __launch_bounds__(256) void k_encode(const DevParam* __restrict__ par
   }
 }
 
-__global__ void k_gather_rows(int32_t P, const double* __restrict__ values, int64_t ld,
+__global__ void k_gather_rows(int32_t NC, const double* __restrict__ values, int64_t ld,
                               const int64_t* __restrict__ idx, int64_t cand_base, int32_t k,
                               double* __restrict__ out, int64_t ldo, const uint32_t* __restrict__ dig,
                               uint32_t* __restrict__ out_dig) {
@@ -150,45 +188,63 @@ __global__ void k_gather_rows(int32_t P, const double* __restrict__ values, int6
   if (j >= k) return;
   const int64_t g = idx[j];
   const int64_t i = g - cand_base;
-  for (int32_t p = 0; p < P; ++p) out[(int64_t)p * ldo + j] = (g >= 0) ? values[(int64_t)p * ld + i] : 0.0;
+  for (int32_t p = 0; p < NC; ++p) out[(int64_t)p * ldo + j] = (g >= 0) ? values[(int64_t)p * ld + i] : 0.0;
   if (out_dig) {
     for (int w = 0; w < 8; ++w) out_dig[(int64_t)j * 8 + w] = (g >= 0) ? dig[i * 8 + w] : 0u;
   }
 }
 
-__global__ void k_pop_replace(int32_t P, double* __restrict__ pop, int64_t ldp, const double* __restrict__ trial,
+__global__ void k_pop_replace(int32_t NC, double* __restrict__ pop, int64_t ldp, const double* __restrict__ trial,
                               int64_t ld, const int64_t* __restrict__ idx, int64_t n) {
   const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= n) return;
   const int64_t dst = idx[j];
-  for (int32_t p = 0; p < P; ++p) pop[(int64_t)p * ldp + dst] = trial[(int64_t)p * ld + j];
+  for (int32_t p = 0; p < NC; ++p) pop[(int64_t)p * ldp + dst] = trial[(int64_t)p * ld + j];
 }
 
 // ---------------------------------------------------------------------------
 // PSO: HybridParticle.move (pso.py:70-77) with the per-kind op3_swarm
-// (manipulator.py:660-700 Int, :709-744 Float, :962-996 Bool, :409-443 Enum).
-// Candidate g moves particle g % npop:  cfg = x, cfg1 = gbest, cfg2 = pbest,
-// c = omega, c1 = phi_g, c2 = phi_l.
+// (manipulator.py:660-700 Int, :709-744 Float, :962-996 Bool, :409-443 Enum,
+// :1115-1140 Permutation).  Candidate g moves particle g % npop:  cfg = x,
+// cfg1 = gbest, cfg2 = pbest, c = omega, c1 = phi_g, c2 = phi_l.
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_pso(const DevParam* __restrict__ params, int32_t P,
                                              const double* __restrict__ vtab, const double* __restrict__ pos, const double* __restrict__ vel,
                                              const double* __restrict__ pbest, int64_t ldp, int64_t npop,
                                              const double* __restrict__ gbest, double c, double c1, double c2,
-                                             double sigma, int32_t enum_mode, uint64_t seed, uint32_t round_,
-                                             int64_t cand_base, int64_t m, double* __restrict__ out_x,
-                                             double* __restrict__ out_v, int64_t ldo) {
+                                             double sigma, int32_t enum_mode, int32_t xop, uint64_t seed,
+                                             uint32_t round_, int64_t cand_base, int64_t m, double* __restrict__ out_x,
+                                             double* __restrict__ out_v, int64_t ldo, double* __restrict__ ws,
+                                             int64_t ldw, int32_t scr_col) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= m) return;
   const uint64_t g = (uint64_t)(cand_base + i);
   const int64_t t = (int64_t)(g % (uint64_t)npop);
   for (int32_t p = 0; p < P; ++p) {
     const DevParam pr = params[p];
-    const int64_t o = (int64_t)p * ldp + t;
+    const int64_t o = (int64_t)pr.col * ldp + t;
+    const u32x4 r = draw(seed, g, (uint32_t)p, round_, OP_PSO);
+    if (pr.kind == UT_PERM) {
+      // op3_swarm: if uniform(0,1) > c: op3_cross(cfg, cfg, g if uniform(0,1) < c1 else l)
+      const int32_t S = pr.psize;
+      const PRow x{pos + o, ldp};
+      WRow ox{out_x + (int64_t)pr.col * ldo + i, ldo};
+      if (u01_from(r.x, r.y) > c) {
+        const PRow other = (u01_from(r.z, r.w) < c1) ? PRow{gbest + pr.col, 1} : PRow{pbest + o, ldp};
+        PermRng R(seed, g, (uint32_t)p | (1u << STREAM_SUB_SHIFT), round_, OP_PSO);
+        perm_cross(xop, ox, x, other, S, (int32_t)rint((double)S * 0.3), WRow{ws + (int64_t)scr_col * ldw + i, ldw},
+                   R);
+      } else {
+        perm_copy(ox, x, S);
+      }
+      if (out_v)  // op3_swarm returns None: the particle keeps no velocity for it
+        for (int32_t k = 0; k < S; ++k) out_v[(int64_t)(pr.col + k) * ldo + i] = 0.0;
+      continue;
+    }
     // scaled kinds move in their search scale (get_value / set_value):
     // LOGINT by the Float rule on log values, POW2 by the Int rule on exponents
     const double xr = pos[o], v = vel[o];
-    const double x = scaled_of(pr, xr, vtab), l = scaled_of(pr, pbest[o], vtab), gb = scaled_of(pr, gbest[p], vtab);
-    const u32x4 r = draw(seed, g, (uint32_t)p, round_, OP_PSO);
+    const double x = scaled_of(pr, xr, vtab), l = scaled_of(pr, pbest[o], vtab), gb = scaled_of(pr, gbest[pr.col], vtab);
     const double r1 = u01_from(r.x, r.y), r2 = u01_from(r.z, r.w);
     double nx, nv;
     if (pr.kind == UT_ENUM) {
@@ -199,7 +255,7 @@ __global__ __launch_bounds__(256) void k_pso(const DevParam* __restrict__ params
         const double rr = u01_from(q.x, q.y);
         const double tot = (c + c1) + c2;
         const double w0 = c / tot, w1 = c1 / tot;
-        nx = rr < w0 ? xr : (rr < w0 + w1 ? gbest[p] : pbest[o]);
+        nx = rr < w0 ? xr : (rr < w0 + w1 ? gbest[pr.col] : pbest[o]);
       }
     } else {
       nv = ((v * c) + (((gb - x) * c1) * r1)) + (((l - x) * c2) * r2);
@@ -222,48 +278,85 @@ __global__ __launch_bounds__(256) void k_pso(const DevParam* __restrict__ params
         nx = ((s - u01_from(q.x, q.y)) > 0.0) ? 1.0 : 0.0;
       }
     }
-    out_x[(int64_t)p * ldo + i] = nx;
-    if (out_v) out_v[(int64_t)p * ldo + i] = nv;
+    out_x[(int64_t)pr.col * ldo + i] = nx;
+    if (out_v) out_v[(int64_t)pr.col * ldo + i] = nv;
   }
 }
 
 // ---------------------------------------------------------------------------
 // GA family: EvolutionaryTechnique.desired_configuration
-// (evolutionarytechniques.py:29-61), NormalMutationMixin (:98-114), GGA
-// crossover (globalGA.py:227-235).  Random d-subsets ("first d of a shuffle")
-// by selection sampling, one uniform per parameter (oracle/ga.py).
+// (evolutionarytechniques.py:29-61), NormalMutationMixin (:98-114),
+// CrossoverMixin (:117-134, PERM params of size > 6), GGA crossover
+// (globalGA.py:227-235).  Random d-subsets ("first d of a shuffle") by
+// selection sampling, one uniform per parameter (oracle/ga.py).
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ double parent_value(const DevParam& pr, const double* parent, int32_t p, uint32_t sub,
                                                uint64_t seed, uint64_t g, uint32_t round_, uint32_t op) {
-  if (parent) return parent[p];
+  if (parent) return parent[pr.col];
   return randomize(pr, draw(seed, g, (uint32_t)p | (sub << STREAM_SUB_SHIFT), round_, op));
+}
+
+// the permutation of a parent: its row (broadcast), or a random one
+// materialised in the workspace (manipulator.random() = seed + shuffle)
+__device__ __forceinline__ PRow parent_perm(const DevParam& pr, const double* parent, int32_t p, uint32_t sub,
+                                            uint64_t seed, uint64_t g, uint32_t round_, uint32_t op, double* wsc,
+                                            int64_t ldw, bool build) {
+  if (parent) return PRow{parent + pr.col, 1};  // a host-supplied row: contiguous
+  WRow w{wsc, ldw};
+  if (build) {
+    perm_identity(w, pr.psize);
+    PermRng R(seed, g, (uint32_t)p | (sub << STREAM_SUB_SHIFT), round_, op);
+    perm_shuffle(w, pr.psize, R);
+  }
+  return w.ro();
 }
 
 __global__ __launch_bounds__(256) void k_ga(const DevParam* __restrict__ params, int32_t P,
                                             const double* __restrict__ vtab, const double* __restrict__ parent1, const double* __restrict__ parent2,
                                             double mutation_rate, double sigma, double crossover_rate, int32_t d_cross,
-                                            int32_t must, int32_t normal, int32_t max_retries, uint32_t op,
+                                            int32_t must, int32_t normal, int32_t max_retries, uint32_t op, int32_t xop,
                                             uint64_t seed, uint32_t round_, int64_t cand_base, int64_t m,
-                                            double* __restrict__ out, int64_t ldo, uint8_t* __restrict__ invalid) {
+                                            double* __restrict__ out, int64_t ldo, uint8_t* __restrict__ invalid,
+                                            double* __restrict__ ws, int64_t ldw, int32_t perm_cols) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= m) return;
   const uint64_t g = (uint64_t)(cand_base + i);
   const u32x4 rc = draw(seed, g, STREAM_CAND | 0u, round_, op);
   const bool two = u01_from(rc.x, rc.y) < crossover_rate;
   const double* p2row = parent2 ? parent2 : parent1;  // select() twice returns the same best config
-  // parent 1 (and the GGA crossover from parent 2)
+  const uint32_t sub2 = 3u;  // random second parent (both parents NULL)
+  const int32_t scr_col = 2 * perm_cols;
+  // parent 1 (and the GGA crossover from parent 2, the GA crossover of permutations)
   double chosen = 0.0;
   for (int32_t p = 0; p < P; ++p) {
     const DevParam pr = params[p];
-    double v = parent_value(pr, parent1, p, 2u, seed, g, round_, op);
+    bool from2 = false;
     if (d_cross > 0 && two) {
       const u32x4 q = draw(seed, g, (uint32_t)p | (4u << STREAM_SUB_SHIFT), round_, op);
       if ((double)(P - p) * u01_from(q.x, q.y) < (double)d_cross - chosen) {
         chosen += 1.0;
-        v = parent_value(pr, p2row, p, 3u, seed, g, round_, op);
+        from2 = true;
       }
     }
-    out[(int64_t)p * ldo + i] = v;
+    if (pr.kind == UT_PERM) {
+      const int32_t S = pr.psize;
+      const PRow a = parent_perm(pr, parent1, p, 2u, seed, g, round_, op, ws + (int64_t)pr.wcol * ldw + i, ldw, true);
+      const PRow b = parent_perm(pr, p2row, p, sub2, seed, g, round_, op,
+                                 ws + (int64_t)(perm_cols + pr.wcol) * ldw + i, ldw, true);
+      WRow o{out + (int64_t)pr.col * ldo + i, ldo};
+      if (from2) {
+        perm_copy(o, b, S);
+      } else if (two && xop != X_NONE && S > 6) {
+        PermRng R(seed, g, (uint32_t)p | (5u << STREAM_SUB_SHIFT), round_, op);
+        perm_cross(xop, o, a, b, S, S / 3, WRow{ws + (int64_t)scr_col * ldw + i, ldw}, R);
+      } else {
+        perm_copy(o, a, S);
+      }
+      continue;
+    }
+    double v = parent_value(pr, parent1, p, 2u, seed, g, round_, op);
+    if (from2) v = parent_value(pr, p2row, p, sub2, seed, g, round_, op);
+    out[(int64_t)pr.col * ldo + i] = v;
   }
   bool accepted = false;
   for (int32_t r = 0; r < max_retries && !accepted; ++r) {
@@ -279,7 +372,29 @@ __global__ __launch_bounds__(256) void k_ga(const DevParam* __restrict__ params,
         mut = true;
       }
       mut = mut || (u01_from(q.z, q.w) < mutation_rate);
-      const int64_t o = (int64_t)p * ldo + i;
+      if (pr.kind == UT_PERM) {
+        const int32_t S = pr.psize;
+        WRow o{out + (int64_t)pr.col * ldo + i, ldo};
+        if (mut) {
+          // uniform: op1_randomize; normal: random.choice(manipulators) =
+          // [op1_randomize, op1_small_random_change]
+          PermRng R(seed, g, sp | (1u << STREAM_SUB_SHIFT), round_, op);
+          bool small = false;
+          if (normal) {
+            const u32x4 qc = draw(seed, g, sp | (1u << STREAM_SUB_SHIFT), round_, op);
+            small = below64(u64_from(qc.z, qc.w), 2) == 1;
+          }
+          if (small) perm_small_change(o, S, R);
+          else perm_shuffle(o, S, R);
+        }
+        const PRow a = parent_perm(pr, parent1, p, 2u, seed, g, round_, op, ws + (int64_t)pr.wcol * ldw + i, ldw, false);
+        const PRow b = parent_perm(pr, p2row, p, sub2, seed, g, round_, op,
+                                   ws + (int64_t)(perm_cols + pr.wcol) * ldw + i, ldw, false);
+        diff1 |= !perm_equal(o.ro(), a, S);
+        diff2 |= !perm_equal(o.ro(), b, S);
+        continue;
+      }
+      const int64_t o = (int64_t)pr.col * ldo + i;
       double v = out[o];
       if (mut) {
         if (normal && is_primitive(pr.kind)) {
@@ -298,13 +413,28 @@ __global__ __launch_bounds__(256) void k_ga(const DevParam* __restrict__ params,
         out[o] = v;
       }
       const double a = parent_value(pr, parent1, p, 2u, seed, g, round_, op);
-      const double b = parent_value(pr, p2row, p, 3u, seed, g, round_, op);
+      const double b = parent_value(pr, p2row, p, sub2, seed, g, round_, op);
       diff1 |= d_to_bits(v) != d_to_bits(a);
       diff2 |= d_to_bits(v) != d_to_bits(b);
     }
     accepted = diff1 && (!two || diff2);
   }
   if (invalid) invalid[i] = accepted ? 0 : 1;
+}
+
+// workspace of the PERM operators: GA parents + crossover scratch, [slot][ldw]
+static int perm_workspace(ut_ctx* c, int64_t m, double** ws, int64_t* ldw) {
+  const Space& s = c->space;
+  *ws = nullptr;
+  *ldw = 0;
+  if (s.n_perm == 0) return 0;
+  const int64_t l = ((m + 63) / 64) * 64;
+  const int64_t slots = 2 * (int64_t)s.perm_cols + 3 * (int64_t)s.perm_smax;
+  int rc = ensure(c, c->perm_ws, (size_t)(slots * l));
+  if (rc) return rc;
+  *ws = c->perm_ws.p;
+  *ldw = l;
+  return 0;
 }
 
 int launch_population_init(ut_ctx* c, uint32_t round_) {
@@ -326,10 +456,14 @@ int launch_de(ut_ctx* c, const ut_de_params* p, uint32_t round_, int64_t cand_ba
 int launch_pso(ut_ctx* c, const ut_pso_params* a, const double* gbest, uint32_t round_, int64_t cand_base,
                int64_t m, double* out_x, double* out_v, int64_t ld) {
   const double* pb = a->alias_pbest ? c->pop : c->pso_best;
+  double* ws;
+  int64_t ldw;
+  int rc = perm_workspace(c, m, &ws, &ldw);
+  if (rc) return rc;
   hipLaunchKernelGGL(k_pso, dim3(grid1(m, 256)), dim3(256), 0, c->stream, c->space.d_params, c->space.P,
                      c->space.d_vtab, c->pop,
                      c->pso_vel, pb, c->npop, c->npop, gbest, a->omega, a->phi_g, a->phi_l, a->sigma, a->enum_mode,
-                     c->seed, round_, cand_base, m, out_x, out_v, ld);
+                     a->crossover, c->seed, round_, cand_base, m, out_x, out_v, ld, ws, ldw, 2 * c->space.perm_cols);
   UT_LAUNCH_CHECK(c);
   return 0;
 }
@@ -337,10 +471,15 @@ int launch_pso(ut_ctx* c, const ut_pso_params* a, const double* gbest, uint32_t 
 int launch_ga(ut_ctx* c, const ut_ga_params* a, const double* parent1, const double* parent2, uint32_t round_,
               int64_t cand_base, int64_t m, double* out, int64_t ld, uint8_t* invalid) {
   const int32_t d = (int32_t)(a->crossover_strength * (double)c->space.P);  // int(strength * len(params))
+  double* ws;
+  int64_t ldw;
+  int rc = perm_workspace(c, m, &ws, &ldw);
+  if (rc) return rc;
   hipLaunchKernelGGL(k_ga, dim3(grid1(m, 256)), dim3(256), 0, c->stream, c->space.d_params, c->space.P,
                      c->space.d_vtab, parent1,
                      parent2, a->mutation_rate, a->sigma, a->crossover_rate, d, a->must_mutate_count, a->normal,
-                     a->max_retries, (uint32_t)a->op, c->seed, round_, cand_base, m, out, ld, invalid);
+                     a->max_retries, (uint32_t)a->op, a->crossover, c->seed, round_, cand_base, m, out, ld, invalid,
+                     ws, ldw, c->space.perm_cols);
   UT_LAUNCH_CHECK(c);
   return 0;
 }
@@ -354,7 +493,7 @@ int launch_encode(ut_ctx* c, const double* values, int64_t ld, int64_t m, double
 
 int launch_gather_rows(ut_ctx* c, const double* values, int64_t ld, const int64_t* idx, int64_t cand_base,
                        int32_t k, double* out, int64_t ldo, const uint32_t* dig, uint32_t* out_dig) {
-  hipLaunchKernelGGL(k_gather_rows, dim3(grid1(k, 64)), dim3(64), 0, c->stream, c->space.P, values, ld, idx,
+  hipLaunchKernelGGL(k_gather_rows, dim3(grid1(k, 64)), dim3(64), 0, c->stream, c->space.ncols, values, ld, idx,
                      cand_base, k, out, ldo, dig, out_dig);
   UT_LAUNCH_CHECK(c);
   return 0;
@@ -367,7 +506,7 @@ extern "C" int ut_population_replace(ut_ctx* c, const double* trial, int64_t ld,
   UT_CHECK(c, c->has_space, UT_ENOSPACE, "space not defined");
   UT_CHECK(c, c->pop != nullptr, UT_EINVAL, "population not initialised");
   if (n <= 0) return 0;
-  hipLaunchKernelGGL(ut::k_pop_replace, dim3(ut::grid1(n, 64)), dim3(64), 0, c->stream, c->space.P, c->pop,
+  hipLaunchKernelGGL(ut::k_pop_replace, dim3(ut::grid1(n, 64)), dim3(64), 0, c->stream, c->space.ncols, c->pop,
                      c->npop, trial, ld, idx, n);
   UT_LAUNCH_CHECK(c);
   return 0;
@@ -376,7 +515,7 @@ extern "C" int ut_population_replace(ut_ctx* c, const double* trial, int64_t ld,
 extern "C" int ut_pso_reset(ut_ctx* c) {
   if (!c) return UT_EINVAL;
   UT_CHECK(c, c->has_space && c->pop != nullptr, UT_EINVAL, "pso_reset: population not initialised");
-  const int64_t need = c->npop * c->space.P;
+  const int64_t need = c->npop * c->space.ncols;
   if (c->pso_cap < need) {
     if (c->pso_vel) {
       UT_HIP(c, ut::sync_all(c));
@@ -396,12 +535,11 @@ extern "C" int ut_propose_pso(ut_ctx* c, const ut_pso_params* a, const double* g
                               int64_t cand_base, int64_t m, double* out_values, double* out_vel, int64_t ld) {
   if (!c) return UT_EINVAL;
   UT_CHECK(c, c->has_space && c->pop != nullptr, UT_EINVAL, "propose_pso: population not initialised");
-  UT_CHECK(c, c->pso_vel != nullptr && c->pso_cap >= c->npop * c->space.P, UT_EINVAL,
+  UT_CHECK(c, c->pso_vel != nullptr && c->pso_cap >= c->npop * c->space.ncols, UT_EINVAL,
            "propose_pso: call ut_pso_reset after (re)initialising the population");
   UT_CHECK(c, a && gbest && out_values && m >= 0 && cand_base >= 0 && ld >= m, UT_EINVAL,
            "propose_pso: bad arguments");
-  for (int32_t p = 0; p < c->space.P; ++p)
-    UT_CHECK(c, c->space.host_params[p].kind != UT_PERM, UT_EUNSUPPORTED, "propose_pso: permutation params");
+  UT_CHECK(c, a->crossover >= UT_X_NONE && a->crossover <= UT_X_PMX, UT_EINVAL, "propose_pso: bad crossover");
   if (m == 0) return 0;
   return ut::launch_pso(c, a, gbest, round_, cand_base, m, out_values, out_vel, ld);
 }
@@ -413,10 +551,10 @@ extern "C" int ut_pso_commit(ut_ctx* c, const double* values, const double* vel,
            UT_EINVAL, "pso_commit: bad arguments");
   if (m == 0) return 0;
   UT_HIP(c, hipMemcpy2DAsync(c->pop + cand_base, sizeof(double) * c->npop, values, sizeof(double) * ld,
-                             sizeof(double) * m, c->space.P, hipMemcpyDeviceToDevice, c->stream));
+                             sizeof(double) * m, c->space.ncols, hipMemcpyDeviceToDevice, c->stream));
   if (vel)
     UT_HIP(c, hipMemcpy2DAsync(c->pso_vel + cand_base, sizeof(double) * c->npop, vel, sizeof(double) * ld,
-                               sizeof(double) * m, c->space.P, hipMemcpyDeviceToDevice, c->stream));
+                               sizeof(double) * m, c->space.ncols, hipMemcpyDeviceToDevice, c->stream));
   return 0;
 }
 
@@ -424,7 +562,7 @@ extern "C" int ut_pso_update_best(ut_ctx* c, const double* values, int64_t ld, c
   if (!c) return UT_EINVAL;
   UT_CHECK(c, c->pso_best != nullptr && values && idx && n >= 0, UT_EINVAL, "pso_update_best: bad arguments");
   if (n == 0) return 0;
-  hipLaunchKernelGGL(ut::k_pop_replace, dim3(ut::grid1(n, 64)), dim3(64), 0, c->stream, c->space.P, c->pso_best,
+  hipLaunchKernelGGL(ut::k_pop_replace, dim3(ut::grid1(n, 64)), dim3(64), 0, c->stream, c->space.ncols, c->pso_best,
                      c->npop, values, ld, idx, n);
   UT_LAUNCH_CHECK(c);
   return 0;
@@ -440,8 +578,7 @@ extern "C" int ut_propose_ga(ut_ctx* c, const ut_ga_params* a, const double* par
   UT_CHECK(c, a->must_mutate_count >= 0 && a->must_mutate_count <= c->space.P, UT_EINVAL,
            "propose_ga: must_mutate_count out of range");
   UT_CHECK(c, a->op >= 0 && a->op < 256, UT_EINVAL, "propose_ga: op must fit 8 bits");
-  for (int32_t p = 0; p < c->space.P; ++p)
-    UT_CHECK(c, c->space.host_params[p].kind != UT_PERM, UT_EUNSUPPORTED, "propose_ga: permutation params");
+  UT_CHECK(c, a->crossover >= UT_X_NONE && a->crossover <= UT_X_PMX, UT_EINVAL, "propose_ga: bad crossover");
   if (m == 0) return 0;
   return ut::launch_ga(c, a, parent1, parent2, round_, cand_base, m, out_values, ld, out_invalid);
 }

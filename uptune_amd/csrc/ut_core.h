@@ -107,6 +107,19 @@ UT_HD u32x4 draw(uint64_t seed, uint64_t cand, uint32_t stream, uint32_t round_,
   return philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
 }
 
+// Permutation-operator draw sites (oracle/perm.py): a site (seed, cand,
+// stream, round, op) yields a stream of 32-bit words; block b of it is the
+// Philox block with op | 0x80 and key_hi ^ b.
+enum : uint32_t { OP_PERM_FLAG = 0x80u };
+UT_HD u32x4 perm_block(uint64_t seed, uint64_t cand, uint32_t stream, uint32_t round_, uint32_t op, uint32_t blk) {
+  u32x4 c;
+  c.x = (uint32_t)cand;
+  c.y = (uint32_t)(cand >> 32);
+  c.z = stream;
+  c.w = (round_ << 8) | ((op | OP_PERM_FLAG) & 0xFFu);
+  return philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32) ^ blk);
+}
+
 // ---------------------------------------------------------------------------
 // SHA-256 (FIPS 180-4)
 // ---------------------------------------------------------------------------

@@ -30,9 +30,13 @@ struct DevParam {
   int32_t n_feat;      // GP feature columns of this param
   int64_t vtab_base;   // LOGINT: first entry of get_value(v) for v = lo.. in the value table
   int64_t vtab_n;      // LOGINT: table entries; 0 = compute the log on the device
+  int32_t col;         // first SoA value column (PERM: `psize` columns of item indices)
+  int32_t psize;       // PERM: permutation size S; 1 for every other kind
+  int32_t wcol;        // PERM: first of its S columns in the GA parent workspace
+  int32_t pslot;       // PERM: slot of its inner digest in the per-round perm digest buffer
 };
 
-enum : int32_t { HM_LUT = 0, HM_FLOAT = 1, HM_INT = 2, HM_LOGINT = 3 };
+enum : int32_t { HM_LUT = 0, HM_FLOAT = 1, HM_INT = 2, HM_LOGINT = 3, HM_PERM = 4 };
 
 // One 32-bit word of the fixed-layout outer hash message: the constant bytes
 // plus, when the word overlaps a digest "hole", where its hex bytes come from
@@ -51,7 +55,11 @@ enum : uint32_t {
 };
 
 struct Space {
-  int32_t P = 0;
+  int32_t P = 0;                          // parameters
+  int32_t ncols = 0;                      // SoA value columns (P + sum over PERM of size - 1)
+  int32_t n_perm = 0;                     // PERM parameters
+  int32_t perm_cols = 0;                  // sum of PERM sizes
+  int32_t perm_smax = 0;                  // largest PERM size
   int32_t n_feat = 0;
   int32_t py2 = 0;
   std::vector<DevParam> host_params;
@@ -64,6 +72,12 @@ struct Space {
   int32_t* d_block_last = nullptr;        // last sorted position needed by each block
   uint32_t* d_lut = nullptr;              // digests [*][8]
   double* d_vtab = nullptr;               // LOGINT get_value tables (host-computed by CPython)
+  int32_t* d_order_col = nullptr;         // sorted position -> first value column
+  int32_t* d_perm_params = nullptr;       // PERM param indices, by digest slot
+  uint8_t* d_perm_bytes = nullptr;        // concatenated repr(item) bytes of every PERM param
+  int32_t* d_perm_off = nullptr;          // per PERM param: S + 1 offsets into d_perm_bytes
+  int32_t* d_perm_offbase = nullptr;      // per PERM slot: first entry in d_perm_off
+  int32_t* d_perm_len = nullptr;          // per PERM slot: len(repr(list)) (constant per param)
 };
 
 template <class T>
@@ -160,6 +174,8 @@ struct ut_ctx {
   ut::DevBuf<double> tk_score[2];
   ut::DevBuf<int64_t> tk_idx[2];
   ut::DevBuf<int64_t> r_topk_idx;
+  ut::DevBuf<double> perm_ws;    // [2 * perm_cols + 3 * perm_smax][ld]: GA parents + crossover scratch
+  ut::DevBuf<uint32_t> perm_dig; // [n_perm][m][8] inner digests of PERM values (hash pre-pass)
   ut::DevBuf<double> r_topk_score;
   int64_t r_ld = 0;
   int64_t r_m = 0;

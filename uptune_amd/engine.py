@@ -36,6 +36,16 @@ def hex_to_digests(hexes: Sequence[str]) -> np.ndarray:
     return raw.astype(np.uint32)
 
 
+def _xop(name) -> int:
+    if name is None:
+        return L.UT_X_NONE
+    if isinstance(name, int):
+        return name
+    if name not in L.CROSSOVERS:
+        raise ValueError(f"unknown permutation crossover {name!r} (one of {sorted(L.CROSSOVERS)})")
+    return L.CROSSOVERS[name]
+
+
 class BatchEngine:
     """One device context over one search space."""
 
@@ -101,7 +111,7 @@ class BatchEngine:
         self.npop = n
 
     def population_get(self) -> torch.Tensor:
-        out = self._empty(self.spec.P, self.npop)
+        out = self._empty(self.spec.ncols, self.npop)
         L.check(self.ctx, self.lib.ut_population_get(self.ctx, _ptr(out), self.npop), "ut_population_get")
         return out
 
@@ -115,7 +125,7 @@ class BatchEngine:
     def propose_de(self, m: int, round_: int = 0, cand_base: int = 0, cr: float = 0.2, n_cross: int = 1,
                    out: Optional[torch.Tensor] = None) -> torch.Tensor:
         if out is None:
-            out = self._empty(self.spec.P, m)
+            out = self._empty(self.spec.ncols, m)
         p = L.DeParams(cr=float(cr), n_cross=int(n_cross))
         L.check(self.ctx, self.lib.ut_propose_de(self.ctx, C.byref(p), int(round_), int(cand_base), int(m),
                                                  _ptr(out), out.stride(0)), "ut_propose_de")
@@ -133,13 +143,14 @@ class BatchEngine:
 
     def propose_pso(self, gbest, m: int, round_: int = 0, cand_base: int = 0, omega: float = 0.5,
                     phi_l: float = 0.5, phi_g: float = 0.5, sigma: float = 0.2, alias_pbest: bool = True,
-                    enum_mode: int = 0):
-        """HybridParticle.move for particles (cand_base + i) % npop (pso.py:70-77)."""
+                    enum_mode: int = 0, crossover: str = "op3_cross_OX1"):
+        """HybridParticle.move for particles (cand_base + i) % npop (pso.py:70-77);
+        `crossover` is PSO(crossover=...) for permutation params (pso.py:80-84)."""
         gb = self._row(gbest)
-        x = self._empty(self.spec.P, m)
-        v = self._empty(self.spec.P, m)
+        x = self._empty(self.spec.ncols, m)
+        v = self._empty(self.spec.ncols, m)
         a = L.PsoParams(omega=omega, phi_l=phi_l, phi_g=phi_g, sigma=sigma, alias_pbest=1 if alias_pbest else 0,
-                        enum_mode=int(enum_mode))
+                        enum_mode=int(enum_mode), crossover=_xop(crossover))
         L.check(self.ctx, self.lib.ut_propose_pso(self.ctx, C.byref(a), _ptr(gb), int(round_), int(cand_base), int(m),
                                                   _ptr(x), _ptr(v), m), "ut_propose_pso")
         return x, v
@@ -151,15 +162,16 @@ class BatchEngine:
     def propose_ga(self, m: int, parent1=None, parent2=None, round_: int = 0, cand_base: int = 0,
                    mutation_rate: float = 0.1, sigma: float = 0.1, crossover_rate: float = 0.0,
                    crossover_strength: float = 0.0, must_mutate_count: int = 1, normal: bool = False,
-                   max_retries: int = 10, op: int = 4):
+                   max_retries: int = 10, op: int = 4, crossover: Optional[str] = None):
         """EvolutionaryTechnique / GGA proposals (evolutionarytechniques.py:29-61,
-        globalGA.py:187-235); returns (values [P][m], invalid [m])."""
+        globalGA.py:187-235); `crossover` = GA(crossover=...) for permutation
+        params (CrossoverMixin, :117-134).  Returns (values [ncols][m], invalid [m])."""
         p1, p2 = self._row(parent1), self._row(parent2)
-        out = self._empty(self.spec.P, m)
+        out = self._empty(self.spec.ncols, m)
         inv = self._empty(m, dtype=torch.uint8)
         a = L.GaParams(mutation_rate=mutation_rate, sigma=sigma, crossover_rate=crossover_rate,
                        crossover_strength=crossover_strength, must_mutate_count=must_mutate_count,
-                       normal=1 if normal else 0, max_retries=max_retries, op=op)
+                       normal=1 if normal else 0, max_retries=max_retries, op=op, crossover=_xop(crossover))
         L.check(self.ctx, self.lib.ut_propose_ga(self.ctx, C.byref(a), _ptr(p1), _ptr(p2), int(round_),
                                                  int(cand_base), int(m), _ptr(out), m, _ptr(inv)), "ut_propose_ga")
         return out, inv
@@ -260,7 +272,7 @@ class BatchEngine:
         idx = self._empty(k, dtype=torch.int64)
         top = self._empty(k)
         dig = self._empty(k, 8, dtype=torch.int32)
-        vals = self._empty(self.spec.P, k) if want_values else None
+        vals = self._empty(self.spec.ncols, k) if want_values else None
         out = L.RoundOut(topk_idx=idx.data_ptr(), topk_score=top.data_ptr(), topk_digest=dig.data_ptr(),
                          topk_values=vals.data_ptr() if vals is not None else None)
         L.check(self.ctx, self.lib.ut_score_round_de(self.ctx, C.byref(de), C.byref(acq), int(round_),

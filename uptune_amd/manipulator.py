@@ -132,7 +132,8 @@ class EnumParameter(ComplexParameter):
 
 
 class PermutationParameter(ComplexParameter):
-    """host API only in this round (device path: UT_EUNSUPPORTED)."""
+    """ordering of `items` (manipulator.py:1048-1356); on the device a value is
+    `size` SoA columns of item indices."""
 
     def __init__(self, name, items):
         super().__init__(name)
@@ -210,8 +211,22 @@ class ParamSpec:
     options: List[Any] = field(default_factory=list)
     feat_col: int = 0
     n_feat: int = 1
+    col: int = 0          # first SoA value column
+    width: int = 1        # SoA columns (PERM: its size)
     lut: bytes = b""
     vtab: Any = None      # LOGINT: float64 get_value table
+
+    def to_columns(self, v) -> List[float]:
+        """stored value -> its SoA column values"""
+        if self.kind == L.UT_PERM:
+            index = {repr(it): k for k, it in enumerate(self.options)}
+            return [float(index[repr(it)]) for it in v]
+        return [self.to_value(v)]
+
+    def from_columns(self, xs):
+        if self.kind == L.UT_PERM:
+            return [self.options[int(x)] for x in xs]
+        return self.from_value(xs[0])
 
     def to_value(self, v) -> float:
         if self.kind == L.UT_FLOAT:
@@ -246,21 +261,26 @@ class SpaceSpec:
     def P(self) -> int:
         return len(self.params)
 
+    @property
+    def ncols(self) -> int:
+        return sum(p.width for p in self.params)
+
     def names(self) -> List[Any]:
         return [p.name for p in self.params]
 
     def encode_configs(self, cfgs: Sequence[Dict[Any, Any]]) -> np.ndarray:
-        """configs -> SoA [P][n] float64"""
-        out = np.empty((self.P, len(cfgs)), dtype=np.float64)
+        """configs -> SoA [ncols][n] float64"""
+        out = np.empty((self.ncols, len(cfgs)), dtype=np.float64)
         for j, cfg in enumerate(cfgs):
-            for p, ps in enumerate(self.params):
-                out[p, j] = ps.to_value(cfg[ps.name])
+            for ps in self.params:
+                out[ps.col:ps.col + ps.width, j] = ps.to_columns(cfg[ps.name])
         return out
 
     def decode_values(self, values: np.ndarray) -> List[Dict[Any, Any]]:
-        """SoA [P][n] -> configs"""
+        """SoA [ncols][n] -> configs"""
         n = values.shape[1]
-        return [{ps.name: ps.from_value(values[p, j]) for p, ps in enumerate(self.params)} for j in range(n)]
+        return [{ps.name: ps.from_columns(values[ps.col:ps.col + ps.width, j]) for ps in self.params}
+                for j in range(n)]
 
 
 def unit_bounds(kind: int, lo, hi):
@@ -280,6 +300,7 @@ def compile_space(params) -> SpaceSpec:
         params = params.params
     specs: List[ParamSpec] = []
     feat = 0
+    col = 0
     for p in params:
         kind = _kind_of(p)
         ps = ParamSpec(name=p.name, kind=kind)
@@ -317,12 +338,18 @@ def compile_space(params) -> SpaceSpec:
             ps.options = list(p.options)
             ps.n_feat = len(ps.options)
             ps.lut = b"".join(_digest(repr(o)) for o in ps.options)
-        else:
-            # still compiled so the host API can describe it; the device
-            # rejects these kinds in ut_space_define
-            ps.n_feat = 1
+        elif kind == L.UT_PERM:
+            # PermutationParameter(name, items): item indices in `size` columns;
+            # GP features = each item's position / (size - 1)
+            ps.options = list(p._items)
+            ps.width = len(ps.options)
+            ps.n_feat = len(ps.options)
+            if len({repr(it) for it in ps.options}) != len(ps.options):
+                raise ValueError(f"permutation {p.name!r}: items must have distinct reprs")
         ps.feat_col = feat
+        ps.col = col
         feat += ps.n_feat
+        col += ps.width
         specs.append(ps)
     order = sorted(range(len(specs)), key=lambda i: specs[i].name)
     return SpaceSpec(params=specs, order=order, n_features=feat)
@@ -342,6 +369,13 @@ def to_descs(spec: SpaceSpec):
         d.lo, d.hi = ps.lo, ps.hi
         d.u_lo, d.u_hi, d.u_span = ps.u_lo, ps.u_hi, ps.u_span
         d.n_options = len(ps.options)
+        if ps.kind == L.UT_PERM:
+            reprs = [repr(it).encode("utf-8") for it in ps.options]
+            rb = np.frombuffer(b"".join(reprs), dtype=np.uint8).copy()
+            ro = np.concatenate([[0], np.cumsum([len(r) for r in reprs])]).astype(np.int32)
+            keep += [rb, ro]
+            d.perm_repr_host = rb.ctypes.data
+            d.perm_repr_off_host = ro.ctypes.data
         nb = str(ps.name).encode("utf-8")
         keep.append(nb)
         d.name = nb

@@ -401,9 +401,10 @@ class GpuDifferentialEvolution(GpuBatchTechnique):
 class GpuPSO(GpuBatchTechnique):
     """Batched PSO (pso.py:11-77); particles move toward the driver's best."""
 
-    def __init__(self, omega=0.5, phi_l=0.5, phi_g=0.5, enum_mode=0, *pargs, **kwargs):
+    def __init__(self, omega=0.5, phi_l=0.5, phi_g=0.5, enum_mode=0, crossover="op3_cross_OX1", *pargs, **kwargs):
         super().__init__(*pargs, **kwargs)
         self.omega, self.phi_l, self.phi_g, self.enum_mode = omega, phi_l, phi_g, enum_mode
+        self.crossover = crossover   # PSO(crossover=...) for permutation params (pso.py:80-84)
 
     def init_population(self):
         super().init_population()
@@ -417,7 +418,8 @@ class GpuPSO(GpuBatchTechnique):
             gb = self.engine.spec.encode_configs([best])[:, 0]
         npop = self.engine.npop
         x, v = self.engine.propose_pso(gb, min(m, npop), round_=self.round, cand_base=0, omega=self.omega,
-                                       phi_l=self.phi_l, phi_g=self.phi_g, enum_mode=self.enum_mode)
+                                       phi_l=self.phi_l, phi_g=self.phi_g, enum_mode=self.enum_mode,
+                                       crossover=self.crossover)
         self.engine.pso_commit(x, v, cand_base=0)   # HybridParticle.move mutates the particle in place
         return x, None
 
@@ -427,11 +429,13 @@ class GpuGA(GpuBatchTechnique):
     (evolutionarytechniques.py:13-158)."""
 
     def __init__(self, mutation_rate=0.1, crossover_rate=0.0, must_mutate_count=1, normal=False, sigma=0.1,
-                 crossover_strength=0.0, op=4, *pargs, **kwargs):
+                 crossover_strength=0.0, op=4, crossover=None, *pargs, **kwargs):
         super().__init__(*pargs, **kwargs)
+        # crossover: GA(crossover='op3_cross_OX3', ...) -- applied to permutation
+        # params of size > 6 when two parents are selected (:117-134, :144-148)
         self.ga = dict(mutation_rate=mutation_rate, crossover_rate=crossover_rate,
                        must_mutate_count=must_mutate_count, normal=normal, sigma=sigma,
-                       crossover_strength=crossover_strength, op=op)
+                       crossover_strength=crossover_strength, op=op, crossover=crossover)
 
     def propose(self, m):
         best = self.driver.best_configuration()
