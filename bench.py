@@ -108,7 +108,15 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--precision", type=int, default=64, choices=(64, 32),
                     help="GP contractions on fp64 MFMA (1e-5 parity) or fp32 MFMA (1e-3 parity)")
+    ap.add_argument("--config", default="c2", choices=("c2", "c3"),
+                    help="c2 = BASELINE configs[1] (R64, m=1M, n=1024: the headline); c3 = configs[2] per GPU "
+                         "(HPL-64 mixed space, 16M/8 = 2M candidates per GPU, n=4096)")
     args = ap.parse_args()
+    if args.config == "c3":
+        if args.m == 1 << 20:
+            args.m = 1 << 21
+        if args.n == 1024:
+            args.n = 4096
 
     import torch
     import torch.distributed as dist
@@ -125,18 +133,33 @@ def main():
     from uptune_amd.manipulator import ConfigurationManipulator, FloatParameter
 
     m, n, d, k = args.m, args.n, args.d, args.k
-    manip = ConfigurationManipulator([FloatParameter(i, -1000.0, 1000.0) for i in range(d)])
+    if args.config == "c3":
+        from uptune_amd import spaces
+        manip = spaces.hpl64()
+    else:
+        manip = ConfigurationManipulator([FloatParameter(i, -1000.0, 1000.0) for i in range(d)])
     eng = BatchEngine(manip, device=local, seed=1)
     npop = m * world                       # replicated population, deterministic init on every rank
     eng.gp_set_precision(args.precision)
     eng.population_init(npop)
     eng.history_reset(0)
-    X, y = training_set(n, d, 101)
+    if args.config == "c3":
+        # training points: n HPL-64 configs (device op1_randomize), features encoded on
+        # the device; synthetic objective = squared distance of the features from 0.3
+        d = eng.spec.n_features
+        tr = BatchEngine(manip, device=local, seed=101)
+        tr.population_init(n)
+        X = tr.encode(tr.population_get()).T.contiguous().cpu().numpy()
+        y = np.sum((X - 0.3) ** 2, axis=1)
+        tr.close()
+    else:
+        X, y = training_set(n, d, 101)
     cand_base = rank * m
     acq = eng.acq("ei", xi=0.0)
+    ell = 1.0 if args.config == "c3" else 0.2
 
     def step(r):
-        eng.gp_fit(X, y, lengthscale=0.2, sigma_f2=1.0, sigma_n2=1e-6, wait=False)   # overlaps propose + hash
+        eng.gp_fit(X, y, lengthscale=ell, sigma_f2=1.0, sigma_n2=1e-6, wait=False)   # overlaps propose + hash
         idx, top, dig, _ = eng.score_round_de(m, k, round_=r, cand_base=cand_base, cr=0.2, n_cross=1, acq=acq,
                                               want_values=False)
         if world > 1:
@@ -178,7 +201,14 @@ def main():
     flops_var = float(m) * n * (n + 1)       # algorithmic: lower-triangular n x n times k* per candidate
     achieved = flops_var / (var_ms * 1e-3) / 1e12 if var_ms else None
     peak = PEAK_FP64_TFLOPS if args.precision == 64 else PEAK_FP32_TFLOPS
-    traffic = load_traffic("var" if args.precision == 64 else "var32")
+    traffic = load_traffic("var" if args.precision == 64 else "var32") if args.config == "c2" else None
+    if args.config == "c3":
+        workload = (f"C3 HPL-64 mixed (24 Int, 16 Enum, 8 Bool, 8 Float, 4 LogInt, 4 Pow2; {d} GP features): "
+                    f"DE-Alt + hash_config + dedup + GP-EI n={n} + top-{k}, {m} candidates per GPU")
+        data = "synthetic (HPL-64 configs from op1_randomize; objective = |features - 0.3|^2; population random-init)"
+    else:
+        workload = f"C2 R64: DE-Alt + hash_config + dedup + GP-EI n={n} + top-{k}"
+        data = "synthetic (Rosenbrock-64 objective on uniform training points; DE population random-init)"
     result = {
         "metric": "candidate configs scored/sec (GP-EI + top-k)",
         "value": value,
@@ -191,9 +221,9 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f64" if args.precision == 64 else "f32 (K*, L^-1 K* MFMA; fit/EI f64)",
-        "data": "synthetic (Rosenbrock-64 objective on uniform training points; DE population random-init)",
-        "config": {"workload": "C2 R64: DE-Alt + hash_config + dedup + GP-EI n=1024 + top-256",
-                   "candidates_per_gpu": m, "gp_n": n, "dims": d, "k": k, "parallelism": f"dp{world}"},
+        "data": data,
+        "config": {"workload": workload, "candidates_per_gpu": m, "gp_n": n, "dims": d, "k": k,
+                   "parallelism": f"dp{world}"},
         "stage_ms": stages,
         "roofline": {"bound": "mfma",
                      "kernel": "k_gp_var<%s> (persistent var contraction L^-1 K*^T, %s)" % (
@@ -204,7 +234,7 @@ def main():
                      "flops_per_launch": flops_var},
         "cpu_baseline": None,
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "c2":
         try:
             result["cpu_baseline"] = cpu_baseline(args.cpu_sample, n, d, k)
         except Exception as ex:  # keep the GPU number even if the baseline fails

@@ -1,0 +1,76 @@
+#!/usr/bin/env python
+"""C5 (BASELINE.json configs[4]): AUC bandit over GPU DE + PSO + GA + GGA with a
+shared GP surrogate on Rosenbrock-64, one process per GPU, per-generation
+results broadcast over RCCL.
+
+    python scripts/c5_bandit.py --generations 100                      # 1 GPU
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 \\
+        --master-addr 127.0.0.1 --master-port 29511 scripts/c5_bandit.py   # 8 GPUs
+
+Rank 0 prints one JSON line: generations, evaluations, best objective, wall
+time, scoring rounds and candidates scored per second (all ranks).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def rosenbrock64(cfg):
+    x = np.array([cfg[i] for i in range(64)], dtype=np.float64) / 500.0   # [-2, 2]
+    return float(np.sum(100.0 * (x[1:] - x[:-1] ** 2) ** 2 + (x[:-1] - 1.0) ** 2))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--generations", type=int, default=100)
+    ap.add_argument("--parallelism", type=int, default=4)
+    ap.add_argument("--n-init", type=int, default=4096, help="initial design = the shared GP's bootstrap set")
+    ap.add_argument("--pool", type=int, default=1 << 18, help="candidates per technique round per GPU")
+    ap.add_argument("--batch", type=int, default=8)
+    ap.add_argument("--population", type=int, default=4096)
+    ap.add_argument("--backend", default="nccl")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(args.backend)
+    from uptune_amd import spaces
+    from uptune_amd.tuner import tune_bandit
+
+    t0 = time.perf_counter()
+    drv = tune_bandit(spaces.r64(), rosenbrock64, generations=args.generations, parallelism=args.parallelism,
+                      n_init=args.n_init, pool=args.pool, batch=args.batch, population=args.population, seed=1,
+                      lengthscale=0.3, device=local)
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    techs = drv.root_technique.techniques
+    rounds = {t.name: t.round for t in techs}
+    scored = sum(t.round * (t.pool * (world if t.sharded else 1) if t.sharded else min(t.pool, t.population))
+                 for t in techs)
+    out = {"config": "C5 AUC bandit over GPU DE+PSO+GA+GGA, shared GP, Rosenbrock-64", "n_gpus": world,
+           "generations": drv.generation, "evaluations": len(drv.results) - args.n_init,
+           "initial_design": args.n_init, "best": drv.best_result.time if drv.best_result else None,
+           "wall_s": wall, "technique_rounds": rounds, "candidates_scored": scored,
+           "candidates_scored_per_s": scored / wall, "bandit_uses": dict(drv.root_technique.bandit.use_counts)}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -90,3 +90,48 @@ def test_merge_topk_unit():
     gi, gs = merge_topk(s, i, d, 4)
     # digest [1]*8 appears as idx 7 and 9 -> 7 survives
     assert gi.tolist() == [2, 7, 3, -1]
+
+
+def _sel_worker(rank, world, port, k, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from uptune_amd.dist import allgather_selection, broadcast_results
+    scores, dig = _pool()
+    m = len(scores)
+    lo, hi = rank * m // world, (rank + 1) * m // world
+    values = np.arange(3 * m, dtype=np.float64).reshape(3, m)   # row j of candidate g = j*m + g
+    hexes = [row.tobytes() for row in dig[lo:hi]]
+    dup = osel.dedup(hexes, set())
+    loc = osel.topk(list(scores[lo:hi]), k, dup=dup, cand_base=lo)
+    li = torch.tensor(loc, dtype=torch.int64)
+    ls = torch.tensor([scores[g] if g >= 0 else float("-inf") for g in loc], dtype=torch.float64)
+    ld = torch.tensor(np.stack([dig[g] if g >= 0 else np.zeros(8, np.int32) for g in loc]), dtype=torch.int32)
+    rows = torch.tensor(np.stack([values[:, g] if g >= 0 else np.zeros(3) for g in loc], axis=1))
+    gi, gs, grows = allgather_selection(li, ls, ld, rows, k)
+    y = torch.tensor([0.5, 1.5]) if rank == 0 else None
+    d = torch.arange(16, dtype=torch.int32).reshape(2, 8) if rank == 0 else None
+    y, d = broadcast_results(y, d, 2, torch.device("cpu"))
+    q.put((rank, gi.tolist(), grows.numpy().tolist(), float(y.sum()), int(d.sum())))
+    dist.destroy_process_group()
+
+
+def test_allgather_selection_rows_and_results_broadcast():
+    k, world = 40, 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_sel_worker, args=(r, world, port, k, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    out = sorted(q.get(timeout=120) for _ in range(world))
+    for p in ps:
+        p.join(timeout=60)
+    scores, dig = _pool()
+    want = _global_ref(scores, dig, k)
+    m = len(scores)
+    for rank, gi, rows, ysum, dsum in out:
+        assert gi == want
+        # every rank gets the selected candidates' value rows, in merged order
+        assert rows == [[j * m + g for g in want] for j in range(3)]
+        assert ysum == 2.0 and dsum == sum(range(16))

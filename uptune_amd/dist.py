@@ -88,3 +88,56 @@ def broadcast_history(X: Optional[torch.Tensor], y: Optional[torch.Tensor], dige
     dist.broadcast(y, src, group=group)
     dist.broadcast(digests, src, group=group)
     return X, y, digests
+
+
+def _comm_device(group, device):
+    """gloo moves CPU tensors (and runs the CPU tests); nccl (= RCCL) moves
+    device tensors over xGMI"""
+    return torch.device("cpu") if dist.get_backend(group) == "gloo" else device
+
+
+def allgather_selection(idx: torch.Tensor, score: torch.Tensor, digest: torch.Tensor, rows: torch.Tensor, k: int,
+                        group: Optional[dist.ProcessGroup] = None
+                        ) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+    """One scoring round's exchange for the technique layer: every rank's local
+    top-k (global idx, score, digest) AND the selected value rows [ncols][k]
+    are all-gathered; the merge (merge_topk) is identical on every rank and the
+    rows of the merged selection are taken from the gathered rows, so every
+    rank queues the same configurations.  Returns (idx [k], score [k],
+    rows [ncols][k]) on the input device; empty slots have idx -1."""
+    dev = idx.device
+    cd = _comm_device(group, dev)
+    world = dist.get_world_size(group)
+    parts = []
+    for t in (idx.to(torch.int64), score.to(torch.float64), digest.to(torch.int32), rows.to(torch.float64)):
+        t = t.to(cd).contiguous()
+        g = [torch.empty_like(t) for _ in range(world)]
+        dist.all_gather(g, t, group=group)
+        parts.append(g)
+    gi = torch.cat(parts[0])
+    gs = torch.cat(parts[1])
+    gd = torch.cat(parts[2])
+    grows = torch.cat(parts[3], dim=1)
+    mi, ms = merge_topk(gs, gi, gd, k)
+    pos = {int(g): p for p, g in enumerate(gi.tolist()) if g >= 0}
+    take = torch.tensor([pos[int(g)] if g >= 0 else 0 for g in mi.tolist()], dtype=torch.int64, device=cd)
+    out_rows = grows[:, take]
+    return mi.to(dev), ms.to(dev), out_rows.to(dev)
+
+
+def broadcast_results(y: Optional[torch.Tensor], digests: Optional[torch.Tensor], n: int, device, src: int = 0,
+                      group: Optional[dist.ProcessGroup] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+    """The per-round history delta of the search loop: objective values [n] f64
+    and digests [n][8] i32 of the configurations evaluated on `src`, sent to
+    every rank (api.sync's result injection, api.py:547-553, mapped onto one
+    RCCL broadcast per tensor)."""
+    cd = _comm_device(group, device)
+    if dist.get_rank(group) == src:
+        y = y.to(cd, torch.float64).contiguous()
+        digests = digests.to(cd, torch.int32).contiguous()
+    else:
+        y = torch.empty((n,), dtype=torch.float64, device=cd)
+        digests = torch.empty((n, 8), dtype=torch.int32, device=cd)
+    dist.broadcast(y, src, group=group)
+    dist.broadcast(digests, src, group=group)
+    return y, digests

@@ -86,6 +86,29 @@ class SearchDriver:
             return self._hash_fn(cfg)
         return self.manipulator.hash_config(cfg)
 
+    def config_keys(self, cfgs) -> List[str]:
+        """keys of many configurations (one batched device hash)"""
+        if self._hash_fn is not None:
+            return [self._hash_fn(c) for c in cfgs]
+        from .engine import default_engine
+        return default_engine(self.manipulator).hash_configs(cfgs) if len(cfgs) else []
+
+    def record_seed(self, cfgs, times, keys=None) -> None:
+        """bootstrap history: already-evaluated configurations (an initial design,
+        or results loaded from a previous run) become results of generation 0"""
+        keys = keys if keys is not None else self.config_keys(cfgs)
+        for cfg, t, key in zip(cfgs, times, keys):
+            if key in self._requested:
+                continue
+            dr = DesiredResult(cfg, key, "seed", self.generation)
+            self._requested[key] = dr
+            self._seen.append(key)
+            self.report(dr, t)
+        self.process_new_results()
+
+    def seed_results(self, cfgs, evaluate) -> None:
+        self.record_seed(cfgs, [evaluate(c) for c in cfgs])
+
     def seen_hashes(self) -> List[str]:
         return self._seen
 
@@ -189,3 +212,68 @@ class SearchDriver:
     def _idle_generations(self) -> bool:
         self._idle = getattr(self, "_idle", 0) + 1
         return self._idle > 50
+
+
+class DistributedSearchDriver(SearchDriver):
+    """SPMD search loop over a torch.distributed group (one process per GPU).
+
+    Every rank runs the same technique tree with the same seeds; the GPU
+    techniques shard each round's candidate pool by global index and
+    all-gather their local top-k (technique.GpuBatchTechnique), so every rank
+    requests the same configurations.  Rank `src` evaluates them and the
+    results -- objective values and hash digests, the per-round history delta
+    -- are broadcast to every rank (dist.broadcast_results; the reference's
+    api.sync result injection, api.py:547-553, and ParallelTuning's batch
+    dispatch, api.py:428-482).  The digests double as a consistency check:
+    a rank whose requests diverge raises instead of training on wrong data.
+    """
+
+    def __init__(self, manipulator, root_technique, objective=None, parallelism: int = 4, hash_fn=None,
+                 group=None, src: int = 0, device=None):
+        super().__init__(manipulator, root_technique, objective, parallelism, hash_fn)
+        self.group, self.src = group, src
+        self.device = device
+
+    def seed_results(self, cfgs, evaluate) -> None:
+        """rank `src` evaluates the initial design; values + digests are broadcast"""
+        import torch
+        import torch.distributed as dist
+
+        from .dist import broadcast_results
+        from .engine import hex_to_digests
+        keys = self.config_keys(cfgs)
+        kd = torch.from_numpy(hex_to_digests(keys).view(np.int32).copy())
+        src = dist.get_rank(self.group) == self.src
+        y = torch.tensor([evaluate(c) for c in cfgs], dtype=torch.float64) if src else None
+        dev = self.device if self.device is not None else torch.device("cpu")
+        y, dig = broadcast_results(y, kd if src else None, len(cfgs), dev, self.src, self.group)
+        if not torch.equal(dig.cpu(), kd):
+            raise RuntimeError("initial design differs between ranks")
+        self.record_seed(cfgs, y.cpu().tolist(), keys)
+
+    def main(self, evaluate: Callable[[Dict[Any, Any]], float], test_limit: int = 100,
+             max_generations: int = 100000) -> Optional[Result]:
+        import torch
+        import torch.distributed as dist
+
+        from .dist import broadcast_results
+        from .engine import hex_to_digests
+
+        rank = dist.get_rank(self.group)
+        dev = self.device if self.device is not None else torch.device("cpu")
+        while self.test_count <= test_limit and self.generation < max_generations:
+            todo = self.run_generation_techniques()
+            n = len(todo)
+            keys = torch.from_numpy(hex_to_digests([dr.key for dr in todo]).view(np.int32).copy())
+            y = torch.tensor([evaluate(dr.configuration) for dr in todo], dtype=torch.float64) \
+                if rank == self.src else None
+            y, dig = broadcast_results(y, keys if rank == self.src else None, n, dev, self.src, self.group)
+            if not torch.equal(dig.cpu(), keys):
+                raise RuntimeError(f"rank {rank}: requested configurations diverged from rank {self.src}")
+            for dr, t in zip(todo, y.cpu().tolist()):
+                self.report(dr, t)
+            self.process_new_results()
+            self.generation += 1
+            if not todo and not self.pending_result_callbacks and self.test_count and self._idle_generations():
+                break
+        return self.best_result

@@ -303,9 +303,10 @@ _DEFAULT: Dict[int, BatchEngine] = {}
 
 
 def default_engine(manipulator) -> BatchEngine:
-    key = id(manipulator)
+    dev = torch.cuda.current_device() if torch.cuda.is_available() else 0   # this rank's GPU
+    key = (id(manipulator), dev)
     eng = _DEFAULT.get(key)
     if eng is None:
-        eng = BatchEngine(manipulator)
+        eng = BatchEngine(manipulator, device=dev)
         _DEFAULT[key] = eng
     return eng

@@ -275,10 +275,18 @@ class GpuBatchTechnique(SearchTechnique):
     `batch`; desired_configuration() then returns them one per call.
     """
 
+    # DE / GA pools shard over the ranks of a process group by GLOBAL candidate
+    # index; PSO moves its (small) swarm on every rank (replicas)
+    sharded = True
+
     def __init__(self, pool: int = 1 << 14, batch: int = 8, population: int = 1024, device: int = 0,
-                 seed: int = 0, lengthscale: float = 0.3, min_train: int = 4, acq: str = "ei", *pargs,
-                 **kwargs):
+                 seed: int = 0, lengthscale: float = 0.3, min_train: int = 4, acq: str = "ei",
+                 group=None, *pargs, **kwargs):
         super().__init__(*pargs, **kwargs)
+        # multi-GPU (SURVEY.md §8(e)): with torch.distributed initialised and
+        # world > 1, rank r scores candidates [base + r*pool, base + (r+1)*pool)
+        # of every round and the local top-k lists are all-gathered and merged
+        self.group = group
         self.pool, self.batch, self.population = int(pool), int(batch), int(population)
         self.device, self.seed, self.lengthscale, self.min_train = device, seed, lengthscale, min_train
         self.acq_kind = acq
@@ -294,8 +302,23 @@ class GpuBatchTechnique(SearchTechnique):
         new = cls.__new__(cls)
         memo[id(self)] = new
         for k, v in self.__dict__.items():
-            setattr(new, k, None if k == "engine" else copy.deepcopy(v, memo))
+            setattr(new, k, None if k == "engine" else (v if k == "group" else copy.deepcopy(v, memo)))
         return new
+
+    def _dist(self):
+        """(rank, world) of the sharded round (world 1 without torch.distributed)"""
+        try:
+            import torch.distributed as dist
+        except Exception:  # pragma: no cover
+            return 0, 1
+        if not self.sharded or not dist.is_available() or not dist.is_initialized():
+            return 0, 1
+        return dist.get_rank(self.group), dist.get_world_size(self.group)
+
+    def round_base(self) -> int:
+        """global index of this rank's first candidate of the current round"""
+        rank, _ = self._dist()
+        return self.cand_base + rank * self.pool
 
     # -- device state ------------------------------------------------------
     def _ensure_engine(self):
@@ -320,7 +343,13 @@ class GpuBatchTechnique(SearchTechnique):
         cfgs, y = self.driver.training_configs()
         if len(y) < self.min_train:
             return False
-        X = self.engine.features_host(cfgs)
+        # the driver's results are append-only: encode only the new ones
+        X = getattr(self, "_X", None)
+        if X is None or X.shape[0] > len(cfgs):
+            X = np.zeros((0, self.engine.spec.n_features))
+        if X.shape[0] < len(cfgs):
+            X = np.vstack([X, self.engine.features_host(cfgs[X.shape[0]:])])
+        self._X = X
         self.engine.gp_fit(X, y, lengthscale=self.lengthscale, sigma_f2=1.0, sigma_n2=1e-6, jitter=1e-8)
         return True
 
@@ -332,6 +361,8 @@ class GpuBatchTechnique(SearchTechnique):
         import torch
         eng = self._ensure_engine()
         self._sync_history()
+        rank, world = self._dist()
+        base = self.round_base()
         vals, invalid = self.propose(self.pool)
         dig = eng.hash(vals)
         dup = eng.dedup(dig)
@@ -342,13 +373,18 @@ class GpuBatchTechnique(SearchTechnique):
             _, _, score = eng.gp_score(feat, acq=eng.acq(self.acq_kind), dup=dup)
         else:  # no model yet: every non-duplicate candidate is equally good (lowest index first)
             score = torch.zeros(vals.shape[1], dtype=torch.float64, device=vals.device)
-        idx, _ = eng.topk(score, self.batch, dup=dup, cand_base=0)
-        idx = idx[idx >= 0]
-        rows = vals[:, idx]
+        idx, top = eng.topk(score, self.batch, dup=dup, cand_base=base)   # GLOBAL candidate indices
+        loc = torch.where(idx >= 0, idx - base, torch.zeros_like(idx))
+        rows = vals[:, loc]
+        if world > 1:
+            from .dist import allgather_selection
+            idx, top, rows = allgather_selection(idx, top, dig[loc], rows, self.batch, group=self.group)
+        keep = idx >= 0
+        idx, rows = idx[keep], rows[:, keep]
         self.queue.extend(eng.decode(rows))
         self.after_round(vals, idx)
         self.round += 1
-        self.cand_base += self.pool
+        self.cand_base += world * self.pool
 
     def after_round(self, vals, idx):
         pass
@@ -376,14 +412,14 @@ class GpuDifferentialEvolution(GpuBatchTechnique):
         self._pending: Dict[str, int] = {}
 
     def propose(self, m):
-        return self.engine.propose_de(m, round_=self.round, cand_base=self.cand_base, cr=self.cr,
+        return self.engine.propose_de(m, round_=self.round, cand_base=self.round_base(), cr=self.cr,
                                       n_cross=self.n_cross), None
 
     def after_round(self, vals, idx):
         npop = self.engine.npop
-        for j, g in enumerate(idx.cpu().numpy().tolist()):
+        for j, g in enumerate(idx.cpu().numpy().tolist()):   # global index g targets member g % npop
             cfg = self.queue[len(self.queue) - len(idx) + j]
-            self._pending[self.driver.config_key(cfg)] = (self.cand_base + g) % npop
+            self._pending[self.driver.config_key(cfg)] = g % npop
 
     def handle_requested_result(self, result):
         import torch
@@ -400,6 +436,8 @@ class GpuDifferentialEvolution(GpuBatchTechnique):
 
 class GpuPSO(GpuBatchTechnique):
     """Batched PSO (pso.py:11-77); particles move toward the driver's best."""
+
+    sharded = False   # the swarm moves on every rank: same particles, same result
 
     def __init__(self, omega=0.5, phi_l=0.5, phi_g=0.5, enum_mode=0, crossover="op3_cross_OX1", *pargs, **kwargs):
         super().__init__(*pargs, **kwargs)
@@ -440,7 +478,7 @@ class GpuGA(GpuBatchTechnique):
     def propose(self, m):
         best = self.driver.best_configuration()
         p1 = None if best is None else self.engine.spec.encode_configs([best])[:, 0]
-        return self.engine.propose_ga(m, p1, None, round_=self.round, cand_base=self.cand_base, **self.ga)
+        return self.engine.propose_ga(m, p1, None, round_=self.round, cand_base=self.round_base(), **self.ga)
 
 
 class GpuGGA(GpuGA):
@@ -451,11 +489,13 @@ class GpuGGA(GpuGA):
         super().__init__(*pargs, crossover_rate=0.5, crossover_strength=0.2, normal=True, op=5, **kwargs)
 
 
-def pso_ga_de_bandit(**kw) -> AUCBanditMetaTechnique:
-    """GPU counterpart of the reference's "PSO_GA_DE" bandit (bandittechniques.py:311-320)."""
+def pso_ga_de_bandit(bandit_seed: Optional[int] = None, **kw) -> AUCBanditMetaTechnique:
+    """GPU counterpart of the reference's "PSO_GA_DE" bandit (bandittechniques.py:311-320).
+    bandit_seed fixes the bandit's tie-break shuffles (required for SPMD runs:
+    every rank must order the techniques the same way)."""
     return AUCBanditMetaTechnique([
         GpuPSO(name="gpu-pso", **kw),
         GpuGA(name="gpu-ga", crossover_rate=0.5, **kw),
         GpuDifferentialEvolution(name="gpu-de", **kw),
         GpuGGA(name="gpu-gga", **kw),
-    ], name="GPU_PSO_GA_DE")
+    ], name="GPU_PSO_GA_DE", seed=bandit_seed)
