@@ -254,6 +254,26 @@ int ut_score_round_de(ut_ctx* ctx, const ut_de_params* de, const ut_acq* acq, ui
 int ut_round_buffers(ut_ctx* ctx, double** values, double** features, uint32_t** digests, uint8_t** dup,
                      double** mu, double** var, double** score, int64_t* ld);
 
+/* ---- tree-ensemble surrogate (the reference's own model family:
+ *      plugins/xgbregressor.py:50-63, src/multi_stage.py:8-22) ------------- */
+/* pred = (base + sum over trees of scale * leaf) / div, trees in order;
+ * LE: go left iff (float)x <= threshold (sklearn), LT: iff (float)x < (float)threshold
+ * (XGBoost); NaN features take default_left.  Leaves have feature < 0. */
+enum { UT_SPLIT_LE = 0, UT_SPLIT_LT = 1 };
+typedef struct ut_tree_node {
+  int32_t feature;       /* GP feature column tested; < 0 = leaf */
+  int32_t left, right;   /* child node indices (global in the node array) */
+  int32_t default_left;  /* NaN goes left */
+  double threshold;
+  double value;          /* leaf value */
+} ut_tree_node;
+int ut_forest_set(ut_ctx* ctx, int32_t n_trees, const int32_t* roots_host, int64_t n_nodes,
+                  const ut_tree_node* nodes_host, int32_t rule, double base, double scale, double div);
+/* features [n_features][ld] (the layout ut_encode_features writes); pred and
+ * score [m] may be NULL; score = sign * pred (sign -1: minimise), -inf where dup[i] */
+int ut_forest_predict(ut_ctx* ctx, const double* features, int64_t ld, int64_t m, int32_t n_features,
+                      const uint8_t* dup, double sign, double* pred, double* score);
+
 /* per-kernel device time of the last ut_score_round_* call (ms), when
  * timing is enabled with ut_set_timing(ctx, 1).  names: "propose", "hash",
  * "dedup", "encode", "gp_fit", "kstar", "var", "finalize", "topk" */

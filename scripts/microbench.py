@@ -1,5 +1,5 @@
 """Per-kernel microbenchmarks on synthetic inputs (one process, HIP events on
-the library stream).  Usage: python scripts/microbench.py [hash|gp|all]"""
+the library stream).  Usage: python scripts/microbench.py [hash|forest|all]"""
 import json
 import os
 import sys
@@ -45,9 +45,45 @@ def bench_hash(m=1 << 20):
     return out
 
 
+def synthetic_forest(n_trees=300, depth=10, d=64, seed=0):
+    """complete binary trees of the reference's XGB size (plugins/xgbregressor.py:
+    n_estimators=300, max_depth=10) with random splits"""
+    from uptune_amd import _lib as L
+    from uptune_amd.forest import NODE_DTYPE, Forest
+    rng = np.random.default_rng(seed)
+    per = (1 << (depth + 1)) - 1
+    nodes = np.zeros(n_trees * per, dtype=NODE_DTYPE)
+    for t in range(n_trees):
+        o = t * per
+        k = np.arange(per)
+        inner = k < (1 << depth) - 1
+        nodes["feature"][o:o + per] = np.where(inner, rng.integers(0, d, per), -1)
+        nodes["left"][o:o + per] = np.where(inner, o + 2 * k + 1, 0)
+        nodes["right"][o:o + per] = np.where(inner, o + 2 * k + 2, 0)
+        nodes["threshold"][o:o + per] = rng.uniform(size=per)
+        nodes["value"][o:o + per] = np.where(inner, 0.0, rng.normal(size=per) * 0.01)
+    return Forest(nodes, np.arange(n_trees, dtype=np.int32) * per, L.UT_SPLIT_LT, 0.5, 1.0, 1.0)
+
+
+def bench_forest(m=1 << 20, d=64):
+    eng = BatchEngine(ConfigurationManipulator([FloatParameter(i, 0.0, 1.0) for i in range(d)]), seed=1)
+    out = {}
+    for n_trees, depth in ((300, 10), (100, 6)):
+        f = synthetic_forest(n_trees, depth, d)
+        eng.forest_set(f)
+        feat = torch.rand(d, m, dtype=torch.float64, device="cuda")
+        ms = timeit(lambda: eng.forest_predict(feat))
+        visits = n_trees * (depth + 1)
+        out[f"{n_trees}x{depth}"] = {"ms": ms, "cands_per_s": m / ms * 1e3, "node_visits_per_cand": visits,
+                                     "node_bytes_GBps": m * visits * 32 / ms / 1e6}
+    return out
+
+
 if __name__ == "__main__":
     which = sys.argv[1] if len(sys.argv) > 1 else "all"
     res = {}
     if which in ("hash", "all"):
         res["hash"] = bench_hash()
+    if which in ("forest", "all"):
+        res["forest"] = bench_forest()
     print(json.dumps(res, indent=1))

@@ -38,6 +38,14 @@ class ParamDesc(C.Structure):
     ]
 
 
+class TreeNode(C.Structure):
+    _fields_ = [("feature", C.c_int32), ("left", C.c_int32), ("right", C.c_int32), ("default_left", C.c_int32),
+                ("threshold", C.c_double), ("value", C.c_double)]
+
+
+UT_SPLIT_LE, UT_SPLIT_LT = 0, 1
+
+
 class DeParams(C.Structure):
     _fields_ = [("cr", C.c_double), ("n_cross", C.c_int32), ("pad", C.c_int32)]
 
@@ -100,6 +108,8 @@ SIGNATURES = {
     "ut_dedup": (C.c_int, [P, P, I64, P]),
     "ut_gp_fit": (C.c_int, [P, P, P, I32, I32, C.POINTER(GpHyper)]),
     "ut_gp_fit_async": (C.c_int, [P, P, P, I32, I32, C.POINTER(GpHyper)]),
+    "ut_forest_set": (C.c_int, [P, I32, P, I64, P, I32, D, D, D]),
+    "ut_forest_predict": (C.c_int, [P, P, I64, I64, I32, P, D, P, P]),
     "ut_gp_score": (C.c_int, [P, P, I64, I64, C.POINTER(Acq), P, P, P, P]),
     "ut_gp_set_precision": (C.c_int, [P, I32]),
     "ut_gp_stats": (C.c_int, [P, C.POINTER(D), C.POINTER(D), C.POINTER(D)]),

@@ -190,7 +190,8 @@ int ut_ctx_destroy(ut_ctx* c) {
   fr(c->kst.p); fr(c->mu_part.p); fr(c->var_part.p); fr(c->cnorm.p);
   fr(c->r_values.p); fr(c->r_feat.p); fr(c->r_mu.p); fr(c->r_var.p); fr(c->r_score.p); fr(c->r_digest.p);
   fr(c->r_dup.p); fr(c->tk_score[0].p); fr(c->tk_score[1].p); fr(c->tk_idx[0].p); fr(c->tk_idx[1].p);
-  fr(c->r_topk_idx.p); fr(c->r_topk_score.p);
+  fr(c->r_topk_idx.p); fr(c->r_topk_score.p); fr(c->perm_ws.p); fr(c->perm_dig.p);
+  fr(c->forest_nodes); fr(c->forest_roots);
   for (auto& m : c->timing.marks) hipEventDestroy(m.ev);
   for (hipEvent_t e : {c->ev_fork, c->ev_join, c->ev_fit, c->ev_prefit})
     if (e) hipEventDestroy(e);

@@ -25,6 +25,7 @@ long long uthc_sizeof(int which) {
     case 4: return (long long)sizeof(ut_acq);
     case 5: return (long long)sizeof(ut_pso_params);
     case 6: return (long long)sizeof(ut_ga_params);
+    case 7: return (long long)sizeof(ut_tree_node);
     default: return -1;
   }
 }

@@ -180,6 +180,12 @@ struct ut_ctx {
   int64_t r_ld = 0;
   int64_t r_m = 0;
 
+  // tree-ensemble surrogate (forest.hip)
+  ut_tree_node* forest_nodes = nullptr;
+  int32_t* forest_roots = nullptr;
+  int32_t forest_trees = 0, forest_rule = 0;
+  double forest_base = 0.0, forest_scale = 1.0, forest_div = 1.0;
+
   ut::Timing timing;
 };
 

@@ -66,6 +66,7 @@ class BatchEngine:
                 "ut_space_define")
         del keep
         self.npop = 0
+        self.forest = None
 
     # -- plumbing ----------------------------------------------------------
     def _bind_stream(self):
@@ -255,6 +256,28 @@ class BatchEngine:
         L.check(self.ctx, self.lib.ut_gp_score(self.ctx, _ptr(feat), feat.stride(0), m, C.byref(acq), _ptr(dup),
                                                _ptr(mu), _ptr(var), _ptr(score)), "ut_gp_score")
         return mu, var, score
+
+    # -- tree-ensemble surrogate ---------------------------------------------
+    def forest_set(self, model):
+        """load a tree ensemble (sklearn regressor, XGBoost JSON or forest.Forest)"""
+        from .forest import as_forest
+        f = as_forest(model)
+        nodes = np.ascontiguousarray(f.nodes)
+        roots = np.ascontiguousarray(f.roots, dtype=np.int32)
+        L.check(self.ctx, self.lib.ut_forest_set(self.ctx, f.n_trees, roots.ctypes.data, nodes.size,
+                                                 nodes.ctypes.data, int(f.rule), float(f.base), float(f.scale),
+                                                 float(f.div)), "ut_forest_set")
+        self.forest = f
+
+    def forest_predict(self, feat: torch.Tensor, m: Optional[int] = None, dup: Optional[torch.Tensor] = None,
+                       sign: float = -1.0):
+        """-> (pred [m], score [m] = sign * pred, -inf on duplicates)"""
+        m = feat.shape[1] if m is None else m
+        pred, score = self._empty(m), self._empty(m)
+        L.check(self.ctx, self.lib.ut_forest_predict(self.ctx, _ptr(feat), feat.stride(0), m, feat.shape[0],
+                                                     _ptr(dup), float(sign), _ptr(pred), _ptr(score)),
+                "ut_forest_predict")
+        return pred, score
 
     # -- selection ---------------------------------------------------------
     def topk(self, score: torch.Tensor, k: int, dup: Optional[torch.Tensor] = None, cand_base: int = 0):

@@ -281,8 +281,13 @@ class GpuBatchTechnique(SearchTechnique):
 
     def __init__(self, pool: int = 1 << 14, batch: int = 8, population: int = 1024, device: int = 0,
                  seed: int = 0, lengthscale: float = 0.3, min_train: int = 4, acq: str = "ei",
-                 group=None, *pargs, **kwargs):
+                 group=None, surrogate=None, *pargs, **kwargs):
         super().__init__(*pargs, **kwargs)
+        # surrogate: None = the GP fitted on the driver's results (EI / UCB); or a
+        # tree ensemble over the same features (sklearn regressor, XGBoost JSON,
+        # forest.Forest) ranking candidates by predicted objective (minimised),
+        # the multi-stage tuner's model scoring (multi_stage.py:8-22, :109-123)
+        self.surrogate = surrogate
         # multi-GPU: with torch.distributed initialised and
         # world > 1, rank r scores candidates [base + r*pool, base + (r+1)*pool)
         # of every round and the local top-k lists are all-gathered and merged
@@ -368,7 +373,11 @@ class GpuBatchTechnique(SearchTechnique):
         dup = eng.dedup(dig)
         if invalid is not None:
             dup = torch.maximum(dup, invalid)
-        if self._fit():
+        if self.surrogate is not None:
+            if getattr(eng, "forest", None) is None:
+                eng.forest_set(self.surrogate)
+            _, score = eng.forest_predict(eng.encode(vals), dup=dup)
+        elif self._fit():
             feat = eng.encode(vals)
             _, _, score = eng.gp_score(feat, acq=eng.acq(self.acq_kind), dup=dup)
         else:  # no model yet: every non-duplicate candidate is equally good (lowest index first)
