@@ -100,7 +100,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--m", type=int, default=1 << 20, help="candidates per GPU per round")
+    ap.add_argument("--m", "--candidates", dest="m", type=int, default=1 << 20, help="candidates per GPU per round")
     ap.add_argument("--n", type=int, default=1024, help="GP training points")
     ap.add_argument("--d", type=int, default=64)
     ap.add_argument("--k", type=int, default=256)
@@ -123,10 +123,17 @@ def main():
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one rank per GPU; more ranks than GPUs (the gloo rehearsal) share them round-robin
+    local = int(os.environ.get("LOCAL_RANK", "0")) % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local)
+    # UT_DIST_BACKEND=gloo rehearses the N > 1 path with several ranks on one GPU
+    # (RCCL needs one GPU per rank); the driver's multi-GPU runs use nccl = RCCL
+    backend = os.environ.get("UT_DIST_BACKEND", "nccl")
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
 
     from uptune_amd.dist import allgather_topk
     from uptune_amd.engine import BatchEngine
@@ -189,7 +196,7 @@ def main():
     elapsed = time.perf_counter() - t0
     eng.set_timing(False)
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda" if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
@@ -201,7 +208,9 @@ def main():
     flops_var = float(m) * n * (n + 1)       # algorithmic: lower-triangular n x n times k* per candidate
     achieved = flops_var / (var_ms * 1e-3) / 1e12 if var_ms else None
     peak = PEAK_FP64_TFLOPS if args.precision == 64 else PEAK_FP32_TFLOPS
-    traffic = load_traffic("var" if args.precision == 64 else "var32") if args.config == "c2" else None
+    # HBM bytes per launch were profiled on the default C2 round (profiles/pmc_summary.json)
+    profiled = args.config == "c2" and (m, n, d) == (1 << 20, 1024, 64)
+    traffic = load_traffic("var" if args.precision == 64 else "var32") if profiled else None
     if args.config == "c3":
         workload = (f"C3 HPL-64 mixed (24 Int, 16 Enum, 8 Bool, 8 Float, 4 LogInt, 4 Pow2; {d} GP features): "
                     f"DE-Alt + hash_config + dedup + GP-EI n={n} + top-{k}, {m} candidates per GPU")

@@ -61,13 +61,17 @@ def allgather_topk(idx: torch.Tensor, score: torch.Tensor, digest: torch.Tensor,
                    group: Optional[dist.ProcessGroup] = None) -> Tuple[torch.Tensor, torch.Tensor]:
     """all_gather the local (idx, score, digest) top-k of every rank and merge."""
     world = dist.get_world_size(group)
+    dev = idx.device
+    cd = _comm_device(group, dev)
+    idx, score, digest = idx.to(cd), score.to(cd), digest.to(cd)
     gi = [torch.empty_like(idx) for _ in range(world)]
     gs = [torch.empty_like(score) for _ in range(world)]
     gd = [torch.empty_like(digest) for _ in range(world)]
     dist.all_gather(gi, idx.contiguous(), group=group)
     dist.all_gather(gs, score.contiguous(), group=group)
     dist.all_gather(gd, digest.contiguous(), group=group)
-    return merge_topk(torch.cat(gs), torch.cat(gi), torch.cat(gd), k)
+    mi, ms = merge_topk(torch.cat(gs), torch.cat(gi), torch.cat(gd), k)
+    return mi.to(dev), ms.to(dev)
 
 
 def broadcast_history(X: Optional[torch.Tensor], y: Optional[torch.Tensor], digests: Optional[torch.Tensor],
