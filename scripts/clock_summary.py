@@ -1,0 +1,39 @@
+"""Effective clock and MFMA busy fraction per kernel from scripts/pmc_clock.sh
+(MI355X_MICROARCH.md 'DVFS give-back': clock = GRBM_GUI_ACTIVE / 8 / duration;
+SQ_VALU_MFMA_BUSY_CYCLES counts cycles of busy MFMA pipes summed over SIMDs).
+
+    python scripts/clock_summary.py gpurun_out/clk > profiles/r01_clock.json
+"""
+import csv
+import json
+import sys
+from collections import defaultdict
+
+KERNELS = {"var": "void ut::k_gp_var<double>", "kstar": "void ut::k_gp_kstar<double>", "hash": "ut::k_hash",
+           "propose": "ut::k_de("}
+
+
+def main(d, n_cu=256, peak_ghz=2.4):
+    rows = defaultdict(dict)
+    with open(f"{d}/run_counter_collection.csv") as f:
+        for r in csv.DictReader(f):
+            rows[int(r["Dispatch_Id"])][r["Counter_Name"]] = float(r["Counter_Value"])
+            rows[int(r["Dispatch_Id"])]["_name"] = r["Kernel_Name"]
+            rows[int(r["Dispatch_Id"])]["_ns"] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+    out = {"_note": "clock_ghz = GRBM_GUI_ACTIVE / 8 / duration; mfma_busy = SQ_VALU_MFMA_BUSY_CYCLES / "
+                    "(4 SIMDs x CUs x clock cycles of the kernel); profiled passes run ~2-5% slower "
+                    "(MI355X_MICROARCH.md DVFS item 2)"}
+    for key, prefix in KERNELS.items():
+        ds = [v for v in rows.values() if v["_name"].startswith(prefix)]
+        if not ds:
+            continue
+        clk = [v["GRBM_GUI_ACTIVE"] / 8 / v["_ns"] for v in ds]           # cycles per ns = GHz
+        busy = [v["SQ_VALU_MFMA_BUSY_CYCLES"] / (4 * n_cu * v["GRBM_GUI_ACTIVE"] / 8) for v in ds]
+        out[key] = {"dispatches": len(ds), "duration_ms": sum(v["_ns"] for v in ds) / len(ds) / 1e6,
+                    "clock_ghz": sum(clk) / len(clk), "mfma_busy": sum(busy) / len(busy),
+                    "clock_adjusted_peak_fraction_scale": peak_ghz / (sum(clk) / len(clk))}
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])
