@@ -79,11 +79,32 @@ def bench_forest(m=1 << 20, d=64):
     return out
 
 
+def bench_fit(d=64):
+    """ut_gp_fit latency (Cholesky, L^-1, alpha on the device) by training-set size"""
+    out = {}
+    eng = BatchEngine(ConfigurationManipulator([FloatParameter(i, 0.0, 1.0) for i in range(d)]), seed=1)
+    rng = np.random.default_rng(0)
+    for n in (256, 1024, 2048, 4096):
+        X = rng.uniform(size=(n, d))
+        y = np.sum((X - 0.4) ** 2, axis=1)
+        eng.gp_fit(X, y, lengthscale=0.5, sigma_f2=1.0, sigma_n2=1e-6, jitter=1e-8)
+        torch.cuda.synchronize()
+        ts = []
+        for _ in range(5):
+            t0 = time.perf_counter()
+            eng.gp_fit(X, y, lengthscale=0.5, sigma_f2=1.0, sigma_n2=1e-6, jitter=1e-8)
+            ts.append((time.perf_counter() - t0) * 1e3)
+        out[n] = {"ms": float(np.median(ts))}
+    return out
+
+
 if __name__ == "__main__":
     which = sys.argv[1] if len(sys.argv) > 1 else "all"
     res = {}
     if which in ("hash", "all"):
         res["hash"] = bench_hash()
+    if which in ("fit", "all"):
+        res["fit"] = bench_fit()
     if which in ("forest", "all"):
         res["forest"] = bench_forest()
     print(json.dumps(res, indent=1))

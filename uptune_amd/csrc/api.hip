@@ -442,7 +442,7 @@ int ut_propose_de(ut_ctx* c, const ut_de_params* p, uint32_t round_, int64_t can
   UT_CHECK(c, c->has_space, UT_ENOSPACE, "space not defined");
   UT_CHECK(c, c->pop != nullptr, UT_EINVAL, "propose_de: population not initialised");
   UT_CHECK(c, p && p->n_cross >= 0 && p->n_cross <= 4, UT_EINVAL, "propose_de: n_cross must be in [0, 4]");
-  UT_CHECK(c, m >= 0 && cand_base >= 0 && out_values && ld >= m, UT_EINVAL, "propose_de: bad arguments");
+  UT_CHECK(c, m >= 0 && cand_base >= 0 && (out_values || m == 0) && ld >= m, UT_EINVAL, "propose_de: bad arguments");
   if (m == 0) return 0;
   return launch_de(c, p, round_, cand_base, m, out_values, ld);
 }
@@ -450,7 +450,7 @@ int ut_propose_de(ut_ctx* c, const ut_de_params* p, uint32_t round_, int64_t can
 int ut_encode_features(ut_ctx* c, const double* values, int64_t ld, int64_t m, double* feat, int64_t ldf) {
   if (!c) return UT_EINVAL;
   UT_CHECK(c, c->has_space, UT_ENOSPACE, "space not defined");
-  UT_CHECK(c, values && feat && ld >= m && ldf >= m, UT_EINVAL, "encode: bad arguments");
+  UT_CHECK(c, m >= 0 && ((values && feat) || m == 0) && ld >= m && ldf >= m, UT_EINVAL, "encode: bad arguments");
   if (m == 0) return 0;
   return launch_encode(c, values, ld, m, feat, ldf);
 }
@@ -458,7 +458,7 @@ int ut_encode_features(ut_ctx* c, const double* values, int64_t ld, int64_t m, d
 int ut_hash(ut_ctx* c, const double* values, int64_t ld, int64_t m, uint32_t* out) {
   if (!c) return UT_EINVAL;
   UT_CHECK(c, c->has_space, UT_ENOSPACE, "space not defined");
-  UT_CHECK(c, values && out && ld >= m && m >= 0, UT_EINVAL, "hash: bad arguments");
+  UT_CHECK(c, m >= 0 && ((values && out) || m == 0) && ld >= m, UT_EINVAL, "hash: bad arguments");
   return launch_hash(c, values, ld, m, out);
 }
 
@@ -519,7 +519,7 @@ int ut_history_add_host(ut_ctx* c, const uint32_t* dig, int64_t n) {
 
 int ut_dedup(ut_ctx* c, const uint32_t* dig, int64_t m, uint8_t* dup) {
   if (!c) return UT_EINVAL;
-  UT_CHECK(c, dig && dup && m >= 0, UT_EINVAL, "dedup: bad arguments");
+  UT_CHECK(c, m >= 0 && ((dig && dup) || m == 0), UT_EINVAL, "dedup: bad arguments");
   return launch_dedup(c, dig, m, dup);
 }
 
@@ -540,7 +540,7 @@ int ut_gp_fit_async(ut_ctx* c, const double* X, const double* y, int32_t n, int3
 int ut_gp_score(ut_ctx* c, const double* feat, int64_t ld, int64_t m, const ut_acq* acq, const uint8_t* dup,
                 double* mu, double* var, double* score) {
   if (!c) return UT_EINVAL;
-  UT_CHECK(c, feat && ld >= m && m >= 0, UT_EINVAL, "gp_score: bad arguments");
+  UT_CHECK(c, m >= 0 && (feat || m == 0) && ld >= m, UT_EINVAL, "gp_score: bad arguments");
   return gp_score_impl(c, feat, ld, m, acq, dup, mu, var, score);
 }
 

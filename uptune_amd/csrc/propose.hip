@@ -537,7 +537,7 @@ extern "C" int ut_propose_pso(ut_ctx* c, const ut_pso_params* a, const double* g
   UT_CHECK(c, c->has_space && c->pop != nullptr, UT_EINVAL, "propose_pso: population not initialised");
   UT_CHECK(c, c->pso_vel != nullptr && c->pso_cap >= c->npop * c->space.ncols, UT_EINVAL,
            "propose_pso: call ut_pso_reset after (re)initialising the population");
-  UT_CHECK(c, a && gbest && out_values && m >= 0 && cand_base >= 0 && ld >= m, UT_EINVAL,
+  UT_CHECK(c, a && gbest && (out_values || m == 0) && m >= 0 && cand_base >= 0 && ld >= m, UT_EINVAL,
            "propose_pso: bad arguments");
   UT_CHECK(c, a->crossover >= UT_X_NONE && a->crossover <= UT_X_PMX, UT_EINVAL, "propose_pso: bad crossover");
   if (m == 0) return 0;
@@ -573,7 +573,7 @@ extern "C" int ut_propose_ga(ut_ctx* c, const ut_ga_params* a, const double* par
                              uint8_t* out_invalid) {
   if (!c) return UT_EINVAL;
   UT_CHECK(c, c->has_space, UT_ENOSPACE, "space not defined");
-  UT_CHECK(c, a && out_values && m >= 0 && cand_base >= 0 && ld >= m, UT_EINVAL, "propose_ga: bad arguments");
+  UT_CHECK(c, a && (out_values || m == 0) && m >= 0 && cand_base >= 0 && ld >= m, UT_EINVAL, "propose_ga: bad arguments");
   UT_CHECK(c, a->max_retries >= 1 && a->max_retries <= 15, UT_EINVAL, "propose_ga: max_retries must be in [1, 15]");
   UT_CHECK(c, a->must_mutate_count >= 0 && a->must_mutate_count <= c->space.P, UT_EINVAL,
            "propose_ga: must_mutate_count out of range");
