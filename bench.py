@@ -185,15 +185,17 @@ def main():
     t0 = time.perf_counter()
     for s in range(args.steps):
         idx, top = step(args.warmup + s)
-        for st in ("propose", "hash", "dedup", "encode", "kstar", "var", "finalize", "topk"):
-            try:
-                stage_ms.setdefault(st, []).append(eng.stage_time(st))
-            except Exception:
-                pass
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    # per-stage device times of the timed rounds (HIP events recorded on the
+    # library's streams during the rounds, read once here)
+    for st in ("propose", "hash", "dedup", "encode", "kstar", "var", "finalize", "topk"):
+        try:
+            stage_ms[st] = [eng.stage_time(st)]
+        except Exception:
+            pass
     eng.set_timing(False)
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda" if backend == "nccl" else "cpu")

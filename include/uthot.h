@@ -274,8 +274,9 @@ int ut_forest_set(ut_ctx* ctx, int32_t n_trees, const int32_t* roots_host, int64
 int ut_forest_predict(ut_ctx* ctx, const double* features, int64_t ld, int64_t m, int32_t n_features,
                       const uint8_t* dup, double sign, double* pred, double* score);
 
-/* per-kernel device time of the last ut_score_round_* call (ms), when
- * timing is enabled with ut_set_timing(ctx, 1).  names: "propose", "hash",
+/* per-kernel device time (ms) of the ut_score_round_* calls since timing was
+ * enabled with ut_set_timing(ctx, 1), averaged over those rounds.  Events are
+ * recorded without host synchronisation; ut_stage_time synchronises once.  names: "propose", "hash",
  * "dedup", "encode", "gp_fit", "kstar", "var", "finalize", "topk" */
 int ut_set_timing(ut_ctx* ctx, int32_t on);
 int ut_stage_time(ut_ctx* ctx, const char* stage, double* ms);

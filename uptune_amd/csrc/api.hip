@@ -20,33 +20,40 @@ void mark(ut_ctx* c, const char* name) {
   hipEvent_t e;
   if (hipEventCreate(&e) != hipSuccess) return;
   hipEventRecord(e, c->stream);
-  c->timing.marks.push_back({name, c->stream, e});
+  c->timing.marks.push_back({name, c->stream, e, c->timing.round});
 }
 
 static void timing_begin(ut_ctx* c) {
   if (!c->timing.on) return;
-  for (auto& m : c->timing.marks) hipEventDestroy(m.ev);
-  c->timing.marks.clear();
+  ++c->timing.round;
   mark(c, "");
 }
 
-static int timing_end(ut_ctx* c) {
-  if (!c->timing.on) return 0;
+static int timing_end(ut_ctx*) { return 0; }
+
+// read every recorded event into the per-stage totals (one host sync)
+static int timing_collect(ut_ctx* c, bool keep) {
+  auto& T = c->timing;
+  if (T.marks.empty()) return 0;
   UT_HIP(c, ut::sync_all(c));
-  c->timing.last.clear();
-  for (size_t i = 0; i < c->timing.marks.size(); ++i) {
-    const auto& m = c->timing.marks[i];
+  for (size_t i = 0; keep && i < T.marks.size(); ++i) {
+    const auto& m = T.marks[i];
     if (m.name.empty()) continue;
-    for (size_t j = i; j-- > 0;) {  // the previous mark on the same stream
-      if (c->timing.marks[j].stream != m.stream) continue;
+    for (size_t j = i; j-- > 0;) {  // the previous mark of the same round on the same stream
+      if (T.marks[j].round != m.round) break;
+      if (T.marks[j].stream != m.stream) continue;
       float ms = 0.f;
-      hipEventElapsedTime(&ms, c->timing.marks[j].ev, m.ev);
-      c->timing.last.emplace_back(m.name, (double)ms);
+      hipEventElapsedTime(&ms, T.marks[j].ev, m.ev);
+      auto it = T.totals.begin();
+      while (it != T.totals.end() && it->first != m.name) ++it;
+      if (it == T.totals.end()) T.totals.push_back({m.name, {0.0, 0}}), it = T.totals.end() - 1;
+      it->second.first += ms;
+      it->second.second += 1;
       break;
     }
   }
-  for (auto& m : c->timing.marks) hipEventDestroy(m.ev);
-  c->timing.marks.clear();
+  for (auto& m : T.marks) hipEventDestroy(m.ev);
+  T.marks.clear();
   return 0;
 }
 
@@ -191,7 +198,7 @@ int ut_ctx_destroy(ut_ctx* c) {
   fr(c->r_values.p); fr(c->r_feat.p); fr(c->r_mu.p); fr(c->r_var.p); fr(c->r_score.p); fr(c->r_digest.p);
   fr(c->r_dup.p); fr(c->tk_score[0].p); fr(c->tk_score[1].p); fr(c->tk_idx[0].p); fr(c->tk_idx[1].p);
   fr(c->r_topk_idx.p); fr(c->r_topk_score.p); fr(c->perm_ws.p); fr(c->perm_dig.p);
-  fr(c->forest_nodes); fr(c->forest_roots);
+  fr(c->forest_nodes); fr(c->forest_roots); fr(c->r_topk_vals.p);
   for (auto& m : c->timing.marks) hipEventDestroy(m.ev);
   for (hipEvent_t e : {c->ev_fork, c->ev_join, c->ev_fit, c->ev_prefit})
     if (e) hipEventDestroy(e);
@@ -627,18 +634,13 @@ int ut_score_round_de(ut_ctx* c, const ut_de_params* de, const ut_acq* acq, uint
                                c->stream));
     if (out->topk_values || out->topk_digest) {
       double* vals = out->topk_values;
-      ut::DevBuf<double> tmp;
-      if (!vals) {
-        if ((rc = ensure(c, tmp, (size_t)NC * k))) return rc;
-        vals = tmp.p;
+      if (!vals) {  // digests only: the rows go to a context buffer (no per-round alloc / sync)
+        if ((rc = ensure(c, c->r_topk_vals, (size_t)NC * k))) return rc;
+        vals = c->r_topk_vals.p;
       }
-      rc = launch_gather_rows(c, c->r_values.p, ld, c->r_topk_idx.p, cand_base, k, vals, k, c->r_digest.p,
-                              out->topk_digest);
-      if (tmp.p) {
-        UT_HIP(c, ut::sync_all(c));
-        hipFree(tmp.p);
-      }
-      if (rc) return rc;
+      if ((rc = launch_gather_rows(c, c->r_values.p, ld, c->r_topk_idx.p, cand_base, k, vals, k, c->r_digest.p,
+                                   out->topk_digest)))
+        return rc;
     }
   }
   return timing_end(c);
@@ -660,15 +662,20 @@ int ut_round_buffers(ut_ctx* c, double** values, double** features, uint32_t** d
 
 int ut_set_timing(ut_ctx* c, int32_t on) {
   if (!c) return UT_EINVAL;
+  int rc = timing_collect(c, false);  // a (re)start discards what was recorded
+  c->timing.totals.clear();
+  c->timing.round = 0;
   c->timing.on = on != 0;
-  return 0;
+  return rc;
 }
 
 int ut_stage_time(ut_ctx* c, const char* stage, double* ms) {
   if (!c || !stage || !ms) return UT_EINVAL;
-  for (auto& e : c->timing.last)
-    if (e.first == stage) {
-      *ms = e.second;
+  int rc = timing_collect(c, true);
+  if (rc) return rc;
+  for (auto& e : c->timing.totals)
+    if (e.first == stage && e.second.second > 0) {
+      *ms = e.second.first / (double)e.second.second;
       return 0;
     }
   return set_err(c, UT_EINVAL, std::string("no timing for stage ") + stage);

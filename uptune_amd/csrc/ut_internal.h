@@ -86,15 +86,20 @@ struct DevBuf {
   size_t n = 0;
 };
 
+// Per-stage device time of the scoring rounds: events are recorded while the
+// rounds run and read only when a stage time is asked for, so timing adds no
+// host synchronisation between rounds (consecutive rounds still overlap).
 struct Timing {
   struct Mark {
-    std::string name;   // "" = a stream's start point, not reported
+    std::string name;   // "" = a stream's start point in its round, not reported
     hipStream_t stream;
     hipEvent_t ev;
+    int64_t round;
   };
   bool on = false;
-  std::vector<Mark> marks;  // a stage's time = its mark - the previous mark on the same stream
-  std::vector<std::pair<std::string, double>> last;
+  int64_t round = 0;
+  std::vector<Mark> marks;  // a stage's time = its mark - the previous mark of the round on the same stream
+  std::vector<std::pair<std::string, std::pair<double, int64_t>>> totals;  // name -> (sum ms, rounds)
 };
 
 }  // namespace ut
@@ -177,6 +182,7 @@ struct ut_ctx {
   ut::DevBuf<double> perm_ws;    // [2 * perm_cols + 3 * perm_smax][ld]: GA parents + crossover scratch
   ut::DevBuf<uint32_t> perm_dig; // [n_perm][m][8] inner digests of PERM values (hash pre-pass)
   ut::DevBuf<double> r_topk_score;
+  ut::DevBuf<double> r_topk_vals;   // gathered top-k rows when the caller wants digests only
   int64_t r_ld = 0;
   int64_t r_m = 0;
 
