@@ -108,15 +108,18 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--precision", type=int, default=64, choices=(64, 32),
                     help="GP contractions on fp64 MFMA (1e-5 parity) or fp32 MFMA (1e-3 parity)")
-    ap.add_argument("--config", default="c2", choices=("c2", "c3"),
+    ap.add_argument("--config", default="c2", choices=("c2", "c3", "c4"),
                     help="c2 = BASELINE configs[1] (R64, m=1M, n=1024: the headline); c3 = configs[2] per GPU "
-                         "(HPL-64 mixed space, 16M/8 = 2M candidates per GPU, n=4096)")
+                         "(HPL-64 mixed space, 16M/8 = 2M candidates per GPU, n=4096); c4 = configs[3] "
+                         "(gcc 339-flag space, GA proposals, dedup against the 3,680 recorded configs, m=4M)")
     args = ap.parse_args()
     if args.config == "c3":
         if args.m == 1 << 20:
             args.m = 1 << 21
         if args.n == 1024:
             args.n = 4096
+    if args.config == "c4" and args.m == 1 << 20:
+        args.m = 1 << 22
 
     import torch
     import torch.distributed as dist
@@ -143,6 +146,9 @@ def main():
     if args.config == "c3":
         from uptune_amd import spaces
         manip = spaces.hpl64()
+    elif args.config == "c4":
+        from uptune_amd import spaces
+        manip = spaces.gcc()
     else:
         manip = ConfigurationManipulator([FloatParameter(i, -1000.0, 1000.0) for i in range(d)])
     eng = BatchEngine(manip, device=local, seed=1)
@@ -159,13 +165,42 @@ def main():
         X = tr.encode(tr.population_get()).T.contiguous().cpu().numpy()
         y = np.sum((X - 0.3) ** 2, axis=1)
         tr.close()
+    elif args.config == "c4":
+        # the recorded gcc configs (samples/gcc-options/matmul-record.csv, as the
+        # fixture tests/golden/gcc_history.npz): all 3,680 are the dedup history,
+        # the first n with their recorded qor are the GP training set, the best
+        # recorded config is the GA parent (GreedySelectionMixin.select)
+        z = np.load(os.path.join(ROOT, "tests", "golden", "gcc_history.npz"))
+        hist, qor = z["values"], z["qor"]
+        hv = torch.from_numpy(np.ascontiguousarray(hist)).to(eng.device)
+        eng.history_add(eng.hash(hv))
+        d = eng.spec.n_features
+        X = eng.encode(hv[:, :n].contiguous()).T.contiguous().cpu().numpy()
+        y = qor[:n].astype(np.float64)
+        parent = hist[:, int(np.argmin(qor))].copy()
     else:
         X, y = training_set(n, d, 101)
     cand_base = rank * m
     acq = eng.acq("ei", xi=0.0)
-    ell = 1.0 if args.config == "c3" else 0.2
+    ell = {"c2": 0.2, "c3": 1.0, "c4": 2.0}[args.config]
+
+    def step_c4(r):
+        """GA round: UniformGreedyMutation proposals from the best recorded config
+        -> hash_config -> dedup vs history + batch -> encode -> GP-EI -> top-k"""
+        eng.gp_fit(X, y, lengthscale=ell, sigma_f2=1.0, sigma_n2=1e-6, jitter=1e-8, wait=False)
+        vals, invalid = eng.propose_ga(m, parent1=parent, round_=r, cand_base=cand_base, mutation_rate=0.1)
+        dig = eng.hash(vals)
+        dup = torch.maximum(eng.dedup(dig), invalid)
+        _, _, score = eng.gp_score(eng.encode(vals), acq=acq, dup=dup)
+        idx, top = eng.topk(score, k, dup=dup, cand_base=cand_base)
+        if world > 1:
+            sel = torch.where(idx >= 0, idx - cand_base, torch.zeros_like(idx))
+            idx, top = allgather_topk(idx, top, dig[sel], k)
+        return idx, top
 
     def step(r):
+        if args.config == "c4":
+            return step_c4(r)
         eng.gp_fit(X, y, lengthscale=ell, sigma_f2=1.0, sigma_n2=1e-6, wait=False)   # overlaps propose + hash
         idx, top, dig, _ = eng.score_round_de(m, k, round_=r, cand_base=cand_base, cr=0.2, n_cross=1, acq=acq,
                                               want_values=False)
@@ -205,15 +240,28 @@ def main():
     ms_per_step = elapsed * 1000.0 / args.steps
     value = world * m / (elapsed / args.steps)
     stages = {st: float(np.mean(v)) for st, v in stage_ms.items()}
-    # dominant kernel: the variance GEMM  V = L^-1 K*^T  (fp64 MFMA)
+    # dominant kernel: the variance GEMM  V = L^-1 K*^T  (fp64 MFMA); at C4 (707
+    # features) the K* contraction (2 n d flops per candidate) carries more flops
     var_ms = stages.get("var")
     flops_var = float(m) * n * (n + 1)       # algorithmic: lower-triangular n x n times k* per candidate
+    kernel = "k_gp_var<%s> (persistent var contraction L^-1 K*^T, %s)" % (
+        ("double", "v_mfma_f64_16x16x4_f64") if args.precision == 64 else ("float", "v_mfma_f32_32x32x2_f32"))
+    if args.config == "c4" and stages.get("kstar", 0.0) > (var_ms or 0.0):
+        var_ms = stages["kstar"]
+        flops_var = 2.0 * m * n * d
+        kernel = "k_gp_kstar<double> (K* = exp(-|x - u|^2 / 2), fused EI mean, v_mfma_f64_16x16x4_f64)"
     achieved = flops_var / (var_ms * 1e-3) / 1e12 if var_ms else None
     peak = PEAK_FP64_TFLOPS if args.precision == 64 else PEAK_FP32_TFLOPS
     # HBM bytes per launch were profiled on the default C2 round (profiles/pmc_summary.json)
     profiled = args.config == "c2" and (m, n, d) == (1 << 20, 1024, 64)
     traffic = load_traffic("var" if args.precision == 64 else "var32") if profiled else None
-    if args.config == "c3":
+    if args.config == "c4":
+        workload = (f"C4 gcc flags (339 params: 1 + 154 Int, 184 Enum{{on,off,default}}; {d} GP features): GA "
+                    f"mutation 0.1 from the best recorded config + hash_config + dedup vs 3,680 recorded configs "
+                    f"+ GP-EI n={n} (recorded qor) + top-{k}, {m} candidates per GPU")
+        data = ("recorded (samples/gcc-options/matmul-record.csv via tests/golden/gcc_history.npz: history, "
+                "GP training configs and qor); proposals synthetic")
+    elif args.config == "c3":
         workload = (f"C3 HPL-64 mixed (24 Int, 16 Enum, 8 Bool, 8 Float, 4 LogInt, 4 Pow2; {d} GP features): "
                     f"DE-Alt + hash_config + dedup + GP-EI n={n} + top-{k}, {m} candidates per GPU")
         data = "synthetic (HPL-64 configs from op1_randomize; objective = |features - 0.3|^2; population random-init)"
@@ -236,10 +284,7 @@ def main():
         "config": {"workload": workload, "candidates_per_gpu": m, "gp_n": n, "dims": d, "k": k,
                    "parallelism": f"dp{world}"},
         "stage_ms": stages,
-        "roofline": {"bound": "mfma",
-                     "kernel": "k_gp_var<%s> (persistent var contraction L^-1 K*^T, %s)" % (
-                         ("double", "v_mfma_f64_16x16x4_f64") if args.precision == 64 else
-                         ("float", "v_mfma_f32_32x32x2_f32")),
+        "roofline": {"bound": "mfma", "kernel": kernel,
                      "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
                      "frac": (achieved / peak) if achieved else None, "traffic": traffic,
                      "flops_per_launch": flops_var},

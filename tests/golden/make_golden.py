@@ -86,6 +86,11 @@ def gcc_space_and_rows(nrows=512, nhash=64):
     vals = np.array([[float(opts.index(v)) if p.kind == ENUM else float(v) for p, v in zip(params, cfg)]
                      for cfg in cfgs]).T
     np.savez_compressed(os.path.join(HERE, "gcc_rows.npz"), values=vals.astype(np.float64))
+    # every recorded configuration, SoA f64 (enum -> option index): the C4 dedup history
+    allv = np.array([[float(opts.index(code[int(v)])) if p.kind == ENUM else float(v) for p, v in zip(params, row)]
+                     for row in data]).T
+    qor = np.array([float(row[header.index("qor")]) for row in rows])
+    np.savez_compressed(os.path.join(HERE, "gcc_history.npz"), values=allv.astype(np.float64), qor=qor)
     with open(os.path.join(HERE, "gcc_space.json"), "w") as f:
         json.dump({"params": spec, "enum_code": {str(k): v for k, v in code.items()},
                    "source": "samples/gcc-options/matmul-record.csv (int ranges = recorded min..max)",

@@ -26,10 +26,14 @@ void mark(ut_ctx* c, const char* name) {
 static void timing_begin(ut_ctx* c) {
   if (!c->timing.on) return;
   ++c->timing.round;
+  c->timing.in_round = true;
   mark(c, "");
 }
 
-static int timing_end(ut_ctx*) { return 0; }
+static int timing_end(ut_ctx* c) {
+  c->timing.in_round = false;
+  return 0;
+}
 
 // read every recorded event into the per-stage totals (one host sync)
 static int timing_collect(ut_ctx* c, bool keep) {
@@ -548,7 +552,12 @@ int ut_gp_score(ut_ctx* c, const double* feat, int64_t ld, int64_t m, const ut_a
                 double* mu, double* var, double* score) {
   if (!c) return UT_EINVAL;
   UT_CHECK(c, m >= 0 && (feat || m == 0) && ld >= m, UT_EINVAL, "gp_score: bad arguments");
-  return gp_score_impl(c, feat, ld, m, acq, dup, mu, var, score);
+  // a stand-alone scoring call is a timing round of its own (stages kstar, var, finalize)
+  const bool own = c->timing.on && !c->timing.in_round;
+  if (own) timing_begin(c);
+  int rc = gp_score_impl(c, feat, ld, m, acq, dup, mu, var, score);
+  if (own) timing_end(c);
+  return rc;
 }
 
 int ut_gp_set_precision(ut_ctx* c, int32_t bits) {

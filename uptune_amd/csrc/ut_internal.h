@@ -97,6 +97,7 @@ struct Timing {
     int64_t round;
   };
   bool on = false;
+  bool in_round = false;   // inside ut_score_round_* (its stages share one round)
   int64_t round = 0;
   std::vector<Mark> marks;  // a stage's time = its mark - the previous mark of the round on the same stream
   std::vector<std::pair<std::string, std::pair<double, int64_t>>> totals;  // name -> (sum ms, rounds)
