@@ -41,6 +41,10 @@ def bench_hash(m=1 << 20):
         ms = timeit(lambda: eng.hash(vals))
         L, nb, _ = eng.space_info()
         out[name] = {"ms": ms, "outer_blocks": nb, "ns_per_cand": ms * 1e6 / m}
+        if name == "r64_float":   # the bench's input: DE-Alt trials of that population
+            trial = eng.propose_de(m, round_=1, cr=0.2)
+            ms = timeit(lambda: eng.hash(trial))
+            out["r64_de_trials"] = {"ms": ms, "outer_blocks": nb, "ns_per_cand": ms * 1e6 / m}
         del eng
     return out
 

@@ -73,6 +73,19 @@ def test_repr_search_ranges(hc):
         assert _repr(hc, x) == repr(x)
 
 
+def test_repr_integral_floats(hc):
+    """integers in [1, 2^53) take the small-integer path of repr_double"""
+    rng = random.Random(7)
+    xs = [float(v) for v in range(1, 20001)] + [float(10 ** k) for k in range(16)]
+    xs += [float(2 ** k) for k in range(54)] + [float(2 ** 53 - 1), float(2 ** 53), float(2 ** 53 + 2)]
+    xs += [float(rng.randrange(1, 2 ** 53)) for _ in range(20000)]
+    xs += [float(rng.randrange(1, 10 ** 6) * 10 ** rng.randrange(0, 10)) for _ in range(20000)]
+    xs += [math.nextafter(x, 0.0) for x in xs[:3000]] + [math.nextafter(x, math.inf) for x in xs[:3000]]
+    for x in xs:
+        assert _repr(hc, x) == repr(x), x
+        assert _repr(hc, -x) == repr(-x), -x
+
+
 def test_repr_int(hc):
     buf = ctypes.create_string_buffer(32)
     for v in [0, 1, -1, 9, 10, 99, 100, 2**31, -2**31, 2**53 + 1, 2**63 - 1, -2**63, 107572959]:

@@ -411,10 +411,28 @@ UT_HD int repr_double(double x, Emit& out) {
   }
   uint64_t digits;
   int32_t n, decpt;
+  const int32_t e2i = (int32_t)expo - 1023 - 52;
+  const uint64_t m2i = (1ull << 52) | mant;
   if (expo == 0 && mant == 0) {
     digits = 0;
     n = 1;
     decpt = 1;
+  } else if (expo != 0 && e2i <= 0 && e2i >= -52 && (m2i & ((1ull << -e2i) - 1)) == 0) {
+    // an integer in [1, 2^53) (Ryu's d2d_small_int): its shortest digits are the
+    // integer without its trailing zeros.  Taking this path keeps such values
+    // (e.g. a parameter clamped to a bound, 1000.0) out of d2d's trailing-zero
+    // branch, whose digit-removal loop would stall every lane of their wave.
+    uint64_t v = m2i >> -e2i;
+    int32_t e10 = 0;
+    for (;;) {
+      const uint64_t q = v / 10;
+      if (v - 10 * q != 0) break;
+      v = q;
+      ++e10;
+    }
+    digits = v;
+    n = (int32_t)decimal_length17(digits);
+    decpt = n + e10;
   } else {
     const Dec64 d = d2d(mant, expo);
     digits = d.mantissa;
@@ -423,16 +441,38 @@ UT_HD int repr_double(double x, Emit& out) {
   }
   const int s = neg ? 1 : 0;
   if (neg) out.put(0, '-');
+  // The four layouts of repr (Python's float_repr_style 'short'):
+  //   exponent  d[.ddd]e(+|-)XX      decpt <= -4 or decpt > 16
+  //   leading   0.000ddd             decpt <= 0
+  //   inner     ddd.ddd              0 < decpt < n
+  //   trailing  ddd000.0             decpt >= n
+  // The digits are emitted by ONE loop for every layout -- digit i goes to
+  // s + i + shift + (i >= split) -- so lanes of a wave that format values of
+  // different layouts (e.g. 1000.0 beside 123.456) do not run several digit
+  // loops (each a 64-bit division by 10 per digit) one after the other.
   const bool use_exp = (decpt <= -4) || (decpt > 16);
+  int shift, split;
   if (use_exp) {
-    // d[.ddd]e(+|-)XX
+    shift = 0;
+    split = 1;
+  } else if (decpt <= 0) {
+    shift = 2 - decpt;
+    split = 1 << 30;
+  } else if (decpt < n) {
+    shift = 0;
+    split = decpt;
+  } else {
+    shift = 0;
+    split = 1 << 30;
+  }
+  for (int i = n - 1; i >= 0; --i) {
+    const uint64_t q = digits / 10;
+    const uint32_t dg = (uint32_t)(digits - 10 * q);
+    digits = q;
+    out.put(s + i + shift + (i >= split ? 1 : 0), (uint8_t)('0' + dg));
+  }
+  if (use_exp) {
     int pos = s + n + (n > 1 ? 1 : 0);
-    for (int i = n - 1; i >= 0; --i) {
-      const uint64_t q = digits / 10;
-      const uint32_t dg = (uint32_t)(digits - 10 * q);
-      digits = q;
-      out.put(s + i + (i >= 1 ? 1 : 0), (uint8_t)('0' + dg));
-    }
     if (n > 1) out.put(s + 1, '.');
     int e = decpt - 1;
     out.put(pos++, 'e');
@@ -447,36 +487,14 @@ UT_HD int repr_double(double x, Emit& out) {
     return pos;
   }
   if (decpt <= 0) {
-    // 0.000ddd
     out.put(s, '0');
     out.put(s + 1, '.');
     for (int z = 0; z < -decpt; ++z) out.put(s + 2 + z, '0');
-    const int base = s + 2 - decpt;
-    for (int i = n - 1; i >= 0; --i) {
-      const uint64_t q = digits / 10;
-      const uint32_t dg = (uint32_t)(digits - 10 * q);
-      digits = q;
-      out.put(base + i, (uint8_t)('0' + dg));
-    }
-    return base + n;
+    return s + 2 - decpt + n;
   }
   if (decpt < n) {
-    // ddd.ddd
-    for (int i = n - 1; i >= 0; --i) {
-      const uint64_t q = digits / 10;
-      const uint32_t dg = (uint32_t)(digits - 10 * q);
-      digits = q;
-      out.put(s + i + (i >= decpt ? 1 : 0), (uint8_t)('0' + dg));
-    }
     out.put(s + decpt, '.');
     return s + n + 1;
-  }
-  // ddd000.0
-  for (int i = n - 1; i >= 0; --i) {
-    const uint64_t q = digits / 10;
-    const uint32_t dg = (uint32_t)(digits - 10 * q);
-    digits = q;
-    out.put(s + i, (uint8_t)('0' + dg));
   }
   for (int z = n; z < decpt; ++z) out.put(s + z, '0');
   out.put(s + decpt, '.');
