@@ -104,7 +104,8 @@ def main():
     ap.add_argument("--n", type=int, default=1024, help="GP training points")
     ap.add_argument("--d", type=int, default=64)
     ap.add_argument("--k", type=int, default=256)
-    ap.add_argument("--cpu-sample", type=int, default=8192)
+    ap.add_argument("--cpu-sample", type=int, default=32768,
+                    help="candidates in the CPU-baseline sample (about 10 s of single-thread oracle work)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--precision", type=int, default=64, choices=(64, 32),
                     help="GP contractions on fp64 MFMA (1e-5 parity) or fp32 MFMA (1e-3 parity)")

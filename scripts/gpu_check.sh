@@ -10,7 +10,7 @@ rc=$?; echo "pytest rc=$rc"; tail -30 gpurun_out/pytest_gpu.log; stop_if_fatal $
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
 rc=$?; echo "smoke rc=$rc"; tail -5 gpurun_out/smoke.log; stop_if_fatal $rc smoke
 [ -n "$SKIP_BENCH" ] && exit 0
-timeout -k 10 ${BENCH_TIMEOUT:-600} python bench.py ${BENCH_ARGS:---steps 5 --warmup 2 --cpu-sample 2048} \
+timeout -k 10 ${BENCH_TIMEOUT:-600} python bench.py ${BENCH_ARGS:---steps 5 --warmup 2 --cpu-sample 32768} \
   > gpurun_out/bench.log 2>&1
 rc=$?; echo "bench rc=$rc"; tail -5 gpurun_out/bench.log
 exit $rc
