@@ -291,7 +291,7 @@ def main():
                      "flops_per_launch": flops_var},
         "cpu_baseline": None,
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "c2":
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.cpu_sample > 0 and args.config == "c2":
         try:
             result["cpu_baseline"] = cpu_baseline(args.cpu_sample, n, d, k)
         except Exception as ex:  # keep the GPU number even if the baseline fails

@@ -34,6 +34,7 @@
 namespace ut {
 
 constexpr int HASH_NT = 128;
+constexpr int HASH_WG_PER_CU = 3;                  // grid cap, see launch_hash
 constexpr int SCR_WORDS = 7;                       // inner message bytes 0..27
 
 typedef uint32_t hex32 __attribute__((ext_vector_type(32)));
@@ -152,74 +153,78 @@ __global__ __launch_bounds__(HASH_NT) void k_hash(const DevParam* __restrict__ p
                                                   uint32_t* __restrict__ out) {
   __shared__ uint32_t lds[SCR_WORDS * HASH_NT];
   const int lane = threadIdx.x;
-  const int64_t i0 = (int64_t)blockIdx.x * HASH_NT + lane;
-  const bool valid = i0 < m;
-  const int64_t i = valid ? i0 : (m - 1);
-  hex32 HX = {};  // two 16-word hex slots: hole j in HX[16 (j % 2) .. 16 (j % 2) + 15]
-  uint32_t H[8];
-  sha256_init(H);
-  int32_t next = 0;
-  // the value of the next parameter to digest is loaded one parameter ahead
-  double vnext = values[(int64_t)order_col[0] * ld + i];
-  for (int32_t b = 0; b < nblocks; ++b) {
-    const int32_t last = block_last[b];
-    while (next <= last) {
-      const int32_t p = order[next];
-      const DevParam pr = params[p];
-      const double v = vnext;
-      uint32_t D[8];
-      if (pr.hash_mode == HM_LUT) {
-        const uint4* src = lut + 2 * lut_row(pr, v);
-        const uint4 a = src[0], c = src[1];  // issued before the prefetch: waits leave it in flight
-        if (next + 1 < P) vnext = values[(int64_t)order_col[next + 1] * ld + i];
-        D[0] = a.x; D[1] = a.y; D[2] = a.z; D[3] = a.w;
-        D[4] = c.x; D[5] = c.y; D[6] = c.z; D[7] = c.w;
-      } else if (pr.hash_mode == HM_PERM) {
-        const uint4* src = perm_dig + 2 * ((int64_t)pr.pslot * m + i);
-        const uint4 a = src[0], c = src[1];
-        if (next + 1 < P) vnext = values[(int64_t)order_col[next + 1] * ld + i];
-        D[0] = a.x; D[1] = a.y; D[2] = a.z; D[3] = a.w;
-        D[4] = c.x; D[5] = c.y; D[6] = c.z; D[7] = c.w;
-      } else {
-        if (next + 1 < P) vnext = values[(int64_t)order_col[next + 1] * ld + i];
-        repr_digest(pr, v, lds, lane, D);
-      }
-      // 64 hex characters as 16 big-endian words into slot next % 2
-      if (next & 1) {
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          HX[16 + 2 * k] = hex4(D[k] >> 16);
-          HX[16 + 2 * k + 1] = hex4(D[k] & 0xFFFFu);
+  // grid-stride over candidate blocks: the grid is sized to leave CU slots
+  // free for the GP fit's small kernels that run beside the hash
+  for (int64_t blk = blockIdx.x; blk * HASH_NT < m; blk += gridDim.x) {
+    const int64_t i0 = blk * HASH_NT + lane;
+    const bool valid = i0 < m;
+    const int64_t i = valid ? i0 : (m - 1);
+    hex32 HX = {};  // two 16-word hex slots: hole j in HX[16 (j % 2) .. 16 (j % 2) + 15]
+    uint32_t H[8];
+    sha256_init(H);
+    int32_t next = 0;
+    // the value of the next parameter to digest is loaded one parameter ahead
+    double vnext = values[(int64_t)order_col[0] * ld + i];
+    for (int32_t b = 0; b < nblocks; ++b) {
+      const int32_t last = block_last[b];
+      while (next <= last) {
+        const int32_t p = order[next];
+        const DevParam pr = params[p];
+        const double v = vnext;
+        uint32_t D[8];
+        if (pr.hash_mode == HM_LUT) {
+          const uint4* src = lut + 2 * lut_row(pr, v);
+          const uint4 a = src[0], c = src[1];  // issued before the prefetch: waits leave it in flight
+          if (next + 1 < P) vnext = values[(int64_t)order_col[next + 1] * ld + i];
+          D[0] = a.x; D[1] = a.y; D[2] = a.z; D[3] = a.w;
+          D[4] = c.x; D[5] = c.y; D[6] = c.z; D[7] = c.w;
+        } else if (pr.hash_mode == HM_PERM) {
+          const uint4* src = perm_dig + 2 * ((int64_t)pr.pslot * m + i);
+          const uint4 a = src[0], c = src[1];
+          if (next + 1 < P) vnext = values[(int64_t)order_col[next + 1] * ld + i];
+          D[0] = a.x; D[1] = a.y; D[2] = a.z; D[3] = a.w;
+          D[4] = c.x; D[5] = c.y; D[6] = c.z; D[7] = c.w;
+        } else {
+          if (next + 1 < P) vnext = values[(int64_t)order_col[next + 1] * ld + i];
+          repr_digest(pr, v, lds, lane, D);
         }
-      } else {
+        // 64 hex characters as 16 big-endian words into slot next % 2
+        if (next & 1) {
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          HX[2 * k] = hex4(D[k] >> 16);
-          HX[2 * k + 1] = hex4(D[k] & 0xFFFFu);
+          for (int k = 0; k < 8; ++k) {
+            HX[16 + 2 * k] = hex4(D[k] >> 16);
+            HX[16 + 2 * k + 1] = hex4(D[k] & 0xFFFFu);
+          }
+        } else {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            HX[2 * k] = hex4(D[k] >> 16);
+            HX[2 * k + 1] = hex4(D[k] & 0xFFFFu);
+          }
         }
+        ++next;
       }
-      ++next;
-    }
-    uint32_t W[16];
-    const uint2* hw = words + (int64_t)b * 16;
+      uint32_t W[16];
+      const uint2* hw = words + (int64_t)b * 16;
 #pragma unroll
-    for (int w = 0; w < 16; ++w) {
-      const uint2 e = hw[w];  // scalar load: the same word for every lane
-      uint32_t x = e.x;
-      if (e.y) {
-        const uint32_t lo = (e.y & HW_LO_VALID) ? HX[e.y & 31u] : 0u;
-        const uint32_t hi = (e.y & HW_HI_VALID) ? HX[(e.y >> HW_HI_POS) & 31u] : 0u;
-        const uint64_t cat = ((uint64_t)lo << 32) | hi;
-        x |= (uint32_t)((cat << ((e.y >> HW_SHIFT_POS) & 31u)) >> 32);
+      for (int w = 0; w < 16; ++w) {
+        const uint2 e = hw[w];  // scalar load: the same word for every lane
+        uint32_t x = e.x;
+        if (e.y) {
+          const uint32_t lo = (e.y & HW_LO_VALID) ? HX[e.y & 31u] : 0u;
+          const uint32_t hi = (e.y & HW_HI_VALID) ? HX[(e.y >> HW_HI_POS) & 31u] : 0u;
+          const uint64_t cat = ((uint64_t)lo << 32) | hi;
+          x |= (uint32_t)((cat << ((e.y >> HW_SHIFT_POS) & 31u)) >> 32);
+        }
+        W[w] = x;
       }
-      W[w] = x;
+      sha256_compress(H, W);
     }
-    sha256_compress(H, W);
-  }
-  if (valid) {
-    uint4* dst = reinterpret_cast<uint4*>(out + i * 8);
-    dst[0] = make_uint4(H[0], H[1], H[2], H[3]);
-    dst[1] = make_uint4(H[4], H[5], H[6], H[7]);
+    if (valid) {
+      uint4* dst = reinterpret_cast<uint4*>(out + i * 8);
+      dst[0] = make_uint4(H[0], H[1], H[2], H[3]);
+      dst[1] = make_uint4(H[4], H[5], H[6], H[7]);
+    }
   }
 }
 
@@ -236,7 +241,17 @@ int launch_hash(ut_ctx* c, const double* values, int64_t ld, int64_t m, uint32_t
     UT_LAUNCH_CHECK(c);
     pd = c->perm_dig.p;
   }
-  hipLaunchKernelGGL(k_hash, dim3(grid1(m, HASH_NT)), dim3(HASH_NT), 0, c->stream, s.d_params, s.d_order,
+  // In a round the hash runs on the side stream beside a GP fit that may still
+  // be in flight on the fit stream.  A full grid then keeps every CU's wave
+  // slots busy and the fit's small Cholesky/trinv kernels queue behind it
+  // (~3 ms per C2 round); capped at 3 resident workgroups per CU the hash is
+  // slower on its own but the round is shorter (C2 sweep, 2/3/4/6 per CU vs
+  // uncapped: 33.7/32.7/33.9/35.1 vs 33.9 ms).  With no fit in flight the
+  // hash takes the whole chip.
+  int64_t nb = (int64_t)grid1(m, HASH_NT);
+  const bool fit_in_flight = c->fit_pending && hipEventQuery(c->ev_fit) == hipErrorNotReady;
+  if (fit_in_flight && nb > (int64_t)c->n_cu * HASH_WG_PER_CU) nb = (int64_t)c->n_cu * HASH_WG_PER_CU;
+  hipLaunchKernelGGL(k_hash, dim3((unsigned)nb), dim3(HASH_NT), 0, c->stream, s.d_params, s.d_order,
                      s.d_order_col, reinterpret_cast<const uint2*>(s.d_words), s.d_block_last,
                      (int32_t)s.outer_blocks, s.P, reinterpret_cast<const uint4*>(s.d_lut), values, ld, m,
                      reinterpret_cast<const uint4*>(pd), out);
