@@ -133,15 +133,25 @@ def broadcast_results(y: Optional[torch.Tensor], digests: Optional[torch.Tensor]
                       group: Optional[dist.ProcessGroup] = None) -> Tuple[torch.Tensor, torch.Tensor]:
     """The per-round history delta of the search loop: objective values [n] f64
     and digests [n][8] i32 of the configurations evaluated on `src`, sent to
-    every rank (api.sync's result injection, api.py:547-553, mapped onto one
-    RCCL broadcast per tensor)."""
+    every rank (api.sync's result injection, api.py:547-553).
+
+    Two broadcasts: src's count, then one [count][5] f64 payload (the value and
+    the digest's 32 bytes reinterpreted as 4 f64).  The count travels first so
+    that a rank whose own `n` differs still receives the payload in step and can
+    report the divergence instead of breaking the collective; the returned
+    tensors are src's (check their length against `n`)."""
     cd = _comm_device(group, device)
-    if dist.get_rank(group) == src:
-        y = y.to(cd, torch.float64).contiguous()
-        digests = digests.to(cd, torch.int32).contiguous()
+    is_src = dist.get_rank(group) == src
+    cnt = torch.tensor([n if is_src else -1], dtype=torch.int64, device=cd)
+    dist.broadcast(cnt, src, group=group)
+    ns = int(cnt.item())
+    if is_src:
+        pay = torch.cat([y.to(cd, torch.float64).reshape(ns, 1),
+                         digests.to(cd, torch.int32).contiguous().view(torch.float64).reshape(ns, 4)], dim=1)
     else:
-        y = torch.empty((n,), dtype=torch.float64, device=cd)
-        digests = torch.empty((n, 8), dtype=torch.int32, device=cd)
-    dist.broadcast(y, src, group=group)
-    dist.broadcast(digests, src, group=group)
+        pay = torch.empty((ns, 5), dtype=torch.float64, device=cd)
+    if ns > 0:
+        dist.broadcast(pay, src, group=group)
+    y = pay[:, 0].contiguous()
+    digests = pay[:, 1:].contiguous().view(torch.int32).reshape(ns, 8)
     return y, digests

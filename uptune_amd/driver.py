@@ -247,7 +247,7 @@ class DistributedSearchDriver(SearchDriver):
         y = torch.tensor([evaluate(c) for c in cfgs], dtype=torch.float64) if src else None
         dev = self.device if self.device is not None else torch.device("cpu")
         y, dig = broadcast_results(y, kd if src else None, len(cfgs), dev, self.src, self.group)
-        if not torch.equal(dig.cpu(), kd):
+        if dig.shape[0] != len(cfgs) or not torch.equal(dig.cpu(), kd):
             raise RuntimeError("initial design differs between ranks")
         self.record_seed(cfgs, y.cpu().tolist(), keys)
 
@@ -268,7 +268,7 @@ class DistributedSearchDriver(SearchDriver):
             y = torch.tensor([evaluate(dr.configuration) for dr in todo], dtype=torch.float64) \
                 if rank == self.src else None
             y, dig = broadcast_results(y, keys if rank == self.src else None, n, dev, self.src, self.group)
-            if not torch.equal(dig.cpu(), keys):
+            if dig.shape[0] != n or not torch.equal(dig.cpu(), keys):
                 raise RuntimeError(f"rank {rank}: requested configurations diverged from rank {self.src}")
             for dr, t in zip(todo, y.cpu().tolist()):
                 self.report(dr, t)
