@@ -1,5 +1,5 @@
 """Per-kernel microbenchmarks on synthetic inputs (one process, HIP events on
-the library stream).  Usage: python scripts/microbench.py [hash|forest|all]"""
+the library stream).  Usage: python scripts/microbench.py [hash|fit|score|forest|all]"""
 import json
 import os
 import sys
@@ -102,6 +102,30 @@ def bench_fit(d=64):
     return out
 
 
+def bench_score(m=1 << 20, d=64):
+    """standalone ut_gp_score stages (K*, variance) at C2 shapes, fp64 and fp32,
+    with nothing running beside them"""
+    out = {}
+    eng = BatchEngine(ConfigurationManipulator([FloatParameter(i, 0.0, 1.0) for i in range(d)]), seed=1)
+    rng = np.random.default_rng(0)
+    X = rng.uniform(size=(1024, d))
+    y = np.sum((X - 0.4) ** 2, axis=1)
+    feat = torch.rand(d, m, dtype=torch.float64, device="cuda")
+    for prec in (64, 32):
+        eng.gp_set_precision(prec)
+        eng.gp_fit(X, y, lengthscale=0.2, sigma_f2=1.0, sigma_n2=1e-6)
+        eng.gp_score(feat)
+        torch.cuda.synchronize()
+        eng.set_timing(True)            # stage times are averaged over the calls from here
+        for _ in range(5):
+            eng.gp_score(feat)
+        torch.cuda.synchronize()
+        out[f"fp{prec}"] = {st: eng.stage_time(st) for st in ("kstar", "var")}
+        eng.set_timing(False)
+    eng.gp_set_precision(64)
+    return out
+
+
 if __name__ == "__main__":
     which = sys.argv[1] if len(sys.argv) > 1 else "all"
     res = {}
@@ -109,6 +133,8 @@ if __name__ == "__main__":
         res["hash"] = bench_hash()
     if which in ("fit", "all"):
         res["fit"] = bench_fit()
+    if which in ("score", "all"):
+        res["score"] = bench_score()
     if which in ("forest", "all"):
         res["forest"] = bench_forest()
     print(json.dumps(res, indent=1))

@@ -30,6 +30,33 @@ __global__ void k_to_f32(const double* __restrict__ src, float* __restrict__ dst
 //   columns >= m zero; written by k_gp_prep_cand)
 // ---------------------------------------------------------------------------
 constexpr int K_NT = 256, K_BM = 128, K_BN = 128, K_BK = 16;
+
+// sf2 * exp(x) for x in [-1000, 0], table-driven: x = (32 k' + j) ln2/32 + r,
+// |r| <= ln2/64, so exp(x) = 2^k' * 2^(j/32) * e^r with a degree-6 polynomial
+// for e^r (truncation < 4e-18) and etab[j] = sf2 * 2^(j/32) built in LDS by each
+// workgroup.  About 16 VALU ops against ~32 for the library exp with its range
+// checks (the epilogue shares the SIMDs with the f64 MFMAs, so every op counts).
+// Max error ~2 ulp; 2^k' underflows to exactly 0 at x = -1000.
+constexpr int EXP_TAB = 32;
+
+__device__ __forceinline__ double sf2_exp_nonpos(double x, const double* etab) {
+  constexpr double INV_L = 46.16624130844683;        // 32 / ln 2
+  constexpr double L_HI = 0.02166084938653512;        // ln2/32 to 32 bits: kf * L_HI is exact
+  constexpr double L_LO = 5.9631716539705866e-12;     // ln2/32 - L_HI
+  const double kf = __builtin_rint(x * INV_L);
+  double r = __builtin_fma(kf, -L_HI, x);
+  r = __builtin_fma(kf, -L_LO, r);
+  double p = 1.0 / 720.0;
+  p = __builtin_fma(p, r, 1.0 / 120.0);
+  p = __builtin_fma(p, r, 1.0 / 24.0);
+  p = __builtin_fma(p, r, 1.0 / 6.0);
+  p = __builtin_fma(p, r, 0.5);
+  p = __builtin_fma(p, r, 1.0);
+  p = __builtin_fma(p, r, 1.0);
+  const int k = (int)kf;
+  return __builtin_ldexp(p * etab[k & 31], k >> 5);
+}
+
 constexpr int K_SA = K_BK * K_BM, K_SB = K_BK * K_BN, K_STAGE = K_SA + K_SB;
 
 __device__ __forceinline__ void kstar_issue(const double* __restrict__ AT, int64_t lda, const double* __restrict__ B,
@@ -58,10 +85,13 @@ __global__ __launch_bounds__(K_NT, 2) void k_gp_kstar(const double* __restrict__
                                                       const double* __restrict__ alpha, double sf2, int32_t n,
                                                       int64_t m, int32_t* __restrict__ ticket, TS* __restrict__ kst,
                                                       int64_t ldk, double* __restrict__ part) {
-  // one __shared__ object (see k_gp_var): the 2-stage ring, then the ticket slot
-  __shared__ __attribute__((aligned(16))) double lds[2 * K_STAGE + 2];
-  int32_t& s_item = *reinterpret_cast<int32_t*>(lds + 2 * K_STAGE);
+  // one __shared__ object (see k_gp_var): the 2-stage ring, the exp table,
+  // then the ticket slot
+  __shared__ __attribute__((aligned(16))) double lds[2 * K_STAGE + EXP_TAB + 2];
+  double* etab = lds + 2 * K_STAGE;
+  int32_t& s_item = *reinterpret_cast<int32_t*>(lds + 2 * K_STAGE + EXP_TAB);
   const int t = threadIdx.x, lane = t & 63;
+  if (t < EXP_TAB) etab[t] = sf2 * exp2((double)t / EXP_TAB);  // published by the first ticket barrier
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
   const int wm = w >> 1, wn = w & 1;
   const int32_t xcd = blockIdx.x & 7;
@@ -110,36 +140,40 @@ __global__ __launch_bounds__(K_NT, 2) void k_gp_kstar(const double* __restrict__
 
     __syncthreads();  // ring free: reuse as the column reduction buffer
     double* red = lds;  // [2][128]
-    // operands of the epilogue loaded up front and unconditionally (rows < npad,
+    // epilogue operands loaded up front and unconditionally (rows < npad,
     // columns < ldk are always in range): a load under a per-element condition
-    // makes hipcc wait vmcnt(0) per element
-    double xn[4][4], al[4][4];
+    // makes hipcc wait vmcnt(0) per element.  Padding rows / columns get a
+    // huge negative half-norm, so their k* is exactly 0 without a select.
+    double hx[4][4], al[4][4];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int32_t row = row0 + wm * 64 + i * 16 + (lane >> 4) + 4 * r;
-        xn[i][r] = xnorm[row];
+        const double xr = xnorm[row];
+        hx[i][r] = row < n ? -0.5 * xr : -1e300;
         al[i][r] = alpha[row];
       }
-    double cn[4];
+    double hc[4];
 #pragma unroll
-    for (int jj = 0; jj < 4; ++jj) cn[jj] = cnorm[col0 + wn * 64 + jj * 16 + (lane & 15)];
+    for (int jj = 0; jj < 4; ++jj) {
+      const int64_t col = col0 + wn * 64 + jj * 16 + (lane & 15);
+      const double cr = cnorm[col];
+      hc[jj] = col < m ? -0.5 * cr : -1e300;
+    }
 #pragma unroll
     for (int jj = 0; jj < 4; ++jj) {
       const int cl = wn * 64 + jj * 16 + (lane & 15);
       const int64_t col = col0 + cl;
-      const bool cin = col < m;
       double s = 0.0;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int32_t row = row0 + wm * 64 + i * 16 + (lane >> 4) + 4 * r;
-          double d2 = xn[i][r] + cn[jj] - 2.0 * acc[i][jj][r];
-          d2 = d2 > 0.0 ? d2 : 0.0;
-          const double e = sf2 * exp(-0.5 * d2);
-          const double ks = (row < n && cin) ? e : 0.0;
+          // -|x - u|^2 / 2 = C - |x|^2/2 - |u|^2/2, clamped to [-1000, 0]
+          const double x = __builtin_fmax(__builtin_fmin((acc[i][jj][r] + hx[i][r]) + hc[jj], 0.0), -1000.0);
+          const double ks = sf2_exp_nonpos(x, etab);
           kst[(int64_t)row * ldk + col] = (TS)ks;
           s += al[i][r] * ks;
         }
