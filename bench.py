@@ -250,7 +250,7 @@ def main():
     if args.config == "c4" and stages.get("kstar", 0.0) > (var_ms or 0.0):
         var_ms = stages["kstar"]
         flops_var = 2.0 * m * n * d
-        kernel = "k_gp_kstar<double> (K* = exp(-|x - u|^2 / 2), fused EI mean, v_mfma_f64_16x16x4_f64)"
+        kernel = "k_gp_kstar<double, false> (K* = exp(-|x - u|^2 / 2), v_mfma_f64_16x16x4_f64)"
     achieved = flops_var / (var_ms * 1e-3) / 1e12 if var_ms else None
     peak = PEAK_FP64_TFLOPS if args.precision == 64 else PEAK_FP32_TFLOPS
     # HBM bytes per launch were profiled on the default C2 round (profiles/pmc_summary.json)

@@ -9,7 +9,7 @@ import json
 import sys
 from collections import defaultdict
 
-KERNELS = {"var": "void ut::k_gp_var<double>", "kstar": "void ut::k_gp_kstar<double>", "hash": "ut::k_hash",
+KERNELS = {"var": "void ut::k_gp_var<double>", "kstar": "void ut::k_gp_kstar<double, false>", "hash": "ut::k_hash",
            "propose": "ut::k_de("}
 
 

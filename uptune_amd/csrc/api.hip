@@ -179,7 +179,8 @@ int ut_ctx_create(int device, uint64_t seed, ut_ctx** out) {
       hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_fit, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&c->ev_prefit, hipEventDisableTiming) != hipSuccess) {
+      hipEventCreateWithFlags(&c->ev_prefit, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_fit_x, hipEventDisableTiming) != hipSuccess) {
     ut_ctx_destroy(c);
     return UT_EHIP;
   }
@@ -196,7 +197,7 @@ int ut_ctx_destroy(ut_ctx* c) {
   auto fr = [](void* p) { if (p) hipFree(p); };
   fr(c->pop); fr(c->pso_vel); fr(c->pso_best); fr(c->hist_keys); fr(c->hist_state); fr(c->batch_slots);
   fr(c->gp_Xs); fr(c->gp_xnorm); fr(c->gp_K); fr(c->gp_Linv); fr(c->gp_y); fr(c->gp_tmp);
-  fr(c->gp_alpha); fr(c->gp_inv_ell); fr(c->gp_stats); fr(c->gp_flag); fr(c->gp_Xs_f); fr(c->gp_T);
+  fr(c->gp_alpha); fr(c->gp_beta); fr(c->gp_inv_ell); fr(c->gp_stats); fr(c->gp_flag); fr(c->gp_Xs_f); fr(c->gp_T);
   fr(c->gp_LinvT); fr(c->gp_LinvT_f); fr(c->gp_ctr); fr(c->gp_XsT); fr(c->ucand.p);
   fr(c->kst.p); fr(c->mu_part.p); fr(c->var_part.p); fr(c->cnorm.p);
   fr(c->r_values.p); fr(c->r_feat.p); fr(c->r_mu.p); fr(c->r_var.p); fr(c->r_score.p); fr(c->r_digest.p);
@@ -204,7 +205,7 @@ int ut_ctx_destroy(ut_ctx* c) {
   fr(c->r_topk_idx.p); fr(c->r_topk_score.p); fr(c->perm_ws.p); fr(c->perm_dig.p);
   fr(c->forest_nodes); fr(c->forest_roots); fr(c->r_topk_vals.p);
   for (auto& m : c->timing.marks) hipEventDestroy(m.ev);
-  for (hipEvent_t e : {c->ev_fork, c->ev_join, c->ev_fit, c->ev_prefit})
+  for (hipEvent_t e : {c->ev_fork, c->ev_join, c->ev_fit, c->ev_prefit, c->ev_fit_x})
     if (e) hipEventDestroy(e);
   if (c->fit_host) hipHostFree(c->fit_host);
   for (hipStream_t st : {c->own_stream, c->side, c->fit_stream})

@@ -458,7 +458,7 @@ static int gp_alloc(ut_ctx* c, int32_t npad, int32_t d) {
   if (c->gp_Xs) {
     UT_HIP(c, ut::sync_all(c));
     hipFree(c->gp_Xs); hipFree(c->gp_xnorm); hipFree(c->gp_K); hipFree(c->gp_Linv);
-    hipFree(c->gp_y); hipFree(c->gp_tmp); hipFree(c->gp_alpha); hipFree(c->gp_inv_ell);
+    hipFree(c->gp_y); hipFree(c->gp_tmp); hipFree(c->gp_alpha); hipFree(c->gp_beta); hipFree(c->gp_inv_ell);
     hipFree(c->gp_stats); hipFree(c->gp_flag);
   }
   UT_HIP(c, hipMalloc((void**)&c->gp_Xs, sizeof(double) * npad * d));
@@ -468,6 +468,7 @@ static int gp_alloc(ut_ctx* c, int32_t npad, int32_t d) {
   UT_HIP(c, hipMalloc((void**)&c->gp_y, sizeof(double) * npad));
   UT_HIP(c, hipMalloc((void**)&c->gp_tmp, sizeof(double) * npad * (d + 1)));
   UT_HIP(c, hipMalloc((void**)&c->gp_alpha, sizeof(double) * npad));
+  UT_HIP(c, hipMalloc((void**)&c->gp_beta, sizeof(double) * npad));
   UT_HIP(c, hipMalloc((void**)&c->gp_inv_ell, sizeof(double) * d));
   UT_HIP(c, hipMalloc((void**)&c->gp_stats, sizeof(double) * 4));
   UT_HIP(c, hipMalloc((void**)&c->gp_flag, sizeof(int32_t)));
@@ -520,6 +521,10 @@ int gp_fit_enqueue(ut_ctx* c, const double* X, const double* y, int32_t n, int32
   UT_HIP(c, hipMemsetAsync(c->gp_flag, 0, sizeof(int32_t), c->stream));
   hipLaunchKernelGGL(k_gp_prep_train, dim3(grid1(npad, 256)), dim3(256), 0, c->stream, dX, n, npad, d,
                      c->gp_inv_ell, c->gp_Xs, c->gp_xnorm);
+  // the candidate side of K* needs only the scaled inputs: fp64 scoring starts
+  // its K* here while the factorisation below is still running
+  if ((rc = launch_xs_t(c, c->gp_Xs, npad, d, ((d + 15) / 16) * 16, c->gp_XsT))) return rc;
+  UT_HIP(c, hipEventRecord(c->ev_fit_x, c->stream));
   hipLaunchKernelGGL(k_gp_kmat, dim3(npad / 64, npad / 64), dim3(256), 0, c->stream, c->gp_Xs,
                      c->gp_xnorm, n, npad, d, h->sigma_f2, h->sigma_n2 + h->jitter, c->gp_K);
   hipLaunchKernelGGL(k_gp_ystats, dim3(1), dim3(256), 0, c->stream, dy, n, npad, c->gp_y, c->gp_stats);
@@ -544,12 +549,11 @@ int gp_fit_enqueue(ut_ctx* c, const double* X, const double* y, int32_t n, int32
   }
   UT_LAUNCH_CHECK(c);
   hipLaunchKernelGGL(k_lower_mv, dim3(grid1(npad, 4)), dim3(256), 0, c->stream, c->gp_Linv, npad, c->gp_y,
-                     c->gp_tmp);
-  hipLaunchKernelGGL(k_lower_tmv, dim3(grid1(npad, 64)), dim3(256), 0, c->stream, c->gp_Linv, npad, c->gp_tmp,
+                     c->gp_beta);
+  hipLaunchKernelGGL(k_lower_tmv, dim3(grid1(npad, 64)), dim3(256), 0, c->stream, c->gp_Linv, npad, c->gp_beta,
                      c->gp_alpha);
   UT_LAUNCH_CHECK(c);
   if (c->gp_prec == 32 && (rc = launch_to_f32(c, c->gp_Xs, c->gp_Xs_f, (int64_t)npad * d))) return rc;
-  if ((rc = launch_xs_t(c, c->gp_Xs, npad, d, ((d + 15) / 16) * 16, c->gp_XsT))) return rc;
   if ((rc = launch_transpose(c, c->gp_Linv, npad, c->gp_LinvT, c->gp_prec == 32 ? c->gp_LinvT_f : nullptr))) return rc;
   c->gp_fit_prec = c->gp_prec;
   UT_HIP(c, hipEventRecord(c->ev_fit, c->stream));
@@ -576,14 +580,19 @@ int gp_score_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, const ut
   UT_CHECK(c, c->gp_ready, UT_EINVAL, "gp_score: call ut_gp_fit first");
   UT_CHECK(c, acq != nullptr, UT_EINVAL, "gp_score: acq is NULL");
   if (m <= 0) return 0;
-  if (c->fit_pending) UT_HIP(c, hipStreamWaitEvent(c->stream, c->ev_fit, 0));  // GP state is written by the fit
+  const bool fp32 = c->gp_fit_prec == 32;
+  // fp64: K* needs only the scaled training inputs (ev_fit_x) and the mean
+  // comes from the variance epilogue, mu = (L^-1 k*) . (L^-1 y), so K*
+  // overlaps the rest of an asynchronous fit and only the variance GEMM waits
+  // for L^-1.  fp32 keeps the mean in K*'s fp64 epilogue (k* . alpha, before
+  // k* is rounded to fp32) and waits for the whole fit.
+  if (c->fit_pending) UT_HIP(c, hipStreamWaitEvent(c->stream, fp32 ? c->ev_fit : c->ev_fit_x, 0));
   const int32_t n = c->gp_n, d = c->gp_d;
   const int32_t npad = ((n + NPAD - 1) / NPAD) * NPAD;
   const int32_t dpad = ((d + 15) / 16) * 16;
   // K* rows padded to whole variance column tiles: the variance kernel reads
   // full 256-candidate strips (the K* kernel writes zeros past m)
   const int64_t ldk = ((m + VAR_BN - 1) / VAR_BN) * VAR_BN;
-  const bool fp32 = c->gp_fit_prec == 32;
   const int32_t RT = npad / NPAD;
   int rc;
   if ((rc = ensure(c, c->kst, (size_t)npad * ldk))) return rc;
@@ -593,11 +602,15 @@ int gp_score_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, const ut
   if ((rc = ensure(c, c->ucand, (size_t)dpad * ldk))) return rc;
   if ((rc = launch_prep_cand(c, feat, ld, m, d, dpad, c->ucand.p, ldk, c->cnorm.p))) return rc;
   mark(c, "cnorm");
-  if ((rc = launch_gemm_kstar(c, fp32, c->gp_XsT, npad, c->ucand.p, dpad, m, c->kst.p, ldk, c->mu_part.p)))
+  if ((rc = launch_gemm_kstar(c, fp32, c->gp_XsT, npad, c->ucand.p, dpad, m, c->kst.p, ldk,
+                              fp32 ? c->mu_part.p : nullptr)))
     return rc;
   mark(c, "kstar");
+  if (c->fit_pending && !fp32) UT_HIP(c, hipStreamWaitEvent(c->stream, c->ev_fit, 0));
+  mark(c, "");  // the wait for the fit is not variance time
   if ((rc = launch_gemm_var(c, fp32, fp32 ? (const void*)c->gp_LinvT_f : (const void*)c->gp_LinvT, npad, c->kst.p,
-                            ldk, npad, m, c->var_part.p)))
+                            ldk, npad, m, c->var_part.p, fp32 ? nullptr : c->gp_beta,
+                            fp32 ? nullptr : c->mu_part.p)))
     return rc;
   mark(c, "var");
   if (dup_ready) UT_HIP(c, hipStreamWaitEvent(c->stream, dup_ready, 0));

@@ -77,7 +77,9 @@ __device__ __forceinline__ void kstar_issue(const double* __restrict__ AT, int64
   }
 }
 
-template <typename TS>
+// MU: also the column partial of the mean, sum_r alpha_r k*_r (fp32 scoring;
+// fp64 takes the mean from the variance epilogue instead)
+template <typename TS, bool MU>
 __global__ __launch_bounds__(K_NT, 2) void k_gp_kstar(const double* __restrict__ AT, int64_t lda,
                                                       const double* __restrict__ B, int64_t ldb, int32_t dpad,
                                                       int32_t RT, int32_t CT, const double* __restrict__ xnorm,
@@ -152,7 +154,7 @@ __global__ __launch_bounds__(K_NT, 2) void k_gp_kstar(const double* __restrict__
         const int32_t row = row0 + wm * 64 + i * 16 + (lane >> 4) + 4 * r;
         const double xr = xnorm[row];
         hx[i][r] = row < n ? -0.5 * xr : -1e300;
-        al[i][r] = alpha[row];
+        if constexpr (MU) al[i][r] = alpha[row];
       }
     double hc[4];
 #pragma unroll
@@ -175,17 +177,21 @@ __global__ __launch_bounds__(K_NT, 2) void k_gp_kstar(const double* __restrict__
           const double x = __builtin_fmax(__builtin_fmin((acc[i][jj][r] + hx[i][r]) + hc[jj], 0.0), -1000.0);
           const double ks = sf2_exp_nonpos(x, etab);
           kst[(int64_t)row * ldk + col] = (TS)ks;
-          s += al[i][r] * ks;
+          if constexpr (MU) s += al[i][r] * ks;
         }
       }
-      s += __shfl_xor(s, 16);
-      s += __shfl_xor(s, 32);
-      if ((lane >> 4) == 0) red[wm * K_BN + cl] = s;
+      if constexpr (MU) {
+        s += __shfl_xor(s, 16);
+        s += __shfl_xor(s, 32);
+        if ((lane >> 4) == 0) red[wm * K_BN + cl] = s;
+      }
     }
-    __syncthreads();
-    if (t < K_BN) {
-      const int64_t col = col0 + t;
-      if (col < m) part[(int64_t)rt * ldk + col] = red[t] + red[K_BN + t];
+    if constexpr (MU) {
+      __syncthreads();
+      if (t < K_BN) {
+        const int64_t col = col0 + t;
+        if (col < m) part[(int64_t)rt * ldk + col] = red[t] + red[K_BN + t];
+      }
     }
   }
 }
@@ -194,6 +200,7 @@ int launch_gemm_kstar(ut_ctx* c, bool fp32, const double* XsT, int32_t npad, con
                       int64_t m, void* kst, int64_t ldk, double* part) {
   UT_CHECK(c, npad % K_BM == 0 && dpad % K_BK == 0 && ldk % K_BN == 0 && ldk >= m, UT_EINVAL,
            "gemm_kstar: bad padding");
+  UT_CHECK(c, (part != nullptr) == fp32, UT_EINVAL, "gemm_kstar: the mean partial is taken here in fp32 mode only");
   const int32_t RT = npad / K_BM;
   const int32_t CT = (int32_t)(ldk / K_BN);  // every column of K* (zeros past m) is written
   const int64_t items = (int64_t)RT * CT;
@@ -201,11 +208,11 @@ int launch_gemm_kstar(ut_ctx* c, bool fp32, const double* XsT, int32_t npad, con
   if (items < nb) nb = (int32_t)(((items + 7) / 8) * 8);
   UT_HIP(c, hipMemsetAsync(c->gp_ctr + 8, 0, sizeof(int32_t) * 8, c->stream));
   if (fp32)
-    hipLaunchKernelGGL(k_gp_kstar<float>, dim3(nb), dim3(K_NT), 0, c->stream, XsT, (int64_t)npad, ucand, ldk, dpad,
+    hipLaunchKernelGGL((k_gp_kstar<float, true>), dim3(nb), dim3(K_NT), 0, c->stream, XsT, (int64_t)npad, ucand, ldk, dpad,
                        RT, CT, c->gp_xnorm, c->cnorm.p, c->gp_alpha, c->gp_sf2, c->gp_n, m, c->gp_ctr + 8,
                        (float*)kst, ldk, part);
   else
-    hipLaunchKernelGGL(k_gp_kstar<double>, dim3(nb), dim3(K_NT), 0, c->stream, XsT, (int64_t)npad, ucand, ldk, dpad,
+    hipLaunchKernelGGL((k_gp_kstar<double, false>), dim3(nb), dim3(K_NT), 0, c->stream, XsT, (int64_t)npad, ucand, ldk, dpad,
                        RT, CT, c->gp_xnorm, c->cnorm.p, c->gp_alpha, c->gp_sf2, c->gp_n, m, c->gp_ctr + 8,
                        (double*)kst, ldk, part);
   UT_LAUNCH_CHECK(c);
@@ -345,7 +352,8 @@ template <typename T>
 __global__ __launch_bounds__(V_NT, 1) void k_gp_var(const T* __restrict__ AT, int64_t lda, const T* __restrict__ B,
                                                      int64_t ldb, int32_t K, int32_t RT, int32_t CT, int64_t m,
                                                      int32_t* __restrict__ ticket, double* __restrict__ part,
-                                                     int64_t ldp) {
+                                                     int64_t ldp, const double* __restrict__ beta,
+                                                     double* __restrict__ mpart) {
   using C = VCfg<T>;
   constexpr int BK = C::BK;
   // ALL LDS in one object: a second __shared__ beside the glds ring makes
@@ -422,21 +430,36 @@ __global__ __launch_bounds__(V_NT, 1) void k_gp_var(const T* __restrict__ AT, in
       }
     }
 
-    // epilogue: column sums of squares over this tile's 128 rows
+    // epilogue: column sums of squares over this tile's 128 rows and (fp64)
+    // the mean partial sum_r V[r][c] beta_r, beta = L^-1 y
     __syncthreads();
-    double* red = reinterpret_cast<double*>(lds);  // [2][256]
+    double* red = reinterpret_cast<double*>(lds);  // [2][256] squares, then [2][256] mean
     if constexpr (sizeof(T) == 8) {
+      double bt[4][4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) bt[i][r] = beta[row0 + wm * 64 + i * 16 + (lane >> 4) + 4 * r];
 #pragma unroll
       for (int jj = 0; jj < 4; ++jj) {
         const int cl = wn * 64 + jj * 16 + (lane & 15);
-        double s = 0.0;
+        double s = 0.0, u = 0.0;
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) s += accd[i][jj][r] * accd[i][jj][r];
+          for (int r = 0; r < 4; ++r) {
+            const double v = accd[i][jj][r];
+            s += v * v;
+            u += v * bt[i][r];
+          }
         s += __shfl_xor(s, 16);
         s += __shfl_xor(s, 32);
-        if ((lane >> 4) == 0) red[wm * VAR_BN + cl] = s;
+        u += __shfl_xor(u, 16);
+        u += __shfl_xor(u, 32);
+        if ((lane >> 4) == 0) {
+          red[wm * VAR_BN + cl] = s;
+          red[2 * VAR_BN + wm * VAR_BN + cl] = u;
+        }
       }
     } else {
 #pragma unroll
@@ -454,13 +477,18 @@ __global__ __launch_bounds__(V_NT, 1) void k_gp_var(const T* __restrict__ AT, in
     __syncthreads();
     if (t < VAR_BN) {
       const int64_t col = col0 + t;
-      if (col < m) part[(int64_t)rt * ldp + col] = red[t] + red[VAR_BN + t];
+      if (col < m) {
+        part[(int64_t)rt * ldp + col] = red[t] + red[VAR_BN + t];
+        if (sizeof(T) == 8) mpart[(int64_t)rt * ldp + col] = red[2 * VAR_BN + t] + red[3 * VAR_BN + t];
+      }
     }
   }
 }
 
 int launch_gemm_var(ut_ctx* c, bool fp32, const void* LinvT, int64_t lda, const void* kst, int64_t ldk, int32_t npad,
-                    int64_t m, double* part) {
+                    int64_t m, double* part, const double* beta, double* mpart) {
+  UT_CHECK(c, (beta != nullptr) == !fp32 && (mpart != nullptr) == !fp32, UT_EINVAL,
+           "gemm_var: the mean partial is taken here in fp64 mode (only)");
   UT_CHECK(c, npad % VAR_BM == 0 && ldk % VAR_BN == 0 && ldk >= m, UT_EINVAL, "gemm_var: bad padding");
   const int32_t RT = npad / VAR_BM;
   const int32_t CT = (int32_t)((m + VAR_BN - 1) / VAR_BN);
@@ -472,10 +500,10 @@ int launch_gemm_var(ut_ctx* c, bool fp32, const void* LinvT, int64_t lda, const 
   UT_HIP(c, hipMemsetAsync(c->gp_ctr, 0, sizeof(int32_t) * 8, c->stream));
   if (fp32)
     hipLaunchKernelGGL(k_gp_var<float>, dim3(nb), dim3(V_NT), 0, c->stream, (const float*)LinvT, lda,
-                       (const float*)kst, ldk, npad, RT, CT, m, c->gp_ctr, part, ldk);
+                       (const float*)kst, ldk, npad, RT, CT, m, c->gp_ctr, part, ldk, nullptr, nullptr);
   else
     hipLaunchKernelGGL(k_gp_var<double>, dim3(nb), dim3(V_NT), 0, c->stream, (const double*)LinvT, lda,
-                       (const double*)kst, ldk, npad, RT, CT, m, c->gp_ctr, part, ldk);
+                       (const double*)kst, ldk, npad, RT, CT, m, c->gp_ctr, part, ldk, beta, mpart);
   UT_LAUNCH_CHECK(c);
   return 0;
 }

@@ -34,7 +34,6 @@
 namespace ut {
 
 constexpr int HASH_NT = 128;
-constexpr int HASH_WG_PER_CU = 3;                  // grid cap, see launch_hash
 constexpr int SCR_WORDS = 7;                       // inner message bytes 0..27
 
 typedef uint32_t hex32 __attribute__((ext_vector_type(32)));
@@ -153,8 +152,8 @@ __global__ __launch_bounds__(HASH_NT) void k_hash(const DevParam* __restrict__ p
                                                   uint32_t* __restrict__ out) {
   __shared__ uint32_t lds[SCR_WORDS * HASH_NT];
   const int lane = threadIdx.x;
-  // grid-stride over candidate blocks: the grid is sized to leave CU slots
-  // free for the GP fit's small kernels that run beside the hash
+  // grid-stride over candidate blocks (launch_hash gives one block per 128
+  // candidates; a smaller grid stays correct)
   for (int64_t blk = blockIdx.x; blk * HASH_NT < m; blk += gridDim.x) {
     const int64_t i0 = blk * HASH_NT + lane;
     const bool valid = i0 < m;
@@ -241,16 +240,7 @@ int launch_hash(ut_ctx* c, const double* values, int64_t ld, int64_t m, uint32_t
     UT_LAUNCH_CHECK(c);
     pd = c->perm_dig.p;
   }
-  // In a round the hash runs on the side stream beside a GP fit that may still
-  // be in flight on the fit stream.  A full grid then keeps every CU's wave
-  // slots busy and the fit's small Cholesky/trinv kernels queue behind it
-  // (~3 ms per C2 round); capped at 3 resident workgroups per CU the hash is
-  // slower on its own but the round is shorter (C2 sweep, 2/3/4/6 per CU vs
-  // uncapped: 33.7/32.7/33.9/35.1 vs 33.9 ms).  With no fit in flight the
-  // hash takes the whole chip.
-  int64_t nb = (int64_t)grid1(m, HASH_NT);
-  const bool fit_in_flight = c->fit_pending && hipEventQuery(c->ev_fit) == hipErrorNotReady;
-  if (fit_in_flight && nb > (int64_t)c->n_cu * HASH_WG_PER_CU) nb = (int64_t)c->n_cu * HASH_WG_PER_CU;
+  const int64_t nb = (int64_t)grid1(m, HASH_NT);
   hipLaunchKernelGGL(k_hash, dim3((unsigned)nb), dim3(HASH_NT), 0, c->stream, s.d_params, s.d_order,
                      s.d_order_col, reinterpret_cast<const uint2*>(s.d_words), s.d_block_last,
                      (int32_t)s.outer_blocks, s.P, reinterpret_cast<const uint4*>(s.d_lut), values, ld, m,

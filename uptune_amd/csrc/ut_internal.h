@@ -116,6 +116,7 @@ struct ut_ctx {
   hipStream_t side = nullptr;
   hipStream_t fit_stream = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_fit = nullptr, ev_prefit = nullptr;
+  hipEvent_t ev_fit_x = nullptr;     // fit stream: scaled training inputs ready (K* may start)
   bool fit_pending = false;          // scoring waits on ev_fit before touching GP state
   double* fit_host = nullptr;        // pinned staging of X, y, 1/ell for the asynchronous fit
   size_t fit_host_n = 0;
@@ -153,7 +154,8 @@ struct ut_ctx {
   double* gp_T = nullptr;      // [n][n] scratch of the recursive inverse
   double* gp_y = nullptr;      // [n] standardised
   double* gp_tmp = nullptr;    // [n]
-  double* gp_alpha = nullptr;  // [n]
+  double* gp_alpha = nullptr;  // [n]  K^-1 y
+  double* gp_beta = nullptr;   // [n]  L^-1 y (mean from the variance epilogue: mu = (L^-1 k*) . beta)
   double* gp_inv_ell = nullptr;// [d]
   double* gp_stats = nullptr;  // [4]: f_best, mean, std, flag
   int32_t* gp_flag = nullptr;
@@ -283,7 +285,7 @@ int launch_prep_cand(ut_ctx* c, const double* feat, int64_t ld, int64_t m, int32
                      int64_t ldu, double* cn);
 int launch_xs_t(ut_ctx* c, const double* Xs, int32_t npad, int32_t d, int32_t dpad, double* XsT);
 int launch_gemm_var(ut_ctx* c, bool fp32, const void* LinvT, int64_t lda, const void* kst, int64_t ldk, int32_t npad,
-                    int64_t m, double* part);
+                    int64_t m, double* part, const double* beta, double* mpart);
 int launch_transpose(ut_ctx* c, const double* src, int32_t n, double* dst, float* dst_f);
 constexpr int VAR_BM = 128, VAR_BN = 256;  // variance-contraction tile (rows of L^-1 x candidates)
 int launch_to_f32(ut_ctx* c, const double* src, float* dst, int64_t n);
