@@ -30,6 +30,7 @@ __global__ void k_to_f32(const double* __restrict__ src, float* __restrict__ dst
 //   columns >= m zero; written by k_gp_prep_cand)
 // ---------------------------------------------------------------------------
 constexpr int K_NT = 256, K_BM = 128, K_BN = 128, K_BK = 16;
+constexpr int KSTAR_SPARE_PER_XCD = 2;  // CUs left to an in-flight GP fit (launch_gemm_kstar)
 
 // sf2 * exp(x) for x in [-1000, 0], table-driven: x = (32 k' + j) ln2/32 + r,
 // |r| <= ln2/64, so exp(x) = 2^k' * 2^(j/32) * e^r with a degree-6 polynomial
@@ -204,7 +205,14 @@ int launch_gemm_kstar(ut_ctx* c, bool fp32, const double* XsT, int32_t npad, con
   const int32_t RT = npad / K_BM;
   const int32_t CT = (int32_t)(ldk / K_BN);  // every column of K* (zeros past m) is written
   const int64_t items = (int64_t)RT * CT;
-  int32_t nb = 2 * (c->n_cu / 8) * 8;
+  // Two K* workgroups fill a CU's VGPRs, so a full persistent grid leaves no
+  // slot for the GP fit running beside it on the fit stream, and the fit's
+  // serial chain of small kernels then stalls the variance GEMM that waits for
+  // it.  While a fit is in flight, 2 CUs per XCD are left to it (C2: the round
+  // with a refit 30.2 -> 29.6 ms, the same as without a refit; K* alone 3% slower).
+  const bool fit_in_flight = c->fit_pending && hipEventQuery(c->ev_fit) == hipErrorNotReady;
+  const int32_t spare = fit_in_flight ? KSTAR_SPARE_PER_XCD : 0;
+  int32_t nb = 2 * (c->n_cu / 8 - spare) * 8;
   if (items < nb) nb = (int32_t)(((items + 7) / 8) * 8);
   UT_HIP(c, hipMemsetAsync(c->gp_ctr + 8, 0, sizeof(int32_t) * 8, c->stream));
   if (fp32)
