@@ -19,9 +19,9 @@ from collections import defaultdict
 STAGES = {  # stage key -> kernel-name prefix
     "var": "void ut::k_gp_var<double>", "kstar": "void ut::k_gp_kstar<double, false>",
     "var32": "void ut::k_gp_var<float>", "kstar32": "void ut::k_gp_kstar<float, true>", "hash": "ut::k_hash",
-    "propose": "ut::k_de", "encode": "ut::k_encode", "finalize": "ut::k_gp_finalize",
+    "propose": "ut::k_de(", "encode": "ut::k_encode", "finalize": "ut::k_gp_finalize",
     "dedup_insert": "ut::k_batch_insert", "dedup_mark": "ut::k_dedup_mark",
-    "topk0": "void ut::k_topk_chunk<0>", "pso": "ut::k_pso", "ga": "ut::k_ga",
+    "topk0": "void ut::k_topk_chunk<0>", "pso": "ut::k_pso(", "ga": "ut::k_ga(",
 }
 
 
