@@ -104,7 +104,7 @@ def main():
     ap.add_argument("--n", type=int, default=1024, help="GP training points")
     ap.add_argument("--d", type=int, default=64)
     ap.add_argument("--k", type=int, default=256)
-    ap.add_argument("--cpu-sample", type=int, default=32768,
+    ap.add_argument("--cpu-sample", type=int, default=81920,
                     help="candidates in the CPU-baseline sample (about 10 s of single-thread oracle work)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--precision", type=int, default=64, choices=(64, 32),
