@@ -179,3 +179,31 @@ def test_gpu_techniques_deepcopy_and_no_device():
     m = _space2()
     d = SearchDriver(m, meta2, parallelism=2, hash_fn=_hash_fn(m))
     assert d.root_technique.desired_result() is None
+
+
+def test_reference_registry_mirrors_reference_techniques():
+    """reference_registry(): one GPU technique per population technique the
+    reference registers (differentialevolution.py:148-151, pso.py:80-84,
+    evolutionarytechniques.py:146-158, globalGA.py:129, bandittechniques.py:311-320);
+    built without touching a device."""
+    from uptune_amd._lib import CROSSOVERS
+    reg = T.reference_registry(pool=256, batch=4)
+    names = [t.name for t in reg]
+    assert len(names) == len(set(names)) == 22
+    by = {t.name: t for t in reg}
+    assert by["GpuDifferentialEvolution"].cr == 0.9 and by["GpuDifferentialEvolutionAlt"].cr == 0.2
+    for xo in ("OX1", "OX3", "PMX", "PX", "CX"):
+        assert by["GpuPSO-" + xo].crossover in CROSSOVERS
+        g = by["GpuGA-" + xo].ga
+        assert g["crossover"] in CROSSOVERS and g["crossover_rate"] == 0.8 and g["mutation_rate"] == 0.1
+    assert by["GpuNormalGreedyMutation20"].ga["normal"] and not by["GpuUniformGreedyMutation05"].ga["normal"]
+    assert by["GpuGGA"].ga["crossover_strength"] == 0.2
+    assert all(getattr(t, "engine", None) is None for t in reg if isinstance(t, T.GpuBatchTechnique))
+    assert by["GPU_PSO_GA_DE"].bandit is not None
+    # the reference-side binding rebases every class through `wrap`
+    class _Tag:
+        pass
+
+    reg2 = T.reference_registry(wrap=lambda c: type("W" + c.__name__, (c, _Tag), {}), pool=256)
+    assert all(isinstance(t, _Tag) for t in reg2[:-1])
+    assert all(isinstance(c, _Tag) for c in reg2[-1].techniques)

@@ -508,3 +508,51 @@ def pso_ga_de_bandit(bandit_seed: Optional[int] = None, **kw) -> AUCBanditMetaTe
         GpuDifferentialEvolution(name="gpu-de", **kw),
         GpuGGA(name="gpu-gga", **kw),
     ], name="GPU_PSO_GA_DE", seed=bandit_seed)
+
+
+_XO = ("op3_cross_OX3", "op3_cross_OX1", "op3_cross_PMX", "op3_cross_PX", "op3_cross_CX")
+
+
+def reference_registry(wrap=None, bandit_cls=None, **kw) -> List[SearchTechniqueBase]:
+    """GPU counterparts of the population techniques the reference registers,
+    same parameters, names prefixed "Gpu" (crossover variants suffixed, since
+    the reference registers all five PSO / GA variants under one class name):
+
+      DifferentialEvolution (cr 0.9), DifferentialEvolutionAlt (cr 0.2),
+      DifferentialEvolution_20_100      differentialevolution.py:148-151
+      PSO(crossover=OX3|OX1|PMX|PX|CX)  pso.py:80-84
+      GA(crossover=..., mutation 0.1, crossover rate 0.8)
+                                        evolutionarytechniques.py:146-150
+      ga-base, UniformGreedyMutation05/10/20, NormalGreedyMutation05/10/20
+                                        evolutionarytechniques.py:151-158
+      GGA                               globalGA.py:129
+      PSO_GA_DE bandit                  bandittechniques.py:311-320
+
+    `wrap(cls)` maps each GPU technique class before construction (the
+    reference-side binding rebases them onto its SearchTechnique)
+    and `bandit_cls` replaces this module's AUCBanditMetaTechnique for the
+    bandit.  `kw` goes to every technique (pool, batch, device, seed, ...).  The
+    DE population size is the device population (`population=`), not 30 / 100:
+    every member is scored each round."""
+    W = wrap or (lambda c: c)
+    DE, PSO, GA, GGA = W(GpuDifferentialEvolution), W(GpuPSO), W(GpuGA), W(GpuGGA)
+    out: List[SearchTechniqueBase] = [
+        DE(name="GpuDifferentialEvolution", cr=0.9, **kw),
+        DE(name="GpuDifferentialEvolutionAlt", cr=0.2, **kw),
+        DE(name="GpuDifferentialEvolution_20_100", cr=0.2, **kw),
+    ]
+    for xo in _XO:
+        out.append(PSO(name="GpuPSO-" + xo[len("op3_cross_"):], crossover=xo, **kw))
+    for xo in _XO:
+        out.append(GA(name="GpuGA-" + xo[len("op3_cross_"):], crossover=xo, mutation_rate=0.10, crossover_rate=0.8,
+                      **kw))
+    out.append(GA(name="Gpuga-base", mutation_rate=0.10, **kw))
+    for r in (5, 10, 20):
+        out.append(GA(name="GpuUniformGreedyMutation%02d" % r, mutation_rate=r / 100.0, **kw))
+    for r in (5, 10, 20):
+        out.append(GA(name="GpuNormalGreedyMutation%02d" % r, mutation_rate=r / 100.0, normal=True, **kw))
+    out.append(GGA(name="GpuGGA", **kw))
+    children = [PSO(name="gpu-pso", **kw), GA(name="gpu-ga", crossover_rate=0.5, **kw), DE(name="gpu-de", **kw),
+                GGA(name="gpu-gga", **kw)]
+    out.append((bandit_cls or AUCBanditMetaTechnique)(children, name="GPU_PSO_GA_DE"))
+    return out
