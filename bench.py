@@ -34,6 +34,7 @@ sys.path.insert(0, ROOT)
 # spec 78.6 TF -- SURVEY.md §8(d))
 PEAK_FP64_TFLOPS = 78.6
 PEAK_FP32_TFLOPS = 157.3
+PEAK_FP16_TFLOPS = 2516.6   # dense fp16 MFMA (256 CU x 4 SIMD x 1024 flop/clk x 2.4 GHz)
 PEAK_HBM_GBS = 8000.0
 
 
@@ -107,8 +108,9 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=81920,
                     help="candidates in the CPU-baseline sample (about 10 s of single-thread oracle work)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--precision", type=int, default=64, choices=(64, 32),
-                    help="GP contractions on fp64 MFMA (1e-5 parity) or fp32 MFMA (1e-3 parity)")
+    ap.add_argument("--precision", type=int, default=64, choices=(64, 32, 16),
+                    help="GP contractions on fp64 MFMA (1e-5 parity) or fp32 MFMA (1e-3 parity); 16 = f16x3: "
+                         "the variance contraction as 3 fp16 MFMA products of hi/lo splits (fp32 tier, 1e-3)")
     ap.add_argument("--config", default="c2", choices=("c2", "c3", "c4"),
                     help="c2 = BASELINE configs[1] (R64, m=1M, n=1024: the headline); c3 = configs[2] per GPU "
                          "(HPL-64 mixed space, 16M/8 = 2M candidates per GPU, n=4096); c4 = configs[3] "
@@ -247,15 +249,18 @@ def main():
     flops_var = float(m) * n * (n + 1)       # algorithmic: lower-triangular n x n times k* per candidate
     kernel = "k_gp_var<%s> (persistent var contraction L^-1 K*^T, %s)" % (
         ("double", "v_mfma_f64_16x16x4_f64") if args.precision == 64 else ("float", "v_mfma_f32_32x32x2_f32"))
+    if args.precision == 16:
+        kernel = ("k_gp_var_h3 (persistent var contraction L^-1 K*^T, 3 x v_mfma_f32_32x32x16_f16 per product "
+                  "on hi/lo fp16 splits; peak = fp16 dense peak / 3)")
     if args.config == "c4" and stages.get("kstar", 0.0) > (var_ms or 0.0):
         var_ms = stages["kstar"]
         flops_var = 2.0 * m * n * d
         kernel = "k_gp_kstar<double, false> (K* = exp(-|x - u|^2 / 2), v_mfma_f64_16x16x4_f64)"
     achieved = flops_var / (var_ms * 1e-3) / 1e12 if var_ms else None
-    peak = PEAK_FP64_TFLOPS if args.precision == 64 else PEAK_FP32_TFLOPS
+    peak = {64: PEAK_FP64_TFLOPS, 32: PEAK_FP32_TFLOPS, 16: PEAK_FP16_TFLOPS / 3.0}[args.precision]
     # HBM bytes per launch were profiled on the default C2 round (profiles/pmc_summary.json)
     profiled = args.config == "c2" and (m, n, d) == (1 << 20, 1024, 64)
-    traffic = load_traffic("var" if args.precision == 64 else "var32") if profiled else None
+    traffic = load_traffic({64: "var", 32: "var32", 16: "var16"}[args.precision]) if profiled else None
     if args.config == "c4":
         workload = (f"C4 gcc flags (339 params: 1 + 154 Int, 184 Enum{{on,off,default}}; {d} GP features): GA "
                     f"mutation 0.1 from the best recorded config + hash_config + dedup vs 3,680 recorded configs "
@@ -280,7 +285,9 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f64" if args.precision == 64 else "f32 (K*, L^-1 K* MFMA; fit/EI f64)",
+        "dtype": {64: "f64", 32: "f32 (K*, L^-1 K* MFMA; fit/EI f64)",
+                  16: "f32-tier f16x3 (L^-1 K*^T as hi*hi + hi*lo + lo*hi fp16 MFMA, f32 accumulate; "
+                      "K*/fit/EI f64)"}[args.precision],
         "data": data,
         "config": {"workload": workload, "candidates_per_gpu": m, "gp_n": n, "dims": d, "k": k,
                    "parallelism": f"dp{world}"},

@@ -228,7 +228,10 @@ int ut_gp_score(ut_ctx* ctx, const double* features, int64_t ld, int64_t m, cons
                 const uint8_t* dup, double* mu, double* var, double* score);
 /* arithmetic of the two scoring contractions (K* and L^-1 K*^T) for fits made
  * after this call: 64 = fp64 MFMA (default; 1e-5 parity), 32 = fp32 MFMA
- * (1e-3 parity).  The fit itself is always fp64. */
+ * (1e-3 parity), 16 = "f16x3": K* in fp64, the variance contraction as three
+ * fp16 MFMA products (hi*hi + hi*lo + lo*hi) of scaled hi/lo splits of L^-1 and
+ * K*, f32 accumulate (fp32-class, the same 1e-3 parity tier).  The fit itself
+ * is always fp64. */
 int ut_gp_set_precision(ut_ctx* ctx, int32_t bits);
 /* f_best (min standardised y), y mean/std used for standardisation */
 int ut_gp_stats(ut_ctx* ctx, double* f_best, double* y_mean, double* y_std);

@@ -206,7 +206,7 @@ def test_gp_small_golden(golden_dir):
     _close(ucb.cpu().numpy(), z["ucb"])
 
 
-@pytest.mark.parametrize("prec", [64, 32])
+@pytest.mark.parametrize("prec", [64, 32, 16])
 @pytest.mark.parametrize("n,d,ell", [(1024, 64, 0.2), (200, 8, 0.5), (77, 3, 0.25), (300, 16, 1.5), (4096, 112, 1.0)])
 def test_gp_vs_oracle(n, d, ell, prec):
     """fp64: 1e-5 relative; fp32 MFMA contractions: 1e-3 relative (north star),

@@ -563,7 +563,7 @@ int ut_gp_score(ut_ctx* c, const double* feat, int64_t ld, int64_t m, const ut_a
 
 int ut_gp_set_precision(ut_ctx* c, int32_t bits) {
   if (!c) return UT_EINVAL;
-  UT_CHECK(c, bits == 64 || bits == 32, UT_EINVAL, "gp precision must be 64 or 32");
+  UT_CHECK(c, bits == 64 || bits == 32 || bits == 16, UT_EINVAL, "gp precision must be 64, 32 or 16 (f16x3)");
   c->gp_prec = bits;
   return 0;
 }

@@ -22,7 +22,8 @@
 //   GEMM2: A = L^-1 [n x n],  B = K*^T [n][m]  (lower-triangular A: K loop stops
 //          at the tile's diagonal)  -> |L^-1 k*|^2 partials
 // Both run in gp_gemm.hip (fp64 MFMA by default, fp32 MFMA when
-// ut_gp_set_precision(ctx, 32)).
+// ut_gp_set_precision(ctx, 32); with 16 the variance GEMM runs as three fp16
+// MFMA products of hi/lo split operands, fp32-class accuracy).
 #include <cstring>
 
 #include "ut_internal.h"
@@ -476,7 +477,7 @@ static int gp_alloc(ut_ctx* c, int32_t npad, int32_t d) {
   UT_HIP(c, hipMalloc((void**)&c->gp_Xs_f, sizeof(float) * npad * d));
   UT_HIP(c, hipMalloc((void**)&c->gp_LinvT, sizeof(double) * npad * npad));
   UT_HIP(c, hipMalloc((void**)&c->gp_LinvT_f, sizeof(float) * npad * npad));
-  UT_HIP(c, hipMalloc((void**)&c->gp_ctr, sizeof(int32_t) * 16));
+  UT_HIP(c, hipMalloc((void**)&c->gp_ctr, sizeof(int32_t) * 32));
   UT_HIP(c, hipMalloc((void**)&c->gp_XsT, sizeof(double) * npad * (((d + 15) / 16) * 16)));
   c->gp_cap_n = npad;
   c->gp_d = d;
@@ -555,6 +556,8 @@ int gp_fit_enqueue(ut_ctx* c, const double* X, const double* y, int32_t n, int32
   UT_LAUNCH_CHECK(c);
   if (c->gp_prec == 32 && (rc = launch_to_f32(c, c->gp_Xs, c->gp_Xs_f, (int64_t)npad * d))) return rc;
   if ((rc = launch_transpose(c, c->gp_Linv, npad, c->gp_LinvT, c->gp_prec == 32 ? c->gp_LinvT_f : nullptr))) return rc;
+  if (c->gp_prec == 16 && (rc = launch_split_h3(c, c->gp_Linv, npad, reinterpret_cast<_Float16*>(c->gp_LinvT_f))))
+    return rc;
   c->gp_fit_prec = c->gp_prec;
   UT_HIP(c, hipEventRecord(c->ev_fit, c->stream));
   c->fit_pending = true;
@@ -580,7 +583,8 @@ int gp_score_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, const ut
   UT_CHECK(c, c->gp_ready, UT_EINVAL, "gp_score: call ut_gp_fit first");
   UT_CHECK(c, acq != nullptr, UT_EINVAL, "gp_score: acq is NULL");
   if (m <= 0) return 0;
-  const bool fp32 = c->gp_fit_prec == 32;
+  const int prec = c->gp_fit_prec;
+  const bool fp32 = prec != 64;  // fp32 and h3 (f16x3) take the mean in K* and wait for the whole fit
   // fp64: K* needs only the scaled training inputs (ev_fit_x) and the mean
   // comes from the variance epilogue, mu = (L^-1 k*) . (L^-1 y), so K*
   // overlaps the rest of an asynchronous fit and only the variance GEMM waits
@@ -602,13 +606,13 @@ int gp_score_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, const ut
   if ((rc = ensure(c, c->ucand, (size_t)dpad * ldk))) return rc;
   if ((rc = launch_prep_cand(c, feat, ld, m, d, dpad, c->ucand.p, ldk, c->cnorm.p))) return rc;
   mark(c, "cnorm");
-  if ((rc = launch_gemm_kstar(c, fp32, c->gp_XsT, npad, c->ucand.p, dpad, m, c->kst.p, ldk,
+  if ((rc = launch_gemm_kstar(c, prec, c->gp_XsT, npad, c->ucand.p, dpad, m, c->kst.p, ldk,
                               fp32 ? c->mu_part.p : nullptr)))
     return rc;
   mark(c, "kstar");
   if (c->fit_pending && !fp32) UT_HIP(c, hipStreamWaitEvent(c->stream, c->ev_fit, 0));
   mark(c, "");  // the wait for the fit is not variance time
-  if ((rc = launch_gemm_var(c, fp32, fp32 ? (const void*)c->gp_LinvT_f : (const void*)c->gp_LinvT, npad, c->kst.p,
+  if ((rc = launch_gemm_var(c, prec, fp32 ? (const void*)c->gp_LinvT_f : (const void*)c->gp_LinvT, npad, c->kst.p,
                             ldk, npad, m, c->var_part.p, fp32 ? nullptr : c->gp_beta,
                             fp32 ? nullptr : c->mu_part.p)))
     return rc;

@@ -87,7 +87,12 @@ __global__ __launch_bounds__(K_NT, 2) void k_gp_kstar(const double* __restrict__
                                                       const double* __restrict__ cnorm,
                                                       const double* __restrict__ alpha, double sf2, int32_t n,
                                                       int64_t m, int32_t* __restrict__ ticket, TS* __restrict__ kst,
-                                                      int64_t ldk, double* __restrict__ part) {
+                                                      int64_t ldk, double* __restrict__ part, double kscale,
+                                                      int64_t lo_off) {
+  // TS = _Float16 (h3): k* * kscale split into fp16 hi + lo, stored candidate-major
+  // [col][row] (ld = npad = RT * K_BM) so the variance MFMA reads k-contiguous
+  // fragments; the lo plane starts lo_off elements after the hi plane
+  constexpr bool H3 = sizeof(TS) == 2;
   // one __shared__ object (see k_gp_var): the 2-stage ring, the exp table,
   // then the ticket slot
   __shared__ __attribute__((aligned(16))) double lds[2 * K_STAGE + EXP_TAB + 2];
@@ -177,7 +182,15 @@ __global__ __launch_bounds__(K_NT, 2) void k_gp_kstar(const double* __restrict__
           // -|x - u|^2 / 2 = C - |x|^2/2 - |u|^2/2, clamped to [-1000, 0]
           const double x = __builtin_fmax(__builtin_fmin((acc[i][jj][r] + hx[i][r]) + hc[jj], 0.0), -1000.0);
           const double ks = sf2_exp_nonpos(x, etab);
-          kst[(int64_t)row * ldk + col] = (TS)ks;
+          if constexpr (H3) {
+            const double xs = ks * kscale;
+            const _Float16 hi = (_Float16)(float)xs;
+            const int64_t o = col * ((int64_t)RT * K_BM) + row;
+            kst[o] = hi;
+            kst[o + lo_off] = (_Float16)(float)(xs - (double)hi);
+          } else {
+            kst[(int64_t)row * ldk + col] = (TS)ks;
+          }
           if constexpr (MU) s += al[i][r] * ks;
         }
       }
@@ -197,11 +210,15 @@ __global__ __launch_bounds__(K_NT, 2) void k_gp_kstar(const double* __restrict__
   }
 }
 
-int launch_gemm_kstar(ut_ctx* c, bool fp32, const double* XsT, int32_t npad, const double* ucand, int32_t dpad,
+int h3_kstar_exp(double sf2) { return H3_KSCALE_EXP - ilogb(sf2); }  // sf2 * 2^e < 2^15
+
+int launch_gemm_kstar(ut_ctx* c, int prec, const double* XsT, int32_t npad, const double* ucand, int32_t dpad,
                       int64_t m, void* kst, int64_t ldk, double* part) {
   UT_CHECK(c, npad % K_BM == 0 && dpad % K_BK == 0 && ldk % K_BN == 0 && ldk >= m, UT_EINVAL,
            "gemm_kstar: bad padding");
-  UT_CHECK(c, (part != nullptr) == fp32, UT_EINVAL, "gemm_kstar: the mean partial is taken here in fp32 mode only");
+  UT_CHECK(c, prec == 64 || prec == 32 || prec == 16, UT_EINVAL, "gemm_kstar: bad precision");
+  UT_CHECK(c, (part != nullptr) == (prec != 64), UT_EINVAL,
+           "gemm_kstar: the mean partial is taken here in fp32 / h3 mode only");
   const int32_t RT = npad / K_BM;
   const int32_t CT = (int32_t)(ldk / K_BN);  // every column of K* (zeros past m) is written
   const int64_t items = (int64_t)RT * CT;
@@ -215,14 +232,18 @@ int launch_gemm_kstar(ut_ctx* c, bool fp32, const double* XsT, int32_t npad, con
   int32_t nb = 2 * (c->n_cu / 8 - spare) * 8;
   if (items < nb) nb = (int32_t)(((items + 7) / 8) * 8);
   UT_HIP(c, hipMemsetAsync(c->gp_ctr + 8, 0, sizeof(int32_t) * 8, c->stream));
-  if (fp32)
+  if (prec == 16)
+    hipLaunchKernelGGL((k_gp_kstar<_Float16, true>), dim3(nb), dim3(K_NT), 0, c->stream, XsT, (int64_t)npad, ucand, ldk,
+                       dpad, RT, CT, c->gp_xnorm, c->cnorm.p, c->gp_alpha, c->gp_sf2, c->gp_n, m, c->gp_ctr + 8,
+                       (_Float16*)kst, ldk, part, ldexp(1.0, h3_kstar_exp(c->gp_sf2)), ldk * (int64_t)npad);
+  else if (prec == 32)
     hipLaunchKernelGGL((k_gp_kstar<float, true>), dim3(nb), dim3(K_NT), 0, c->stream, XsT, (int64_t)npad, ucand, ldk, dpad,
                        RT, CT, c->gp_xnorm, c->cnorm.p, c->gp_alpha, c->gp_sf2, c->gp_n, m, c->gp_ctr + 8,
-                       (float*)kst, ldk, part);
+                       (float*)kst, ldk, part, 1.0, (int64_t)0);
   else
     hipLaunchKernelGGL((k_gp_kstar<double, false>), dim3(nb), dim3(K_NT), 0, c->stream, XsT, (int64_t)npad, ucand, ldk, dpad,
                        RT, CT, c->gp_xnorm, c->cnorm.p, c->gp_alpha, c->gp_sf2, c->gp_n, m, c->gp_ctr + 8,
-                       (double*)kst, ldk, part);
+                       (double*)kst, ldk, part, 1.0, (int64_t)0);
   UT_LAUNCH_CHECK(c);
   return 0;
 }
@@ -493,8 +514,205 @@ __global__ __launch_bounds__(V_NT, 1) void k_gp_var(const T* __restrict__ AT, in
   }
 }
 
-int launch_gemm_var(ut_ctx* c, bool fp32, const void* LinvT, int64_t lda, const void* kst, int64_t ldk, int32_t npad,
+// ---------------------------------------------------------------------------
+// Variance contraction, f16x3 ("h3"): fp32-class accuracy at the fp16 MFMA rate.
+// Both operands are split once into fp16 planes, x * 2^e = hi + lo (hi = fp16(x 2^e),
+// lo = fp16(x 2^e - hi): 22 significant bits), and each product is taken as
+// hi*hi + hi*lo + lo*hi (lo*lo, ~2^-22 relative, dropped) by three
+// v_mfma_f32_32x32x16_f16 into one f32 accumulator: 3 x 16 = 48 fp16-MFMA flops
+// per algorithmic pair against 16 at the fp32 MFMA's 1/16 rate, i.e. 5.3x the
+// fp32 MFMA's arithmetic rate.  The scales keep both operands inside fp16's
+// normal range: K* (<= sf2) by 2^h3_kstar_exp(sf2), L^-1 by 2^(14 - ilogb max|L^-1|)
+// (from the device-side max), so hi < 2^15 and lo's subnormal floor sits ~2^-40
+// below the largest element.  The epilogue unscales the f32 column sums.
+//   A = L^-1 [row][k] (fp16 hi, lo planes; ld npad)      -- k-contiguous fragments
+//   B = K* [col][k]   (fp16 hi, lo planes; ld npad)      -- written so by K* (h3)
+// Tiles, tickets, the 3-deep glds ring and the triangular skip are k_gp_var's;
+// a stage is 32 k x (128 A rows + 256 B rows) x {hi, lo} = 48 KiB, 6 glds per wave.
+// LDS image: 64-B operand rows, 16-B chunk c of row r at position c ^ ((r>>2)&3):
+// conflict-free for the ds_read_b128 lane groups of the 32x32x16 fragments.
+// ---------------------------------------------------------------------------
+constexpr int H_BK = 32;
+constexpr int H_SA = VAR_BM * H_BK, H_SB = VAR_BN * H_BK;  // fp16 elements per plane
+constexpr int H_STAGE = 2 * H_SA + 2 * H_SB;
+typedef _Float16 vh8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ void h3_glds(const _Float16* __restrict__ src, int64_t ld, int32_t r16, int32_t k0,
+                                        _Float16* plane, int lane) {
+  const int r = r16 + (lane >> 2);
+  const int ch = (lane & 3) ^ ((r >> 2) & 3);  // data chunk held by this lane's LDS slot
+  __builtin_amdgcn_global_load_lds(src + (int64_t)r * ld + k0 + ch * 8,
+                                   (__attribute__((address_space(3))) void*)(plane + r16 * H_BK), 16, 0, 0);
+}
+
+__device__ __forceinline__ void h3_issue(const _Float16* __restrict__ A, int64_t a_lo, const _Float16* __restrict__ B,
+                                         int64_t b_lo, int64_t ld, int32_t k0, _Float16* st, int w, int lane) {
+  // wave w: A rows 16w.. (hi, lo), B rows 32w.. (2 x hi, 2 x lo); A / B already at row0 / col0
+  h3_glds(A, ld, 16 * w, k0, st, lane);
+  h3_glds(A + a_lo, ld, 16 * w, k0, st + H_SA, lane);
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    h3_glds(B, ld, 32 * w + 16 * u, k0, st + 2 * H_SA, lane);
+    h3_glds(B + b_lo, ld, 32 * w + 16 * u, k0, st + 2 * H_SA + H_SB, lane);
+  }
+}
+
+__device__ __forceinline__ vh8 h3_frag(const _Float16* plane, int r, int c) {
+  return *reinterpret_cast<const vh8*>(plane + r * H_BK + ((c ^ ((r >> 2) & 3)) << 3));
+}
+
+__device__ __forceinline__ void var_step_h3(const _Float16* st, int wm, int wn, int lane, int imin,
+                                            vf16 (&acc)[2][2]) {
+  const _Float16* ah = st;
+  const _Float16* al = st + H_SA;
+  const _Float16* bh = st + 2 * H_SA;
+  const _Float16* bl = bh + H_SB;
+#pragma unroll
+  for (int s = 0; s < H_BK / 16; ++s) {
+    const int c = 2 * s + (lane >> 5);
+    vh8 fbh[2], fbl[2];
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) {
+      const int r = wn * 64 + jj * 32 + (lane & 31);
+      fbh[jj] = h3_frag(bh, r, c);
+      fbl[jj] = h3_frag(bl, r, c);
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      if (i < imin) continue;
+      const int r = wm * 64 + i * 32 + (lane & 31);
+      const vh8 fah = h3_frag(ah, r, c), fal = h3_frag(al, r, c);
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) {
+        acc[i][jj] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fal, fbh[jj], acc[i][jj], 0, 0, 0);
+        acc[i][jj] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fah, fbl[jj], acc[i][jj], 0, 0, 0);
+        acc[i][jj] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fah, fbh[jj], acc[i][jj], 0, 0, 0);
+      }
+    }
+  }
+}
+
+__device__ __forceinline__ int h3_linv_exp(const unsigned long long* amax_bits) {
+  return H3_KSCALE_EXP - ilogb(__longlong_as_double((long long)*amax_bits));
+}
+
+__global__ __launch_bounds__(V_NT, 1) void k_gp_var_h3(const _Float16* __restrict__ A, int64_t a_lo,
+                                                        const _Float16* __restrict__ B, int64_t b_lo, int64_t ld,
+                                                        int32_t K, int32_t RT, int32_t CT, int64_t m,
+                                                        int32_t* __restrict__ ticket, double* __restrict__ part,
+                                                        int64_t ldp, const unsigned long long* __restrict__ amax_bits,
+                                                        int32_t kexp) {
+  __shared__ __attribute__((aligned(16))) _Float16 lds[V_ST * H_STAGE + 8];
+  int32_t& s_item = *reinterpret_cast<int32_t*>(lds + V_ST * H_STAGE);
+  const int t = threadIdx.x, lane = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wm = w >> 2, wn = w & 3;
+  const int32_t xcd = blockIdx.x & 7;
+  const double unscale2 = __builtin_ldexp(1.0, -2 * (h3_linv_exp(amax_bits) + kexp));
+
+  for (;;) {
+    if (t == 0) s_item = atomicAdd(&ticket[xcd], 1);
+    __syncthreads();
+    const int32_t j = s_item;
+    const int32_t ct = (j / RT) * 8 + xcd;
+    if (ct >= CT) break;
+    const int32_t rt = RT - 1 - (j % RT);
+    const int64_t col0 = (int64_t)ct * VAR_BN;
+    const int32_t row0 = rt * VAR_BM;
+    const int32_t nk = min(K, row0 + VAR_BM) / H_BK;
+    const _Float16* At = A + (int64_t)row0 * ld;
+    const _Float16* Bt = B + col0 * ld;
+
+    vf16 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][jj][r] = 0.0f;
+
+    h3_issue(At, a_lo, Bt, b_lo, ld, 0, lds, w, lane);
+    if (nk > 1) h3_issue(At, a_lo, Bt, b_lo, ld, H_BK, lds + H_STAGE, w, lane);
+    auto pipe = [&](int32_t kt) -> const _Float16* {
+      if (kt + 1 < nk)
+        asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      if (kt + 2 < nk) h3_issue(At, a_lo, Bt, b_lo, ld, (kt + 2) * H_BK, lds + ((kt + 2) % V_ST) * H_STAGE, w, lane);
+      return lds + (kt % V_ST) * H_STAGE;
+    };
+    const int32_t nfull = min(nk, row0 / H_BK);
+    for (int32_t kt = 0; kt < nfull; ++kt) var_step_h3(pipe(kt), wm, wn, lane, 0, acc);
+    for (int32_t kt = nfull; kt < nk; ++kt) {
+      const _Float16* st = pipe(kt);
+      const int kd = kt - nfull - 2 * wm;
+      const int imin = kd < 0 ? 0 : kd;
+      if (imin < 2) var_step_h3(st, wm, wn, lane, imin, acc);
+    }
+
+    __syncthreads();
+    double* red = reinterpret_cast<double*>(lds);  // [2][256]
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) {
+      const int cl = wn * 64 + jj * 32 + (lane & 31);
+      double s = 0.0;
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) s += (double)acc[i][jj][r] * (double)acc[i][jj][r];
+      s += __shfl_xor(s, 32);
+      if ((lane >> 5) == 0) red[wm * VAR_BN + cl] = s;
+    }
+    __syncthreads();
+    if (t < VAR_BN) {
+      const int64_t col = col0 + t;
+      if (col < m) part[(int64_t)rt * ldp + col] = (red[t] + red[VAR_BN + t]) * unscale2;
+    }
+  }
+}
+
+// max |x| over cnt doubles into *out (as bits: non-negative doubles order like their bits)
+__global__ __launch_bounds__(256) void k_absmax(const double* __restrict__ x, int64_t cnt,
+                                                unsigned long long* __restrict__ out) {
+  double v = 0.0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < cnt; i += (int64_t)gridDim.x * blockDim.x)
+    v = fmax(v, fabs(x[i]));
+  for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o));
+  __shared__ double red[4];
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    v = fmax(fmax(red[0], red[1]), fmax(red[2], red[3]));
+    atomicMax(out, (unsigned long long)__double_as_longlong(v));
+  }
+}
+
+__global__ void k_split_h3(const double* __restrict__ x, int64_t cnt, const unsigned long long* __restrict__ amax_bits,
+                           _Float16* __restrict__ dst) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= cnt) return;
+  const double xs = __builtin_ldexp(x[i], h3_linv_exp(amax_bits));
+  const _Float16 hi = (_Float16)(float)xs;
+  dst[i] = hi;
+  dst[cnt + i] = (_Float16)(float)(xs - (double)hi);
+}
+
+int launch_split_h3(ut_ctx* c, const double* Linv, int32_t n, _Float16* dst) {
+  const int64_t cnt = (int64_t)n * n;
+  unsigned long long* amax = reinterpret_cast<unsigned long long*>(c->gp_ctr + 16);
+  UT_HIP(c, hipMemsetAsync(amax, 0, sizeof(unsigned long long), c->stream));
+  hipLaunchKernelGGL(k_absmax, dim3(1024), dim3(256), 0, c->stream, Linv, cnt, amax);
+  hipLaunchKernelGGL(k_split_h3, dim3(grid1(cnt, 256)), dim3(256), 0, c->stream, Linv, cnt, amax, dst);
+  UT_LAUNCH_CHECK(c);
+  return 0;
+}
+
+int launch_gemm_var(ut_ctx* c, int prec, const void* LinvT, int64_t lda, const void* kst, int64_t ldk, int32_t npad,
                     int64_t m, double* part, const double* beta, double* mpart) {
+  const bool fp32 = prec != 64;
+  UT_CHECK(c, prec == 64 || prec == 32 || prec == 16, UT_EINVAL, "gemm_var: bad precision");
   UT_CHECK(c, (beta != nullptr) == !fp32 && (mpart != nullptr) == !fp32, UT_EINVAL,
            "gemm_var: the mean partial is taken here in fp64 mode (only)");
   UT_CHECK(c, npad % VAR_BM == 0 && ldk % VAR_BN == 0 && ldk >= m, UT_EINVAL, "gemm_var: bad padding");
@@ -506,7 +724,11 @@ int launch_gemm_var(ut_ctx* c, bool fp32, const void* LinvT, int64_t lda, const 
   int32_t nb = (c->n_cu / 8) * 8;
   if (items < nb) nb = (int32_t)(((items + 7) / 8) * 8);
   UT_HIP(c, hipMemsetAsync(c->gp_ctr, 0, sizeof(int32_t) * 8, c->stream));
-  if (fp32)
+  if (prec == 16)  // LinvT: L^-1 [row][k] hi/lo planes; kst: K* [col][row] hi/lo planes (see k_gp_var_h3)
+    hipLaunchKernelGGL(k_gp_var_h3, dim3(nb), dim3(V_NT), 0, c->stream, (const _Float16*)LinvT, lda * (int64_t)npad,
+                       (const _Float16*)kst, ldk * (int64_t)npad, (int64_t)npad, npad, RT, CT, m, c->gp_ctr, part, ldk,
+                       reinterpret_cast<const unsigned long long*>(c->gp_ctr + 16), h3_kstar_exp(c->gp_sf2));
+  else if (fp32)
     hipLaunchKernelGGL(k_gp_var<float>, dim3(nb), dim3(V_NT), 0, c->stream, (const float*)LinvT, lda,
                        (const float*)kst, ldk, npad, RT, CT, m, c->gp_ctr, part, ldk, nullptr, nullptr);
   else

@@ -165,8 +165,8 @@ struct ut_ctx {
   float* gp_Xs_f = nullptr;    // fp32 copies for the fp32 MFMA path
   double* gp_LinvT = nullptr;  // (L^-1)^T [k][row]: the A operand of the variance contraction
   double* gp_XsT = nullptr;    // (X/ell)^T [dpad][npad]: the A operand of the K* contraction
-  float* gp_LinvT_f = nullptr;
-  int32_t* gp_ctr = nullptr;   // [16] per-XCD work tickets: [0,8) variance, [8,16) K*
+  float* gp_LinvT_f = nullptr;  // fp32 (L^-1)^T; in h3 mode the fp16 hi/lo planes of L^-1 [row][k]
+  int32_t* gp_ctr = nullptr;   // [32] per-XCD work tickets: [0,8) variance, [8,16) K*; [16,18) max|L^-1| bits (h3)
   int32_t n_cu = 256;
   int64_t gp_cap_n = 0;
 
@@ -279,14 +279,21 @@ int gp_score_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, const ut
                   double* mu, double* var, double* score, hipEvent_t dup_ready = nullptr);
 int topk_impl(ut_ctx* c, const double* score, const uint8_t* dup, int64_t m, int64_t cand_base, int32_t k,
               int64_t* out_idx, double* out_score);
-int launch_gemm_kstar(ut_ctx* c, bool fp32, const double* XsT, int32_t npad, const double* ucand, int32_t dpad,
+// prec: 64 (fp64 MFMA), 32 (fp32 MFMA), 16 (f16x3: fp16 hi/lo split operands,
+// three fp16 MFMA products, f32 accumulate -- see gp_gemm.hip)
+constexpr int H3_KSCALE_EXP = 14;  // K* (<= sf2) is scaled by 2^(14 - ceil(log2 sf2)) before the split
+int h3_kstar_exp(double sf2);
+int launch_gemm_kstar(ut_ctx* c, int prec, const double* XsT, int32_t npad, const double* ucand, int32_t dpad,
                       int64_t m, void* kst, int64_t ldk, double* part);
 int launch_prep_cand(ut_ctx* c, const double* feat, int64_t ld, int64_t m, int32_t d, int32_t dpad, double* u,
                      int64_t ldu, double* cn);
 int launch_xs_t(ut_ctx* c, const double* Xs, int32_t npad, int32_t d, int32_t dpad, double* XsT);
-int launch_gemm_var(ut_ctx* c, bool fp32, const void* LinvT, int64_t lda, const void* kst, int64_t ldk, int32_t npad,
+int launch_gemm_var(ut_ctx* c, int prec, const void* LinvT, int64_t lda, const void* kst, int64_t ldk, int32_t npad,
                     int64_t m, double* part, const double* beta, double* mpart);
 int launch_transpose(ut_ctx* c, const double* src, int32_t n, double* dst, float* dst_f);
+// L^-1 [row][k] (n x n, fp64) -> scaled fp16 hi/lo planes [row][k] (h3 A operand);
+// the scale exponent is derived on the device from max|L^-1| (kept in gp_ctr[16..17])
+int launch_split_h3(ut_ctx* c, const double* Linv, int32_t n, _Float16* dst);
 constexpr int VAR_BM = 128, VAR_BN = 256;  // variance-contraction tile (rows of L^-1 x candidates)
 int launch_to_f32(ut_ctx* c, const double* src, float* dst, int64_t n);
 int launch_gather_rows(ut_ctx* c, const double* values, int64_t ld, const int64_t* idx, int64_t cand_base,
