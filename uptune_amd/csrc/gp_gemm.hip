@@ -95,9 +95,17 @@ __global__ __launch_bounds__(K_NT, 2) void k_gp_kstar(const double* __restrict__
   constexpr bool H3 = sizeof(TS) == 2;
   // one __shared__ object (see k_gp_var): the 2-stage ring, the exp table,
   // then the ticket slot
-  __shared__ __attribute__((aligned(16))) double lds[2 * K_STAGE + EXP_TAB + 2];
-  double* etab = lds + 2 * K_STAGE;
-  int32_t& s_item = *reinterpret_cast<int32_t*>(lds + 2 * K_STAGE + EXP_TAB);
+  // h3: the epilogue transposes the tile through LDS, [plane][col][row] with a
+  // 264-B column pitch (2-way at worst on the ds_write_b16s), then stores whole
+  // 256-B candidate rows; the mean reduction sits after that image
+  constexpr int T_PITCH = K_BM + 4;                                  // fp16 elements
+  constexpr int T_DBL = H3 ? 2 * K_BN * T_PITCH * 2 / 8 : 0;          // image size in doubles
+  constexpr int RED_OFF = H3 ? T_DBL : 0;
+  constexpr int MAIN = H3 ? (T_DBL + 2 * K_BN > 2 * K_STAGE ? T_DBL + 2 * K_BN : 2 * K_STAGE) : 2 * K_STAGE;
+  __shared__ __attribute__((aligned(16))) double lds[MAIN + EXP_TAB + 2];
+  double* etab = lds + MAIN;
+  int32_t& s_item = *reinterpret_cast<int32_t*>(lds + MAIN + EXP_TAB);
+  _Float16* timg = reinterpret_cast<_Float16*>(lds);
   const int t = threadIdx.x, lane = t & 63;
   if (t < EXP_TAB) etab[t] = sf2 * exp2((double)t / EXP_TAB);  // published by the first ticket barrier
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
@@ -146,8 +154,8 @@ __global__ __launch_bounds__(K_NT, 2) void k_gp_kstar(const double* __restrict__
       }
     }
 
-    __syncthreads();  // ring free: reuse as the column reduction buffer
-    double* red = lds;  // [2][128]
+    __syncthreads();  // ring free: reuse as the column reduction buffer (and the h3 image)
+    double* red = lds + RED_OFF;  // [2][128]
     // epilogue operands loaded up front and unconditionally (rows < npad,
     // columns < ldk are always in range): a load under a per-element condition
     // makes hipcc wait vmcnt(0) per element.  Padding rows / columns get a
@@ -185,9 +193,9 @@ __global__ __launch_bounds__(K_NT, 2) void k_gp_kstar(const double* __restrict__
           if constexpr (H3) {
             const double xs = ks * kscale;
             const _Float16 hi = (_Float16)(float)xs;
-            const int64_t o = col * ((int64_t)RT * K_BM) + row;
-            kst[o] = hi;
-            kst[o + lo_off] = (_Float16)(float)(xs - (double)hi);
+            const int o = cl * T_PITCH + (row - row0);
+            timg[o] = hi;
+            timg[K_BN * T_PITCH + o] = (_Float16)(float)(xs - (double)hi);
           } else {
             kst[(int64_t)row * ldk + col] = (TS)ks;
           }
@@ -200,11 +208,23 @@ __global__ __launch_bounds__(K_NT, 2) void k_gp_kstar(const double* __restrict__
         if ((lane >> 4) == 0) red[wm * K_BN + cl] = s;
       }
     }
+    if constexpr (MU || H3) __syncthreads();
     if constexpr (MU) {
-      __syncthreads();
       if (t < K_BN) {
         const int64_t col = col0 + t;
         if (col < m) part[(int64_t)rt * ldk + col] = red[t] + red[K_BN + t];
+      }
+    }
+    if constexpr (H3) {
+      // 2 planes x 128 candidate rows of 256 B: a wave instruction stores two rows
+      const int64_t npad = (int64_t)RT * K_BM;
+      const int half = lane >> 5, q = lane & 31;
+#pragma unroll 4
+      for (int it = 0; it < 2 * K_BN / 8; ++it) {
+        const int u = it * 8 + w * 2 + half;  // plane * 128 + column
+        const int pl = u / K_BN, cl = u % K_BN;
+        const uint2 v = *reinterpret_cast<const uint2*>(timg + (pl * K_BN + cl) * T_PITCH + q * 4);
+        *reinterpret_cast<uint2*>(kst + pl * lo_off + (col0 + cl) * npad + row0 + q * 4) = v;
       }
     }
   }
