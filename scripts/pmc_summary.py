@@ -22,6 +22,8 @@ STAGES = {  # stage key -> kernel-name prefix
     "propose": "ut::k_de(", "encode": "ut::k_encode", "finalize": "ut::k_gp_finalize",
     "dedup_insert": "ut::k_batch_insert", "dedup_mark": "ut::k_dedup_mark",
     "topk0": "void ut::k_topk_chunk<0>", "pso": "ut::k_pso(", "ga": "ut::k_ga(",
+    # rocprofv3 leaves the _Float16 instantiations mangled
+    "var16": "_ZN2ut11k_gp_var_h3", "kstar16": "_ZN2ut10k_gp_kstarIDF16_",
 }
 
 
@@ -61,8 +63,17 @@ def main(prof, tag):
             "hbm_bytes_per_launch": 2.0 * fr * 1024.0 + wr * 1024.0,
             "avg_ns": float(stats[ks[0]]["AverageNs"]) if ks else None,
         }
+    # merge: a profile of another precision / config adds its stages beside the default C2 ones
+    merged = {}
+    try:
+        with open(os.path.join(out_dir, "pmc_summary.json")) as f:
+            merged = json.load(f)
+    except Exception:
+        pass
+    merged.update({k: v for k, v in summary.items() if k != "_note"})
+    merged["_note"] = summary["_note"] if "var" in summary else merged.get("_note", summary["_note"])
     with open(os.path.join(out_dir, "pmc_summary.json"), "w") as f:
-        json.dump(summary, f, indent=1)
+        json.dump(merged, f, indent=1)
     with open(os.path.join(out_dir, f"{tag}_pmc_summary.json"), "w") as f:
         json.dump(summary, f, indent=1)
     print(json.dumps(summary, indent=1))

@@ -552,56 +552,91 @@ __global__ __launch_bounds__(V_NT, 1) void k_gp_var(const T* __restrict__ AT, in
 // LDS image: 64-B operand rows, 16-B chunk c of row r at position c ^ ((r>>2)&3):
 // conflict-free for the ds_read_b128 lane groups of the 32x32x16 fragments.
 // ---------------------------------------------------------------------------
-constexpr int H_BK = 32;
-constexpr int H_SA = VAR_BM * H_BK, H_SB = VAR_BN * H_BK;  // fp16 elements per plane
-constexpr int H_STAGE = 2 * H_SA + 2 * H_SB;
+// H3Cfg<BK, NS>: BK k per stage (64-B or 32-B operand rows), NS ring slots;
+// NS - 2 stages stay in flight behind the one being consumed.
+template <int BK, int NS>
+struct H3Cfg {
+  static constexpr int SA = VAR_BM * BK, SB = VAR_BN * BK;  // fp16 elements per plane
+  static constexpr int STAGE = 2 * SA + 2 * SB;
+  static constexpr int CH = BK / 8;                          // 16-B chunks per operand row
+  static constexpr int RPI = 64 / CH;                        // operand rows per glds wave-instruction
+  static constexpr int PER_WAVE = 2 * (VAR_BM + VAR_BN) / RPI / 8;  // glds per wave per stage
+  // conflict-free position of chunk c in row r for the ds_read_b128 groups
+  static __device__ __forceinline__ int swz(int r, int c) {
+    return BK == 32 ? c ^ ((r >> 2) & 3) : c ^ ((r >> 3) & 1);
+  }
+};
 typedef _Float16 vh8 __attribute__((ext_vector_type(8)));
 
-__device__ __forceinline__ void h3_glds(const _Float16* __restrict__ src, int64_t ld, int32_t r16, int32_t k0,
-                                        _Float16* plane, int lane) {
-  const int r = r16 + (lane >> 2);
-  const int ch = (lane & 3) ^ ((r >> 2) & 3);  // data chunk held by this lane's LDS slot
-  __builtin_amdgcn_global_load_lds(src + (int64_t)r * ld + k0 + ch * 8,
-                                   (__attribute__((address_space(3))) void*)(plane + r16 * H_BK), 16, 0, 0);
+// s_waitcnt vmcnt(N) (N < 64), lgkmcnt / expcnt left alone
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
 }
 
+template <int BK, int NS>
+__device__ __forceinline__ void h3_glds(const _Float16* __restrict__ src, int64_t ld, int32_t rb, int32_t k0,
+                                        _Float16* plane, int lane) {
+  using C = H3Cfg<BK, NS>;
+  const int r = rb + lane / C::CH;
+  const int ch = C::swz(r, lane % C::CH);  // data chunk held by this lane's LDS slot (swz is an involution)
+  __builtin_amdgcn_global_load_lds(src + (int64_t)r * ld + k0 + ch * 8,
+                                   (__attribute__((address_space(3))) void*)(plane + rb * BK), 16, 0, 0);
+}
+
+template <int BK, int NS>
 __device__ __forceinline__ void h3_issue(const _Float16* __restrict__ A, int64_t a_lo, const _Float16* __restrict__ B,
                                          int64_t b_lo, int64_t ld, int32_t k0, _Float16* st, int w, int lane) {
-  // wave w: A rows 16w.. (hi, lo), B rows 32w.. (2 x hi, 2 x lo); A / B already at row0 / col0
-  h3_glds(A, ld, 16 * w, k0, st, lane);
-  h3_glds(A + a_lo, ld, 16 * w, k0, st + H_SA, lane);
+  // A / B already at row0 / col0.  Per wave: A rows [w*128/8, +128/8) of each plane,
+  // B rows [w*256/8, +256/8) of each plane, RPI rows per instruction.
+  using C = H3Cfg<BK, NS>;
+  constexpr int AR = VAR_BM / 8, BR = VAR_BN / 8;  // rows per wave
+  if constexpr (AR >= C::RPI) {
 #pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    h3_glds(B, ld, 32 * w + 16 * u, k0, st + 2 * H_SA, lane);
-    h3_glds(B + b_lo, ld, 32 * w + 16 * u, k0, st + 2 * H_SA + H_SB, lane);
+    for (int u = 0; u < AR / C::RPI; ++u) {
+      h3_glds<BK, NS>(A, ld, w * AR + u * C::RPI, k0, st, lane);
+      h3_glds<BK, NS>(A + a_lo, ld, w * AR + u * C::RPI, k0, st + C::SA, lane);
+    }
+  } else {  // one instruction covers the A rows of two waves: even waves hi, odd waves lo
+    const int rb = (w >> 1) * C::RPI;
+    h3_glds<BK, NS>(A + (w & 1) * a_lo, ld, rb, k0, st + (w & 1) * C::SA, lane);
+  }
+#pragma unroll
+  for (int u = 0; u < BR / C::RPI; ++u) {
+    h3_glds<BK, NS>(B, ld, w * BR + u * C::RPI, k0, st + 2 * C::SA, lane);
+    h3_glds<BK, NS>(B + b_lo, ld, w * BR + u * C::RPI, k0, st + 2 * C::SA + C::SB, lane);
   }
 }
 
+template <int BK, int NS>
 __device__ __forceinline__ vh8 h3_frag(const _Float16* plane, int r, int c) {
-  return *reinterpret_cast<const vh8*>(plane + r * H_BK + ((c ^ ((r >> 2) & 3)) << 3));
+  return *reinterpret_cast<const vh8*>(plane + r * BK + (H3Cfg<BK, NS>::swz(r, c) << 3));
 }
 
+template <int BK, int NS>
 __device__ __forceinline__ void var_step_h3(const _Float16* st, int wm, int wn, int lane, int imin,
                                             vf16 (&acc)[2][2]) {
+  using C = H3Cfg<BK, NS>;
   const _Float16* ah = st;
-  const _Float16* al = st + H_SA;
-  const _Float16* bh = st + 2 * H_SA;
-  const _Float16* bl = bh + H_SB;
+  const _Float16* al = st + C::SA;
+  const _Float16* bh = st + 2 * C::SA;
+  const _Float16* bl = bh + C::SB;
 #pragma unroll
-  for (int s = 0; s < H_BK / 16; ++s) {
+  for (int s = 0; s < BK / 16; ++s) {
     const int c = 2 * s + (lane >> 5);
     vh8 fbh[2], fbl[2];
 #pragma unroll
     for (int jj = 0; jj < 2; ++jj) {
       const int r = wn * 64 + jj * 32 + (lane & 31);
-      fbh[jj] = h3_frag(bh, r, c);
-      fbl[jj] = h3_frag(bl, r, c);
+      fbh[jj] = h3_frag<BK, NS>(bh, r, c);
+      fbl[jj] = h3_frag<BK, NS>(bl, r, c);
     }
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       if (i < imin) continue;
       const int r = wm * 64 + i * 32 + (lane & 31);
-      const vh8 fah = h3_frag(ah, r, c), fal = h3_frag(al, r, c);
+      const vh8 fah = h3_frag<BK, NS>(ah, r, c), fal = h3_frag<BK, NS>(al, r, c);
 #pragma unroll
       for (int jj = 0; jj < 2; ++jj) {
         acc[i][jj] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fal, fbh[jj], acc[i][jj], 0, 0, 0);
@@ -616,14 +651,17 @@ __device__ __forceinline__ int h3_linv_exp(const unsigned long long* amax_bits) 
   return H3_KSCALE_EXP - ilogb(__longlong_as_double((long long)*amax_bits));
 }
 
+template <int BK, int NS>
 __global__ __launch_bounds__(V_NT, 1) void k_gp_var_h3(const _Float16* __restrict__ A, int64_t a_lo,
                                                         const _Float16* __restrict__ B, int64_t b_lo, int64_t ld,
                                                         int32_t K, int32_t RT, int32_t CT, int64_t m,
                                                         int32_t* __restrict__ ticket, double* __restrict__ part,
                                                         int64_t ldp, const unsigned long long* __restrict__ amax_bits,
                                                         int32_t kexp) {
-  __shared__ __attribute__((aligned(16))) _Float16 lds[V_ST * H_STAGE + 8];
-  int32_t& s_item = *reinterpret_cast<int32_t*>(lds + V_ST * H_STAGE);
+  using C = H3Cfg<BK, NS>;
+  static_assert(NS * C::STAGE * 2 <= 160 * 1024 - 64, "LDS");
+  __shared__ __attribute__((aligned(16))) _Float16 lds[NS * C::STAGE + 8];
+  int32_t& s_item = *reinterpret_cast<int32_t*>(lds + NS * C::STAGE);
   const int t = threadIdx.x, lane = t & 63;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
   const int wm = w >> 2, wn = w & 3;
@@ -639,7 +677,7 @@ __global__ __launch_bounds__(V_NT, 1) void k_gp_var_h3(const _Float16* __restric
     const int32_t rt = RT - 1 - (j % RT);
     const int64_t col0 = (int64_t)ct * VAR_BN;
     const int32_t row0 = rt * VAR_BM;
-    const int32_t nk = min(K, row0 + VAR_BM) / H_BK;
+    const int32_t nk = min(K, row0 + VAR_BM) / BK;
     const _Float16* At = A + (int64_t)row0 * ld;
     const _Float16* Bt = B + col0 * ld;
 
@@ -651,25 +689,30 @@ __global__ __launch_bounds__(V_NT, 1) void k_gp_var_h3(const _Float16* __restric
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[i][jj][r] = 0.0f;
 
-    h3_issue(At, a_lo, Bt, b_lo, ld, 0, lds, w, lane);
-    if (nk > 1) h3_issue(At, a_lo, Bt, b_lo, ld, H_BK, lds + H_STAGE, w, lane);
+    // prologue: stages 0 .. NS-2 in flight (nk >= 4 always: K and row0 + 128 are multiples of 128)
+#pragma unroll
+    for (int q = 0; q < NS - 1; ++q)
+      if (q < nk) h3_issue<BK, NS>(At, a_lo, Bt, b_lo, ld, q * BK, lds + q * C::STAGE, w, lane);
+    // retire stage kt (NS - 2 younger stages may stay in flight), then refill
+    // the slot of stage kt - 1 with stage kt + NS - 1
     auto pipe = [&](int32_t kt) -> const _Float16* {
-      if (kt + 1 < nk)
-        asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      if (kt + NS - 2 < nk)
+        wait_vmcnt<C::PER_WAVE * (NS - 2)>();
       else
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        wait_vmcnt<0>();
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
-      if (kt + 2 < nk) h3_issue(At, a_lo, Bt, b_lo, ld, (kt + 2) * H_BK, lds + ((kt + 2) % V_ST) * H_STAGE, w, lane);
-      return lds + (kt % V_ST) * H_STAGE;
+      if (kt + NS - 1 < nk)
+        h3_issue<BK, NS>(At, a_lo, Bt, b_lo, ld, (kt + NS - 1) * BK, lds + ((kt + NS - 1) % NS) * C::STAGE, w, lane);
+      return lds + (kt % NS) * C::STAGE;
     };
-    const int32_t nfull = min(nk, row0 / H_BK);
-    for (int32_t kt = 0; kt < nfull; ++kt) var_step_h3(pipe(kt), wm, wn, lane, 0, acc);
+    const int32_t nfull = min(nk, row0 / BK);
+    for (int32_t kt = 0; kt < nfull; ++kt) var_step_h3<BK, NS>(pipe(kt), wm, wn, lane, 0, acc);
     for (int32_t kt = nfull; kt < nk; ++kt) {
       const _Float16* st = pipe(kt);
-      const int kd = kt - nfull - 2 * wm;
+      const int kd = ((kt - nfull) * BK) / 32 - 2 * wm;  // 32-row blocks of this wave entirely above the diagonal
       const int imin = kd < 0 ? 0 : kd;
-      if (imin < 2) var_step_h3(st, wm, wn, lane, imin, acc);
+      if (imin < 2) var_step_h3<BK, NS>(st, wm, wn, lane, imin, acc);
     }
 
     __syncthreads();
@@ -744,10 +787,14 @@ int launch_gemm_var(ut_ctx* c, int prec, const void* LinvT, int64_t lda, const v
   int32_t nb = (c->n_cu / 8) * 8;
   if (items < nb) nb = (int32_t)(((items + 7) / 8) * 8);
   UT_HIP(c, hipMemsetAsync(c->gp_ctr, 0, sizeof(int32_t) * 8, c->stream));
-  if (prec == 16)  // LinvT: L^-1 [row][k] hi/lo planes; kst: K* [col][row] hi/lo planes (see k_gp_var_h3)
-    hipLaunchKernelGGL(k_gp_var_h3, dim3(nb), dim3(V_NT), 0, c->stream, (const _Float16*)LinvT, lda * (int64_t)npad,
+  if (prec == 16) {  // LinvT: L^-1 [row][k] hi/lo planes; kst: K* [col][row] hi/lo planes (see k_gp_var_h3)
+    // ring: 32 k x 3 slots (48-KiB stages).  16 k x 6 slots (4 stages in flight)
+    // measured slower: C3 var 95.8 -> 118.5 ms (twice the barriers per flop)
+    auto kern = k_gp_var_h3<32, 3>;
+    hipLaunchKernelGGL(kern, dim3(nb), dim3(V_NT), 0, c->stream, (const _Float16*)LinvT, lda * (int64_t)npad,
                        (const _Float16*)kst, ldk * (int64_t)npad, (int64_t)npad, npad, RT, CT, m, c->gp_ctr, part, ldk,
                        reinterpret_cast<const unsigned long long*>(c->gp_ctr + 16), h3_kstar_exp(c->gp_sf2));
+  }
   else if (fp32)
     hipLaunchKernelGGL(k_gp_var<float>, dim3(nb), dim3(V_NT), 0, c->stream, (const float*)LinvT, lda,
                        (const float*)kst, ldk, npad, RT, CT, m, c->gp_ctr, part, ldk, nullptr, nullptr);
