@@ -10,7 +10,7 @@ import sys
 from collections import defaultdict
 
 KERNELS = {"var": "void ut::k_gp_var<double>", "kstar": "void ut::k_gp_kstar<double, false>", "hash": "ut::k_hash",
-           "propose": "ut::k_de("}
+           "propose": "ut::k_de(", "var16": "_ZN2ut11k_gp_var_h3", "kstar16": "_ZN2ut10k_gp_kstarIDF16_"}
 
 
 def main(d, n_cu=256, peak_ghz=2.4):

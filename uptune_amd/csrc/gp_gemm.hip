@@ -585,13 +585,13 @@ __device__ __forceinline__ void h3_glds(const _Float16* __restrict__ src, int64_
                                    (__attribute__((address_space(3))) void*)(plane + rb * BK), 16, 0, 0);
 }
 
-template <int BK, int NS>
+template <int BK, int NS, int NW>
 __device__ __forceinline__ void h3_issue(const _Float16* __restrict__ A, int64_t a_lo, const _Float16* __restrict__ B,
                                          int64_t b_lo, int64_t ld, int32_t k0, _Float16* st, int w, int lane) {
-  // A / B already at row0 / col0.  Per wave: A rows [w*128/8, +128/8) of each plane,
-  // B rows [w*256/8, +256/8) of each plane, RPI rows per instruction.
+  // A / B already at row0 / col0.  Per wave: A rows [w*128/NW, +128/NW) of each plane,
+  // B rows [w*256/NW, +256/NW) of each plane, RPI rows per instruction.
   using C = H3Cfg<BK, NS>;
-  constexpr int AR = VAR_BM / 8, BR = VAR_BN / 8;  // rows per wave
+  constexpr int AR = VAR_BM / NW, BR = VAR_BN / NW;  // rows per wave
   if constexpr (AR >= C::RPI) {
 #pragma unroll
     for (int u = 0; u < AR / C::RPI; ++u) {
@@ -614,9 +614,9 @@ __device__ __forceinline__ vh8 h3_frag(const _Float16* plane, int r, int c) {
   return *reinterpret_cast<const vh8*>(plane + r * BK + (H3Cfg<BK, NS>::swz(r, c) << 3));
 }
 
-template <int BK, int NS>
+template <int BK, int NS, int JB>
 __device__ __forceinline__ void var_step_h3(const _Float16* st, int wm, int wn, int lane, int imin,
-                                            vf16 (&acc)[2][2]) {
+                                            vf16 (&acc)[2][JB]) {
   using C = H3Cfg<BK, NS>;
   const _Float16* ah = st;
   const _Float16* al = st + C::SA;
@@ -625,10 +625,10 @@ __device__ __forceinline__ void var_step_h3(const _Float16* st, int wm, int wn, 
 #pragma unroll
   for (int s = 0; s < BK / 16; ++s) {
     const int c = 2 * s + (lane >> 5);
-    vh8 fbh[2], fbl[2];
+    vh8 fbh[JB], fbl[JB];
 #pragma unroll
-    for (int jj = 0; jj < 2; ++jj) {
-      const int r = wn * 64 + jj * 32 + (lane & 31);
+    for (int jj = 0; jj < JB; ++jj) {
+      const int r = wn * (32 * JB) + jj * 32 + (lane & 31);
       fbh[jj] = h3_frag<BK, NS>(bh, r, c);
       fbl[jj] = h3_frag<BK, NS>(bl, r, c);
     }
@@ -638,7 +638,7 @@ __device__ __forceinline__ void var_step_h3(const _Float16* st, int wm, int wn, 
       const int r = wm * 64 + i * 32 + (lane & 31);
       const vh8 fah = h3_frag<BK, NS>(ah, r, c), fal = h3_frag<BK, NS>(al, r, c);
 #pragma unroll
-      for (int jj = 0; jj < 2; ++jj) {
+      for (int jj = 0; jj < JB; ++jj) {
         acc[i][jj] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fal, fbh[jj], acc[i][jj], 0, 0, 0);
         acc[i][jj] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fah, fbl[jj], acc[i][jj], 0, 0, 0);
         acc[i][jj] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fah, fbh[jj], acc[i][jj], 0, 0, 0);
@@ -651,20 +651,24 @@ __device__ __forceinline__ int h3_linv_exp(const unsigned long long* amax_bits) 
   return H3_KSCALE_EXP - ilogb(__longlong_as_double((long long)*amax_bits));
 }
 
-template <int BK, int NS>
-__global__ __launch_bounds__(V_NT, 1) void k_gp_var_h3(const _Float16* __restrict__ A, int64_t a_lo,
+// NW = 8: one 512-thread workgroup per CU, waves 2 x 4 of 64 x 64;
+// NW = 4: 256-thread workgroups, waves 2 x 2 of 64 x 128, two per CU (their
+// barriers do not align, so one's glds issue and barrier overlap the other's MFMAs)
+template <int BK, int NS, int NW>
+__global__ __launch_bounds__(NW * 64, 8 / NW) void k_gp_var_h3(const _Float16* __restrict__ A, int64_t a_lo,
                                                         const _Float16* __restrict__ B, int64_t b_lo, int64_t ld,
                                                         int32_t K, int32_t RT, int32_t CT, int64_t m,
                                                         int32_t* __restrict__ ticket, double* __restrict__ part,
                                                         int64_t ldp, const unsigned long long* __restrict__ amax_bits,
                                                         int32_t kexp) {
   using C = H3Cfg<BK, NS>;
-  static_assert(NS * C::STAGE * 2 <= 160 * 1024 - 64, "LDS");
+  static_assert(NS * C::STAGE * 2 <= (160 * 1024 - 128) / (8 / NW), "LDS");
+  constexpr int JB = VAR_BN / (NW / 2) / 32;  // 32-column blocks per wave
   __shared__ __attribute__((aligned(16))) _Float16 lds[NS * C::STAGE + 8];
   int32_t& s_item = *reinterpret_cast<int32_t*>(lds + NS * C::STAGE);
   const int t = threadIdx.x, lane = t & 63;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
-  const int wm = w >> 2, wn = w & 3;
+  const int wm = w / (NW / 2), wn = w % (NW / 2);
   const int32_t xcd = blockIdx.x & 7;
   const double unscale2 = __builtin_ldexp(1.0, -2 * (h3_linv_exp(amax_bits) + kexp));
 
@@ -681,18 +685,18 @@ __global__ __launch_bounds__(V_NT, 1) void k_gp_var_h3(const _Float16* __restric
     const _Float16* At = A + (int64_t)row0 * ld;
     const _Float16* Bt = B + col0 * ld;
 
-    vf16 acc[2][2];
+    vf16 acc[2][JB];
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
-      for (int jj = 0; jj < 2; ++jj)
+      for (int jj = 0; jj < JB; ++jj)
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[i][jj][r] = 0.0f;
 
     // prologue: stages 0 .. NS-2 in flight (nk >= 4 always: K and row0 + 128 are multiples of 128)
 #pragma unroll
     for (int q = 0; q < NS - 1; ++q)
-      if (q < nk) h3_issue<BK, NS>(At, a_lo, Bt, b_lo, ld, q * BK, lds + q * C::STAGE, w, lane);
+      if (q < nk) h3_issue<BK, NS, NW>(At, a_lo, Bt, b_lo, ld, q * BK, lds + q * C::STAGE, w, lane);
     // retire stage kt (NS - 2 younger stages may stay in flight), then refill
     // the slot of stage kt - 1 with stage kt + NS - 1
     auto pipe = [&](int32_t kt) -> const _Float16* {
@@ -703,23 +707,23 @@ __global__ __launch_bounds__(V_NT, 1) void k_gp_var_h3(const _Float16* __restric
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
       if (kt + NS - 1 < nk)
-        h3_issue<BK, NS>(At, a_lo, Bt, b_lo, ld, (kt + NS - 1) * BK, lds + ((kt + NS - 1) % NS) * C::STAGE, w, lane);
+        h3_issue<BK, NS, NW>(At, a_lo, Bt, b_lo, ld, (kt + NS - 1) * BK, lds + ((kt + NS - 1) % NS) * C::STAGE, w, lane);
       return lds + (kt % NS) * C::STAGE;
     };
     const int32_t nfull = min(nk, row0 / BK);
-    for (int32_t kt = 0; kt < nfull; ++kt) var_step_h3<BK, NS>(pipe(kt), wm, wn, lane, 0, acc);
+    for (int32_t kt = 0; kt < nfull; ++kt) var_step_h3<BK, NS, JB>(pipe(kt), wm, wn, lane, 0, acc);
     for (int32_t kt = nfull; kt < nk; ++kt) {
       const _Float16* st = pipe(kt);
       const int kd = ((kt - nfull) * BK) / 32 - 2 * wm;  // 32-row blocks of this wave entirely above the diagonal
       const int imin = kd < 0 ? 0 : kd;
-      if (imin < 2) var_step_h3<BK, NS>(st, wm, wn, lane, imin, acc);
+      if (imin < 2) var_step_h3<BK, NS, JB>(st, wm, wn, lane, imin, acc);
     }
 
     __syncthreads();
     double* red = reinterpret_cast<double*>(lds);  // [2][256]
 #pragma unroll
-    for (int jj = 0; jj < 2; ++jj) {
-      const int cl = wn * 64 + jj * 32 + (lane & 31);
+    for (int jj = 0; jj < JB; ++jj) {
+      const int cl = wn * (32 * JB) + jj * 32 + (lane & 31);
       double s = 0.0;
 #pragma unroll
       for (int i = 0; i < 2; ++i)
@@ -729,9 +733,9 @@ __global__ __launch_bounds__(V_NT, 1) void k_gp_var_h3(const _Float16* __restric
       if ((lane >> 5) == 0) red[wm * VAR_BN + cl] = s;
     }
     __syncthreads();
-    if (t < VAR_BN) {
-      const int64_t col = col0 + t;
-      if (col < m) part[(int64_t)rt * ldp + col] = (red[t] + red[VAR_BN + t]) * unscale2;
+    for (int u = t; u < VAR_BN; u += NW * 64) {
+      const int64_t col = col0 + u;
+      if (col < m) part[(int64_t)rt * ldp + col] = (red[u] + red[VAR_BN + u]) * unscale2;
     }
   }
 }
@@ -788,10 +792,12 @@ int launch_gemm_var(ut_ctx* c, int prec, const void* LinvT, int64_t lda, const v
   if (items < nb) nb = (int32_t)(((items + 7) / 8) * 8);
   UT_HIP(c, hipMemsetAsync(c->gp_ctr, 0, sizeof(int32_t) * 8, c->stream));
   if (prec == 16) {  // LinvT: L^-1 [row][k] hi/lo planes; kst: K* [col][row] hi/lo planes (see k_gp_var_h3)
-    // ring: 32 k x 3 slots (48-KiB stages).  16 k x 6 slots (4 stages in flight)
-    // measured slower: C3 var 95.8 -> 118.5 ms (twice the barriers per flop)
-    auto kern = k_gp_var_h3<32, 3>;
-    hipLaunchKernelGGL(kern, dim3(nb), dim3(V_NT), 0, c->stream, (const _Float16*)LinvT, lda * (int64_t)npad,
+    // 32 k x 3 slots (48-KiB stages), one 8-wave workgroup per CU.  Measured
+    // slower: 16 k x 6 slots (C3 var 95.8 -> 118.5 ms: twice the barriers per
+    // flop) and two 4-wave workgroups per CU (C3 var 96.7 -> 164.0 ms: two
+    // K* strips per XCD no longer fit its L2)
+    hipLaunchKernelGGL((k_gp_var_h3<32, 3, 8>), dim3(nb), dim3(V_NT), 0, c->stream, (const _Float16*)LinvT,
+                       lda * (int64_t)npad,
                        (const _Float16*)kst, ldk * (int64_t)npad, (int64_t)npad, npad, RT, CT, m, c->gp_ctr, part, ldk,
                        reinterpret_cast<const unsigned long long*>(c->gp_ctr + 16), h3_kstar_exp(c->gp_sf2));
   }

@@ -223,7 +223,11 @@ class BatchEngine:
         return out
 
     # -- GP ----------------------------------------------------------------
-    def gp_set_precision(self, bits: int):
+    def gp_set_precision(self, bits):
+        """64 (fp64 MFMA, 1e-5 tier), 32 (fp32 MFMA, 1e-3 tier) or 16 / "f16x3"
+        (variance contraction as three fp16 MFMA products of hi/lo splits, f32
+        accumulate: the 1e-3 tier at the fp16 MFMA rate); applies to later fits"""
+        bits = 16 if bits == "f16x3" else bits
         L.check(self.ctx, self.lib.ut_gp_set_precision(self.ctx, int(bits)), "ut_gp_set_precision")
 
     def gp_fit(self, X: np.ndarray, y: np.ndarray, lengthscale, sigma_f2: float = 1.0, sigma_n2: float = 1e-6,
