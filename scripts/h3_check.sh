@@ -3,7 +3,7 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out/h3
 O=gpurun_out/h3
-timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -k "gp_vs_oracle" -x -v --timeout 120 --timeout-method thread -p no:cacheprovider > $O/pytest.log 2>&1
+timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -k "gp_vs_oracle or f16x3" -x -v --timeout 120 --timeout-method thread -p no:cacheprovider > $O/pytest.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -25 $O/pytest.log; [ $rc -eq 0 ] || exit $rc
 for cfg in ${H3_CONFIGS:-c2 c3}; do
   for p in ${H3_PRECS:-16 32}; do

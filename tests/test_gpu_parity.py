@@ -209,8 +209,12 @@ def test_gp_small_golden(golden_dir):
 @pytest.mark.parametrize("prec", [64, 32, 16])
 @pytest.mark.parametrize("n,d,ell", [(1024, 64, 0.2), (200, 8, 0.5), (77, 3, 0.25), (300, 16, 1.5), (4096, 112, 1.0)])
 def test_gp_vs_oracle(n, d, ell, prec):
-    """fp64: 1e-5 relative; fp32 MFMA contractions: 1e-3 relative (north star),
-    absolute floor 1e-4 (variance near training points is a cancellation)."""
+    """fp64: 1e-5 relative; fp32 MFMA / f16x3 variance contraction: 1e-3 relative
+    (north star), absolute floor 1e-5 (variance near training points is a
+    cancellation).  K* and mu stay fp64 in both lower tiers: the first ten
+    candidates sit 1e-3 from training points, where |x/ell|^2 ~ 500 and a K*
+    exponent taken from an f32-accumulated x.u loses ~1e-4 of var (measured with
+    an f16x3 K*, not kept)."""
     rng = np.random.default_rng(n + d)
     X = rng.uniform(size=(n, d))
     y = np.sum((X - 0.4) ** 2, axis=1) + 0.01 * rng.standard_normal(n)
@@ -234,6 +238,39 @@ def test_gp_vs_oracle(n, d, ell, prec):
         _close(mu.cpu().numpy(), mu_o)                     # K* and mu stay fp64
         _close(var.cpu().numpy(), var_o, rtol=1e-3, atol=1e-5)
         _close(ei.cpu().numpy(), ei_o, rtol=1e-3, atol=1e-5)
+
+
+@pytest.mark.parametrize("sf2,ell,sn2,tier", [(1e-3, 0.4, 1e-9, True), (37.0, 0.6, 1e-4, True),
+                                              (2.0, 2.0, 1e-6, False)])
+def test_gp_f16x3_scaling(sf2, ell, sn2, tier):
+    """f16x3 operand scales: sigma_f2 far from 1 (K* scale 2^(14 - ilogb sf2)) and a
+    long lengthscale (near-singular K, large |L^-1| entries: the device-side max
+    sets L^-1's scale).  The fp32-tier bound (relative to sf2) where the problem is
+    conditioned for it; in the near-singular case (ell = 2 on the unit 6-cube,
+    every var ~1e-6, sf2 - |L^-1 k*|^2 cancels to ~1e-6 relative) neither 32-bit
+    tier meets 1e-5 absolute, and f16x3 is held to the fp32-MFMA path's own error."""
+    rng = np.random.default_rng(int(sf2 * 1000) + 7)
+    n, d = 500, 6
+    X = rng.uniform(size=(n, d))
+    y = np.sin(3 * X).sum(axis=1) + 0.01 * rng.standard_normal(n)
+    U = rng.uniform(size=(2000, d))
+    U[:20] = X[:20] + 1e-3
+    space = [Param(f"u{k}", FLOAT, 0.0, 1.0) for k in range(d)]
+    g = ogp.GP(X, y, lengthscale=ell, sigma_f2=sf2, sigma_n2=sn2, jitter=1e-8)
+    mu_o, var_o = g.posterior(U)
+    got = {}
+    for prec in (32, 16):
+        e = engine(space)
+        e.gp_set_precision(prec)
+        e.gp_fit(X, y, lengthscale=ell, sigma_f2=sf2, sigma_n2=sn2, jitter=1e-8)
+        mu, var, _ = e.gp_score(dev(U.T))
+        got[prec] = var.cpu().numpy()
+        _close(mu.cpu().numpy(), mu_o)
+    err = {p: np.max(np.abs(v - var_o)) / sf2 for p, v in got.items()}
+    if tier:
+        _close(got[16], var_o, rtol=1e-3, atol=1e-5 * sf2)
+    # f16x3 stays within a small factor of the fp32-MFMA path's own error
+    assert err[16] <= max(4 * err[32], 1e-7), err
 
 
 # --------------------------------------------------------------------------- top-k
