@@ -585,14 +585,16 @@ __device__ __forceinline__ void h3_glds(const _Float16* __restrict__ src, int64_
                                    (__attribute__((address_space(3))) void*)(plane + rb * BK), 16, 0, 0);
 }
 
-template <int BK, int NS, int NW>
+// PART: 3 = the whole stage, 1 = its A planes only, 2 = its B planes only
+template <int BK, int NS, int NW, int PART = 3>
 __device__ __forceinline__ void h3_issue(const _Float16* __restrict__ A, int64_t a_lo, const _Float16* __restrict__ B,
                                          int64_t b_lo, int64_t ld, int32_t k0, _Float16* st, int w, int lane) {
   // A / B already at row0 / col0.  Per wave: A rows [w*128/NW, +128/NW) of each plane,
   // B rows [w*256/NW, +256/NW) of each plane, RPI rows per instruction.
   using C = H3Cfg<BK, NS>;
   constexpr int AR = VAR_BM / NW, BR = VAR_BN / NW;  // rows per wave
-  if constexpr (AR >= C::RPI) {
+  if constexpr (!(PART & 1)) {
+  } else if constexpr (AR >= C::RPI) {
 #pragma unroll
     for (int u = 0; u < AR / C::RPI; ++u) {
       h3_glds<BK, NS>(A, ld, w * AR + u * C::RPI, k0, st, lane);
@@ -603,7 +605,7 @@ __device__ __forceinline__ void h3_issue(const _Float16* __restrict__ A, int64_t
     h3_glds<BK, NS>(A + (w & 1) * a_lo, ld, rb, k0, st + (w & 1) * C::SA, lane);
   }
 #pragma unroll
-  for (int u = 0; u < BR / C::RPI; ++u) {
+  for (int u = 0; u < ((PART & 2) ? BR / C::RPI : 0); ++u) {
     h3_glds<BK, NS>(B, ld, w * BR + u * C::RPI, k0, st + 2 * C::SA, lane);
     h3_glds<BK, NS>(B + b_lo, ld, w * BR + u * C::RPI, k0, st + 2 * C::SA + C::SB, lane);
   }
@@ -614,9 +616,11 @@ __device__ __forceinline__ vh8 h3_frag(const _Float16* plane, int r, int c) {
   return *reinterpret_cast<const vh8*>(plane + r * BK + (H3Cfg<BK, NS>::swz(r, c) << 3));
 }
 
-template <int BK, int NS, int JB>
+// mid(): called between the first and second k16 sub-steps (the B half of the
+// next stage's glds goes there, behind this stage's first MFMAs)
+template <int BK, int NS, int JB, class Mid>
 __device__ __forceinline__ void var_step_h3(const _Float16* st, int wm, int wn, int lane, int imin,
-                                            vf16 (&acc)[2][JB]) {
+                                            vf16 (&acc)[2][JB], Mid&& mid) {
   using C = H3Cfg<BK, NS>;
   const _Float16* ah = st;
   const _Float16* al = st + C::SA;
@@ -624,6 +628,11 @@ __device__ __forceinline__ void var_step_h3(const _Float16* st, int wm, int wn, 
   const _Float16* bl = bh + C::SB;
 #pragma unroll
   for (int s = 0; s < BK / 16; ++s) {
+    if (s == 1) {
+      __builtin_amdgcn_sched_barrier(0);
+      mid();
+      __builtin_amdgcn_sched_barrier(0);
+    }
     const int c = 2 * s + (lane >> 5);
     vh8 fbh[JB], fbl[JB];
 #pragma unroll
@@ -699,6 +708,9 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void k_gp_var_h3(const _Float16* _
       if (q < nk) h3_issue<BK, NS, NW>(At, a_lo, Bt, b_lo, ld, q * BK, lds + q * C::STAGE, w, lane);
     // retire stage kt (NS - 2 younger stages may stay in flight), then refill
     // the slot of stage kt - 1 with stage kt + NS - 1
+    // the refill of stage kt + NS - 1 is split: A planes right after the
+    // barrier, B planes between the stage's two k16 sub-steps (spreads the glds
+    // issue cost over the MFMAs; the vmcnt count per stage is unchanged)
     auto pipe = [&](int32_t kt) -> const _Float16* {
       if (kt + NS - 2 < nk)
         wait_vmcnt<C::PER_WAVE * (NS - 2)>();
@@ -707,16 +719,25 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void k_gp_var_h3(const _Float16* _
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
       if (kt + NS - 1 < nk)
-        h3_issue<BK, NS, NW>(At, a_lo, Bt, b_lo, ld, (kt + NS - 1) * BK, lds + ((kt + NS - 1) % NS) * C::STAGE, w, lane);
+        h3_issue<BK, NS, NW, 1>(At, a_lo, Bt, b_lo, ld, (kt + NS - 1) * BK, lds + ((kt + NS - 1) % NS) * C::STAGE, w,
+                                lane);
       return lds + (kt % NS) * C::STAGE;
     };
+    auto refill_b = [&](int32_t kt) {
+      return [&, kt]() {
+        if (kt + NS - 1 < nk)
+          h3_issue<BK, NS, NW, 2>(At, a_lo, Bt, b_lo, ld, (kt + NS - 1) * BK, lds + ((kt + NS - 1) % NS) * C::STAGE,
+                                  w, lane);
+      };
+    };
     const int32_t nfull = min(nk, row0 / BK);
-    for (int32_t kt = 0; kt < nfull; ++kt) var_step_h3<BK, NS, JB>(pipe(kt), wm, wn, lane, 0, acc);
+    for (int32_t kt = 0; kt < nfull; ++kt) var_step_h3<BK, NS, JB>(pipe(kt), wm, wn, lane, 0, acc, refill_b(kt));
     for (int32_t kt = nfull; kt < nk; ++kt) {
       const _Float16* st = pipe(kt);
       const int kd = ((kt - nfull) * BK) / 32 - 2 * wm;  // 32-row blocks of this wave entirely above the diagonal
       const int imin = kd < 0 ? 0 : kd;
-      if (imin < 2) var_step_h3<BK, NS, JB>(st, wm, wn, lane, imin, acc);
+      if (imin < 2) var_step_h3<BK, NS, JB>(st, wm, wn, lane, imin, acc, refill_b(kt));
+      else refill_b(kt)();
     }
 
     __syncthreads();
