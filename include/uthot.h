@@ -84,7 +84,8 @@ typedef struct ut_param_desc {
                               ENUM, 0=False/1=True for BOOL */
   int32_t vtab_count;  /* LOGINT: >0 = get_value(v) = math.log(v + 1.0 - min, 2.0) for
                           v = lo .. lo+vtab_count-1, computed by the host's CPython;
-                          0 = computed on the device (correctly rounded log) */
+                          0 = computed on the device (ut_core.h libm_log: glibc's
+                          log restated bit for bit, so the same values) */
   int32_t pad;
   const double* vtab_host;
   /* PERM: repr(item) bytes of the n_options items, concatenated, and their
@@ -100,7 +101,9 @@ enum { UT_X_NONE = 0, UT_X_OX1 = 1, UT_X_OX3 = 2, UT_X_PX = 3, UT_X_CX = 4, UT_X
 typedef struct ut_de_params {   /* differentialevolution.py:34-40,142-151 */
   double cr;                    /* crossover rate (0.9 DE, 0.2 DE-Alt) */
   int32_t n_cross;              /* forced crossovers (1), <= 4 */
-  int32_t pad;
+  int32_t information_sharing;  /* copies of the driver's best config added to the donor pool (1);
+                                   used only when best != NULL (differentialevolution.py:112-116) */
+  const double* best;           /* device row [ncols]: driver.best_result's values, NULL = no result yet */
 } ut_de_params;
 
 typedef struct ut_gp_hyper {
@@ -149,7 +152,11 @@ int ut_population_replace(ut_ctx* ctx, const double* trial, int64_t ld, const in
 
 /* ---- proposal ----------------------------------------------------------- */
 /* DE/rand/1/bin: one trial per candidate; candidate g targets population
- * member g % npop (differentialevolution.py:105-129). */
+ * member g % npop (differentialevolution.py:105-129).  Donors x1, x2, x3 are
+ * the first three of a shuffle of population - {target} plus
+ * information_sharing copies of `best` (:109-118): three distinct pool
+ * positions, so x1..x3 may all be copies of the best config.  Needs
+ * npop - 1 + (best ? information_sharing : 0) >= 3. */
 int ut_propose_de(ut_ctx* ctx, const ut_de_params* p, uint32_t round_, int64_t cand_base, int64_t m,
                   double* out_values, int64_t ld);
 

@@ -5,7 +5,10 @@ Batch semantics (the build's): candidate g (global index)
 targets population member g % npop and produces one trial.  The reference's
 random draws are replaced by Philox draws keyed by (seed, g, stream, round):
 
-  donors  x1,x2,x3 : 3 distinct members != target      (:109-118, shuffle(set(pop)-{target}))
+  donors  x1,x2,x3 : the first 3 of shuffle(list(set(pop) - {target})
+                     + [best] * information_sharing)     (:109-118)
+                     = 3 distinct positions of that pool; a position past the
+                     npop - 1 other members is a copy of the best config
   use_f   = random()/2.0 + 0.5                          (:120)
   forced  = first n_cross names of a shuffled name list (:122-125)
             == the n_cross params with the smallest per-param keys
@@ -23,24 +26,27 @@ from .space import (PERM, columns, get_unit_value_vec, op4_set_linear_primitive,
                     width)
 
 
-def donors(g, npop, seed, round_):
-    """3 distinct members != t = g % npop (vectorised)"""
+def donors(g, npop, seed, round_, share=0):
+    """(t, d1, d2, d3) for t = g % npop (vectorised).  The donor pool is the
+    npop - 1 members other than t followed by `share` copies of the best
+    config (differentialevolution.py:110-116); three distinct positions a, b, c
+    of it are drawn (shuffle()[0:3]); a member position q maps to member
+    q + (q >= t), a best-copy position to -1."""
     g = np.asarray(g, dtype=np.uint64)
     t = (g % np.uint64(npop)).astype(np.int64)
+    Q = npop - 1 + share
     x, y, z, _ = ph.draw(seed, g, ph.STREAM_CAND | 0, round_, ph.OP_DE)
-    a = ph.umulhi32(x, npop - 1).astype(np.int64)
-    d1 = a + (a >= t)
-    e0, e1 = np.minimum(t, d1), np.maximum(t, d1)
-    b = ph.umulhi32(y, npop - 2).astype(np.int64)
-    b = b + (b >= e0)
-    b = b + (b >= e1)
-    d2 = b
-    s = np.sort(np.stack([t, d1, d2]), axis=0)
-    c = ph.umulhi32(z, npop - 3).astype(np.int64)
-    c = c + (c >= s[0])
-    c = c + (c >= s[1])
-    c = c + (c >= s[2])
-    return t, d1, d2, c
+    a = ph.umulhi32(x, Q).astype(np.int64)
+    b = ph.umulhi32(y, Q - 1).astype(np.int64)
+    b = b + (b >= a)
+    s0, s1 = np.minimum(a, b), np.maximum(a, b)
+    c = ph.umulhi32(z, Q - 2).astype(np.int64)
+    c = c + (c >= s0)
+    c = c + (c >= s1)
+
+    def member(q):
+        return np.where(q < npop - 1, q + (q >= t), -1)
+    return t, member(a), member(b), member(c)
 
 
 def use_f(g, seed, round_):
@@ -59,13 +65,19 @@ def forced_mask(g, P, n_cross, seed, round_):
     return keys <= kth
 
 
-def propose_de_vec(space, pop, seed, round_, cand_base, m, cr, n_cross=1):
-    """pop: SoA [ncols][npop] float64 -> trial SoA [ncols][m]"""
+def propose_de_vec(space, pop, seed, round_, cand_base, m, cr, n_cross=1, best=None, information_sharing=1):
+    """pop: SoA [ncols][npop] float64 -> trial SoA [ncols][m].  best: the
+    driver's best config as a value row [ncols] (None: no result yet, the pool
+    is the population only)."""
     ncols, npop = pop.shape
     P = len(space)
     starts, _ = columns(space)
     g = np.arange(cand_base, cand_base + m, dtype=np.uint64)
-    t, d1, d2, d3 = donors(g, npop, seed, round_)
+    share = information_sharing if best is not None else 0
+    t, d1, d2, d3 = donors(g, npop, seed, round_, share)
+    if share:   # the best config as an extra population column npop
+        pop = np.concatenate([pop, np.asarray(best, dtype=np.float64).reshape(ncols, 1)], axis=1)
+        d1, d2, d3 = (np.where(d < 0, npop, d) for d in (d1, d2, d3))
     F = use_f(g, seed, round_)
     forced = forced_mask(g, P, n_cross, seed, round_)
     out = np.empty((ncols, m), dtype=np.float64)
@@ -107,13 +119,15 @@ def propose_de_vec(space, pop, seed, round_, cand_base, m, cr, n_cross=1):
     return out
 
 
-def propose_de_scalar(space, pop_cfgs, seed, round_, g, cr, n_cross=1):
+def propose_de_scalar(space, pop_cfgs, seed, round_, g, cr, n_cross=1, best_cfg=None, information_sharing=1):
     """One trial, written like create_new_configuration (:105-129) over
     Python values.  pop_cfgs: list of configs (lists of stored values)."""
     npop = len(pop_cfgs)
-    t, d1, d2, d3 = (int(v[0]) for v in donors(np.array([g]), npop, seed, round_))
+    share = information_sharing if best_cfg is not None else 0
+    t, d1, d2, d3 = (int(v[0]) for v in donors(np.array([g]), npop, seed, round_, share))
     cfg = list(pop_cfgs[t])                         # manipulator.copy(parent.config.data)
-    x1, x2, x3 = pop_cfgs[d1], pop_cfgs[d2], pop_cfgs[d3]
+    # shuffled_pop += [PopulationMember(best)] * information_sharing (:113-116)
+    x1, x2, x3 = (best_cfg if d < 0 else pop_cfgs[d] for d in (d1, d2, d3))
     F = float(use_f(np.array([g]), seed, round_)[0])
     forced = forced_mask(np.array([g]), len(space), n_cross, seed, round_)[:, 0]
     for p, prm in enumerate(space):

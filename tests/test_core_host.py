@@ -120,23 +120,35 @@ def _batch(lib, name, xs):
     return out
 
 
-def test_py_log2_correctly_rounded(hc):
-    """log_cr / py_log2 (math.log(x, 2.0) = log(x) / log(2.0)) are correctly
-    rounded: checked against 80-digit Decimal on integer and random arguments.
-    (CPython's libm log is not: it differs from the correctly rounded value on
-    ~2e-5 of integer arguments on this host, which is why LogInteger digests
-    and log values come from host tables computed by CPython itself -- see
-    uptune_amd/manipulator.py LOGINT_TABLE_MAX.)"""
-    from decimal import Decimal, getcontext
-    getcontext().prec = 80
+def test_py_log2_matches_cpython(hc):
+    """ut::libm_log / py_log2 restate glibc's __log_fma (the log CPython's
+    math.log calls here) bit for bit: LogIntegerParameter._scale =
+    math.log(v + 1.0 - min, 2.0) (manipulator.py:784-787) on every integer
+    argument in [1, 2^22], 10^6 random integers below 2^31, integers near 2^53,
+    and random positive doubles (subnormals and the |x - 1| < 1/16 branch
+    included).  This is what removes the LogInteger table-size limit on
+    bit-exact digests."""
     rng = random.Random(7)
-    xs = [0.5001, 1.4999, 2.4999, 1e6 + 0.4999, 2.0 ** 40 + 3, 2.0 ** 52 - 1, 9170.0, 136837.0, 277862.0] + \
-         [float(rng.randrange(1, 1 << 24)) for _ in range(5000)] + [rng.uniform(0.5, 1e12) for _ in range(5000)]
-    got = _batch(hc, "uthc_py_log2", xs)
-    ln2 = math.log(2.0)
-    for x, g in zip(xs, got):
-        want = float(Decimal(x).ln()) / ln2
-        assert g == want, (x, g, want)
+    ints = np.arange(1, (1 << 22) + 1, dtype=np.float64)
+    rnd = np.array([rng.randrange(1, 1 << 31) for _ in range(1000000)], dtype=np.float64)
+    big = np.array([2.0 ** 53 - k for k in range(1, 2000)] + [float(rng.randrange(1 << 31, 1 << 53))
+                                                               for _ in range(100000)])
+    bits = np.array([rng.getrandbits(63) for _ in range(200000)], dtype=np.uint64).view(np.float64)
+    bits = bits[np.isfinite(bits) & (bits > 0)]
+    near1 = np.array([1.0 + rng.uniform(-0.0625, 0.0647) for _ in range(100000)])
+    special = np.array([0.5001, 1.4999, 2.4999, 1e6 + 0.4999, 5e-324, 2.2250738585072014e-308, 1.7976931348623157e308,
+                        1.0, 0.9375, float.fromhex("0x1.09p+0"), float("inf")])
+    for xs in (ints, rnd, big, bits, near1, special):
+        got = _batch(hc, "uthc_py_log2", xs)
+        want = np.array([math.log(x, 2.0) for x in xs.tolist()])
+        bad = np.flatnonzero(got.view(np.uint64) != want.view(np.uint64))
+        assert bad.size == 0, [(xs[i], got[i], want[i]) for i in bad[:5]]
+        gl = _batch(hc, "uthc_libm_log", xs)
+        wl = np.array([math.log(x) for x in xs.tolist()])
+        assert np.array_equal(gl.view(np.uint64), wl.view(np.uint64))
+    # domain edges of log itself
+    assert _batch(hc, "uthc_libm_log", [0.0])[0] == float("-inf")
+    assert math.isnan(_batch(hc, "uthc_libm_log", [-1.0])[0])
 
 
 def test_logint_unscale_matches_cpython(hc):

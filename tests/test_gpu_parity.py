@@ -129,6 +129,45 @@ def test_de_matches_oracle(cr, n_cross):
     np.testing.assert_array_equal(got, want)
 
 
+@pytest.mark.parametrize("npop,share", [(30, 1), (30, 0), (4, 3), (257, 2)])
+def test_de_information_sharing_matches_oracle(npop, share):
+    """donor pool = population - {target} + [best] * information_sharing
+    (differentialevolution.py:110-118), the reference's 30-member population
+    included; the best row is a device row passed per call"""
+    space = mixed_space()
+    e = engine(space, seed=22)
+    pop = ode.population_init(space, npop, seed=5)
+    best = ode.population_init(space, 1, seed=77)[:, 0]
+    e.population_set(dev(pop))
+    got = e.propose_de(3000, round_=2, cand_base=9, cr=0.5, n_cross=1, best=best,
+                       information_sharing=share).cpu().numpy()
+    want = ode.propose_de_vec(space, pop, 22, 2, 9, 3000, 0.5, 1, best=best, information_sharing=share)
+    np.testing.assert_array_equal(got, want)
+    if share:   # the best config's values do reach the trials
+        assert not np.array_equal(got, ode.propose_de_vec(space, pop, 22, 2, 9, 3000, 0.5, 1))
+
+
+def test_de_information_sharing_perm():
+    space = perm_space()
+    e = engine(space, seed=24)
+    pop = ode.population_init(space, 30, seed=6)
+    best = ode.population_init(space, 1, seed=88)[:, 0]
+    e.population_set(dev(pop))
+    got = e.propose_de(2000, round_=3, cand_base=1, cr=0.5, n_cross=2, best=best).cpu().numpy()
+    np.testing.assert_array_equal(got, ode.propose_de_vec(space, pop, 24, 3, 1, 2000, 0.5, 2, best=best))
+
+
+def test_de_donor_pool_too_small():
+    from uptune_amd._lib import UthotError
+    space = mixed_space()
+    e = engine(space, seed=1)
+    e.population_set(dev(ode.population_init(space, 3, seed=1)))
+    with pytest.raises(UthotError):
+        e.propose_de(10)                                         # 2 members besides the target
+    best = ode.population_init(space, 1, seed=2)[:, 0]
+    e.propose_de(10, best=best, information_sharing=1)           # 2 + 1 best copy: OK
+
+
 def test_de_golden(golden_dir):
     z = np.load(os.path.join(golden_dir, "de_mixed.npz"))
     e = engine(mixed_space(), seed=11)
@@ -444,13 +483,21 @@ def hpl_space():
     return oracle_space(spaces.hpl64())
 
 
-def _libm_log_is_cr(x):
-    """True when CPython's math.log(x) is the correctly rounded log (the
-    device's LogInteger log is; glibc's is not on ~2e-5 of arguments)"""
+def _non_cr_log_ints(lo, hi, count, seed=5):
+    """integers x in [lo, hi) where CPython's math.log(x) is NOT the correctly
+    rounded log -- the arguments a correctly rounded device log got wrong in
+    round 1 (glibc's log is <= 0.52 ulp, not correctly rounded)"""
     import math
+    import random
     from decimal import Decimal, getcontext
     getcontext().prec = 60
-    return math.log(x) == float(Decimal(x).ln())
+    rng = random.Random(seed)
+    out = []
+    while len(out) < count:
+        x = rng.randrange(lo, hi)
+        if math.log(x) != float(Decimal(x).ln()):
+            out.append(x)
+    return out
 
 
 def test_hpl_population_de_encode_hash():
@@ -463,15 +510,31 @@ def test_hpl_population_de_encode_hash():
     want = ode.propose_de_vec(space, pop, 13, 3, 77, 6000, 0.5, 2)
     np.testing.assert_array_equal(got, want)
     np.testing.assert_array_equal(e.encode(dev(got)).cpu().numpy(), features(space, got))
-    # hashes: bit-exact, except where the large-range LogInteger (device log)
-    # meets one of libm's non-correctly-rounded logs
-    li3 = [i for i, p in enumerate(space) if p.name == "logint_3"][0]
+    # hashes bit-exact everywhere, including logint_3 (range 2^30: no host
+    # table, the device's libm_log restatement)
     hx = hexes(e.hash(dev(got)))
     want_h = oracle_hashes(space, got)
     bad = [j for j in range(got.shape[1]) if hx[j] != want_h[j]]
-    for j in bad:
-        assert not _libm_log_is_cr(got[li3, j] + 1.0 - 0.0), j
-    assert len(bad) <= 2
+    assert bad == []
+
+
+def test_logint_large_range_bit_exact():
+    """LogIntegerParameter over [0, 2^31) (no host table): get_value =
+    math.log(v + 1.0 - min, 2.0) restated on the device (ut_core.h libm_log)
+    is bit-identical to THIS box's CPython on random values and on integers
+    where libm's log is not correctly rounded; digests and unit features
+    follow (manipulator.py:784-787, :456-459)."""
+    from oracle.space import LOGINT
+    space = [Param("big_log", LOGINT, 0, (1 << 31) - 1), Param("f", FLOAT, 0.0, 1.0)]
+    e = engine(space, seed=3)
+    assert e.spec.params[0].vtab is None
+    rng = np.random.default_rng(11)
+    xs = _non_cr_log_ints(1 << 22, 1 << 31, 300) + [int(v) for v in rng.integers(0, (1 << 31) - 1, 4000)]
+    vals = np.zeros((2, len(xs)))
+    vals[0] = [x - 1 for x in xs]          # v + 1.0 - min = x
+    vals[1] = rng.uniform(size=len(xs))
+    assert hexes(e.hash(dev(vals))) == oracle_hashes(space, vals)
+    np.testing.assert_array_equal(e.encode(dev(vals)).cpu().numpy(), features(space, vals))
 
 
 @pytest.mark.parametrize("alias,enum_mode", [(True, 0), (False, 1)])

@@ -112,6 +112,40 @@ def test_de_invariants():
     assert np.all(forced.sum(axis=0) == 1)
 
 
+def test_de_information_sharing():
+    """donor pool = population - {target} + [best] * information_sharing
+    (differentialevolution.py:110-118): the scalar restatement (written like the
+    reference, over config lists) equals the vectorised one; without a best
+    result the pool is the population alone and the trials are unchanged; with
+    a 30-member population the best is among the 3 donors 3/30 of the time."""
+    space = _space()
+    pop = ode.population_init(space, 30, seed=12)
+    best = ode.population_init(space, 1, seed=99)[:, 0]
+    pop_cfgs = [[from_f64(p, pop[j, i]) for j, p in enumerate(space)] for i in range(30)]
+    best_cfg = [from_f64(p, best[j]) for j, p in enumerate(space)]
+    for share in (1, 3):
+        trial = ode.propose_de_vec(space, pop, 12, 4, 7, 64, 0.6, 1, best=best, information_sharing=share)
+        for i in range(64):
+            cfg = ode.propose_de_scalar(space, pop_cfgs, 12, 4, 7 + i, 0.6, 1, best_cfg=best_cfg,
+                                        information_sharing=share)
+            assert [from_f64(p, trial[j, i]) for j, p in enumerate(space)] == cfg
+    np.testing.assert_array_equal(ode.propose_de_vec(space, pop, 12, 4, 7, 64, 0.6, 1, best=None),
+                                  ode.propose_de_vec(space, pop, 12, 4, 7, 64, 0.6, 1))
+    np.testing.assert_array_equal(ode.propose_de_vec(space, pop, 12, 4, 7, 64, 0.6, 1, best=best,
+                                                     information_sharing=0),
+                                  ode.propose_de_vec(space, pop, 12, 4, 7, 64, 0.6, 1))
+    g = np.arange(200000, dtype=np.uint64)
+    t, d1, d2, d3 = ode.donors(g, 30, seed=3, round_=1, share=1)
+    st = np.stack([d1, d2, d3])
+    frac = np.mean((st < 0).any(axis=0))
+    assert abs(frac - 3.0 / 30.0) < 0.004, frac
+    assert np.all((st < 0).sum(axis=0) <= 1)                   # one best copy: at most one best donor
+    assert np.all((st != t) | (st < 0))
+    # share = 5 copies: distinct POSITIONS, so several donors may be the best
+    _, e1, e2, e3 = ode.donors(g[:20000], 4, seed=3, round_=1, share=5)
+    assert np.any((np.stack([e1, e2, e3]) < 0).sum(axis=0) == 3)
+
+
 def test_r64_hash_golden(golden_dir):
     z = np.load(os.path.join(golden_dir, "r64_hashes.npz"))
     space = [Param(d, FLOAT, -1000.0, 1000.0) for d in range(64)]

@@ -47,7 +47,8 @@ UT_SPLIT_LE, UT_SPLIT_LT = 0, 1
 
 
 class DeParams(C.Structure):
-    _fields_ = [("cr", C.c_double), ("n_cross", C.c_int32), ("pad", C.c_int32)]
+    _fields_ = [("cr", C.c_double), ("n_cross", C.c_int32), ("information_sharing", C.c_int32),
+                ("best", C.c_void_p)]
 
 
 class PsoParams(C.Structure):

@@ -27,7 +27,7 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("UT_OFFLOAD_ARCH", "gfx950")
 
 SOURCES = ["api.hip", "propose.hip", "hash.hip", "dedup.hip", "gp.hip", "gp_gemm.hip", "topk.hip", "forest.hip"]
-HEADERS = ["ut_core.h", "ut_internal.h", "ut_param.h", "ut_perm.h", "ryu_tables.h", os.path.join("..", "..", "include", "uthot.h")]
+HEADERS = ["ut_core.h", "ut_internal.h", "ut_param.h", "ut_perm.h", "ryu_tables.h", "libm_log_data.h", os.path.join("..", "..", "include", "uthot.h")]
 
 HIP_FLAGS = [
     "-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}",

@@ -454,6 +454,10 @@ int ut_propose_de(ut_ctx* c, const ut_de_params* p, uint32_t round_, int64_t can
   UT_CHECK(c, c->has_space, UT_ENOSPACE, "space not defined");
   UT_CHECK(c, c->pop != nullptr, UT_EINVAL, "propose_de: population not initialised");
   UT_CHECK(c, p && p->n_cross >= 0 && p->n_cross <= 4, UT_EINVAL, "propose_de: n_cross must be in [0, 4]");
+  UT_CHECK(c, p->information_sharing >= 0 && p->information_sharing <= (1 << 20), UT_EINVAL,
+           "propose_de: information_sharing must be in [0, 2^20]");
+  UT_CHECK(c, c->npop - 1 + (p->best ? (int64_t)p->information_sharing : 0) >= 3, UT_EINVAL,
+           "propose_de: the donor pool (population - target + best copies) needs >= 3 entries");
   UT_CHECK(c, m >= 0 && cand_base >= 0 && (out_values || m == 0) && ld >= m, UT_EINVAL, "propose_de: bad arguments");
   if (m == 0) return 0;
   return launch_de(c, p, round_, cand_base, m, out_values, ld);

@@ -70,6 +70,9 @@ void uthc_philox(unsigned long long seed, unsigned long long cand, unsigned stre
 void uthc_py_log2(const double* x, double* out, long long n) {
   for (long long i = 0; i < n; ++i) out[i] = ut::py_log2(x[i]);
 }
+void uthc_libm_log(const double* x, double* out, long long n) {
+  for (long long i = 0; i < n; ++i) out[i] = ut::libm_log(x[i]);
+}
 void uthc_exp2(const double* x, double* out, long long n) {
   for (long long i = 0; i < n; ++i) out[i] = ut::exp2_cr(x[i]);
 }

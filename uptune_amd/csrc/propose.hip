@@ -44,27 +44,28 @@ __global__ __launch_bounds__(256) void k_population_init(const DevParam* __restr
   }
 }
 
-// Sample 3 distinct population members other than `t` (the reference draws
-// x1,x2,x3 from shuffle(set(population) - {target}),
-// differentialevolution.py:109-118).
-__device__ __forceinline__ void pick_donors(uint32_t w0, uint32_t w1, uint32_t w2, int64_t npop, int64_t t,
-                                            int64_t& d1, int64_t& d2, int64_t& d3) {
-  int64_t a = (int64_t)umulhi32(w0, (uint32_t)(npop - 1));
-  d1 = a + (a >= t ? 1 : 0);
-  int64_t e0 = t < d1 ? t : d1, e1 = t < d1 ? d1 : t;
-  int64_t b = (int64_t)umulhi32(w1, (uint32_t)(npop - 2));
-  if (b >= e0) ++b;
-  if (b >= e1) ++b;
-  d2 = b;
-  // sort {t, d1, d2}
-  int64_t s0 = e0, s1 = e1, s2 = d2;
-  if (s2 < s1) { int64_t x = s1; s1 = s2; s2 = x; }
-  if (s1 < s0) { int64_t x = s0; s0 = s1; s1 = x; }
-  int64_t c = (int64_t)umulhi32(w2, (uint32_t)(npop - 3));
+// x1, x2, x3 = the first 3 of shuffle(list(set(population) - {target}) +
+// [best] * information_sharing) (differentialevolution.py:109-118): three
+// distinct positions of a pool of Q = (npop - 1) + share entries.  Position
+// q < npop - 1 is the q-th member other than t (q + (q >= t)); positions
+// >= npop - 1 are copies of the best config, returned as -1.  With share = 0
+// this is exactly 3 distinct members != t.
+__device__ __forceinline__ int64_t pool_member(int64_t q, int64_t npop, int64_t t) {
+  return q < npop - 1 ? q + (q >= t ? 1 : 0) : -1;
+}
+__device__ __forceinline__ void pick_donors(uint32_t w0, uint32_t w1, uint32_t w2, int64_t npop, int64_t share,
+                                            int64_t t, int64_t& d1, int64_t& d2, int64_t& d3) {
+  const int64_t Q = npop - 1 + share;
+  const int64_t a = (int64_t)umulhi32(w0, (uint32_t)Q);
+  int64_t b = (int64_t)umulhi32(w1, (uint32_t)(Q - 1));
+  b += (b >= a ? 1 : 0);
+  const int64_t s0 = a < b ? a : b, s1 = a < b ? b : a;
+  int64_t c = (int64_t)umulhi32(w2, (uint32_t)(Q - 2));
   if (c >= s0) ++c;
   if (c >= s1) ++c;
-  if (c >= s2) ++c;
-  d3 = c;
+  d1 = pool_member(a, npop, t);
+  d2 = pool_member(b, npop, t);
+  d3 = pool_member(c, npop, t);
 }
 
 // One DE trial per candidate.  Candidate g (global) targets member g % npop.
@@ -73,6 +74,7 @@ __device__ __forceinline__ void pick_donors(uint32_t w0, uint32_t w1, uint32_t w
 // differentialevolution.py:122-125).
 __global__ __launch_bounds__(256) void k_de(const DevParam* __restrict__ params, int32_t P,
                                             const double* __restrict__ vtab, const double* __restrict__ pop, int64_t ldp, int64_t npop,
+                                            const double* __restrict__ best, int64_t share,
                                             double cr, int32_t n_cross, uint64_t seed, uint32_t round_,
                                             int64_t cand_base, int64_t m, double* __restrict__ out,
                                             int64_t ldo) {
@@ -82,7 +84,7 @@ __global__ __launch_bounds__(256) void k_de(const DevParam* __restrict__ params,
   const int64_t t = (int64_t)(g % (uint64_t)npop);
   const u32x4 rc = draw(seed, g, STREAM_CAND | 0u, round_, OP_DE);
   int64_t d1, d2, d3;
-  pick_donors(rc.x, rc.y, rc.z, npop, t, d1, d2, d3);
+  pick_donors(rc.x, rc.y, rc.z, npop, share, t, d1, d2, d3);
   const u32x4 rf = draw(seed, g, STREAM_CAND | 1u, round_, OP_DE);
   // use_f = old_div(random.random(), 2.0) + 0.5
   const double F = __dadd_rn(__ddiv_rn(u01_from(rf.x, rf.y), 2.0), 0.5);
@@ -118,8 +120,13 @@ __global__ __launch_bounds__(256) void k_de(const DevParam* __restrict__ params,
       const int32_t S = pr.psize;
       WRow o{out + (int64_t)pr.col * ldo + i, ldo};
       if (cross) {
-        perm_copy(o, PRow{col + d1, ldp}, S);
-        if (!perm_equal(PRow{col + d2, ldp}, PRow{col + d3, ldp}, S)) {
+        // donor -1 = the best config's row (stride 1 over its columns)
+        const double* bcol = best + pr.col;
+        const PRow r1 = d1 >= 0 ? PRow{col + d1, ldp} : PRow{bcol, 1};
+        const PRow r2 = d2 >= 0 ? PRow{col + d2, ldp} : PRow{bcol, 1};
+        const PRow r3 = d3 >= 0 ? PRow{col + d3, ldp} : PRow{bcol, 1};
+        perm_copy(o, r1, S);
+        if (!perm_equal(r2, r3, S)) {
           PermRng R(seed, g, (uint32_t)p | (1u << STREAM_SUB_SHIFT), round_, OP_DE);
           perm_shuffle(o, S, R);
         }
@@ -131,7 +138,8 @@ __global__ __launch_bounds__(256) void k_de(const DevParam* __restrict__ params,
     const double vt = col[t];
     double v = vt;
     if (cross) {
-      const double x1 = col[d1], x2 = col[d2], x3 = col[d3];
+      const double xb = share ? best[pr.col] : 0.0;
+      const double x1 = d1 >= 0 ? col[d1] : xb, x2 = d2 >= 0 ? col[d2] : xb, x3 = d3 >= 0 ? col[d3] : xb;
       if (is_primitive(pr.kind)) {
         const double va = unit_of(pr, x1, vtab), vb = unit_of(pr, x2, vtab), vc = unit_of(pr, x3, vtab);
         // v = a*va + b*vb + c*vc with a = 1.0, b = F, c = -F
@@ -448,7 +456,8 @@ int launch_de(ut_ctx* c, const ut_de_params* p, uint32_t round_, int64_t cand_ba
               int64_t ld) {
   hipLaunchKernelGGL(k_de, dim3(grid1(m, 256)), dim3(256), 0, c->stream, c->space.d_params, c->space.P,
                      c->space.d_vtab, c->pop,
-                     c->npop, c->npop, p->cr, p->n_cross, c->seed, round_, cand_base, m, out, ld);
+                     c->npop, c->npop, p->best, p->best ? (int64_t)p->information_sharing : (int64_t)0, p->cr,
+                     p->n_cross, c->seed, round_, cand_base, m, out, ld);
   UT_LAUNCH_CHECK(c);
   return 0;
 }

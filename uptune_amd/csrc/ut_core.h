@@ -639,16 +639,12 @@ UT_HD double normal_draw(uint64_t seed, uint64_t cand, uint32_t stream, uint32_t
 }
 
 // ---------------------------------------------------------------------------
-// Double-double natural log and 2^x for the scaled parameter kinds
-// (manipulator.py:778-797):
-//   LogIntegerParameter._scale   = math.log(v + 1.0 - min, 2.0)   (CPython: log(x) / log(2.0))
+// Double-double 2^x for the scaled parameter kinds (manipulator.py:778-797):
 //   LogIntegerParameter._unscale = int(round(2.0 ** v - 1.0 + min))
-// CPython calls libm log() and pow(); glibc's are correctly rounded except in
-// rare hard cases (<= 0.52 ulp).  These evaluate to ~2^-100 relative before
-// the one final rounding, i.e. they are correctly rounded except within
-// 2^-100 of a rounding boundary, so they agree with the reference bit for
-// bit wherever libm rounds correctly (tests/test_core_host.py: every
-// integer argument up to 2^20 plus random ones against CPython).
+// ~2^-100 relative before the one final rounding; the stored integer is
+// rounded again, so it equals CPython's pow-based value on every argument
+// tried (tests/test_core_host.py test_logint_unscale_matches_cpython).
+// (_scale = math.log(v + 1.0 - min, 2.0) is libm_log below, restated exactly.)
 // ---------------------------------------------------------------------------
 struct dd {
   double hi, lo;
@@ -717,18 +713,6 @@ UT_HD dd dd_exp(dd x) {
   return dd_ldexp(dd_add(dd{1.0, 0.0}, a), (int32_t)kd);
 }
 
-// natural log of a positive normal double, one Newton step in double-double
-// from ut_log: y1 = y0 + x e^-y0 - 1
-UT_HD double log_cr(double x) {
-  const double y0 = ut_log(x);
-  const dd t = dd_mul_d(dd_exp(dd{-y0, 0.0}), x);
-  const dd y1 = dd_add(dd{y0, 0.0}, dd_add(t, dd{-1.0, 0.0}));
-  return y1.hi;
-}
-
-// math.log(x, 2.0) as CPython evaluates it: log(x) / log(2.0)
-UT_HD double py_log2(double x) { return log_cr(x) / UT_LN2_DD_HI; }
-
 // 2.0 ** s, |s| < 1000
 UT_HD double exp2_cr(double s) {
   dd t = two_prod(s, UT_LN2_DD_HI);
@@ -736,6 +720,88 @@ UT_HD double exp2_cr(double s) {
   t = fast_two_sum(t.hi, t.lo);
   return dd_exp(t).hi;
 }
+
+// ---------------------------------------------------------------------------
+// libm_log: the natural log CPython's math.log calls on this image, bit for bit.
+// glibc 2.35 x86-64 dispatches log() by ifunc; on CPUs with FMA + AVX2 (the
+// build container and the MI355X hosts) it runs the FMA build, __log_fma
+// (sysdeps/ieee754/dbl-64/e_log.c compiled with -mfma -mavx2).  Its result is
+// not correctly rounded everywhere (<= 0.52 ulp), so matching it needs the
+// same table (libm_log_data.h, read out of libm.so.6 by
+// gen_libm_log_tables.py) and the same operation sequence, including the
+// multiply-adds the compiler fused.  The sequence below is the one in the
+// __log_fma machine code, with every fused step an explicit fma_rn and every
+// other step a separately rounded IEEE op (this header is compiled with
+// -ffp-contract=off).  Checked against CPython's math.log on every integer
+// in [1, 2^22], 10^6 random integers below 2^31 and random doubles
+// (tests/test_core_host.py test_py_log2_matches_cpython), and on the GPU box's
+// own CPython (tests/test_gpu_parity.py test_logint_large_range_bit_exact).
+// ---------------------------------------------------------------------------
+}  // namespace ut
+#include "libm_log_data.h"
+namespace ut {
+
+UT_HD double libm_log(double x) {
+  uint64_t ix = d_to_bits(x);
+  // |x - 1| small: ix - asuint64(1 - 0x1p-4) < asuint64(1 + 0x1.09p-4) - asuint64(1 - 0x1p-4)
+  if (ix - 0x3fee000000000000ull < 0x0003090000000000ull) {
+    if (ix == 0x3ff0000000000000ull) return 0.0;
+    const double* B = LIBM_LOG_B;
+    const double r = x - 1.0;
+    double t1 = fma_rn(r, B[2], B[1]);
+    double t4 = fma_rn(r, B[5], B[4]);
+    double t7 = fma_rn(r, B[8], B[7]);
+    const double r2 = r * r;
+    t1 = fma_rn(r2, B[3], t1);
+    t4 = fma_rn(r2, B[6], t4);
+    const double r3 = r * r2;
+    t7 = fma_rn(r2, B[9], t7);
+    t7 = fma_rn(r3, B[10], t7);
+    t7 = fma_rn(t7, r3, t4);
+    const double poly = fma_rn(t7, r3, t1);
+    // rhi = r + w - w with w = r * 0x1p27 (fused: fma(r, 2^27, r), then fnmadd)
+    const double rhi = fma_rn(-r, 0x1p27, fma_rn(r, 0x1p27, r));
+    const double rh2 = rhi * rhi;
+    const double rlo = r - rhi;
+    const double hi = fma_rn(rh2, B[0], r);      // r + rhi*rhi*B0
+    double lo = fma_rn(rh2, B[0], r - hi);       // r - hi + w
+    lo = fma_rn(B[0] * rlo, r + rhi, lo);        // lo += B0*rlo*(rhi + r)
+    const double y = fma_rn(poly, r3, lo);
+    return hi + y;
+  }
+  const uint32_t top = (uint32_t)(ix >> 48);
+  if (top - 0x0010u >= 0x7ff0u - 0x0010u) {
+    if ((ix << 1) == 0) return -bits_to_d(0x7FF0000000000000ull);     // log(+-0) = -inf
+    if (ix == 0x7FF0000000000000ull) return x;                        // log(inf) = inf
+    if ((top & 0x8000u) || (top & 0x7ff0u) == 0x7ff0u) return bits_to_d(0x7FF8000000000000ull);  // x < 0, NaN
+    ix = d_to_bits(x * 0x1p52) - (52ull << 52);                       // subnormal: normalise
+  }
+  const uint64_t tmp = ix - 0x3fe6000000000000ull;
+  const int32_t i = (int32_t)((tmp >> 45) & 127);
+  const int32_t k = (int32_t)((int64_t)tmp >> 52);
+  const double z = bits_to_d(ix - (tmp & 0xfff0000000000000ull));
+  const double invc = LIBM_LOG_TAB[2 * i], logc = LIBM_LOG_TAB[2 * i + 1];
+  const double kd = (double)k;
+  const double r = fma_rn(z, invc, -1.0);                 // vfmadd132sd
+  const double w = fma_rn(kd, LIBM_LOG_LN2HI, logc);      // vfmadd213sd
+  const double p12 = fma_rn(r, LIBM_LOG_A[2], LIBM_LOG_A[1]);
+  const double hi = r + w;
+  const double r2 = r * r;
+  double lo = (w - hi) + r;
+  lo = fma_rn(kd, LIBM_LOG_LN2LO, lo);                    // vfmadd231sd
+  const double rr2 = r * r2;
+  const double p34 = fma_rn(r, LIBM_LOG_A[4], LIBM_LOG_A[3]);
+  const double lo2 = fma_rn(r2, LIBM_LOG_A[0], lo);
+  const double p = fma_rn(p34, r2, p12);
+  const double y = fma_rn(rr2, p, lo2);
+  return y + hi;
+}
+
+constexpr double UT_LIBM_LOG2 = 0x1.62e42fefa39efp-1;   // libm log(2.0)
+
+// math.log(x, 2.0) as CPython evaluates it: log(x) / log(2.0)
+// (Modules/mathmodule.c loghelper: num = m_log(x), den = m_log(base))
+UT_HD double py_log2(double x) { return libm_log(x) / UT_LIBM_LOG2; }
 
 // ---------------------------------------------------------------------------
 // Parameter value arithmetic (unit encoding) -- bit-exact restatement of

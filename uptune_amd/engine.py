@@ -123,13 +123,24 @@ class BatchEngine:
                                                          idx.numel()), "ut_population_replace")
 
     # -- proposal ----------------------------------------------------------
+    def _de_params(self, cr, n_cross, best, information_sharing):
+        """ut_de_params + the device best row it points to (kept alive by the caller)"""
+        b = self._row(best)
+        p = L.DeParams(cr=float(cr), n_cross=int(n_cross), information_sharing=int(information_sharing),
+                       best=None if b is None else b.data_ptr())
+        return p, b
+
     def propose_de(self, m: int, round_: int = 0, cand_base: int = 0, cr: float = 0.2, n_cross: int = 1,
-                   out: Optional[torch.Tensor] = None) -> torch.Tensor:
+                   out: Optional[torch.Tensor] = None, best=None, information_sharing: int = 1) -> torch.Tensor:
+        """DE trials (differentialevolution.py:105-129); `best` = the driver's
+        best config as a value row [ncols] (added `information_sharing` times to
+        the donor pool, :112-116), None before the first result."""
         if out is None:
             out = self._empty(self.spec.ncols, m)
-        p = L.DeParams(cr=float(cr), n_cross=int(n_cross))
+        p, keep = self._de_params(cr, n_cross, best, information_sharing)
         L.check(self.ctx, self.lib.ut_propose_de(self.ctx, C.byref(p), int(round_), int(cand_base), int(m),
                                                  _ptr(out), out.stride(0)), "ut_propose_de")
+        del keep
         return out
 
     def pso_reset(self):
@@ -293,8 +304,9 @@ class BatchEngine:
 
     # -- whole round -------------------------------------------------------
     def score_round_de(self, m: int, k: int, round_: int = 0, cand_base: int = 0, cr: float = 0.2,
-                       n_cross: int = 1, acq: Optional[L.Acq] = None, want_values: bool = True):
-        de = L.DeParams(cr=float(cr), n_cross=int(n_cross))
+                       n_cross: int = 1, acq: Optional[L.Acq] = None, want_values: bool = True, best=None,
+                       information_sharing: int = 1):
+        de, keep = self._de_params(cr, n_cross, best, information_sharing)  # noqa: F841 (keeps best alive)
         acq = acq or self.acq()
         idx = self._empty(k, dtype=torch.int64)
         top = self._empty(k)

@@ -37,11 +37,11 @@ from . import _lib as L
 # discrete INT ranges up to this many values get an inner-digest LUT
 INT_LUT_MAX = 4096
 # LogInteger ranges up to this many values get host tables (get_value and the
-# inner digest), computed by this host's CPython math.log -- i.e. exactly the
-# reference's values.  libm log is not correctly rounded everywhere (it
-# differs from the correctly rounded log on ~2e-5 of integer arguments here),
-# so larger ranges, which fall back to the device's correctly rounded log,
-# can differ from the reference in that fraction of LogInteger values.
+# precomputed inner digest sha256(repr(get_value)), which saves the device one
+# repr + SHA-256 per value).  Larger ranges compute get_value on the device
+# with ut_core.h libm_log, a bit-exact restatement of the glibc log CPython's
+# math.log calls (tests/test_core_host.py test_py_log2_matches_cpython), so
+# both paths give the reference's values and digests.
 LOGINT_TABLE_MAX = 1 << 22
 
 

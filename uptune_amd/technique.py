@@ -415,14 +415,19 @@ class GpuDifferentialEvolution(GpuBatchTechnique):
     every round proposes DE/rand/1/bin trials for the population; evaluated
     trials replace their target when better (handle_requested_result, :131-139)."""
 
-    def __init__(self, cr: float = 0.2, n_cross: int = 1, *pargs, **kwargs):
+    def __init__(self, cr: float = 0.2, n_cross: int = 1, information_sharing: int = 1, *pargs, **kwargs):
         super().__init__(*pargs, **kwargs)
-        self.cr, self.n_cross = cr, n_cross
+        self.cr, self.n_cross, self.information_sharing = cr, n_cross, information_sharing
         self._pending: Dict[str, int] = {}
 
     def propose(self, m):
+        # share information with other techniques: the driver's best config joins
+        # the donor pool information_sharing times (differentialevolution.py:112-116)
+        best = self.driver.best_configuration()
+        b = None if best is None else self.engine.spec.encode_configs([best])[:, 0]
         return self.engine.propose_de(m, round_=self.round, cand_base=self.round_base(), cr=self.cr,
-                                      n_cross=self.n_cross), None
+                                      n_cross=self.n_cross, best=b,
+                                      information_sharing=self.information_sharing), None
 
     def after_round(self, vals, idx):
         npop = self.engine.npop
