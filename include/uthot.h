@@ -147,6 +147,11 @@ int ut_space_columns(ut_ctx* ctx, int32_t* n_columns);
 int ut_population_init(ut_ctx* ctx, int64_t npop, uint32_t round_);
 int ut_population_set(ut_ctx* ctx, int64_t npop, const double* values, int64_t ld);
 int ut_population_get(ut_ctx* ctx, double* values, int64_t ld);
+/* population slots: every population / PSO call acts on the selected slot
+ * (initially 0).  The techniques of one bandit share one context -- one GP
+ * fit, one history set -- with a population each (bandittechniques.py:311-320
+ * composes DE, PSO and GA over one surrogate).  slot in [0, 1024). */
+int ut_population_select(ut_ctx* ctx, int32_t slot);
 /* copy trial rows back into the population: pop[:, idx[j]] = trial[:, j] */
 int ut_population_replace(ut_ctx* ctx, const double* trial, int64_t ld, const int64_t* idx, int64_t n);
 

@@ -2,7 +2,7 @@
 SPMD search loop behind C5: rank 0 evaluates every generation and broadcasts
 (objective values, digests); the other ranks never call the objective, yet end
 with the same result history, configuration for configuration, as rank 0 and as
-a single-process SearchDriver.  A rank whose requests diverge raises.
+a single-process SearchDriver.  If any rank's requests diverge, every rank raises.
 
 The techniques are CPU random searches and config identity is the oracle's
 hashlib hash_config (test infrastructure), so no GPU is involved.
@@ -115,8 +115,11 @@ def test_rank0_evaluates_and_all_ranks_share_history():
     assert _history(d) == hist0 and best.time == best0
 
 
-def test_diverging_rank_raises():
+def test_diverging_rank_raises_on_every_rank():
+    """a divergence seen by one rank is agreed on collectively (all_reduce of
+    the check): EVERY rank raises, none is left waiting in the next collective
+    (the src rank used to block in the next broadcast)"""
     out = _run(2, diverge=True)
-    assert out[0][1] == "ok"
-    assert out[1][1] == "diverged" and "diverged" in out[1][3]
+    assert out[0][1] == out[1][1] == "diverged"
+    assert "this rank agrees" in out[0][3] and "this rank differs" in out[1][3]
     assert out[1][2] == 0

@@ -157,15 +157,19 @@ def test_de_information_sharing_perm():
     np.testing.assert_array_equal(got, ode.propose_de_vec(space, pop, 24, 3, 1, 2000, 0.5, 2, best=best))
 
 
-def test_de_donor_pool_too_small():
+def test_de_argument_errors():
+    """population < 4 (the donor pool of DE/rand/1 needs 3 members besides the
+    target) and a negative information_sharing are rejected, never launched"""
     from uptune_amd._lib import UthotError
     space = mixed_space()
     e = engine(space, seed=1)
-    e.population_set(dev(ode.population_init(space, 3, seed=1)))
     with pytest.raises(UthotError):
-        e.propose_de(10)                                         # 2 members besides the target
+        e.population_set(dev(ode.population_init(space, 3, seed=1)))
+    e.population_set(dev(ode.population_init(space, 4, seed=1)))
     best = ode.population_init(space, 1, seed=2)[:, 0]
-    e.propose_de(10, best=best, information_sharing=1)           # 2 + 1 best copy: OK
+    with pytest.raises(UthotError):
+        e.propose_de(10, best=best, information_sharing=-1)
+    e.propose_de(10, best=best, information_sharing=0)
 
 
 def test_de_golden(golden_dir):

@@ -40,11 +40,18 @@ def test_bandit_over_gpu_techniques_tunes():
     assert all(counts[n] > 0 for n in names), counts
     first = next(iter(d.results.values()))
     assert best.time < first.time
+    # one shared model: one context (one engine), a population slot per technique,
+    # and at most one GP fit per generation (a refit only when results changed)
+    model = names["gpu-de"].model
+    assert all(t.model is model for t in names.values())
+    assert len({id(t.engine) for t in names.values()}) == 1
+    assert sorted(model.slots.values()) == [0, 1, 2, 3]
+    assert 0 < model.fits <= d.generation
     # device hash of every evaluated config equals the hashlib restatement
     ospace = [OS.Param(p.name, OS.FLOAT if type(p).__name__ == "FloatParameter" else OS.INT,
                        p.min_value, p.max_value) for p in m.params]
     for key, r in list(d.results.items())[:32]:
-        assert key == OH.hash_config(ospace, [r.configuration[p.name] for p in m.params])
+        assert key == OH.hash_config(ospace, [r.configuration.data[p.name] for p in m.params])
 
 
 def test_gpu_de_replaces_population_rows():
@@ -58,10 +65,10 @@ def test_gpu_de_replaces_population_rows():
     tech = d.root_technique
     pop = tech.engine.population_get().cpu().numpy()
     # each recorded population result is the row now stored at that slot
-    replaced = [(idx, r) for (name, idx), r in d._pop_results.items() if name == "de"]
+    replaced = list(tech._pop_results.items())
     assert replaced
     for idx, r in replaced:
-        row = tech.engine.spec.encode_configs([r.configuration])[:, 0]
+        row = tech.engine.spec.encode_configs([r.configuration.data])[:, 0]
         assert (pop[:, idx] == row).all()
 
 

@@ -1,0 +1,120 @@
+"""The reference-side binding (uptune_amd/refbinding.py)
+driven by a stand-in of the reference's own driver and technique module
+(tests/_refstandin.py: the reference SearchDriver / DriverBase / SearchTechnique
+surface, technique.py:70-111, driver.py:130-281, driverbase.py:24-47), with the
+device engine replaced by the oracle-backed CPU engine (tests/_oracle_engine.py).
+tests/test_gpu_refbinding.py runs the same scenarios on the real device path.
+
+VERDICT r1 (missing #1): the round-1 binding resolved desired_result to
+uptune_amd's own and called driver methods the reference does not have; every
+request raised.  Here every registered technique must produce requests through
+the REFERENCE's desired_result, read results via result.configuration.data,
+and never request a configuration twice.
+"""
+import pytest
+
+import _refstandin as R
+from _oracle_engine import OracleEngine
+from uptune_amd import refbinding
+from uptune_amd import technique as T
+from uptune_amd.manipulator import (BooleanParameter, ConfigurationManipulator, EnumParameter, FloatParameter,
+                                    IntegerParameter)
+
+
+def _mirror():
+    return ConfigurationManipulator([FloatParameter("x", -2.0, 2.0), FloatParameter("y", -2.0, 2.0),
+                                     IntegerParameter("n", 0, 50), EnumParameter("mode", ["a", "b", "c"]),
+                                     BooleanParameter("flag")])
+
+
+def _obj(cfg):
+    x, y = cfg["x"], cfg["y"]
+    return (100.0 * (y - x * x) ** 2 + (x - 1.0) ** 2 + 0.01 * abs(cfg["n"] - 17)
+            + (0.5 if cfg["mode"] != "b" else 0.0) + (0.25 if cfg["flag"] else 0.0))
+
+
+KW = dict(pool=512, batch=4, population=64, seed=5, lengthscale=0.5)
+
+
+@pytest.fixture()
+def registry():
+    R.the_registry.clear()
+    ts = refbinding.register_all(R, bandit_cls=T.AUCBanditMetaTechnique, engine_factory=OracleEngine, **KW)
+    yield ts
+    R.the_registry.clear()
+
+
+def _run(tech, generations=6, parallelism=4):
+    m = R.Manipulator(_mirror())
+    d = R.SearchDriver(m, tech, parallelism=parallelism)
+    d.main(_obj, test_limit=generations * parallelism)
+    return d
+
+
+def test_register_all_wraps_every_technique(registry):
+    assert R.the_registry == registry and len(registry) == 22
+    for t in registry[:-1]:
+        assert isinstance(t, R.SearchTechnique)                       # the reference's class
+        assert t.desired_result.__func__ is R.SearchTechnique.desired_result
+        assert isinstance(t.gpu, T.GpuBatchTechnique)
+    bandit = registry[-1]
+    assert bandit.name == "GPU_PSO_GA_DE"
+    assert all(isinstance(c, R.SearchTechnique) for c in bandit.techniques)
+    models = {id(c.gpu.model) for c in bandit.techniques}
+    assert len(models) == 1                                            # one shared surrogate
+
+
+@pytest.mark.parametrize("name", ["GpuDifferentialEvolutionAlt", "GpuPSO-OX1", "GpuGA-OX3", "GpuGGA",
+                                  "GpuNormalGreedyMutation10", "GPU_PSO_GA_DE"])
+def test_reference_driver_runs_gpu_technique(registry, name, caplog):
+    tech = {t.name: t for t in registry}[name]
+    with caplog.at_level("WARNING"):
+        d = _run(tech)
+    assert "round failed" not in caplog.text
+    assert d.test_count > 20
+    # the reference's row types went through the whole loop
+    assert all(type(dr) is R.DesiredResult and type(dr.configuration) is R.Configuration for dr in d._drs)
+    # requests are unique: the device dedup set is fed from requests_query()
+    hashes = [dr.configuration.hash for dr in d._drs]
+    assert len(hashes) == len(set(hashes))
+    # and every config hash is what the reference manipulator computes
+    for dr in d._drs[:16]:
+        assert dr.configuration.hash == d.manipulator.hash_config(dr.configuration.data)
+    assert d.best_result.time < max(r.time for r in d._results)
+
+
+def test_de_handle_requested_result_reads_orm_rows(registry):
+    """GpuDifferentialEvolution.handle_requested_result gets the reference's
+    Result: result.configuration is a Configuration whose dict is .data; a
+    better trial replaces its target member (differentialevolution.py:131-139)"""
+    de = {t.name: t for t in registry}["GpuDifferentialEvolution"]
+    d = _run(de, generations=5)
+    inner = d.root_technique.gpu
+    assert inner._pop_results                                         # some members were replaced
+    eng = inner.model.engine_for(inner)
+    pop = eng.population_get().numpy()
+    for idx, r in inner._pop_results.items():
+        assert type(r) is R.Result
+        assert (pop[:, idx] == eng.spec.encode_configs([r.configuration.data])[:, 0]).all()
+
+
+def test_shared_model_fits_once_per_generation(registry):
+    """the bandit's four techniques share one engine and refit the GP only
+    when the driver's results changed (north_star C5: a shared surrogate)"""
+    bandit = registry[-1]
+    d = _run(bandit, generations=8)
+    model = d.root_technique.techniques[0].gpu.model
+    eng = model.engine
+    assert all(c.gpu.model is model for c in d.root_technique.techniques)
+    assert sorted(model.slots.values()) == list(range(len(model.slots)))
+    assert 0 < eng.calls["gp_fit"] <= d.generation
+    assert eng.calls["gp_fit"] == model.fits
+
+
+def test_deepcopy_per_driver_keeps_sharing(registry):
+    import copy
+    bandit = registry[-1]
+    b2 = copy.deepcopy(bandit)
+    models = {id(c.gpu.model) for c in b2.techniques}
+    assert len(models) == 1 and b2.techniques[0].gpu.model is not bandit.techniques[0].gpu.model
+    assert b2.techniques[0].gpu.model.engine is None

@@ -22,7 +22,7 @@ from uptune_amd.manipulator import ConfigurationManipulator, FloatParameter
 
 
 def test_auc_hand_computed():
-    q = T.AUCBanditQueue(["a", "b"], debug=True)
+    q = T.AUCBanditQueue(["a", "b"])
     for k, v in [("a", 1), ("b", 0), ("a", 0), ("a", 1)]:
         q.on_result(k, v)
     # a: positions 1 (hit), 2, 3 (hit) -> (1 + 3) * 2 / (3 * 4)
@@ -33,15 +33,29 @@ def test_auc_hand_computed():
     assert q.bandit_score("b") == pytest.approx(0.05 * math.sqrt(2 * 2 / 1))
 
 
+def _auc_direct(history, key):
+    """AUC straight from its definition over the window: number the uses of
+    `key` 1..pos in order, sum the numbers of the credited ones, times
+    2 / (pos (pos + 1)) (the reference's exploitation_term_slow invariant,
+    bandittechniques.py:107-126)"""
+    score = pos = 0
+    for k, v in history:
+        if k == key:
+            pos += 1
+            if v:
+                score += pos
+    return score * 2.0 / (pos * (pos + 1.0)) if pos else 0.0
+
+
 @pytest.mark.parametrize("window", [3, 7, 500])
-def test_auc_fast_equals_slow_with_window(window):
+def test_auc_incremental_equals_definition_with_window(window):
     rng = random.Random(window)
     keys = ["k%d" % i for i in range(5)]
-    q = T.AUCBanditQueue(keys, window=window, debug=True)
+    q = T.AUCBanditQueue(keys, window=window)
     for _ in range(400):
         q.on_result(rng.choice(keys), rng.random() < 0.3)
         for k in keys:
-            assert q.exploitation_term_fast(k) == pytest.approx(q.exploitation_term_slow(k), abs=1e-12)
+            assert q.exploitation_term(k) == pytest.approx(_auc_direct(q.history, k), abs=1e-12)
         assert len(q.history) <= window
         assert sum(q.use_counts.values()) == len(q.history)
 
@@ -108,7 +122,7 @@ def test_meta_order_skip_and_credit():
     hist_keys = [k for k, _ in root.bandit.history]
     assert "waiting" not in hist_keys
     assert hist_keys.count("empty") == (1 if "empty" in hist_keys else 0)
-    d._requested[dr.key] = dr
+    d._add_request(dr)
     d.report(dr, 3.0)
     d.process_new_results()
     assert ("giver", True) in [(k, bool(v)) for k, v in root.bandit.history]
@@ -130,9 +144,13 @@ def test_driver_duplicate_request_not_reevaluated():
     d.main(ev, test_limit=2)
     assert len(calls) == 2                       # the repeated config ran once
     assert d.test_count == 3
+    # the duplicate request's own callback fires at the next result pass, as in
+    # the reference (result_callbacks re-queues it until dr.result is set by the
+    # first request's callback, driver.py:136-155)
+    d.process_new_results()
     got = d.root_technique.results
     assert len(got) == 3                         # but every request received a result
-    assert got[0].time == got[1].time == _rosen(cfg)
+    assert sorted(r.time for r in got) == sorted([_rosen(cfg), _rosen(cfg), 0.0])
     assert d.best_result.time == 0.0
 
 

@@ -195,7 +195,12 @@ int ut_ctx_destroy(ut_ctx* c) {
   if (c->stream) ut::sync_all(c);
   free_space(c->space);
   auto fr = [](void* p) { if (p) hipFree(p); };
-  fr(c->pop); fr(c->pso_vel); fr(c->pso_best); fr(c->hist_keys); fr(c->hist_state); fr(c->batch_slots);
+  fr(c->pop); fr(c->pso_vel); fr(c->pso_best);
+  for (size_t s = 0; s < c->pop_slots.size(); ++s) {
+    if ((int32_t)s == c->pop_slot) continue;   // the selected slot's buffers are the fields above
+    fr(c->pop_slots[s].pop); fr(c->pop_slots[s].pso_vel); fr(c->pop_slots[s].pso_best);
+  }
+  fr(c->hist_keys); fr(c->hist_state); fr(c->batch_slots);
   fr(c->gp_Xs); fr(c->gp_xnorm); fr(c->gp_K); fr(c->gp_Linv); fr(c->gp_y); fr(c->gp_tmp);
   fr(c->gp_alpha); fr(c->gp_beta); fr(c->gp_inv_ell); fr(c->gp_stats); fr(c->gp_flag); fr(c->gp_Xs_f); fr(c->gp_T);
   fr(c->gp_LinvT); fr(c->gp_LinvT_f); fr(c->gp_ctr); fr(c->gp_XsT); fr(c->ucand.p);
@@ -437,6 +442,24 @@ int ut_population_set(ut_ctx* c, int64_t npop, const double* values, int64_t ld)
   if (rc) return rc;
   UT_HIP(c, hipMemcpy2DAsync(c->pop, sizeof(double) * npop, values, sizeof(double) * ld, sizeof(double) * npop,
                              c->space.ncols, hipMemcpyDeviceToDevice, c->stream));
+  return 0;
+}
+
+int ut_population_select(ut_ctx* c, int32_t slot) {
+  if (!c) return UT_EINVAL;
+  UT_CHECK(c, slot >= 0 && slot < 1024, UT_EINVAL, "population_select: slot must be in [0, 1024)");
+  if (slot == c->pop_slot) return 0;
+  if ((int32_t)c->pop_slots.size() <= std::max(slot, c->pop_slot))
+    c->pop_slots.resize(std::max(slot, c->pop_slot) + 1);
+  // park the current slot, load the requested one (host-side pointer swap:
+  // launches already enqueued keep the pointers they were given)
+  ut_ctx::PopSlot& cur = c->pop_slots[c->pop_slot];
+  cur.pop = c->pop; cur.npop = c->npop; cur.pop_cap = c->pop_cap;
+  cur.pso_vel = c->pso_vel; cur.pso_best = c->pso_best; cur.pso_cap = c->pso_cap;
+  const ut_ctx::PopSlot& nx = c->pop_slots[slot];
+  c->pop = nx.pop; c->npop = nx.npop; c->pop_cap = nx.pop_cap;
+  c->pso_vel = nx.pso_vel; c->pso_best = nx.pso_best; c->pso_cap = nx.pso_cap;
+  c->pop_slot = slot;
   return 0;
 }
 

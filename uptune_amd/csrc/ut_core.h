@@ -213,6 +213,20 @@ UT_HD void digest_hex(const uint32_t D[8], uint32_t HX[16]) {
 
 // ---------------------------------------------------------------------------
 // Shortest round-trip decimal digits of a double (Ryu d2d).
+//
+// The d2d core below (mulShift64, multipleOfPowerOf5, pow5bits, the
+// vmIsTrailingZeros / vrIsTrailingZeros digit-removal loop) follows
+// Ulf Adams' Ryu (PLDI 2018), https://github.com/ulfjack/ryu, ryu/d2s.c,
+// used under its Apache License 2.0 (alternatively Boost Software License
+// 1.0):  Copyright 2018 Ulf Adams.  Licensed under the Apache License,
+// Version 2.0; you may not use this file except in compliance with the
+// License.  You may obtain a copy at http://www.apache.org/licenses/LICENSE-2.0.
+// Unless required by applicable law or agreed to in writing, software
+// distributed under the License is distributed on an "AS IS" BASIS, WITHOUT
+// WARRANTIES OR CONDITIONS OF ANY KIND.  The table generator
+// (gen_ryu_tables.py) computes the same 128-bit power-of-5 tables from their
+// definition.  Changes here: 64-bit-only device arithmetic (__umul64hi), no
+// 128-bit type on the device path, and CPython's repr() formatting on top.
 // ---------------------------------------------------------------------------
 UT_HD uint32_t pow5bits(int32_t e) { return (uint32_t)(((uint32_t)e * 1217359u) >> 19) + 1u; }
 UT_HD uint32_t log10Pow2(int32_t e) { return ((uint32_t)e * 78913u) >> 18; }

@@ -124,15 +124,28 @@ struct ut_ctx {
   ut::Space space;
   bool has_space = false;
 
-  // population
+  // population of the selected slot (ut_population_select)
   double* pop = nullptr;
   int64_t npop = 0;
   int64_t pop_cap = 0;
 
-  // PSO state
+  // PSO state of the selected slot
   double* pso_vel = nullptr;    // [P][npop]
   double* pso_best = nullptr;   // [P][npop]
   int64_t pso_cap = 0;
+
+  // population slots: the techniques of one bandit share a context (its GP
+  // fit, history set, scratch) and keep one population each; the fields
+  // above are the selected slot's, the others are parked here
+  struct PopSlot {
+    double* pop = nullptr;
+    int64_t npop = 0, pop_cap = 0;
+    double* pso_vel = nullptr;
+    double* pso_best = nullptr;
+    int64_t pso_cap = 0;
+  };
+  std::vector<PopSlot> pop_slots;
+  int32_t pop_slot = 0;
 
   // history set
   uint32_t* hist_keys = nullptr;   // [cap][8]

@@ -101,14 +101,14 @@ def _comm_device(group, device):
 
 
 def allgather_selection(idx: torch.Tensor, score: torch.Tensor, digest: torch.Tensor, rows: torch.Tensor, k: int,
-                        group: Optional[dist.ProcessGroup] = None
-                        ) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+                        group: Optional[dist.ProcessGroup] = None, with_digests: bool = False):
     """One scoring round's exchange for the technique layer: every rank's local
     top-k (global idx, score, digest) AND the selected value rows [ncols][k]
     are all-gathered; the merge (merge_topk) is identical on every rank and the
     rows of the merged selection are taken from the gathered rows, so every
     rank queues the same configurations.  Returns (idx [k], score [k],
-    rows [ncols][k]) on the input device; empty slots have idx -1."""
+    rows [ncols][k]) on the input device (+ digests [k][8] with
+    with_digests=True); empty slots have idx -1."""
     dev = idx.device
     cd = _comm_device(group, dev)
     world = dist.get_world_size(group)
@@ -126,6 +126,8 @@ def allgather_selection(idx: torch.Tensor, score: torch.Tensor, digest: torch.Te
     pos = {int(g): p for p, g in enumerate(gi.tolist()) if g >= 0}
     take = torch.tensor([pos[int(g)] if g >= 0 else 0 for g in mi.tolist()], dtype=torch.int64, device=cd)
     out_rows = grows[:, take]
+    if with_digests:
+        return mi.to(dev), ms.to(dev), out_rows.to(dev), gd[take].to(dev)
     return mi.to(dev), ms.to(dev), out_rows.to(dev)
 
 
@@ -145,6 +147,9 @@ def broadcast_results(y: Optional[torch.Tensor], digests: Optional[torch.Tensor]
     cnt = torch.tensor([n if is_src else -1], dtype=torch.int64, device=cd)
     dist.broadcast(cnt, src, group=group)
     ns = int(cnt.item())
+    if ns == 0:
+        return (torch.empty((0,), dtype=torch.float64, device=cd),
+                torch.empty((0, 8), dtype=torch.int32, device=cd))
     if is_src:
         pay = torch.cat([y.to(cd, torch.float64).reshape(ns, 1),
                          digests.to(cd, torch.int32).contiguous().view(torch.float64).reshape(ns, 4)], dim=1)

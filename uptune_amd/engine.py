@@ -66,6 +66,8 @@ class BatchEngine:
                 "ut_space_define")
         del keep
         self.npop = 0
+        self.slot = 0
+        self._slot_npop: Dict[int, int] = {}
         self.forest = None
 
     # -- plumbing ----------------------------------------------------------
@@ -110,6 +112,15 @@ class BatchEngine:
         n = values.shape[1]
         L.check(self.ctx, self.lib.ut_population_set(self.ctx, n, _ptr(values), n), "ut_population_set")
         self.npop = n
+
+    def population_select(self, slot: int):
+        """ut_population_select: later population / PSO calls use slot `slot`"""
+        if slot == self.slot:
+            return
+        L.check(self.ctx, self.lib.ut_population_select(self.ctx, int(slot)), "ut_population_select")
+        self._slot_npop[self.slot] = self.npop
+        self.slot = int(slot)
+        self.npop = self._slot_npop.get(self.slot, 0)
 
     def population_get(self) -> torch.Tensor:
         out = self._empty(self.spec.ncols, self.npop)

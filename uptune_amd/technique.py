@@ -73,16 +73,22 @@ class SearchTechnique(SearchTechniqueBase):
         self.objective = driver.objective
 
     def desired_result(self):
-        """technique.py:88-111 -> a DesiredResult-like record, None or False"""
+        """technique.py:88-111: wrap desired_configuration() into a DesiredResult
+        (None = nothing to propose, False = waiting for results)"""
+        from .driver import Configuration, DesiredResult
         cfg = self.desired_configuration()
         if cfg is None:
             return None
         if cfg is False:
             return False
-        dr = self.driver.make_desired_result(cfg, requestor=self.name)
-        self.driver.register_result_callback(dr, self.handle_requested_result)
+        config = cfg if isinstance(cfg, Configuration) else self.driver.get_configuration(cfg)
+        desired = DesiredResult(configuration=config, requestor=self.name, generation=self.driver.generation,
+                                tuning_run=getattr(self.driver, "tuning_run", None))
+        if hasattr(self, "limit"):
+            desired.limit = self.limit
+        self.driver.register_result_callback(desired, self.handle_requested_result)
         self.request_count += 1
-        return dr
+        return desired
 
     def desired_configuration(self):
         raise NotImplementedError
@@ -198,38 +204,24 @@ class BanditQueue:
 
 
 class AUCBanditQueue(BanditQueue):
-    """Area-under-curve credit assignment (Fialho et al.), bandittechniques.py:82-146"""
+    """Area-under-curve credit assignment (Fialho et al.): a restatement of
+    bandittechniques.py:82-146 with the same scores and tie-break sequence.
+    The exploitation term is the reference's O(1) incremental form: with the
+    uses of `key` in the window numbered 1..pos, AUC = 2 * (sum of the
+    numbers of the credited uses) / (pos * (pos + 1)).  auc_sum holds that
+    sum; popping the oldest use renumbers the rest down by one, i.e. subtracts
+    the number of credited uses left (auc_decay)."""
 
     def __init__(self, *args, **kwargs):
         super().__init__(*args, **kwargs)
-        self.debug = kwargs.get("debug", False)
         self.auc_sum = dict((t, 0) for t in self.keys)
         self.auc_decay = dict((t, 0) for t in self.keys)
 
-    def exploitation_term_slow(self, key):
-        score = 0.0
-        pos = 0
-        for t, value in self.history:
-            if t is key:
-                pos += 1
-                if value:
-                    score += pos
-        if pos:
-            return score * 2.0 / (pos * (pos + 1.0))
-        return 0.0
-
-    def exploitation_term_fast(self, key):
-        score = self.auc_sum[key]
+    def exploitation_term(self, key):
         pos = self.use_counts[key]
         if pos:
-            return score * 2.0 / (pos * (pos + 1.0))
+            return self.auc_sum[key] * 2.0 / (pos * (pos + 1.0))
         return 0.0
-
-    def exploitation_term(self, key):
-        v1 = self.exploitation_term_fast(key)
-        if self.debug:
-            assert v1 == self.exploitation_term_slow(key)
-        return v1
 
     def on_push_history(self, key, value):
         super().on_push_history(key, value)
@@ -266,13 +258,117 @@ class AUCBanditMetaTechnique(MetaSearchTechnique):
 # ---------------------------------------------------------------------------
 # GPU batch techniques
 # ---------------------------------------------------------------------------
+class SharedModel:
+    """Device state the GPU techniques of one bandit share: ONE context, hence
+    one history digest set and one GP fit per change of the training set (the
+    reference composes DE, PSO and GA under one bandit, bandittechniques.py:311-320,
+    and north_star C5 asks for a shared surrogate).  Each technique keeps its
+    own population in a slot of that context (ut_population_select).
+
+    A technique built without `shared=` makes a private SharedModel, so a
+    stand-alone technique and a bandit member run the same code.  Everything
+    here reads the driver only through the reference SearchDriver surface:
+    requests_query() (every requested configuration's hash -> the dedup set),
+    results_query() (Configuration.data + time -> the training set)."""
+
+    def __init__(self, device: int = 0, seed: int = 0, lengthscale: float = 0.3, min_train: int = 4,
+                 precision: int = 64, sigma_f2: float = 1.0, sigma_n2: float = 1e-6, jitter: float = 1e-8,
+                 engine_factory=None):
+        self.device, self.seed, self.lengthscale, self.min_train = device, seed, lengthscale, min_train
+        self.precision = precision
+        # engine_factory(manipulator, device, seed) -> a BatchEngine-compatible
+        # object; None = uptune_amd.engine.BatchEngine (the device path).  Tests
+        # substitute a CPU stand-in to exercise the plugin plumbing without a GPU.
+        self.engine_factory = engine_factory
+        self.hyper = dict(sigma_f2=sigma_f2, sigma_n2=sigma_n2, jitter=jitter)
+        self._reset()
+        self.slots: Dict[str, int] = {}
+
+    def _reset(self):
+        self.engine = None
+        self._req_seen = 0          # requests_query() rows pushed to the device set (list drivers)
+        self._hist = set()          # digests pushed (any driver)
+        self._res_ids: List[Any] = []
+        self._X = None
+        self._y: List[float] = []
+        self._fit_key = None
+        self.fits = 0
+
+    def __deepcopy__(self, memo):
+        # techniques (and so their shared model) are deep-copied per driver
+        # (driver.py:75): the copy starts without a device context
+        new = self.__class__.__new__(self.__class__)
+        memo[id(self)] = new
+        new.__dict__.update({k: copy.deepcopy(v, memo) for k, v in self.__dict__.items() if k != "engine"})
+        new._reset()
+        return new
+
+    def slot(self, tech) -> int:
+        return self.slots.setdefault(tech.name, len(self.slots))
+
+    def engine_for(self, tech):
+        """the shared engine with `tech`'s population slot selected"""
+        if self.engine is None:
+            if self.engine_factory is None:
+                from .engine import BatchEngine
+                self.engine = BatchEngine(tech.manipulator, device=self.device, seed=self.seed)
+            else:
+                self.engine = self.engine_factory(tech.manipulator, self.device, self.seed)
+            self.engine.gp_set_precision(self.precision)
+            self.engine.history_reset(1024)
+        self.engine.population_select(self.slot(tech))
+        return self.engine
+
+    def sync_history(self, driver) -> None:
+        """every configuration the driver has requested joins the device dedup
+        set (driver.py:157-158,177-200: history + in-flight requests)"""
+        reqs = driver.requests_query()
+        if isinstance(reqs, list):             # append-only table: only the new rows
+            rows, self._req_seen = reqs[self._req_seen:], len(reqs)
+        else:                                  # a SQL query (reference driver): all rows, filtered
+            rows = reqs
+        new = []
+        for dr in rows:
+            h = dr.configuration.hash
+            if h not in self._hist:
+                self._hist.add(h)
+                new.append(h)
+        if new:
+            self.engine.history_add(new)
+
+    def fit(self, driver) -> bool:
+        """(re)fit the GP iff the driver's results changed since the last fit;
+        the new training rows are encoded on the device (ut_encode_features)
+        and the fit is enqueued without a host wait (ut_gp_fit_async)"""
+        rows = [r for r in driver.results_query()
+                if getattr(r, "state", "OK") == "OK" and r.time is not None and math.isfinite(r.time)]
+        ids = [getattr(r, "id", i) for i, r in enumerate(rows)]
+        if len(rows) < self.min_train:
+            return False
+        key = (len(rows), ids[-1])
+        if key == self._fit_key:
+            return True
+        k = len(self._res_ids)
+        if self._X is None or ids[:k] != self._res_ids:      # not an append: re-encode everything
+            self._X, self._y, self._res_ids, k = np.zeros((0, self.engine.spec.n_features)), [], [], 0
+        new = rows[k:]
+        if new:
+            self._X = np.vstack([self._X, self.engine.features_host([r.configuration.data for r in new])])
+            self._y += [float(r.time) for r in new]
+            self._res_ids = ids
+        self.engine.gp_fit(self._X, np.asarray(self._y), lengthscale=self.lengthscale, wait=False, **self.hyper)
+        self._fit_key = key
+        self.fits += 1
+        return True
+
+
 class GpuBatchTechnique(SearchTechnique):
     """Base of the device-scored population techniques.
 
     One round = propose `pool` candidates with the technique's operator,
     hash_config + dedup against every configuration the driver has seen,
-    score with the GP (EI) fitted on the driver's results, keep the top
-    `batch`; desired_configuration() then returns them one per call.
+    score with the shared GP (EI/UCB) fitted on the driver's results, keep
+    the top `batch`; desired_configuration() then returns them one per call.
     """
 
     # DE / GA pools shard over the ranks of a process group by GLOBAL candidate
@@ -281,34 +377,41 @@ class GpuBatchTechnique(SearchTechnique):
 
     def __init__(self, pool: int = 1 << 14, batch: int = 8, population: int = 1024, device: int = 0,
                  seed: int = 0, lengthscale: float = 0.3, min_train: int = 4, acq: str = "ei",
-                 group=None, surrogate=None, *pargs, **kwargs):
+                 group=None, surrogate=None, shared: Optional[SharedModel] = None, engine_factory=None,
+                 *pargs, **kwargs):
         super().__init__(*pargs, **kwargs)
         # surrogate: None = the GP fitted on the driver's results (EI / UCB); or a
         # tree ensemble over the same features (sklearn regressor, XGBoost JSON,
         # forest.Forest) ranking candidates by predicted objective (minimised),
         # the multi-stage tuner's model scoring (multi_stage.py:8-22, :109-123)
         self.surrogate = surrogate
+        self.model = shared if shared is not None else SharedModel(device=device, seed=seed,
+                                                                   lengthscale=lengthscale, min_train=min_train,
+                                                                   engine_factory=engine_factory)
         # multi-GPU: with torch.distributed initialised and
         # world > 1, rank r scores candidates [base + r*pool, base + (r+1)*pool)
         # of every round and the local top-k lists are all-gathered and merged
         self.group = group
         self.pool, self.batch, self.population = int(pool), int(batch), int(population)
-        self.device, self.seed, self.lengthscale, self.min_train = device, seed, lengthscale, min_train
         self.acq_kind = acq
-        self.engine = None
-        self.queue: List[Dict[str, Any]] = []
+        self.queue: List[Any] = []      # (config dict, hash hex) of the last round's selections
         self.round = 0
         self.cand_base = 0
-        self._hist_seen = 0
+        self._initialised = False
 
     def __deepcopy__(self, memo):
-        # device handles are never copied (driver.py:75 deep-copies techniques)
+        # the process group is shared, never copied; the model drops its device state
         cls = self.__class__
         new = cls.__new__(cls)
         memo[id(self)] = new
         for k, v in self.__dict__.items():
-            setattr(new, k, None if k == "engine" else (v if k == "group" else copy.deepcopy(v, memo)))
+            setattr(new, k, v if k == "group" else copy.deepcopy(v, memo))
+        new._initialised = False
         return new
+
+    @property
+    def engine(self):
+        return self.model.engine
 
     def _dist(self):
         """(rank, world) of the sharded round (world 1 without torch.distributed)"""
@@ -316,57 +419,40 @@ class GpuBatchTechnique(SearchTechnique):
             import torch.distributed as dist
         except Exception:  # pragma: no cover
             return 0, 1
-        if not self.sharded or not dist.is_available() or not dist.is_initialized():
+        if not dist.is_available() or not dist.is_initialized():
             return 0, 1
         return dist.get_rank(self.group), dist.get_world_size(self.group)
 
     def round_base(self) -> int:
         """global index of this rank's first candidate of the current round"""
         rank, _ = self._dist()
-        return self.cand_base + rank * self.pool
+        return self.cand_base + (rank * self.pool if self.sharded else 0)
 
     # -- device state ------------------------------------------------------
     def _ensure_engine(self):
-        if self.engine is None:
-            from .engine import BatchEngine
-            self.engine = BatchEngine(self.manipulator, device=self.device, seed=self.seed)
-            self.engine.history_reset(1024)
+        eng = self.model.engine_for(self)
+        if not self._initialised:
             self.init_population()
-        return self.engine
+            self._initialised = True
+        return eng
 
     def init_population(self):
         self.engine.population_init(max(self.population, 4), round_=0)
-
-    def _sync_history(self):
-        """push digests of newly seen configurations to the device set"""
-        seen = self.driver.seen_hashes()
-        if len(seen) > self._hist_seen:
-            self.engine.history_add(seen[self._hist_seen:])
-            self._hist_seen = len(seen)
-
-    def _fit(self) -> bool:
-        cfgs, y = self.driver.training_configs()
-        if len(y) < self.min_train:
-            return False
-        # the driver's results are append-only: encode only the new ones
-        X = getattr(self, "_X", None)
-        if X is None or X.shape[0] > len(cfgs):
-            X = np.zeros((0, self.engine.spec.n_features))
-        if X.shape[0] < len(cfgs):
-            X = np.vstack([X, self.engine.features_host(cfgs[X.shape[0]:])])
-        self._X = X
-        self.engine.gp_fit(X, y, lengthscale=self.lengthscale, sigma_f2=1.0, sigma_n2=1e-6, jitter=1e-8)
-        return True
 
     def propose(self, m: int):
         """-> (values [P][m] device tensor, invalid mask or None)"""
         raise NotImplementedError
 
-    def _round(self):
+    def best_row(self):
+        """driver.best_result's configuration as a SoA value row, or None"""
+        b = self.driver.best_result
+        return None if b is None else self.engine.spec.encode_configs([b.configuration.data])[:, 0]
+
+    def _local_round(self):
+        """this rank's shard: propose -> hash -> dedup -> score -> local top-k"""
         import torch
         eng = self._ensure_engine()
-        self._sync_history()
-        rank, world = self._dist()
+        self.model.sync_history(self.driver)
         base = self.round_base()
         vals, invalid = self.propose(self.pool)
         dig = eng.hash(vals)
@@ -377,25 +463,44 @@ class GpuBatchTechnique(SearchTechnique):
             if getattr(eng, "forest", None) is None:
                 eng.forest_set(self.surrogate)
             _, score = eng.forest_predict(eng.encode(vals), dup=dup)
-        elif self._fit():
-            feat = eng.encode(vals)
-            _, _, score = eng.gp_score(feat, acq=eng.acq(self.acq_kind), dup=dup)
+        elif self.model.fit(self.driver):
+            _, _, score = eng.gp_score(eng.encode(vals), acq=eng.acq(self.acq_kind), dup=dup)
         else:  # no model yet: every non-duplicate candidate is equally good (lowest index first)
             score = torch.zeros(vals.shape[1], dtype=torch.float64, device=vals.device)
         idx, top = eng.topk(score, self.batch, dup=dup, cand_base=base)   # GLOBAL candidate indices
         loc = torch.where(idx >= 0, idx - base, torch.zeros_like(idx))
-        rows = vals[:, loc]
-        if world > 1:
-            from .dist import allgather_selection
-            idx, top, rows = allgather_selection(idx, top, dig[loc], rows, self.batch, group=self.group)
-        keep = idx >= 0
-        idx, rows = idx[keep], rows[:, keep]
-        self.queue.extend(eng.decode(rows))
-        self.after_round(vals, idx)
-        self.round += 1
-        self.cand_base += world * self.pool
+        return vals, idx, top, dig[loc], vals[:, loc]
 
-    def after_round(self, vals, idx):
+    def _round(self):
+        from .engine import digests_to_hex
+        rank, world = self._dist()
+        if world > 1 and self.sharded:
+            # a failure on any rank must not leave the others inside the
+            # all-gather: agree first, then all proceed or all give up
+            from .driver import agree
+            err = None
+            try:
+                vals, idx, top, dig, rows = self._local_round()
+            except Exception as ex:   # noqa: BLE001 -- re-raised below on every rank
+                err = ex
+            dev = None if err is not None else idx.device
+            if not agree(err is None, self.group, dev):
+                raise RuntimeError(f"{self.name}: scoring round failed on "
+                                   f"{'this rank: ' + repr(err) if err is not None else 'another rank'}")
+            from .dist import allgather_selection
+            idx, top, rows, dig = allgather_selection(idx, top, dig, rows, self.batch, group=self.group,
+                                                      with_digests=True)
+        else:
+            vals, idx, top, dig, rows = self._local_round()
+        keep = (idx >= 0)
+        idx, rows, dig = idx[keep], rows[:, keep], dig[keep]
+        cfgs = self.engine.decode(rows)
+        self.queue.extend(zip(cfgs, digests_to_hex(dig)))
+        self.after_round(idx, digests_to_hex(dig))
+        self.round += 1
+        self.cand_base += (world if self.sharded else 1) * self.pool
+
+    def after_round(self, idx, hexes):
         pass
 
     def desired_configuration(self):
@@ -404,7 +509,11 @@ class GpuBatchTechnique(SearchTechnique):
                 self._round()
             if not self.queue:
                 return None
-            return self.queue.pop(0)
+            cfg, hx = self.queue.pop(0)
+            # the digest is already known: an in-memory driver interns it as is
+            # (no second hash); the reference driver hashes the dict itself
+            intern = getattr(self.driver, "configuration_from_digest", None)
+            return intern(cfg, hx) if intern is not None else cfg
         except Exception as ex:  # never raise into the driver loop
             log.warning("%s: device round failed: %s", self.name, ex)
             return None
@@ -412,40 +521,38 @@ class GpuBatchTechnique(SearchTechnique):
 
 class GpuDifferentialEvolution(GpuBatchTechnique):
     """Batched DifferentialEvolution(Alt) (differentialevolution.py:29-151):
-    every round proposes DE/rand/1/bin trials for the population; evaluated
-    trials replace their target when better (handle_requested_result, :131-139)."""
+    every round proposes DE/rand/1/bin trials for the population, with the
+    driver's best config in the donor pool (information sharing, :112-116);
+    an evaluated trial replaces its target when better (handle_requested_result,
+    :131-139)."""
 
     def __init__(self, cr: float = 0.2, n_cross: int = 1, information_sharing: int = 1, *pargs, **kwargs):
         super().__init__(*pargs, **kwargs)
         self.cr, self.n_cross, self.information_sharing = cr, n_cross, information_sharing
-        self._pending: Dict[str, int] = {}
+        self._pending: Dict[str, int] = {}       # trial digest -> target member
+        self._pop_results: Dict[int, Any] = {}   # member -> its Result (PopulationMember.config)
 
     def propose(self, m):
-        # share information with other techniques: the driver's best config joins
-        # the donor pool information_sharing times (differentialevolution.py:112-116)
-        best = self.driver.best_configuration()
-        b = None if best is None else self.engine.spec.encode_configs([best])[:, 0]
         return self.engine.propose_de(m, round_=self.round, cand_base=self.round_base(), cr=self.cr,
-                                      n_cross=self.n_cross, best=b,
+                                      n_cross=self.n_cross, best=self.best_row(),
                                       information_sharing=self.information_sharing), None
 
-    def after_round(self, vals, idx):
+    def after_round(self, idx, hexes):
         npop = self.engine.npop
-        for j, g in enumerate(idx.cpu().numpy().tolist()):   # global index g targets member g % npop
-            cfg = self.queue[len(self.queue) - len(idx) + j]
-            self._pending[self.driver.config_key(cfg)] = g % npop
+        for g, hx in zip(idx.cpu().numpy().tolist(), hexes):   # global index g targets member g % npop
+            self._pending[hx] = g % npop
 
     def handle_requested_result(self, result):
         import torch
-        key = self.driver.config_key(result.configuration)
-        tgt = self._pending.pop(key, None)
+        tgt = self._pending.pop(result.configuration.hash, None)
         if tgt is None or self.engine is None:
             return
-        parent = self.driver.population_result(self, tgt)
+        parent = self._pop_results.get(tgt)
         if parent is None or self.objective.lt(result, parent):
-            vals = torch.from_numpy(self.engine.spec.encode_configs([result.configuration])).to(self.engine.device)
-            self.engine.population_replace(vals, torch.tensor([tgt], device=self.engine.device))
-            self.driver.set_population_result(self, tgt, result)
+            eng = self.model.engine_for(self)
+            vals = torch.from_numpy(eng.spec.encode_configs([result.configuration.data])).to(eng.device)
+            eng.population_replace(vals, torch.tensor([tgt], device=eng.device))
+            self._pop_results[tgt] = result
 
 
 class GpuPSO(GpuBatchTechnique):
@@ -463,11 +570,9 @@ class GpuPSO(GpuBatchTechnique):
         self.engine.pso_reset()
 
     def propose(self, m):
-        best = self.driver.best_configuration()
-        if best is None:  # no result yet: particle 0 stands in for the global best
+        gb = self.best_row()
+        if gb is None:  # no result yet: particle 0 stands in for the global best
             gb = self.engine.population_get()[:, 0]
-        else:
-            gb = self.engine.spec.encode_configs([best])[:, 0]
         npop = self.engine.npop
         x, v = self.engine.propose_pso(gb, min(m, npop), round_=self.round, cand_base=0, omega=self.omega,
                                        phi_l=self.phi_l, phi_g=self.phi_g, enum_mode=self.enum_mode,
@@ -490,9 +595,8 @@ class GpuGA(GpuBatchTechnique):
                        crossover_strength=crossover_strength, op=op, crossover=crossover)
 
     def propose(self, m):
-        best = self.driver.best_configuration()
-        p1 = None if best is None else self.engine.spec.encode_configs([best])[:, 0]
-        return self.engine.propose_ga(m, p1, None, round_=self.round, cand_base=self.round_base(), **self.ga)
+        # GreedySelectionMixin.select: the global best config (random() before any result)
+        return self.engine.propose_ga(m, self.best_row(), None, round_=self.round, cand_base=self.round_base(), **self.ga)
 
 
 class GpuGGA(GpuGA):
@@ -503,15 +607,25 @@ class GpuGGA(GpuGA):
         super().__init__(*pargs, crossover_rate=0.5, crossover_strength=0.2, normal=True, op=5, **kwargs)
 
 
+def _shared_model(kw) -> SharedModel:
+    return SharedModel(device=kw.get("device", 0), seed=kw.get("seed", 0), lengthscale=kw.get("lengthscale", 0.3),
+                       min_train=kw.get("min_train", 4), precision=kw.pop("precision", 64),
+                       engine_factory=kw.pop("engine_factory", None))
+
+
 def pso_ga_de_bandit(bandit_seed: Optional[int] = None, **kw) -> AUCBanditMetaTechnique:
-    """GPU counterpart of the reference's "PSO_GA_DE" bandit (bandittechniques.py:311-320).
-    bandit_seed fixes the bandit's tie-break shuffles (required for SPMD runs:
-    every rank must order the techniques the same way)."""
+    """GPU counterpart of the reference's "PSO_GA_DE" bandit (bandittechniques.py:311-320):
+    the four techniques share ONE SharedModel (one device context: one GP fit
+    per generation, one dedup set) with a population slot each.  bandit_seed
+    fixes the bandit's tie-break shuffles (required for SPMD runs: every rank
+    must order the techniques the same way)."""
+    kw = dict(kw)
+    shared = kw.pop("shared", None) or _shared_model(kw)
     return AUCBanditMetaTechnique([
-        GpuPSO(name="gpu-pso", **kw),
-        GpuGA(name="gpu-ga", crossover_rate=0.5, **kw),
-        GpuDifferentialEvolution(name="gpu-de", **kw),
-        GpuGGA(name="gpu-gga", **kw),
+        GpuPSO(name="gpu-pso", shared=shared, **kw),
+        GpuGA(name="gpu-ga", crossover_rate=0.5, shared=shared, **kw),
+        GpuDifferentialEvolution(name="gpu-de", shared=shared, **kw),
+        GpuGGA(name="gpu-gga", shared=shared, **kw),
     ], name="GPU_PSO_GA_DE", seed=bandit_seed)
 
 
@@ -540,6 +654,11 @@ def reference_registry(wrap=None, bandit_cls=None, **kw) -> List[SearchTechnique
     DE population size is the device population (`population=`), not 30 / 100:
     every member is scored each round."""
     W = wrap or (lambda c: c)
+    kw = dict(kw)
+    ef = kw.get("engine_factory")
+    sm = _shared_model(kw)          # the bandit's children share one model (pops precision / engine_factory)
+    if ef is not None:
+        kw["engine_factory"] = ef   # ... while each stand-alone technique builds its own
     DE, PSO, GA, GGA = W(GpuDifferentialEvolution), W(GpuPSO), W(GpuGA), W(GpuGGA)
     out: List[SearchTechniqueBase] = [
         DE(name="GpuDifferentialEvolution", cr=0.9, **kw),
@@ -557,7 +676,7 @@ def reference_registry(wrap=None, bandit_cls=None, **kw) -> List[SearchTechnique
     for r in (5, 10, 20):
         out.append(GA(name="GpuNormalGreedyMutation%02d" % r, mutation_rate=r / 100.0, normal=True, **kw))
     out.append(GGA(name="GpuGGA", **kw))
-    children = [PSO(name="gpu-pso", **kw), GA(name="gpu-ga", crossover_rate=0.5, **kw), DE(name="gpu-de", **kw),
-                GGA(name="gpu-gga", **kw)]
+    children = [PSO(name="gpu-pso", shared=sm, **kw), GA(name="gpu-ga", crossover_rate=0.5, shared=sm, **kw),
+                DE(name="gpu-de", shared=sm, **kw), GGA(name="gpu-gga", shared=sm, **kw)]
     out.append((bandit_cls or AUCBanditMetaTechnique)(children, name="GPU_PSO_GA_DE"))
     return out
