@@ -13,6 +13,11 @@ Inputs read as DATA from the reference:
     the BLOCK_SIZE whose Python-2-layout hash_config reproduces it.
   * samples/gcc-options/matmul-record.csv  -- recorded gcc-flag configs
     (enum codes 1..3 decoded with the sorted mapping of api.py:296-300).
+  * samples/gcc-options/params.def  -- text; the DEFPARAM(name, desc,
+    default, min, max) records give the integer --param ranges exactly as
+    tune_gcc.py:136-158 extracts them (the same regex, the same three textual
+    substitutions, ast.literal_eval of the literal argument list -- data
+    parsing, no code) and tune_gcc.py:264-282 clamps them (--scaler 4).
 
 Everything else is produced by the oracle (oracle/*) from fixed seeds.
 """
@@ -51,6 +56,33 @@ def tutorial_db():
                   indent=1)
 
 
+def params_def_ranges(scaler=4):
+    """{param: (min, max)} of the gcc --params as tune_gcc.py builds them:
+    defaults from params.def (:136-158), then (:264-282)
+        if max <= min: max = inf
+        max = min(max, max(1, default) * scaler)
+        min = max(min, old_div(max(1, default), scaler))      (ints: floor division)
+    and l1-cache-line-size = 2 ** tune(default, (2, 8)): the tuned (and
+    recorded) value is the exponent in [2, 8]."""
+    import ast
+    import re
+    text = open(os.path.join(REF, "samples/gcc-options/params.def")).read()
+    out = {}
+    for m in re.finditer(r'DEFPARAM *\((([^")]|"[^"]*")*)\)', text):
+        s = (m.group(1).replace("GGC_MIN_EXPAND_DEFAULT", "30").replace("GGC_MIN_HEAPSIZE_DEFAULT", "4096")
+             .replace("50 * 1024 * 1024", "52428800"))
+        try:
+            name, _desc, default, pmin, pmax = ast.literal_eval("[" + s.split(",", 1)[1] + "]")
+        except (ValueError, SyntaxError):
+            continue
+        if pmax <= pmin:
+            pmax = float("inf")
+        pmax = min(pmax, max(1, default) * scaler)
+        pmin = max(pmin, max(1, default) // scaler)
+        out[name] = (2, 8) if name == "l1-cache-line-size" else (int(pmin), int(pmax))
+    return out
+
+
 def gcc_space_and_rows(nrows=512, nhash=64):
     path = os.path.join(REF, "samples/gcc-options/matmul-record.csv")
     with open(path) as f:
@@ -61,6 +93,7 @@ def gcc_space_and_rows(nrows=512, nhash=64):
     idx = [header.index(c) for c in cols]
     data = np.array([[int(float(row[i])) for i in idx] for row in rows], dtype=np.int64)
     opts = ["on", "off", "default"]                 # tune_gcc.py:262 option order
+    ranges = params_def_ranges()
     code = {x + 1: y for x, y in enumerate(sorted(set(opts)))}   # api.py:296-300
     params = []
     spec = []
@@ -72,7 +105,8 @@ def gcc_space_and_rows(nrows=512, nhash=64):
             params.append(Param(c, ENUM, options=list(opts)))
             spec.append(["EnumParameter", c, list(opts)])
         else:
-            lo, hi = int(data[:, j].min()), int(data[:, j].max())
+            lo, hi = ranges[c]
+            assert lo <= data[:, j].min() and data[:, j].max() <= hi, (c, lo, hi)   # recorded configs fit
             params.append(Param(c, INT, lo, hi))
             spec.append(["IntegerParameter", c, [lo, hi]])
     cfgs = []
@@ -93,7 +127,9 @@ def gcc_space_and_rows(nrows=512, nhash=64):
     np.savez_compressed(os.path.join(HERE, "gcc_history.npz"), values=allv.astype(np.float64), qor=qor)
     with open(os.path.join(HERE, "gcc_space.json"), "w") as f:
         json.dump({"params": spec, "enum_code": {str(k): v for k, v in code.items()},
-                   "source": "samples/gcc-options/matmul-record.csv (int ranges = recorded min..max)",
+                   "source": "samples/gcc-options/matmul-record.csv header (-O in [0, 3], 184 flags "
+                             "{on, off, default}); int ranges from samples/gcc-options/params.def via "
+                             "tune_gcc.py:264-282 (scaler 4; l1-cache-line-size = its exponent in [2, 8])",
                    "hashes_py3": hashes}, f)
 
 

@@ -151,6 +151,21 @@ def test_py_log2_matches_cpython(hc):
     assert math.isnan(_batch(hc, "uthc_libm_log", [-1.0])[0])
 
 
+def test_libm_log_fixture_cases(hc):
+    """tests/golden/libm_log_non_cr.json: arguments where glibc's log is not
+    correctly rounded (confirmed here with Decimal); the restatement follows
+    glibc there too"""
+    import json
+    from decimal import Decimal, getcontext
+    getcontext().prec = 60
+    xs = json.load(open(os.path.join(ROOT, "tests", "golden", "libm_log_non_cr.json")))["ints"]
+    assert len(xs) >= 200
+    for x in xs[:40]:
+        assert math.log(x) != float(Decimal(x).ln())
+    got = _batch(hc, "uthc_py_log2", [float(x) for x in xs])
+    assert got.tolist() == [math.log(float(x), 2.0) for x in xs]
+
+
 def test_logint_unscale_matches_cpython(hc):
     """LogIntegerParameter._unscale int(round(2.0 ** v - 1.0 + min))
     (manipulator.py:787-790): the device's correctly rounded 2^v gives the same

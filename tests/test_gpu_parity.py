@@ -487,21 +487,12 @@ def hpl_space():
     return oracle_space(spaces.hpl64())
 
 
-def _non_cr_log_ints(lo, hi, count, seed=5):
-    """integers x in [lo, hi) where CPython's math.log(x) is NOT the correctly
-    rounded log -- the arguments a correctly rounded device log got wrong in
-    round 1 (glibc's log is <= 0.52 ulp, not correctly rounded)"""
-    import math
-    import random
-    from decimal import Decimal, getcontext
-    getcontext().prec = 60
-    rng = random.Random(seed)
-    out = []
-    while len(out) < count:
-        x = rng.randrange(lo, hi)
-        if math.log(x) != float(Decimal(x).ln()):
-            out.append(x)
-    return out
+def _non_cr_log_ints(golden_dir):
+    """integers x in [2^22, 2^31) where CPython's math.log(x) is NOT the
+    correctly rounded log -- the arguments a correctly rounded device log got
+    wrong in round 1 (tests/golden/make_libm_log_cases.py)"""
+    with open(os.path.join(golden_dir, "libm_log_non_cr.json")) as f:
+        return json.load(f)["ints"]
 
 
 def test_hpl_population_de_encode_hash():
@@ -522,7 +513,7 @@ def test_hpl_population_de_encode_hash():
     assert bad == []
 
 
-def test_logint_large_range_bit_exact():
+def test_logint_large_range_bit_exact(golden_dir):
     """LogIntegerParameter over [0, 2^31) (no host table): get_value =
     math.log(v + 1.0 - min, 2.0) restated on the device (ut_core.h libm_log)
     is bit-identical to THIS box's CPython on random values and on integers
@@ -533,7 +524,7 @@ def test_logint_large_range_bit_exact():
     e = engine(space, seed=3)
     assert e.spec.params[0].vtab is None
     rng = np.random.default_rng(11)
-    xs = _non_cr_log_ints(1 << 22, 1 << 31, 300) + [int(v) for v in rng.integers(0, (1 << 31) - 1, 4000)]
+    xs = _non_cr_log_ints(golden_dir) + [int(v) for v in rng.integers(1, (1 << 31) - 1, 4000)]
     vals = np.zeros((2, len(xs)))
     vals[0] = [x - 1 for x in xs]          # v + 1.0 - min = x
     vals[1] = rng.uniform(size=len(xs))
