@@ -49,6 +49,33 @@ def training_set(n, d, seed):
     return X, rosenbrock_decoded(X)
 
 
+def host_info():
+    """CPU model, logical CPUs of the machine, and the threads this job may use
+    (OMP_NUM_THREADS, else the affinity mask: 16 per GPU on the MI355X boxes)"""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:  # pragma: no cover
+        aff = os.cpu_count()
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or aff
+    return {"cpu_model": model, "nproc": os.cpu_count(), "affinity_cpus": aff, "threads": min(threads, aff)}
+
+
+def cpu_baseline_b1(m_sample, n, d, k, threads, seed=1):
+    """B1: the same C2 round vectorised on `threads` host
+    cores -- C++/OpenMP DE + hash_config + dedup, BLAS GP (oracle/cpu_batch.*)"""
+    from oracle import cpu_batch
+    return cpu_batch.b1_baseline(m_sample, n, d, k, seed=seed, threads=threads)
+
+
 def cpu_baseline(m_sample, n, d, k, seed=1):
     """The oracle (CPU restatement of the reference path) on a bounded sample,
     single-threaded like the reference search loop (api.py:428-446)."""
@@ -86,14 +113,17 @@ def cpu_baseline(m_sample, n, d, k, seed=1):
                       f"hash_config + dedup + posterior + EI + top-{k}, 1 thread, {dt:.2f} s"}
 
 
-def load_traffic(kernel_key):
+def load_pmc(kernel_key):
+    """the rocprofv3 record of a kernel (profiles/pmc_summary.json: HBM bytes
+    per launch from the FETCH_SIZE / WRITE_SIZE passes, average duration from
+    the --kernel-trace --stats pass of the same command)"""
     path = os.path.join(ROOT, "profiles", "pmc_summary.json")
     try:
         with open(path) as f:
             d = json.load(f)
-        return d.get(kernel_key, {}).get("hbm_bytes_per_launch")
+        return d.get(kernel_key) or {}, d.get("_note", "")
     except Exception:
-        return None
+        return {}, ""
 
 
 def main():
@@ -105,8 +135,10 @@ def main():
     ap.add_argument("--n", type=int, default=1024, help="GP training points")
     ap.add_argument("--d", type=int, default=64)
     ap.add_argument("--k", type=int, default=256)
-    ap.add_argument("--cpu-sample", type=int, default=81920,
-                    help="candidates in the CPU-baseline sample (about 10 s of single-thread oracle work)")
+    ap.add_argument("--cpu-sample", type=int, default=32768,
+                    help="candidates in the 1-thread oracle baseline sample (about 4 s of single-thread work)")
+    ap.add_argument("--b1-sample", type=int, default=1 << 18,
+                    help="candidates in the B1 batch baseline sample (C++/OpenMP + BLAS on the host cores)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--precision", type=int, default=64, choices=(64, 32, 16),
                     help="GP contractions on fp64 MFMA (1e-5 parity) or fp32 MFMA (1e-3 parity); 16 = f16x3: "
@@ -158,14 +190,20 @@ def main():
     npop = m * world                       # replicated population, deterministic init on every rank
     eng.gp_set_precision(args.precision)
     eng.population_init(npop)
-    eng.history_reset(0)
+    # the results history holds the evaluated configurations: the n training
+    # points (C2/C3) or the 3,680 recorded gcc configs (C4), plus every round's
+    # selections (appended on the device after the round, as an evaluation
+    # would); capacity reserved up front so no growth happens in the timed loop
+    eng.history_reset(4 * (n + 3680 + (args.warmup + args.steps) * k))
     if args.config == "c3":
         # training points: n HPL-64 configs (device op1_randomize), features encoded on
         # the device; synthetic objective = squared distance of the features from 0.3
         d = eng.spec.n_features
         tr = BatchEngine(manip, device=local, seed=101)
         tr.population_init(n)
-        X = tr.encode(tr.population_get()).T.contiguous().cpu().numpy()
+        tv = tr.population_get()
+        X = tr.encode(tv).T.contiguous().cpu().numpy()
+        eng.history_add(eng.hash(tv))
         y = np.sum((X - 0.3) ** 2, axis=1)
         tr.close()
     elif args.config == "c4":
@@ -183,6 +221,8 @@ def main():
         parent = hist[:, int(np.argmin(qor))].copy()
     else:
         X, y = training_set(n, d, 101)
+        hv = torch.from_numpy(np.ascontiguousarray((X * 2000.0 - 1000.0).T)).to(eng.device)   # decoded configs
+        eng.history_add(eng.hash(hv))
     cand_base = rank * m
     acq = eng.acq("ei", xi=0.0)
     ell = {"c2": 0.2, "c3": 1.0, "c4": 2.0}[args.config]
@@ -207,6 +247,7 @@ def main():
         eng.gp_fit(X, y, lengthscale=ell, sigma_f2=1.0, sigma_n2=1e-6, wait=False)   # overlaps propose + hash
         idx, top, dig, _ = eng.score_round_de(m, k, round_=r, cand_base=cand_base, cr=0.2, n_cross=1, acq=acq,
                                               want_values=False)
+        eng.history_add(dig)                              # the selections join the history (device-side)
         if world > 1:
             idx, top = allgather_topk(idx, top, dig, k)   # RCCL all_gather + deterministic merge
         return idx, top
@@ -258,9 +299,12 @@ def main():
         kernel = "k_gp_kstar<double, false> (K* = exp(-|x - u|^2 / 2), v_mfma_f64_16x16x4_f64)"
     achieved = flops_var / (var_ms * 1e-3) / 1e12 if var_ms else None
     peak = {64: PEAK_FP64_TFLOPS, 32: PEAK_FP32_TFLOPS, 16: PEAK_FP16_TFLOPS / 3.0}[args.precision]
-    # HBM bytes per launch were profiled on the default C2 round (profiles/pmc_summary.json)
+    # HBM bytes per launch and the rocprof average duration were profiled on the
+    # default C2 round (profiles/pmc_summary.json)
     profiled = args.config == "c2" and (m, n, d) == (1 << 20, 1024, 64)
-    traffic = load_traffic({64: "var", 32: "var32", 16: "var16"}[args.precision]) if profiled else None
+    pmc, pmc_note = load_pmc({64: "var", 32: "var32", 16: "var16"}[args.precision]) if profiled else ({}, "")
+    traffic = pmc.get("hbm_bytes_per_launch")
+    frac_rocprof = (flops_var / (pmc["avg_ns"] * 1e-9) / 1e12 / peak) if pmc.get("avg_ns") else None
     if args.config == "c4":
         workload = (f"C4 gcc flags (339 params: 1 + 154 Int, 184 Enum{{on,off,default}}; {d} GP features): GA "
                     f"mutation 0.1 from the best recorded config + hash_config + dedup vs 3,680 recorded configs "
@@ -295,14 +339,25 @@ def main():
         "roofline": {"bound": "mfma", "kernel": kernel,
                      "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
                      "frac": (achieved / peak) if achieved else None, "traffic": traffic,
+                     "frac_rocprof": frac_rocprof,
+                     "rocprof_source": ("profiles/pmc_summary.json (" + pmc_note.split("source:")[-1].strip() + ")")
+                     if pmc else None,
                      "flops_per_launch": flops_var},
         "cpu_baseline": None,
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.cpu_sample > 0 and args.config == "c2":
-        try:
-            result["cpu_baseline"] = cpu_baseline(args.cpu_sample, n, d, k)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "c2":
+        host = host_info()
+        result["host"] = host
+        try:       # B1: the batch port on this job's host cores (the stronger CPU baseline)
+            if args.b1_sample > 0:
+                result["cpu_baseline"] = cpu_baseline_b1(args.b1_sample, n, d, k, host["threads"])
         except Exception as ex:  # keep the GPU number even if the baseline fails
             result["cpu_baseline"] = {"error": repr(ex)}
+        try:       # the reference's per-candidate, single-threaded search loop (api.py:428-446)
+            if args.cpu_sample > 0:
+                result["cpu_baseline_1thread"] = cpu_baseline(args.cpu_sample, n, d, k)
+        except Exception as ex:
+            result["cpu_baseline_1thread"] = {"error": repr(ex)}
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:
