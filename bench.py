@@ -216,9 +216,11 @@ def main():
         hv = torch.from_numpy(np.ascontiguousarray(hist)).to(eng.device)
         eng.history_add(eng.hash(hv))
         d = eng.spec.n_features
-        X = eng.encode(hv[:, :n].contiguous()).T.contiguous().cpu().numpy()
-        y = qor[:n].astype(np.float64)
+        ok_rows = torch.from_numpy(np.flatnonzero(np.isfinite(qor))[:n]).to(eng.device)   # 149 runs failed: inf
+        X = eng.encode(hv[:, ok_rows].contiguous()).T.contiguous().cpu().numpy()
+        y = qor[ok_rows.cpu().numpy()].astype(np.float64)
         parent = hist[:, int(np.argmin(qor))].copy()
+        assert np.all(np.isfinite(y)) and X.shape[0] == n
     else:
         X, y = training_set(n, d, 101)
         hv = torch.from_numpy(np.ascontiguousarray((X * 2000.0 - 1000.0).T)).to(eng.device)   # decoded configs

@@ -213,6 +213,13 @@ int ut_encode_features(ut_ctx* ctx, const double* values, int64_t ld, int64_t m,
 
 /* ---- identity + dedup (hash_config, driver.get_configuration) ----------- */
 int ut_hash(ut_ctx* ctx, const double* values, int64_t ld, int64_t m, uint32_t* out_digest);
+/* The same digests for DE trials of the selected population: candidate i's
+ * target is member (cand_base + i) % npop (ut_propose_de).  Inner digests of
+ * values bitwise equal to the target's are taken from a per-population cache
+ * (built on first use, patched by ut_population_replace); only the changed
+ * values are formatted and hashed.  Correct for any values (a value that does
+ * not match its "target" is simply recomputed); fast when most match. */
+int ut_hash_de(ut_ctx* ctx, const double* values, int64_t ld, int64_t m, int64_t cand_base, uint32_t* out_digest);
 int ut_history_reset(ut_ctx* ctx, int64_t capacity);
 int ut_history_add(ut_ctx* ctx, const uint32_t* digests, int64_t n);   /* device [n][8] */
 int ut_history_add_host(ut_ctx* ctx, const uint32_t* digests_host, int64_t n);

@@ -95,6 +95,9 @@ class OracleEngine:
         raw = np.frombuffer(b"".join(bytes.fromhex(h) for h in hx), dtype=">u4").reshape(-1, 8)
         return torch.from_numpy(raw.astype(np.uint32).view(np.int32).copy())
 
+    def hash_de(self, vals, cand_base=0):
+        return self.hash(vals)
+
     def hash_configs(self, cfgs):
         from uptune_amd.engine import digests_to_hex
         return digests_to_hex(self.hash(torch.from_numpy(self.spec.encode_configs(cfgs))))

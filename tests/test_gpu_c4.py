@@ -90,8 +90,9 @@ def _score_and_check(c4, vals, dup, k=64):
     """device GP-EI on the recorded qor vs the oracle; top-k equality"""
     e, space = c4["e"], c4["space"]
     n = 1024
-    X = features(space, c4["hist"][:, :n]).T
-    y = c4["qor"][:n].astype(np.float64)
+    ok_rows = np.flatnonzero(np.isfinite(c4["qor"]))[:n]   # 149 recorded runs failed (qor = inf)
+    X = features(space, c4["hist"][:, ok_rows]).T
+    y = c4["qor"][ok_rows].astype(np.float64)
     e.gp_fit(X, y, lengthscale=2.0, sigma_f2=1.0, sigma_n2=1e-6, jitter=1e-8)
     feat = e.encode(torch.from_numpy(np.ascontiguousarray(vals)).cuda())
     np.testing.assert_array_equal(feat.cpu().numpy(), features(space, vals))

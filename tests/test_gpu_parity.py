@@ -172,6 +172,37 @@ def test_de_argument_errors():
     e.propose_de(10, best=best, information_sharing=0)
 
 
+@pytest.mark.parametrize("which", ["mixed", "r64", "hpl", "perm"])
+def test_hash_de_reuses_population_digests(which):
+    """ut_hash_de (inner digests of values equal to the target member's taken
+    from the population cache) == ut_hash == the oracle, for DE trials, for
+    unrelated values, after ut_population_replace (cache patched per row) and
+    after ut_pso_commit (cache rebuilt)"""
+    space = {"mixed": mixed_space, "r64": r64_space, "hpl": hpl_space, "perm": perm_space}[which]()
+    e = engine(space, seed=31)
+    e.population_init(3000, round_=1)
+    pop = e.population_get().cpu().numpy()
+    m, base = 5000, 1234
+    trial = e.propose_de(m, round_=2, cand_base=base, cr=0.2)
+    want = oracle_hashes(space, trial.cpu().numpy()) if which != "perm" else _row_hashes(space, trial.cpu().numpy())
+    assert hexes(e.hash_de(trial, base)) == want
+    assert hexes(e.hash(trial)) == want
+    # unrelated values (nothing matches a target): every digest is recomputed
+    other = torch.from_numpy(ode.population_init(space, 700, seed=99)).cuda()
+    assert hexes(e.hash_de(other, 0)) == hexes(e.hash(other))
+    # replace some members, then trials of the new population
+    rows = torch.tensor([0, 5, 1233 % 3000, 2999], device="cuda")
+    e.population_replace(other[:, :4].contiguous(), rows)
+    trial2 = e.propose_de(m, round_=3, cand_base=base, cr=0.2)
+    assert hexes(e.hash_de(trial2, base)) == hexes(e.hash(trial2))
+    if which == "r64":   # PSO commit moves positions: the cache is rebuilt
+        e.pso_reset()
+        x, v = e.propose_pso(pop[:, 0].copy(), 3000, round_=1)
+        e.pso_commit(x, v)
+        trial3 = e.propose_de(m, round_=4, cand_base=0, cr=0.2)
+        assert hexes(e.hash_de(trial3, 0)) == hexes(e.hash(trial3))
+
+
 def test_de_golden(golden_dir):
     z = np.load(os.path.join(golden_dir, "de_mixed.npz"))
     e = engine(mixed_space(), seed=11)

@@ -96,6 +96,7 @@ SIGNATURES = {
     "ut_population_get": (C.c_int, [P, P, I64]),
     "ut_population_replace": (C.c_int, [P, P, I64, P, I64]),
     "ut_population_select": (C.c_int, [P, I32]),
+    "ut_hash_de": (C.c_int, [P, P, I64, I64, I64, P]),
     "ut_propose_de": (C.c_int, [P, C.POINTER(DeParams), U32, I64, I64, P, I64]),
     "ut_pso_reset": (C.c_int, [P]),
     "ut_propose_pso": (C.c_int, [P, C.POINTER(PsoParams), P, U32, I64, I64, P, P, I64]),

@@ -69,7 +69,7 @@ static void free_space(Space& s) {
   if (s.d_lut) hipFree(s.d_lut);
   if (s.d_vtab) hipFree(s.d_vtab);
   for (void* q : {(void*)s.d_order_col, (void*)s.d_perm_params, (void*)s.d_perm_bytes, (void*)s.d_perm_off,
-                  (void*)s.d_perm_offbase, (void*)s.d_perm_len})
+                  (void*)s.d_perm_offbase, (void*)s.d_perm_len, (void*)s.d_comp})
     if (q) hipFree(q);
   s = Space();
 }
@@ -196,10 +196,12 @@ int ut_ctx_destroy(ut_ctx* c) {
   free_space(c->space);
   auto fr = [](void* p) { if (p) hipFree(p); };
   fr(c->pop); fr(c->pso_vel); fr(c->pso_best);
+  fr(c->pop_dig);
   for (size_t s = 0; s < c->pop_slots.size(); ++s) {
     if ((int32_t)s == c->pop_slot) continue;   // the selected slot's buffers are the fields above
-    fr(c->pop_slots[s].pop); fr(c->pop_slots[s].pso_vel); fr(c->pop_slots[s].pso_best);
+    fr(c->pop_slots[s].pop); fr(c->pop_slots[s].pso_vel); fr(c->pop_slots[s].pso_best); fr(c->pop_slots[s].pop_dig);
   }
+  fr(c->r_mask.p); fr(c->r_fresh.p); fr(c->r_pairs.p); fr(c->r_npairs.p);
   fr(c->hist_keys); fr(c->hist_state); fr(c->batch_slots);
   fr(c->gp_Xs); fr(c->gp_xnorm); fr(c->gp_K); fr(c->gp_Linv); fr(c->gp_y); fr(c->gp_tmp);
   fr(c->gp_alpha); fr(c->gp_beta); fr(c->gp_inv_ell); fr(c->gp_stats); fr(c->gp_flag); fr(c->gp_Xs_f); fr(c->gp_T);
@@ -249,7 +251,7 @@ int ut_space_define(ut_ctx* c, int32_t P, const ut_param_desc* params, int32_t p
   std::vector<bool> primitive(P);
   std::vector<uint32_t> lut;
   std::vector<double> vtab;
-  std::vector<int32_t> perm_params, perm_off, perm_offbase, perm_len;
+  std::vector<int32_t> perm_params, perm_off, perm_offbase, perm_len, comp;
   std::vector<uint8_t> perm_bytes;
   int32_t feat = 0, col = 0;
   for (int32_t p = 0; p < P; ++p) {
@@ -260,6 +262,8 @@ int ut_space_define(ut_ctx* c, int32_t P, const ut_param_desc* params, int32_t p
     q.psize = 1;
     q.wcol = 0;
     q.pslot = -1;
+    q.cslot = -1;
+    q.pad_ = 0;
     q.lo = d.lo; q.hi = d.hi;
     q.u_lo = d.u_lo; q.u_hi = d.u_hi; q.u_span = d.u_span;
     q.n_opt = d.n_options;
@@ -347,6 +351,8 @@ int ut_space_define(ut_ctx* c, int32_t P, const ut_param_desc* params, int32_t p
       else if (d.kind == UT_INT) q.hash_mode = HM_INT;
       else if (d.kind == UT_LOGINT) q.hash_mode = HM_LOGINT;
       else return set_err(c, UT_EINVAL, "space: BOOL/ENUM/POW2 parameters need an inner-digest LUT");
+      q.cslot = s.n_comp++;
+      comp.push_back(p);
     }
   }
   s.n_feat = feat;
@@ -379,16 +385,22 @@ int ut_space_define(ut_ctx* c, int32_t P, const ut_param_desc* params, int32_t p
     UT_HIP(c, up(s.d_perm_offbase, perm_offbase));
     UT_HIP(c, up(s.d_perm_len, perm_len));
   }
+  if (s.n_comp > 0) {
+    UT_HIP(c, hipMalloc((void**)&s.d_comp, sizeof(int32_t) * comp.size()));
+    UT_HIP(c, hipMemcpy(s.d_comp, comp.data(), sizeof(int32_t) * comp.size(), hipMemcpyHostToDevice));
+  }
   int rc = compile_hash_layout(c, names, primitive);
   if (rc) return rc;
   c->has_space = true;
-  // a new space invalidates the population
+  // a new space invalidates the population (and its digest cache)
   if (c->pop) {
     hipFree(c->pop);
     c->pop = nullptr;
     c->npop = 0;
     c->pop_cap = 0;
   }
+  c->pop_dig_valid = false;
+  for (auto& ps : c->pop_slots) ps.pop_dig_valid = false;
   return 0;
 }
 
@@ -430,6 +442,7 @@ int ut_population_init(ut_ctx* c, int64_t npop, uint32_t round_) {
   UT_CHECK(c, npop >= 4 && npop < (int64_t)0xFFFFFFFF, UT_EINVAL, "population size must be in [4, 2^32)");
   int rc = pop_alloc(c, npop);
   if (rc) return rc;
+  c->pop_dig_valid = false;
   return launch_population_init(c, round_);
 }
 
@@ -440,6 +453,7 @@ int ut_population_set(ut_ctx* c, int64_t npop, const double* values, int64_t ld)
            "population_set: bad arguments");
   int rc = pop_alloc(c, npop);
   if (rc) return rc;
+  c->pop_dig_valid = false;
   UT_HIP(c, hipMemcpy2DAsync(c->pop, sizeof(double) * npop, values, sizeof(double) * ld, sizeof(double) * npop,
                              c->space.ncols, hipMemcpyDeviceToDevice, c->stream));
   return 0;
@@ -456,9 +470,11 @@ int ut_population_select(ut_ctx* c, int32_t slot) {
   ut_ctx::PopSlot& cur = c->pop_slots[c->pop_slot];
   cur.pop = c->pop; cur.npop = c->npop; cur.pop_cap = c->pop_cap;
   cur.pso_vel = c->pso_vel; cur.pso_best = c->pso_best; cur.pso_cap = c->pso_cap;
+  cur.pop_dig = c->pop_dig; cur.pop_dig_cap = c->pop_dig_cap; cur.pop_dig_valid = c->pop_dig_valid;
   const ut_ctx::PopSlot& nx = c->pop_slots[slot];
   c->pop = nx.pop; c->npop = nx.npop; c->pop_cap = nx.pop_cap;
   c->pso_vel = nx.pso_vel; c->pso_best = nx.pso_best; c->pso_cap = nx.pso_cap;
+  c->pop_dig = nx.pop_dig; c->pop_dig_cap = nx.pop_dig_cap; c->pop_dig_valid = nx.pop_dig_valid;
   c->pop_slot = slot;
   return 0;
 }
@@ -499,6 +515,14 @@ int ut_hash(ut_ctx* c, const double* values, int64_t ld, int64_t m, uint32_t* ou
   UT_CHECK(c, c->has_space, UT_ENOSPACE, "space not defined");
   UT_CHECK(c, m >= 0 && ((values && out) || m == 0) && ld >= m, UT_EINVAL, "hash: bad arguments");
   return launch_hash(c, values, ld, m, out);
+}
+
+int ut_hash_de(ut_ctx* c, const double* values, int64_t ld, int64_t m, int64_t cand_base, uint32_t* out) {
+  if (!c) return UT_EINVAL;
+  UT_CHECK(c, c->has_space, UT_ENOSPACE, "space not defined");
+  UT_CHECK(c, c->pop != nullptr, UT_EINVAL, "hash_de: population not initialised");
+  UT_CHECK(c, m >= 0 && cand_base >= 0 && ((values && out) || m == 0) && ld >= m, UT_EINVAL, "hash_de: bad arguments");
+  return launch_hash_de(c, values, ld, m, cand_base, out);
 }
 
 int ut_history_reset(ut_ctx* c, int64_t capacity) {
@@ -647,7 +671,7 @@ int ut_score_round_de(ut_ctx* c, const ut_de_params* de, const ut_acq* acq, uint
   {
     StreamScope on_side(c, c->side);
     mark(c, "");
-    if ((rc = launch_hash(c, c->r_values.p, ld, m, c->r_digest.p))) return rc;
+    if ((rc = launch_hash_de(c, c->r_values.p, ld, m, cand_base, c->r_digest.p))) return rc;
     mark(c, "hash");
     if ((rc = launch_dedup(c, c->r_digest.p, m, c->r_dup.p))) return rc;
     mark(c, "dedup");

@@ -141,6 +141,125 @@ __global__ __launch_bounds__(PD_NT) void k_perm_digest(const DevParam* __restric
   }
 }
 
+// ---------------------------------------------------------------------------
+// Inner-digest reuse for DE rounds.  A DE trial copies its target member's
+// value for every parameter it does not cross (differentialevolution.py:122-127:
+// with cr = 0.2 and n_cross = 1, ~80% of them), and hash_value depends on the
+// value alone, so the target's inner digest sha256(repr(v)) is the trial's.
+// The population keeps those digests ([n_comp][npop][8], rebuilt when the
+// population is re-initialised, patched per replaced row); a round then
+//   k_de_diff     marks which computed-digest values differ from the target
+//                 (bitwise) and compacts them into (candidate, cslot) pairs,
+//   k_inner_pairs computes repr + SHA-256 only for those pairs, densely (a
+//                 wave of 64 lanes always has 64 digests to do -- skipping
+//                 per lane inside k_hash would not save anything: almost every
+//                 wave has a lane crossing every parameter),
+//   k_hash        reads each inner digest from the cache or the fresh buffer.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(HASH_NT) void k_pop_digests(const DevParam* __restrict__ params,
+                                                         const int32_t* __restrict__ comp, int32_t n_comp,
+                                                         const double* __restrict__ pop, int64_t npop,
+                                                         const int64_t* __restrict__ rows, int64_t nrows,
+                                                         uint4* __restrict__ cache) {
+  __shared__ uint32_t lds[SCR_WORDS * HASH_NT];
+  const int lane = threadIdx.x;
+  const int32_t s = blockIdx.y;
+  const int64_t r = (int64_t)blockIdx.x * HASH_NT + lane;
+  const int64_t n = rows ? nrows : npop;
+  if (s >= n_comp || r >= n) return;   // no barriers below: every lane owns its LDS column
+  int64_t j = rows ? rows[r] : r;
+  j = j < 0 ? 0 : (j >= npop ? npop - 1 : j);
+  const DevParam pr = params[comp[s]];
+  uint32_t D[8];
+  repr_digest(pr, pop[(int64_t)pr.col * npop + j], lds, lane, D);
+  uint4* dst = cache + 2 * ((int64_t)s * npop + j);
+  dst[0] = make_uint4(D[0], D[1], D[2], D[3]);
+  dst[1] = make_uint4(D[4], D[5], D[6], D[7]);
+}
+
+constexpr int DIFF_NT = 256;
+
+__device__ __forceinline__ uint64_t d_bits(double x) { return (uint64_t)__double_as_longlong(x); }
+
+// one lane per candidate: mask bits of the values that differ from the target
+// member (g % npop) and their (candidate, cslot) pairs, appended with one
+// atomic per wave (the pair order does not matter: each pair's digest has its
+// own slot in the fresh buffer)
+__global__ __launch_bounds__(DIFF_NT) void k_de_diff(const DevParam* __restrict__ params,
+                                                     const int32_t* __restrict__ comp, int32_t n_comp,
+                                                     const double* __restrict__ values, int64_t ld, int64_t m,
+                                                     const double* __restrict__ pop, int64_t npop, int64_t cand_base,
+                                                     uint32_t* __restrict__ mask, uint64_t* __restrict__ pairs,
+                                                     unsigned long long* __restrict__ npairs) {
+  const int64_t i = (int64_t)blockIdx.x * DIFF_NT + threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  const bool valid = i < m;
+  const int64_t t = valid ? (int64_t)((uint64_t)(cand_base + i) % (uint64_t)npop) : 0;
+  uint32_t cnt = 0;
+  for (int32_t w = 0; w * 32 < n_comp; ++w) {
+    uint32_t bits = 0;
+    const int32_t hi = n_comp - w * 32 < 32 ? n_comp - w * 32 : 32;
+    for (int32_t b = 0; b < hi; ++b) {
+      const int32_t col = params[comp[w * 32 + b]].col;
+      if (valid && d_bits(values[(int64_t)col * ld + i]) != d_bits(pop[(int64_t)col * npop + t])) bits |= 1u << b;
+    }
+    if (valid) mask[(int64_t)w * ld + i] = bits;
+    cnt += __builtin_popcount(bits);
+  }
+  // wave-inclusive prefix sum of the counts, one atomic per wave for its base
+  uint32_t incl = cnt;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t o = __shfl_up(incl, d, 64);
+    if (lane >= d) incl += o;
+  }
+  const uint32_t total = __shfl(incl, 63, 64);
+  unsigned long long base = 0;
+  if (lane == 63 && total) base = atomicAdd(npairs, (unsigned long long)total);
+  base = __shfl(base, 63, 64);
+  if (!cnt) return;
+  uint64_t pos = base + (incl - cnt);
+  for (int32_t w = 0; w * 32 < n_comp; ++w) {
+    uint32_t bits = mask[(int64_t)w * ld + i];
+    while (bits) {
+      const int b = __builtin_ctz(bits);
+      bits &= bits - 1;
+      pairs[pos++] = ((uint64_t)i << 20) | (uint64_t)(w * 32 + b);
+    }
+  }
+}
+
+// repr + SHA-256 of the changed values, a dense grid-stride over the pairs
+__global__ __launch_bounds__(HASH_NT) void k_inner_pairs(const DevParam* __restrict__ params,
+                                                         const int32_t* __restrict__ comp,
+                                                         const double* __restrict__ values, int64_t ld,
+                                                         const uint64_t* __restrict__ pairs,
+                                                         const unsigned long long* __restrict__ npairs,
+                                                         uint4* __restrict__ fresh) {
+  __shared__ uint32_t lds[SCR_WORDS * HASH_NT];
+  const int lane = threadIdx.x;
+  const int64_t n = (int64_t)*npairs;
+  for (int64_t q = (int64_t)blockIdx.x * HASH_NT + lane; q < n; q += (int64_t)gridDim.x * HASH_NT) {
+    const uint64_t e = pairs[q];
+    const int64_t i = (int64_t)(e >> 20);
+    const int32_t s = (int32_t)(e & 0xFFFFFu);
+    const DevParam pr = params[comp[s]];
+    uint32_t D[8];
+    repr_digest(pr, values[(int64_t)pr.col * ld + i], lds, lane, D);
+    uint4* dst = fresh + 2 * ((int64_t)s * ld + i);
+    dst[0] = make_uint4(D[0], D[1], D[2], D[3]);
+    dst[1] = make_uint4(D[4], D[5], D[6], D[7]);
+  }
+}
+
+// Inner digests of the computed-digest params, when k_hash reuses them (DE rounds)
+struct InnerRef {
+  const uint32_t* mask;   // [ceil(n_comp / 32)][ld]
+  const uint4* fresh;     // [n_comp][ld][8 words]
+  const uint4* cache;     // [n_comp][npop][8 words]; nullptr = compute every inner digest in k_hash
+  int64_t npop, cand_base;
+};
+
 __global__ __launch_bounds__(HASH_NT) void k_hash(const DevParam* __restrict__ params,
                                                   const int32_t* __restrict__ order,
                                                   const int32_t* __restrict__ order_col,
@@ -149,7 +268,7 @@ __global__ __launch_bounds__(HASH_NT) void k_hash(const DevParam* __restrict__ p
                                                   int32_t P, const uint4* __restrict__ lut,
                                                   const double* __restrict__ values, int64_t ld, int64_t m,
                                                   const uint4* __restrict__ perm_dig,
-                                                  uint32_t* __restrict__ out) {
+                                                  uint32_t* __restrict__ out, InnerRef ref) {
   __shared__ uint32_t lds[SCR_WORDS * HASH_NT];
   const int lane = threadIdx.x;
   // grid-stride over candidate blocks (launch_hash gives one block per 128
@@ -158,6 +277,7 @@ __global__ __launch_bounds__(HASH_NT) void k_hash(const DevParam* __restrict__ p
     const int64_t i0 = blk * HASH_NT + lane;
     const bool valid = i0 < m;
     const int64_t i = valid ? i0 : (m - 1);
+    const int64_t t = ref.cache ? (int64_t)((uint64_t)(ref.cand_base + i) % (uint64_t)ref.npop) : 0;
     hex32 HX = {};  // two 16-word hex slots: hole j in HX[16 (j % 2) .. 16 (j % 2) + 15]
     uint32_t H[8];
     sha256_init(H);
@@ -179,6 +299,15 @@ __global__ __launch_bounds__(HASH_NT) void k_hash(const DevParam* __restrict__ p
           D[4] = c.x; D[5] = c.y; D[6] = c.z; D[7] = c.w;
         } else if (pr.hash_mode == HM_PERM) {
           const uint4* src = perm_dig + 2 * ((int64_t)pr.pslot * m + i);
+          const uint4 a = src[0], c = src[1];
+          if (next + 1 < P) vnext = values[(int64_t)order_col[next + 1] * ld + i];
+          D[0] = a.x; D[1] = a.y; D[2] = a.z; D[3] = a.w;
+          D[4] = c.x; D[5] = c.y; D[6] = c.z; D[7] = c.w;
+        } else if (ref.cache) {
+          // the target's cached digest, or this trial's fresh one (k_inner_pairs)
+          const uint32_t mw = ref.mask[(int64_t)(pr.cslot >> 5) * ld + i];
+          const uint4* src = ((mw >> (pr.cslot & 31)) & 1u) ? ref.fresh + 2 * ((int64_t)pr.cslot * ld + i)
+                                                             : ref.cache + 2 * ((int64_t)pr.cslot * ref.npop + t);
           const uint4 a = src[0], c = src[1];
           if (next + 1 < P) vnext = values[(int64_t)order_col[next + 1] * ld + i];
           D[0] = a.x; D[1] = a.y; D[2] = a.z; D[3] = a.w;
@@ -227,7 +356,7 @@ __global__ __launch_bounds__(HASH_NT) void k_hash(const DevParam* __restrict__ p
   }
 }
 
-int launch_hash(ut_ctx* c, const double* values, int64_t ld, int64_t m, uint32_t* out) {
+static int launch_hash_impl(ut_ctx* c, const double* values, int64_t ld, int64_t m, uint32_t* out, InnerRef ref) {
   if (m <= 0) return 0;
   const Space& s = c->space;
   const uint32_t* pd = nullptr;
@@ -244,9 +373,65 @@ int launch_hash(ut_ctx* c, const double* values, int64_t ld, int64_t m, uint32_t
   hipLaunchKernelGGL(k_hash, dim3((unsigned)nb), dim3(HASH_NT), 0, c->stream, s.d_params, s.d_order,
                      s.d_order_col, reinterpret_cast<const uint2*>(s.d_words), s.d_block_last,
                      (int32_t)s.outer_blocks, s.P, reinterpret_cast<const uint4*>(s.d_lut), values, ld, m,
-                     reinterpret_cast<const uint4*>(pd), out);
+                     reinterpret_cast<const uint4*>(pd), out, ref);
   UT_LAUNCH_CHECK(c);
   return 0;
+}
+
+int launch_hash(ut_ctx* c, const double* values, int64_t ld, int64_t m, uint32_t* out) {
+  return launch_hash_impl(c, values, ld, m, out, InnerRef{nullptr, nullptr, nullptr, 1, 0});
+}
+
+int launch_pop_digests(ut_ctx* c, const int64_t* idx, int64_t n) {
+  const Space& s = c->space;
+  if (s.n_comp == 0 || c->npop == 0) return 0;
+  if (!idx) {  // full rebuild
+    const int64_t need = (int64_t)s.n_comp * c->npop * 8;
+    if (c->pop_dig_cap < need) {
+      if (c->pop_dig) {
+        UT_HIP(c, sync_all(c));
+        hipFree(c->pop_dig);
+        c->pop_dig = nullptr;
+        c->pop_dig_cap = 0;
+      }
+      const hipError_t e = hipMalloc((void**)&c->pop_dig, sizeof(uint32_t) * need);
+      if (e != hipSuccess) return set_err(c, UT_ENOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
+      c->pop_dig_cap = need;
+    }
+    n = c->npop;
+  }
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(k_pop_digests, dim3(grid1(n, HASH_NT), (unsigned)s.n_comp), dim3(HASH_NT), 0, c->stream,
+                     s.d_params, s.d_comp, s.n_comp, c->pop, c->npop, idx, idx ? n : 0,
+                     reinterpret_cast<uint4*>(c->pop_dig));
+  UT_LAUNCH_CHECK(c);
+  if (!idx) c->pop_dig_valid = true;
+  return 0;
+}
+
+int launch_hash_de(ut_ctx* c, const double* values, int64_t ld, int64_t m, int64_t cand_base, uint32_t* out) {
+  const Space& s = c->space;
+  if (s.n_comp == 0 || m <= 0) return launch_hash(c, values, ld, m, out);
+  int rc;
+  if (!c->pop_dig_valid && (rc = launch_pop_digests(c, nullptr, 0))) return rc;
+  const int32_t nw = (s.n_comp + 31) / 32;
+  if ((rc = ensure(c, c->r_mask, (size_t)nw * ld))) return rc;
+  if ((rc = ensure(c, c->r_fresh, (size_t)s.n_comp * ld * 8))) return rc;
+  if ((rc = ensure(c, c->r_pairs, (size_t)s.n_comp * ld))) return rc;
+  if ((rc = ensure(c, c->r_npairs, 1))) return rc;
+  UT_HIP(c, hipMemsetAsync(c->r_npairs.p, 0, sizeof(int64_t), c->stream));
+  unsigned long long* np = reinterpret_cast<unsigned long long*>(c->r_npairs.p);
+  hipLaunchKernelGGL(k_de_diff, dim3(grid1(m, DIFF_NT)), dim3(DIFF_NT), 0, c->stream, s.d_params, s.d_comp, s.n_comp,
+                     values, ld, m, c->pop, c->npop, cand_base, c->r_mask.p, c->r_pairs.p, np);
+  UT_LAUNCH_CHECK(c);
+  const int64_t want = ((int64_t)s.n_comp * m + HASH_NT - 1) / HASH_NT;
+  const unsigned grid = (unsigned)std::min<int64_t>(std::max<int64_t>(want, 1), (int64_t)c->n_cu * 8);
+  hipLaunchKernelGGL(k_inner_pairs, dim3(grid), dim3(HASH_NT), 0, c->stream, s.d_params, s.d_comp, values, ld,
+                     c->r_pairs.p, np, reinterpret_cast<uint4*>(c->r_fresh.p));
+  UT_LAUNCH_CHECK(c);
+  return launch_hash_impl(c, values, ld, m, out,
+                          InnerRef{c->r_mask.p, reinterpret_cast<const uint4*>(c->r_fresh.p),
+                                   reinterpret_cast<const uint4*>(c->pop_dig), c->npop, cand_base});
 }
 
 }  // namespace ut

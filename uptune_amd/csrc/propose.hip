@@ -518,6 +518,8 @@ extern "C" int ut_population_replace(ut_ctx* c, const double* trial, int64_t ld,
   hipLaunchKernelGGL(ut::k_pop_replace, dim3(ut::grid1(n, 64)), dim3(64), 0, c->stream, c->space.ncols, c->pop,
                      c->npop, trial, ld, idx, n);
   UT_LAUNCH_CHECK(c);
+  // keep the population's inner-digest cache current: only the replaced rows
+  if (c->pop_dig_valid) return ut::launch_pop_digests(c, idx, n);
   return 0;
 }
 
@@ -559,6 +561,7 @@ extern "C" int ut_pso_commit(ut_ctx* c, const double* values, const double* vel,
   UT_CHECK(c, c->pso_vel != nullptr && values && cand_base >= 0 && m >= 0 && cand_base + m <= c->npop && ld >= m,
            UT_EINVAL, "pso_commit: bad arguments");
   if (m == 0) return 0;
+  c->pop_dig_valid = false;   // positions moved: the inner-digest cache is rebuilt when a DE round needs it
   UT_HIP(c, hipMemcpy2DAsync(c->pop + cand_base, sizeof(double) * c->npop, values, sizeof(double) * ld,
                              sizeof(double) * m, c->space.ncols, hipMemcpyDeviceToDevice, c->stream));
   if (vel)

@@ -34,6 +34,9 @@ struct DevParam {
   int32_t psize;       // PERM: permutation size S; 1 for every other kind
   int32_t wcol;        // PERM: first of its S columns in the GA parent workspace
   int32_t pslot;       // PERM: slot of its inner digest in the per-round perm digest buffer
+  int32_t cslot;       // HM_FLOAT / HM_INT / HM_LOGINT (inner digest computed on the device):
+                       // its slot in the population inner-digest cache; -1 otherwise
+  int32_t pad_;
 };
 
 enum : int32_t { HM_LUT = 0, HM_FLOAT = 1, HM_INT = 2, HM_LOGINT = 3, HM_PERM = 4 };
@@ -78,6 +81,8 @@ struct Space {
   int32_t* d_perm_off = nullptr;          // per PERM param: S + 1 offsets into d_perm_bytes
   int32_t* d_perm_offbase = nullptr;      // per PERM slot: first entry in d_perm_off
   int32_t* d_perm_len = nullptr;          // per PERM slot: len(repr(list)) (constant per param)
+  int32_t n_comp = 0;                     // params whose inner digest is computed (cslot >= 0)
+  int32_t* d_comp = nullptr;              // cslot -> param index
 };
 
 template <class T>
@@ -137,12 +142,23 @@ struct ut_ctx {
   // population slots: the techniques of one bandit share a context (its GP
   // fit, history set, scratch) and keep one population each; the fields
   // above are the selected slot's, the others are parked here
+  // inner digests sha256(repr(get_value)) of the selected population's
+  // computed-digest params ([n_comp][npop][8]): a DE trial keeps most of its
+  // target's values, so its hash reuses the target's inner digests and
+  // computes only the changed ones (hash.hip launch_hash_de)
+  uint32_t* pop_dig = nullptr;
+  int64_t pop_dig_cap = 0;
+  bool pop_dig_valid = false;
+
   struct PopSlot {
     double* pop = nullptr;
     int64_t npop = 0, pop_cap = 0;
     double* pso_vel = nullptr;
     double* pso_best = nullptr;
     int64_t pso_cap = 0;
+    uint32_t* pop_dig = nullptr;
+    int64_t pop_dig_cap = 0;
+    bool pop_dig_valid = false;
   };
   std::vector<PopSlot> pop_slots;
   int32_t pop_slot = 0;
@@ -199,6 +215,10 @@ struct ut_ctx {
   ut::DevBuf<uint32_t> perm_dig; // [n_perm][m][8] inner digests of PERM values (hash pre-pass)
   ut::DevBuf<double> r_topk_score;
   ut::DevBuf<double> r_topk_vals;   // gathered top-k rows when the caller wants digests only
+  ut::DevBuf<uint32_t> r_mask;      // [ceil(n_comp / 32)][ld]: bit s = trial's cslot-s value differs from its target's
+  ut::DevBuf<uint32_t> r_fresh;     // [n_comp][ld][8]: inner digests of the changed values
+  ut::DevBuf<uint64_t> r_pairs;     // compacted (candidate << 20 | cslot) of the changed values
+  ut::DevBuf<int64_t> r_npairs;     // [1] their count
   int64_t r_ld = 0;
   int64_t r_m = 0;
 
@@ -285,6 +305,12 @@ int launch_ga(ut_ctx* c, const ut_ga_params* a, const double* parent1, const dou
               int64_t cand_base, int64_t m, double* out, int64_t ld, uint8_t* invalid);
 int launch_encode(ut_ctx* c, const double* values, int64_t ld, int64_t m, double* feat, int64_t ldf);
 int launch_hash(ut_ctx* c, const double* values, int64_t ld, int64_t m, uint32_t* out);
+// hash_config of DE trials of the selected population (candidate g targets
+// member g % npop): inner digests of values equal to the target's come from
+// the population cache (rebuilt if stale), the rest are computed once
+int launch_hash_de(ut_ctx* c, const double* values, int64_t ld, int64_t m, int64_t cand_base, uint32_t* out);
+// population cache maintenance: full rebuild, or the rows idx[0..n) after a replace
+int launch_pop_digests(ut_ctx* c, const int64_t* idx, int64_t n);
 int launch_hist_insert(ut_ctx* c, const uint32_t* dig, int64_t n);
 int launch_hist_rehash(ut_ctx* c, const uint32_t* okeys, const uint32_t* ostate, int64_t ocap);
 int launch_dedup(ut_ctx* c, const uint32_t* dig, int64_t m, uint8_t* dup);

@@ -220,6 +220,15 @@ class BatchEngine:
         L.check(self.ctx, self.lib.ut_hash(self.ctx, _ptr(values), values.stride(0), m, _ptr(out)), "ut_hash")
         return out
 
+    def hash_de(self, values: torch.Tensor, cand_base: int = 0, m: Optional[int] = None) -> torch.Tensor:
+        """ut_hash_de: hash_config of DE trials proposed from the selected
+        population with this cand_base, reusing the targets' inner digests"""
+        m = values.shape[1] if m is None else m
+        out = self._empty(m, 8, dtype=torch.int32)
+        L.check(self.ctx, self.lib.ut_hash_de(self.ctx, _ptr(values), values.stride(0), m, int(cand_base), _ptr(out)),
+                "ut_hash_de")
+        return out
+
     def hash_configs(self, cfgs: Sequence[Dict[Any, Any]]) -> List[str]:
         vals = torch.from_numpy(self.spec.encode_configs(cfgs)).to(self.device)
         d = self.hash(vals)

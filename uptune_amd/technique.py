@@ -443,6 +443,10 @@ class GpuBatchTechnique(SearchTechnique):
         """-> (values [P][m] device tensor, invalid mask or None)"""
         raise NotImplementedError
 
+    def hash_proposals(self, vals, base):
+        """hash_config of this round's proposals"""
+        return self.engine.hash(vals)
+
     def best_row(self):
         """driver.best_result's configuration as a SoA value row, or None"""
         b = self.driver.best_result
@@ -455,7 +459,7 @@ class GpuBatchTechnique(SearchTechnique):
         self.model.sync_history(self.driver)
         base = self.round_base()
         vals, invalid = self.propose(self.pool)
-        dig = eng.hash(vals)
+        dig = self.hash_proposals(vals, base)
         dup = eng.dedup(dig)
         if invalid is not None:
             dup = torch.maximum(dup, invalid)
@@ -536,6 +540,10 @@ class GpuDifferentialEvolution(GpuBatchTechnique):
         return self.engine.propose_de(m, round_=self.round, cand_base=self.round_base(), cr=self.cr,
                                       n_cross=self.n_cross, best=self.best_row(),
                                       information_sharing=self.information_sharing), None
+
+    def hash_proposals(self, vals, base):
+        # trials keep most of their target's values: reuse its inner digests
+        return self.engine.hash_de(vals, base)
 
     def after_round(self, idx, hexes):
         npop = self.engine.npop
