@@ -245,6 +245,27 @@ int ut_gp_fit_async(ut_ctx* ctx, const double* X_host, const double* y_host, int
  * candidates excluded from selection (score forced to -inf). */
 int ut_gp_score(ut_ctx* ctx, const double* features, int64_t ld, int64_t m, const ut_acq* acq,
                 const uint8_t* dup, double* mu, double* var, double* score);
+/* Selection-exact pruned scoring + top-k (fp64 fits only; EI, or UCB with
+ * kappa >= 0: scores that increase with sigma).  sigma^2 = sf2 - |L^-1 k*|^2
+ * and every row of L^-1 k* adds a square, so the first `bound_rows` rows give
+ * an upper bound on sigma^2, hence on the score, at a (bound_rows / n)^2
+ * fraction of the variance GEMM.  The exact scores of the 1024 best bounds
+ * give a threshold tau (their k-th best); only candidates whose bound reaches
+ * tau get the full variance GEMM, and the top-k of those is the top-k of the
+ * dense evaluation (every pruned candidate's exact score < tau <= the k-th
+ * best).  out_idx/out_score [k] as ut_topk (global indices cand_base + i).
+ * The mean is k* . alpha (K* epilogue), so the whole fit is waited for.  One
+ * host synchronisation (the survivor count).  stats (host, may be NULL):
+ * survivors, the bound rows used, tau. */
+typedef struct ut_prune_stats {
+  int64_t survivors;     /* candidates that got the full variance (m if the round fell back to dense) */
+  int32_t bound_rows;    /* rows of L^-1 k* in the bound (a multiple of 128) */
+  int32_t dense;         /* 1: too many survivors, the round ran the dense variance instead */
+  double threshold;      /* tau */
+} ut_prune_stats;
+int ut_gp_topk_pruned(ut_ctx* ctx, const double* features, int64_t ld, int64_t m, const ut_acq* acq,
+                      const uint8_t* dup, int64_t cand_base, int32_t k, int32_t bound_rows, int64_t* out_idx,
+                      double* out_score, ut_prune_stats* stats_host);
 /* arithmetic of the two scoring contractions (K* and L^-1 K*^T) for fits made
  * after this call: 64 = fp64 MFMA (default; 1e-5 parity), 32 = fp32 MFMA
  * (1e-3 parity), 16 = "f16x3": K* in fp64, the variance contraction as three

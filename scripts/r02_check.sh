@@ -6,7 +6,9 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 stop_if_fatal() { case "$1" in 0|1) ;; *) echo "fatal rc=$1 ($2)"; exit "$1";; esac; }
 if [ -z "$SKIP_TESTS" ]; then
-timeout -k 10 ${PYTEST_TIMEOUT:-900} python -u -m pytest tests -m gpu -x -v --timeout 150 --timeout-method thread -p no:cacheprovider ${PYTEST_ARGS} \
+KARGS=()
+[ -n "$PYTEST_K" ] && KARGS=(-k "$PYTEST_K")
+timeout -k 10 ${PYTEST_TIMEOUT:-900} python -u -m pytest tests -m gpu -x -v --timeout 150 --timeout-method thread -p no:cacheprovider "${KARGS[@]}" \
   > gpurun_out/pytest_gpu.log 2>&1
 rc=$?; echo "pytest rc=$rc"; grep -E "passed|failed|error" gpurun_out/pytest_gpu.log | tail -3; stop_if_fatal $rc pytest
 [ $rc -ne 0 ] && { tail -60 gpurun_out/pytest_gpu.log; exit 1; }

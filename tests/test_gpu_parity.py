@@ -704,3 +704,60 @@ def test_perm_score_round():
     gaps = np.abs(np.diff(np.sort(np.asarray(ei)[np.asarray(dup) == 0])[::-1][:33]))
     if gaps.min() > 1e-6:
         assert idx_l == want
+
+
+# --------------------------------------------------------------------------- EI-bound pruning
+@pytest.mark.parametrize("acq,bound_rows", [("ei", 128), ("ei", 384), ("ucb", 256)])
+def test_gp_topk_pruned_equals_dense(acq, bound_rows):
+    """ut_gp_topk_pruned: the top-k of a non-degenerate GP --
+    training points drawn from the population the candidates come from, so
+    many candidates sit near training data and their bound is loose -- equals
+    the dense device top-k and the oracle's; the survivors are a strict subset"""
+    space = mixed_space()
+    e = engine(space, seed=8)
+    pop = ode.population_init(space, 4096, seed=8)
+    e.population_set(dev(pop))
+    n = 640
+    X = features(space, pop[:, :n]).T
+    rng = np.random.default_rng(4)
+    y = np.sum((X - 0.3) ** 2, axis=1) + 0.05 * rng.standard_normal(n)
+    e.gp_fit(X, y, lengthscale=0.6, sigma_f2=1.0, sigma_n2=1e-6, jitter=1e-8)
+    m, k = 20000, 64
+    trial = e.propose_de(m, round_=1, cr=0.5)
+    feat = e.encode(trial)
+    dup = torch.zeros(m, dtype=torch.uint8, device="cuda")
+    dup[::97] = 1
+    a = e.acq(acq, xi=0.0, kappa=2.0)
+    idx, top, st = e.gp_topk_pruned(feat, k, acq=a, dup=dup, cand_base=5, bound_rows=bound_rows)
+    _, _, score = e.gp_score(feat, acq=a, dup=dup)
+    i2, t2 = e.topk(score, k, dup=dup, cand_base=5)
+    assert 0 < st["survivors"] < m and not st["dense"] and st["bound_rows"] >= bound_rows
+    g = ogp.GP(X, y, lengthscale=0.6, sigma_f2=1.0, sigma_n2=1e-6, jitter=1e-8)
+    mu, var = g.posterior(features(space, trial.cpu().numpy()).T)
+    sc = ogp.acquisition(mu, var, g.f_best, kind=acq, kappa=2.0)
+    sc = np.where(dup.cpu().numpy() != 0, -np.inf, sc)
+    want = [5 + i for i in sorted(range(m), key=lambda i: (-sc[i], i))[:k]]
+    gaps = np.abs(np.diff(np.sort(sc[np.isfinite(sc)])[::-1][:k + 1]))
+    _close(top.cpu().numpy(), t2.cpu().numpy(), rtol=1e-9, atol=1e-12)
+    if gaps.min() > 1e-9:
+        assert idx.cpu().numpy().tolist() == i2.cpu().numpy().tolist() == want
+
+
+def test_gp_topk_pruned_degenerate_and_fallback():
+    """far-away candidates (k* ~ 0 everywhere): the bound is exact, nearly all
+    candidates are pruned and the selection is the dense one; a bound of the
+    whole factor (bound_rows >= n) needs no second pass"""
+    space = r64_space()
+    e = engine(space, seed=3)
+    e.population_init(8192)
+    rng = np.random.default_rng(7)
+    X = rng.uniform(size=(1024, 64))
+    y = rng.standard_normal(1024)
+    e.gp_fit(X, y, lengthscale=0.2)
+    vals = e.propose_de(8192, round_=1)
+    feat = e.encode(vals)
+    idx, top, st = e.gp_topk_pruned(feat, 32, bound_rows=128)
+    _, _, score = e.gp_score(feat)
+    i2, t2 = e.topk(score, 32)
+    assert idx.cpu().numpy().tolist() == i2.cpu().numpy().tolist()
+    assert st["survivors"] < 8192

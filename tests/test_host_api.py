@@ -46,7 +46,7 @@ def test_struct_layouts():
     hc = ctypes.CDLL(os.path.join(os.path.dirname(L.LIB_PATH), "libuthot_hostcheck.so"))
     hc.uthc_sizeof.restype = ctypes.c_longlong
     for i, st in enumerate([L.ParamDesc, L.GpHyper, L.RoundOut, L.DeParams, L.Acq, L.PsoParams, L.GaParams,
-                            L.TreeNode]):
+                            L.TreeNode, L.PruneStats]):
         assert ctypes.sizeof(st) == hc.uthc_sizeof(i), st.__name__
     assert ctypes.sizeof(L.ParamDesc) == 112
 

@@ -51,6 +51,10 @@ class DeParams(C.Structure):
                 ("best", C.c_void_p)]
 
 
+class PruneStats(C.Structure):
+    _fields_ = [("survivors", C.c_int64), ("bound_rows", C.c_int32), ("dense", C.c_int32), ("threshold", C.c_double)]
+
+
 class PsoParams(C.Structure):
     _fields_ = [("omega", C.c_double), ("phi_l", C.c_double), ("phi_g", C.c_double), ("sigma", C.c_double),
                 ("alias_pbest", C.c_int32), ("enum_mode", C.c_int32), ("crossover", C.c_int32),
@@ -96,6 +100,7 @@ SIGNATURES = {
     "ut_population_get": (C.c_int, [P, P, I64]),
     "ut_population_replace": (C.c_int, [P, P, I64, P, I64]),
     "ut_population_select": (C.c_int, [P, I32]),
+    "ut_gp_topk_pruned": (C.c_int, [P, P, I64, I64, C.POINTER(Acq), P, I64, I32, I32, P, P, C.POINTER(PruneStats)]),
     "ut_hash_de": (C.c_int, [P, P, I64, I64, I64, P]),
     "ut_propose_de": (C.c_int, [P, C.POINTER(DeParams), U32, I64, I64, P, I64]),
     "ut_pso_reset": (C.c_int, [P]),

@@ -202,6 +202,8 @@ int ut_ctx_destroy(ut_ctx* c) {
     fr(c->pop_slots[s].pop); fr(c->pop_slots[s].pso_vel); fr(c->pop_slots[s].pso_best); fr(c->pop_slots[s].pop_dig);
   }
   fr(c->r_mask.p); fr(c->r_fresh.p); fr(c->r_pairs.p); fr(c->r_npairs.p);
+  fr(c->pr_mu.p); fr(c->pr_ub.p); fr(c->pr_score.p); fr(c->pr_mpart.p); fr(c->pr_kst.p); fr(c->pr_vpart.p);
+  fr(c->pr_idx.p); fr(c->pr_count.p);
   fr(c->hist_keys); fr(c->hist_state); fr(c->batch_slots);
   fr(c->gp_Xs); fr(c->gp_xnorm); fr(c->gp_K); fr(c->gp_Linv); fr(c->gp_y); fr(c->gp_tmp);
   fr(c->gp_alpha); fr(c->gp_beta); fr(c->gp_inv_ell); fr(c->gp_stats); fr(c->gp_flag); fr(c->gp_Xs_f); fr(c->gp_T);
@@ -608,6 +610,19 @@ int ut_gp_score(ut_ctx* c, const double* feat, int64_t ld, int64_t m, const ut_a
   const bool own = c->timing.on && !c->timing.in_round;
   if (own) timing_begin(c);
   int rc = gp_score_impl(c, feat, ld, m, acq, dup, mu, var, score);
+  if (own) timing_end(c);
+  return rc;
+}
+
+int ut_gp_topk_pruned(ut_ctx* c, const double* feat, int64_t ld, int64_t m, const ut_acq* acq, const uint8_t* dup,
+                      int64_t cand_base, int32_t k, int32_t bound_rows, int64_t* out_idx, double* out_score,
+                      ut_prune_stats* stats) {
+  if (!c) return UT_EINVAL;
+  UT_CHECK(c, m >= 1 && feat && ld >= m && acq && out_idx && out_score && cand_base >= 0, UT_EINVAL,
+           "gp_topk_pruned: bad arguments");
+  const bool own = c->timing.on && !c->timing.in_round;
+  if (own) timing_begin(c);
+  int rc = gp_topk_pruned_impl(c, feat, ld, m, acq, dup, cand_base, k, bound_rows, out_idx, out_score, stats);
   if (own) timing_end(c);
   return rc;
 }

@@ -626,4 +626,209 @@ int gp_score_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, const ut
   return 0;
 }
 
+
+// ---------------------------------------------------------------------------
+// Selection-exact EI-bound pruning (ut_gp_topk_pruned).
+//   var = sf2 - sum_r (L^-1 k*)_r^2 and every term is >= 0, so the partial
+//   sum over the first R row tiles bounds var from above; EI (and UCB with
+//   kappa >= 0) increases with sigma, so the same holds for the score.  The
+//   R-tile partials are bitwise the first R partials of the full GEMM (same
+//   tiles, same k order) and fp addition of non-negative terms and sf2 - x are
+//   monotone, so var_exact <= var_bound holds in floating point too; the score
+//   bound gets a 1e-12 relative margin for the acquisition's own rounding.
+// ---------------------------------------------------------------------------
+__global__ void k_prune_bound(int64_t m, int32_t RTm, const double* __restrict__ mu_part, int32_t RTv,
+                              const double* __restrict__ var_part, int64_t ldp, double sf2,
+                              const double* __restrict__ stats, const int32_t* __restrict__ fit_flag, int32_t kind,
+                              double xi, double kappa, const uint8_t* __restrict__ dup, double* __restrict__ mu_out,
+                              double* __restrict__ ub_out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= m) return;
+  double mu = 0.0, vs = 0.0;
+  for (int32_t r = 0; r < RTm; ++r) mu += mu_part[(int64_t)r * ldp + i];
+  for (int32_t r = 0; r < RTv; ++r) vs += var_part[(int64_t)r * ldp + i];
+  double var = sf2 - vs;
+  var = var > 0.0 ? var : 0.0;
+  double ub = acq_score(kind, mu, var, stats[0], xi, kappa);
+  ub = ub + fabs(ub) * 1e-12 + 1e-300;
+  if (*fit_flag != 0) mu = ub = __builtin_nan("");
+  if (dup && dup[i]) ub = -1.0 / 0.0;
+  mu_out[i] = mu;
+  ub_out[i] = ub;
+}
+
+// out[r][j] = K*[r][idx[j] - base] for j < n (idx < 0: 0), zero columns up to ldo
+__global__ void k_gather_kst_cols(const double* __restrict__ kst, int64_t ldk, const int64_t* __restrict__ idx,
+                                  int64_t base, int64_t n, int64_t ldo, double* __restrict__ out) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t r = blockIdx.y;
+  if (j >= ldo) return;
+  double v = 0.0;
+  if (j < n) {
+    const int64_t q = idx[j];
+    if (q >= 0) v = kst[r * ldk + (q - base)];
+  }
+  out[r * ldo + j] = v;
+}
+
+// exact scores of the gathered candidates: compact[j], and scattered to full[idx[j]]
+__global__ void k_prune_exact(int64_t n, const int64_t* __restrict__ idx, int64_t base, int32_t RT,
+                              const double* __restrict__ var_part, int64_t ldp, const double* __restrict__ mu_full,
+                              double sf2, const double* __restrict__ stats, const int32_t* __restrict__ fit_flag,
+                              int32_t kind, double xi, double kappa, double* __restrict__ compact,
+                              double* __restrict__ full) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  const int64_t q = idx[j];
+  if (q < 0) {
+    if (compact) compact[j] = -1.0 / 0.0;
+    return;
+  }
+  double vs = 0.0;
+  for (int32_t r = 0; r < RT; ++r) vs += var_part[(int64_t)r * ldp + j];
+  double var = sf2 - vs;
+  var = var > 0.0 ? var : 0.0;
+  double sc = acq_score(kind, mu_full[q - base], var, stats[0], xi, kappa);
+  if (*fit_flag != 0) sc = __builtin_nan("");
+  if (compact) compact[j] = sc;
+  if (full) full[q - base] = sc;
+}
+
+// survivors: bound >= tau (tau = the k-th best exact score of the threshold
+// set, a device scalar); appended with one atomic per wave
+__global__ void k_prune_survivors(int64_t m, const double* __restrict__ ub, const double* __restrict__ tau_p,
+                                  int64_t* __restrict__ out, unsigned long long* __restrict__ count) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  const double tau = *tau_p;
+  const bool keep = i < m && ub[i] >= tau;
+  const unsigned long long ball = __ballot(keep);
+  const uint32_t n = __builtin_popcountll(ball);
+  unsigned long long base = 0;
+  if (lane == 0 && n) base = atomicAdd(count, (unsigned long long)n);
+  base = __shfl(base, 0, 64);
+  if (keep) out[base + __builtin_popcountll(ball & ((1ull << lane) - 1ull))] = i;
+}
+
+__global__ void k_fill(double* __restrict__ p, int64_t n, double v) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) p[i] = v;
+}
+
+int gp_topk_pruned_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, const ut_acq* acq, const uint8_t* dup,
+                        int64_t cand_base, int32_t k, int32_t bound_rows, int64_t* out_idx, double* out_score,
+                        ut_prune_stats* stats) {
+  UT_CHECK(c, c->gp_ready, UT_EINVAL, "gp_topk_pruned: call ut_gp_fit first");
+  UT_CHECK(c, c->gp_fit_prec == 64, UT_EINVAL, "gp_topk_pruned: needs an fp64 fit (ut_gp_set_precision 64)");
+  UT_CHECK(c, acq->kind == UT_ACQ_EI || (acq->kind == UT_ACQ_UCB && acq->kappa >= 0.0), UT_EINVAL,
+           "gp_topk_pruned: the score must increase with sigma (EI, or UCB with kappa >= 0)");
+  UT_CHECK(c, k >= 1 && k <= 1024, UT_EINVAL, "gp_topk_pruned: k must be in [1, 1024]");
+  if (c->fit_pending) UT_HIP(c, hipStreamWaitEvent(c->stream, c->ev_fit, 0));   // K* takes mu = k* . alpha
+  const int32_t n = c->gp_n, d = c->gp_d;
+  const int32_t npad = ((n + NPAD - 1) / NPAD) * NPAD;
+  const int32_t dpad = ((d + 15) / 16) * 16;
+  const int32_t RT = npad / NPAD;
+  int32_t R = (bound_rows + NPAD - 1) / NPAD;
+  R = R < 1 ? 1 : (R > RT ? RT : R);
+  const int64_t ldk = ((m + VAR_BN - 1) / VAR_BN) * VAR_BN;
+  int rc;
+  if ((rc = ensure(c, c->kst, (size_t)npad * ldk))) return rc;
+  if ((rc = ensure(c, c->mu_part, (size_t)RT * ldk))) return rc;
+  if ((rc = ensure(c, c->var_part, (size_t)RT * ldk))) return rc;
+  if ((rc = ensure(c, c->pr_mpart, (size_t)RT * ldk))) return rc;
+  if ((rc = ensure(c, c->cnorm, (size_t)ldk))) return rc;
+  if ((rc = ensure(c, c->ucand, (size_t)dpad * ldk))) return rc;
+  if ((rc = ensure(c, c->pr_mu, (size_t)ldk))) return rc;
+  if ((rc = ensure(c, c->pr_ub, (size_t)ldk))) return rc;
+  if ((rc = ensure(c, c->pr_score, (size_t)ldk + 2048))) return rc;   // + the threshold set's two [1024] arrays
+  if ((rc = ensure(c, c->pr_idx, (size_t)ldk + 2048))) return rc;
+  if ((rc = ensure(c, c->pr_count, 1))) return rc;
+  const double* LinvT = c->gp_LinvT;
+  // 1. K* with the mean in its epilogue, 2. the first R row tiles of L^-1 K*^T
+  if ((rc = launch_prep_cand(c, feat, ld, m, d, dpad, c->ucand.p, ldk, c->cnorm.p))) return rc;
+  if ((rc = launch_gemm_kstar(c, 64, c->gp_XsT, npad, c->ucand.p, dpad, m, c->kst.p, ldk, c->mu_part.p))) return rc;
+  mark(c, "kstar");
+  if ((rc = launch_gemm_var(c, 64, LinvT, npad, c->kst.p, ldk, R * NPAD, m, c->var_part.p, c->gp_beta,
+                            c->pr_mpart.p)))
+    return rc;
+  mark(c, "bound");
+  hipLaunchKernelGGL(k_prune_bound, dim3(grid1(m, 256)), dim3(256), 0, c->stream, m, RT, c->mu_part.p, R,
+                     c->var_part.p, ldk, c->gp_sf2, c->gp_stats, c->gp_flag, acq->kind, acq->xi, acq->kappa, dup,
+                     c->pr_mu.p, c->pr_ub.p);
+  UT_LAUNCH_CHECK(c);
+  // 3. threshold: exact scores of the best 1024 bounds, tau = their k-th best
+  const int32_t kp = (int32_t)(m < 1024 ? m : 1024);
+  int64_t* tset = c->pr_idx.p + ldk;                   // [1024] threshold set (global indices)
+  double* tsc = c->pr_score.p + ldk;                   // [1024] their bounds
+  double* tex = c->pr_score.p + ldk + 1024;            // [1024] their exact scores
+  if ((rc = topk_impl(c, c->pr_ub.p, dup, m, cand_base, kp < k ? k : kp, tset, tsc))) return rc;
+  const int64_t ldt = ((int64_t)kp + VAR_BN - 1) / VAR_BN * VAR_BN;
+  if ((rc = ensure(c, c->pr_kst, (size_t)npad * ldt))) return rc;
+  if ((rc = ensure(c, c->pr_vpart, (size_t)RT * ldt))) return rc;
+  hipLaunchKernelGGL(k_gather_kst_cols, dim3(grid1(ldt, 256), (unsigned)npad), dim3(256), 0, c->stream, c->kst.p, ldk,
+                     tset, cand_base, (int64_t)kp, ldt, c->pr_kst.p);
+  UT_LAUNCH_CHECK(c);
+  if ((rc = launch_gemm_var(c, 64, LinvT, npad, c->pr_kst.p, ldt, npad, kp, c->pr_vpart.p, c->gp_beta,
+                            c->pr_mpart.p)))
+    return rc;
+  hipLaunchKernelGGL(k_prune_exact, dim3(grid1(kp, 256)), dim3(256), 0, c->stream, (int64_t)kp, tset, cand_base, RT,
+                     c->pr_vpart.p, ldt, c->pr_mu.p, c->gp_sf2, c->gp_stats, c->gp_flag, acq->kind, acq->xi,
+                     acq->kappa, tex, nullptr);
+  UT_LAUNCH_CHECK(c);
+  int64_t* tk_i = out_idx;   // the caller's [k] outputs hold tau's top-k for now
+  double* tk_s = out_score;
+  if ((rc = topk_impl(c, tex, nullptr, kp, 0, k, tk_i, tk_s))) return rc;
+  // 4. survivors: bound >= tau
+  UT_HIP(c, hipMemsetAsync(c->pr_count.p, 0, sizeof(int64_t), c->stream));
+  hipLaunchKernelGGL(k_prune_survivors, dim3(grid1(m, 256)), dim3(256), 0, c->stream, m, c->pr_ub.p, tk_s + (k - 1),
+                     c->pr_idx.p, reinterpret_cast<unsigned long long*>(c->pr_count.p));
+  UT_LAUNCH_CHECK(c);
+  int64_t ns = 0;
+  double tau = 0.0;
+  UT_HIP(c, hipMemcpyAsync(&ns, c->pr_count.p, sizeof(int64_t), hipMemcpyDeviceToHost, c->stream));
+  UT_HIP(c, hipMemcpyAsync(&tau, tk_s + (k - 1), sizeof(double), hipMemcpyDeviceToHost, c->stream));
+  UT_HIP(c, hipStreamSynchronize(c->stream));
+  mark(c, "prune");
+  const bool dense = ns * 2 > m;
+  if (dense) {
+    // most candidates survive: the dense variance on K* as is
+    if ((rc = launch_gemm_var(c, 64, LinvT, npad, c->kst.p, ldk, npad, m, c->var_part.p, c->gp_beta,
+                              c->pr_mpart.p)))
+      return rc;
+    hipLaunchKernelGGL(k_gp_finalize, dim3(grid1(m, 256)), dim3(256), 0, c->stream, m, RT, RT, c->mu_part.p,
+                       c->var_part.p, ldk, c->gp_sf2, c->gp_stats, c->gp_flag, acq->kind, acq->xi, acq->kappa, dup,
+                       nullptr, nullptr, c->pr_score.p);
+    UT_LAUNCH_CHECK(c);
+  } else {
+    // 5. the full variance for the survivors only, their exact scores into a -inf array
+    hipLaunchKernelGGL(k_fill, dim3(grid1(m, 256)), dim3(256), 0, c->stream, c->pr_score.p, m, -1.0 / 0.0);
+    UT_LAUNCH_CHECK(c);
+    if (ns > 0) {
+      const int64_t lds = (ns + VAR_BN - 1) / VAR_BN * VAR_BN;
+      if ((rc = ensure(c, c->pr_kst, (size_t)npad * lds))) return rc;
+      if ((rc = ensure(c, c->pr_vpart, (size_t)RT * lds))) return rc;
+      hipLaunchKernelGGL(k_gather_kst_cols, dim3(grid1(lds, 256), (unsigned)npad), dim3(256), 0, c->stream, c->kst.p,
+                         ldk, c->pr_idx.p, (int64_t)0, ns, lds, c->pr_kst.p);
+      UT_LAUNCH_CHECK(c);
+      if ((rc = launch_gemm_var(c, 64, LinvT, npad, c->pr_kst.p, lds, npad, ns, c->pr_vpart.p, c->gp_beta,
+                                c->pr_mpart.p)))
+        return rc;
+      hipLaunchKernelGGL(k_prune_exact, dim3(grid1(ns, 256)), dim3(256), 0, c->stream, ns, c->pr_idx.p, (int64_t)0,
+                         RT, c->pr_vpart.p, lds, c->pr_mu.p, c->gp_sf2, c->gp_stats, c->gp_flag, acq->kind, acq->xi,
+                         acq->kappa, nullptr, c->pr_score.p);
+      UT_LAUNCH_CHECK(c);
+    }
+  }
+  mark(c, "var");
+  if ((rc = topk_impl(c, c->pr_score.p, dup, m, cand_base, k, out_idx, out_score))) return rc;
+  mark(c, "topk");
+  if (stats) {
+    stats->survivors = dense ? m : ns;
+    stats->bound_rows = R * NPAD;
+    stats->dense = dense ? 1 : 0;
+    stats->threshold = tau;
+  }
+  return 0;
+}
+
 }  // namespace ut

@@ -237,8 +237,8 @@ int launch_gemm_kstar(ut_ctx* c, int prec, const double* XsT, int32_t npad, cons
   UT_CHECK(c, npad % K_BM == 0 && dpad % K_BK == 0 && ldk % K_BN == 0 && ldk >= m, UT_EINVAL,
            "gemm_kstar: bad padding");
   UT_CHECK(c, prec == 64 || prec == 32 || prec == 16, UT_EINVAL, "gemm_kstar: bad precision");
-  UT_CHECK(c, (part != nullptr) == (prec != 64), UT_EINVAL,
-           "gemm_kstar: the mean partial is taken here in fp32 / h3 mode only");
+  UT_CHECK(c, part != nullptr || prec == 64, UT_EINVAL,
+           "gemm_kstar: fp32 / h3 mode takes the mean partial here");
   const int32_t RT = npad / K_BM;
   const int32_t CT = (int32_t)(ldk / K_BN);  // every column of K* (zeros past m) is written
   const int64_t items = (int64_t)RT * CT;
@@ -260,6 +260,10 @@ int launch_gemm_kstar(ut_ctx* c, int prec, const double* XsT, int32_t npad, cons
     hipLaunchKernelGGL((k_gp_kstar<float, true>), dim3(nb), dim3(K_NT), 0, c->stream, XsT, (int64_t)npad, ucand, ldk, dpad,
                        RT, CT, c->gp_xnorm, c->cnorm.p, c->gp_alpha, c->gp_sf2, c->gp_n, m, c->gp_ctr + 8,
                        (float*)kst, ldk, part, 1.0, (int64_t)0);
+  else if (part)   // fp64 with the mean k* . alpha in the epilogue (pruned scoring: needs the whole fit)
+    hipLaunchKernelGGL((k_gp_kstar<double, true>), dim3(nb), dim3(K_NT), 0, c->stream, XsT, (int64_t)npad, ucand, ldk, dpad,
+                       RT, CT, c->gp_xnorm, c->cnorm.p, c->gp_alpha, c->gp_sf2, c->gp_n, m, c->gp_ctr + 8,
+                       (double*)kst, ldk, part, 1.0, (int64_t)0);
   else
     hipLaunchKernelGGL((k_gp_kstar<double, false>), dim3(nb), dim3(K_NT), 0, c->stream, XsT, (int64_t)npad, ucand, ldk, dpad,
                        RT, CT, c->gp_xnorm, c->cnorm.p, c->gp_alpha, c->gp_sf2, c->gp_n, m, c->gp_ctr + 8,

@@ -26,6 +26,7 @@ long long uthc_sizeof(int which) {
     case 5: return (long long)sizeof(ut_pso_params);
     case 6: return (long long)sizeof(ut_ga_params);
     case 7: return (long long)sizeof(ut_tree_node);
+    case 8: return (long long)sizeof(ut_prune_stats);
     default: return -1;
   }
 }

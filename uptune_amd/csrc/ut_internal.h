@@ -219,6 +219,12 @@ struct ut_ctx {
   ut::DevBuf<uint32_t> r_fresh;     // [n_comp][ld][8]: inner digests of the changed values
   ut::DevBuf<uint64_t> r_pairs;     // compacted (candidate << 20 | cslot) of the changed values
   ut::DevBuf<int64_t> r_npairs;     // [1] their count
+  // EI-bound pruned scoring (gp.hip ut_gp_topk_pruned)
+  ut::DevBuf<double> pr_mu, pr_ub, pr_score;   // [ld] exact mean, score bound, exact scores (-inf if pruned)
+  ut::DevBuf<double> pr_mpart;                 // [RT][ldk] unused mean partials of the bound / survivor GEMMs
+  ut::DevBuf<double> pr_kst, pr_vpart;         // survivors' K* columns [npad][lds] and variance partials
+  ut::DevBuf<int64_t> pr_idx;                  // [ld] survivor indices (+ the threshold set)
+  ut::DevBuf<int64_t> pr_count;                // [1]
   int64_t r_ld = 0;
   int64_t r_m = 0;
 
@@ -318,6 +324,9 @@ int gp_score_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, const ut
                   double* mu, double* var, double* score, hipEvent_t dup_ready = nullptr);
 int topk_impl(ut_ctx* c, const double* score, const uint8_t* dup, int64_t m, int64_t cand_base, int32_t k,
               int64_t* out_idx, double* out_score);
+int gp_topk_pruned_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, const ut_acq* acq, const uint8_t* dup,
+                        int64_t cand_base, int32_t k, int32_t bound_rows, int64_t* out_idx, double* out_score,
+                        ut_prune_stats* stats);
 // prec: 64 (fp64 MFMA), 32 (fp32 MFMA), 16 (f16x3: fp16 hi/lo split operands,
 // three fp16 MFMA products, f32 accumulate -- see gp_gemm.hip)
 constexpr int H3_KSCALE_EXP = 14;  // K* (<= sf2) is scaled by 2^(14 - ceil(log2 sf2)) before the split
