@@ -147,7 +147,12 @@ def main():
                     help="c2 = BASELINE configs[1] (R64, m=1M, n=1024: the headline); c3 = configs[2] per GPU "
                          "(HPL-64 mixed space, 16M/8 = 2M candidates per GPU, n=4096); c4 = configs[3] "
                          "(gcc 339-flag space, GA proposals, dedup against the 3,680 recorded configs, m=4M)")
+    ap.add_argument("--prune", type=int, default=0, metavar="ROWS",
+                    help="selection-exact EI-bound pruning (ut_score_round_de_pruned) with the first ROWS rows of "
+                         "L^-1 k* as the bound; a secondary line, fp64 only (the dense round stays the headline)")
     args = ap.parse_args()
+    if args.prune and args.precision != 64:
+        ap.error("--prune needs --precision 64")
     if args.config == "c3":
         if args.m == 1 << 20:
             args.m = 1 << 21
@@ -243,12 +248,19 @@ def main():
             idx, top = allgather_topk(idx, top, dig[sel], k)
         return idx, top
 
+    prune_stats = []
+
     def step(r):
         if args.config == "c4":
             return step_c4(r)
         eng.gp_fit(X, y, lengthscale=ell, sigma_f2=1.0, sigma_n2=1e-6, wait=False)   # overlaps propose + hash
-        idx, top, dig, _ = eng.score_round_de(m, k, round_=r, cand_base=cand_base, cr=0.2, n_cross=1, acq=acq,
-                                              want_values=False)
+        if args.prune:
+            idx, top, dig, _, st = eng.score_round_de_pruned(m, k, round_=r, cand_base=cand_base, cr=0.2, n_cross=1,
+                                                             acq=acq, want_values=False, bound_rows=args.prune)
+            prune_stats.append(st)
+        else:
+            idx, top, dig, _ = eng.score_round_de(m, k, round_=r, cand_base=cand_base, cr=0.2, n_cross=1, acq=acq,
+                                                  want_values=False)
         eng.history_add(dig)                              # the selections join the history (device-side)
         if world > 1:
             idx, top = allgather_topk(idx, top, dig, k)   # RCCL all_gather + deterministic merge
@@ -272,7 +284,7 @@ def main():
     elapsed = time.perf_counter() - t0
     # per-stage device times of the timed rounds (HIP events recorded on the
     # library's streams during the rounds, read once here)
-    for st in ("propose", "hash", "dedup", "encode", "kstar", "var", "finalize", "topk"):
+    for st in ("propose", "hash", "dedup", "encode", "kstar", "bound", "prune", "var", "finalize", "topk"):
         try:
             stage_ms[st] = [eng.stage_time(st)]
         except Exception:
@@ -299,6 +311,12 @@ def main():
         var_ms = stages["kstar"]
         flops_var = 2.0 * m * n * d
         kernel = "k_gp_kstar<double, false> (K* = exp(-|x - u|^2 / 2), v_mfma_f64_16x16x4_f64)"
+    if args.prune and prune_stats:
+        # the variance GEMM of the survivors (+ the 1024-candidate threshold set)
+        timed = prune_stats[-args.steps:]
+        surv = float(np.mean([s["survivors"] for s in timed]))
+        flops_var = (surv + min(m, 1024)) * n * (n + 1)
+        kernel += " [pruned: survivors + threshold set only]"
     achieved = flops_var / (var_ms * 1e-3) / 1e12 if var_ms else None
     peak = {64: PEAK_FP64_TFLOPS, 32: PEAK_FP32_TFLOPS, 16: PEAK_FP16_TFLOPS / 3.0}[args.precision]
     # HBM bytes per launch and the rocprof average duration were profiled on the
@@ -307,6 +325,15 @@ def main():
     pmc, pmc_note = load_pmc({64: "var", 32: "var32", 16: "var16"}[args.precision]) if profiled else ({}, "")
     traffic = pmc.get("hbm_bytes_per_launch")
     frac_rocprof = (flops_var / (pmc["avg_ns"] * 1e-9) / 1e12 / peak) if pmc.get("avg_ns") else None
+    prune_info = None
+    if args.prune and prune_stats:
+        timed = prune_stats[-args.steps:]
+        prune_info = {"bound_rows": timed[-1]["bound_rows"],
+                      "survivor_frac": float(np.mean([s["survivors"] / m for s in timed])),
+                      "dense_rounds": int(sum(s["dense"] for s in timed)),
+                      "dense_equivalent_tflops": float(m) * n * (n + 1) / (elapsed / args.steps) / 1e12,
+                      "note": "selection-exact: every pruned candidate's exact score is below the k-th best "
+                              "(ut_gp_topk_pruned); value counts all m candidates of a round"}
     if args.config == "c4":
         workload = (f"C4 gcc flags (339 params: 1 + 154 Int, 184 Enum{{on,off,default}}; {d} GP features): GA "
                     f"mutation 0.1 from the best recorded config + hash_config + dedup vs 3,680 recorded configs "
@@ -319,6 +346,8 @@ def main():
         data = "synthetic (HPL-64 configs from op1_randomize; objective = |features - 0.3|^2; population random-init)"
     else:
         workload = f"C2 R64: DE-Alt + hash_config + dedup + GP-EI n={n} + top-{k}"
+    if args.prune:
+        workload += f", EI-bound pruned (first {args.prune} rows of L^-1 k* as the bound)"
         data = "synthetic (Rosenbrock-64 objective on uniform training points; DE population random-init)"
     result = {
         "metric": "candidate configs scored/sec (GP-EI + top-k)",
@@ -338,6 +367,7 @@ def main():
         "config": {"workload": workload, "candidates_per_gpu": m, "gp_n": n, "dims": d, "k": k,
                    "parallelism": f"dp{world}"},
         "stage_ms": stages,
+        "prune": prune_info,
         "roofline": {"bound": "mfma", "kernel": kernel,
                      "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
                      "frac": (achieved / peak) if achieved else None, "traffic": traffic,

@@ -744,9 +744,10 @@ def test_gp_topk_pruned_equals_dense(acq, bound_rows):
 
 
 def test_gp_topk_pruned_degenerate_and_fallback():
-    """far-away candidates (k* ~ 0 everywhere): the bound is exact, nearly all
-    candidates are pruned and the selection is the dense one; a bound of the
-    whole factor (bound_rows >= n) needs no second pass"""
+    """far-away candidates (k* underflows to 0 everywhere): every score is the
+    same, so every bound reaches the threshold (ties are broken by index and
+    cannot be pruned): the round falls back to the dense variance and still
+    selects exactly the dense top-k"""
     space = r64_space()
     e = engine(space, seed=3)
     e.population_init(8192)
@@ -759,5 +760,5 @@ def test_gp_topk_pruned_degenerate_and_fallback():
     idx, top, st = e.gp_topk_pruned(feat, 32, bound_rows=128)
     _, _, score = e.gp_score(feat)
     i2, t2 = e.topk(score, 32)
-    assert idx.cpu().numpy().tolist() == i2.cpu().numpy().tolist()
-    assert st["survivors"] < 8192
+    assert idx.cpu().numpy().tolist() == i2.cpu().numpy().tolist() == list(range(32))
+    assert st["dense"] and st["survivors"] == 8192

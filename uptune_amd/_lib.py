@@ -100,6 +100,8 @@ SIGNATURES = {
     "ut_population_get": (C.c_int, [P, P, I64]),
     "ut_population_replace": (C.c_int, [P, P, I64, P, I64]),
     "ut_population_select": (C.c_int, [P, I32]),
+    "ut_score_round_de_pruned": (C.c_int, [P, C.POINTER(DeParams), C.POINTER(Acq), U32, I64, I64, I32, I32,
+                                           C.POINTER(RoundOut), C.POINTER(PruneStats)]),
     "ut_gp_topk_pruned": (C.c_int, [P, P, I64, I64, C.POINTER(Acq), P, I64, I32, I32, P, P, C.POINTER(PruneStats)]),
     "ut_hash_de": (C.c_int, [P, P, I64, I64, I64, P]),
     "ut_propose_de": (C.c_int, [P, C.POINTER(DeParams), U32, I64, I64, P, I64]),

@@ -655,8 +655,26 @@ int ut_topk(ut_ctx* c, const double* score, const uint8_t* dup, int64_t m, int64
   return topk_impl(c, score, dup, m, cand_base, k, out_idx, out_score);
 }
 
+static int score_round_de_impl(ut_ctx* c, const ut_de_params* de, const ut_acq* acq, uint32_t round_,
+                               int64_t cand_base, int64_t m, int32_t k, const ut_round_out* out, int32_t prune_rows,
+                               ut_prune_stats* stats);
+
 int ut_score_round_de(ut_ctx* c, const ut_de_params* de, const ut_acq* acq, uint32_t round_, int64_t cand_base,
                       int64_t m, int32_t k, const ut_round_out* out) {
+  return score_round_de_impl(c, de, acq, round_, cand_base, m, k, out, 0, nullptr);
+}
+
+int ut_score_round_de_pruned(ut_ctx* c, const ut_de_params* de, const ut_acq* acq, uint32_t round_,
+                             int64_t cand_base, int64_t m, int32_t k, int32_t bound_rows, const ut_round_out* out,
+                             ut_prune_stats* stats) {
+  if (!c) return UT_EINVAL;
+  UT_CHECK(c, bound_rows >= 1, UT_EINVAL, "score_round_pruned: bound_rows must be >= 1");
+  return score_round_de_impl(c, de, acq, round_, cand_base, m, k, out, bound_rows, stats);
+}
+
+static int score_round_de_impl(ut_ctx* c, const ut_de_params* de, const ut_acq* acq, uint32_t round_,
+                               int64_t cand_base, int64_t m, int32_t k, const ut_round_out* out, int32_t prune_rows,
+                               ut_prune_stats* stats) {
   if (!c) return UT_EINVAL;
   UT_CHECK(c, c->has_space, UT_ENOSPACE, "space not defined");
   UT_CHECK(c, c->pop != nullptr, UT_EINVAL, "score_round: population not initialised");
@@ -694,13 +712,21 @@ int ut_score_round_de(ut_ctx* c, const ut_de_params* de, const ut_acq* acq, uint
   }
   if ((rc = launch_encode(c, c->r_values.p, ld, m, c->r_feat.p, ld))) return rc;
   mark(c, "encode");
-  // join before the finalize kernel, which masks duplicates
-  if ((rc = gp_score_impl(c, c->r_feat.p, ld, m, acq, c->r_dup.p, c->r_mu.p, c->r_var.p, c->r_score.p,
-                          c->ev_join)))
-    return rc;
-  if ((rc = topk_impl(c, c->r_score.p, c->r_dup.p, m, cand_base, k, c->r_topk_idx.p, c->r_topk_score.p)))
-    return rc;
-  mark(c, "topk");
+  if (prune_rows > 0) {
+    // pruned: only candidates whose score bound reaches the threshold get the
+    // full variance (the bound kernel joins the dup mask first)
+    if ((rc = gp_topk_pruned_impl(c, c->r_feat.p, ld, m, acq, c->r_dup.p, cand_base, k, prune_rows, c->r_topk_idx.p,
+                                  c->r_topk_score.p, stats, c->ev_join)))
+      return rc;
+  } else {
+    // join before the finalize kernel, which masks duplicates
+    if ((rc = gp_score_impl(c, c->r_feat.p, ld, m, acq, c->r_dup.p, c->r_mu.p, c->r_var.p, c->r_score.p,
+                            c->ev_join)))
+      return rc;
+    if ((rc = topk_impl(c, c->r_score.p, c->r_dup.p, m, cand_base, k, c->r_topk_idx.p, c->r_topk_score.p)))
+      return rc;
+    mark(c, "topk");
+  }
   if (out) {
     if (out->topk_idx)
       UT_HIP(c, hipMemcpyAsync(out->topk_idx, c->r_topk_idx.p, sizeof(int64_t) * k, hipMemcpyDeviceToDevice,

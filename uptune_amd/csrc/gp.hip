@@ -717,7 +717,7 @@ __global__ void k_fill(double* __restrict__ p, int64_t n, double v) {
 
 int gp_topk_pruned_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, const ut_acq* acq, const uint8_t* dup,
                         int64_t cand_base, int32_t k, int32_t bound_rows, int64_t* out_idx, double* out_score,
-                        ut_prune_stats* stats) {
+                        ut_prune_stats* stats, hipEvent_t dup_ready) {
   UT_CHECK(c, c->gp_ready, UT_EINVAL, "gp_topk_pruned: call ut_gp_fit first");
   UT_CHECK(c, c->gp_fit_prec == 64, UT_EINVAL, "gp_topk_pruned: needs an fp64 fit (ut_gp_set_precision 64)");
   UT_CHECK(c, acq->kind == UT_ACQ_EI || (acq->kind == UT_ACQ_UCB && acq->kappa >= 0.0), UT_EINVAL,
@@ -752,6 +752,7 @@ int gp_topk_pruned_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, co
                             c->pr_mpart.p)))
     return rc;
   mark(c, "bound");
+  if (dup_ready) UT_HIP(c, hipStreamWaitEvent(c->stream, dup_ready, 0));   // the dup mask (side stream)
   hipLaunchKernelGGL(k_prune_bound, dim3(grid1(m, 256)), dim3(256), 0, c->stream, m, RT, c->mu_part.p, R,
                      c->var_part.p, ldk, c->gp_sf2, c->gp_stats, c->gp_flag, acq->kind, acq->xi, acq->kappa, dup,
                      c->pr_mu.p, c->pr_ub.p);

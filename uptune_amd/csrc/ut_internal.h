@@ -326,7 +326,7 @@ int topk_impl(ut_ctx* c, const double* score, const uint8_t* dup, int64_t m, int
               int64_t* out_idx, double* out_score);
 int gp_topk_pruned_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, const ut_acq* acq, const uint8_t* dup,
                         int64_t cand_base, int32_t k, int32_t bound_rows, int64_t* out_idx, double* out_score,
-                        ut_prune_stats* stats);
+                        ut_prune_stats* stats, hipEvent_t dup_ready = nullptr);
 // prec: 64 (fp64 MFMA), 32 (fp32 MFMA), 16 (f16x3: fp16 hi/lo split operands,
 // three fp16 MFMA products, f32 accumulate -- see gp_gemm.hip)
 constexpr int H3_KSCALE_EXP = 14;  // K* (<= sf2) is scaled by 2^(14 - ceil(log2 sf2)) before the split

@@ -355,6 +355,26 @@ class BatchEngine:
                 "ut_score_round_de")
         return idx, top, dig, vals
 
+    def score_round_de_pruned(self, m: int, k: int, round_: int = 0, cand_base: int = 0, cr: float = 0.2,
+                              n_cross: int = 1, acq: Optional[L.Acq] = None, want_values: bool = True, best=None,
+                              information_sharing: int = 1, bound_rows: int = 256):
+        """score_round_de with ut_gp_topk_pruned's selection-exact pruning;
+        -> (idx, top, digests, values, stats dict)"""
+        de, keep = self._de_params(cr, n_cross, best, information_sharing)  # noqa: F841
+        acq = acq or self.acq()
+        idx = self._empty(k, dtype=torch.int64)
+        top = self._empty(k)
+        dig = self._empty(k, 8, dtype=torch.int32)
+        vals = self._empty(self.spec.ncols, k) if want_values else None
+        out = L.RoundOut(topk_idx=idx.data_ptr(), topk_score=top.data_ptr(), topk_digest=dig.data_ptr(),
+                         topk_values=vals.data_ptr() if vals is not None else None)
+        st = L.PruneStats()
+        L.check(self.ctx, self.lib.ut_score_round_de_pruned(self.ctx, C.byref(de), C.byref(acq), int(round_),
+                                                            int(cand_base), int(m), int(k), int(bound_rows),
+                                                            C.byref(out), C.byref(st)), "ut_score_round_de_pruned")
+        return idx, top, dig, vals, {"survivors": st.survivors, "bound_rows": st.bound_rows, "dense": bool(st.dense),
+                                     "threshold": st.threshold, "m": m}
+
     def round_buffers(self):
         ptrs = [C.c_void_p() for _ in range(7)]
         ld = C.c_int64()
