@@ -346,9 +346,9 @@ def main():
         data = "synthetic (HPL-64 configs from op1_randomize; objective = |features - 0.3|^2; population random-init)"
     else:
         workload = f"C2 R64: DE-Alt + hash_config + dedup + GP-EI n={n} + top-{k}"
+        data = "synthetic (Rosenbrock-64 objective on uniform training points; DE population random-init)"
     if args.prune:
         workload += f", EI-bound pruned (first {args.prune} rows of L^-1 k* as the bound)"
-        data = "synthetic (Rosenbrock-64 objective on uniform training points; DE population random-init)"
     result = {
         "metric": "candidate configs scored/sec (GP-EI + top-k)",
         "value": value,

@@ -8,7 +8,11 @@ results broadcast over RCCL.
         --master-addr 127.0.0.1 --master-port 29511 scripts/c5_bandit.py   # 8 GPUs
 
 Rank 0 prints one JSON line: generations, evaluations, best objective, wall
-time, scoring rounds and candidates scored per second (all ranks).
+time, scoring rounds (and rounds/s), GP fits of the shared model, candidates
+scored per second (all ranks), and the same engine's stand-alone round rate
+at the final training-set size (one DE round of `pool` candidates: propose,
+hash, dedup, encode, GP-EI, top-k), so the loop's overhead over the kernels
+is visible as end_to_end_vs_round.
 """
 import argparse
 import json
@@ -35,6 +39,7 @@ def main():
     ap.add_argument("--batch", type=int, default=8)
     ap.add_argument("--population", type=int, default=4096)
     ap.add_argument("--backend", default="nccl")
+    ap.add_argument("--precision", type=int, default=64, choices=(64, 32, 16))
     args = ap.parse_args()
 
     import torch
@@ -54,18 +59,41 @@ def main():
     t0 = time.perf_counter()
     drv = tune_bandit(spaces.r64(), rosenbrock64, generations=args.generations, parallelism=args.parallelism,
                       n_init=args.n_init, pool=args.pool, batch=args.batch, population=args.population, seed=1,
-                      lengthscale=0.3, device=local)
+                      lengthscale=0.3, device=local, precision=args.precision)
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
     techs = drv.root_technique.techniques
     rounds = {t.name: t.round for t in techs}
     scored = sum(t.round * (t.pool * (world if t.sharded else 1) if t.sharded else min(t.pool, t.population))
                  for t in techs)
+    # the stand-alone round rate of the same engine at the final training set
+    model = techs[0].model
+    de = [t for t in techs if t.name == "gpu-de"][0]
+    eng = model.engine_for(de)
+    acq = eng.acq("ei")
+    model.fit(drv)
+    rr = []
+    for r in range(3):
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        v = eng.propose_de(args.pool, round_=10000 + r, cand_base=0)
+        dg = eng.hash_de(v, 0)
+        dup = eng.dedup(dg)
+        _, _, sc = eng.gp_score(eng.encode(v), acq=acq, dup=dup)
+        eng.topk(sc, args.batch, dup=dup)
+        torch.cuda.synchronize()
+        rr.append(time.perf_counter() - t1)
+    round_rate = args.pool / min(rr)
+    n_train = len(drv.results_query())
     out = {"config": "C5 AUC bandit over GPU DE+PSO+GA+GGA, shared GP, Rosenbrock-64", "n_gpus": world,
            "generations": drv.generation, "evaluations": len(drv.results) - args.n_init,
            "initial_design": args.n_init, "best": drv.best_result.time if drv.best_result else None,
-           "wall_s": wall, "technique_rounds": rounds, "candidates_scored": scored,
-           "candidates_scored_per_s": scored / wall, "bandit_uses": dict(drv.root_technique.bandit.use_counts)}
+           "wall_s": wall, "technique_rounds": rounds, "rounds_per_s": sum(rounds.values()) / wall,
+           "gp_fits": model.fits, "gp_n_final": n_train, "candidates_scored": scored,
+           "candidates_scored_per_s": scored / wall,
+           "round_rate_candidates_per_s": round_rate * (world if world > 1 else 1),
+           "end_to_end_vs_round": (scored / wall) / (round_rate * (world if world > 1 else 1)),
+           "bandit_uses": dict(drv.root_technique.bandit.use_counts)}
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -762,3 +762,28 @@ def test_gp_topk_pruned_degenerate_and_fallback():
     i2, t2 = e.topk(score, 32)
     assert idx.cpu().numpy().tolist() == i2.cpu().numpy().tolist() == list(range(32))
     assert st["dense"] and st["survivors"] == 8192
+
+
+def test_score_round_de_pruned_equals_dense_round():
+    """the whole DE round with pruning (ut_score_round_de_pruned) selects the
+    same candidates, scores, digests and rows as the dense round"""
+    space = mixed_space()
+    e = engine(space, seed=12)
+    pop = ode.population_init(space, 8192, seed=12)
+    e.population_set(dev(pop))
+    n = 512
+    X = features(space, pop[:, :n]).T
+    y = np.sum((X - 0.6) ** 2, axis=1)
+    e.gp_fit(X, y, lengthscale=0.6, sigma_f2=1.0, sigma_n2=1e-6, jitter=1e-8)
+    e.history_reset(0)
+    e.history_add(e.hash(dev(pop[:, :n])))
+    a = e.score_round_de(8192, 48, round_=3, cand_base=100, cr=0.3)
+    b = e.score_round_de_pruned(8192, 48, round_=3, cand_base=100, cr=0.3, bound_rows=128)
+    st = b[4]
+    assert 0 < st["survivors"] < 8192 and not st["dense"]
+    sa, sb = a[1].cpu().numpy(), b[1].cpu().numpy()
+    _close(sb, sa, rtol=1e-9, atol=1e-12)
+    if np.abs(np.diff(sa)).min() > 1e-9:
+        assert a[0].cpu().numpy().tolist() == b[0].cpu().numpy().tolist()
+        assert hexes(a[2]) == hexes(b[2])
+        np.testing.assert_array_equal(a[3].cpu().numpy(), b[3].cpu().numpy())

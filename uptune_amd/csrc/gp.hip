@@ -657,8 +657,8 @@ __global__ void k_prune_bound(int64_t m, int32_t RTm, const double* __restrict__
   ub_out[i] = ub;
 }
 
-// out[r][j] = K*[r][idx[j] - base] for j < n (idx < 0: 0), zero columns up to ldo
-__global__ void k_gather_kst_cols(const double* __restrict__ kst, int64_t ldk, const int64_t* __restrict__ idx,
+// out[r][j] = src[r][idx[j] - base] for j < n (idx < 0: 0), zero columns up to ldo
+__global__ void k_gather_cols(const double* __restrict__ kst, int64_t ldk, const int64_t* __restrict__ idx,
                                   int64_t base, int64_t n, int64_t ldo, double* __restrict__ out) {
   const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t r = blockIdx.y;
@@ -746,7 +746,12 @@ int gp_topk_pruned_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, co
   const double* LinvT = c->gp_LinvT;
   // 1. K* with the mean in its epilogue, 2. the first R row tiles of L^-1 K*^T
   if ((rc = launch_prep_cand(c, feat, ld, m, d, dpad, c->ucand.p, ldk, c->cnorm.p))) return rc;
-  if ((rc = launch_gemm_kstar(c, 64, c->gp_XsT, npad, c->ucand.p, dpad, m, c->kst.p, ldk, c->mu_part.p))) return rc;
+  // K* stores only the bound rows; the mean sums every row.  The few
+  // candidates that need every row (threshold set, survivors) get their K*
+  // columns recomputed from their features (recompute_cols below): cheaper than
+  // writing and re-reading the whole n x m matrix
+  if ((rc = launch_gemm_kstar(c, 64, c->gp_XsT, npad, c->ucand.p, dpad, m, c->kst.p, ldk, c->mu_part.p, R * NPAD)))
+    return rc;
   mark(c, "kstar");
   if ((rc = launch_gemm_var(c, 64, LinvT, npad, c->kst.p, ldk, R * NPAD, m, c->var_part.p, c->gp_beta,
                             c->pr_mpart.p)))
@@ -763,12 +768,24 @@ int gp_topk_pruned_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, co
   double* tsc = c->pr_score.p + ldk;                   // [1024] their bounds
   double* tex = c->pr_score.p + ldk + 1024;            // [1024] their exact scores
   if ((rc = topk_impl(c, c->pr_ub.p, dup, m, cand_base, kp < k ? k : kp, tset, tsc))) return rc;
+  // full K* columns of the candidates idx[0..nc) (global indices - base): their
+  // scaled features and norms gathered, then the K* GEMM on those columns only
+  auto recompute_cols = [&](const int64_t* idx, int64_t base, int64_t nc, int64_t ldc) -> int {
+    int r2;
+    if ((r2 = ensure(c, c->pr_kst, (size_t)npad * ldc))) return r2;
+    if ((r2 = ensure(c, c->pr_vpart, (size_t)RT * ldc))) return r2;
+    if ((r2 = ensure(c, c->pr_ucand, (size_t)dpad * ldc))) return r2;
+    if ((r2 = ensure(c, c->pr_cnorm, (size_t)ldc))) return r2;
+    hipLaunchKernelGGL(k_gather_cols, dim3(grid1(ldc, 256), (unsigned)dpad), dim3(256), 0, c->stream, c->ucand.p, ldk,
+                       idx, base, nc, ldc, c->pr_ucand.p);
+    hipLaunchKernelGGL(k_gather_cols, dim3(grid1(ldc, 256), 1u), dim3(256), 0, c->stream, c->cnorm.p, ldk, idx, base,
+                       nc, ldc, c->pr_cnorm.p);
+    UT_LAUNCH_CHECK(c);
+    return launch_gemm_kstar(c, 64, c->gp_XsT, npad, c->pr_ucand.p, dpad, nc, c->pr_kst.p, ldc, nullptr, -1,
+                             c->pr_cnorm.p);
+  };
   const int64_t ldt = ((int64_t)kp + VAR_BN - 1) / VAR_BN * VAR_BN;
-  if ((rc = ensure(c, c->pr_kst, (size_t)npad * ldt))) return rc;
-  if ((rc = ensure(c, c->pr_vpart, (size_t)RT * ldt))) return rc;
-  hipLaunchKernelGGL(k_gather_kst_cols, dim3(grid1(ldt, 256), (unsigned)npad), dim3(256), 0, c->stream, c->kst.p, ldk,
-                     tset, cand_base, (int64_t)kp, ldt, c->pr_kst.p);
-  UT_LAUNCH_CHECK(c);
+  if ((rc = recompute_cols(tset, cand_base, kp, ldt))) return rc;
   if ((rc = launch_gemm_var(c, 64, LinvT, npad, c->pr_kst.p, ldt, npad, kp, c->pr_vpart.p, c->gp_beta,
                             c->pr_mpart.p)))
     return rc;
@@ -792,7 +809,8 @@ int gp_topk_pruned_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, co
   mark(c, "prune");
   const bool dense = ns * 2 > m;
   if (dense) {
-    // most candidates survive: the dense variance on K* as is
+    // most candidates survive: the whole K* (this time every row) and the dense variance
+    if ((rc = launch_gemm_kstar(c, 64, c->gp_XsT, npad, c->ucand.p, dpad, m, c->kst.p, ldk, c->mu_part.p))) return rc;
     if ((rc = launch_gemm_var(c, 64, LinvT, npad, c->kst.p, ldk, npad, m, c->var_part.p, c->gp_beta,
                               c->pr_mpart.p)))
       return rc;
@@ -806,11 +824,7 @@ int gp_topk_pruned_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, co
     UT_LAUNCH_CHECK(c);
     if (ns > 0) {
       const int64_t lds = (ns + VAR_BN - 1) / VAR_BN * VAR_BN;
-      if ((rc = ensure(c, c->pr_kst, (size_t)npad * lds))) return rc;
-      if ((rc = ensure(c, c->pr_vpart, (size_t)RT * lds))) return rc;
-      hipLaunchKernelGGL(k_gather_kst_cols, dim3(grid1(lds, 256), (unsigned)npad), dim3(256), 0, c->stream, c->kst.p,
-                         ldk, c->pr_idx.p, (int64_t)0, ns, lds, c->pr_kst.p);
-      UT_LAUNCH_CHECK(c);
+      if ((rc = recompute_cols(c->pr_idx.p, 0, ns, lds))) return rc;
       if ((rc = launch_gemm_var(c, 64, LinvT, npad, c->pr_kst.p, lds, npad, ns, c->pr_vpart.p, c->gp_beta,
                                 c->pr_mpart.p)))
         return rc;

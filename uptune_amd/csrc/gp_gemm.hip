@@ -88,7 +88,7 @@ __global__ __launch_bounds__(K_NT, 2) void k_gp_kstar(const double* __restrict__
                                                       const double* __restrict__ alpha, double sf2, int32_t n,
                                                       int64_t m, int32_t* __restrict__ ticket, TS* __restrict__ kst,
                                                       int64_t ldk, double* __restrict__ part, double kscale,
-                                                      int64_t lo_off) {
+                                                      int64_t lo_off, int32_t store_rt) {
   // TS = _Float16 (h3): k* * kscale split into fp16 hi + lo, stored candidate-major
   // [col][row] (ld = npad = RT * K_BM) so the variance MFMA reads k-contiguous
   // fragments; the lo plane starts lo_off elements after the hi plane
@@ -197,7 +197,7 @@ __global__ __launch_bounds__(K_NT, 2) void k_gp_kstar(const double* __restrict__
             timg[o] = hi;
             timg[K_BN * T_PITCH + o] = (_Float16)(float)(xs - (double)hi);
           } else {
-            kst[(int64_t)row * ldk + col] = (TS)ks;
+            if (rt < store_rt) kst[(int64_t)row * ldk + col] = (TS)ks;   // pruned scoring stores the bound rows only
           }
           if constexpr (MU) s += al[i][r] * ks;
         }
@@ -233,7 +233,7 @@ __global__ __launch_bounds__(K_NT, 2) void k_gp_kstar(const double* __restrict__
 int h3_kstar_exp(double sf2) { return H3_KSCALE_EXP - ilogb(sf2); }  // sf2 * 2^e < 2^15
 
 int launch_gemm_kstar(ut_ctx* c, int prec, const double* XsT, int32_t npad, const double* ucand, int32_t dpad,
-                      int64_t m, void* kst, int64_t ldk, double* part) {
+                      int64_t m, void* kst, int64_t ldk, double* part, int32_t store_rows, const double* cn) {
   UT_CHECK(c, npad % K_BM == 0 && dpad % K_BK == 0 && ldk % K_BN == 0 && ldk >= m, UT_EINVAL,
            "gemm_kstar: bad padding");
   UT_CHECK(c, prec == 64 || prec == 32 || prec == 16, UT_EINVAL, "gemm_kstar: bad precision");
@@ -241,6 +241,9 @@ int launch_gemm_kstar(ut_ctx* c, int prec, const double* XsT, int32_t npad, cons
            "gemm_kstar: fp32 / h3 mode takes the mean partial here");
   const int32_t RT = npad / K_BM;
   const int32_t CT = (int32_t)(ldk / K_BN);  // every column of K* (zeros past m) is written
+  // fp64: only the first store_rows rows of K* are written (the mean still
+  // sums every row); the other precisions always store everything
+  const int32_t store_rt = store_rows < 0 ? RT : (store_rows + K_BM - 1) / K_BM;
   const int64_t items = (int64_t)RT * CT;
   // Two K* workgroups fill a CU's VGPRs, so a full persistent grid leaves no
   // slot for the GP fit running beside it on the fit stream, and the fit's
@@ -254,20 +257,20 @@ int launch_gemm_kstar(ut_ctx* c, int prec, const double* XsT, int32_t npad, cons
   UT_HIP(c, hipMemsetAsync(c->gp_ctr + 8, 0, sizeof(int32_t) * 8, c->stream));
   if (prec == 16)
     hipLaunchKernelGGL((k_gp_kstar<_Float16, true>), dim3(nb), dim3(K_NT), 0, c->stream, XsT, (int64_t)npad, ucand, ldk,
-                       dpad, RT, CT, c->gp_xnorm, c->cnorm.p, c->gp_alpha, c->gp_sf2, c->gp_n, m, c->gp_ctr + 8,
-                       (_Float16*)kst, ldk, part, ldexp(1.0, h3_kstar_exp(c->gp_sf2)), ldk * (int64_t)npad);
+                       dpad, RT, CT, c->gp_xnorm, cn ? cn : c->cnorm.p, c->gp_alpha, c->gp_sf2, c->gp_n, m, c->gp_ctr + 8,
+                       (_Float16*)kst, ldk, part, ldexp(1.0, h3_kstar_exp(c->gp_sf2)), ldk * (int64_t)npad, RT);
   else if (prec == 32)
     hipLaunchKernelGGL((k_gp_kstar<float, true>), dim3(nb), dim3(K_NT), 0, c->stream, XsT, (int64_t)npad, ucand, ldk, dpad,
-                       RT, CT, c->gp_xnorm, c->cnorm.p, c->gp_alpha, c->gp_sf2, c->gp_n, m, c->gp_ctr + 8,
-                       (float*)kst, ldk, part, 1.0, (int64_t)0);
+                       RT, CT, c->gp_xnorm, cn ? cn : c->cnorm.p, c->gp_alpha, c->gp_sf2, c->gp_n, m, c->gp_ctr + 8,
+                       (float*)kst, ldk, part, 1.0, (int64_t)0, RT);
   else if (part)   // fp64 with the mean k* . alpha in the epilogue (pruned scoring: needs the whole fit)
     hipLaunchKernelGGL((k_gp_kstar<double, true>), dim3(nb), dim3(K_NT), 0, c->stream, XsT, (int64_t)npad, ucand, ldk, dpad,
-                       RT, CT, c->gp_xnorm, c->cnorm.p, c->gp_alpha, c->gp_sf2, c->gp_n, m, c->gp_ctr + 8,
-                       (double*)kst, ldk, part, 1.0, (int64_t)0);
+                       RT, CT, c->gp_xnorm, cn ? cn : c->cnorm.p, c->gp_alpha, c->gp_sf2, c->gp_n, m, c->gp_ctr + 8,
+                       (double*)kst, ldk, part, 1.0, (int64_t)0, store_rt);
   else
     hipLaunchKernelGGL((k_gp_kstar<double, false>), dim3(nb), dim3(K_NT), 0, c->stream, XsT, (int64_t)npad, ucand, ldk, dpad,
-                       RT, CT, c->gp_xnorm, c->cnorm.p, c->gp_alpha, c->gp_sf2, c->gp_n, m, c->gp_ctr + 8,
-                       (double*)kst, ldk, part, 1.0, (int64_t)0);
+                       RT, CT, c->gp_xnorm, cn ? cn : c->cnorm.p, c->gp_alpha, c->gp_sf2, c->gp_n, m, c->gp_ctr + 8,
+                       (double*)kst, ldk, part, 1.0, (int64_t)0, store_rt);
   UT_LAUNCH_CHECK(c);
   return 0;
 }

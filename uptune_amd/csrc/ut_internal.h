@@ -223,6 +223,7 @@ struct ut_ctx {
   ut::DevBuf<double> pr_mu, pr_ub, pr_score;   // [ld] exact mean, score bound, exact scores (-inf if pruned)
   ut::DevBuf<double> pr_mpart;                 // [RT][ldk] unused mean partials of the bound / survivor GEMMs
   ut::DevBuf<double> pr_kst, pr_vpart;         // survivors' K* columns [npad][lds] and variance partials
+  ut::DevBuf<double> pr_ucand, pr_cnorm;       // survivors' scaled features [dpad][lds] and norms [lds]
   ut::DevBuf<int64_t> pr_idx;                  // [ld] survivor indices (+ the threshold set)
   ut::DevBuf<int64_t> pr_count;                // [1]
   int64_t r_ld = 0;
@@ -332,7 +333,8 @@ int gp_topk_pruned_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, co
 constexpr int H3_KSCALE_EXP = 14;  // K* (<= sf2) is scaled by 2^(14 - ceil(log2 sf2)) before the split
 int h3_kstar_exp(double sf2);
 int launch_gemm_kstar(ut_ctx* c, int prec, const double* XsT, int32_t npad, const double* ucand, int32_t dpad,
-                      int64_t m, void* kst, int64_t ldk, double* part);
+                      int64_t m, void* kst, int64_t ldk, double* part, int32_t store_rows = -1,
+                      const double* cn = nullptr);   // candidate norms (nullptr: c->cnorm)
 int launch_prep_cand(ut_ctx* c, const double* feat, int64_t ld, int64_t m, int32_t d, int32_t dpad, double* u,
                      int64_t ldu, double* cn);
 int launch_xs_t(ut_ctx* c, const double* Xs, int32_t npad, int32_t d, int32_t dpad, double* XsT);
