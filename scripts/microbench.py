@@ -45,6 +45,13 @@ def bench_hash(m=1 << 20):
             trial = eng.propose_de(m, round_=1, cr=0.2)
             ms = timeit(lambda: eng.hash(trial))
             out["r64_de_trials"] = {"ms": ms, "outer_blocks": nb, "ns_per_cand": ms * 1e6 / m}
+            # the same trials through ut_hash_de (target inner digests reused; the
+            # population cache is built by the warm-up call)
+            ms = timeit(lambda: eng.hash_de(trial, 0))
+            out["r64_de_trials_reuse"] = {"ms": ms, "outer_blocks": nb, "ns_per_cand": ms * 1e6 / m}
+            # the outer message alone (every inner digest reused: trial == population)
+            ms = timeit(lambda: eng.hash_de(vals, 0))
+            out["r64_outer_only"] = {"ms": ms, "outer_blocks": nb, "ns_per_cand": ms * 1e6 / m}
         del eng
     return out
 

@@ -24,6 +24,7 @@ STAGES = {  # stage key -> kernel-name prefix
     "topk0": "void ut::k_topk_chunk<0>", "pso": "ut::k_pso(", "ga": "ut::k_ga(",
     # rocprofv3 leaves the _Float16 instantiations mangled
     "var16": "_ZN2ut11k_gp_var_h3", "kstar16": "_ZN2ut10k_gp_kstarIDF16_",
+    "inner_pairs": "ut::k_inner_pairs", "de_diff": "ut::k_de_diff", "pop_digests": "ut::k_pop_digests",
 }
 
 
