@@ -185,6 +185,7 @@ int ut_ctx_create(int device, uint64_t seed, ut_ctx** out) {
     return UT_EHIP;
   }
   c->stream = c->own_stream;
+  if (const char* e = getenv("UT_JOIN_BEFORE_VAR")) c->join_before_var = atoi(e) != 0;
   *out = c;
   return 0;
 }

@@ -611,6 +611,7 @@ int gp_score_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, const ut
     return rc;
   mark(c, "kstar");
   if (c->fit_pending && !fp32) UT_HIP(c, hipStreamWaitEvent(c->stream, c->ev_fit, 0));
+  if (dup_ready && c->join_before_var) UT_HIP(c, hipStreamWaitEvent(c->stream, dup_ready, 0));
   mark(c, "");  // the wait for the fit is not variance time
   if ((rc = launch_gemm_var(c, prec, fp32 ? (const void*)c->gp_LinvT_f : (const void*)c->gp_LinvT, npad, c->kst.p,
                             ldk, npad, m, c->var_part.p, fp32 ? nullptr : c->gp_beta,

@@ -123,6 +123,10 @@ struct ut_ctx {
   hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_fit = nullptr, ev_prefit = nullptr;
   hipEvent_t ev_fit_x = nullptr;     // fit stream: scaled training inputs ready (K* may start)
   bool fit_pending = false;          // scoring waits on ev_fit before touching GP state
+  // round schedule: 1 = the variance GEMM waits for the side stream's hash +
+  // dedup (they share CUs with K* only), 0 = only the finalize waits (the hash
+  // may spill into the variance GEMM).  UT_JOIN_BEFORE_VAR overrides.
+  int32_t join_before_var = 0;
   double* fit_host = nullptr;        // pinned staging of X, y, 1/ell for the asynchronous fit
   size_t fit_host_n = 0;
   std::string err;
