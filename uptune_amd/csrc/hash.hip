@@ -260,7 +260,14 @@ struct InnerRef {
   int64_t npop, cand_base;
 };
 
-__global__ __launch_bounds__(HASH_NT) void k_hash(const DevParam* __restrict__ params,
+// REF: every computed inner digest comes from ref (cache / fresh) and the
+// repr + SHA-256 path is not compiled in: 175 -> 135 VGPRs, and with a
+// 4-waves/SIMD bound 128 (9 spilled), outer-message-only hashing 3.54 ->
+// 3.42 ms at C2.  Tried and not kept: the two hex slots in LDS instead of 32
+// VGPRs (104 VGPRs, still 4 waves: 3.59 ms, the ds_reads cost more than the
+// registers), 5 or 6 waves/SIMD (107 / 137 VGPRs spilled: 4.53 / 6.87 ms).
+template <bool REF, int MINW>
+__global__ __launch_bounds__(HASH_NT, MINW) void k_hash(const DevParam* __restrict__ params,
                                                   const int32_t* __restrict__ order,
                                                   const int32_t* __restrict__ order_col,
                                                   const uint2* __restrict__ words,
@@ -269,7 +276,7 @@ __global__ __launch_bounds__(HASH_NT) void k_hash(const DevParam* __restrict__ p
                                                   const double* __restrict__ values, int64_t ld, int64_t m,
                                                   const uint4* __restrict__ perm_dig,
                                                   uint32_t* __restrict__ out, InnerRef ref) {
-  __shared__ uint32_t lds[SCR_WORDS * HASH_NT];
+  __shared__ uint32_t lds[REF ? 1 : SCR_WORDS * HASH_NT];
   const int lane = threadIdx.x;
   // grid-stride over candidate blocks (launch_hash gives one block per 128
   // candidates; a smaller grid stays correct)
@@ -277,7 +284,7 @@ __global__ __launch_bounds__(HASH_NT) void k_hash(const DevParam* __restrict__ p
     const int64_t i0 = blk * HASH_NT + lane;
     const bool valid = i0 < m;
     const int64_t i = valid ? i0 : (m - 1);
-    const int64_t t = ref.cache ? (int64_t)((uint64_t)(ref.cand_base + i) % (uint64_t)ref.npop) : 0;
+    const int64_t t = REF ? (int64_t)((uint64_t)(ref.cand_base + i) % (uint64_t)ref.npop) : 0;
     hex32 HX = {};  // two 16-word hex slots: hole j in HX[16 (j % 2) .. 16 (j % 2) + 15]
     uint32_t H[8];
     sha256_init(H);
@@ -303,7 +310,7 @@ __global__ __launch_bounds__(HASH_NT) void k_hash(const DevParam* __restrict__ p
           if (next + 1 < P) vnext = values[(int64_t)order_col[next + 1] * ld + i];
           D[0] = a.x; D[1] = a.y; D[2] = a.z; D[3] = a.w;
           D[4] = c.x; D[5] = c.y; D[6] = c.z; D[7] = c.w;
-        } else if (ref.cache) {
+        } else if constexpr (REF) {
           // the target's cached digest, or this trial's fresh one (k_inner_pairs)
           const uint32_t mw = ref.mask[(int64_t)(pr.cslot >> 5) * ld + i];
           const uint4* src = ((mw >> (pr.cslot & 31)) & 1u) ? ref.fresh + 2 * ((int64_t)pr.cslot * ld + i)
@@ -316,6 +323,7 @@ __global__ __launch_bounds__(HASH_NT) void k_hash(const DevParam* __restrict__ p
           if (next + 1 < P) vnext = values[(int64_t)order_col[next + 1] * ld + i];
           repr_digest(pr, v, lds, lane, D);
         }
+        (void)v;
         // 64 hex characters as 16 big-endian words into slot next % 2
         if (next & 1) {
 #pragma unroll
@@ -370,7 +378,8 @@ static int launch_hash_impl(ut_ctx* c, const double* values, int64_t ld, int64_t
     pd = c->perm_dig.p;
   }
   const int64_t nb = (int64_t)grid1(m, HASH_NT);
-  hipLaunchKernelGGL(k_hash, dim3((unsigned)nb), dim3(HASH_NT), 0, c->stream, s.d_params, s.d_order,
+  auto kern = ref.cache ? k_hash<true, 4> : k_hash<false, 1>;
+  hipLaunchKernelGGL(kern, dim3((unsigned)nb), dim3(HASH_NT), 0, c->stream, s.d_params, s.d_order,
                      s.d_order_col, reinterpret_cast<const uint2*>(s.d_words), s.d_block_last,
                      (int32_t)s.outer_blocks, s.P, reinterpret_cast<const uint4*>(s.d_lut), values, ld, m,
                      reinterpret_cast<const uint4*>(pd), out, ref);

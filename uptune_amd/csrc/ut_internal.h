@@ -124,9 +124,12 @@ struct ut_ctx {
   hipEvent_t ev_fit_x = nullptr;     // fit stream: scaled training inputs ready (K* may start)
   bool fit_pending = false;          // scoring waits on ev_fit before touching GP state
   // round schedule: 1 = the variance GEMM waits for the side stream's hash +
-  // dedup (they share CUs with K* only), 0 = only the finalize waits (the hash
-  // may spill into the variance GEMM).  UT_JOIN_BEFORE_VAR overrides.
-  int32_t join_before_var = 0;
+  // dedup (they share CUs with K* only, and the variance GEMM runs alone),
+  // 0 = only the finalize waits (the hash may spill into the variance GEMM).
+  // Measured at C2: 28.2 vs 27.95 ms per round, variance GEMM 0.80 vs 0.74 of
+  // the fp64 peak (it shares CUs with the tail of the hash).  1 is the
+  // default; UT_JOIN_BEFORE_VAR=0 selects the other schedule.
+  int32_t join_before_var = 1;
   double* fit_host = nullptr;        // pinned staging of X, y, 1/ell for the asynchronous fit
   size_t fit_host_n = 0;
   std::string err;
