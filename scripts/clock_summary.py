@@ -9,8 +9,9 @@ import json
 import sys
 from collections import defaultdict
 
-KERNELS = {"var": "void ut::k_gp_var<double>", "kstar": "void ut::k_gp_kstar<double, false>", "hash": "ut::k_hash",
-           "propose": "ut::k_de(", "var16": "_ZN2ut11k_gp_var_h3", "kstar16": "_ZN2ut10k_gp_kstarIDF16_"}
+KERNELS = {"var": ("ut::k_gp_var_pp(", "void ut::k_gp_var<double>"), "kstar": ("void ut::k_gp_kstar<double, false>",),
+           "hash": ("void ut::k_hash<", "ut::k_hash("), "propose": ("void ut::k_de<", "ut::k_de("),
+           "var16": ("_ZN2ut11k_gp_var_h3",), "kstar16": ("_ZN2ut10k_gp_kstarIDF16_",)}
 
 
 def main(d, n_cu=256, peak_ghz=2.4):
@@ -23,8 +24,8 @@ def main(d, n_cu=256, peak_ghz=2.4):
     out = {"_note": "clock_ghz = GRBM_GUI_ACTIVE / 8 / duration; mfma_busy = SQ_VALU_MFMA_BUSY_CYCLES / "
                     "(4 SIMDs x CUs x clock cycles of the kernel); profiled passes run ~2-5% slower "
                     "(MI355X_MICROARCH.md DVFS item 2)"}
-    for key, prefix in KERNELS.items():
-        ds = [v for v in rows.values() if v["_name"].startswith(prefix)]
+    for key, prefixes in KERNELS.items():
+        ds = [v for v in rows.values() if v["_name"].startswith(prefixes)]
         if not ds:
             continue
         clk = [v["GRBM_GUI_ACTIVE"] / 8 / v["_ns"] for v in ds]           # cycles per ns = GHz

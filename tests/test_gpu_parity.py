@@ -351,7 +351,10 @@ def test_gp_f16x3_scaling(sf2, ell, sn2, tier):
 def test_topk_matches_oracle():
     e = engine([Param("x", FLOAT, 0.0, 1.0)])
     rng = np.random.default_rng(0)
-    for m, k in [(10, 4), (5000, 256), (100000, 1000), (2048 * 3 + 7, 17)]:
+    # power-of-two k with several re-merge passes (sorted-list fast path), and
+    # k that are not powers of two (full network every pass)
+    for m, k in [(10, 4), (5000, 256), (100000, 1000), (2048 * 3 + 7, 17), (1 << 20, 256), (600001, 64),
+                 (300000, 1024)]:
         s = np.round(rng.standard_normal(m), 2)  # many ties
         s[::97] = np.nan
         dup = (rng.uniform(size=m) < 0.1).astype(np.uint8)

@@ -186,6 +186,7 @@ int ut_ctx_create(int device, uint64_t seed, ut_ctx** out) {
   }
   c->stream = c->own_stream;
   if (const char* e = getenv("UT_JOIN_BEFORE_VAR")) c->join_before_var = atoi(e) != 0;
+  if (const char* e = getenv("UT_VAR_KERNEL")) c->var_kernel = atoi(e);
   *out = c;
   return 0;
 }
@@ -490,9 +491,7 @@ int ut_population_get(ut_ctx* c, double* values, int64_t ld) {
   return 0;
 }
 
-int ut_propose_de(ut_ctx* c, const ut_de_params* p, uint32_t round_, int64_t cand_base, int64_t m,
-                  double* out_values, int64_t ld) {
-  if (!c) return UT_EINVAL;
+static int check_de_params(ut_ctx* c, const ut_de_params* p, int64_t m, int64_t cand_base) {
   UT_CHECK(c, c->has_space, UT_ENOSPACE, "space not defined");
   UT_CHECK(c, c->pop != nullptr, UT_EINVAL, "propose_de: population not initialised");
   UT_CHECK(c, p && p->n_cross >= 0 && p->n_cross <= 4, UT_EINVAL, "propose_de: n_cross must be in [0, 4]");
@@ -500,7 +499,16 @@ int ut_propose_de(ut_ctx* c, const ut_de_params* p, uint32_t round_, int64_t can
            "propose_de: information_sharing must be in [0, 2^20]");
   UT_CHECK(c, c->npop - 1 + (p->best ? (int64_t)p->information_sharing : 0) >= 3, UT_EINVAL,
            "propose_de: the donor pool (population - target + best copies) needs >= 3 entries");
-  UT_CHECK(c, m >= 0 && cand_base >= 0 && (out_values || m == 0) && ld >= m, UT_EINVAL, "propose_de: bad arguments");
+  UT_CHECK(c, m >= 0 && cand_base >= 0, UT_EINVAL, "propose_de: bad arguments");
+  return 0;
+}
+
+int ut_propose_de(ut_ctx* c, const ut_de_params* p, uint32_t round_, int64_t cand_base, int64_t m,
+                  double* out_values, int64_t ld) {
+  if (!c) return UT_EINVAL;
+  int rc = check_de_params(c, p, m, cand_base);
+  if (rc) return rc;
+  UT_CHECK(c, (out_values || m == 0) && ld >= m, UT_EINVAL, "propose_de: bad arguments");
   if (m == 0) return 0;
   return launch_de(c, p, round_, cand_base, m, out_values, ld);
 }
@@ -697,7 +705,9 @@ static int score_round_de_impl(ut_ctx* c, const ut_de_params* de, const ut_acq* 
   c->r_ld = ld;
   c->r_m = m;
   timing_begin(c);
-  if ((rc = ut_propose_de(c, de, round_, cand_base, m, c->r_values.p, ld))) return rc;
+  // the proposal also writes the DE-diff mask / pairs the hash reuses
+  if ((rc = check_de_params(c, de, m, cand_base))) return rc;
+  if ((rc = launch_de(c, de, round_, cand_base, m, c->r_values.p, ld, true))) return rc;
   mark(c, "propose");
   // fork: hash_config + dedup on the side stream, beside encode + GP scoring
   UT_HIP(c, hipEventRecord(c->ev_fork, c->stream));
@@ -705,7 +715,7 @@ static int score_round_de_impl(ut_ctx* c, const ut_de_params* de, const ut_acq* 
   {
     StreamScope on_side(c, c->side);
     mark(c, "");
-    if ((rc = launch_hash_de(c, c->r_values.p, ld, m, cand_base, c->r_digest.p))) return rc;
+    if ((rc = launch_hash_de(c, c->r_values.p, ld, m, cand_base, c->r_digest.p, true))) return rc;
     mark(c, "hash");
     if ((rc = launch_dedup(c, c->r_digest.p, m, c->r_dup.p))) return rc;
     mark(c, "dedup");

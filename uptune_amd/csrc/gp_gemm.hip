@@ -542,6 +542,149 @@ __global__ __launch_bounds__(V_NT, 1) void k_gp_var(const T* __restrict__ AT, in
 }
 
 // ---------------------------------------------------------------------------
+// Variance contraction, fp64, "ping-pong": TWO 256-thread workgroups per CU
+// (__launch_bounds__(256, 2), 68 KiB of LDS each), so every SIMD holds one wave
+// of each and one workgroup's barrier wait, pipeline fill and epilogue overlap
+// the other's MFMAs.  k_gp_var<double> (one 512-thread workgroup per CU) puts
+// both waves of a SIMD behind the same barrier every 16 k.
+//   tile: 128 rows of L^-1 x 128 candidates, 2 x 2 waves of 64 x 64 outputs;
+//   rows interleaved by 16-row sub-tiles (wave wm owns sub-tiles 2i + wm), so
+//   in the diagonal block -- where (L^-1)^T is zero for k > row and the
+//   all-zero sub-tiles are skipped -- the two wave rows of a workgroup skip
+//   about equally (with contiguous halves the upper waves idle half of it
+//   while the barrier holds the lower ones);
+//   ring: 2 stages of 16 k (32 KiB), global_load_lds_dwordx4, 8 per wave per
+//   stage; stage kt+1 is issued right after the barrier of step kt.
+// Measured on MI355X, C2 shape (scripts/exp/var_probe.hip): 16.9 ms (0.83 of
+// the fp64 peak) against 18.1 ms for k_gp_var<double>; 0.88 without any global
+// loads, 0.93 without the triangle (full K, no loads).
+// Work items, tickets and the part / mpart layouts are k_gp_var's.
+// ---------------------------------------------------------------------------
+constexpr int VP_NT = 256, VP_BN = 128, VP_BK = 16, VP_ST = 2;
+constexpr int VP_SA = VP_BK * VAR_BM, VP_STAGE = VP_SA + VP_BK * VP_BN;
+
+__global__ __launch_bounds__(VP_NT, 2) void k_gp_var_pp(const double* __restrict__ AT, int64_t lda,
+                                                        const double* __restrict__ B, int64_t ldb, int32_t K,
+                                                        int32_t RT, int32_t CT, int64_t m,
+                                                        int32_t* __restrict__ ticket, double* __restrict__ part,
+                                                        int64_t ldp, const double* __restrict__ beta,
+                                                        double* __restrict__ mpart) {
+  // one __shared__ object (see k_gp_var): ring, reduction buffer, ticket slot
+  __shared__ __attribute__((aligned(16))) double lds[VP_ST * VP_STAGE + 4 * VP_BN + VAR_BM + 2];
+  double* red = lds + VP_ST * VP_STAGE;  // [2][128] squares, [2][128] mean
+  double* sbeta = red + 4 * VP_BN;        // beta of the item's 128 rows
+  int32_t& s_item = *reinterpret_cast<int32_t*>(sbeta + VAR_BM);
+  const int t = threadIdx.x, lane = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wm = w >> 1, wn = w & 1;
+  const int32_t xcd = blockIdx.x & 7;
+  // stage image: A [16 k][128 rows], B [16 k][128 cols]; one glds wave-instruction
+  // moves one k row (128 doubles): wave w moves A rows 4w..4w+3 and B rows 4w..4w+3
+  auto issue = [&](int32_t row0, int64_t col0, int32_t k0, double* st) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int q = 4 * w + u;
+      __builtin_amdgcn_global_load_lds(AT + (int64_t)(k0 + q) * lda + row0 + lane * 2,
+                                       (__attribute__((address_space(3))) void*)(st + q * VAR_BM), 16, 0, 0);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int q = 4 * w + u;
+      __builtin_amdgcn_global_load_lds(B + (int64_t)(k0 + q) * ldb + col0 + lane * 2,
+                                       (__attribute__((address_space(3))) void*)(st + VP_SA + q * VP_BN), 16, 0, 0);
+    }
+  };
+  for (;;) {
+    if (t == 0) s_item = atomicAdd(&ticket[xcd], 1);
+    __syncthreads();  // also: the previous item's epilogue is done with `red`
+    const int32_t j = s_item;
+    const int32_t ct = (j / RT) * 8 + xcd;
+    if (ct >= CT) break;  // uniform: every wave of the block leaves together
+    const int32_t rt = RT - 1 - (j % RT);
+    const int64_t col0 = (int64_t)ct * VP_BN;
+    const int32_t row0 = rt * VAR_BM;
+    const int32_t nk = min(K, row0 + VAR_BM) / VP_BK;
+    vd4 acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) acc[i][jj] = (vd4){0.0, 0.0, 0.0, 0.0};
+    // beta of this row tile, staged for the epilogue beside stage 0 (its load
+    // retires with stage 0's vmcnt wait; the previous epilogue's reads of
+    // sbeta ended before the ticket barrier)
+    if (w == 0)  // 128 doubles = one glds wave-instruction, asynchronous like the ring
+      __builtin_amdgcn_global_load_lds(beta + row0 + lane * 2, (__attribute__((address_space(3))) void*)sbeta, 16, 0,
+                                       0);
+    issue(row0, col0, 0, lds);
+    const int32_t nfull = min(nk, row0 / VP_BK);
+    for (int32_t kt = 0; kt < nk; ++kt) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();  // stage kt landed everywhere; stage kt-1 fully read
+      asm volatile("" ::: "memory");
+      if (kt + 1 < nk) issue(row0, col0, (kt + 1) * VP_BK, lds + ((kt + 1) & 1) * VP_STAGE);
+      const double* as = lds + (kt & 1) * VP_STAGE;
+      const double* bs = as + VP_SA;
+      // diagonal block: sub-tile i (rows (2i + wm) * 16 ..) is all zero once
+      // 16 kd >= (2i + wm + 1) * 16, i.e. for i < ceil((kd - wm) / 2); skipped
+      // terms are exact zeros
+      int imin = 0;
+      if (kt >= nfull) {
+        const int z = kt - nfull - wm;
+        imin = z <= 0 ? 0 : (z + 1) >> 1;
+      }
+      if (imin < 4) {
+#pragma unroll
+        for (int ks = 0; ks < VP_BK / 4; ++ks) {
+          const int kr = ks * 4 + (lane >> 4);
+          double af[4], bf[4];
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj) bf[jj] = bs[kr * VP_BN + wn * 64 + jj * 16 + (lane & 15)];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            if (i < imin) continue;
+            af[i] = as[kr * VAR_BM + (2 * i + wm) * 16 + (lane & 15)];
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj)
+              acc[i][jj] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[i], bf[jj], acc[i][jj], 0, 0, 0);
+          }
+        }
+      }
+    }
+    // epilogue: column sums of squares over the tile's 128 rows and the mean
+    // partial sum_r V[r][c] beta_r (beta = L^-1 y)
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+      const int cl = wn * 64 + jj * 16 + (lane & 15);
+      double s = 0.0, u = 0.0;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const double v = acc[i][jj][r];
+          s += v * v;
+          u += v * sbeta[(2 * i + wm) * 16 + (lane >> 4) + 4 * r];
+        }
+      s += __shfl_xor(s, 16);
+      s += __shfl_xor(s, 32);
+      u += __shfl_xor(u, 16);
+      u += __shfl_xor(u, 32);
+      if ((lane >> 4) == 0) {
+        red[wm * VP_BN + cl] = s;
+        red[2 * VP_BN + wm * VP_BN + cl] = u;
+      }
+    }
+    __syncthreads();
+    if (t < VP_BN) {
+      const int64_t col = col0 + t;
+      if (col < m) {
+        part[(int64_t)rt * ldp + col] = red[t] + red[VP_BN + t];
+        mpart[(int64_t)rt * ldp + col] = red[2 * VP_BN + t] + red[3 * VP_BN + t];
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Variance contraction, f16x3 ("h3"): fp32-class accuracy at the fp16 MFMA rate.
 // Both operands are split once into fp16 planes, x * 2^e = hi + lo (hi = fp16(x 2^e),
 // lo = fp16(x 2^e - hi): 22 significant bits), and each product is taken as
@@ -832,9 +975,18 @@ int launch_gemm_var(ut_ctx* c, int prec, const void* LinvT, int64_t lda, const v
   else if (fp32)
     hipLaunchKernelGGL(k_gp_var<float>, dim3(nb), dim3(V_NT), 0, c->stream, (const float*)LinvT, lda,
                        (const float*)kst, ldk, npad, RT, CT, m, c->gp_ctr, part, ldk, nullptr, nullptr);
-  else
+  else if (c->var_kernel == 1)   // UT_VAR_KERNEL=1: the one-workgroup-per-CU kernel (measurements)
     hipLaunchKernelGGL(k_gp_var<double>, dim3(nb), dim3(V_NT), 0, c->stream, (const double*)LinvT, lda,
                        (const double*)kst, ldk, npad, RT, CT, m, c->gp_ctr, part, ldk, beta, mpart);
+  else {
+    // two workgroups per CU on 128-candidate column tiles
+    const int32_t CTp = (int32_t)((m + VP_BN - 1) / VP_BN);
+    const int64_t items_p = (int64_t)RT * CTp;
+    int32_t nbp = 2 * (c->n_cu / 8) * 8;
+    if (items_p < nbp) nbp = (int32_t)(((items_p + 7) / 8) * 8);
+    hipLaunchKernelGGL(k_gp_var_pp, dim3(nbp), dim3(VP_NT), 0, c->stream, (const double*)LinvT, lda,
+                       (const double*)kst, ldk, npad, RT, CTp, m, c->gp_ctr, part, ldk, beta, mpart);
+  }
   UT_LAUNCH_CHECK(c);
   return 0;
 }

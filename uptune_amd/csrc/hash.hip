@@ -418,21 +418,30 @@ int launch_pop_digests(ut_ctx* c, const int64_t* idx, int64_t n) {
   return 0;
 }
 
-int launch_hash_de(ut_ctx* c, const double* values, int64_t ld, int64_t m, int64_t cand_base, uint32_t* out) {
+int ensure_de_diff(ut_ctx* c, int64_t ld) {
+  const Space& s = c->space;
+  const int32_t nw = (s.n_comp + 31) / 32;
+  int rc;
+  if ((rc = ensure(c, c->r_mask, (size_t)nw * ld))) return rc;
+  if ((rc = ensure(c, c->r_fresh, (size_t)s.n_comp * ld * 8))) return rc;
+  if ((rc = ensure(c, c->r_pairs, (size_t)s.n_comp * ld))) return rc;
+  return ensure(c, c->r_npairs, 1);
+}
+
+int launch_hash_de(ut_ctx* c, const double* values, int64_t ld, int64_t m, int64_t cand_base, uint32_t* out,
+                   bool have_diff) {
   const Space& s = c->space;
   if (s.n_comp == 0 || m <= 0) return launch_hash(c, values, ld, m, out);
   int rc;
   if (!c->pop_dig_valid && (rc = launch_pop_digests(c, nullptr, 0))) return rc;
-  const int32_t nw = (s.n_comp + 31) / 32;
-  if ((rc = ensure(c, c->r_mask, (size_t)nw * ld))) return rc;
-  if ((rc = ensure(c, c->r_fresh, (size_t)s.n_comp * ld * 8))) return rc;
-  if ((rc = ensure(c, c->r_pairs, (size_t)s.n_comp * ld))) return rc;
-  if ((rc = ensure(c, c->r_npairs, 1))) return rc;
-  UT_HIP(c, hipMemsetAsync(c->r_npairs.p, 0, sizeof(int64_t), c->stream));
+  if ((rc = ensure_de_diff(c, ld))) return rc;
   unsigned long long* np = reinterpret_cast<unsigned long long*>(c->r_npairs.p);
-  hipLaunchKernelGGL(k_de_diff, dim3(grid1(m, DIFF_NT)), dim3(DIFF_NT), 0, c->stream, s.d_params, s.d_comp, s.n_comp,
-                     values, ld, m, c->pop, c->npop, cand_base, c->r_mask.p, c->r_pairs.p, np);
-  UT_LAUNCH_CHECK(c);
+  if (!have_diff) {
+    UT_HIP(c, hipMemsetAsync(c->r_npairs.p, 0, sizeof(int64_t), c->stream));
+    hipLaunchKernelGGL(k_de_diff, dim3(grid1(m, DIFF_NT)), dim3(DIFF_NT), 0, c->stream, s.d_params, s.d_comp,
+                       s.n_comp, values, ld, m, c->pop, c->npop, cand_base, c->r_mask.p, c->r_pairs.p, np);
+    UT_LAUNCH_CHECK(c);
+  }
   const int64_t want = ((int64_t)s.n_comp * m + HASH_NT - 1) / HASH_NT;
   const unsigned grid = (unsigned)std::min<int64_t>(std::max<int64_t>(want, 1), (int64_t)c->n_cu * 8);
   hipLaunchKernelGGL(k_inner_pairs, dim3(grid), dim3(HASH_NT), 0, c->stream, s.d_params, s.d_comp, values, ld,

@@ -68,18 +68,47 @@ __device__ __forceinline__ void pick_donors(uint32_t w0, uint32_t w1, uint32_t w
   d3 = pool_member(c, npop, t);
 }
 
+// Fused DE-diff outputs (DE scoring rounds, ut_score_round_de): which
+// computed-digest values of the trial differ bitwise from the target's, as the
+// mask [ceil(n_comp/32)][ldo] and compacted (candidate << 20 | cslot) pairs --
+// what k_de_diff derives by re-reading both rows, taken here from registers.
+struct DeDiffOut {
+  uint32_t* mask;
+  uint64_t* pairs;
+  unsigned long long* npairs;
+  int32_t n_comp;
+};
+
 // One DE trial per candidate.  Candidate g (global) targets member g % npop.
 // Forced crossover set = the n_cross parameters with the smallest per-param
 // random keys (= the first n_cross names of a uniform shuffle,
 // differentialevolution.py:122-125).
+//
+// Each param's draw (seed, g, p, round, OP_DE) serves twice: its z word is the
+// forced-set key, its x, y words the `random() < cr` test.  The first pass
+// over the params keeps the test's outcome as one bit per param in LDS
+// ([ceil(P/32)][256] words, each lane its own column), so the second pass
+// draws nothing for the crossover decision: 1 + 1 Philox blocks per param
+// became 1 (k_de is Philox-issue-bound: ~220 VALU cycles per block).
+template <bool DIFF>
 __global__ __launch_bounds__(256) void k_de(const DevParam* __restrict__ params, int32_t P,
                                             const double* __restrict__ vtab, const double* __restrict__ pop, int64_t ldp, int64_t npop,
                                             const double* __restrict__ best, int64_t share,
                                             double cr, int32_t n_cross, uint64_t seed, uint32_t round_,
                                             int64_t cand_base, int64_t m, double* __restrict__ out,
-                                            int64_t ldo) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= m) return;
+                                            int64_t ldo, DeDiffOut dd, uint32_t* __restrict__ xglob) {
+  extern __shared__ uint32_t xlds[];  // [ceil(P/32)][256]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int64_t i0 = (int64_t)blockIdx.x * blockDim.x + tid;
+  // the bits live in LDS, or (spaces of more than 2048 params) in a global
+  // [ceil(P/32)][grid * 256] scratch
+  uint32_t* const xb = xglob ? xglob + i0 : xlds + tid;
+  const int64_t xs = xglob ? (int64_t)gridDim.x * blockDim.x : (int64_t)blockDim.x;
+  // out-of-range lanes of the last block run along (on candidate m-1) and
+  // write nothing: the DIFF epilogue takes one atomic per whole wave
+  const bool valid = i0 < m;
+  if (!DIFF && !valid) return;
+  const int64_t i = valid ? i0 : m - 1;
   const uint64_t g = (uint64_t)(cand_base + i);
   const int64_t t = (int64_t)(g % (uint64_t)npop);
   const u32x4 rc = draw(seed, g, STREAM_CAND | 0u, round_, OP_DE);
@@ -90,11 +119,17 @@ __global__ __launch_bounds__(256) void k_de(const DevParam* __restrict__ params,
   const double F = __dadd_rn(__ddiv_rn(u01_from(rf.x, rf.y), 2.0), 0.5);
   const double nF = -F;
 
-  // forced set: up to 4 smallest (key, p)
+  // pass 1: forced set (up to 4 smallest (key, p)) and the cr-test bits
   uint64_t fk[4] = {~0ull, ~0ull, ~0ull, ~0ull};
-  if (n_cross > 0) {
+  {
+    uint32_t acc = 0;
     for (int32_t p = 0; p < P; ++p) {
       const u32x4 r = draw(seed, g, (uint32_t)p, round_, OP_DE);
+      if (u01_from(r.x, r.y) < cr) acc |= 1u << (p & 31);
+      if ((p & 31) == 31 || p == P - 1) {
+        xb[(p >> 5) * xs] = acc;
+        acc = 0;
+      }
       uint64_t key = ((uint64_t)r.z << 32) | (uint32_t)p;
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
@@ -105,17 +140,22 @@ __global__ __launch_bounds__(256) void k_de(const DevParam* __restrict__ params,
     }
   }
 
+  uint32_t xw = 0;                  // the cr-test bits of params [32 (p>>5), +32)
+  uint32_t dw = 0;                  // DIFF: mask bits of the current word
+  int32_t dwi = 0;                  // DIFF: its word index
+  uint32_t dcnt = 0;                // DIFF: changed computed-digest values
   for (int32_t p = 0; p < P; ++p) {
     const DevParam pr = params[p];
-    const u32x4 r = draw(seed, g, (uint32_t)p, round_, OP_DE);
+    if ((p & 31) == 0) xw = xb[(p >> 5) * xs];
     bool forced = false;
 #pragma unroll
     for (int s = 0; s < 4; ++s) forced |= (s < n_cross) && ((uint32_t)fk[s] == (uint32_t)p) && (fk[s] != ~0ull);
     const double* col = pop + (int64_t)pr.col * ldp;
     // `i < n_cross or random() < cr` (short-circuit: the draw is only
     // consulted for non-forced params, which is what selecting on it does)
-    const bool cross = forced || u01_from(r.x, r.y) < cr;
+    const bool cross = forced || ((xw >> (p & 31)) & 1u);
     if (pr.kind == UT_PERM) {
+      if (!valid) continue;  // no computed digest (cslot -1): nothing for the DIFF epilogue
       // ComplexParameter.op4_set_linear: copy x1, shuffle it iff x2 != x3
       const int32_t S = pr.psize;
       WRow o{out + (int64_t)pr.col * ldo + i, ldo};
@@ -156,7 +196,48 @@ __global__ __launch_bounds__(256) void k_de(const DevParam* __restrict__ params,
         }
       }
     }
-    out[(int64_t)pr.col * ldo + i] = v;
+    if (valid) out[(int64_t)pr.col * ldo + i] = v;
+    if constexpr (DIFF) {
+      // cslots are assigned in param order, so the mask words fill in order
+      const int32_t cs = pr.cslot;
+      if (cs >= 0) {
+        if ((cs >> 5) != dwi) {
+          if (valid) dd.mask[(int64_t)dwi * ldo + i] = dw;
+          dw = 0;
+          dwi = cs >> 5;
+        }
+        if (__double_as_longlong(v) != __double_as_longlong(vt)) {
+          dw |= 1u << (cs & 31);
+          ++dcnt;
+        }
+      }
+    }
+  }
+  if constexpr (DIFF) {
+    if (dd.n_comp <= 0) return;
+    if (valid) dd.mask[(int64_t)dwi * ldo + i] = dw;
+    if (!valid) dcnt = 0;
+    // one atomic per wave for the wave's pair count, then the pairs slot-major
+    // within the wave (ballot + mbcnt: each store instruction writes one
+    // contiguous run, and k_inner_pairs sees mostly one param per wave)
+    uint32_t tot = dcnt;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) tot += __shfl_xor(tot, d, 64);
+    unsigned long long base = 0;
+    if (lane == 0 && tot) base = atomicAdd(dd.npairs, (unsigned long long)tot);
+    base = __shfl(base, 0, 64);
+    if (!tot) return;
+    const uint64_t lt = (1ull << lane) - 1ull;   // lanes below this one
+    for (int32_t w = 0; w * 32 < dd.n_comp; ++w) {
+      const uint32_t bits = valid ? dd.mask[(int64_t)w * ldo + i] : 0u;
+      const int32_t hi = dd.n_comp - w * 32 < 32 ? dd.n_comp - w * 32 : 32;
+      for (int32_t b = 0; b < hi; ++b) {
+        const bool on = (bits >> b) & 1u;
+        const uint64_t bal = __ballot(on);
+        if (on) dd.pairs[base + __popcll(bal & lt)] = ((uint64_t)i << 20) | (uint64_t)(w * 32 + b);
+        base += __popcll(bal);
+      }
+    }
   }
 }
 
@@ -453,11 +534,31 @@ int launch_population_init(ut_ctx* c, uint32_t round_) {
 }
 
 int launch_de(ut_ctx* c, const ut_de_params* p, uint32_t round_, int64_t cand_base, int64_t m, double* out,
-              int64_t ld) {
-  hipLaunchKernelGGL(k_de, dim3(grid1(m, 256)), dim3(256), 0, c->stream, c->space.d_params, c->space.P,
-                     c->space.d_vtab, c->pop,
-                     c->npop, c->npop, p->best, p->best ? (int64_t)p->information_sharing : (int64_t)0, p->cr,
-                     p->n_cross, c->seed, round_, cand_base, m, out, ld);
+              int64_t ld, bool diff) {
+  constexpr int NT = 256;
+  const unsigned grid = grid1(m, NT);
+  const int32_t nw = (c->space.P + 31) / 32;
+  size_t lds = sizeof(uint32_t) * (size_t)nw * NT;
+  uint32_t* xg = nullptr;
+  if (nw > 64) {  // > 2048 params: the cr-test bits go to a global scratch
+    const int rc = ensure(c, c->de_xbits, (size_t)nw * grid * NT);
+    if (rc) return rc;
+    xg = c->de_xbits.p;
+    lds = 0;
+  }
+  DeDiffOut dd{nullptr, nullptr, nullptr, 0};
+  diff = diff && c->space.n_comp > 0;
+  if (diff) {
+    const int rc = ensure_de_diff(c, ld);
+    if (rc) return rc;
+    UT_HIP(c, hipMemsetAsync(c->r_npairs.p, 0, sizeof(int64_t), c->stream));
+    dd = DeDiffOut{c->r_mask.p, c->r_pairs.p, reinterpret_cast<unsigned long long*>(c->r_npairs.p),
+                   c->space.n_comp};
+  }
+  hipLaunchKernelGGL(diff ? k_de<true> : k_de<false>, dim3(grid), dim3(NT), lds, c->stream, c->space.d_params,
+                     c->space.P, c->space.d_vtab, c->pop, c->npop, c->npop, p->best,
+                     p->best ? (int64_t)p->information_sharing : (int64_t)0, p->cr, p->n_cross, c->seed, round_,
+                     cand_base, m, out, ld, dd, xg);
   UT_LAUNCH_CHECK(c);
   return 0;
 }

@@ -6,6 +6,10 @@
 // Each 256-thread workgroup bitonic-sorts a 2048-entry chunk in LDS
 // ((score, index) pairs, index -1 = invalid) and keeps its best k; passes
 // repeat on the survivors until one chunk remains.  k <= 1024.
+// A re-merge pass (mode 1) reads whole sorted lists of k from the pass before;
+// for a power-of-two k it loads every odd list reversed, which makes the chunk
+// the state of the network after its level-k stage, and starts at level 2k
+// (k = 256: 30 compare-exchange phases instead of 66).
 #include "ut_internal.h"
 
 namespace ut {
@@ -32,8 +36,14 @@ __global__ __launch_bounds__(TK_NT) void k_topk_chunk(const double* __restrict__
   __shared__ int64_t si[TK_CH];
   const int t = threadIdx.x;
   const int64_t base = (int64_t)blockIdx.x * TK_CH;
+  // mode 1, k a power of two: the chunk holds 2048 / k sorted lists (best
+  // first; invalid entries last, whole padding lists invalid)
+  const bool runs = MODE == 1 && (k & (k - 1)) == 0 && k >= 2;
   for (int e = t; e < TK_CH; e += TK_NT) {
-    const int64_t p = base + e;
+    // odd lists enter reversed: alternating best-first / worst-first runs are
+    // exactly the network's state after its size-k level
+    const int src = (runs && ((e / k) & 1)) ? (e / k) * k + (k - 1 - e % k) : e;
+    const int64_t p = base + src;
     double s = 0.0;
     int64_t ix = -1;
     if (p < count) {
@@ -48,7 +58,7 @@ __global__ __launch_bounds__(TK_NT) void k_topk_chunk(const double* __restrict__
     ss[e] = s;
     si[e] = ix;
   }
-  for (int size = 2; size <= TK_CH; size <<= 1) {
+  for (int size = runs ? 2 * k : 2; size <= TK_CH; size <<= 1) {
     for (int stride = size >> 1; stride > 0; stride >>= 1) {
       __syncthreads();
       for (int q = t; q < TK_CH / 2; q += TK_NT) {

@@ -130,6 +130,9 @@ struct ut_ctx {
   // the fp64 peak (it shares CUs with the tail of the hash).  1 is the
   // default; UT_JOIN_BEFORE_VAR=0 selects the other schedule.
   int32_t join_before_var = 1;
+  // fp64 variance kernel: 0 = k_gp_var_pp (two 4-wave workgroups per CU, the
+  // default), 1 = k_gp_var<double> (one 8-wave workgroup per CU); UT_VAR_KERNEL
+  int32_t var_kernel = 0;
   double* fit_host = nullptr;        // pinned staging of X, y, 1/ell for the asynchronous fit
   size_t fit_host_n = 0;
   std::string err;
@@ -226,6 +229,7 @@ struct ut_ctx {
   ut::DevBuf<uint32_t> r_fresh;     // [n_comp][ld][8]: inner digests of the changed values
   ut::DevBuf<uint64_t> r_pairs;     // compacted (candidate << 20 | cslot) of the changed values
   ut::DevBuf<int64_t> r_npairs;     // [1] their count
+  ut::DevBuf<uint32_t> de_xbits;    // k_de's cr-test bits when they outgrow LDS (> 2048 params)
   // EI-bound pruned scoring (gp.hip ut_gp_topk_pruned)
   ut::DevBuf<double> pr_mu, pr_ub, pr_score;   // [ld] exact mean, score bound, exact scores (-inf if pruned)
   ut::DevBuf<double> pr_mpart;                 // [RT][ldk] unused mean partials of the bound / survivor GEMMs
@@ -311,8 +315,10 @@ int gp_wait_fit(ut_ctx* c);
 
 // kernel launchers implemented in the .hip translation units
 int launch_population_init(ut_ctx* c, uint32_t round_);
+// diff = true (DE scoring rounds): k_de also writes the DE-diff mask, pairs and
+// pair count (r_mask / r_pairs / r_npairs) that launch_hash_de would derive
 int launch_de(ut_ctx* c, const ut_de_params* p, uint32_t round_, int64_t cand_base, int64_t m, double* out,
-              int64_t ld);
+              int64_t ld, bool diff = false);
 int launch_pso(ut_ctx* c, const ut_pso_params* a, const double* gbest, uint32_t round_, int64_t cand_base,
                int64_t m, double* out_x, double* out_v, int64_t ld);
 int launch_ga(ut_ctx* c, const ut_ga_params* a, const double* parent1, const double* parent2, uint32_t round_,
@@ -322,7 +328,11 @@ int launch_hash(ut_ctx* c, const double* values, int64_t ld, int64_t m, uint32_t
 // hash_config of DE trials of the selected population (candidate g targets
 // member g % npop): inner digests of values equal to the target's come from
 // the population cache (rebuilt if stale), the rest are computed once
-int launch_hash_de(ut_ctx* c, const double* values, int64_t ld, int64_t m, int64_t cand_base, uint32_t* out);
+// have_diff: the mask / pairs / count were written by k_de (launch_de diff = true)
+int launch_hash_de(ut_ctx* c, const double* values, int64_t ld, int64_t m, int64_t cand_base, uint32_t* out,
+                   bool have_diff = false);
+// the DE-diff buffers for m candidates (ld): r_mask, r_fresh, r_pairs, r_npairs
+int ensure_de_diff(ut_ctx* c, int64_t ld);
 // population cache maintenance: full rebuild, or the rows idx[0..n) after a replace
 int launch_pop_digests(ut_ctx* c, const int64_t* idx, int64_t n);
 int launch_hist_insert(ut_ctx* c, const uint32_t* dig, int64_t n);
