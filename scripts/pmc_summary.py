@@ -16,16 +16,25 @@ import shutil
 import sys
 from collections import defaultdict
 
-STAGES = {  # stage key -> kernel-name prefix
-    "var": "void ut::k_gp_var<double>", "kstar": "void ut::k_gp_kstar<double, false>",
-    "var32": "void ut::k_gp_var<float>", "kstar32": "void ut::k_gp_kstar<float, true>", "hash": "ut::k_hash",
-    "propose": "ut::k_de(", "encode": "ut::k_encode", "finalize": "ut::k_gp_finalize",
-    "dedup_insert": "ut::k_batch_insert", "dedup_mark": "ut::k_dedup_mark",
-    "topk0": "void ut::k_topk_chunk<0>", "pso": "ut::k_pso(", "ga": "ut::k_ga(",
+STAGES = {  # stage key -> kernel-name prefixes (the first match wins)
+    "var": ("ut::k_gp_var_pp(", "void ut::k_gp_var<double>"), "var_1wg": ("void ut::k_gp_var<double>",),
+    "kstar": ("void ut::k_gp_kstar<double, false>",),
+    "var32": ("void ut::k_gp_var<float>",), "kstar32": ("void ut::k_gp_kstar<float, true>",),
+    "hash": ("void ut::k_hash<true", "void ut::k_hash<", "ut::k_hash("),
+    "propose": ("void ut::k_de<", "ut::k_de("), "encode": ("ut::k_encode",), "prep_cand": ("ut::k_gp_prep_cand",),
+    "finalize": ("ut::k_gp_finalize",),
+    "dedup_insert": ("ut::k_batch_insert",), "dedup_mark": ("ut::k_dedup_mark",),
+    "topk0": ("void ut::k_topk_chunk<0>",), "topk1": ("void ut::k_topk_chunk<1>",), "pso": ("ut::k_pso(",),
+    "ga": ("ut::k_ga(",),
     # rocprofv3 leaves the _Float16 instantiations mangled
-    "var16": "_ZN2ut11k_gp_var_h3", "kstar16": "_ZN2ut10k_gp_kstarIDF16_",
-    "inner_pairs": "ut::k_inner_pairs", "de_diff": "ut::k_de_diff", "pop_digests": "ut::k_pop_digests",
+    "var16": ("_ZN2ut11k_gp_var_h3",), "kstar16": ("_ZN2ut10k_gp_kstarIDF16_",),
+    "inner_pairs": ("ut::k_inner_pairs",), "de_diff": ("ut::k_de_diff",), "pop_digests": ("ut::k_pop_digests",),
 }
+# stages of the default C2 round that a refreshed C2 profile replaces (a key
+# absent from the new profile -- e.g. de_diff, now folded into k_de -- is dropped)
+C2_ROUND = ("var", "var_1wg", "kstar", "hash", "propose", "encode", "prep_cand", "finalize", "dedup_insert",
+            "dedup_mark", "topk0", "topk1", "inner_pairs", "de_diff", "pop_digests")
+
 
 
 def per_kernel(path, counter):
@@ -50,10 +59,14 @@ def main(prof, tag):
             stats[row["Name"]] = row
     summary = {"_note": "bytes per launch; read = 2 x FETCH_SIZE x 1024 (gfx950 correction, MI355X_MICROARCH.md "
                         "§HBM), write = WRITE_SIZE x 1024; raw counters kept. source: " + tag}
-    for key, prefix in STAGES.items():
-        kf = [k for k in fetch if k.startswith(prefix)]
-        kw = [k for k in write if k.startswith(prefix)]
-        ks = [k for k in stats if k.startswith(prefix)]
+    for key, prefixes in STAGES.items():
+        def first(names):
+            for pre in prefixes:
+                hit = [k for k in names if k.startswith(pre)]
+                if hit:
+                    return hit
+            return []
+        kf, kw, ks = first(fetch), first(write), first(stats)
         if not (kf and kw):
             continue
         fr, wr = fetch[kf[0]], write[kw[0]]
@@ -71,6 +84,9 @@ def main(prof, tag):
             merged = json.load(f)
     except Exception:
         pass
+    if "var" in summary:
+        for k in C2_ROUND:
+            merged.pop(k, None)
     merged.update({k: v for k, v in summary.items() if k != "_note"})
     merged["_note"] = summary["_note"] if "var" in summary else merged.get("_note", summary["_note"])
     with open(os.path.join(out_dir, "pmc_summary.json"), "w") as f:
