@@ -721,7 +721,16 @@ static int score_round_de_impl(ut_ctx* c, const ut_de_params* de, const ut_acq* 
     mark(c, "dedup");
     UT_HIP(c, hipEventRecord(c->ev_join, c->side));
   }
-  if ((rc = launch_encode(c, c->r_values.p, ld, m, c->r_feat.p, ld))) return rc;
+  // dense rounds encode straight into the K* operand (features * 1/ell and
+  // their norms); the pruned round keeps the features, which it gathers for
+  // its threshold set and survivors
+  if (prune_rows > 0) {
+    if ((rc = launch_encode(c, c->r_values.p, ld, m, c->r_feat.p, ld))) return rc;
+    c->r_feat_valid = true;
+  } else {
+    if ((rc = gp_encode_scaled(c, c->r_values.p, ld, m))) return rc;
+    c->r_feat_valid = false;
+  }
   mark(c, "encode");
   if (prune_rows > 0) {
     // pruned: only candidates whose score bound reaches the threshold get the
@@ -731,7 +740,7 @@ static int score_round_de_impl(ut_ctx* c, const ut_de_params* de, const ut_acq* 
       return rc;
   } else {
     // join before the finalize kernel, which masks duplicates
-    if ((rc = gp_score_impl(c, c->r_feat.p, ld, m, acq, c->r_dup.p, c->r_mu.p, c->r_var.p, c->r_score.p,
+    if ((rc = gp_score_impl(c, nullptr, ld, m, acq, c->r_dup.p, c->r_mu.p, c->r_var.p, c->r_score.p,
                             c->ev_join)))
       return rc;
     if ((rc = topk_impl(c, c->r_score.p, c->r_dup.p, m, cand_base, k, c->r_topk_idx.p, c->r_topk_score.p)))
@@ -763,7 +772,7 @@ int ut_round_buffers(ut_ctx* c, double** values, double** features, uint32_t** d
                      double** mu, double** var, double** score, int64_t* ld) {
   if (!c) return UT_EINVAL;
   if (values) *values = c->r_values.p;
-  if (features) *features = c->r_feat.p;
+  if (features) *features = c->r_feat_valid ? c->r_feat.p : nullptr;   // dense rounds keep no feature matrix
   if (digests) *digests = c->r_digest.p;
   if (dup) *dup = c->r_dup.p;
   if (mu) *mu = c->r_mu.p;

@@ -578,6 +578,19 @@ int gp_wait_fit(ut_ctx* c) {
   return 0;
 }
 
+int gp_encode_scaled(ut_ctx* c, const double* values, int64_t ld, int64_t m) {
+  UT_CHECK(c, c->gp_ready, UT_EINVAL, "gp_score: call ut_gp_fit first");
+  if (m <= 0) return 0;
+  // 1/ell comes with the fit's scaled training inputs
+  if (c->fit_pending) UT_HIP(c, hipStreamWaitEvent(c->stream, c->ev_fit_x, 0));
+  const int32_t dpad = ((c->gp_d + 15) / 16) * 16;
+  const int64_t ldk = ((m + VAR_BN - 1) / VAR_BN) * VAR_BN;   // as gp_score_impl
+  int rc;
+  if ((rc = ensure(c, c->cnorm, (size_t)ldk))) return rc;
+  if ((rc = ensure(c, c->ucand, (size_t)dpad * ldk))) return rc;
+  return launch_encode_scaled(c, values, ld, m, c->ucand.p, dpad, ldk, c->cnorm.p);
+}
+
 int gp_score_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, const ut_acq* acq, const uint8_t* dup,
                   double* mu, double* var, double* score, hipEvent_t dup_ready) {
   UT_CHECK(c, c->gp_ready, UT_EINVAL, "gp_score: call ut_gp_fit first");
@@ -604,8 +617,10 @@ int gp_score_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, const ut
   if ((rc = ensure(c, c->var_part, (size_t)RT * ldk))) return rc;
   if ((rc = ensure(c, c->cnorm, (size_t)ldk))) return rc;
   if ((rc = ensure(c, c->ucand, (size_t)dpad * ldk))) return rc;
-  if ((rc = launch_prep_cand(c, feat, ld, m, d, dpad, c->ucand.p, ldk, c->cnorm.p))) return rc;
-  mark(c, "cnorm");
+  if (feat) {
+    if ((rc = launch_prep_cand(c, feat, ld, m, d, dpad, c->ucand.p, ldk, c->cnorm.p))) return rc;
+    mark(c, "cnorm");
+  }
   if ((rc = launch_gemm_kstar(c, prec, c->gp_XsT, npad, c->ucand.p, dpad, m, c->kst.p, ldk,
                               fp32 ? c->mu_part.p : nullptr)))
     return rc;

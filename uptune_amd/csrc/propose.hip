@@ -241,32 +241,64 @@ __global__ __launch_bounds__(256) void k_de(const DevParam* __restrict__ params,
   }
 }
 
-// GP features of a configuration.
+// GP features of a configuration: emit(feature column, value) for each feature
+// of param pr at candidate i (every column of the param is emitted)
+template <class Emit>
+__device__ __forceinline__ void encode_param(const DevParam& pr, const double* __restrict__ values, int64_t ld,
+                                             int64_t i, const double* __restrict__ vtab, Emit&& emit) {
+  const double v = values[(int64_t)pr.col * ld + i];
+  if (is_primitive(pr.kind)) {
+    emit(pr.feat_col, unit_of(pr, v, vtab));
+  } else if (pr.kind == UT_BOOL) {
+    emit(pr.feat_col, v);
+  } else if (pr.kind == UT_PERM) {
+    // position of each item, normalised: feature[item] = k / (S - 1)
+    const int32_t S = pr.psize;
+    for (int32_t k = 0; k < S; ++k) {
+      int32_t item = (int32_t)values[(int64_t)(pr.col + k) * ld + i];
+      item = item < 0 ? 0 : (item >= S ? S - 1 : item);  // never fault on garbage input
+      emit(pr.feat_col + item, S > 1 ? (double)k / (double)(S - 1) : 0.0);
+    }
+  } else {
+    const int64_t o = (int64_t)v;
+    for (int64_t k = 0; k < pr.n_opt; ++k) emit(pr.feat_col + (int32_t)k, (k == o) ? 1.0 : 0.0);
+  }
+}
+
 __global__ __launch_bounds__(256) void k_encode(const DevParam* __restrict__ params, int32_t P,
                                                 const double* __restrict__ vtab, const double* __restrict__ values, int64_t ld, int64_t m,
                                                 double* __restrict__ feat, int64_t ldf) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= m) return;
-  for (int32_t p = 0; p < P; ++p) {
-    const DevParam pr = params[p];
-    const double v = values[(int64_t)pr.col * ld + i];
-    if (is_primitive(pr.kind)) {
-      feat[(int64_t)pr.feat_col * ldf + i] = unit_of(pr, v, vtab);
-    } else if (pr.kind == UT_BOOL) {
-      feat[(int64_t)pr.feat_col * ldf + i] = v;
-    } else if (pr.kind == UT_PERM) {
-      // position of each item, normalised: feature[item] = k / (S - 1)
-      const int32_t S = pr.psize;
-      for (int32_t k = 0; k < S; ++k) {
-        int32_t item = (int32_t)values[(int64_t)(pr.col + k) * ld + i];
-        item = item < 0 ? 0 : (item >= S ? S - 1 : item);  // never fault on garbage input
-        feat[(int64_t)(pr.feat_col + item) * ldf + i] = S > 1 ? (double)k / (double)(S - 1) : 0.0;
-      }
-    } else {
-      const int64_t o = (int64_t)v;
-      for (int64_t k = 0; k < pr.n_opt; ++k) feat[(int64_t)(pr.feat_col + k) * ldf + i] = (k == o) ? 1.0 : 0.0;
-    }
+  for (int32_t p = 0; p < P; ++p)
+    encode_param(params[p], values, ld, i, vtab, [&](int32_t c, double f) { feat[(int64_t)c * ldf + i] = f; });
+}
+
+// k_encode and k_gp_prep_cand in one pass (dense scoring rounds): the K* B
+// operand U'[k][i] = feature_k / ell_k straight from the values (0 for k >= F
+// and for the padding columns i >= m) and cnorm[i] = |u'_i|^2, summed in
+// feature order as k_gp_prep_cand sums (a PERM's items in position order).
+// Saves the feature matrix's write and re-read (2 x 8 F bytes per candidate).
+__global__ __launch_bounds__(256) void k_encode_scaled(const DevParam* __restrict__ params, int32_t P,
+                                                       const double* __restrict__ vtab,
+                                                       const double* __restrict__ values, int64_t ld, int64_t m,
+                                                       int32_t F, const double* __restrict__ inv_ell, int32_t dpad,
+                                                       double* __restrict__ u, int64_t ldu, double* __restrict__ cn) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= ldu) return;
+  double s = 0.0;
+  if (i < m) {
+    for (int32_t p = 0; p < P; ++p)
+      encode_param(params[p], values, ld, i, vtab, [&](int32_t c, double f) {
+        const double v = f * inv_ell[c];
+        u[(int64_t)c * ldu + i] = v;
+        s += v * v;
+      });
+  } else {
+    for (int32_t k = 0; k < F; ++k) u[(int64_t)k * ldu + i] = 0.0;
   }
+  for (int32_t k = F; k < dpad; ++k) u[(int64_t)k * ldu + i] = 0.0;
+  cn[i] = s;
 }
 
 __global__ void k_gather_rows(int32_t NC, const double* __restrict__ values, int64_t ld,
@@ -597,6 +629,14 @@ int launch_ga(ut_ctx* c, const ut_ga_params* a, const double* parent1, const dou
 int launch_encode(ut_ctx* c, const double* values, int64_t ld, int64_t m, double* feat, int64_t ldf) {
   hipLaunchKernelGGL(k_encode, dim3(grid1(m, 256)), dim3(256), 0, c->stream, c->space.d_params, c->space.P,
                      c->space.d_vtab, values, ld, m, feat, ldf);
+  UT_LAUNCH_CHECK(c);
+  return 0;
+}
+
+int launch_encode_scaled(ut_ctx* c, const double* values, int64_t ld, int64_t m, double* u, int32_t dpad, int64_t ldu,
+                         double* cn) {
+  hipLaunchKernelGGL(k_encode_scaled, dim3(grid1(ldu, 256)), dim3(256), 0, c->stream, c->space.d_params, c->space.P,
+                     c->space.d_vtab, values, ld, m, c->space.n_feat, c->gp_inv_ell, dpad, u, ldu, cn);
   UT_LAUNCH_CHECK(c);
   return 0;
 }

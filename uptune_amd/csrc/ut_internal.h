@@ -239,6 +239,7 @@ struct ut_ctx {
   ut::DevBuf<int64_t> pr_count;                // [1]
   int64_t r_ld = 0;
   int64_t r_m = 0;
+  bool r_feat_valid = false;        // r_feat holds the last round's features (pruned rounds only)
 
   // tree-ensemble surrogate (forest.hip)
   ut_tree_node* forest_nodes = nullptr;
@@ -338,8 +339,14 @@ int launch_pop_digests(ut_ctx* c, const int64_t* idx, int64_t n);
 int launch_hist_insert(ut_ctx* c, const uint32_t* dig, int64_t n);
 int launch_hist_rehash(ut_ctx* c, const uint32_t* okeys, const uint32_t* ostate, int64_t ocap);
 int launch_dedup(ut_ctx* c, const uint32_t* dig, int64_t m, uint8_t* dup);
+// feat == nullptr: the candidates' scaled features and norms are already in
+// c->ucand / c->cnorm (gp_encode_scaled)
 int gp_score_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, const ut_acq* acq, const uint8_t* dup,
                   double* mu, double* var, double* score, hipEvent_t dup_ready = nullptr);
+// encode + scale in one pass into c->ucand / c->cnorm (sized for m), for gp_score_impl(feat = nullptr)
+int gp_encode_scaled(ut_ctx* c, const double* values, int64_t ld, int64_t m);
+int launch_encode_scaled(ut_ctx* c, const double* values, int64_t ld, int64_t m, double* u, int32_t dpad, int64_t ldu,
+                         double* cn);
 int topk_impl(ut_ctx* c, const double* score, const uint8_t* dup, int64_t m, int64_t cand_base, int32_t k,
               int64_t* out_idx, double* out_score);
 int gp_topk_pruned_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, const ut_acq* acq, const uint8_t* dup,
