@@ -21,7 +21,7 @@ STAGES = {  # stage key -> kernel-name prefixes (the first match wins)
     "kstar": ("void ut::k_gp_kstar<double, false>",),
     "var32": ("void ut::k_gp_var<float>",), "kstar32": ("void ut::k_gp_kstar<float, true>",),
     "hash": ("void ut::k_hash<true", "void ut::k_hash<", "ut::k_hash("),
-    "propose": ("void ut::k_de<", "ut::k_de("), "encode": ("ut::k_encode",), "prep_cand": ("ut::k_gp_prep_cand",),
+    "propose": ("void ut::k_de<", "ut::k_de("), "encode": ("ut::k_encode_scaled", "ut::k_encode("), "prep_cand": ("ut::k_gp_prep_cand",),
     "finalize": ("ut::k_gp_finalize",),
     "dedup_insert": ("ut::k_batch_insert",), "dedup_mark": ("ut::k_dedup_mark",),
     "topk0": ("void ut::k_topk_chunk<0>",), "topk1": ("void ut::k_topk_chunk<1>",), "pso": ("ut::k_pso(",),
