@@ -407,6 +407,38 @@ def test_score_round_de_small():
         assert idx_l == want
 
 
+def test_score_round_de_best_row_digests():
+    """the scoring round's fused DE-diff (k_de writes the changed-value mask and
+    pairs the hash reuses) with the best config in the donor pool, before and
+    after a population replace: every selected row's values and digest equal
+    the oracle's trial and hash_config"""
+    space = mixed_space()
+    seed, npop, m, k = 31, 300, 4000, 1024
+    e = engine(space, seed=seed)
+    pop = ode.population_init(space, npop, seed=seed)
+    e.population_set(dev(pop))
+    X = features(space, pop[:, :100]).T
+    e.gp_fit(X, np.sum((X - 0.5) ** 2, axis=1), lengthscale=0.7, sigma_f2=1.0, sigma_n2=1e-6, jitter=1e-8)
+    e.history_reset(0)
+    best = ode.population_init(space, 1, seed=5)[:, 0]
+    for rnd, base in ((4, 7), (5, 4007)):
+        idx, top, dig, vals = e.score_round_de(m, k, round_=rnd, cand_base=base, cr=0.5, best=best,
+                                               information_sharing=3)
+        trial = ode.propose_de_vec(space, pop, seed, rnd, base, m, 0.5, 1, best=best, information_sharing=3)
+        e.sync()
+        idx_l = idx.cpu().numpy().tolist()
+        sel = [g - base for g in idx_l]
+        assert all(0 <= j < m for j in sel)
+        np.testing.assert_array_equal(vals.cpu().numpy(), trial[:, sel])
+        assert hexes(dig) == oracle_hashes(space, trial[:, sel])
+        # accept the first 64 selections into the population (rows 0..63): the
+        # next round reuses the patched inner-digest cache
+        rows = np.arange(64)
+        e.population_replace(vals[:, :64].contiguous(), dev(rows.astype(np.int64)))
+        pop = pop.copy()
+        pop[:, rows] = trial[:, sel[:64]]
+
+
 def test_sharding_invariance():
     """top-k over a pool split into shards (global candidate indices) and
     merged equals the single-shot top-k -- the multi-GPU contract."""
