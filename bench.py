@@ -324,7 +324,7 @@ def main():
     peak = {64: PEAK_FP64_TFLOPS, 32: PEAK_FP32_TFLOPS, 16: PEAK_FP16_TFLOPS / 3.0}[args.precision]
     # HBM bytes per launch and the rocprof average duration were profiled on the
     # default C2 round (profiles/pmc_summary.json)
-    profiled = args.config == "c2" and (m, n, d) == (1 << 20, 1024, 64)
+    profiled = args.config == "c2" and (m, n, d) == (1 << 20, 1024, 64) and not args.prune
     pmc, pmc_note = load_pmc({64: "var", 32: "var32", 16: "var16"}[args.precision]) if profiled else ({}, "")
     traffic = pmc.get("hbm_bytes_per_launch")
     frac_rocprof = (flops_var / (pmc["avg_ns"] * 1e-9) / 1e12 / peak) if pmc.get("avg_ns") else None

@@ -40,6 +40,8 @@ def main():
     ap.add_argument("--population", type=int, default=4096)
     ap.add_argument("--backend", default="nccl")
     ap.add_argument("--precision", type=int, default=64, choices=(64, 32, 16))
+    ap.add_argument("--prune", type=int, default=0, metavar="ROWS",
+                    help="score technique rounds with the selection-exact EI-bound pruning (fp64)")
     args = ap.parse_args()
 
     import torch
@@ -59,7 +61,7 @@ def main():
     t0 = time.perf_counter()
     drv = tune_bandit(spaces.r64(), rosenbrock64, generations=args.generations, parallelism=args.parallelism,
                       n_init=args.n_init, pool=args.pool, batch=args.batch, population=args.population, seed=1,
-                      lengthscale=0.3, device=local, precision=args.precision)
+                      lengthscale=0.3, device=local, precision=args.precision, prune_rows=args.prune)
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
     techs = drv.root_technique.techniques
@@ -79,13 +81,17 @@ def main():
         v = eng.propose_de(args.pool, round_=10000 + r, cand_base=0)
         dg = eng.hash_de(v, 0)
         dup = eng.dedup(dg)
-        _, _, sc = eng.gp_score(eng.encode(v), acq=acq, dup=dup)
-        eng.topk(sc, args.batch, dup=dup)
+        if args.prune:
+            eng.gp_topk_pruned(eng.encode(v), args.batch, acq=acq, dup=dup, bound_rows=args.prune)
+        else:
+            _, _, sc = eng.gp_score(eng.encode(v), acq=acq, dup=dup)
+            eng.topk(sc, args.batch, dup=dup)
         torch.cuda.synchronize()
         rr.append(time.perf_counter() - t1)
     round_rate = args.pool / min(rr)
     n_train = len(drv.results_query())
-    out = {"config": "C5 AUC bandit over GPU DE+PSO+GA+GGA, shared GP, Rosenbrock-64", "n_gpus": world,
+    out = {"config": "C5 AUC bandit over GPU DE+PSO+GA+GGA, shared GP, Rosenbrock-64"
+                     + (f", EI-bound pruned ({args.prune} rows)" if args.prune else ""), "n_gpus": world,
            "generations": drv.generation, "evaluations": len(drv.results) - args.n_init,
            "initial_design": args.n_init, "best": drv.best_result.time if drv.best_result else None,
            "wall_s": wall, "technique_rounds": rounds, "rounds_per_s": sum(rounds.values()) / wall,

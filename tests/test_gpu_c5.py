@@ -65,3 +65,20 @@ def test_c5_two_ranks_equal_one_rank():
     assert [r.time for r in ref.results.values()] == out[0][2]
     assert len(ref.results) > KW["n_init"] + 20
     assert ref.best_result.time < min(t for t in out[0][2][:KW["n_init"]])   # the search improved on the design
+
+
+@pytest.mark.parametrize("lengthscale", [0.5, 0.05])
+def test_c5_pruned_scoring_equals_dense(lengthscale):
+    """the bandit loop with every technique round scored by ut_gp_topk_pruned
+    (selection-exact) evaluates the same configurations, in the same order,
+    as with the dense variance -- for an informative GP (ell 0.5) and a flat
+    one (ell 0.05: k* ~ 0 far from the data, scores tie and are broken by
+    index inside the pruning)"""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from uptune_amd.tuner import tune_bandit
+    kw = dict(KW, lengthscale=lengthscale)
+    dense = tune_bandit(_manip(), _obj, pool=4096, **kw)
+    pruned = tune_bandit(_manip(), _obj, pool=4096, prune_rows=128, **kw)
+    assert list(pruned.results.keys()) == list(dense.results.keys())
+    assert [r.time for r in pruned.results.values()] == [r.time for r in dense.results.values()]

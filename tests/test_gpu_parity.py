@@ -778,11 +778,11 @@ def test_gp_topk_pruned_equals_dense(acq, bound_rows):
         assert idx.cpu().numpy().tolist() == i2.cpu().numpy().tolist() == want
 
 
-def test_gp_topk_pruned_degenerate_and_fallback():
-    """far-away candidates (k* underflows to 0 everywhere): every score is the
-    same, so every bound reaches the threshold (ties are broken by index and
-    cannot be pruned): the round falls back to the dense variance and still
-    selects exactly the dense top-k"""
+def test_gp_topk_pruned_degenerate_exact_ties():
+    """far-away candidates (k* ~ 0 everywhere): every score is the same.  The
+    tail bound |L^-1|_F^2 |k*|^2 proves each candidate's variance from the first
+    row tile (exact flag), so ties are broken by index in the pruning itself:
+    exactly k survivors, and the dense top-k"""
     space = r64_space()
     e = engine(space, seed=3)
     e.population_init(8192)
@@ -792,11 +792,31 @@ def test_gp_topk_pruned_degenerate_and_fallback():
     e.gp_fit(X, y, lengthscale=0.2)
     vals = e.propose_de(8192, round_=1)
     feat = e.encode(vals)
-    idx, top, st = e.gp_topk_pruned(feat, 32, bound_rows=128)
+    for base in (0, 1000):
+        idx, top, st = e.gp_topk_pruned(feat, 32, bound_rows=128, cand_base=base)
+        _, _, score = e.gp_score(feat)
+        i2, t2 = e.topk(score, 32, cand_base=base)
+        assert idx.cpu().numpy().tolist() == i2.cpu().numpy().tolist() == list(range(base, base + 32))
+        assert not st["dense"] and st["survivors"] == 32, st
+
+
+def test_gp_topk_pruned_dense_fallback():
+    """every candidate at the same training point: identical scores whose
+    variance the tail bound cannot pin (k* ~ sf2), so every bound reaches the
+    threshold, the round falls back to the dense variance, and the selection
+    is still the dense top-k (the smallest indices)"""
+    space = r64_space()
+    e = engine(space, seed=3)
+    rng = np.random.default_rng(9)
+    X = rng.uniform(size=(512, 64))
+    y = rng.standard_normal(512)
+    e.gp_fit(X, y, lengthscale=0.5)
+    feat = dev(np.repeat(X[5:6].T, 4096, axis=1))
+    idx, top, st = e.gp_topk_pruned(feat, 16, bound_rows=128)
     _, _, score = e.gp_score(feat)
-    i2, t2 = e.topk(score, 32)
-    assert idx.cpu().numpy().tolist() == i2.cpu().numpy().tolist() == list(range(32))
-    assert st["dense"] and st["survivors"] == 8192
+    i2, t2 = e.topk(score, 16)
+    assert idx.cpu().numpy().tolist() == i2.cpu().numpy().tolist() == list(range(16))
+    assert st["dense"] and st["survivors"] == 4096, st
 
 
 def test_score_round_de_pruned_equals_dense_round():

@@ -206,6 +206,7 @@ int ut_ctx_destroy(ut_ctx* c) {
   fr(c->r_mask.p); fr(c->r_fresh.p); fr(c->r_pairs.p); fr(c->r_npairs.p); fr(c->de_xbits.p);
   fr(c->pr_mu.p); fr(c->pr_ub.p); fr(c->pr_score.p); fr(c->pr_mpart.p); fr(c->pr_kst.p); fr(c->pr_vpart.p);
   fr(c->pr_idx.p); fr(c->pr_count.p); fr(c->pr_ucand.p); fr(c->pr_cnorm.p);
+  fr(c->pr_k2.p); fr(c->pr_f2.p); fr(c->pr_exact.p);
   fr(c->hist_keys); fr(c->hist_state); fr(c->batch_slots);
   fr(c->gp_Xs); fr(c->gp_xnorm); fr(c->gp_K); fr(c->gp_Linv); fr(c->gp_y); fr(c->gp_tmp);
   fr(c->gp_alpha); fr(c->gp_beta); fr(c->gp_inv_ell); fr(c->gp_stats); fr(c->gp_flag); fr(c->gp_Xs_f); fr(c->gp_T);

@@ -493,6 +493,7 @@ int gp_fit_enqueue(ut_ctx* c, const double* X, const double* y, int32_t n, int32
   const int32_t npad = ((n + NPAD - 1) / NPAD) * NPAD;
   int rc = gp_alloc(c, npad, d);
   if (rc) return rc;
+  c->pr_f2_valid = false;   // |L^-1|_F^2 (pruned scoring) belongs to the previous factor
   // pinned staging (the previous fit's copies out of it are complete once ev_fit is)
   const size_t need = (size_t)n * d + n + d;
   if (c->fit_pending) UT_HIP(c, hipEventSynchronize(c->ev_fit));
@@ -653,27 +654,80 @@ int gp_score_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, const ut
 //   monotone, so var_exact <= var_bound holds in floating point too; the score
 //   bound gets a 1e-12 relative margin for the acquisition's own rounding.
 // ---------------------------------------------------------------------------
+// The score bound of a candidate from the first RTv row tiles of the
+// variance contraction.  The mean is exact (every row's k* went into it).
+//   var_ub = sf2 - S_R, S_R = the sum of the first RTv partials; the score of
+//   var_ub, raised by a 1e-12 relative margin for the rounding of the
+//   acquisition function, bounds the exact score from above.
+//   Exactness test: the rows past the bound contribute at most
+//   T = sum_{r >= R} v_r^2 <= |L^-1|_F^2 |k*|^2 (|v_r| <= |L^-1_r| |k*|), the
+//   computed partials at most 1.001 T, and the exact path's running sum starts
+//   from the same S_R (its first RTv partials are bitwise these) and only adds
+//   non-negative terms, so its var lies in [max(sf2 - S_hi, 0), var_ub] with
+//   S_hi = (S_R + 1.001 T)(1 + 2^-40).  When both ends round to the same double
+//   the exact var IS var_ub, and so is the exact score: it is stored without
+//   the margin and flagged exact, and ties with it can be broken by index
+//   (a flat GP -- every k* ~ 0 -- gives every candidate the same score).
 __global__ void k_prune_bound(int64_t m, int32_t RTm, const double* __restrict__ mu_part, int32_t RTv,
                               const double* __restrict__ var_part, int64_t ldp, double sf2,
                               const double* __restrict__ stats, const int32_t* __restrict__ fit_flag, int32_t kind,
                               double xi, double kappa, const uint8_t* __restrict__ dup, double* __restrict__ mu_out,
-                              double* __restrict__ ub_out) {
+                              double* __restrict__ ub_out, const double* __restrict__ k2_part,
+                              const double* __restrict__ linv_f2, uint8_t* __restrict__ exact_out) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= m) return;
-  double mu = 0.0, vs = 0.0;
+  double mu = 0.0, vs = 0.0, k2 = 0.0;
   for (int32_t r = 0; r < RTm; ++r) mu += mu_part[(int64_t)r * ldp + i];
   for (int32_t r = 0; r < RTv; ++r) vs += var_part[(int64_t)r * ldp + i];
   double var = sf2 - vs;
   var = var > 0.0 ? var : 0.0;
   double ub = acq_score(kind, mu, var, stats[0], xi, kappa);
-  ub = ub + fabs(ub) * 1e-12 + 1e-300;
-  if (*fit_flag != 0) mu = ub = __builtin_nan("");
+  bool exact = false;
+  if (k2_part && RTv < RTm) {
+    for (int32_t r = 0; r < RTm; ++r) k2 += k2_part[(int64_t)r * ldp + i];
+    const double tail = 1.001 * (*linv_f2) * k2;
+    const double s_hi = (vs + tail) * (1.0 + 0x1p-40);
+    double var_lo = sf2 - s_hi;
+    var_lo = var_lo > 0.0 ? var_lo : 0.0;
+    exact = tail == tail && var_lo == var;   // (NaN tail: not exact)
+  } else if (RTv >= RTm) {
+    exact = true;   // the bound GEMM covered every row
+  }
+  if (!exact) ub = ub + fabs(ub) * 1e-12 + 1e-300;
+  if (*fit_flag != 0) {
+    mu = ub = __builtin_nan("");
+    exact = false;
+  }
   if (dup && dup[i]) ub = -1.0 / 0.0;
   mu_out[i] = mu;
   ub_out[i] = ub;
+  if (exact_out) exact_out[i] = exact ? 1 : 0;
 }
 
-// out[r][j] = src[r][idx[j] - base] for j < n (idx < 0: 0), zero columns up to ldo
+// sum of squares of cnt doubles (|L^-1|_F^2), deterministic: pass 1 writes one
+// partial per block (grid-stride), pass 2 (one block) adds them in order
+constexpr int SQ_BLOCKS = 1024;
+__global__ __launch_bounds__(256) void k_sumsq_part(const double* __restrict__ x, int64_t cnt,
+                                                    double* __restrict__ part) {
+  __shared__ double red[4];
+  double s = 0.0;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < cnt; e += (int64_t)gridDim.x * 256) s += x[e] * x[e];
+  for (int d = 32; d > 0; d >>= 1) s += __shfl_xor(s, d, 64);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) part[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+__global__ __launch_bounds__(256) void k_sumsq_final(const double* __restrict__ part, int32_t n,
+                                                     double* __restrict__ out) {
+  __shared__ double red[4];
+  double s = 0.0;
+  for (int32_t e = threadIdx.x; e < n; e += 256) s += part[e];
+  for (int d = 32; d > 0; d >>= 1) s += __shfl_xor(s, d, 64);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) *out = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
 __global__ void k_gather_cols(const double* __restrict__ kst, int64_t ldk, const int64_t* __restrict__ idx,
                                   int64_t base, int64_t n, int64_t ldo, double* __restrict__ out) {
   const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -712,12 +766,25 @@ __global__ void k_prune_exact(int64_t n, const int64_t* __restrict__ idx, int64_
 
 // survivors: bound >= tau (tau = the k-th best exact score of the threshold
 // set, a device scalar); appended with one atomic per wave
+// survivors: candidates that may be in the top-k.  An exact candidate (its
+// stored score is its exact score) survives iff (score, -index) >= (tau,
+// -tau_index), the k-th best pair of the threshold set -- a lower bound on the
+// k-th best pair overall; any other survives iff its bound >= tau.
 __global__ void k_prune_survivors(int64_t m, const double* __restrict__ ub, const double* __restrict__ tau_p,
-                                  int64_t* __restrict__ out, unsigned long long* __restrict__ count) {
+                                  const int64_t* __restrict__ tau_idx_p, const uint8_t* __restrict__ exact,
+                                  int64_t cand_base, int64_t* __restrict__ out, unsigned long long* __restrict__ count) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int lane = threadIdx.x & 63;
   const double tau = *tau_p;
-  const bool keep = i < m && ub[i] >= tau;
+  const int64_t tau_g = *tau_idx_p;
+  bool keep = false;
+  if (i < m) {
+    const double b = ub[i];
+    if (exact && exact[i])
+      keep = b > tau || (b == tau && (tau_g < 0 || cand_base + i <= tau_g));
+    else
+      keep = b >= tau;
+  }
   const unsigned long long ball = __ballot(keep);
   const uint32_t n = __builtin_popcountll(ball);
   unsigned long long base = 0;
@@ -759,6 +826,9 @@ int gp_topk_pruned_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, co
   if ((rc = ensure(c, c->pr_score, (size_t)ldk + 2048))) return rc;   // + the threshold set's two [1024] arrays
   if ((rc = ensure(c, c->pr_idx, (size_t)ldk + 2048))) return rc;
   if ((rc = ensure(c, c->pr_count, 1))) return rc;
+  if ((rc = ensure(c, c->pr_k2, (size_t)RT * ldk))) return rc;
+  if ((rc = ensure(c, c->pr_f2, 1 + SQ_BLOCKS))) return rc;   // [0] the norm, [1..] block partials
+  if ((rc = ensure(c, c->pr_exact, (size_t)ldk))) return rc;
   const double* LinvT = c->gp_LinvT;
   // 1. K* with the mean in its epilogue, 2. the first R row tiles of L^-1 K*^T
   if ((rc = launch_prep_cand(c, feat, ld, m, d, dpad, c->ucand.p, ldk, c->cnorm.p))) return rc;
@@ -766,8 +836,17 @@ int gp_topk_pruned_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, co
   // candidates that need every row (threshold set, survivors) get their K*
   // columns recomputed from their features (recompute_cols below): cheaper than
   // writing and re-reading the whole n x m matrix
-  if ((rc = launch_gemm_kstar(c, 64, c->gp_XsT, npad, c->ucand.p, dpad, m, c->kst.p, ldk, c->mu_part.p, R * NPAD)))
+  if ((rc = launch_gemm_kstar(c, 64, c->gp_XsT, npad, c->ucand.p, dpad, m, c->kst.p, ldk, c->mu_part.p, R * NPAD,
+                              nullptr, c->pr_k2.p)))
     return rc;
+  // |L^-1|_F^2 for the variance tail bound, once per fit
+  if (!c->pr_f2_valid) {
+    hipLaunchKernelGGL(k_sumsq_part, dim3(SQ_BLOCKS), dim3(256), 0, c->stream, c->gp_Linv, (int64_t)npad * npad,
+                       c->pr_f2.p + 1);
+    hipLaunchKernelGGL(k_sumsq_final, dim3(1), dim3(256), 0, c->stream, c->pr_f2.p + 1, SQ_BLOCKS, c->pr_f2.p);
+    UT_LAUNCH_CHECK(c);
+    c->pr_f2_valid = true;
+  }
   mark(c, "kstar");
   if ((rc = launch_gemm_var(c, 64, LinvT, npad, c->kst.p, ldk, R * NPAD, m, c->var_part.p, c->gp_beta,
                             c->pr_mpart.p)))
@@ -776,7 +855,7 @@ int gp_topk_pruned_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, co
   if (dup_ready) UT_HIP(c, hipStreamWaitEvent(c->stream, dup_ready, 0));   // the dup mask (side stream)
   hipLaunchKernelGGL(k_prune_bound, dim3(grid1(m, 256)), dim3(256), 0, c->stream, m, RT, c->mu_part.p, R,
                      c->var_part.p, ldk, c->gp_sf2, c->gp_stats, c->gp_flag, acq->kind, acq->xi, acq->kappa, dup,
-                     c->pr_mu.p, c->pr_ub.p);
+                     c->pr_mu.p, c->pr_ub.p, c->pr_k2.p, c->pr_f2.p, c->pr_exact.p);
   UT_LAUNCH_CHECK(c);
   // 3. threshold: exact scores of the best 1024 bounds, tau = their k-th best
   const int32_t kp = (int32_t)(m < 1024 ? m : 1024);
@@ -811,11 +890,13 @@ int gp_topk_pruned_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, co
   UT_LAUNCH_CHECK(c);
   int64_t* tk_i = out_idx;   // the caller's [k] outputs hold tau's top-k for now
   double* tk_s = out_score;
-  if ((rc = topk_impl(c, tex, nullptr, kp, 0, k, tk_i, tk_s))) return rc;
+  // tau: the k-th best (exact score, global index) pair of the threshold set
+  if ((rc = topk_pairs_impl(c, tex, tset, kp, k, tk_i, tk_s))) return rc;
   // 4. survivors: bound >= tau
   UT_HIP(c, hipMemsetAsync(c->pr_count.p, 0, sizeof(int64_t), c->stream));
   hipLaunchKernelGGL(k_prune_survivors, dim3(grid1(m, 256)), dim3(256), 0, c->stream, m, c->pr_ub.p, tk_s + (k - 1),
-                     c->pr_idx.p, reinterpret_cast<unsigned long long*>(c->pr_count.p));
+                     tk_i + (k - 1), c->pr_exact.p, cand_base, c->pr_idx.p,
+                     reinterpret_cast<unsigned long long*>(c->pr_count.p));
   UT_LAUNCH_CHECK(c);
   int64_t ns = 0;
   double tau = 0.0;

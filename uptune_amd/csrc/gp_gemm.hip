@@ -88,7 +88,9 @@ __global__ __launch_bounds__(K_NT, 2) void k_gp_kstar(const double* __restrict__
                                                       const double* __restrict__ alpha, double sf2, int32_t n,
                                                       int64_t m, int32_t* __restrict__ ticket, TS* __restrict__ kst,
                                                       int64_t ldk, double* __restrict__ part, double kscale,
-                                                      int64_t lo_off, int32_t store_rt) {
+                                                      int64_t lo_off, int32_t store_rt, double* __restrict__ part2) {
+  // part2 (MU, fp64/fp32 only; pruned scoring): the column partial sum_r k*_r^2
+  // as well, for the tail bound of the variance (gp.hip k_prune_bound)
   // TS = _Float16 (h3): k* * kscale split into fp16 hi + lo, stored candidate-major
   // [col][row] (ld = npad = RT * K_BM) so the variance MFMA reads k-contiguous
   // fragments; the lo plane starts lo_off elements after the hi plane
@@ -177,11 +179,12 @@ __global__ __launch_bounds__(K_NT, 2) void k_gp_kstar(const double* __restrict__
       const double cr = cnorm[col];
       hc[jj] = col < m ? -0.5 * cr : -1e300;
     }
+    const bool want2 = !H3 && MU && part2 != nullptr;
 #pragma unroll
     for (int jj = 0; jj < 4; ++jj) {
       const int cl = wn * 64 + jj * 16 + (lane & 15);
       const int64_t col = col0 + cl;
-      double s = 0.0;
+      double s = 0.0, s2 = 0.0;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
 #pragma unroll
@@ -200,19 +203,28 @@ __global__ __launch_bounds__(K_NT, 2) void k_gp_kstar(const double* __restrict__
             if (rt < store_rt) kst[(int64_t)row * ldk + col] = (TS)ks;   // pruned scoring stores the bound rows only
           }
           if constexpr (MU) s += al[i][r] * ks;
+          if constexpr (MU && !H3) s2 += ks * ks;
         }
       }
       if constexpr (MU) {
         s += __shfl_xor(s, 16);
         s += __shfl_xor(s, 32);
         if ((lane >> 4) == 0) red[wm * K_BN + cl] = s;
+        if (want2) {
+          s2 += __shfl_xor(s2, 16);
+          s2 += __shfl_xor(s2, 32);
+          if ((lane >> 4) == 0) red[2 * K_BN + wm * K_BN + cl] = s2;
+        }
       }
     }
     if constexpr (MU || H3) __syncthreads();
     if constexpr (MU) {
       if (t < K_BN) {
         const int64_t col = col0 + t;
-        if (col < m) part[(int64_t)rt * ldk + col] = red[t] + red[K_BN + t];
+        if (col < m) {
+          part[(int64_t)rt * ldk + col] = red[t] + red[K_BN + t];
+          if (want2) part2[(int64_t)rt * ldk + col] = red[2 * K_BN + t] + red[3 * K_BN + t];
+        }
       }
     }
     if constexpr (H3) {
@@ -233,7 +245,8 @@ __global__ __launch_bounds__(K_NT, 2) void k_gp_kstar(const double* __restrict__
 int h3_kstar_exp(double sf2) { return H3_KSCALE_EXP - ilogb(sf2); }  // sf2 * 2^e < 2^15
 
 int launch_gemm_kstar(ut_ctx* c, int prec, const double* XsT, int32_t npad, const double* ucand, int32_t dpad,
-                      int64_t m, void* kst, int64_t ldk, double* part, int32_t store_rows, const double* cn) {
+                      int64_t m, void* kst, int64_t ldk, double* part, int32_t store_rows, const double* cn,
+                      double* part2) {
   UT_CHECK(c, npad % K_BM == 0 && dpad % K_BK == 0 && ldk % K_BN == 0 && ldk >= m, UT_EINVAL,
            "gemm_kstar: bad padding");
   UT_CHECK(c, prec == 64 || prec == 32 || prec == 16, UT_EINVAL, "gemm_kstar: bad precision");
@@ -258,19 +271,20 @@ int launch_gemm_kstar(ut_ctx* c, int prec, const double* XsT, int32_t npad, cons
   if (prec == 16)
     hipLaunchKernelGGL((k_gp_kstar<_Float16, true>), dim3(nb), dim3(K_NT), 0, c->stream, XsT, (int64_t)npad, ucand, ldk,
                        dpad, RT, CT, c->gp_xnorm, cn ? cn : c->cnorm.p, c->gp_alpha, c->gp_sf2, c->gp_n, m, c->gp_ctr + 8,
-                       (_Float16*)kst, ldk, part, ldexp(1.0, h3_kstar_exp(c->gp_sf2)), ldk * (int64_t)npad, RT);
+                       (_Float16*)kst, ldk, part, ldexp(1.0, h3_kstar_exp(c->gp_sf2)), ldk * (int64_t)npad, RT,
+                       nullptr);
   else if (prec == 32)
     hipLaunchKernelGGL((k_gp_kstar<float, true>), dim3(nb), dim3(K_NT), 0, c->stream, XsT, (int64_t)npad, ucand, ldk, dpad,
                        RT, CT, c->gp_xnorm, cn ? cn : c->cnorm.p, c->gp_alpha, c->gp_sf2, c->gp_n, m, c->gp_ctr + 8,
-                       (float*)kst, ldk, part, 1.0, (int64_t)0, RT);
+                       (float*)kst, ldk, part, 1.0, (int64_t)0, RT, nullptr);
   else if (part)   // fp64 with the mean k* . alpha in the epilogue (pruned scoring: needs the whole fit)
     hipLaunchKernelGGL((k_gp_kstar<double, true>), dim3(nb), dim3(K_NT), 0, c->stream, XsT, (int64_t)npad, ucand, ldk, dpad,
                        RT, CT, c->gp_xnorm, cn ? cn : c->cnorm.p, c->gp_alpha, c->gp_sf2, c->gp_n, m, c->gp_ctr + 8,
-                       (double*)kst, ldk, part, 1.0, (int64_t)0, store_rt);
+                       (double*)kst, ldk, part, 1.0, (int64_t)0, store_rt, part2);
   else
     hipLaunchKernelGGL((k_gp_kstar<double, false>), dim3(nb), dim3(K_NT), 0, c->stream, XsT, (int64_t)npad, ucand, ldk, dpad,
                        RT, CT, c->gp_xnorm, cn ? cn : c->cnorm.p, c->gp_alpha, c->gp_sf2, c->gp_n, m, c->gp_ctr + 8,
-                       (double*)kst, ldk, part, 1.0, (int64_t)0, store_rt);
+                       (double*)kst, ldk, part, 1.0, (int64_t)0, store_rt, nullptr);
   UT_LAUNCH_CHECK(c);
   return 0;
 }

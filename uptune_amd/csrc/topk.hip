@@ -25,7 +25,8 @@ __device__ __forceinline__ bool better(double sa, int64_t ia, double sb, int64_t
 }
 
 // mode 0: input = raw scores (+ dup mask), index = cand_base + position
-// mode 1: input = (score, index) pairs
+// mode 1: input = (score, index) pairs, sorted lists of k from a previous pass
+// mode 2: input = (score, index) pairs in any order
 template <int MODE>
 __global__ __launch_bounds__(TK_NT) void k_topk_chunk(const double* __restrict__ in_s,
                                                       const int64_t* __restrict__ in_i,
@@ -53,6 +54,7 @@ __global__ __launch_bounds__(TK_NT) void k_topk_chunk(const double* __restrict__
       } else {
         ix = in_i[p];
       }
+      if (ix < 0) ix = -1;
       if (s != s) ix = -1;  // NaN never selected
     }
     ss[e] = s;
@@ -80,6 +82,40 @@ __global__ __launch_bounds__(TK_NT) void k_topk_chunk(const double* __restrict__
     out_s[(int64_t)blockIdx.x * k + e] = ss[e];
     out_i[(int64_t)blockIdx.x * k + e] = si[e];
   }
+}
+
+// the top-k of explicit (score, index) pairs (index -1 = invalid), ties broken
+// by the smallest index: the re-merge passes from the start
+int topk_pairs_impl(ut_ctx* c, const double* score, const int64_t* idx, int64_t n, int32_t k, int64_t* out_idx,
+                    double* out_score) {
+  UT_CHECK(c, k >= 1 && k <= TK_CH / 2, UT_EINVAL, "topk: k must be in [1, 1024]");
+  int64_t count = n < 1 ? 1 : n;
+  int64_t chunks = (count + TK_CH - 1) / TK_CH;
+  int rc;
+  if ((rc = ensure(c, c->tk_score[0], (size_t)chunks * k))) return rc;
+  if ((rc = ensure(c, c->tk_idx[0], (size_t)chunks * k))) return rc;
+  if ((rc = ensure(c, c->tk_score[1], (size_t)chunks * k))) return rc;
+  if ((rc = ensure(c, c->tk_idx[1], (size_t)chunks * k))) return rc;
+  // first pass: whole network (the input is not made of sorted lists)
+  hipLaunchKernelGGL(k_topk_chunk<2>, dim3((unsigned)chunks), dim3(TK_NT), 0, c->stream, score, idx, nullptr, n, 0, k,
+                     c->tk_score[0].p, c->tk_idx[0].p);
+  UT_LAUNCH_CHECK(c);
+  int cur = 0;
+  count = chunks * k;
+  while (chunks > 1) {
+    chunks = (count + TK_CH - 1) / TK_CH;
+    hipLaunchKernelGGL(k_topk_chunk<1>, dim3((unsigned)chunks), dim3(TK_NT), 0, c->stream, c->tk_score[cur].p,
+                       c->tk_idx[cur].p, nullptr, count, 0, k, c->tk_score[cur ^ 1].p, c->tk_idx[cur ^ 1].p);
+    UT_LAUNCH_CHECK(c);
+    cur ^= 1;
+    count = chunks * k;
+  }
+  if (out_idx)
+    UT_HIP(c, hipMemcpyAsync(out_idx, c->tk_idx[cur].p, sizeof(int64_t) * k, hipMemcpyDeviceToDevice, c->stream));
+  if (out_score)
+    UT_HIP(c, hipMemcpyAsync(out_score, c->tk_score[cur].p, sizeof(double) * k, hipMemcpyDeviceToDevice,
+                             c->stream));
+  return 0;
 }
 
 int topk_impl(ut_ctx* c, const double* score, const uint8_t* dup, int64_t m, int64_t cand_base, int32_t k,

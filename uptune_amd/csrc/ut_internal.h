@@ -237,6 +237,10 @@ struct ut_ctx {
   ut::DevBuf<double> pr_ucand, pr_cnorm;       // survivors' scaled features [dpad][lds] and norms [lds]
   ut::DevBuf<int64_t> pr_idx;                  // [ld] survivor indices (+ the threshold set)
   ut::DevBuf<int64_t> pr_count;                // [1]
+  ut::DevBuf<double> pr_k2;                    // [RT][ldk] partials of |k*|^2 (the variance tail bound)
+  ut::DevBuf<double> pr_f2;                    // [1] |L^-1|_F^2 (+ its block partials)
+  bool pr_f2_valid = false;                    // pr_f2 belongs to the current fit
+  ut::DevBuf<uint8_t> pr_exact;                // [ld] the stored score is the exact score
   int64_t r_ld = 0;
   int64_t r_m = 0;
   bool r_feat_valid = false;        // r_feat holds the last round's features (pruned rounds only)
@@ -349,6 +353,8 @@ int launch_encode_scaled(ut_ctx* c, const double* values, int64_t ld, int64_t m,
                          double* cn);
 int topk_impl(ut_ctx* c, const double* score, const uint8_t* dup, int64_t m, int64_t cand_base, int32_t k,
               int64_t* out_idx, double* out_score);
+int topk_pairs_impl(ut_ctx* c, const double* score, const int64_t* idx, int64_t n, int32_t k, int64_t* out_idx,
+                    double* out_score);
 int gp_topk_pruned_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, const ut_acq* acq, const uint8_t* dup,
                         int64_t cand_base, int32_t k, int32_t bound_rows, int64_t* out_idx, double* out_score,
                         ut_prune_stats* stats, hipEvent_t dup_ready = nullptr);
@@ -358,7 +364,8 @@ constexpr int H3_KSCALE_EXP = 14;  // K* (<= sf2) is scaled by 2^(14 - ceil(log2
 int h3_kstar_exp(double sf2);
 int launch_gemm_kstar(ut_ctx* c, int prec, const double* XsT, int32_t npad, const double* ucand, int32_t dpad,
                       int64_t m, void* kst, int64_t ldk, double* part, int32_t store_rows = -1,
-                      const double* cn = nullptr);   // candidate norms (nullptr: c->cnorm)
+                      const double* cn = nullptr,    // candidate norms (nullptr: c->cnorm)
+                      double* part2 = nullptr);      // fp64 with part: also sum_r k*_r^2 partials
 int launch_prep_cand(ut_ctx* c, const double* feat, int64_t ld, int64_t m, int32_t d, int32_t dpad, double* u,
                      int64_t ldu, double* cn);
 int launch_xs_t(ut_ctx* c, const double* Xs, int32_t npad, int32_t d, int32_t dpad, double* XsT);

@@ -378,8 +378,13 @@ class GpuBatchTechnique(SearchTechnique):
     def __init__(self, pool: int = 1 << 14, batch: int = 8, population: int = 1024, device: int = 0,
                  seed: int = 0, lengthscale: float = 0.3, min_train: int = 4, acq: str = "ei",
                  group=None, surrogate=None, shared: Optional[SharedModel] = None, engine_factory=None,
-                 *pargs, **kwargs):
+                 prune_rows: int = 0, *pargs, **kwargs):
         super().__init__(*pargs, **kwargs)
+        # prune_rows > 0: score rounds with ut_gp_topk_pruned (selection-exact EI
+        # bound from the first prune_rows rows of L^-1 k*; fp64 fits, EI / UCB):
+        # the same selections as the dense variance at a fraction of its cost
+        # when the bounds are tight (or the GP is flat: exact ties by index)
+        self.prune_rows = int(prune_rows)
         # surrogate: None = the GP fitted on the driver's results (EI / UCB); or a
         # tree ensemble over the same features (sklearn regressor, XGBoost JSON,
         # forest.Forest) ranking candidates by predicted objective (minimised),
@@ -468,6 +473,11 @@ class GpuBatchTechnique(SearchTechnique):
                 eng.forest_set(self.surrogate)
             _, score = eng.forest_predict(eng.encode(vals), dup=dup)
         elif self.model.fit(self.driver):
+            if self.prune_rows > 0 and self.model.precision == 64:
+                idx, top, _ = eng.gp_topk_pruned(eng.encode(vals), self.batch, acq=eng.acq(self.acq_kind), dup=dup,
+                                                 cand_base=base, bound_rows=self.prune_rows)
+                loc = torch.where(idx >= 0, idx - base, torch.zeros_like(idx))
+                return vals, idx, top, dig[loc], vals[:, loc]
             _, _, score = eng.gp_score(eng.encode(vals), acq=eng.acq(self.acq_kind), dup=dup)
         else:  # no model yet: every non-duplicate candidate is equally good (lowest index first)
             score = torch.zeros(vals.shape[1], dtype=torch.float64, device=vals.device)

@@ -33,14 +33,15 @@ def random_configs(manipulator, n: int, seed: int, device: int = 0):
 def tune_bandit(manipulator, objective: Callable[[Dict[Any, Any]], float], generations: int = 100,
                 parallelism: int = 4, n_init: int = 0, pool: int = 1 << 16, batch: int = 8, population: int = 1024,
                 seed: int = 0, lengthscale: float = 0.3, device: int = 0, group=None,
-                precision: int = 64) -> SearchDriver:
+                precision: int = 64, prune_rows: int = 0) -> SearchDriver:
     """Run the bandit for `generations` generations; returns the driver (results,
     best_result, bandit statistics).  With torch.distributed initialised and
     world > 1 the run is SPMD: call it on every rank with the same arguments."""
     import torch.distributed as dist
     world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
     meta = pso_ga_de_bandit(bandit_seed=seed, pool=pool, batch=batch, population=population, seed=seed,
-                            device=device, lengthscale=lengthscale, group=group, precision=precision)
+                            device=device, lengthscale=lengthscale, group=group, precision=precision,
+                            prune_rows=prune_rows)
     if world > 1:
         import torch
         drv = DistributedSearchDriver(manipulator, meta, parallelism=parallelism, group=group,
