@@ -240,6 +240,18 @@ int ut_gp_fit(ut_ctx* ctx, const double* X_host, const double* y_host, int32_t n
  * score NaN (nothing is selected). */
 int ut_gp_fit_async(ut_ctx* ctx, const double* X_host, const double* y_host, int32_t n, int32_t d,
                     const ut_gp_hyper* hyper);
+/* Incremental fits (default on; UT_FIT_APPEND=0 or enable=0 turns them off):
+ * when a fit's training set extends the previous fit's -- its first n_old
+ * rows bitwise equal to the previous X, the same hyperparameters, the same
+ * padded size (n rounded up to 128) and a positive-definite previous factor --
+ * the factor is extended by block rows (B = K21 L^-T, D = chol(K22 - B B^T),
+ * new L^-1 rows -D^-1 B L^-1) instead of refactored: O(n^2 k) instead of
+ * O(n^3).  The posterior equals the refit's to rounding.  The tuning loop's
+ * per-generation refit (SharedModel.fit: the results table only grows) is
+ * exactly this case.  ut_gp_last_fit_kind: 0 = the last fit refactored,
+ * 1 = it appended. */
+int ut_gp_set_fit_append(ut_ctx* ctx, int32_t enable);
+int ut_gp_last_fit_kind(ut_ctx* ctx, int32_t* kind);
 /* posterior of standardised y and the acquisition score for m candidates
  * (features [d][ld]).  mu/var/score may be NULL.  dup (may be NULL) marks
  * candidates excluded from selection (score forced to -inf). */

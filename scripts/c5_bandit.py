@@ -97,6 +97,8 @@ def main():
            "wall_s": wall, "technique_rounds": rounds, "rounds_per_s": sum(rounds.values()) / wall,
            "gp_fits": model.fits, "gp_n_final": n_train, "candidates_scored": scored,
            "candidates_scored_per_s": scored / wall,
+           # the generation loop alone (wall minus the initial design's draw + evaluation)
+           "seed_s": drv.seed_s, "loop_candidates_scored_per_s": scored / (wall - drv.seed_s),
            "round_rate_candidates_per_s": round_rate * (world if world > 1 else 1),
            "end_to_end_vs_round": (scored / wall) / (round_rate * (world if world > 1 else 1)),
            "bandit_uses": dict(drv.root_technique.bandit.use_counts)}

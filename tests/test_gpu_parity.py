@@ -347,6 +347,98 @@ def test_gp_f16x3_scaling(sf2, ell, sn2, tier):
     assert err[16] <= max(4 * err[32], 1e-7), err
 
 
+@pytest.mark.parametrize("prec", [64, 32, 16])
+@pytest.mark.parametrize("n0,steps,d", [(130, [120], 8), (1000, [4], 64), (513, [1] * 7 + [3], 16),
+                                        (40, [4] * 6, 7), (700, [60, 60, 60], 32)])
+def test_gp_fit_append_equals_refit(n0, steps, d, prec):
+    """incremental fits (ut_gp_set_fit_append): a training set that grows by
+    appended rows extends the factor by block rows; the posterior equals a
+    fresh full fit's (fp64: 1e-10 relative) and the oracle's at the tier's
+    tolerance, over chains of appends inside and across 64-row blocks"""
+    rng = np.random.default_rng(n0 + d)
+    n1 = n0 + sum(steps)
+    X = rng.uniform(size=(n1, d))
+    y = np.sum((X - 0.4) ** 2, axis=1) + 0.01 * rng.standard_normal(n1)
+    U = rng.uniform(size=(3000, d))
+    U[:10] = X[n1 - 10:] + 1e-3          # next to appended rows
+    space = [Param(f"u{k}", FLOAT, 0.0, 1.0) for k in range(d)]
+    e = engine(space)
+    e.gp_set_precision(prec)
+    n = n0
+    e.gp_fit(X[:n], y[:n], lengthscale=0.5, sigma_f2=1.0, sigma_n2=1e-6, jitter=1e-8)
+    assert e.gp_last_fit_kind() == "refit"
+    for s in steps:
+        n += s
+        e.gp_fit(X[:n], y[:n], lengthscale=0.5, sigma_f2=1.0, sigma_n2=1e-6, jitter=1e-8)
+        want = "append" if (n + 127) // 128 == (n - s + 127) // 128 else "refit"
+        assert e.gp_last_fit_kind() == want, (n, s)
+    mu, var, ei = [t.cpu().numpy() for t in e.gp_score(dev(U.T))]
+    f = engine(space)
+    f.gp_set_precision(prec)
+    f.gp_fit(X, y, lengthscale=0.5, sigma_f2=1.0, sigma_n2=1e-6, jitter=1e-8)
+    mu_f, var_f, ei_f = [t.cpu().numpy() for t in f.gp_score(dev(U.T))]
+    assert e.gp_stats() == f.gp_stats()
+    g = ogp.GP(X, y, lengthscale=0.5, sigma_f2=1.0, sigma_n2=1e-6, jitter=1e-8)
+    mu_o, var_o = g.posterior(U)
+    ei_o = ogp.acquisition(mu_o, var_o, g.f_best)
+    if prec == 64:
+        _close(mu, mu_f, rtol=1e-10, atol=1e-12)
+        _close(var, var_f, rtol=1e-10, atol=1e-12)
+        _close(mu, mu_o)
+        _close(var, var_o, atol=1e-8)
+        _close(ei, ei_o, atol=1e-8)
+    else:
+        _close(mu, mu_o)
+        _close(var, var_o, rtol=1e-3, atol=1e-5)
+        _close(ei, ei_o, rtol=1e-3, atol=1e-5)
+
+
+def test_gp_fit_append_conditions():
+    """an append is taken only for a bitwise prefix with the same
+    hyperparameters and a positive-definite previous factor; the pruned
+    scoring after an append uses the new factor's |L^-1|_F^2"""
+    rng = np.random.default_rng(3)
+    d = 6
+    X = rng.uniform(size=(300, d))
+    y = np.sin(4 * X).sum(axis=1)
+    space = [Param(f"u{k}", FLOAT, 0.0, 1.0) for k in range(d)]
+    e = engine(space)
+    hy = dict(lengthscale=0.4, sigma_f2=1.0, sigma_n2=1e-6, jitter=1e-8)
+    e.gp_fit(X[:260], y[:260], **hy)
+    e.gp_fit(X[:270], y[:270], **hy)
+    assert e.gp_last_fit_kind() == "append"
+    e.gp_fit(X[:280], y[:280], **dict(hy, lengthscale=0.41))          # lengthscale changed
+    assert e.gp_last_fit_kind() == "refit"
+    e.gp_fit(X[:285], y[:285], **dict(hy, lengthscale=0.41, jitter=1e-7))   # noise changed
+    assert e.gp_last_fit_kind() == "refit"
+    X2 = X.copy()
+    X2[3, 2] += 1e-12                                                   # not a prefix
+    e.gp_fit(X2[:290], y[:290], **dict(hy, lengthscale=0.41, jitter=1e-7))
+    assert e.gp_last_fit_kind() == "refit"
+    e.gp_set_fit_append(False)
+    e.gp_fit(X2[:295], y[:295], **dict(hy, lengthscale=0.41, jitter=1e-7))
+    assert e.gp_last_fit_kind() == "refit"
+    e.gp_set_fit_append(True)
+    e.gp_fit(X2[:300], y[:300], **dict(hy, lengthscale=0.41, jitter=1e-7))
+    assert e.gp_last_fit_kind() == "append"
+    # a failed (not positive definite) factor is never extended
+    Xd = np.repeat(X[:1], 300, axis=0)
+    e.gp_fit(Xd[:260], y[:260], lengthscale=0.4, sigma_f2=1.0, sigma_n2=0.0, jitter=0.0, wait=False)
+    e.gp_fit(Xd[:270], y[:270], lengthscale=0.4, sigma_f2=1.0, sigma_n2=0.0, jitter=0.0, wait=False)
+    assert e.gp_last_fit_kind() == "refit"
+    # pruned top-k after appends equals the dense top-k
+    e.gp_fit(X[:200], y[:200], **hy)
+    feat = dev(rng.uniform(size=(d, 20000)))
+    e.gp_topk_pruned(feat, 16, bound_rows=128)
+    e.gp_fit(X[:250], y[:250], **hy)
+    assert e.gp_last_fit_kind() == "append"
+    idx, top, st = e.gp_topk_pruned(feat, 16, bound_rows=128)
+    _, _, score = e.gp_score(feat)
+    i2, t2 = e.topk(score, 16)
+    _close(top.cpu().numpy(), t2.cpu().numpy(), rtol=1e-9, atol=1e-12)
+    assert idx.cpu().numpy().tolist() == i2.cpu().numpy().tolist()
+
+
 # --------------------------------------------------------------------------- top-k
 def test_topk_matches_oracle():
     e = engine([Param("x", FLOAT, 0.0, 1.0)])

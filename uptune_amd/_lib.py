@@ -118,6 +118,8 @@ SIGNATURES = {
     "ut_dedup": (C.c_int, [P, P, I64, P]),
     "ut_gp_fit": (C.c_int, [P, P, P, I32, I32, C.POINTER(GpHyper)]),
     "ut_gp_fit_async": (C.c_int, [P, P, P, I32, I32, C.POINTER(GpHyper)]),
+    "ut_gp_set_fit_append": (C.c_int, [P, I32]),
+    "ut_gp_last_fit_kind": (C.c_int, [P, C.POINTER(I32)]),
     "ut_forest_set": (C.c_int, [P, I32, P, I64, P, I32, D, D, D]),
     "ut_forest_predict": (C.c_int, [P, P, I64, I64, I32, P, D, P, P]),
     "ut_gp_score": (C.c_int, [P, P, I64, I64, C.POINTER(Acq), P, P, P, P]),

@@ -187,6 +187,7 @@ int ut_ctx_create(int device, uint64_t seed, ut_ctx** out) {
   c->stream = c->own_stream;
   if (const char* e = getenv("UT_JOIN_BEFORE_VAR")) c->join_before_var = atoi(e) != 0;
   if (const char* e = getenv("UT_VAR_KERNEL")) c->var_kernel = atoi(e);
+  if (const char* e = getenv("UT_FIT_APPEND")) c->fit_append = atoi(e) != 0;
   *out = c;
   return 0;
 }
@@ -206,7 +207,7 @@ int ut_ctx_destroy(ut_ctx* c) {
   fr(c->r_mask.p); fr(c->r_fresh.p); fr(c->r_pairs.p); fr(c->r_npairs.p); fr(c->de_xbits.p);
   fr(c->pr_mu.p); fr(c->pr_ub.p); fr(c->pr_score.p); fr(c->pr_mpart.p); fr(c->pr_kst.p); fr(c->pr_vpart.p);
   fr(c->pr_idx.p); fr(c->pr_count.p); fr(c->pr_ucand.p); fr(c->pr_cnorm.p);
-  fr(c->pr_k2.p); fr(c->pr_f2.p); fr(c->pr_exact.p);
+  fr(c->pr_k2.p); fr(c->pr_f2.p); fr(c->pr_exact.p); fr(c->app_ws.p);
   fr(c->hist_keys); fr(c->hist_state); fr(c->batch_slots);
   fr(c->gp_Xs); fr(c->gp_xnorm); fr(c->gp_K); fr(c->gp_Linv); fr(c->gp_y); fr(c->gp_tmp);
   fr(c->gp_alpha); fr(c->gp_beta); fr(c->gp_inv_ell); fr(c->gp_stats); fr(c->gp_flag); fr(c->gp_Xs_f); fr(c->gp_T);
@@ -220,6 +221,7 @@ int ut_ctx_destroy(ut_ctx* c) {
   for (hipEvent_t e : {c->ev_fork, c->ev_join, c->ev_fit, c->ev_prefit, c->ev_fit_x})
     if (e) hipEventDestroy(e);
   if (c->fit_host) hipHostFree(c->fit_host);
+  if (c->flag_host) hipHostFree(c->flag_host);
   for (hipStream_t st : {c->own_stream, c->side, c->fit_stream})
     if (st) hipStreamDestroy(st);
   delete c;
@@ -610,6 +612,18 @@ int ut_gp_fit_async(ut_ctx* c, const double* X, const double* y, int32_t n, int3
   if (!c) return UT_EINVAL;
   UT_HIP(c, hipSetDevice(c->device));
   return gp_fit_enqueue(c, X, y, n, d, h);
+}
+
+int ut_gp_set_fit_append(ut_ctx* c, int32_t enable) {
+  if (!c) return UT_EINVAL;
+  c->fit_append = enable != 0;
+  return 0;
+}
+
+int ut_gp_last_fit_kind(ut_ctx* c, int32_t* kind) {
+  if (!c || !kind) return UT_EINVAL;
+  *kind = c->gp_fit_kind;
+  return 0;
 }
 
 int ut_gp_score(ut_ctx* c, const double* feat, int64_t ld, int64_t m, const ut_acq* acq, const uint8_t* dup,

@@ -257,13 +257,13 @@ __global__ __launch_bounds__(256) void k_chol_update(double* __restrict__ K, int
 }
 
 // K = sf2 exp(-0.5 |xs_i - xs_j|^2) + diag I, 64 x 64 tiles on fp64 MFMA;
-// padded rows/columns (>= n) form an identity block
+// padded rows/columns (>= n) form an identity block; block rows from rb0 on
 __global__ __launch_bounds__(256) void k_gp_kmat(const double* __restrict__ Xs, const double* __restrict__ xnorm,
                                                  int32_t n, int32_t npad, int32_t d, double sf2, double diag,
-                                                 double* __restrict__ K) {
+                                                 double* __restrict__ K, int32_t rb0) {
   __shared__ double As[16 * 80];
   __shared__ double Bs[16 * 80];
-  const int64_t ib = (int64_t)blockIdx.y * 64, jb = (int64_t)blockIdx.x * 64;
+  const int64_t ib = (int64_t)(blockIdx.y + rb0) * 64, jb = (int64_t)blockIdx.x * 64;
   fd4 acc[2][2];
 #pragma unroll
   for (int a = 0; a < 2; ++a)
@@ -380,18 +380,133 @@ __global__ __launch_bounds__(256) void k_lower_mv(const double* __restrict__ Li,
   if (lane == 0) out[r] = s;
 }
 
-// out = Linv^T * v: 64 columns per workgroup, 4 row phases reduced in LDS
-__global__ __launch_bounds__(256) void k_lower_tmv(const double* __restrict__ Li, int32_t npad,
-                                                   const double* __restrict__ v, double* __restrict__ out) {
-  __shared__ double red[4][64];
-  const int t = threadIdx.x, cl = t & 63, ph = t >> 6;
-  const int32_t c = blockIdx.x * 64 + cl;
+// out = Linv^T * v, read through LinvT (row c of LinvT = column c of L^-1,
+// nonzero from c on): one wave per row, coalesced (the column-strided read of
+// L^-1 ran on npad / 64 workgroups at ~250 GB/s)
+__global__ __launch_bounds__(256) void k_upper_mv(const double* __restrict__ LiT, int32_t npad,
+                                                  const double* __restrict__ v, double* __restrict__ out) {
+  const int32_t r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (r >= npad) return;
   double s = 0.0;
-  if (c < npad)
-    for (int32_t r = c + ph; r < npad; r += 4) s += Li[(int64_t)r * npad + c] * v[r];
-  red[ph][cl] = s;
-  __syncthreads();
-  if (ph == 0 && c < npad) out[c] = (red[0][cl] + red[1][cl]) + (red[2][cl] + red[3][cl]);
+  for (int32_t c = r + lane; c < npad; c += 64) s += LiT[(int64_t)r * npad + c] * v[c];
+  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
+  if (lane == 0) out[r] = s;
+}
+
+// ---------------------------------------------------------------------------
+// incremental fit: append block row b (64 rows) to an existing factor
+// ---------------------------------------------------------------------------
+// With the old factor L (rows < 64 b) and its inverse L^-1, the new rows'
+// kernel block [K21 K22] extends it as
+//   [[L, 0], [B, D]],  B = K21 L^-T,  D = chol(K22 - B B^T)
+// and the inverse as
+//   [[L^-1, 0], [-D^-1 B L^-1, D^-1]].
+// A few small launches per block (O(n^2) work against the O(n^3) refit); the
+// scratch T holds B [64][npad] at offset 0 and E = B L^-1, transposed
+// ([npad][64]), at offset 64 npad.  Padded rows (>= n) are identity rows of
+// K, so they stay identity rows of L^-1.
+
+// The three products of block b, split over K in APP_KC chunks (one
+// workgroup per tile x chunk, so a few hundred workgroups instead of b long
+// serial K loops) and summed in chunk order by k_app_red (deterministic):
+//   MODE 0  B[j][c]     = sum_c' K21[j][c'] L^-1[c][c']   tile cb < b, c' < 64 cb + 64
+//   MODE 1  (B B^T)[j][j'] = sum_c' B[j][c'] B[j'][c']     one tile,   c' < 64 b
+//   MODE 2  E^T[c][j]   = sum_c' B[j][c'] L^-1[c'][c]     tile cb < b, 64 cb <= c' < 64 b
+//           (L^-1 read through LinvT, whose rows are its columns)
+constexpr int APP_KC = 256;
+
+struct AppGemm {
+  const double* A;
+  const double* B;
+  int32_t klo, khi;
+};
+
+template <int MODE>
+__device__ __forceinline__ AppGemm app_gemm(const double* Li, const double* LinvT, const double* K,
+                                            const double* T, int32_t npad, int32_t b, int64_t t) {
+  if (MODE == 0) return {Li + t * 64 * npad, K + (int64_t)b * 64 * npad, 0, (int32_t)(t * 64 + 64)};
+  if (MODE == 1) return {T, T, 0, b * 64};
+  return {T, LinvT + t * 64 * npad, (int32_t)(t * 64), b * 64};
+}
+
+template <int MODE>
+__global__ __launch_bounds__(256) void k_app_part(const double* __restrict__ Li, const double* __restrict__ LinvT,
+                                                  const double* __restrict__ K, const double* __restrict__ T,
+                                                  int32_t npad, int32_t b, int32_t maxq, double* __restrict__ W) {
+  __shared__ double As[16 * 80];
+  __shared__ double Bs[16 * 80];
+  const int64_t q = blockIdx.x, t = blockIdx.y;
+  const AppGemm g = app_gemm<MODE>(Li, LinvT, K, T, npad, b, t);
+  const int32_t k0 = g.klo + (int32_t)q * APP_KC;
+  if (k0 >= g.khi) return;
+  fd4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = (fd4){0.0, 0.0, 0.0, 0.0};
+  tile64_nt(g.A + k0, npad, g.B + k0, npad, min(APP_KC, g.khi - k0), As, Bs, acc);
+  double* w = W + (t * maxq + q) * 4096;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) w[tile_row(i, r) * 64 + tile_col(j)] = acc[i][j][r];
+}
+
+// MODE 0 -> B into T [64][npad];  MODE 1 -> K22 -= B B^T (in place; k_chol_diag
+// factors it next);  MODE 2 -> E^T into Et [npad][64]
+template <int MODE>
+__global__ __launch_bounds__(256) void k_app_red(const double* __restrict__ Li, const double* __restrict__ LinvT,
+                                                 double* __restrict__ K, double* __restrict__ T, int32_t npad,
+                                                 int32_t b, int32_t maxq, const double* __restrict__ W,
+                                                 double* __restrict__ Et) {
+  const int64_t t = blockIdx.x, base = (int64_t)b * 64;
+  const AppGemm g = app_gemm<MODE>(Li, LinvT, K, T, npad, b, t);
+  const int32_t nq = (g.khi - g.klo + APP_KC - 1) / APP_KC;
+  const double* w = W + t * maxq * 4096;
+  for (int e = threadIdx.x; e < 4096; e += 256) {
+    double s = 0.0;
+    for (int32_t q = 0; q < nq; ++q) s += w[(int64_t)q * 4096 + e];
+    const int i = e >> 6, j = e & 63;
+    if (MODE == 0) T[(int64_t)j * npad + t * 64 + i] = s;
+    else if (MODE == 1) K[(base + i) * npad + base + j] -= s;
+    else Et[(t * 64 + j) * 64 + i] = s;
+  }
+}
+
+// new L^-1 rows: C = -D^-1 E for column blocks cb < b (written to L^-1 and
+// LinvT); workgroup cb == b copies D^-1 (k_chol_diag's output) into LinvT
+__global__ __launch_bounds__(256) void k_app_c(double* __restrict__ Li, double* __restrict__ LinvT,
+                                               const double* __restrict__ Et, int32_t npad, int32_t b) {
+  __shared__ double As[16 * 80];
+  __shared__ double Bs[16 * 80];
+  const int64_t cb = blockIdx.x, base = (int64_t)b * 64;
+  if (cb == b) {
+    for (int e = threadIdx.x; e < 64 * 64; e += 256) {
+      const int j = e >> 6, cc = e & 63;
+      LinvT[(base + cc) * npad + base + j] = Li[(base + j) * npad + base + cc];
+    }
+    return;
+  }
+  fd4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = (fd4){0.0, 0.0, 0.0, 0.0};
+  tile64_nt(Li + base * npad + base, npad, Et + cb * 64 * 64, 64, 64, As, Bs, acc);
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t row = base + tile_row(i, r), col = cb * 64 + tile_col(j);
+        const double v = -acc[i][j][r];
+        Li[row * npad + col] = v;
+        LinvT[col * npad + row] = v;
+      }
 }
 
 // ---------------------------------------------------------------------------
@@ -491,12 +606,34 @@ static int gp_alloc(ut_ctx* c, int32_t npad, int32_t d) {
 int gp_fit_enqueue(ut_ctx* c, const double* X, const double* y, int32_t n, int32_t d, const ut_gp_hyper* h) {
   UT_CHECK(c, n >= 1 && d >= 1 && X && y && h && h->lengthscale_host, UT_EINVAL, "gp_fit: bad arguments");
   const int32_t npad = ((n + NPAD - 1) / NPAD) * NPAD;
+  // the previous fit's copies out of the pinned staging (and its factor) are
+  // complete once ev_fit is
+  if (c->fit_pending) UT_HIP(c, hipEventSynchronize(c->ev_fit));
+  // Incremental fit: new rows appended to the previous fit's training set
+  // (its rows a bitwise prefix of X, same hyperparameters, same padded size,
+  // a positive-definite previous factor) extend L^-1 by block rows instead of
+  // refactoring (k_app_*).  y is restandardised in full either way.
+  const int32_t n0 = c->gp_n;
+  bool app = false;
+  if (c->fit_append && c->gp_ready && c->gp_Xs && n > n0 && npad == c->gp_npad_fit && d == c->gp_d &&
+      c->gp_prec == c->gp_fit_prec && c->gp_sf2 == h->sigma_f2 && c->gp_diag_fit == h->sigma_n2 + h->jitter) {
+    const double* oinv = c->fit_host + (size_t)n0 * d + n0;
+    app = std::memcmp(c->fit_host, X, sizeof(double) * n0 * d) == 0;
+    for (int32_t k = 0; app && k < d; ++k) {
+      const double v = 1.0 / h->lengthscale_host[k];
+      app = std::memcmp(&v, oinv + k, sizeof(double)) == 0;
+    }
+    if (app) {
+      if (!c->flag_host) UT_HIP(c, hipHostMalloc((void**)&c->flag_host, sizeof(int32_t), hipHostMallocDefault));
+      UT_HIP(c, hipMemcpyAsync(c->flag_host, c->gp_flag, sizeof(int32_t), hipMemcpyDeviceToHost, c->fit_stream));
+      UT_HIP(c, hipStreamSynchronize(c->fit_stream));
+      app = *c->flag_host == 0;
+    }
+  }
   int rc = gp_alloc(c, npad, d);
   if (rc) return rc;
   c->pr_f2_valid = false;   // |L^-1|_F^2 (pruned scoring) belongs to the previous factor
-  // pinned staging (the previous fit's copies out of it are complete once ev_fit is)
   const size_t need = (size_t)n * d + n + d;
-  if (c->fit_pending) UT_HIP(c, hipEventSynchronize(c->ev_fit));
   if (c->fit_host_n < need) {
     if (c->fit_host) hipHostFree(c->fit_host);
     c->fit_host = nullptr;
@@ -520,46 +657,89 @@ int gp_fit_enqueue(ut_ctx* c, const double* X, const double* y, int32_t n, int32
   UT_HIP(c, hipMemcpyAsync(c->gp_inv_ell, hinv, sizeof(double) * d, hipMemcpyHostToDevice, c->stream));
   UT_HIP(c, hipMemcpyAsync(dX, hX, sizeof(double) * n * d, hipMemcpyHostToDevice, c->stream));
   UT_HIP(c, hipMemcpyAsync(dy, hy, sizeof(double) * n, hipMemcpyHostToDevice, c->stream));
-  UT_HIP(c, hipMemsetAsync(c->gp_flag, 0, sizeof(int32_t), c->stream));
+  if (!app) UT_HIP(c, hipMemsetAsync(c->gp_flag, 0, sizeof(int32_t), c->stream));
   hipLaunchKernelGGL(k_gp_prep_train, dim3(grid1(npad, 256)), dim3(256), 0, c->stream, dX, n, npad, d,
                      c->gp_inv_ell, c->gp_Xs, c->gp_xnorm);
   // the candidate side of K* needs only the scaled inputs: fp64 scoring starts
   // its K* here while the factorisation below is still running
   if ((rc = launch_xs_t(c, c->gp_Xs, npad, d, ((d + 15) / 16) * 16, c->gp_XsT))) return rc;
   UT_HIP(c, hipEventRecord(c->ev_fit_x, c->stream));
-  hipLaunchKernelGGL(k_gp_kmat, dim3(npad / 64, npad / 64), dim3(256), 0, c->stream, c->gp_Xs,
-                     c->gp_xnorm, n, npad, d, h->sigma_f2, h->sigma_n2 + h->jitter, c->gp_K);
-  hipLaunchKernelGGL(k_gp_ystats, dim3(1), dim3(256), 0, c->stream, dy, n, npad, c->gp_y, c->gp_stats);
-  UT_LAUNCH_CHECK(c);
-  const int32_t nb = npad / NB;
-  UT_HIP(c, hipMemsetAsync(c->gp_Linv, 0, sizeof(double) * npad * npad, c->stream));
-  for (int32_t kb = 0; kb < nb; ++kb) {
-    hipLaunchKernelGGL(k_chol_diag, dim3(1), dim3(256), 0, c->stream, c->gp_K, c->gp_Linv, npad, kb, c->gp_flag);
-    const int32_t T = nb - kb - 1;
-    if (T > 0) {
-      hipLaunchKernelGGL(k_chol_rows, dim3(T), dim3(256), 0, c->stream, c->gp_K, c->gp_Linv, npad, kb);
-      hipLaunchKernelGGL(k_chol_update, dim3(T * (T + 1) / 2), dim3(256), 0, c->stream, c->gp_K, npad, kb);
+  const double diag = h->sigma_n2 + h->jitter;
+  if (app) {
+    // block rows b0 .. b1 hold the new rows (b0 may also hold old ones: it is
+    // recomputed whole)
+    const int32_t b0 = n0 / NB, b1 = (n - 1) / NB;
+    hipLaunchKernelGGL(k_gp_kmat, dim3(b1 + 1, b1 - b0 + 1), dim3(256), 0, c->stream, c->gp_Xs, c->gp_xnorm, n,
+                       npad, d, h->sigma_f2, diag, c->gp_K, b0);
+    hipLaunchKernelGGL(k_gp_ystats, dim3(1), dim3(256), 0, c->stream, dy, n, npad, c->gp_y, c->gp_stats);
+    double* Et = c->gp_T + (int64_t)NB * npad;
+    for (int32_t b = b0; b <= b1; ++b) {
+      const int32_t maxq = (b * NB + APP_KC - 1) / APP_KC;
+      if (b > 0) {
+        if ((rc = ensure(c, c->app_ws, (size_t)b * maxq * 4096))) return rc;
+        double* W = c->app_ws.p;
+        hipLaunchKernelGGL(k_app_part<0>, dim3(maxq, b), dim3(256), 0, c->stream, c->gp_Linv, c->gp_LinvT,
+                           c->gp_K, c->gp_T, npad, b, maxq, W);
+        hipLaunchKernelGGL(k_app_red<0>, dim3(b), dim3(256), 0, c->stream, c->gp_Linv, c->gp_LinvT, c->gp_K,
+                           c->gp_T, npad, b, maxq, W, Et);
+        hipLaunchKernelGGL(k_app_part<1>, dim3(maxq, 1), dim3(256), 0, c->stream, c->gp_Linv, c->gp_LinvT,
+                           c->gp_K, c->gp_T, npad, b, maxq, W);
+        hipLaunchKernelGGL(k_app_red<1>, dim3(1), dim3(256), 0, c->stream, c->gp_Linv, c->gp_LinvT, c->gp_K,
+                           c->gp_T, npad, b, maxq, W, Et);
+      }
+      hipLaunchKernelGGL(k_chol_diag, dim3(1), dim3(256), 0, c->stream, c->gp_K, c->gp_Linv, npad, b, c->gp_flag);
+      if (b > 0) {
+        double* W = c->app_ws.p;
+        hipLaunchKernelGGL(k_app_part<2>, dim3(maxq, b), dim3(256), 0, c->stream, c->gp_Linv, c->gp_LinvT,
+                           c->gp_K, c->gp_T, npad, b, maxq, W);
+        hipLaunchKernelGGL(k_app_red<2>, dim3(b), dim3(256), 0, c->stream, c->gp_Linv, c->gp_LinvT, c->gp_K,
+                           c->gp_T, npad, b, maxq, W, Et);
+      }
+      hipLaunchKernelGGL(k_app_c, dim3(b + 1), dim3(256), 0, c->stream, c->gp_Linv, c->gp_LinvT, Et, npad, b);
     }
+    UT_LAUNCH_CHECK(c);
+  } else {
+    hipLaunchKernelGGL(k_gp_kmat, dim3(npad / 64, npad / 64), dim3(256), 0, c->stream, c->gp_Xs,
+                       c->gp_xnorm, n, npad, d, h->sigma_f2, diag, c->gp_K, 0);
+    hipLaunchKernelGGL(k_gp_ystats, dim3(1), dim3(256), 0, c->stream, dy, n, npad, c->gp_y, c->gp_stats);
+    UT_LAUNCH_CHECK(c);
+    const int32_t nb = npad / NB;
+    UT_HIP(c, hipMemsetAsync(c->gp_Linv, 0, sizeof(double) * npad * npad, c->stream));
+    for (int32_t kb = 0; kb < nb; ++kb) {
+      hipLaunchKernelGGL(k_chol_diag, dim3(1), dim3(256), 0, c->stream, c->gp_K, c->gp_Linv, npad, kb, c->gp_flag);
+      const int32_t T = nb - kb - 1;
+      if (T > 0) {
+        hipLaunchKernelGGL(k_chol_rows, dim3(T), dim3(256), 0, c->stream, c->gp_K, c->gp_Linv, npad, kb);
+        hipLaunchKernelGGL(k_chol_update, dim3(T * (T + 1) / 2), dim3(256), 0, c->stream, c->gp_K, npad, kb);
+      }
+    }
+    UT_LAUNCH_CHECK(c);
+    // off-diagonal blocks of L^-1 by recursive doubling (diagonal blocks came from k_chol_diag)
+    for (int32_t lv = NB; lv < npad; lv *= 2) {
+      const int32_t pairs = (int32_t)((npad - lv + 2 * lv - 1) / (2 * lv));
+      const dim3 grid(lv / 64, lv / 64, pairs);
+      hipLaunchKernelGGL(k_trinv_level, grid, dim3(256), 0, c->stream, c->gp_K, c->gp_Linv, c->gp_T, npad, lv, 0);
+      hipLaunchKernelGGL(k_trinv_level, grid, dim3(256), 0, c->stream, c->gp_K, c->gp_Linv, c->gp_T, npad, lv, 1);
+    }
+    UT_LAUNCH_CHECK(c);
   }
-  UT_LAUNCH_CHECK(c);
-  // off-diagonal blocks of L^-1 by recursive doubling (diagonal blocks came from k_chol_diag)
-  for (int32_t lv = NB; lv < npad; lv *= 2) {
-    const int32_t pairs = (int32_t)((npad - lv + 2 * lv - 1) / (2 * lv));
-    const dim3 grid(lv / 64, lv / 64, pairs);
-    hipLaunchKernelGGL(k_trinv_level, grid, dim3(256), 0, c->stream, c->gp_K, c->gp_Linv, c->gp_T, npad, lv, 0);
-    hipLaunchKernelGGL(k_trinv_level, grid, dim3(256), 0, c->stream, c->gp_K, c->gp_Linv, c->gp_T, npad, lv, 1);
-  }
-  UT_LAUNCH_CHECK(c);
   hipLaunchKernelGGL(k_lower_mv, dim3(grid1(npad, 4)), dim3(256), 0, c->stream, c->gp_Linv, npad, c->gp_y,
                      c->gp_beta);
-  hipLaunchKernelGGL(k_lower_tmv, dim3(grid1(npad, 64)), dim3(256), 0, c->stream, c->gp_Linv, npad, c->gp_beta,
-                     c->gp_alpha);
   UT_LAUNCH_CHECK(c);
   if (c->gp_prec == 32 && (rc = launch_to_f32(c, c->gp_Xs, c->gp_Xs_f, (int64_t)npad * d))) return rc;
-  if ((rc = launch_transpose(c, c->gp_Linv, npad, c->gp_LinvT, c->gp_prec == 32 ? c->gp_LinvT_f : nullptr))) return rc;
+  // (an append wrote its rows of LinvT itself)
+  if ((!app || c->gp_prec == 32) &&
+      (rc = launch_transpose(c, c->gp_Linv, npad, c->gp_LinvT, c->gp_prec == 32 ? c->gp_LinvT_f : nullptr)))
+    return rc;
+  hipLaunchKernelGGL(k_upper_mv, dim3(grid1(npad, 4)), dim3(256), 0, c->stream, c->gp_LinvT, npad, c->gp_beta,
+                     c->gp_alpha);
+  UT_LAUNCH_CHECK(c);
   if (c->gp_prec == 16 && (rc = launch_split_h3(c, c->gp_Linv, npad, reinterpret_cast<_Float16*>(c->gp_LinvT_f))))
     return rc;
   c->gp_fit_prec = c->gp_prec;
+  c->gp_npad_fit = npad;
+  c->gp_diag_fit = diag;
+  c->gp_fit_kind = app ? 1 : 0;
   UT_HIP(c, hipEventRecord(c->ev_fit, c->stream));
   c->fit_pending = true;
   c->gp_ready = true;

@@ -201,6 +201,13 @@ struct ut_ctx {
   double gp_sf2 = 1.0;
   int32_t gp_prec = 64;        // precision requested for the next fit
   int32_t gp_fit_prec = 64;    // precision of the fitted factors used by scoring
+  // incremental fit (gp.hip gp_fit_enqueue): 1 = a fit whose training set
+  // extends the previous one's extends its factor (ut_gp_set_fit_append, UT_FIT_APPEND)
+  int32_t fit_append = 1;
+  int32_t gp_npad_fit = 0;     // padded size of the current factor
+  double gp_diag_fit = 0.0;    // its sigma_n2 + jitter
+  int32_t gp_fit_kind = 0;     // 0 = the last fit refactored, 1 = it appended rows
+  int32_t* flag_host = nullptr;  // pinned readback of the previous fit's flag
   float* gp_Xs_f = nullptr;    // fp32 copies for the fp32 MFMA path
   double* gp_LinvT = nullptr;  // (L^-1)^T [k][row]: the A operand of the variance contraction
   double* gp_XsT = nullptr;    // (X/ell)^T [dpad][npad]: the A operand of the K* contraction
@@ -237,6 +244,7 @@ struct ut_ctx {
   ut::DevBuf<double> pr_ucand, pr_cnorm;       // survivors' scaled features [dpad][lds] and norms [lds]
   ut::DevBuf<int64_t> pr_idx;                  // [ld] survivor indices (+ the threshold set)
   ut::DevBuf<int64_t> pr_count;                // [1]
+  ut::DevBuf<double> app_ws;                   // split-K partials of the incremental fit [b][maxq][64][64]
   ut::DevBuf<double> pr_k2;                    // [RT][ldk] partials of |k*|^2 (the variance tail bound)
   ut::DevBuf<double> pr_f2;                    // [1] |L^-1|_F^2 (+ its block partials)
   bool pr_f2_valid = false;                    // pr_f2 belongs to the current fit

@@ -274,6 +274,15 @@ class BatchEngine:
         fn = self.lib.ut_gp_fit if wait else self.lib.ut_gp_fit_async
         L.check(self.ctx, fn(self.ctx, X.ctypes.data, y.ctypes.data, n, d, C.byref(h)), "ut_gp_fit")
 
+    def gp_set_fit_append(self, enable: bool):
+        """incremental fits when the training set only grows (on by default)"""
+        L.check(self.ctx, self.lib.ut_gp_set_fit_append(self.ctx, int(bool(enable))), "ut_gp_set_fit_append")
+
+    def gp_last_fit_kind(self) -> str:
+        k = C.c_int32()
+        L.check(self.ctx, self.lib.ut_gp_last_fit_kind(self.ctx, C.byref(k)), "ut_gp_last_fit_kind")
+        return "append" if k.value == 1 else "refit"
+
     def gp_stats(self) -> Tuple[float, float, float]:
         a, b, c = C.c_double(), C.c_double(), C.c_double()
         L.check(self.ctx, self.lib.ut_gp_stats(self.ctx, C.byref(a), C.byref(b), C.byref(c)), "ut_gp_stats")

@@ -49,7 +49,10 @@ def tune_bandit(manipulator, objective: Callable[[Dict[Any, Any]], float], gener
                                       else None)
     else:
         drv = SearchDriver(manipulator, meta, parallelism=parallelism)
+    import time
+    t0 = time.perf_counter()
     if n_init:
         drv.seed_results(random_configs(manipulator, n_init, seed + 7919, device), objective)
+    drv.seed_s = time.perf_counter() - t0    # initial design: draw, evaluate, record (host)
     drv.main(objective, test_limit=generations * parallelism, max_generations=generations)
     return drv
