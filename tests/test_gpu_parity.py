@@ -393,6 +393,33 @@ def test_gp_fit_append_equals_refit(n0, steps, d, prec):
         _close(ei, ei_o, rtol=1e-3, atol=1e-5)
 
 
+@pytest.mark.parametrize("m,n", [(300, 4096), (3000, 1024), (100, 300)])
+def test_gp_var_split_equals_unsplit(monkeypatch, m, n):
+    """few candidate strips: the fp64 variance splits each row tile's k loop
+    over workgroups (k_gp_var_pp<true> + k_var_split_red, the survivor /
+    threshold passes of pruned scoring); it equals the one-item-per-row-tile
+    contraction (UT_VAR_SPLIT=0) to rounding"""
+    rng = np.random.default_rng(m + n)
+    d = 16
+    X = rng.uniform(size=(n, d))
+    y = np.sin(3 * X).sum(axis=1)
+    U = rng.uniform(size=(m, d))
+    U[:5] = X[:5] + 1e-3
+    space = [Param(f"u{k}", FLOAT, 0.0, 1.0) for k in range(d)]
+    out = {}
+    for split in ("1", "0"):
+        monkeypatch.setenv("UT_VAR_SPLIT", split)
+        e = engine(space)
+        e.gp_fit(X, y, lengthscale=0.5, sigma_f2=1.0, sigma_n2=1e-6, jitter=1e-8)
+        out[split] = [t.cpu().numpy() for t in e.gp_score(dev(U.T))]
+    for a, b in zip(out["1"], out["0"]):
+        _close(a, b, rtol=1e-11, atol=1e-13)
+    g = ogp.GP(X, y, lengthscale=0.5, sigma_f2=1.0, sigma_n2=1e-6, jitter=1e-8)
+    mu_o, var_o = g.posterior(U)
+    _close(out["1"][0], mu_o)
+    _close(out["1"][1], var_o, atol=1e-8)
+
+
 def test_gp_fit_append_conditions():
     """an append is taken only for a bitwise prefix with the same
     hyperparameters and a positive-definite previous factor; the pruned

@@ -187,6 +187,7 @@ int ut_ctx_create(int device, uint64_t seed, ut_ctx** out) {
   c->stream = c->own_stream;
   if (const char* e = getenv("UT_JOIN_BEFORE_VAR")) c->join_before_var = atoi(e) != 0;
   if (const char* e = getenv("UT_VAR_KERNEL")) c->var_kernel = atoi(e);
+  if (const char* e = getenv("UT_VAR_SPLIT")) c->var_split = atoi(e) != 0;
   if (const char* e = getenv("UT_FIT_APPEND")) c->fit_append = atoi(e) != 0;
   *out = c;
   return 0;
@@ -207,7 +208,7 @@ int ut_ctx_destroy(ut_ctx* c) {
   fr(c->r_mask.p); fr(c->r_fresh.p); fr(c->r_pairs.p); fr(c->r_npairs.p); fr(c->de_xbits.p);
   fr(c->pr_mu.p); fr(c->pr_ub.p); fr(c->pr_score.p); fr(c->pr_mpart.p); fr(c->pr_kst.p); fr(c->pr_vpart.p);
   fr(c->pr_idx.p); fr(c->pr_count.p); fr(c->pr_ucand.p); fr(c->pr_cnorm.p);
-  fr(c->pr_k2.p); fr(c->pr_f2.p); fr(c->pr_exact.p); fr(c->app_ws.p);
+  fr(c->pr_k2.p); fr(c->pr_f2.p); fr(c->pr_exact.p); fr(c->app_ws.p); fr(c->var_vbuf.p);
   fr(c->hist_keys); fr(c->hist_state); fr(c->batch_slots);
   fr(c->gp_Xs); fr(c->gp_xnorm); fr(c->gp_K); fr(c->gp_Linv); fr(c->gp_y); fr(c->gp_tmp);
   fr(c->gp_alpha); fr(c->gp_beta); fr(c->gp_inv_ell); fr(c->gp_stats); fr(c->gp_flag); fr(c->gp_Xs_f); fr(c->gp_T);

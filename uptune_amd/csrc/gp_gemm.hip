@@ -577,12 +577,23 @@ __global__ __launch_bounds__(V_NT, 1) void k_gp_var(const T* __restrict__ AT, in
 constexpr int VP_NT = 256, VP_BN = 128, VP_BK = 16, VP_ST = 2;
 constexpr int VP_SA = VP_BK * VAR_BM, VP_STAGE = VP_SA + VP_BK * VP_BN;
 
+// SPLIT: few candidate strips (survivor and threshold-set passes of the pruned
+// scoring): the item count RT x CT is far below the chip's workgroup slots and
+// each item is a long serial k loop, so items are split into chunks of kcs
+// k-steps.  Item g (over all XCDs) -> strip ct, row tile rt, chunk kc (chunks
+// of a strip in row-tile order); the raw 128 x 128 tile of L^-1 K*^T partial
+// sums goes to vbuf[g], and k_var_split_red sums the chunks in order, then
+// squares (deterministic).
+__device__ __forceinline__ int32_t var_nk(int32_t K, int32_t rt) { return min(K, (rt + 1) * VAR_BM) / VP_BK; }
+
+template <bool SPLIT>
 __global__ __launch_bounds__(VP_NT, 2) void k_gp_var_pp(const double* __restrict__ AT, int64_t lda,
                                                         const double* __restrict__ B, int64_t ldb, int32_t K,
                                                         int32_t RT, int32_t CT, int64_t m,
                                                         int32_t* __restrict__ ticket, double* __restrict__ part,
                                                         int64_t ldp, const double* __restrict__ beta,
-                                                        double* __restrict__ mpart) {
+                                                        double* __restrict__ mpart, int32_t kcs, int32_t per_strip,
+                                                        double* __restrict__ vbuf) {
   // one __shared__ object (see k_gp_var): ring, reduction buffer, ticket slot
   __shared__ __attribute__((aligned(16))) double lds[VP_ST * VP_STAGE + 4 * VP_BN + VAR_BM + 2];
   double* red = lds + VP_ST * VP_STAGE;  // [2][128] squares, [2][128] mean
@@ -612,12 +623,30 @@ __global__ __launch_bounds__(VP_NT, 2) void k_gp_var_pp(const double* __restrict
     if (t == 0) s_item = atomicAdd(&ticket[xcd], 1);
     __syncthreads();  // also: the previous item's epilogue is done with `red`
     const int32_t j = s_item;
-    const int32_t ct = (j / RT) * 8 + xcd;
-    if (ct >= CT) break;  // uniform: every wave of the block leaves together
-    const int32_t rt = RT - 1 - (j % RT);
+    int32_t ct, rt, kt0, kt1, g = 0;
+    if constexpr (SPLIT) {
+      g = j * 8 + xcd;
+      if (g >= CT * per_strip) break;
+      ct = g / per_strip;
+      int32_t rem = g - ct * per_strip;
+      rt = 0;
+      for (;;) {
+        const int32_t nc = (var_nk(K, rt) + kcs - 1) / kcs;
+        if (rem < nc) break;
+        rem -= nc;
+        ++rt;
+      }
+      kt0 = rem * kcs;
+      kt1 = min(var_nk(K, rt), kt0 + kcs);
+    } else {
+      ct = (j / RT) * 8 + xcd;
+      if (ct >= CT) break;  // uniform: every wave of the block leaves together
+      rt = RT - 1 - (j % RT);
+      kt0 = 0;
+      kt1 = var_nk(K, rt);
+    }
     const int64_t col0 = (int64_t)ct * VP_BN;
     const int32_t row0 = rt * VAR_BM;
-    const int32_t nk = min(K, row0 + VAR_BM) / VP_BK;
     vd4 acc[4][4];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -626,16 +655,16 @@ __global__ __launch_bounds__(VP_NT, 2) void k_gp_var_pp(const double* __restrict
     // beta of this row tile, staged for the epilogue beside stage 0 (its load
     // retires with stage 0's vmcnt wait; the previous epilogue's reads of
     // sbeta ended before the ticket barrier)
-    if (w == 0)  // 128 doubles = one glds wave-instruction, asynchronous like the ring
+    if (!SPLIT && w == 0)  // 128 doubles = one glds wave-instruction, asynchronous like the ring
       __builtin_amdgcn_global_load_lds(beta + row0 + lane * 2, (__attribute__((address_space(3))) void*)sbeta, 16, 0,
                                        0);
-    issue(row0, col0, 0, lds);
-    const int32_t nfull = min(nk, row0 / VP_BK);
-    for (int32_t kt = 0; kt < nk; ++kt) {
+    issue(row0, col0, kt0 * VP_BK, lds + (kt0 & 1) * VP_STAGE);
+    const int32_t nfull = min(var_nk(K, rt), row0 / VP_BK);
+    for (int32_t kt = kt0; kt < kt1; ++kt) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();  // stage kt landed everywhere; stage kt-1 fully read
       asm volatile("" ::: "memory");
-      if (kt + 1 < nk) issue(row0, col0, (kt + 1) * VP_BK, lds + ((kt + 1) & 1) * VP_STAGE);
+      if (kt + 1 < kt1) issue(row0, col0, (kt + 1) * VP_BK, lds + ((kt + 1) & 1) * VP_STAGE);
       const double* as = lds + (kt & 1) * VP_STAGE;
       const double* bs = as + VP_SA;
       // diagonal block: sub-tile i (rows (2i + wm) * 16 ..) is all zero once
@@ -663,6 +692,17 @@ __global__ __launch_bounds__(VP_NT, 2) void k_gp_var_pp(const double* __restrict
           }
         }
       }
+    }
+    if constexpr (SPLIT) {   // the raw partial tile; k_var_split_red squares the chunk sums
+      double* vt = vbuf + (int64_t)g * (VAR_BM * VP_BN);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            vt[((2 * i + wm) * 16 + (lane >> 4) + 4 * r) * VP_BN + wn * 64 + jj * 16 + (lane & 15)] = acc[i][jj][r];
+      continue;   // the next ticket's barrier orders the LDS ring's reuse
     }
     // epilogue: column sums of squares over the tile's 128 rows and the mean
     // partial sum_r V[r][c] beta_r (beta = L^-1 y)
@@ -695,6 +735,48 @@ __global__ __launch_bounds__(VP_NT, 2) void k_gp_var_pp(const double* __restrict
         mpart[(int64_t)rt * ldp + col] = red[2 * VP_BN + t] + red[3 * VP_BN + t];
       }
     }
+  }
+}
+
+// chunk sums of the split partial tiles -> part / mpart (k_gp_var_pp's epilogue);
+// one 1024-thread workgroup per (row tile, strip): thread = (column, 16-row group),
+// four chunk loads in flight per thread
+__global__ __launch_bounds__(1024) void k_var_split_red(const double* __restrict__ vbuf, int32_t K, int32_t kcs,
+                                                        int32_t per_strip, int64_t m, const double* __restrict__ beta,
+                                                        double* __restrict__ part, double* __restrict__ mpart,
+                                                        int64_t ldp) {
+  __shared__ double red[2][8][VP_BN];
+  const int32_t rt = blockIdx.x, ct = blockIdx.y;
+  int32_t first = ct * per_strip;
+  for (int32_t r = 0; r < rt; ++r) first += (var_nk(K, r) + kcs - 1) / kcs;
+  const int32_t nc = (var_nk(K, rt) + kcs - 1) / kcs;
+  const int t = threadIdx.x, c = t & (VP_BN - 1), h = t >> 7;   // column, 16-row group
+  const double* vb = vbuf + (int64_t)first * VAR_BM * VP_BN + c;
+  double s = 0.0, u = 0.0;
+  for (int r = h * 16; r < h * 16 + 16; ++r) {
+    const double* p = vb + r * VP_BN;
+    double v0 = 0.0, v1 = 0.0, v2 = 0.0, v3 = 0.0;
+    int32_t q = 0;
+    for (; q + 4 <= nc; q += 4) {
+      v0 += p[(int64_t)q * VAR_BM * VP_BN];
+      v1 += p[(int64_t)(q + 1) * VAR_BM * VP_BN];
+      v2 += p[(int64_t)(q + 2) * VAR_BM * VP_BN];
+      v3 += p[(int64_t)(q + 3) * VAR_BM * VP_BN];
+    }
+    for (; q < nc; ++q) v0 += p[(int64_t)q * VAR_BM * VP_BN];
+    const double v = (v0 + v1) + (v2 + v3);
+    s += v * v;
+    u += v * beta[rt * VAR_BM + r];
+  }
+  red[0][h][c] = s;
+  red[1][h][c] = u;
+  __syncthreads();
+  const int64_t col = (int64_t)ct * VP_BN + c;
+  if (h < 2 && col < m) {
+    double a = 0.0;
+#pragma unroll
+    for (int g = 0; g < 8; ++g) a += red[h][g][c];
+    (h == 0 ? part : mpart)[(int64_t)rt * ldp + col] = a;
   }
 }
 
@@ -996,10 +1078,30 @@ int launch_gemm_var(ut_ctx* c, int prec, const void* LinvT, int64_t lda, const v
     // two workgroups per CU on 128-candidate column tiles
     const int32_t CTp = (int32_t)((m + VP_BN - 1) / VP_BN);
     const int64_t items_p = (int64_t)RT * CTp;
-    int32_t nbp = 2 * (c->n_cu / 8) * 8;
-    if (items_p < nbp) nbp = (int32_t)(((items_p + 7) / 8) * 8);
-    hipLaunchKernelGGL(k_gp_var_pp, dim3(nbp), dim3(VP_NT), 0, c->stream, (const double*)LinvT, lda,
-                       (const double*)kst, ldk, npad, RT, CTp, m, c->gp_ctr, part, ldk, beta, mpart);
+    const int32_t slots = 2 * (c->n_cu / 8) * 8;
+    int32_t nbp = slots;
+    // few strips (pruned scoring's survivor / threshold passes): split the k loops
+    int64_t steps = 0;   // k-steps per strip
+    for (int32_t r = 0; r < RT; ++r) steps += min(npad, (r + 1) * VAR_BM) / VP_BK;
+    if (c->var_split && items_p < slots && steps >= 64) {
+      int32_t kcs = (int32_t)((steps * CTp + 2 * slots - 1) / (2 * slots));   // ~2 items per workgroup slot
+      kcs = kcs < 8 ? 8 : kcs;
+      int32_t per_strip = 0;
+      for (int32_t r = 0; r < RT; ++r) per_strip += (min(npad, (r + 1) * VAR_BM) / VP_BK + kcs - 1) / kcs;
+      const int64_t items_s = (int64_t)per_strip * CTp;
+      int rc;
+      if ((rc = ensure(c, c->var_vbuf, (size_t)items_s * VAR_BM * VP_BN))) return rc;
+      if (items_s < nbp) nbp = (int32_t)(((items_s + 7) / 8) * 8);
+      hipLaunchKernelGGL(k_gp_var_pp<true>, dim3(nbp), dim3(VP_NT), 0, c->stream, (const double*)LinvT, lda,
+                         (const double*)kst, ldk, npad, RT, CTp, m, c->gp_ctr, part, ldk, beta, mpart, kcs, per_strip,
+                         c->var_vbuf.p);
+      hipLaunchKernelGGL(k_var_split_red, dim3(RT, CTp), dim3(1024), 0, c->stream, c->var_vbuf.p, npad, kcs, per_strip,
+                         m, beta, part, mpart, ldk);
+    } else {
+      if (items_p < nbp) nbp = (int32_t)(((items_p + 7) / 8) * 8);
+      hipLaunchKernelGGL(k_gp_var_pp<false>, dim3(nbp), dim3(VP_NT), 0, c->stream, (const double*)LinvT, lda,
+                         (const double*)kst, ldk, npad, RT, CTp, m, c->gp_ctr, part, ldk, beta, mpart, 0, 0, nullptr);
+    }
   }
   UT_LAUNCH_CHECK(c);
   return 0;

@@ -133,6 +133,9 @@ struct ut_ctx {
   // fp64 variance kernel: 0 = k_gp_var_pp (two 4-wave workgroups per CU, the
   // default), 1 = k_gp_var<double> (one 8-wave workgroup per CU); UT_VAR_KERNEL
   int32_t var_kernel = 0;
+  // fp64 variance with few candidate strips: 1 = split the k loops
+  // (k_gp_var_pp<true> + k_var_split_red), 0 = one item per row tile; UT_VAR_SPLIT
+  int32_t var_split = 1;
   double* fit_host = nullptr;        // pinned staging of X, y, 1/ell for the asynchronous fit
   size_t fit_host_n = 0;
   std::string err;
@@ -244,6 +247,7 @@ struct ut_ctx {
   ut::DevBuf<double> pr_ucand, pr_cnorm;       // survivors' scaled features [dpad][lds] and norms [lds]
   ut::DevBuf<int64_t> pr_idx;                  // [ld] survivor indices (+ the threshold set)
   ut::DevBuf<int64_t> pr_count;                // [1]
+  ut::DevBuf<double> var_vbuf;                 // split variance: raw partial tiles [items][128][128]
   ut::DevBuf<double> app_ws;                   // split-K partials of the incremental fit [b][maxq][64][64]
   ut::DevBuf<double> pr_k2;                    // [RT][ldk] partials of |k*|^2 (the variance tail bound)
   ut::DevBuf<double> pr_f2;                    // [1] |L^-1|_F^2 (+ its block partials)
