@@ -69,7 +69,8 @@ static void free_space(Space& s) {
   if (s.d_lut) hipFree(s.d_lut);
   if (s.d_vtab) hipFree(s.d_vtab);
   for (void* q : {(void*)s.d_order_col, (void*)s.d_perm_params, (void*)s.d_perm_bytes, (void*)s.d_perm_off,
-                  (void*)s.d_perm_offbase, (void*)s.d_perm_len, (void*)s.d_comp})
+                  (void*)s.d_perm_offbase, (void*)s.d_perm_len, (void*)s.d_comp,
+                  (void*)s.d_col_param})
     if (q) hipFree(q);
   s = Space();
 }
@@ -189,6 +190,7 @@ int ut_ctx_create(int device, uint64_t seed, ut_ctx** out) {
   if (const char* e = getenv("UT_VAR_KERNEL")) c->var_kernel = atoi(e);
   if (const char* e = getenv("UT_VAR_SPLIT")) c->var_split = atoi(e) != 0;
   if (const char* e = getenv("UT_FIT_APPEND")) c->fit_append = atoi(e) != 0;
+  if (const char* e = getenv("UT_DE_AOS")) c->de_aos = atoi(e) != 0;
   *out = c;
   return 0;
 }
@@ -200,10 +202,11 @@ int ut_ctx_destroy(ut_ctx* c) {
   free_space(c->space);
   auto fr = [](void* p) { if (p) hipFree(p); };
   fr(c->pop); fr(c->pso_vel); fr(c->pso_best);
-  fr(c->pop_dig);
+  fr(c->pop_dig); fr(c->pop_aos);
   for (size_t s = 0; s < c->pop_slots.size(); ++s) {
     if ((int32_t)s == c->pop_slot) continue;   // the selected slot's buffers are the fields above
     fr(c->pop_slots[s].pop); fr(c->pop_slots[s].pso_vel); fr(c->pop_slots[s].pso_best); fr(c->pop_slots[s].pop_dig);
+    fr(c->pop_slots[s].pop_aos);
   }
   fr(c->r_mask.p); fr(c->r_fresh.p); fr(c->r_pairs.p); fr(c->r_npairs.p); fr(c->de_xbits.p);
   fr(c->pr_mu.p); fr(c->pr_ub.p); fr(c->pr_score.p); fr(c->pr_mpart.p); fr(c->pr_kst.p); fr(c->pr_vpart.p);
@@ -397,6 +400,13 @@ int ut_space_define(ut_ctx* c, int32_t P, const ut_param_desc* params, int32_t p
     UT_HIP(c, hipMalloc((void**)&s.d_comp, sizeof(int32_t) * comp.size()));
     UT_HIP(c, hipMemcpy(s.d_comp, comp.data(), sizeof(int32_t) * comp.size(), hipMemcpyHostToDevice));
   }
+  {
+    std::vector<int32_t> col_param(s.ncols > 0 ? s.ncols : 1, -1);
+    for (int32_t j = 0; j < P; ++j)
+      if (s.host_params[j].kind != UT_PERM) col_param[s.host_params[j].col] = j;
+    UT_HIP(c, hipMalloc((void**)&s.d_col_param, sizeof(int32_t) * col_param.size()));
+    UT_HIP(c, hipMemcpy(s.d_col_param, col_param.data(), sizeof(int32_t) * col_param.size(), hipMemcpyHostToDevice));
+  }
   int rc = compile_hash_layout(c, names, primitive);
   if (rc) return rc;
   c->has_space = true;
@@ -408,7 +418,8 @@ int ut_space_define(ut_ctx* c, int32_t P, const ut_param_desc* params, int32_t p
     c->pop_cap = 0;
   }
   c->pop_dig_valid = false;
-  for (auto& ps : c->pop_slots) ps.pop_dig_valid = false;
+  c->pop_aos_valid = false;
+  for (auto& ps : c->pop_slots) ps.pop_dig_valid = ps.pop_aos_valid = false;
   return 0;
 }
 
@@ -451,6 +462,7 @@ int ut_population_init(ut_ctx* c, int64_t npop, uint32_t round_) {
   int rc = pop_alloc(c, npop);
   if (rc) return rc;
   c->pop_dig_valid = false;
+  c->pop_aos_valid = false;
   return launch_population_init(c, round_);
 }
 
@@ -462,6 +474,7 @@ int ut_population_set(ut_ctx* c, int64_t npop, const double* values, int64_t ld)
   int rc = pop_alloc(c, npop);
   if (rc) return rc;
   c->pop_dig_valid = false;
+  c->pop_aos_valid = false;
   UT_HIP(c, hipMemcpy2DAsync(c->pop, sizeof(double) * npop, values, sizeof(double) * ld, sizeof(double) * npop,
                              c->space.ncols, hipMemcpyDeviceToDevice, c->stream));
   return 0;
@@ -479,10 +492,12 @@ int ut_population_select(ut_ctx* c, int32_t slot) {
   cur.pop = c->pop; cur.npop = c->npop; cur.pop_cap = c->pop_cap;
   cur.pso_vel = c->pso_vel; cur.pso_best = c->pso_best; cur.pso_cap = c->pso_cap;
   cur.pop_dig = c->pop_dig; cur.pop_dig_cap = c->pop_dig_cap; cur.pop_dig_valid = c->pop_dig_valid;
+  cur.pop_aos = c->pop_aos; cur.pop_aos_cap = c->pop_aos_cap; cur.pop_aos_valid = c->pop_aos_valid;
   const ut_ctx::PopSlot& nx = c->pop_slots[slot];
   c->pop = nx.pop; c->npop = nx.npop; c->pop_cap = nx.pop_cap;
   c->pso_vel = nx.pso_vel; c->pso_best = nx.pso_best; c->pso_cap = nx.pso_cap;
   c->pop_dig = nx.pop_dig; c->pop_dig_cap = nx.pop_dig_cap; c->pop_dig_valid = nx.pop_dig_valid;
+  c->pop_aos = nx.pop_aos; c->pop_aos_cap = nx.pop_aos_cap; c->pop_aos_valid = nx.pop_aos_valid;
   c->pop_slot = slot;
   return 0;
 }

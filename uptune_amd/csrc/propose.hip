@@ -90,24 +90,56 @@ struct DeDiffOut {
 // ([ceil(P/32)][256] words, each lane its own column), so the second pass
 // draws nothing for the crossover decision: 1 + 1 Philox blocks per param
 // became 1 (k_de is Philox-issue-bound: ~220 VALU cycles per block).
-template <bool DIFF>
-__global__ __launch_bounds__(256) void k_de(const DevParam* __restrict__ params, int32_t P,
+// AOS (the default): block = one wave; the donors' values come from the
+// member-major donor copy (pop_aos, [npop + 1][lda], row npop = the best
+// config; primitive params as unit values, so no unit_of is left here), staged
+// DE_GW columns at a time into LDS by global_load_lds row gathers of 64-B
+// pieces: 3 x 64 pieces per wave and group instead of one 8-B gather (a cache
+// line each) per crossing (param, donor).  The first group's loads are issued
+// before pass 1, so the Philox work hides them.  The target's raw values are
+// read column-major one param ahead.
+// LDS image per donor k: [64 candidates][DE_CH chunks of 16 B], chunk ch of
+// candidate c at position ch ^ ((c >> DE_SW) & (DE_CH - 1)) (the swizzle goes on
+// the source address: a glds writes lane-linear), so a wave's ds_read_b64 of
+// one column is at worst 2-way bank-conflicted.
+// Measured at C2 (k_de alone, m = 2^20): 0.99 ms column-major gathers; staged
+// whole lines with the target row too (32 KiB per wave, 4 waves per CU) 1.12 ms;
+// 64-B pieces (16 KiB, 9 waves per CU) 0.82 ms; 32-B pieces 1.32 ms.
+#ifndef UT_DE_GW
+#define UT_DE_GW 8
+#endif
+constexpr int DE_GW = UT_DE_GW;                  // columns per staged group (8: 64-B half lines, 16: whole lines)
+constexpr int DE_CH = DE_GW / 2;                 // 16-B chunks per row and group
+constexpr int DE_SW = DE_CH == 8 ? 1 : (DE_CH == 4 ? 2 : 3);  // swizzle: chunk ^ ((candidate >> DE_SW) & (DE_CH - 1))
+#ifndef UT_DE_DB
+#define UT_DE_DB 0
+#endif
+constexpr int DE_NBUF = UT_DE_DB ? 2 : 1;        // 2: group g + 1 is in flight while group g is processed
+constexpr int DE_AOS_BUF = 3 * 64 * DE_GW;       // the donor rows of one group per wave
+constexpr int DE_AOS_LDS_DBL = DE_NBUF * DE_AOS_BUF;
+
+template <bool DIFF, bool AOS>
+__global__ __launch_bounds__(AOS ? 64 : 256) void k_de(const DevParam* __restrict__ params, int32_t P,
                                             const double* __restrict__ vtab, const double* __restrict__ pop, int64_t ldp, int64_t npop,
                                             const double* __restrict__ best, int64_t share,
                                             double cr, int32_t n_cross, uint64_t seed, uint32_t round_,
                                             int64_t cand_base, int64_t m, double* __restrict__ out,
-                                            int64_t ldo, DeDiffOut dd, uint32_t* __restrict__ xglob) {
-  extern __shared__ uint32_t xlds[];  // [ceil(P/32)][256]
+                                            int64_t ldo, DeDiffOut dd, uint32_t* __restrict__ xglob,
+                                            const double* __restrict__ aos, int64_t lda) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t dyn_lds[];
+  double* const stg = reinterpret_cast<double*>(dyn_lds);                    // AOS: the donor lines
+  uint32_t* const xlds = AOS ? dyn_lds + 2 * DE_AOS_LDS_DBL : dyn_lds;       // [ceil(P/32)][blockDim]
   const int tid = threadIdx.x, lane = tid & 63;
   const int64_t i0 = (int64_t)blockIdx.x * blockDim.x + tid;
   // the bits live in LDS, or (spaces of more than 2048 params) in a global
-  // [ceil(P/32)][grid * 256] scratch
+  // [ceil(P/32)][grid * blockDim] scratch
   uint32_t* const xb = xglob ? xglob + i0 : xlds + tid;
   const int64_t xs = xglob ? (int64_t)gridDim.x * blockDim.x : (int64_t)blockDim.x;
   // out-of-range lanes of the last block run along (on candidate m-1) and
-  // write nothing: the DIFF epilogue takes one atomic per whole wave
+  // write nothing: the DIFF epilogue takes one atomic per whole wave, and the
+  // AOS gathers load the rows of every lane's donors
   const bool valid = i0 < m;
-  if (!DIFF && !valid) return;
+  if (!DIFF && !AOS && !valid) return;
   const int64_t i = valid ? i0 : m - 1;
   const uint64_t g = (uint64_t)(cand_base + i);
   const int64_t t = (int64_t)(g % (uint64_t)npop);
@@ -118,6 +150,64 @@ __global__ __launch_bounds__(256) void k_de(const DevParam* __restrict__ params,
   // use_f = old_div(random.random(), 2.0) + 0.5
   const double F = __dadd_rn(__ddiv_rn(u01_from(rf.x, rf.y), 2.0), 0.5);
   const double nF = -F;
+
+  // AOS: the donor rows of the 8 candidates each of this lane's 24 gather
+  // pieces ((donor k, candidate block q): candidate 8q + lane / 8, 16-B chunk
+  // lane % 8 of its line)
+  uint32_t srow[3][DE_CH];
+  int32_t cur_grp = -1;
+  int32_t staged[2] = {-1, -1};   // the group held by each LDS buffer
+  auto issue_group = [&](int32_t gi) {
+    staged[gi % DE_NBUF] = gi;
+    double* const buf = stg + (gi % DE_NBUF) * DE_AOS_BUF;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the previous group's LDS reads are done
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+#pragma unroll
+      for (int q = 0; q < DE_CH; ++q) {
+        const int cnd = (64 / DE_CH) * q + lane / DE_CH;
+        const int ch = (lane % DE_CH) ^ ((cnd >> DE_SW) & (DE_CH - 1));
+        const double* src = aos + (int64_t)srow[k][q] * lda + gi * DE_GW + ch * 2;
+        __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(buf + k * 64 * DE_GW + q * 128), 16,
+                                         0, 0);
+      }
+  };
+  if constexpr (AOS) {
+    const uint32_t r1 = d1 >= 0 ? (uint32_t)d1 : (uint32_t)npop, r2 = d2 >= 0 ? (uint32_t)d2 : (uint32_t)npop,
+                   r3 = d3 >= 0 ? (uint32_t)d3 : (uint32_t)npop;
+#pragma unroll
+    for (int q = 0; q < DE_CH; ++q) {
+      const int src_lane = (64 / DE_CH) * q + lane / DE_CH;
+      srow[0][q] = (uint32_t)__shfl((int)r1, src_lane, 64);
+      srow[1][q] = (uint32_t)__shfl((int)r2, src_lane, 64);
+      srow[2][q] = (uint32_t)__shfl((int)r3, src_lane, 64);
+    }
+    // the first group with a non-PERM column, issued ahead of the Philox pass
+    for (int32_t p = 0; p < P; ++p) {
+      const DevParam pr = params[p];
+      if (pr.kind != UT_PERM) {
+        cur_grp = pr.col / DE_GW;
+        break;
+      }
+    }
+    if (cur_grp >= 0) {
+      issue_group(cur_grp);
+      if (DE_NBUF == 2 && (cur_grp + 1) * DE_GW < lda) issue_group(cur_grp + 1);
+    }
+  }
+  // AOS: the target's value of param p, loaded one param ahead
+  auto load_vt = [&](int32_t p) -> double {
+    const DevParam q = params[p];
+    return q.kind != UT_PERM ? pop[(int64_t)q.col * ldp + t] : 0.0;
+  };
+  double vt_next = 0.0;
+  if constexpr (AOS) vt_next = load_vt(0);
+  // donor k's value of column col (AOS: from the staged group of col)
+  auto donor = [&](int k, int32_t col) -> double {
+    const int cc = col % DE_GW;
+    return stg[(cur_grp % DE_NBUF) * DE_AOS_BUF + k * 64 * DE_GW + lane * DE_GW +
+               ((((cc >> 1) ^ ((lane >> DE_SW) & (DE_CH - 1))) << 1) | (cc & 1))];
+  };
 
   // pass 1: forced set (up to 4 smallest (key, p)) and the cr-test bits
   uint64_t fk[4] = {~0ull, ~0ull, ~0ull, ~0ull};
@@ -144,9 +234,27 @@ __global__ __launch_bounds__(256) void k_de(const DevParam* __restrict__ params,
   uint32_t dw = 0;                  // DIFF: mask bits of the current word
   int32_t dwi = 0;                  // DIFF: its word index
   uint32_t dcnt = 0;                // DIFF: changed computed-digest values
+  if constexpr (AOS) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the first group landed
+  }
   for (int32_t p = 0; p < P; ++p) {
     const DevParam pr = params[p];
     if ((p & 31) == 0) xw = xb[(p >> 5) * xs];
+    if constexpr (AOS) {
+      // wave-uniform: columns grow with p, so the groups are staged in order
+      if (pr.kind != UT_PERM && pr.col / DE_GW != cur_grp) {
+        cur_grp = pr.col / DE_GW;
+        if (staged[cur_grp % DE_NBUF] != cur_grp) issue_group(cur_grp);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        // the next group into the other buffer (its previous group is consumed)
+        if (DE_NBUF == 2 && (cur_grp + 1) * DE_GW < lda) issue_group(cur_grp + 1);
+      }
+    }
+    double vt_pf = 0.0;
+    if constexpr (AOS) {
+      vt_pf = vt_next;
+      if (p + 1 < P) vt_next = load_vt(p + 1);
+    }
     bool forced = false;
 #pragma unroll
     for (int s = 0; s < 4; ++s) forced |= (s < n_cross) && ((uint32_t)fk[s] == (uint32_t)p) && (fk[s] != ~0ull);
@@ -175,13 +283,29 @@ __global__ __launch_bounds__(256) void k_de(const DevParam* __restrict__ params,
       }
       continue;
     }
-    const double vt = col[t];
+    double vt;
+    if constexpr (AOS) vt = vt_pf;
+    else vt = col[t];
     double v = vt;
     if (cross) {
-      const double xb = share ? best[pr.col] : 0.0;
-      const double x1 = d1 >= 0 ? col[d1] : xb, x2 = d2 >= 0 ? col[d2] : xb, x3 = d3 >= 0 ? col[d3] : xb;
+      double x1, x2, x3;
+      if constexpr (AOS) {
+        x1 = donor(0, pr.col);
+        x2 = donor(1, pr.col);
+        x3 = donor(2, pr.col);
+      } else {
+        const double xb = share ? best[pr.col] : 0.0;
+        x1 = d1 >= 0 ? col[d1] : xb;
+        x2 = d2 >= 0 ? col[d2] : xb;
+        x3 = d3 >= 0 ? col[d3] : xb;
+      }
       if (is_primitive(pr.kind)) {
-        const double va = unit_of(pr, x1, vtab), vb = unit_of(pr, x2, vtab), vc = unit_of(pr, x3, vtab);
+        double va = x1, vb = x2, vc = x3;   // AOS: the donor copy holds unit values
+        if constexpr (!AOS) {
+          va = unit_of(pr, x1, vtab);
+          vb = unit_of(pr, x2, vtab);
+          vc = unit_of(pr, x3, vtab);
+        }
         // v = a*va + b*vb + c*vc with a = 1.0, b = F, c = -F
         double u = __dadd_rn(__dadd_rn(__dmul_rn(1.0, va), __dmul_rn(F, vb)), __dmul_rn(nF, vc));
         u = py_max(0.0, py_min(u, 1.0));
@@ -565,18 +689,128 @@ int launch_population_init(ut_ctx* c, uint32_t round_) {
   return 0;
 }
 
+// the donor copy's value of column col: unit_of for a primitive param's
+// column, the raw value otherwise (complex params, PERM item columns)
+__device__ __forceinline__ double aos_value(const DevParam* __restrict__ params, const int32_t* __restrict__ col_param,
+                                            const double* __restrict__ vtab, int32_t col, double v) {
+  const int32_t pp = col_param[col];
+  if (pp < 0) return v;
+  const DevParam& pr = params[pp];
+  return is_primitive(pr.kind) ? unit_of(pr, v, vtab) : v;
+}
+
+// pop (column-major [ncols][ldp]) -> aos (member-major [npop][lda], donor
+// values): 64 members x 16 columns per 256-thread block through an LDS tile,
+// coalesced on both sides (64-member runs read, 128-B member lines written)
+__global__ __launch_bounds__(256) void k_pop_to_aos(const DevParam* __restrict__ params,
+                                                    const int32_t* __restrict__ col_param,
+                                                    const double* __restrict__ vtab, int32_t NC,
+                                                    const double* __restrict__ pop, int64_t ldp, int64_t npop,
+                                                    double* __restrict__ aos, int64_t lda) {
+  __shared__ double tile[64][17];
+  const int t = threadIdx.x;
+  const int64_t m0 = (int64_t)blockIdx.x * 64;
+  const int32_t c0 = blockIdx.y * 16;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int idx = t + 256 * r, cl = idx >> 6, ml = idx & 63;
+    const int64_t mem = m0 + ml;
+    const int32_t col = c0 + cl;
+    tile[ml][cl] = (mem < npop && col < NC) ? aos_value(params, col_param, vtab, col, pop[(int64_t)col * ldp + mem])
+                                            : 0.0;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int idx = t + 256 * r, ml = idx >> 4, cl = idx & 15;
+    const int64_t mem = m0 + ml;
+    if (mem < npop) aos[mem * lda + c0 + cl] = tile[ml][cl];
+  }
+}
+
+// aos rows idx[j] = donor values of trial column j (after ut_population_replace)
+__global__ void k_pop_aos_rows(const DevParam* __restrict__ params, const int32_t* __restrict__ col_param,
+                               const double* __restrict__ vtab, int32_t NC, double* __restrict__ aos, int64_t lda,
+                               const double* __restrict__ trial, int64_t ld, const int64_t* __restrict__ idx,
+                               int64_t n) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n * NC) return;
+  const int64_t j = e / NC;
+  const int32_t p = (int32_t)(e - j * NC);
+  aos[idx[j] * lda + p] = aos_value(params, col_param, vtab, p, trial[(int64_t)p * ld + j]);
+}
+
+int ensure_pop_aos(ut_ctx* c) {
+  if (c->pop_aos_valid) return 0;
+  const int64_t lda = pop_aos_ld(c);
+  const int64_t need = (c->npop + 1) * lda;   // + the best-config row
+  if (c->pop_aos_cap < need) {
+    if (c->pop_aos) {
+      UT_HIP(c, sync_all(c));
+      (void)hipFree(c->pop_aos);
+      c->pop_aos = nullptr;
+      c->pop_aos_cap = 0;
+    }
+    const hipError_t e = hipMalloc((void**)&c->pop_aos, sizeof(double) * need);
+    if (e != hipSuccess) return set_err(c, UT_ENOMEM, std::string("hipMalloc(pop_aos): ") + hipGetErrorString(e));
+    c->pop_aos_cap = need;
+  }
+  hipLaunchKernelGGL(k_pop_to_aos, dim3(grid1(c->npop, 64), (unsigned)(lda / 16)), dim3(256), 0, c->stream,
+                     c->space.d_params, c->space.d_col_param, c->space.d_vtab, c->space.ncols, c->pop, c->npop,
+                     c->npop, c->pop_aos, lda);
+  UT_LAUNCH_CHECK(c);
+  c->pop_aos_valid = true;
+  return 0;
+}
+
+int launch_pop_aos_rows(ut_ctx* c, const double* trial, int64_t ld, const int64_t* idx, int64_t n) {
+  const int64_t e = n * c->space.ncols;
+  hipLaunchKernelGGL(k_pop_aos_rows, dim3(grid1(e, 256)), dim3(256), 0, c->stream, c->space.d_params,
+                     c->space.d_col_param, c->space.d_vtab, c->space.ncols, c->pop_aos, pop_aos_ld(c), trial, ld, idx,
+                     n);
+  UT_LAUNCH_CHECK(c);
+  return 0;
+}
+
+__global__ void k_aos_row(const DevParam* __restrict__ params, const int32_t* __restrict__ col_param,
+                          const double* __restrict__ vtab, int32_t NC, const double* __restrict__ src,
+                          double* __restrict__ dst) {
+  const int32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p < NC) dst[p] = aos_value(params, col_param, vtab, p, src[p]);
+}
+
+int launch_aos_row(ut_ctx* c, const double* src, int64_t row) {
+  hipLaunchKernelGGL(k_aos_row, dim3(grid1(c->space.ncols, 64)), dim3(64), 0, c->stream, c->space.d_params,
+                     c->space.d_col_param, c->space.d_vtab, c->space.ncols, src, c->pop_aos + row * pop_aos_ld(c));
+  UT_LAUNCH_CHECK(c);
+  return 0;
+}
+
 int launch_de(ut_ctx* c, const ut_de_params* p, uint32_t round_, int64_t cand_base, int64_t m, double* out,
               int64_t ld, bool diff) {
-  constexpr int NT = 256;
-  const unsigned grid = grid1(m, NT);
   const int32_t nw = (c->space.P + 31) / 32;
-  size_t lds = sizeof(uint32_t) * (size_t)nw * NT;
+  // member-major donor gathers (k_de<., true>) up to 2048 params (cr-test bits in LDS)
+  const bool aos = c->de_aos && nw <= 64;
+  const int NT = aos ? 64 : 256;
+  const unsigned grid = grid1(m, NT);
+  size_t lds = sizeof(uint32_t) * (size_t)nw * NT + (aos ? sizeof(double) * DE_AOS_LDS_DBL : 0);
   uint32_t* xg = nullptr;
   if (nw > 64) {  // > 2048 params: the cr-test bits go to a global scratch
     const int rc = ensure(c, c->de_xbits, (size_t)nw * grid * NT);
     if (rc) return rc;
     xg = c->de_xbits.p;
     lds = 0;
+  }
+  const int64_t share = p->best ? (int64_t)p->information_sharing : (int64_t)0;
+  int64_t lda = 0;
+  if (aos) {
+    const int rc = ensure_pop_aos(c);
+    if (rc) return rc;
+    lda = pop_aos_ld(c);
+    if (share) {   // row npop: the best config, the donor of pool positions >= npop - 1
+      const int rc = launch_aos_row(c, p->best, c->npop);
+      if (rc) return rc;
+    }
   }
   DeDiffOut dd{nullptr, nullptr, nullptr, 0};
   diff = diff && c->space.n_comp > 0;
@@ -587,10 +821,10 @@ int launch_de(ut_ctx* c, const ut_de_params* p, uint32_t round_, int64_t cand_ba
     dd = DeDiffOut{c->r_mask.p, c->r_pairs.p, reinterpret_cast<unsigned long long*>(c->r_npairs.p),
                    c->space.n_comp};
   }
-  hipLaunchKernelGGL(diff ? k_de<true> : k_de<false>, dim3(grid), dim3(NT), lds, c->stream, c->space.d_params,
-                     c->space.P, c->space.d_vtab, c->pop, c->npop, c->npop, p->best,
-                     p->best ? (int64_t)p->information_sharing : (int64_t)0, p->cr, p->n_cross, c->seed, round_,
-                     cand_base, m, out, ld, dd, xg);
+  auto kern = aos ? (diff ? k_de<true, true> : k_de<false, true>) : (diff ? k_de<true, false> : k_de<false, false>);
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(NT), lds, c->stream, c->space.d_params, c->space.P, c->space.d_vtab,
+                     c->pop, c->npop, c->npop, p->best, share, p->cr, p->n_cross, c->seed, round_, cand_base, m, out,
+                     ld, dd, xg, c->pop_aos, lda);
   UT_LAUNCH_CHECK(c);
   return 0;
 }
@@ -659,6 +893,10 @@ extern "C" int ut_population_replace(ut_ctx* c, const double* trial, int64_t ld,
   hipLaunchKernelGGL(ut::k_pop_replace, dim3(ut::grid1(n, 64)), dim3(64), 0, c->stream, c->space.ncols, c->pop,
                      c->npop, trial, ld, idx, n);
   UT_LAUNCH_CHECK(c);
+  if (c->pop_aos_valid) {
+    const int rc = ut::launch_pop_aos_rows(c, trial, ld, idx, n);
+    if (rc) return rc;
+  }
   // keep the population's inner-digest cache current: only the replaced rows
   if (c->pop_dig_valid) return ut::launch_pop_digests(c, idx, n);
   return 0;
@@ -703,6 +941,7 @@ extern "C" int ut_pso_commit(ut_ctx* c, const double* values, const double* vel,
            UT_EINVAL, "pso_commit: bad arguments");
   if (m == 0) return 0;
   c->pop_dig_valid = false;   // positions moved: the inner-digest cache is rebuilt when a DE round needs it
+  c->pop_aos_valid = false;   // and so is the member-major copy
   UT_HIP(c, hipMemcpy2DAsync(c->pop + cand_base, sizeof(double) * c->npop, values, sizeof(double) * ld,
                              sizeof(double) * m, c->space.ncols, hipMemcpyDeviceToDevice, c->stream));
   if (vel)

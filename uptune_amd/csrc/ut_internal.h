@@ -83,6 +83,7 @@ struct Space {
   int32_t* d_perm_len = nullptr;          // per PERM slot: len(repr(list)) (constant per param)
   int32_t n_comp = 0;                     // params whose inner digest is computed (cslot >= 0)
   int32_t* d_comp = nullptr;              // cslot -> param index
+  int32_t* d_col_param = nullptr;         // value column -> its param (first column of a non-PERM param), or -1
 };
 
 template <class T>
@@ -162,6 +163,16 @@ struct ut_ctx {
   uint32_t* pop_dig = nullptr;
   int64_t pop_dig_cap = 0;
   bool pop_dig_valid = false;
+  // member-major donor copy of the selected population ([npop + 1][ld], ld =
+  // ncols rounded up to 16 columns = whole 128-B lines), primitive params
+  // stored as their unit values (unit_of), the others raw: k_de gathers its
+  // donors' rows from it in line pieces staged in LDS, with no unit_of left to
+  // compute; row npop holds the best config of the current DE launch.  Rebuilt
+  // from pop when stale, patched by replace.
+  double* pop_aos = nullptr;
+  int64_t pop_aos_cap = 0;
+  bool pop_aos_valid = false;
+  int32_t de_aos = 1;   // 0: k_de gathers donor values from the column-major population (UT_DE_AOS=0)
 
   struct PopSlot {
     double* pop = nullptr;
@@ -172,6 +183,9 @@ struct ut_ctx {
     uint32_t* pop_dig = nullptr;
     int64_t pop_dig_cap = 0;
     bool pop_dig_valid = false;
+    double* pop_aos = nullptr;
+    int64_t pop_aos_cap = 0;
+    bool pop_aos_valid = false;
   };
   std::vector<PopSlot> pop_slots;
   int32_t pop_slot = 0;
@@ -352,6 +366,13 @@ int launch_hash_de(ut_ctx* c, const double* values, int64_t ld, int64_t m, int64
 int ensure_de_diff(ut_ctx* c, int64_t ld);
 // population cache maintenance: full rebuild, or the rows idx[0..n) after a replace
 int launch_pop_digests(ut_ctx* c, const int64_t* idx, int64_t n);
+// the member-major population copy: rebuilt if stale (ensure), or the rows
+// idx[0..n) patched from trial after a replace
+int ensure_pop_aos(ut_ctx* c);
+int launch_pop_aos_rows(ut_ctx* c, const double* trial, int64_t ld, const int64_t* idx, int64_t n);
+// row `row` of the donor copy = the config `src` (device, ncols values)
+int launch_aos_row(ut_ctx* c, const double* src, int64_t row);
+inline int64_t pop_aos_ld(const ut_ctx* c) { return ((int64_t)c->space.ncols + 15) / 16 * 16; }
 int launch_hist_insert(ut_ctx* c, const uint32_t* dig, int64_t n);
 int launch_hist_rehash(ut_ctx* c, const uint32_t* okeys, const uint32_t* ostate, int64_t ocap);
 int launch_dedup(ut_ctx* c, const uint32_t* dig, int64_t m, uint8_t* dup);
