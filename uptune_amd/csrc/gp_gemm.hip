@@ -104,9 +104,14 @@ __global__ __launch_bounds__(K_NT, 2) void k_gp_kstar(const double* __restrict__
   constexpr int T_DBL = H3 ? 2 * K_BN * T_PITCH * 2 / 8 : 0;          // image size in doubles
   constexpr int RED_OFF = H3 ? T_DBL : 0;
   constexpr int MAIN = H3 ? (T_DBL + 2 * K_BN > 2 * K_STAGE ? T_DBL + 2 * K_BN : 2 * K_STAGE) : 2 * K_STAGE;
-  __shared__ __attribute__((aligned(16))) double lds[MAIN + EXP_TAB + 2];
+  // + the item's epilogue operands, staged by glds with its first K stage:
+  // |x_r|^2 and alpha_r of its 128 rows, |u_c|^2 of its 128 columns (read from
+  // LDS in the epilogue instead of 16 + 16 + 4 doubles held in VGPRs per lane:
+  // the fp64 MU variant spilled 100 B/lane)
+  __shared__ __attribute__((aligned(16))) double lds[MAIN + EXP_TAB + 2 + 3 * K_BM];
   double* etab = lds + MAIN;
   int32_t& s_item = *reinterpret_cast<int32_t*>(lds + MAIN + EXP_TAB);
+  double* const rowop = lds + MAIN + EXP_TAB + 2;   // [xnorm 128][alpha 128][cnorm 128]
   _Float16* timg = reinterpret_cast<_Float16*>(lds);
   const int t = threadIdx.x, lane = t & 63;
   if (t < EXP_TAB) etab[t] = sf2 * exp2((double)t / EXP_TAB);  // published by the first ticket barrier
@@ -133,6 +138,12 @@ __global__ __launch_bounds__(K_NT, 2) void k_gp_kstar(const double* __restrict__
       for (int jj = 0; jj < 4; ++jj) acc[i][jj] = (d4){0.0, 0.0, 0.0, 0.0};
 
     kstar_issue(AT, lda, B, ldb, row0, col0, 0, lds, w, lane);
+    {  // one 1-KiB glds per operand (rows < npad, columns < ldk are in range)
+      const double* src = w == 0 ? xnorm + row0 : (w == 1 ? alpha + row0 : cnorm + col0);
+      if (w < 3 && (MU || w != 1))
+        __builtin_amdgcn_global_load_lds(src + lane * 2, (__attribute__((address_space(3))) void*)(rowop + w * K_BM),
+                                         16, 0, 0);
+    }
     for (int32_t kt = 0; kt < nk; ++kt) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();  // stage kt landed everywhere; stage kt-1 fully read
@@ -158,62 +169,60 @@ __global__ __launch_bounds__(K_NT, 2) void k_gp_kstar(const double* __restrict__
 
     __syncthreads();  // ring free: reuse as the column reduction buffer (and the h3 image)
     double* red = lds + RED_OFF;  // [2][128]
-    // epilogue operands loaded up front and unconditionally (rows < npad,
-    // columns < ldk are always in range): a load under a per-element condition
-    // makes hipcc wait vmcnt(0) per element.  Padding rows / columns get a
-    // huge negative half-norm, so their k* is exactly 0 without a select.
-    double hx[4][4], al[4][4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int32_t row = row0 + wm * 64 + i * 16 + (lane >> 4) + 4 * r;
-        const double xr = xnorm[row];
-        hx[i][r] = row < n ? -0.5 * xr : -1e300;
-        if constexpr (MU) al[i][r] = alpha[row];
-      }
+    // epilogue operands from the LDS copies (landed with the first K stage).
+    // Padding rows / columns get a huge negative half-norm, so their k* is
+    // exactly 0 without a select.
     double hc[4];
 #pragma unroll
     for (int jj = 0; jj < 4; ++jj) {
-      const int64_t col = col0 + wn * 64 + jj * 16 + (lane & 15);
-      const double cr = cnorm[col];
-      hc[jj] = col < m ? -0.5 * cr : -1e300;
+      const int cl = wn * 64 + jj * 16 + (lane & 15);
+      hc[jj] = col0 + cl < m ? -0.5 * rowop[2 * K_BM + cl] : -1e300;
     }
     const bool want2 = !H3 && MU && part2 != nullptr;
+    double s[4] = {0.0, 0.0, 0.0, 0.0}, s2[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-    for (int jj = 0; jj < 4; ++jj) {
-      const int cl = wn * 64 + jj * 16 + (lane & 15);
-      const int64_t col = col0 + cl;
-      double s = 0.0, s2 = 0.0;
+    for (int i = 0; i < 4; ++i) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
+      for (int r = 0; r < 4; ++r) {
+        const int rl = wm * 64 + i * 16 + (lane >> 4) + 4 * r;
+        const int32_t row = row0 + rl;
+        const double hx = row < n ? -0.5 * rowop[rl] : -1e300;
+        double al = 0.0;
+        if constexpr (MU) al = rowop[K_BM + rl];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int32_t row = row0 + wm * 64 + i * 16 + (lane >> 4) + 4 * r;
+        for (int jj = 0; jj < 4; ++jj) {
+          const int cl = wn * 64 + jj * 16 + (lane & 15);
+          const int64_t col = col0 + cl;
           // -|x - u|^2 / 2 = C - |x|^2/2 - |u|^2/2, clamped to [-1000, 0]
-          const double x = __builtin_fmax(__builtin_fmin((acc[i][jj][r] + hx[i][r]) + hc[jj], 0.0), -1000.0);
+          const double x = __builtin_fmax(__builtin_fmin((acc[i][jj][r] + hx) + hc[jj], 0.0), -1000.0);
           const double ks = sf2_exp_nonpos(x, etab);
           if constexpr (H3) {
             const double xs = ks * kscale;
             const _Float16 hi = (_Float16)(float)xs;
-            const int o = cl * T_PITCH + (row - row0);
+            const int o = cl * T_PITCH + rl;
             timg[o] = hi;
             timg[K_BN * T_PITCH + o] = (_Float16)(float)(xs - (double)hi);
           } else {
             if (rt < store_rt) kst[(int64_t)row * ldk + col] = (TS)ks;   // pruned scoring stores the bound rows only
           }
-          if constexpr (MU) s += al[i][r] * ks;
-          if constexpr (MU && !H3) s2 += ks * ks;
+          if constexpr (MU) s[jj] += al * ks;
+          if constexpr (MU && !H3) s2[jj] += ks * ks;
         }
       }
-      if constexpr (MU) {
-        s += __shfl_xor(s, 16);
-        s += __shfl_xor(s, 32);
-        if ((lane >> 4) == 0) red[wm * K_BN + cl] = s;
+    }
+    if constexpr (MU) {
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        const int cl = wn * 64 + jj * 16 + (lane & 15);
+        double a = s[jj];
+        a += __shfl_xor(a, 16);
+        a += __shfl_xor(a, 32);
+        if ((lane >> 4) == 0) red[wm * K_BN + cl] = a;
         if (want2) {
-          s2 += __shfl_xor(s2, 16);
-          s2 += __shfl_xor(s2, 32);
-          if ((lane >> 4) == 0) red[2 * K_BN + wm * K_BN + cl] = s2;
+          double b = s2[jj];
+          b += __shfl_xor(b, 16);
+          b += __shfl_xor(b, 32);
+          if ((lane >> 4) == 0) red[2 * K_BN + wm * K_BN + cl] = b;
         }
       }
     }
