@@ -32,30 +32,29 @@ __global__ void k_to_f32(const double* __restrict__ src, float* __restrict__ dst
 constexpr int K_NT = 256, K_BM = 128, K_BN = 128, K_BK = 16;
 constexpr int KSTAR_SPARE_PER_XCD = 2;  // CUs left to an in-flight GP fit (launch_gemm_kstar)
 
-// sf2 * exp(x) for x in [-1000, 0], table-driven: x = (32 k' + j) ln2/32 + r,
-// |r| <= ln2/64, so exp(x) = 2^k' * 2^(j/32) * e^r with a degree-6 polynomial
-// for e^r (truncation < 4e-18) and etab[j] = sf2 * 2^(j/32) built in LDS by each
-// workgroup.  About 16 VALU ops against ~32 for the library exp with its range
-// checks (the epilogue shares the SIMDs with the f64 MFMAs, so every op counts).
+// sf2 * exp(x) for x in [-1000, 0], table-driven: x = (256 k' + j) ln2/256 + r,
+// |r| <= ln2/512, so exp(x) = 2^k' * 2^(j/256) * e^r with a degree-4 polynomial
+// for e^r (truncation < 4e-17) and etab[j] = sf2 * 2^(j/256) built in LDS by each
+// workgroup (2 KiB).  About 14 VALU ops against ~32 for the library exp with its
+// range checks (the epilogue shares the SIMDs with the f64 MFMAs, so every op
+// counts; the 32-entry table with a degree-6 polynomial took two more FMAs).
 // Max error ~2 ulp; 2^k' underflows to exactly 0 at x = -1000.
-constexpr int EXP_TAB = 32;
+constexpr int EXP_TAB = 256;
 
 __device__ __forceinline__ double sf2_exp_nonpos(double x, const double* etab) {
-  constexpr double INV_L = 46.16624130844683;        // 32 / ln 2
-  constexpr double L_HI = 0.02166084938653512;        // ln2/32 to 32 bits: kf * L_HI is exact
-  constexpr double L_LO = 5.9631716539705866e-12;     // ln2/32 - L_HI
+  constexpr double INV_L = 369.3299304675746;         // 256 / ln 2
+  constexpr double L_HI = 0.00270760617331689;        // ln2/256 to 32 bits: kf * L_HI is exact
+  constexpr double L_LO = 7.453964567463233e-13;      // ln2/256 - L_HI
   const double kf = __builtin_rint(x * INV_L);
   double r = __builtin_fma(kf, -L_HI, x);
   r = __builtin_fma(kf, -L_LO, r);
-  double p = 1.0 / 720.0;
-  p = __builtin_fma(p, r, 1.0 / 120.0);
-  p = __builtin_fma(p, r, 1.0 / 24.0);
+  double p = 1.0 / 24.0;
   p = __builtin_fma(p, r, 1.0 / 6.0);
   p = __builtin_fma(p, r, 0.5);
   p = __builtin_fma(p, r, 1.0);
   p = __builtin_fma(p, r, 1.0);
   const int k = (int)kf;
-  return __builtin_ldexp(p * etab[k & 31], k >> 5);
+  return __builtin_ldexp(p * etab[k & (EXP_TAB - 1)], k >> 8);
 }
 
 constexpr int K_SA = K_BK * K_BM, K_SB = K_BK * K_BN, K_STAGE = K_SA + K_SB;
