@@ -373,8 +373,13 @@ int ut_space_define(ut_ctx* c, int32_t P, const ut_param_desc* params, int32_t p
   UT_HIP(c, hipMalloc((void**)&s.d_order, sizeof(int32_t) * P));
   UT_HIP(c, hipMemcpy(s.d_order, s.host_order.data(), sizeof(int32_t) * P, hipMemcpyHostToDevice));
   if (lut.empty()) lut.resize(8, 0u);
-  UT_HIP(c, hipMalloc((void**)&s.d_lut, sizeof(uint32_t) * lut.size()));
-  UT_HIP(c, hipMemcpy(s.d_lut, lut.data(), sizeof(uint32_t) * lut.size(), hipMemcpyHostToDevice));
+  {  // the device LUT holds each digest as its 64 hex characters (16 big-endian
+     // words, what the outer message holds): k_hash copies them into its hex slot
+    std::vector<uint32_t> luthex(lut.size() * 2);
+    for (size_t e = 0; e < lut.size() / 8; ++e) ut::digest_hex(&lut[8 * e], &luthex[16 * e]);
+    UT_HIP(c, hipMalloc((void**)&s.d_lut, sizeof(uint32_t) * luthex.size()));
+    UT_HIP(c, hipMemcpy(s.d_lut, luthex.data(), sizeof(uint32_t) * luthex.size(), hipMemcpyHostToDevice));
+  }
   if (vtab.empty()) vtab.resize(1, 0.0);
   UT_HIP(c, hipMalloc((void**)&s.d_vtab, sizeof(double) * vtab.size()));
   UT_HIP(c, hipMemcpy(s.d_vtab, vtab.data(), sizeof(double) * vtab.size(), hipMemcpyHostToDevice));

@@ -34,6 +34,16 @@
 namespace ut {
 
 constexpr int HASH_NT = 128;
+
+// a digest as its 64 hex characters: 16 big-endian words, 4 x 16-B stores
+__device__ __forceinline__ void store_hex(uint4* dst, const uint32_t D[8]) {
+  uint32_t X[16];
+  digest_hex(D, X);
+  dst[0] = make_uint4(X[0], X[1], X[2], X[3]);
+  dst[1] = make_uint4(X[4], X[5], X[6], X[7]);
+  dst[2] = make_uint4(X[8], X[9], X[10], X[11]);
+  dst[3] = make_uint4(X[12], X[13], X[14], X[15]);
+}
 constexpr int SCR_WORDS = 7;                       // inner message bytes 0..27
 
 typedef uint32_t hex32 __attribute__((ext_vector_type(32)));
@@ -172,9 +182,7 @@ __global__ __launch_bounds__(HASH_NT) void k_pop_digests(const DevParam* __restr
   const DevParam pr = params[comp[s]];
   uint32_t D[8];
   repr_digest(pr, pop[(int64_t)pr.col * npop + j], lds, lane, D);
-  uint4* dst = cache + 2 * ((int64_t)s * npop + j);
-  dst[0] = make_uint4(D[0], D[1], D[2], D[3]);
-  dst[1] = make_uint4(D[4], D[5], D[6], D[7]);
+  store_hex(cache + 4 * ((int64_t)s * npop + j), D);
 }
 
 constexpr int DIFF_NT = 256;
@@ -246,17 +254,17 @@ __global__ __launch_bounds__(HASH_NT) void k_inner_pairs(const DevParam* __restr
     const DevParam pr = params[comp[s]];
     uint32_t D[8];
     repr_digest(pr, values[(int64_t)pr.col * ld + i], lds, lane, D);
-    uint4* dst = fresh + 2 * ((int64_t)s * ld + i);
-    dst[0] = make_uint4(D[0], D[1], D[2], D[3]);
-    dst[1] = make_uint4(D[4], D[5], D[6], D[7]);
+    store_hex(fresh + 4 * ((int64_t)s * ld + i), D);
   }
 }
 
-// Inner digests of the computed-digest params, when k_hash reuses them (DE rounds)
+// Inner digests of the computed-digest params, when k_hash reuses them (DE
+// rounds), kept as their 64 hex characters (16 big-endian words: what the
+// outer message holds), so k_hash moves them into its hex slot as they are
 struct InnerRef {
   const uint32_t* mask;   // [ceil(n_comp / 32)][ld]
-  const uint4* fresh;     // [n_comp][ld][8 words]
-  const uint4* cache;     // [n_comp][npop][8 words]; nullptr = compute every inner digest in k_hash
+  const uint4* fresh;     // [n_comp][ld][16 hex words]
+  const uint4* cache;     // [n_comp][npop][16 hex words]; nullptr = compute every inner digest in k_hash
   int64_t npop, cand_base;
 };
 
@@ -266,6 +274,19 @@ struct InnerRef {
 // 3.42 ms at C2.  Tried and not kept: the two hex slots in LDS instead of 32
 // VGPRs (104 VGPRs, still 4 waves: 3.59 ms, the ds_reads cost more than the
 // registers), 5 or 6 waves/SIMD (107 / 137 VGPRs spilled: 4.53 / 6.87 ms).
+// 16 hex words into hex slot `odd` (static register indices in both branches)
+__device__ __forceinline__ void put_hex(hex32& HX, int odd, uint4 q0, uint4 q1, uint4 q2, uint4 q3) {
+  const uint32_t q[16] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w,
+                          q2.x, q2.y, q2.z, q2.w, q3.x, q3.y, q3.z, q3.w};
+  if (odd) {
+#pragma unroll
+    for (int k = 0; k < 16; ++k) HX[16 + k] = q[k];
+  } else {
+#pragma unroll
+    for (int k = 0; k < 16; ++k) HX[k] = q[k];
+  }
+}
+
 template <bool REF, int MINW>
 __global__ __launch_bounds__(HASH_NT, MINW) void k_hash(const DevParam* __restrict__ params,
                                                   const int32_t* __restrict__ order,
@@ -299,11 +320,13 @@ __global__ __launch_bounds__(HASH_NT, MINW) void k_hash(const DevParam* __restri
         const double v = vnext;
         uint32_t D[8];
         if (pr.hash_mode == HM_LUT) {
-          const uint4* src = lut + 2 * lut_row(pr, v);
-          const uint4 a = src[0], c = src[1];  // issued before the prefetch: waits leave it in flight
+          // the value's hex digest from the LUT, straight into the hex slot
+          const uint4* src = lut + 4 * lut_row(pr, v);
+          const uint4 q0 = src[0], q1 = src[1], q2 = src[2], q3 = src[3];  // issued before the prefetch
           if (next + 1 < P) vnext = values[(int64_t)order_col[next + 1] * ld + i];
-          D[0] = a.x; D[1] = a.y; D[2] = a.z; D[3] = a.w;
-          D[4] = c.x; D[5] = c.y; D[6] = c.z; D[7] = c.w;
+          put_hex(HX, next & 1, q0, q1, q2, q3);
+          ++next;
+          continue;
         } else if (pr.hash_mode == HM_PERM) {
           const uint4* src = perm_dig + 2 * ((int64_t)pr.pslot * m + i);
           const uint4 a = src[0], c = src[1];
@@ -311,14 +334,16 @@ __global__ __launch_bounds__(HASH_NT, MINW) void k_hash(const DevParam* __restri
           D[0] = a.x; D[1] = a.y; D[2] = a.z; D[3] = a.w;
           D[4] = c.x; D[5] = c.y; D[6] = c.z; D[7] = c.w;
         } else if constexpr (REF) {
-          // the target's cached digest, or this trial's fresh one (k_inner_pairs)
+          // the target's cached hex digest, or this trial's fresh one (k_inner_pairs),
+          // straight into the hex slot
           const uint32_t mw = ref.mask[(int64_t)(pr.cslot >> 5) * ld + i];
-          const uint4* src = ((mw >> (pr.cslot & 31)) & 1u) ? ref.fresh + 2 * ((int64_t)pr.cslot * ld + i)
-                                                             : ref.cache + 2 * ((int64_t)pr.cslot * ref.npop + t);
-          const uint4 a = src[0], c = src[1];
+          const uint4* src = ((mw >> (pr.cslot & 31)) & 1u) ? ref.fresh + 4 * ((int64_t)pr.cslot * ld + i)
+                                                             : ref.cache + 4 * ((int64_t)pr.cslot * ref.npop + t);
+          const uint4 q0 = src[0], q1 = src[1], q2 = src[2], q3 = src[3];
           if (next + 1 < P) vnext = values[(int64_t)order_col[next + 1] * ld + i];
-          D[0] = a.x; D[1] = a.y; D[2] = a.z; D[3] = a.w;
-          D[4] = c.x; D[5] = c.y; D[6] = c.z; D[7] = c.w;
+          put_hex(HX, next & 1, q0, q1, q2, q3);
+          ++next;
+          continue;
         } else {
           if (next + 1 < P) vnext = values[(int64_t)order_col[next + 1] * ld + i];
           repr_digest(pr, v, lds, lane, D);
@@ -395,7 +420,7 @@ int launch_pop_digests(ut_ctx* c, const int64_t* idx, int64_t n) {
   const Space& s = c->space;
   if (s.n_comp == 0 || c->npop == 0) return 0;
   if (!idx) {  // full rebuild
-    const int64_t need = (int64_t)s.n_comp * c->npop * 8;
+    const int64_t need = (int64_t)s.n_comp * c->npop * 16;   // 64 hex characters per digest
     if (c->pop_dig_cap < need) {
       if (c->pop_dig) {
         UT_HIP(c, sync_all(c));
@@ -423,7 +448,7 @@ int ensure_de_diff(ut_ctx* c, int64_t ld) {
   const int32_t nw = (s.n_comp + 31) / 32;
   int rc;
   if ((rc = ensure(c, c->r_mask, (size_t)nw * ld))) return rc;
-  if ((rc = ensure(c, c->r_fresh, (size_t)s.n_comp * ld * 8))) return rc;
+  if ((rc = ensure(c, c->r_fresh, (size_t)s.n_comp * ld * 16))) return rc;   // hex digests
   if ((rc = ensure(c, c->r_pairs, (size_t)s.n_comp * ld))) return rc;
   return ensure(c, c->r_npairs, 1);
 }

@@ -73,7 +73,7 @@ struct Space {
   int32_t* d_order = nullptr;             // sorted position -> param index
   HashWord* d_words = nullptr;            // outer_blocks * 16
   int32_t* d_block_last = nullptr;        // last sorted position needed by each block
-  uint32_t* d_lut = nullptr;              // digests [*][8]
+  uint32_t* d_lut = nullptr;              // digests as hex [*][16 words]
   double* d_vtab = nullptr;               // LOGINT get_value tables (host-computed by CPython)
   int32_t* d_order_col = nullptr;         // sorted position -> first value column
   int32_t* d_perm_params = nullptr;       // PERM param indices, by digest slot
