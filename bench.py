@@ -126,6 +126,68 @@ def load_pmc(kernel_key):
         return {}, ""
 
 
+SHA256_CEIL_GCPS = 28.5   # measured chip ceiling of SHA-256 compressions (scripts/exp/sha_rate.hip)
+
+
+def kernel_table(m, n, d, outer_blocks):
+    """Per-kernel rooflines of the default C2 round from the committed rocprofv3
+    record (profiles/pmc_summary.json: average launch duration from the
+    --kernel-trace --stats pass, HBM bytes from the FETCH_SIZE / WRITE_SIZE
+    passes of the same command).  Algorithmic work per launch:
+      k_de: 40 d B per candidate (target, 3 donors, trial); k_hash (outer):
+      outer_blocks compressions per candidate; K*: 2 n dpad flops; encode: 16 F B."""
+    out = {}
+    try:
+        with open(os.path.join(ROOT, "profiles", "pmc_summary.json")) as f:
+            pmc = json.load(f)
+    except Exception:
+        return out
+    try:   # the counter pass of the same round (dispatches serialized: each kernel alone on the chip)
+        with open(os.path.join(ROOT, "profiles", "clock_summary.json")) as f:
+            clk = json.load(f)
+    except Exception:
+        clk = {}
+
+    def rec(key):
+        r = pmc.get(key) or {}
+        c = clk.get(key) or {}
+        t = c.get("duration_ms", 0.0) * 1e-3 or (r.get("avg_ns") or 0.0) * 1e-9
+        return t, r.get("hbm_bytes_per_launch")
+
+    def hbm(key, alg_bytes):
+        t, traffic = rec(key)
+        if t <= 0:
+            return
+        out[key] = {"bound": "hbm", "ms": t * 1e3, "achieved_GBps": alg_bytes / t / 1e9,
+                    "frac": alg_bytes / t / 1e9 / PEAK_HBM_GBS, "algorithmic_bytes": alg_bytes,
+                    "traffic_bytes": traffic, "traffic_GBps": (traffic / t / 1e9) if traffic else None}
+
+    def mfma(key, flops):
+        t, traffic = rec(key)
+        if t <= 0:
+            return
+        out[key] = {"bound": "mfma", "ms": t * 1e3, "achieved_TFps": flops / t / 1e12,
+                    "frac": flops / t / 1e12 / PEAK_FP64_TFLOPS, "flops": flops, "traffic_bytes": traffic}
+
+    hbm("propose", 40.0 * d * m)
+    hbm("encode", 16.0 * d * m)
+    mfma("kstar", 2.0 * n * (d + (-d) % 16) * m)   # the variance GEMM is `roofline` (HIP events of this run)
+    t, traffic = rec("hash")
+    if t > 0:
+        c = float(outer_blocks) * m
+        out["hash"] = {"bound": "int VALU (SHA-256)", "ms": t * 1e3, "achieved_Gcompressions_ps": c / t / 1e9,
+                       "frac": c / t / 1e9 / SHA256_CEIL_GCPS, "compressions": c, "traffic_bytes": traffic,
+                       "ceiling": f"{SHA256_CEIL_GCPS} G compressions/s (measured, scripts/exp/sha_rate.hip)"}
+    for key, r in out.items():
+        if key in clk:
+            r["clock_ghz"] = clk[key].get("clock_ghz")
+            r["mfma_busy"] = clk[key].get("mfma_busy")
+    out["_source"] = ("durations: profiles/clock_summary.json (rocprofv3 counter pass of the C2 round, dispatches "
+                      "serialized, so each kernel ran alone), else the --kernel-trace --stats average; HBM bytes: "
+                      "profiles/pmc_summary.json (" + pmc.get("_note", "").split("source:")[-1].strip() + ")")
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -370,6 +432,7 @@ def main():
         "config": {"workload": workload, "candidates_per_gpu": m, "gp_n": n, "dims": d, "k": k,
                    "parallelism": f"dp{world}"},
         "stage_ms": stages,
+        "kernels": (kernel_table(m, n, d, eng.space_info()[1]) if profiled else None),
         "prune": prune_info,
         "roofline": {"bound": "mfma", "kernel": kernel,
                      "achieved": achieved, "peak": peak, "unit": "TFLOP/s",

@@ -9,8 +9,10 @@ import json
 import sys
 from collections import defaultdict
 
-KERNELS = {"var": ("ut::k_gp_var_pp(", "void ut::k_gp_var<double>"), "kstar": ("void ut::k_gp_kstar<double, false>",),
-           "hash": ("void ut::k_hash<", "ut::k_hash("), "propose": ("void ut::k_de<", "ut::k_de("),
+KERNELS = {"var": ("void ut::k_gp_var_pp<false>(", "ut::k_gp_var_pp(", "void ut::k_gp_var<double>"),
+           "kstar": ("void ut::k_gp_kstar<double, false>",), "inner_pairs": ("ut::k_inner_pairs",),
+           "encode": ("ut::k_encode_scaled",),
+           "hash": ("void ut::k_hash<true", "void ut::k_hash<", "ut::k_hash("), "propose": ("void ut::k_de<", "ut::k_de("),
            "var16": ("_ZN2ut11k_gp_var_h3",), "kstar16": ("_ZN2ut10k_gp_kstarIDF16_",)}
 
 
@@ -25,7 +27,11 @@ def main(d, n_cu=256, peak_ghz=2.4):
                     "(4 SIMDs x CUs x clock cycles of the kernel); profiled passes run ~2-5% slower "
                     "(MI355X_MICROARCH.md DVFS item 2)"}
     for key, prefixes in KERNELS.items():
-        ds = [v for v in rows.values() if v["_name"].startswith(prefixes)]
+        ds = []
+        for pre in prefixes:   # the first prefix with dispatches wins
+            ds = [v for v in rows.values() if v["_name"].startswith(pre)]
+            if ds:
+                break
         if not ds:
             continue
         clk = [v["GRBM_GUI_ACTIVE"] / 8 / v["_ns"] for v in ds]           # cycles per ns = GHz

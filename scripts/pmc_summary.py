@@ -17,7 +17,7 @@ import sys
 from collections import defaultdict
 
 STAGES = {  # stage key -> kernel-name prefixes (the first match wins)
-    "var": ("ut::k_gp_var_pp(", "void ut::k_gp_var<double>"), "var_1wg": ("void ut::k_gp_var<double>",),
+    "var": ("void ut::k_gp_var_pp<false>(", "ut::k_gp_var_pp(", "void ut::k_gp_var<double>"), "var_1wg": ("void ut::k_gp_var<double>",),
     "kstar": ("void ut::k_gp_kstar<double, false>",),
     "var32": ("void ut::k_gp_var<float>",), "kstar32": ("void ut::k_gp_kstar<float, true>",),
     "hash": ("void ut::k_hash<true", "void ut::k_hash<", "ut::k_hash("),
