@@ -99,24 +99,16 @@ int cpub_de_hash_float(int32_t P, const double* lo, const double* hi, const int3
     pick_donors(rc.x, rc.y, rc.z, npop, t, d1, d2, d3);
     const ut::u32x4 rf = ut::draw(seed, g, ut::STREAM_CAND | 1u, round_, ut::OP_DE);
     const double F = ut::u01_from(rf.x, rf.y) / 2.0 + 0.5;
-    uint64_t fk[4] = {~0ull, ~0ull, ~0ull, ~0ull};
-    for (int32_t p = 0; p < P && n_cross > 0; ++p) {
-      const ut::u32x4 r = ut::draw(seed, g, (uint32_t)p, round_, ut::OP_DE);
-      uint64_t key = ((uint64_t)r.z << 32) | (uint32_t)p;
-      for (int s = 0; s < 4; ++s)
-        if (s < n_cross && key < fk[s]) {
-          const uint64_t x = fk[s];
-          fk[s] = key;
-          key = x;
-        }
-    }
+    int32_t fset[4];
+    ut::de_forced_set(ut::draw(seed, g, ut::STREAM_CAND | 2u, round_, ut::OP_DE), P, n_cross, fset);
+    ut::u32x4 r{0, 0, 0, 0};
     for (int32_t p = 0; p < P; ++p) {
-      const ut::u32x4 r = ut::draw(seed, g, (uint32_t)p, round_, ut::OP_DE);
-      bool forced = false;
-      for (int s = 0; s < 4; ++s) forced |= (s < n_cross) && ((uint32_t)fk[s] == (uint32_t)p) && (fk[s] != ~0ull);
+      if ((p & 3) == 0) r = ut::draw(seed, g, ut::STREAM_CAND | (ut::DE_CR_STREAM + (uint32_t)(p >> 2)), round_, ut::OP_DE);
+      const uint32_t w = (p & 3) == 0 ? r.x : (p & 3) == 1 ? r.y : (p & 3) == 2 ? r.z : r.w;
+      const bool forced = p == fset[0] || p == fset[1] || p == fset[2] || p == fset[3];
       const double* col = pop + (int64_t)p * npop;
       double v = col[t];
-      if (forced || ut::u01_from(r.x, r.y) < cr) {
+      if (forced || ut::de_cr_pass(w, cr)) {
         const double span = hi[p] - lo[p];
         if (lo[p] < hi[p]) {
           const double va = (col[d1] - lo[p]) / span, vb = (col[d2] - lo[p]) / span, vc = (col[d3] - lo[p]) / span;

@@ -11,8 +11,9 @@ random draws are replaced by Philox draws keyed by (seed, g, stream, round):
                      npop - 1 other members is a copy of the best config
   use_f   = random()/2.0 + 0.5                          (:120)
   forced  = first n_cross names of a shuffled name list (:122-125)
-            == the n_cross params with the smallest per-param keys
-  cross   = forced or random() < cr                     (:125)
+            == a uniform n_cross-subset, drawn by skip-rank (forced_mask)
+  cross   = forced or random() < cr                     (:125; cr_tests:
+            32-bit uniforms, four params per Philox block)
   primitive: op4_set_linear(x1, x2, x3, 1.0, F, -F)     (manipulator.py:523-542)
   complex:   copy x1; randomize iff x2 != x3            (manipulator.py:866-914)
              (PERM: randomize = shuffle of the x1 copy, oracle/perm.py)
@@ -54,15 +55,45 @@ def use_f(g, seed, round_):
     return ph.u01(x, y) / 2.0 + 0.5
 
 
+DE_CR_STREAM = 0x100
+
+
 def forced_mask(g, P, n_cross, seed, round_):
-    """bool [P][m]: param p is among the n_cross smallest (key, p)"""
+    """bool [P][m]: the forced set, a uniform n_cross-subset of the params
+    (the first n_cross names of the shuffled list, :122-125; n_cross <= 4),
+    drawn by skip-rank from the words of block (STREAM_CAND | 2): element k is
+    the (umulhi32(word_k, P - k))-th param not yet chosen (ut_core.h de_forced_set)"""
     g = np.asarray(g, dtype=np.uint64)
-    if n_cross <= 0:
-        return np.zeros((P, g.size), dtype=bool)
-    keys = np.stack([(ph.draw(seed, g, p, round_, ph.OP_DE)[2].astype(np.uint64) << np.uint64(32)) | np.uint64(p)
-                     for p in range(P)])
-    kth = np.sort(keys, axis=0)[min(n_cross, P) - 1]
-    return keys <= kth
+    out = np.zeros((P, g.size), dtype=bool)
+    nc = min(n_cross, P)
+    if nc <= 0:
+        return out
+    assert nc <= 4, "n_cross <= 4"
+    words = ph.draw(seed, g, ph.STREAM_CAND | 2, round_, ph.OP_DE)
+    chosen = []
+    cols = np.arange(g.size)
+    for k in range(nc):
+        v = ph.umulhi32(words[k], P - k).astype(np.int64)
+        if chosen:
+            for c in np.sort(np.stack(chosen), axis=0):   # skip the chosen ones, ascending
+                v = v + (v >= c)
+        chosen.append(v)
+        out[v, cols] = True
+    return out
+
+
+def cr_tests(g, P, cr, seed, round_):
+    """bool [P][m]: `random() < cr` (:125) of param p = word p % 4 of block
+    (STREAM_CAND | (DE_CR_STREAM + p // 4)), a 32-bit uniform"""
+    g = np.asarray(g, dtype=np.uint64)
+    out = np.empty((P, g.size), dtype=bool)
+    for b in range((P + 3) // 4):
+        ws = ph.draw(seed, g, ph.STREAM_CAND | (DE_CR_STREAM + b), round_, ph.OP_DE)
+        for q in range(4):
+            p = 4 * b + q
+            if p < P:
+                out[p] = ws[q].astype(np.float64) * 2.0 ** -32 < cr
+    return out
 
 
 def propose_de_vec(space, pop, seed, round_, cand_base, m, cr, n_cross=1, best=None, information_sharing=1):
@@ -80,10 +111,10 @@ def propose_de_vec(space, pop, seed, round_, cand_base, m, cr, n_cross=1, best=N
         d1, d2, d3 = (np.where(d < 0, npop, d) for d in (d1, d2, d3))
     F = use_f(g, seed, round_)
     forced = forced_mask(g, P, n_cross, seed, round_)
+    crt = cr_tests(g, P, cr, seed, round_)
     out = np.empty((ncols, m), dtype=np.float64)
     for p, prm in enumerate(space):
-        x, y, _, _ = ph.draw(seed, g, p, round_, ph.OP_DE)
-        cross = forced[p] | (ph.u01(x, y) < cr)
+        cross = forced[p] | crt[p]
         c0 = starts[p]
         if prm.kind == PERM:
             S = width(prm)
@@ -130,9 +161,9 @@ def propose_de_scalar(space, pop_cfgs, seed, round_, g, cr, n_cross=1, best_cfg=
     x1, x2, x3 = (best_cfg if d < 0 else pop_cfgs[d] for d in (d1, d2, d3))
     F = float(use_f(np.array([g]), seed, round_)[0])
     forced = forced_mask(np.array([g]), len(space), n_cross, seed, round_)[:, 0]
+    crt = cr_tests(np.array([g]), len(space), cr, seed, round_)[:, 0]
     for p, prm in enumerate(space):
-        x, y, _, _ = ph.draw(seed, np.array([g]), p, round_, ph.OP_DE)
-        if forced[p] or float(ph.u01(x, y)[0]) < cr:
+        if forced[p] or crt[p]:
             if prm.is_primitive():
                 cfg[p] = op4_set_linear_primitive(prm, x1[p], x2[p], x3[p], 1.0, F, -F, cfg[p])
             elif prm.kind == PERM:

@@ -1,6 +1,6 @@
 cd "$GRAFT_REPO_ROOT"
 timeout -k 10 200 python scripts/microbench.py hash > gpurun_out/mh_new.json 2>&1 || exit 1
-UTHOT_LIB=$PWD/gpurun_tmp/libuthot_hold.so timeout -k 10 200 python scripts/microbench.py hash > gpurun_out/mh_old.json 2>&1 || exit 1
+UTHOT_LIB=$PWD/gpurun_tmp/libuthot_h3w.so timeout -k 10 200 python scripts/microbench.py hash > gpurun_out/mh_old.json 2>&1 || exit 1
 python - <<'PY'
 import json
 for f in ("mh_new", "mh_old"):

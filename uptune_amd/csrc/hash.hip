@@ -403,7 +403,10 @@ static int launch_hash_impl(ut_ctx* c, const double* values, int64_t ld, int64_t
     pd = c->perm_dig.p;
   }
   const int64_t nb = (int64_t)grid1(m, HASH_NT);
-  auto kern = ref.cache ? k_hash<true, 4> : k_hash<false, 1>;
+#ifndef UT_HASH_REF_WAVES
+#define UT_HASH_REF_WAVES 4
+#endif
+  auto kern = ref.cache ? k_hash<true, UT_HASH_REF_WAVES> : k_hash<false, 1>;
   hipLaunchKernelGGL(kern, dim3((unsigned)nb), dim3(HASH_NT), 0, c->stream, s.d_params, s.d_order,
                      s.d_order_col, reinterpret_cast<const uint2*>(s.d_words), s.d_block_last,
                      (int32_t)s.outer_blocks, s.P, reinterpret_cast<const uint4*>(s.d_lut), values, ld, m,

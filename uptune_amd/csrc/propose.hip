@@ -80,16 +80,13 @@ struct DeDiffOut {
 };
 
 // One DE trial per candidate.  Candidate g (global) targets member g % npop.
-// Forced crossover set = the n_cross parameters with the smallest per-param
-// random keys (= the first n_cross names of a uniform shuffle,
-// differentialevolution.py:122-125).
-//
-// Each param's draw (seed, g, p, round, OP_DE) serves twice: its z word is the
-// forced-set key, its x, y words the `random() < cr` test.  The first pass
-// over the params keeps the test's outcome as one bit per param in LDS
-// ([ceil(P/32)][256] words, each lane its own column), so the second pass
-// draws nothing for the crossover decision: 1 + 1 Philox blocks per param
-// became 1 (k_de is Philox-issue-bound: ~220 VALU cycles per block).
+// Forced crossover set = a uniform n_cross-subset of the params (the first
+// n_cross names of a uniform shuffle, differentialevolution.py:122-125), drawn
+// by skip-rank from one block; the `random() < cr` tests are 32-bit uniforms,
+// four params per Philox block (ut_core.h de_forced_set / DE_CR_STREAM).  The
+// first pass keeps the tests' outcomes as one bit per param in LDS
+// ([ceil(P/32)][blockDim] words, each lane its own column), so the second pass
+// draws nothing for the crossover decision.
 // AOS (the default): block = one wave; the donors' values come from the
 // member-major donor copy (pop_aos, [npop + 1][lda], row npop = the best
 // config; primitive params as unit values, so no unit_of is left here), staged
@@ -209,23 +206,22 @@ __global__ __launch_bounds__(AOS ? 64 : 256) void k_de(const DevParam* __restric
                ((((cc >> 1) ^ ((lane >> DE_SW) & (DE_CH - 1))) << 1) | (cc & 1))];
   };
 
-  // pass 1: forced set (up to 4 smallest (key, p)) and the cr-test bits
-  uint64_t fk[4] = {~0ull, ~0ull, ~0ull, ~0ull};
+  // pass 1: the forced set and the cr-test bits (four params per Philox block)
+  int32_t fset[4];
+  de_forced_set(draw(seed, g, STREAM_CAND | 2u, round_, OP_DE), P, n_cross, fset);
   {
     uint32_t acc = 0;
-    for (int32_t p = 0; p < P; ++p) {
-      const u32x4 r = draw(seed, g, (uint32_t)p, round_, OP_DE);
-      if (u01_from(r.x, r.y) < cr) acc |= 1u << (p & 31);
-      if ((p & 31) == 31 || p == P - 1) {
-        xb[(p >> 5) * xs] = acc;
-        acc = 0;
-      }
-      uint64_t key = ((uint64_t)r.z << 32) | (uint32_t)p;
+    for (int32_t p0 = 0; p0 < P; p0 += 4) {
+      const u32x4 r = draw(seed, g, STREAM_CAND | (DE_CR_STREAM + (uint32_t)(p0 >> 2)), round_, OP_DE);
+      const uint32_t ws[4] = {r.x, r.y, r.z, r.w};
 #pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        if (s < n_cross && key < fk[s]) {
-          uint64_t x = fk[s]; fk[s] = key; key = x;
-        }
+      for (int q = 0; q < 4; ++q) {
+        const int32_t p = p0 + q;
+        if (p < P && de_cr_pass(ws[q], cr)) acc |= 1u << (p & 31);
+      }
+      if ((p0 & 31) == 28 || p0 + 4 >= P) {   // a 32-param word is complete
+        xb[(p0 >> 5) * xs] = acc;
+        acc = 0;
       }
     }
   }
@@ -255,9 +251,7 @@ __global__ __launch_bounds__(AOS ? 64 : 256) void k_de(const DevParam* __restric
       vt_pf = vt_next;
       if (p + 1 < P) vt_next = load_vt(p + 1);
     }
-    bool forced = false;
-#pragma unroll
-    for (int s = 0; s < 4; ++s) forced |= (s < n_cross) && ((uint32_t)fk[s] == (uint32_t)p) && (fk[s] != ~0ull);
+    const bool forced = p == fset[0] || p == fset[1] || p == fset[2] || p == fset[3];
     const double* col = pop + (int64_t)pr.col * ldp;
     // `i < n_cross or random() < cr` (short-circuit: the draw is only
     // consulted for non-forced params, which is what selecting on it does)

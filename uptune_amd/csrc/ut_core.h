@@ -107,6 +107,34 @@ UT_HD u32x4 draw(uint64_t seed, uint64_t cand, uint32_t stream, uint32_t round_,
   return philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
 }
 
+// DE draw layout (oracle/de.py): the cr tests `random() < cr` of params
+// 4b .. 4b + 3 are the four words of block (STREAM_CAND | (DE_CR_STREAM + b)),
+// each a 32-bit uniform; the forced set (the first n_cross names of the
+// shuffled name list, differentialevolution.py:122-125: a uniform n_cross-subset,
+// n_cross <= 4) is drawn from block (STREAM_CAND | 2) by skip-rank, one word per
+// element.  17 blocks per candidate at P = 64 where one block per param (its
+// x, y words the cr test, its z word a sort key) took 64.
+constexpr uint32_t DE_CR_STREAM = 0x100u;
+UT_HD bool de_cr_pass(uint32_t w, double cr) { return (double)w * 2.3283064365386963e-10 < cr; }
+UT_HD void de_forced_set(u32x4 r, int32_t P, int32_t n_cross, int32_t f[4]) {
+  const uint32_t ws[4] = {r.x, r.y, r.z, r.w};
+  int32_t srt[4];   // the chosen params, ascending
+  const int32_t nc = n_cross < P ? n_cross : P;
+  for (int k = 0; k < 4; ++k) f[k] = -1;
+  for (int k = 0; k < 4; ++k) {
+    if (k >= nc) break;
+    int32_t v = (int32_t)umulhi32(ws[k], (uint32_t)(P - k));   // rank among the P - k unchosen params
+    for (int a = 0; a < k; ++a) v += (v >= srt[a]) ? 1 : 0;
+    f[k] = v;
+    int a = k;
+    while (a > 0 && srt[a - 1] > v) {
+      srt[a] = srt[a - 1];
+      --a;
+    }
+    srt[a] = v;
+  }
+}
+
 // Permutation-operator draw sites (oracle/perm.py): a site (seed, cand,
 // stream, round, op) yields a stream of 32-bit words; block b of it is the
 // Philox block with op | 0x80 and key_hi ^ b.
