@@ -135,3 +135,31 @@ def test_allgather_selection_rows_and_results_broadcast():
         # every rank gets the selected candidates' value rows, in merged order
         assert rows == [[j * m + g for g in want] for j in range(3)]
         assert ysum == 2.0 and dsum == sum(range(16))
+
+
+def test_merge_topk_random_vs_python():
+    """the fixed-size merge equals the plain definition: drop empty slots, keep
+    the smallest index of each digest, order by (-score, index), pad with -1"""
+    from uptune_amd.dist import merge_topk
+    rng = np.random.default_rng(5)
+    for trial in range(50):
+        R, k = int(rng.integers(1, 9)), int(rng.integers(1, 12))
+        n = R * k
+        idx = rng.choice(10 * n, size=n, replace=False).astype(np.int64)
+        idx[rng.random(n) < 0.2] = -1
+        sc = rng.choice([0.1, 0.5, 0.9, float("-inf")], size=n)        # ties on purpose
+        dg = rng.integers(0, 4, size=(n, 8)).astype(np.int32)          # collisions on purpose
+        dg[:, 1:] = dg[:, :1]
+        best = {}
+        for j in range(n):
+            if idx[j] < 0:
+                continue
+            key = tuple(dg[j])
+            if key not in best or idx[j] < idx[best[key]]:
+                best[key] = j
+        rows = sorted(best.values(), key=lambda j: (-sc[j], idx[j]))[:k]
+        want_i = [int(idx[j]) for j in rows] + [-1] * (k - len(rows))
+        want_s = [float(sc[j]) for j in rows] + [float("-inf")] * (k - len(rows))
+        gi, gs = merge_topk(torch.from_numpy(sc), torch.from_numpy(idx), torch.from_numpy(dg), k)
+        assert gi.tolist() == want_i, trial
+        assert gs.tolist() == want_s, trial

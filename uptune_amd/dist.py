@@ -31,46 +31,60 @@ def merge_topk(scores: torch.Tensor, idx: torch.Tensor, digests: torch.Tensor, k
 
     scores [R*k] f64, idx [R*k] i64 (-1 = empty slot), digests [R*k][8] i32.
     Returns (idx [k], score [k]) sorted by (-score, idx), empty slots -1.
+    Cross-shard duplicates (equal digests) keep the smallest global index.
+
+    Fixed-size tensor ops only -- no boolean indexing, no .item(): the merge
+    never waits for the device, so the host keeps enqueueing the next round
+    while this one computes (the N > 1 bench loop stays asynchronous).
     """
+    n = idx.numel()
+    dev = idx.device
+    big = torch.iinfo(torch.int64).max
     valid = idx >= 0
-    s = scores[valid]
-    i = idx[valid]
-    d = digests[valid]
-    if i.numel():
-        # first (smallest global index) occurrence of each digest survives
-        _, inv = torch.unique(d, dim=0, return_inverse=True)
-        big = torch.iinfo(torch.int64).max
-        first = torch.full((int(inv.max().item()) + 1,), big, dtype=torch.int64, device=i.device)
-        first = first.scatter_reduce(0, inv, i, reduce="amin")
-        keep = i == first[inv]
-        s, i = s[keep], i[keep]
-        # sort by index, then stable by descending score -> (-score, idx) order
-        o = torch.argsort(i, stable=True)
-        s, i = s[o], i[o]
-        o = torch.argsort(-s, stable=True)
-        s, i = s[o], i[o]
-    out_i = torch.full((k,), -1, dtype=torch.int64, device=idx.device)
-    out_s = torch.full((k,), float("-inf"), dtype=scores.dtype, device=idx.device)
-    n = min(k, i.numel())
-    out_i[:n] = i[:n]
-    out_s[:n] = s[:n]
+    key = torch.where(valid, idx, torch.full_like(idx, big))
+    d64 = digests.to(torch.int32).contiguous().view(n, 8).view(torch.int64)      # [n][4]
+    # lexicographic (digest, index) order by stable sorts, least significant first
+    o = torch.argsort(key, stable=True)
+    for c in (3, 2, 1, 0):
+        o = o[torch.argsort(d64[o, c], stable=True)]
+    ds, vs = d64[o], valid[o]
+    dup = torch.zeros(n, dtype=torch.bool, device=dev)
+    if n > 1:   # a valid record equal to its predecessor: a later (larger-index) copy
+        dup[1:] = (ds[1:] == ds[:-1]).all(dim=1) & vs[1:] & vs[:-1]
+    keep = torch.empty_like(vs)
+    keep[o] = vs & ~dup
+    s = torch.where(keep, scores, torch.full_like(scores, float("-inf")))
+    i = torch.where(keep, idx, torch.full_like(idx, big))
+    # (-score, idx) order: stable by index, then stable by descending score
+    o = torch.argsort(i, stable=True)
+    o = o[torch.argsort(-s[o], stable=True)]
+    top = o[:k]
+    out_i = torch.where(keep[top], idx[top], torch.full_like(idx[top], -1))
+    out_s = torch.where(keep[top], scores[top], torch.full_like(scores[top], float("-inf")))
+    if out_i.numel() < k:
+        pad = k - out_i.numel()
+        out_i = torch.cat([out_i, torch.full((pad,), -1, dtype=idx.dtype, device=dev)])
+        out_s = torch.cat([out_s, torch.full((pad,), float("-inf"), dtype=scores.dtype, device=dev)])
     return out_i, out_s
 
 
 def allgather_topk(idx: torch.Tensor, score: torch.Tensor, digest: torch.Tensor, k: int,
                    group: Optional[dist.ProcessGroup] = None) -> Tuple[torch.Tensor, torch.Tensor]:
-    """all_gather the local (idx, score, digest) top-k of every rank and merge."""
+    """all_gather the local (idx, score, digest) top-k of every rank and merge:
+    one all_gather of packed [k][6] int64 records (index, score bits, digest
+    as 4 words), then merge_topk -- no host synchronisation."""
     world = dist.get_world_size(group)
     dev = idx.device
     cd = _comm_device(group, dev)
-    idx, score, digest = idx.to(cd), score.to(cd), digest.to(cd)
-    gi = [torch.empty_like(idx) for _ in range(world)]
-    gs = [torch.empty_like(score) for _ in range(world)]
-    gd = [torch.empty_like(digest) for _ in range(world)]
-    dist.all_gather(gi, idx.contiguous(), group=group)
-    dist.all_gather(gs, score.contiguous(), group=group)
-    dist.all_gather(gd, digest.contiguous(), group=group)
-    mi, ms = merge_topk(torch.cat(gs), torch.cat(gi), torch.cat(gd), k)
+    kk = idx.numel()
+    rec = torch.cat([idx.to(torch.int64).reshape(kk, 1),
+                     score.to(torch.float64).contiguous().view(torch.int64).reshape(kk, 1),
+                     digest.to(torch.int32).contiguous().reshape(kk, 8).view(torch.int64)], dim=1).to(cd)
+    parts = [torch.empty_like(rec) for _ in range(world)]
+    dist.all_gather(parts, rec, group=group)
+    g = torch.cat(parts)
+    gd = g[:, 2:].contiguous().view(torch.int32)
+    mi, ms = merge_topk(g[:, 1].contiguous().view(torch.float64), g[:, 0].contiguous(), gd, k)
     return mi.to(dev), ms.to(dev)
 
 
