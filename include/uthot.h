@@ -220,6 +220,14 @@ int ut_hash(ut_ctx* ctx, const double* values, int64_t ld, int64_t m, uint32_t* 
  * values are formatted and hashed.  Correct for any values (a value that does
  * not match its "target" is simply recomputed); fast when most match. */
 int ut_hash_de(ut_ctx* ctx, const double* values, int64_t ld, int64_t m, int64_t cand_base, uint32_t* out_digest);
+/* The same digests for GA / GGA children of one parent config (ut_propose_ga:
+ * parent1, a device row of ncols values; mutation and crossover change a few
+ * params, the rest are the parent's): inner digests of values bitwise equal
+ * to the parent's come from the parent's own digests (computed once per call);
+ * only the changed values are formatted and hashed.  Correct for any values.
+ * Replaces the per-child hash_config of evolutionarytechniques.py:38-49. */
+int ut_hash_parent(ut_ctx* ctx, const double* values, int64_t ld, int64_t m, const double* parent,
+                   uint32_t* out_digest);
 int ut_history_reset(ut_ctx* ctx, int64_t capacity);
 int ut_history_add(ut_ctx* ctx, const uint32_t* digests, int64_t n);   /* device [n][8] */
 int ut_history_add_host(ut_ctx* ctx, const uint32_t* digests_host, int64_t n);

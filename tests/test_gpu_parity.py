@@ -961,3 +961,30 @@ def test_score_round_de_pruned_equals_dense_round():
         assert a[0].cpu().numpy().tolist() == b[0].cpu().numpy().tolist()
         assert hexes(a[2]) == hexes(b[2])
         np.testing.assert_array_equal(a[3].cpu().numpy(), b[3].cpu().numpy())
+
+
+@pytest.mark.parametrize("which", ["mixed", "r64", "hpl", "perm"])
+def test_hash_parent_reuses_parent_digests(which):
+    """ut_hash_parent (inner digests of values equal to the parent's taken from
+    the parent's own) == ut_hash == the oracle, for GA / GGA children of that
+    parent, for two-parent crossovers, and for values unrelated to the parent"""
+    space = {"mixed": mixed_space, "r64": r64_space, "hpl": hpl_space, "perm": perm_space}[which]()
+    e = engine(space, seed=41)
+    e.population_init(64, round_=1)
+    pop = e.population_get().cpu().numpy()
+    p1, p2 = pop[:, 3].copy(), pop[:, 7].copy()
+    for kw in ({"mutation_rate": 0.1}, {"mutation_rate": 0.05, "normal": True, "op": 5},
+               {"mutation_rate": 0.1, "crossover_rate": 0.5, "crossover_strength": 0.2}):
+        kids, _ = e.propose_ga(4000, parent1=p1, parent2=p2 if "crossover_rate" in kw else None, round_=2,
+                               cand_base=17, **kw)
+        want = hexes(e.hash(kids))
+        assert hexes(e.hash_parent(kids, p1)) == want
+        vals = kids.cpu().numpy()
+        sub = slice(0, 300)
+        ref = oracle_hashes(space, vals[:, sub]) if which != "perm" else _row_hashes(space, vals[:, sub])
+        assert want[sub] == ref
+    other = torch.from_numpy(ode.population_init(space, 500, seed=98)).cuda()
+    assert hexes(e.hash_parent(other, p1)) == hexes(e.hash(other))
+    # the parent itself and an empty batch
+    assert hexes(e.hash_parent(torch.from_numpy(p1.reshape(-1, 1).copy()).cuda(), p1)) == \
+        hexes(e.hash(torch.from_numpy(p1.reshape(-1, 1).copy()).cuda()))

@@ -104,6 +104,7 @@ SIGNATURES = {
                                            C.POINTER(RoundOut), C.POINTER(PruneStats)]),
     "ut_gp_topk_pruned": (C.c_int, [P, P, I64, I64, C.POINTER(Acq), P, I64, I32, I32, P, P, C.POINTER(PruneStats)]),
     "ut_hash_de": (C.c_int, [P, P, I64, I64, I64, P]),
+    "ut_hash_parent": (C.c_int, [P, P, I64, I64, P, P]),
     "ut_propose_de": (C.c_int, [P, C.POINTER(DeParams), U32, I64, I64, P, I64]),
     "ut_pso_reset": (C.c_int, [P]),
     "ut_propose_pso": (C.c_int, [P, C.POINTER(PsoParams), P, U32, I64, I64, P, P, I64]),

@@ -208,7 +208,7 @@ int ut_ctx_destroy(ut_ctx* c) {
     fr(c->pop_slots[s].pop); fr(c->pop_slots[s].pso_vel); fr(c->pop_slots[s].pso_best); fr(c->pop_slots[s].pop_dig);
     fr(c->pop_slots[s].pop_aos);
   }
-  fr(c->r_mask.p); fr(c->r_fresh.p); fr(c->r_pairs.p); fr(c->r_npairs.p); fr(c->de_xbits.p);
+  fr(c->r_mask.p); fr(c->r_fresh.p); fr(c->r_pairs.p); fr(c->r_npairs.p); fr(c->de_xbits.p); fr(c->par_dig.p);
   fr(c->pr_mu.p); fr(c->pr_ub.p); fr(c->pr_score.p); fr(c->pr_mpart.p); fr(c->pr_kst.p); fr(c->pr_vpart.p);
   fr(c->pr_idx.p); fr(c->pr_count.p); fr(c->pr_ucand.p); fr(c->pr_cnorm.p);
   fr(c->pr_k2.p); fr(c->pr_f2.p); fr(c->pr_exact.p); fr(c->app_ws.p); fr(c->var_vbuf.p);
@@ -558,6 +558,13 @@ int ut_hash_de(ut_ctx* c, const double* values, int64_t ld, int64_t m, int64_t c
   UT_CHECK(c, c->pop != nullptr, UT_EINVAL, "hash_de: population not initialised");
   UT_CHECK(c, m >= 0 && cand_base >= 0 && ((values && out) || m == 0) && ld >= m, UT_EINVAL, "hash_de: bad arguments");
   return launch_hash_de(c, values, ld, m, cand_base, out);
+}
+
+int ut_hash_parent(ut_ctx* c, const double* values, int64_t ld, int64_t m, const double* parent, uint32_t* out) {
+  if (!c) return UT_EINVAL;
+  UT_CHECK(c, c->has_space, UT_ENOSPACE, "space not defined");
+  UT_CHECK(c, m >= 0 && parent && ((values && out) || m == 0) && ld >= m, UT_EINVAL, "hash_parent: bad arguments");
+  return launch_hash_parent(c, values, ld, m, parent, out);
 }
 
 int ut_history_reset(ut_ctx* c, int64_t capacity) {

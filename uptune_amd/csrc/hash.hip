@@ -480,4 +480,31 @@ int launch_hash_de(ut_ctx* c, const double* values, int64_t ld, int64_t m, int64
                                    reinterpret_cast<const uint4*>(c->pop_dig), c->npop, cand_base});
 }
 
+int launch_hash_parent(ut_ctx* c, const double* values, int64_t ld, int64_t m, const double* parent, uint32_t* out) {
+  const Space& s = c->space;
+  if (s.n_comp == 0 || m <= 0) return launch_hash(c, values, ld, m, out);
+  int rc;
+  if ((rc = ensure(c, c->par_dig, (size_t)s.n_comp * 16))) return rc;
+  if ((rc = ensure_de_diff(c, ld))) return rc;
+  // the parent's hex inner digests: a population of one member (column p at parent[col])
+  hipLaunchKernelGGL(k_pop_digests, dim3(1, (unsigned)s.n_comp), dim3(HASH_NT), 0, c->stream, s.d_params, s.d_comp,
+                     s.n_comp, parent, (int64_t)1, (const int64_t*)nullptr, (int64_t)0,
+                     reinterpret_cast<uint4*>(c->par_dig.p));
+  UT_LAUNCH_CHECK(c);
+  // which computed-digest values differ from the parent's: every child "targets" member 0
+  unsigned long long* np = reinterpret_cast<unsigned long long*>(c->r_npairs.p);
+  UT_HIP(c, hipMemsetAsync(c->r_npairs.p, 0, sizeof(int64_t), c->stream));
+  hipLaunchKernelGGL(k_de_diff, dim3(grid1(m, DIFF_NT)), dim3(DIFF_NT), 0, c->stream, s.d_params, s.d_comp, s.n_comp,
+                     values, ld, m, parent, (int64_t)1, (int64_t)0, c->r_mask.p, c->r_pairs.p, np);
+  UT_LAUNCH_CHECK(c);
+  const int64_t want = ((int64_t)s.n_comp * m + HASH_NT - 1) / HASH_NT;
+  const unsigned grid = (unsigned)std::min<int64_t>(std::max<int64_t>(want, 1), (int64_t)c->n_cu * 8);
+  hipLaunchKernelGGL(k_inner_pairs, dim3(grid), dim3(HASH_NT), 0, c->stream, s.d_params, s.d_comp, values, ld,
+                     c->r_pairs.p, np, reinterpret_cast<uint4*>(c->r_fresh.p));
+  UT_LAUNCH_CHECK(c);
+  return launch_hash_impl(c, values, ld, m, out,
+                          InnerRef{c->r_mask.p, reinterpret_cast<const uint4*>(c->r_fresh.p),
+                                   reinterpret_cast<const uint4*>(c->par_dig.p), 1, 0});
+}
+
 }  // namespace ut

@@ -254,6 +254,7 @@ struct ut_ctx {
   ut::DevBuf<uint64_t> r_pairs;     // compacted (candidate << 20 | cslot) of the changed values
   ut::DevBuf<int64_t> r_npairs;     // [1] their count
   ut::DevBuf<uint32_t> de_xbits;    // k_de's cr-test bits when they outgrow LDS (> 2048 params)
+  ut::DevBuf<uint32_t> par_dig;     // [n_comp][16]: hex inner digests of ut_hash_parent's parent row
   // EI-bound pruned scoring (gp.hip ut_gp_topk_pruned)
   ut::DevBuf<double> pr_mu, pr_ub, pr_score;   // [ld] exact mean, score bound, exact scores (-inf if pruned)
   ut::DevBuf<double> pr_mpart;                 // [RT][ldk] unused mean partials of the bound / survivor GEMMs
@@ -362,6 +363,9 @@ int launch_hash(ut_ctx* c, const double* values, int64_t ld, int64_t m, uint32_t
 // have_diff: the mask / pairs / count were written by k_de (launch_de diff = true)
 int launch_hash_de(ut_ctx* c, const double* values, int64_t ld, int64_t m, int64_t cand_base, uint32_t* out,
                    bool have_diff = false);
+// hash_config of children of one parent row (ut_hash_parent): inner digests of
+// the values equal to the parent's are the parent's own
+int launch_hash_parent(ut_ctx* c, const double* values, int64_t ld, int64_t m, const double* parent, uint32_t* out);
 // the DE-diff buffers for m candidates (ld): r_mask, r_fresh, r_pairs, r_npairs
 int ensure_de_diff(ut_ctx* c, int64_t ld);
 // population cache maintenance: full rebuild, or the rows idx[0..n) after a replace

@@ -229,6 +229,16 @@ class BatchEngine:
                 "ut_hash_de")
         return out
 
+    def hash_parent(self, values: torch.Tensor, parent, m: Optional[int] = None) -> torch.Tensor:
+        """ut_hash_parent: hash_config of GA / GGA children of `parent` (a value
+        row), reusing the parent's inner digests for the unchanged params"""
+        m = values.shape[1] if m is None else m
+        p = self._row(parent)
+        out = self._empty(m, 8, dtype=torch.int32)
+        L.check(self.ctx, self.lib.ut_hash_parent(self.ctx, _ptr(values), values.stride(0), m, _ptr(p), _ptr(out)),
+                "ut_hash_parent")
+        return out
+
     def hash_configs(self, cfgs: Sequence[Dict[Any, Any]]) -> List[str]:
         vals = torch.from_numpy(self.spec.encode_configs(cfgs)).to(self.device)
         d = self.hash(vals)

@@ -614,7 +614,16 @@ class GpuGA(GpuBatchTechnique):
 
     def propose(self, m):
         # GreedySelectionMixin.select: the global best config (random() before any result)
-        return self.engine.propose_ga(m, self.best_row(), None, round_=self.round, cand_base=self.round_base(), **self.ga)
+        self._parent = self.best_row()
+        return self.engine.propose_ga(m, self._parent, None, round_=self.round, cand_base=self.round_base(), **self.ga)
+
+    def hash_proposals(self, vals, base):
+        # children keep most of the parent's values: reuse its inner digests
+        parent = getattr(self, "_parent", None)
+        hp = getattr(self.engine, "hash_parent", None)
+        if parent is None or hp is None:
+            return self.engine.hash(vals)
+        return hp(vals, parent)
 
 
 class GpuGGA(GpuGA):
