@@ -988,3 +988,47 @@ def test_hash_parent_reuses_parent_digests(which):
     # the parent itself and an empty batch
     assert hexes(e.hash_parent(torch.from_numpy(p1.reshape(-1, 1).copy()).cuda(), p1)) == \
         hexes(e.hash(torch.from_numpy(p1.reshape(-1, 1).copy()).cuda()))
+
+
+@pytest.mark.parametrize("which", ["mixed", "hpl", "perm"])
+def test_de_donor_copy_follows_population_changes(which):
+    """k_de gathers its donors from a member-major unit-value copy of the
+    population: after every way the population changes (replace: rows patched;
+    set, PSO commit, re-init: rebuilt; slot switch: the slot's own copy; the
+    best config row rewritten per call) the trials still equal the oracle's on
+    the population as it is then"""
+    space = {"mixed": mixed_space, "hpl": hpl_space, "perm": perm_space}[which]()
+    e = engine(space, seed=51)
+    e.population_init(500, round_=1)
+    best = None
+
+    def check(rnd, share=0):
+        pop = e.population_get().cpu().numpy()
+        got = e.propose_de(3000, round_=rnd, cand_base=7, cr=0.3, best=best, information_sharing=share).cpu().numpy()
+        want = ode.propose_de_vec(space, pop, 51, rnd, 7, 3000, 0.3, 1, best=best if share else None,
+                                  information_sharing=share)
+        np.testing.assert_array_equal(got, want)
+
+    check(1)
+    other = ode.population_init(space, 500, seed=77)
+    e.population_replace(dev(other[:, :40]), torch.arange(100, 140, device="cuda"))   # rows patched
+    check(2)
+    best = other[:, 3].copy()
+    check(3, share=2)                                  # the best row of the copy
+    best = other[:, 9].copy()
+    check(4, share=1)                                  # ... rewritten per call
+    best = None
+    e.population_set(dev(other))                       # rebuilt
+    check(5)
+    if which != "perm":
+        e.pso_reset()
+        x, v = e.propose_pso(other[:, 0].copy(), 500, round_=1)
+        e.pso_commit(x, v)                             # positions moved: rebuilt
+        check(6)
+    e.population_select(1)                             # another slot, its own population and copy
+    e.population_init(300, round_=4)
+    check(7)
+    e.population_select(0)
+    check(8)
+    e.population_init(500, round_=9)                   # re-init: rebuilt
+    check(9)
