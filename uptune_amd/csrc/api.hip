@@ -191,6 +191,7 @@ int ut_ctx_create(int device, uint64_t seed, ut_ctx** out) {
   if (const char* e = getenv("UT_VAR_SPLIT")) c->var_split = atoi(e) != 0;
   if (const char* e = getenv("UT_FIT_APPEND")) c->fit_append = atoi(e) != 0;
   if (const char* e = getenv("UT_DE_AOS")) c->de_aos = atoi(e) != 0;
+  if (const char* e = getenv("UT_HASH_AFTER_FIT")) c->hash_after_fit = atoi(e);
   *out = c;
   return 0;
 }
@@ -758,7 +759,10 @@ static int score_round_de_impl(ut_ctx* c, const ut_de_params* de, const ut_acq* 
   {
     StreamScope on_side(c, c->side);
     mark(c, "");
-    if ((rc = launch_hash_de(c, c->r_values.p, ld, m, cand_base, c->r_digest.p, true))) return rc;
+    c->round_hash_hold = (prune_rows == 0 && c->gp_fit_prec == 64) ? c->hash_after_fit : 0;
+    rc = launch_hash_de(c, c->r_values.p, ld, m, cand_base, c->r_digest.p, true);
+    c->round_hash_hold = 0;
+    if (rc) return rc;
     mark(c, "hash");
     if ((rc = launch_dedup(c, c->r_digest.p, m, c->r_dup.p))) return rc;
     mark(c, "dedup");

@@ -472,9 +472,12 @@ int launch_hash_de(ut_ctx* c, const double* values, int64_t ld, int64_t m, int64
   }
   const int64_t want = ((int64_t)s.n_comp * m + HASH_NT - 1) / HASH_NT;
   const unsigned grid = (unsigned)std::min<int64_t>(std::max<int64_t>(want, 1), (int64_t)c->n_cu * 8);
+  const bool hold = c->round_hash_hold > 0 && c->fit_pending && hipEventQuery(c->ev_fit) == hipErrorNotReady;
+  if (hold && c->round_hash_hold == 2) UT_HIP(c, hipStreamWaitEvent(c->stream, c->ev_fit, 0));
   hipLaunchKernelGGL(k_inner_pairs, dim3(grid), dim3(HASH_NT), 0, c->stream, s.d_params, s.d_comp, values, ld,
                      c->r_pairs.p, np, reinterpret_cast<uint4*>(c->r_fresh.p));
   UT_LAUNCH_CHECK(c);
+  if (hold && c->round_hash_hold == 1) UT_HIP(c, hipStreamWaitEvent(c->stream, c->ev_fit, 0));
   return launch_hash_impl(c, values, ld, m, out,
                           InnerRef{c->r_mask.p, reinterpret_cast<const uint4*>(c->r_fresh.p),
                                    reinterpret_cast<const uint4*>(c->pop_dig), c->npop, cand_base});

@@ -173,6 +173,15 @@ struct ut_ctx {
   int64_t pop_aos_cap = 0;
   bool pop_aos_valid = false;
   int32_t de_aos = 1;   // 0: k_de gathers donor values from the column-major population (UT_DE_AOS=0)
+  // round schedule of dense fp64 DE rounds (the only ones whose K* does not
+  // wait for the whole GP fit): 2 = the side stream's inner digests and outer
+  // hash wait for an in-flight fit, 1 = only the outer hash, 0 = neither
+  // (UT_HASH_AFTER_FIT).  Beside the hash, the fit's chain of ~70 small kernels
+  // finds no free CU slots and stretches from ~1.5 to ~9 ms, and the variance
+  // GEMM waits for it; held, the fit runs beside K* alone.  Measured at C2:
+  // 26.10-26.12 ms per round (2), 26.32-26.34 (1), 26.54-26.80 (0).
+  int32_t hash_after_fit = 2;
+  int32_t round_hash_hold = 0;   // the value in force for the round being enqueued
 
   struct PopSlot {
     double* pop = nullptr;
