@@ -293,6 +293,12 @@ class SharedModel:
         self._y: List[float] = []
         self._fit_key = None
         self.fits = 0
+        # list drivers (append-only results table): the usable rows found so
+        # far and how far the table has been scanned
+        self._scan_n = 0
+        self._scan_last = None
+        self._scan_rows: List[Any] = []
+        self._scan_ids: List[Any] = []
 
     def __deepcopy__(self, memo):
         # techniques (and so their shared model) are deep-copied per driver
@@ -340,9 +346,25 @@ class SharedModel:
         """(re)fit the GP iff the driver's results changed since the last fit;
         the new training rows are encoded on the device (ut_encode_features)
         and the fit is enqueued without a host wait (ut_gp_fit_async)"""
-        rows = [r for r in driver.results_query()
-                if getattr(r, "state", "OK") == "OK" and r.time is not None and math.isfinite(r.time)]
-        ids = [getattr(r, "id", i) for i, r in enumerate(rows)]
+        def usable(r):
+            return getattr(r, "state", "OK") == "OK" and r.time is not None and math.isfinite(r.time)
+
+        res = driver.results_query()
+        if isinstance(res, list):
+            # an in-memory table only grows: scan the rows added since the last
+            # call (a table that shrank or changed under us is rescanned)
+            if len(res) < self._scan_n or (self._scan_n and res[self._scan_n - 1] is not self._scan_last):
+                self._scan_n, self._scan_rows, self._scan_ids = 0, [], []
+            for r in res[self._scan_n:]:
+                if usable(r):
+                    self._scan_ids.append(getattr(r, "id", len(self._scan_rows)))
+                    self._scan_rows.append(r)
+            self._scan_n = len(res)
+            self._scan_last = res[-1] if res else None
+            rows, ids = self._scan_rows, self._scan_ids
+        else:   # a SQL query (reference driver): every row, filtered
+            rows = [r for r in res if usable(r)]
+            ids = [getattr(r, "id", i) for i, r in enumerate(rows)]
         if len(rows) < self.min_train:
             return False
         key = (len(rows), ids[-1])
@@ -355,7 +377,7 @@ class SharedModel:
         if new:
             self._X = np.vstack([self._X, self.engine.features_host([r.configuration.data for r in new])])
             self._y += [float(r.time) for r in new]
-            self._res_ids = ids
+            self._res_ids = list(ids)   # a copy: the scan list keeps growing
         self.engine.gp_fit(self._X, np.asarray(self._y), lengthscale=self.lengthscale, wait=False, **self.hyper)
         self._fit_key = key
         self.fits += 1
