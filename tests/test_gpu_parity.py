@@ -1032,3 +1032,31 @@ def test_de_donor_copy_follows_population_changes(which):
     check(8)
     e.population_init(500, round_=9)                   # re-init: rebuilt
     check(9)
+
+
+def _wide_space(P):
+    kinds = [lambda i: Param("f%d" % i, FLOAT, -3.0, 7.5), lambda i: Param("i%d" % i, INT, -50, 900),
+             lambda i: Param("b%d" % i, BOOL), lambda i: Param("e%d" % i, ENUM, options=["on", "off", "default"])]
+    return [kinds[i % 4](i) for i in range(P)]
+
+
+@pytest.mark.parametrize("P,aos", [(339, "1"), (339, "0"), (61, "1"), (2100, "1")])
+def test_de_wide_spaces(P, aos, monkeypatch):
+    """k_de on wide spaces: 339 params (the C4 gcc shape; a column count that is
+    no multiple of the 8-column staging group or the 16-column row pitch) and 61
+    (< one group of 64), through the member-major donor copy and, with
+    UT_DE_AOS=0, the column-major gather; 2100 params (> 2048: the cr-test bits
+    spill to the global scratch and the column-major path is taken)"""
+    monkeypatch.setenv("UT_DE_AOS", aos)
+    space = _wide_space(P)
+    e = engine(space, seed=61)
+    e.population_init(97, round_=1)
+    pop = e.population_get().cpu().numpy()
+    best = ode.population_init(space, 1, seed=5)[:, 0]
+    m = 600 if P > 1000 else 2500
+    for rnd, cr, n_cross, share in ((2, 0.1, 1, 0), (3, 0.6, 4, 2)):
+        got = e.propose_de(m, round_=rnd, cand_base=11, cr=cr, n_cross=n_cross, best=best,
+                           information_sharing=share).cpu().numpy()
+        want = ode.propose_de_vec(space, pop, 61, rnd, 11, m, cr, n_cross, best=best if share else None,
+                                  information_sharing=share)
+        np.testing.assert_array_equal(got, want)
