@@ -133,6 +133,8 @@ def test_c4_ga_round(c4, mutation_rate, crossover_rate, two):
     dig = e.hash(torch.from_numpy(allv).cuda())
     hx = digests_to_hex(dig)
     assert hx == c4["H"](allv)
+    # the bench's C4 step hashes through ut_hash_parent (parent1's inner digests reused)
+    assert digests_to_hex(e.hash_parent(torch.from_numpy(allv).cuda(), c4["best"])) == hx
     dup = e.dedup(dig)
     wdup = osel.dedup(hx, c4["hist_hex"])
     assert dup.cpu().numpy().tolist() == wdup
