@@ -565,8 +565,65 @@ __global__ __launch_bounds__(256) void k_ga(const DevParam* __restrict__ params,
   const double* p2row = parent2 ? parent2 : parent1;  // select() twice returns the same best config
   const uint32_t sub2 = 3u;  // random second parent (both parents NULL)
   const int32_t scr_col = 2 * perm_cols;
-  // parent 1 (and the GGA crossover from parent 2, the GA crossover of permutations)
-  double chosen = 0.0;
+  double chosen = 0.0, sel = 0.0;
+  bool diff1 = false, diff2 = false;
+  // one parameter of mutation attempt r: PERM in place in `out`, the other
+  // kinds on v, stored when mutated or when `fresh` (attempt 0 runs fused with
+  // the parent copy, so the copy is stored once and never read back)
+  auto attempt = [&](const DevParam& pr, int32_t p, int32_t r, double v, bool fresh) {
+    const uint32_t sp = (uint32_t)p | ((uint32_t)r << STREAM_RETRY_SHIFT);
+    const u32x4 q = draw(seed, g, sp, round_, op);
+    bool mut = false;
+    if ((double)(P - p) * u01_from(q.x, q.y) < (double)must - sel) {
+      sel += 1.0;
+      mut = true;
+    }
+    mut = mut || (u01_from(q.z, q.w) < mutation_rate);
+    if (pr.kind == UT_PERM) {
+      const int32_t S = pr.psize;
+      WRow o{out + (int64_t)pr.col * ldo + i, ldo};
+      if (mut) {
+        // uniform: op1_randomize; normal: random.choice(manipulators) =
+        // [op1_randomize, op1_small_random_change]
+        PermRng R(seed, g, sp | (1u << STREAM_SUB_SHIFT), round_, op);
+        bool small = false;
+        if (normal) {
+          const u32x4 qc = draw(seed, g, sp | (1u << STREAM_SUB_SHIFT), round_, op);
+          small = below64(u64_from(qc.z, qc.w), 2) == 1;
+        }
+        if (small) perm_small_change(o, S, R);
+        else perm_shuffle(o, S, R);
+      }
+      const PRow a = parent_perm(pr, parent1, p, 2u, seed, g, round_, op, ws + (int64_t)pr.wcol * ldw + i, ldw, false);
+      const PRow b = parent_perm(pr, p2row, p, sub2, seed, g, round_, op,
+                                 ws + (int64_t)(perm_cols + pr.wcol) * ldw + i, ldw, false);
+      diff1 |= !perm_equal(o.ro(), a, S);
+      diff2 |= !perm_equal(o.ro(), b, S);
+      return;
+    }
+    if (mut) {
+      if (normal && is_primitive(pr.kind)) {
+        // op1_normal_mutation (manipulator.py:505-521)
+        double u = unit_of(pr, v, vtab);
+        const double z = normal_draw(seed, g, sp | (2u << STREAM_SUB_SHIFT), round_, op);
+        u = u + (0.0 + z * sigma);
+        if (u < 0.0) u = u * -1.0;
+        if (u > 1.0) u = 1.0 - fmod(u, 1.0);
+        v = from_unit(pr, u, v);
+      } else if (normal && pr.kind == UT_BOOL) {
+        v = 1.0 - v;  // op1_flip
+      } else {
+        v = randomize(pr, draw(seed, g, sp | (1u << STREAM_SUB_SHIFT), round_, op));
+      }
+    }
+    if (mut || fresh) out[(int64_t)pr.col * ldo + i] = v;
+    const double a = parent_value(pr, parent1, p, 2u, seed, g, round_, op);
+    const double b = parent_value(pr, p2row, p, sub2, seed, g, round_, op);
+    diff1 |= d_to_bits(v) != d_to_bits(a);
+    diff2 |= d_to_bits(v) != d_to_bits(b);
+  };
+  // the child (parent 1, the GGA crossover from parent 2, the GA crossover of
+  // permutations) and, in the same pass, mutation attempt 0
   for (int32_t p = 0; p < P; ++p) {
     const DevParam pr = params[p];
     bool from2 = false;
@@ -591,70 +648,20 @@ __global__ __launch_bounds__(256) void k_ga(const DevParam* __restrict__ params,
       } else {
         perm_copy(o, a, S);
       }
+      attempt(pr, p, 0, 0.0, false);
       continue;
     }
     double v = parent_value(pr, parent1, p, 2u, seed, g, round_, op);
     if (from2) v = parent_value(pr, p2row, p, sub2, seed, g, round_, op);
-    out[(int64_t)pr.col * ldo + i] = v;
+    attempt(pr, p, 0, v, true);
   }
-  bool accepted = false;
-  for (int32_t r = 0; r < max_retries && !accepted; ++r) {
-    bool diff1 = false, diff2 = false;
-    double sel = 0.0;
+  bool accepted = diff1 && (!two || diff2);
+  for (int32_t r = 1; r < max_retries && !accepted; ++r) {
+    diff1 = diff2 = false;
+    sel = 0.0;
     for (int32_t p = 0; p < P; ++p) {
       const DevParam pr = params[p];
-      const uint32_t sp = (uint32_t)p | ((uint32_t)r << STREAM_RETRY_SHIFT);
-      const u32x4 q = draw(seed, g, sp, round_, op);
-      bool mut = false;
-      if ((double)(P - p) * u01_from(q.x, q.y) < (double)must - sel) {
-        sel += 1.0;
-        mut = true;
-      }
-      mut = mut || (u01_from(q.z, q.w) < mutation_rate);
-      if (pr.kind == UT_PERM) {
-        const int32_t S = pr.psize;
-        WRow o{out + (int64_t)pr.col * ldo + i, ldo};
-        if (mut) {
-          // uniform: op1_randomize; normal: random.choice(manipulators) =
-          // [op1_randomize, op1_small_random_change]
-          PermRng R(seed, g, sp | (1u << STREAM_SUB_SHIFT), round_, op);
-          bool small = false;
-          if (normal) {
-            const u32x4 qc = draw(seed, g, sp | (1u << STREAM_SUB_SHIFT), round_, op);
-            small = below64(u64_from(qc.z, qc.w), 2) == 1;
-          }
-          if (small) perm_small_change(o, S, R);
-          else perm_shuffle(o, S, R);
-        }
-        const PRow a = parent_perm(pr, parent1, p, 2u, seed, g, round_, op, ws + (int64_t)pr.wcol * ldw + i, ldw, false);
-        const PRow b = parent_perm(pr, p2row, p, sub2, seed, g, round_, op,
-                                   ws + (int64_t)(perm_cols + pr.wcol) * ldw + i, ldw, false);
-        diff1 |= !perm_equal(o.ro(), a, S);
-        diff2 |= !perm_equal(o.ro(), b, S);
-        continue;
-      }
-      const int64_t o = (int64_t)pr.col * ldo + i;
-      double v = out[o];
-      if (mut) {
-        if (normal && is_primitive(pr.kind)) {
-          // op1_normal_mutation (manipulator.py:505-521)
-          double u = unit_of(pr, v, vtab);
-          const double z = normal_draw(seed, g, sp | (2u << STREAM_SUB_SHIFT), round_, op);
-          u = u + (0.0 + z * sigma);
-          if (u < 0.0) u = u * -1.0;
-          if (u > 1.0) u = 1.0 - fmod(u, 1.0);
-          v = from_unit(pr, u, v);
-        } else if (normal && pr.kind == UT_BOOL) {
-          v = 1.0 - v;  // op1_flip
-        } else {
-          v = randomize(pr, draw(seed, g, sp | (1u << STREAM_SUB_SHIFT), round_, op));
-        }
-        out[o] = v;
-      }
-      const double a = parent_value(pr, parent1, p, 2u, seed, g, round_, op);
-      const double b = parent_value(pr, p2row, p, sub2, seed, g, round_, op);
-      diff1 |= d_to_bits(v) != d_to_bits(a);
-      diff2 |= d_to_bits(v) != d_to_bits(b);
+      attempt(pr, p, r, pr.kind == UT_PERM ? 0.0 : out[(int64_t)pr.col * ldo + i], false);
     }
     accepted = diff1 && (!two || diff2);
   }
