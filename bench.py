@@ -298,12 +298,12 @@ def main():
 
     def step_c4(r):
         """GA round: UniformGreedyMutation proposals from the best recorded config
-        -> hash_config -> dedup vs history + batch -> encode -> GP-EI -> top-k"""
+        -> hash_config -> dedup vs history + batch -> encode (fused) -> GP-EI -> top-k"""
         eng.gp_fit(X, y, lengthscale=ell, sigma_f2=1.0, sigma_n2=1e-6, jitter=1e-8, wait=False)
         vals, invalid = eng.propose_ga(m, parent1=parent, round_=r, cand_base=cand_base, mutation_rate=0.1)
         dig = eng.hash_parent(vals, parent)   # children keep most of the parent's values: its inner digests are reused
         dup = torch.maximum(eng.dedup(dig), invalid)
-        _, _, score = eng.gp_score(eng.encode(vals), acq=acq, dup=dup)
+        _, _, score = eng.gp_score_values(vals, acq=acq, dup=dup)   # encode fused into the K* operand pass
         idx, top = eng.topk(score, k, dup=dup, cand_base=cand_base)
         if world > 1:
             sel = torch.where(idx >= 0, idx - cand_base, torch.zeros_like(idx))

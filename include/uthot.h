@@ -265,6 +265,12 @@ int ut_gp_last_fit_kind(ut_ctx* ctx, int32_t* kind);
  * candidates excluded from selection (score forced to -inf). */
 int ut_gp_score(ut_ctx* ctx, const double* features, int64_t ld, int64_t m, const ut_acq* acq,
                 const uint8_t* dup, double* mu, double* var, double* score);
+/* ut_gp_score on raw values [ncols][ld] instead of features: the encoding
+ * (ut_encode_features), the 1/lengthscale scaling and |u|^2 run as one pass
+ * that writes only what the K* GEMM reads, so no [d][m] feature matrix is
+ * written and read back.  Same results as ut_gp_score(ut_encode_features(values)). */
+int ut_gp_score_values(ut_ctx* ctx, const double* values, int64_t ld, int64_t m, const ut_acq* acq,
+                       const uint8_t* dup, double* mu, double* var, double* score);
 /* Selection-exact pruned scoring + top-k (fp64 fits only; EI, or UCB with
  * kappa >= 0: scores that increase with sigma).  sigma^2 = sf2 - |L^-1 k*|^2
  * and every row of L^-1 k* adds a square, so the first `bound_rows` rows give

@@ -1060,3 +1060,30 @@ def test_de_wide_spaces(P, aos, monkeypatch):
         want = ode.propose_de_vec(space, pop, 61, rnd, 11, m, cr, n_cross, best=best if share else None,
                                   information_sharing=share)
         np.testing.assert_array_equal(got, want)
+
+
+@pytest.mark.parametrize("which", ["mixed", "hpl"])
+def test_gp_score_values_equals_score_of_encoded(which):
+    """ut_gp_score_values (encode + 1/ell scaling fused into the K* operand
+    pass) == ut_gp_score(ut_encode_features(values)), and == the oracle's
+    posterior within RTOL"""
+    space = {"mixed": mixed_space, "hpl": hpl_space}[which]()
+    e = engine(space, seed=71)
+    pop = ode.population_init(space, 3000, seed=12)
+    F = features(space, pop)
+    d = F.shape[0]
+    rng = np.random.default_rng(3)
+    X = features(space, ode.population_init(space, 200, seed=13)).T.copy()
+    y = rng.normal(size=200)
+    ell = rng.uniform(0.5, 2.0, size=d)
+    e.gp_fit(X, y, lengthscale=ell, sigma_f2=1.0, sigma_n2=1e-6, jitter=1e-8)
+    dup = np.zeros(3000, np.uint8)
+    dup[::17] = 1
+    vals, dupd = dev(pop), dev(dup)
+    mu0, var0, s0 = e.gp_score(e.encode(vals), dup=dupd)
+    mu1, var1, s1 = e.gp_score_values(vals, dup=dupd)
+    for a, b in ((mu0, mu1), (var0, var1), (s0, s1)):
+        np.testing.assert_allclose(b.cpu().numpy(), a.cpu().numpy(), rtol=1e-12, atol=1e-14)
+    mu, var = ogp.GP(X, y, lengthscale=ell, sigma_f2=1.0, sigma_n2=1e-6, jitter=1e-8).posterior(F.T)
+    np.testing.assert_allclose(mu1.cpu().numpy(), mu, rtol=RTOL, atol=ATOL)
+    np.testing.assert_allclose(var1.cpu().numpy(), var, rtol=RTOL, atol=ATOL)

@@ -124,6 +124,7 @@ SIGNATURES = {
     "ut_forest_set": (C.c_int, [P, I32, P, I64, P, I32, D, D, D]),
     "ut_forest_predict": (C.c_int, [P, P, I64, I64, I32, P, D, P, P]),
     "ut_gp_score": (C.c_int, [P, P, I64, I64, C.POINTER(Acq), P, P, P, P]),
+    "ut_gp_score_values": (C.c_int, [P, P, I64, I64, C.POINTER(Acq), P, P, P, P]),
     "ut_gp_set_precision": (C.c_int, [P, I32]),
     "ut_gp_stats": (C.c_int, [P, C.POINTER(D), C.POINTER(D), C.POINTER(D)]),
     "ut_topk": (C.c_int, [P, P, P, I64, I64, I32, P, P]),

@@ -667,6 +667,20 @@ int ut_gp_score(ut_ctx* c, const double* feat, int64_t ld, int64_t m, const ut_a
   return rc;
 }
 
+int ut_gp_score_values(ut_ctx* c, const double* values, int64_t ld, int64_t m, const ut_acq* acq,
+                       const uint8_t* dup, double* mu, double* var, double* score) {
+  if (!c) return UT_EINVAL;
+  UT_CHECK(c, m >= 0 && (values || m == 0) && ld >= m, UT_EINVAL, "gp_score_values: bad arguments");
+  UT_CHECK(c, acq != nullptr, UT_EINVAL, "gp_score: acq is NULL");
+  const bool own = c->timing.on && !c->timing.in_round;
+  if (own) timing_begin(c);
+  // encode + 1/ell scaling + |u'|^2 in one pass (k_encode_scaled): no feature matrix
+  int rc = gp_encode_scaled(c, values, ld, m);
+  if (!rc) rc = gp_score_impl(c, nullptr, ld, m, acq, dup, mu, var, score);
+  if (own) timing_end(c);
+  return rc;
+}
+
 int ut_gp_topk_pruned(ut_ctx* c, const double* feat, int64_t ld, int64_t m, const ut_acq* acq, const uint8_t* dup,
                       int64_t cand_base, int32_t k, int32_t bound_rows, int64_t* out_idx, double* out_score,
                       ut_prune_stats* stats) {

@@ -311,6 +311,18 @@ class BatchEngine:
                                                _ptr(mu), _ptr(var), _ptr(score)), "ut_gp_score")
         return mu, var, score
 
+    def gp_score_values(self, values: torch.Tensor, m: Optional[int] = None, acq: Optional[L.Acq] = None,
+                        dup: Optional[torch.Tensor] = None):
+        """ut_gp_score_values: gp_score(encode(values)) with the encoding fused
+        into the K* operand pass (no feature matrix)"""
+        m = values.shape[1] if m is None else m
+        acq = acq or self.acq()
+        mu, var, score = self._empty(m), self._empty(m), self._empty(m)
+        L.check(self.ctx, self.lib.ut_gp_score_values(self.ctx, _ptr(values), values.stride(0), m, C.byref(acq),
+                                                      _ptr(dup), _ptr(mu), _ptr(var), _ptr(score)),
+                "ut_gp_score_values")
+        return mu, var, score
+
     def gp_topk_pruned(self, feat: torch.Tensor, k: int, m: Optional[int] = None, acq: Optional[L.Acq] = None,
                        dup: Optional[torch.Tensor] = None, cand_base: int = 0, bound_rows: int = 256):
         """ut_gp_topk_pruned: the top-k of the GP score, selection-exact, with the
