@@ -141,6 +141,9 @@ class OracleEngine:
             sc = np.where(dup.numpy() != 0, -np.inf, sc)
         return torch.from_numpy(mu), torch.from_numpy(var), torch.from_numpy(sc)
 
+    def gp_score_values(self, values, m=None, acq=None, dup=None):
+        return self.gp_score(self.encode(values), m, acq, dup)
+
     def topk(self, score, k, dup=None, cand_base=0):
         s = score.numpy().tolist()
         d = None if dup is None else dup.numpy().tolist()

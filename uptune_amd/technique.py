@@ -500,7 +500,8 @@ class GpuBatchTechnique(SearchTechnique):
                                                  cand_base=base, bound_rows=self.prune_rows)
                 loc = torch.where(idx >= 0, idx - base, torch.zeros_like(idx))
                 return vals, idx, top, dig[loc], vals[:, loc]
-            _, _, score = eng.gp_score(eng.encode(vals), acq=eng.acq(self.acq_kind), dup=dup)
+            # encoding fused into the K* operand pass (no feature matrix)
+            _, _, score = eng.gp_score_values(vals, acq=eng.acq(self.acq_kind), dup=dup)
         else:  # no model yet: every non-duplicate candidate is equally good (lowest index first)
             score = torch.zeros(vals.shape[1], dtype=torch.float64, device=vals.device)
         idx, top = eng.topk(score, self.batch, dup=dup, cand_base=base)   # GLOBAL candidate indices
