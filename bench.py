@@ -12,10 +12,22 @@ top-k (+ all-gather merge of the local top-k over RCCL when N > 1).
 
     python bench.py [--gpus N --steps K --warmup W]
 
-N > 1 is launched by torch.distributed.run (one rank per GPU, backend nccl =
-RCCL); each rank scores its own shard of global candidate indices (weak
-scaling: m per GPU is fixed) and the local top-k lists are all-gathered and
-merged.  Prints ONE JSON line on rank 0.
+N > 1: one process per GPU.  Under torch.distributed.run (WORLD_SIZE set)
+each process is one rank; run directly with --gpus N, the script starts the N
+rank processes itself (before anything touches a GPU) and relays rank 0's line.
+Each rank scores its own shard of global candidate indices (weak scaling: m
+per GPU is fixed); the local top-k lists travel through libuthot's own RCCL
+communicator (ut_comm_allgather_topk: all-gather + HIP merge kernel) and the
+merged selections join every rank's history, so every rank -- and every N --
+selects the same candidates.  torch.distributed (gloo) only bootstraps the
+communicator and carries the barriers.  UT_DIST_BACKEND=gloo rehearses N ranks
+on fewer GPUs (records over gloo, merge on the device).
+
+After the timed rounds (outside the timed region) rank 0 checks the last
+round's selections against the oracle (`parity`: DE trials, hash_config
+digests, EI) and runs one extra round at a lengthscale whose EI top-k is
+score-determined, checking it against the oracle EI of a random sample of the
+other candidates.  Prints ONE JSON line on rank 0.
 """
 from __future__ import annotations
 
@@ -188,7 +200,96 @@ def kernel_table(m, n, d, outer_blocks):
     return out
 
 
+def spawn_ranks(n):
+    """--gpus N without a launcher: start N rank processes (one GPU each) before
+    this process touches a GPU, relay rank 0's output, and fail if any rank
+    fails (the others are stopped then, so none waits in a collective)."""
+    import socket
+    import subprocess
+    import tempfile
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    out0 = tempfile.TemporaryFile(mode="w+")
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      stdout=out0 if r == 0 else subprocess.DEVNULL))
+    rc = 0
+    live = list(procs)
+    while live:
+        time.sleep(0.2)
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                print(f"bench: rank {procs.index(p)} exited with {code}; stopping the other ranks",
+                      file=sys.stderr, flush=True)
+                for q in live:
+                    q.terminate()
+                for q in live:
+                    try:
+                        q.wait(timeout=20)
+                    except subprocess.TimeoutExpired:
+                        q.kill()
+                live = []
+    out0.seek(0)
+    sys.stdout.write(out0.read())
+    sys.stdout.flush()
+    return rc
+
+
+def oracle_space_of(manip):
+    """uptune_amd manipulator -> oracle Param list (the checker's view of the space)"""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from tests._spaces import oracle_space
+    return oracle_space(manip)
+
+
+def parity_de_round(eng, space, idx, top, dig, npop, seed, round_, X, y, ell, jitter, k):
+    """The checker (outside the timed region): a DE round's merged selections
+    (global indices idx, scores top, digests dig) against the oracle --
+    the trials the oracle proposes at those indices (differentialevolution.py:105-129
+    restated in oracle/de.py) equal the device's, their hash_config digests
+    (manipulator.py:233-243) equal the round's, and the round's scores equal
+    the oracle GP's EI (oracle/gp.py) within 1e-5 relative.
+    -> (report dict, oracle trials [ncols][k'], oracle EI [k'])"""
+    import torch
+    from oracle import de as ode
+    from oracle import gp as ogp
+    from oracle import hashing as oh
+    from oracle.space import features, from_f64
+    from uptune_amd.engine import digests_to_hex
+    ii = idx.cpu().numpy()
+    sel = np.flatnonzero(ii >= 0)
+    g = ii[sel]
+    want = ode.propose_de_at(space, g, npop, seed, round_, 0.2, 1)
+    got = torch.stack([eng.propose_de(1, round_=round_, cand_base=int(j), cr=0.2, n_cross=1)[:, 0] for j in g],
+                      dim=1).cpu().numpy() if len(g) else np.zeros_like(want)
+    hexes = [oh.hash_config(space, [from_f64(p, want[c, j]) for c, p in enumerate(space)]) for j in range(len(g))]
+    ghex = digests_to_hex(dig[torch.as_tensor(sel, device=dig.device)]) if len(g) else []
+    gp = ogp.GP(X, y, lengthscale=ell, sigma_f2=1.0, sigma_n2=1e-6, jitter=jitter)
+    mu, var = gp.posterior(features(space, want).T)
+    ei = ogp.acquisition(mu, var, gp.f_best)
+    s = top.cpu().numpy()[sel]
+    rel = float(np.max(np.abs(s - ei) / np.maximum(np.abs(ei), 1e-300))) if len(g) else 0.0
+    return ({"rows": int(len(g)), "trials_equal": bool(np.array_equal(got, want)),
+             "digests_equal": bool(ghex == hexes), "ei_max_rel_err": rel, "round": int(round_)}, want, ei)
+
+
 def main():
+    if "WORLD_SIZE" not in os.environ:
+        pre = argparse.ArgumentParser(add_help=False)
+        pre.add_argument("--gpus", type=int, default=1)
+        n_req = pre.parse_known_args()[0].gpus
+        if n_req > 1:
+            sys.exit(spawn_ranks(n_req))
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
@@ -202,6 +303,9 @@ def main():
     ap.add_argument("--b1-sample", type=int, default=1 << 18,
                     help="candidates in the B1 batch baseline sample (C++/OpenMP + BLAS on the host cores)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-parity", action="store_true", help="skip the oracle check of the selections")
+    ap.add_argument("--parity-sample", type=int, default=1 << 16,
+                    help="random other candidates whose oracle EI must not beat the score-determined top-k")
     ap.add_argument("--precision", type=int, default=64, choices=(64, 32, 16),
                     help="GP contractions on fp64 MFMA (1e-5 parity) or fp32 MFMA (1e-3 parity); 16 = f16x3: "
                          "the variance contraction as 3 fp16 MFMA products of hi/lo splits (fp32 tier, 1e-3)")
@@ -228,19 +332,21 @@ def main():
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    # one rank per GPU; more ranks than GPUs (the gloo rehearsal) share them round-robin
-    local = int(os.environ.get("LOCAL_RANK", "0")) % max(torch.cuda.device_count(), 1)
-    torch.cuda.set_device(local)
-    # UT_DIST_BACKEND=gloo rehearses the N > 1 path with several ranks on one GPU
-    # (RCCL needs one GPU per rank); the driver's multi-GPU runs use nccl = RCCL
+    if world != args.gpus:
+        ap.error(f"--gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks")
+    ndev = torch.cuda.device_count()
+    # UT_DIST_BACKEND=gloo rehearses the N > 1 path with several ranks on fewer
+    # GPUs (they share them round-robin); the multi-GPU runs use RCCL, one GPU per rank
     backend = os.environ.get("UT_DIST_BACKEND", "nccl")
-    if world > 1:
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        else:
-            dist.init_process_group(backend)
+    if world > 1 and backend == "nccl" and world > ndev:
+        ap.error(f"{world} RCCL ranks need {world} GPUs, {ndev} visible (UT_DIST_BACKEND=gloo shares GPUs)")
+    local = int(os.environ.get("LOCAL_RANK", "0")) % max(ndev, 1)
+    torch.cuda.set_device(local)
+    n_gpus = min(world, max(ndev, 1))      # distinct devices of the job
+    if world > 1:   # host-side control (bootstrap, barriers, timing max); the data path is below
+        dist.init_process_group("gloo")
 
-    from uptune_amd.dist import allgather_topk
+    from uptune_amd.dist import DeviceComm, allgather_topk
     from uptune_amd.engine import BatchEngine
     from uptune_amd.manipulator import ConfigurationManipulator, FloatParameter
 
@@ -296,6 +402,20 @@ def main():
     acq = eng.acq("ei", xi=0.0)
     ell = {"c2": 0.2, "c3": 1.0, "c4": 2.0}[args.config]
 
+    comm = None
+    if world > 1 and backend == "nccl":
+        comm = DeviceComm.from_group(None, eng.device)   # libuthot's RCCL communicator (id over gloo)
+
+    def exchange(idx, top, dig):
+        """merged top-k of every rank (identical on all ranks); world 1: the local list"""
+        if world == 1:
+            return idx, top, dig
+        if comm is not None:
+            i, s_, d_, _ = comm.allgather_topk(idx, top, dig, k)
+        else:
+            i, s_, d_, _ = allgather_topk(idx, top, dig, k)
+        return i, s_, d_
+
     def step_c4(r):
         """GA round: UniformGreedyMutation proposals from the best recorded config
         -> hash_config -> dedup vs history + batch -> encode (fused) -> GP-EI -> top-k"""
@@ -305,14 +425,15 @@ def main():
         dup = torch.maximum(eng.dedup(dig), invalid)
         _, _, score = eng.gp_score_values(vals, acq=acq, dup=dup)   # encode fused into the K* operand pass
         idx, top = eng.topk(score, k, dup=dup, cand_base=cand_base)
-        if world > 1:
-            sel = torch.where(idx >= 0, idx - cand_base, torch.zeros_like(idx))
-            idx, top = allgather_topk(idx, top, dig[sel], k)
-        return idx, top
+        sel = torch.where(idx >= 0, idx - cand_base, torch.zeros_like(idx))
+        sdig = torch.where((idx >= 0).unsqueeze(1), dig[sel], torch.zeros_like(dig[sel]))
+        idx, top, sdig = exchange(idx, top, sdig)
+        eng.history_add(sdig)                             # the merged selections join every rank's history
+        return idx, top, sdig
 
     prune_stats = []
 
-    def step(r):
+    def step(r, ell=ell):
         if args.config == "c4":
             return step_c4(r)
         eng.gp_fit(X, y, lengthscale=ell, sigma_f2=1.0, sigma_n2=1e-6, wait=False)   # overlaps propose + hash
@@ -323,10 +444,9 @@ def main():
         else:
             idx, top, dig, _ = eng.score_round_de(m, k, round_=r, cand_base=cand_base, cr=0.2, n_cross=1, acq=acq,
                                                   want_values=False)
-        eng.history_add(dig)                              # the selections join the history (device-side)
-        if world > 1:
-            idx, top = allgather_topk(idx, top, dig, k)   # RCCL all_gather + deterministic merge
-        return idx, top
+        idx, top, dig = exchange(idx, top, dig)           # RCCL all-gather + HIP merge (world > 1)
+        eng.history_add(dig)                              # the merged selections join every rank's history
+        return idx, top, dig
 
     for w in range(args.warmup):
         step(w)
@@ -339,7 +459,7 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for s in range(args.steps):
-        idx, top = step(args.warmup + s)
+        idx, top, sdig = step(args.warmup + s)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -353,9 +473,49 @@ def main():
             pass
     eng.set_timing(False)
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda" if backend == "nccl" else "cpu")
+        t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+
+    # ---- the checker, outside the timed region ------------------------------
+    parity = None
+    if not args.no_parity and args.config in ("c2", "c3") and not args.prune:
+        r_last = args.warmup + args.steps - 1
+        space = oracle_space_of(manip)
+        jit = 0.0
+        rep = None
+        if rank == 0:
+            rep, _, _ = parity_de_round(eng, space, idx, top, sdig, npop, 1, r_last, X, y, ell, jit, k)
+        parity = {"last_round": rep}
+        if args.config == "c2":
+            # a round whose top-k the scores decide (ell = 2.0: EI values spread,
+            # where the headline's ell = 0.2 makes every k* underflow to ~1e-58
+            # and the selection is decided by index order)
+            r_x = r_last + 1
+            ix, tx, dx = step(r_x, ell=2.0)
+            torch.cuda.synchronize()
+            if rank == 0:
+                rep2, _, ei_sel = parity_de_round(eng, space, ix, tx, dx, npop, 1, r_x, X, y, 2.0, jit, k)
+                from oracle import de as ode
+                from oracle import gp as ogp
+                from oracle.space import features
+                rng = np.random.default_rng(12345)
+                chosen = set(ix.cpu().numpy().tolist())
+                samp = rng.choice(npop, size=min(args.parity_sample, npop), replace=False)
+                samp = np.array([g for g in samp if g not in chosen], dtype=np.int64)
+                gp = ogp.GP(X, y, lengthscale=2.0, sigma_f2=1.0, sigma_n2=1e-6)
+                mu, var = gp.posterior(features(space, ode.propose_de_at(space, samp, npop, 1, r_x, 0.2, 1)).T)
+                ei_s = ogp.acquisition(mu, var, gp.f_best)
+                kth = float(np.min(ei_sel)) if len(ei_sel) else float("inf")
+                rep2.update({"lengthscale": 2.0, "sample": int(len(samp)),
+                             "kth_selected_ei": kth, "best_unselected_sample_ei": float(np.max(ei_s)),
+                             "topk_beats_sample": bool(np.max(ei_s) <= kth * (1.0 + 1e-5)),
+                             "distinct_selected_scores": int(len(np.unique(tx.cpu().numpy())))})
+                parity["score_determined"] = rep2
+        if rank == 0:
+            legs = [v for v in parity.values() if v]
+            parity["all_ok"] = all(v["trials_equal"] and v["digests_equal"] and v["ei_max_rel_err"] <= 1e-5 and
+                                   v.get("topk_beats_sample", True) for v in legs)
 
     ms_per_step = elapsed * 1000.0 / args.steps
     value = world * m / (elapsed / args.steps)
@@ -418,7 +578,8 @@ def main():
         "metric": "candidate configs scored/sec (GP-EI + top-k)",
         "value": value,
         "unit": "candidates/s",
-        "n_gpus": world,
+        "n_gpus": n_gpus,
+        "world": world,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": ms_per_step,
@@ -430,7 +591,10 @@ def main():
                       "K*/fit/EI f64)"}[args.precision],
         "data": data,
         "config": {"workload": workload, "candidates_per_gpu": m, "gp_n": n, "dims": d, "k": k,
-                   "parallelism": f"dp{world}"},
+                   "parallelism": f"dp{world}",
+                   "exchange": (None if world == 1 else "libuthot RCCL (ut_comm_allgather_topk + HIP merge)"
+                                if comm is not None else "gloo records + HIP merge (rehearsal)")},
+        "parity": parity,
         "stage_ms": stages,
         "kernels": (kernel_table(m, n, d, eng.space_info()[1]) if profiled else None),
         "prune": prune_info,
@@ -459,6 +623,9 @@ def main():
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:
+        dist.barrier()
+        if comm is not None:
+            comm.close()
         dist.destroy_process_group()
 
 

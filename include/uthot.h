@@ -51,7 +51,8 @@ enum {
   UT_ENOSPACE = -3,    /* ut_space_define not called */
   UT_EUNSUPPORTED = -4,
   UT_ENOTPD = -5,      /* GP kernel matrix not positive definite */
-  UT_ENOMEM = -6
+  UT_ENOMEM = -6,
+  UT_ECOMM = -7        /* RCCL error (multi-GPU exchange) */
 };
 
 /* parameter kinds: manipulator.py:651-1356 (the kinds create_params builds,
@@ -299,6 +300,10 @@ int ut_gp_topk_pruned(ut_ctx* ctx, const double* features, int64_t ld, int64_t m
  * K*, f32 accumulate (fp32-class, the same 1e-3 parity tier).  The fit itself
  * is always fp64. */
 int ut_gp_set_precision(ut_ctx* ctx, int32_t bits);
+/* wait for the last (possibly asynchronous) fit and report whether its kernel
+ * matrix was positive definite (*ok = 1) or not (*ok = 0: later scoring
+ * yields NaN scores until a new fit succeeds); not an error either way */
+int ut_gp_fit_status(ut_ctx* ctx, int32_t* ok);
 /* f_best (min standardised y), y mean/std used for standardisation */
 int ut_gp_stats(ut_ctx* ctx, double* f_best, double* y_mean, double* y_std);
 
@@ -350,6 +355,56 @@ int ut_forest_set(ut_ctx* ctx, int32_t n_trees, const int32_t* roots_host, int64
  * score [m] may be NULL; score = sign * pred (sign -1: minimise), -inf where dup[i] */
 int ut_forest_predict(ut_ctx* ctx, const double* features, int64_t ld, int64_t m, int32_t n_features,
                       const uint8_t* dup, double sign, double* pred, double* score);
+
+/* ---- multi-GPU exchange over RCCL -------------
+ * One process per GPU, one communicator per context.  Rank r scores the
+ * global candidate indices [r*m, (r+1)*m) of a round; population, training
+ * set, GP factor and history set are replicated.  These calls replace the
+ * reference's result exchange between its parallel_factor search instances
+ * (python/uptune/api.py:400-401 creates them, :547-553 api.sync injects every
+ * instance's results into the others; opentuner/api.py:87-104 TuningRunManager.sync).
+ * Collectives are enqueued on the context's stream (ut_set_stream) with no
+ * host wait, except ut_comm_bcast_results (it returns the broadcast count)
+ * and ut_comm_barrier. */
+#define UT_COMM_ID_BYTES 128
+/* a fresh communicator id (rank 0 creates it; the caller hands the 128 bytes
+ * to every rank, e.g. over torch.distributed's store) */
+int ut_comm_unique_id(uint8_t* id_host);
+/* join the communicator (blocks until all nranks ranks have joined); the
+ * context's device is this rank's GPU */
+int ut_comm_init(ut_ctx* ctx, int32_t rank, int32_t nranks, const uint8_t* id_host);
+int ut_comm_destroy(ut_ctx* ctx);
+int ut_comm_info(ut_ctx* ctx, int32_t* rank, int32_t* nranks);
+/* the merged top-k of every rank's local top-k (all-gather + ut_topk_merge):
+ * in: idx [k] (global, -1 = empty), score [k], digest [k][8], and optionally
+ * the selected rows [ncols][ld_rows] (ncols = 0: none).  out: the merged
+ * idx / score / digest [k] and rows [ncols][ld_out], identical on every rank
+ * (any output may be NULL). */
+int ut_comm_allgather_topk(ut_ctx* ctx, int32_t k, const int64_t* idx, const double* score, const uint32_t* digest,
+                           const double* rows, int64_t ld_rows, int32_t ncols, int64_t* out_idx, double* out_score,
+                           uint32_t* out_digest, double* out_rows, int64_t ld_out);
+/* the merge alone, on n gathered records (no communicator needed): records
+ * with idx < 0 or a NaN score are empty; among records with equal digests only
+ * the smallest global index survives (a configuration proposed on two shards
+ * is requested once); the k best survivors by (-score, idx) fill the output in
+ * that order, empty slots get idx -1, score -inf, a zero digest and zero rows. */
+int ut_topk_merge(ut_ctx* ctx, int64_t n, int32_t k, const int64_t* idx, const double* score, const uint32_t* digest,
+                  const double* rows, int64_t ld_rows, int32_t ncols, int64_t* out_idx, double* out_score,
+                  uint32_t* out_digest, double* out_rows, int64_t ld_out);
+/* the per-round history delta from `root`: objective values y [n] and digests
+ * [n][8] (device buffers of capacity `cap` on every rank).  The root's n goes
+ * first, so every rank learns it (*n_out_host) and takes part in the payload
+ * broadcast even when its own n differs; n > cap is UT_EINVAL after the
+ * collective (rows beyond cap are dropped). */
+int ut_comm_bcast_results(ut_ctx* ctx, int32_t root, int64_t n, double* y, uint32_t* digest, int64_t cap,
+                          int64_t* n_out_host);
+/* raw broadcast of `bytes` bytes of a device buffer from `root` */
+int ut_comm_bcast(ut_ctx* ctx, void* buf, int64_t bytes, int32_t root);
+/* in-place all-reduce of n doubles (device buffer) */
+enum { UT_RED_SUM = 0, UT_RED_MAX = 1, UT_RED_MIN = 2 };
+int ut_comm_allreduce_f64(ut_ctx* ctx, double* buf, int64_t n, int32_t op);
+/* every rank's stream reaches this point (an all-reduce, then a stream sync) */
+int ut_comm_barrier(ut_ctx* ctx);
 
 /* per-kernel device time (ms) of the ut_score_round_* calls since timing was
  * enabled with ut_set_timing(ctx, 1), averaged over those rounds.  Events are

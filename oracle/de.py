@@ -101,14 +101,34 @@ def propose_de_vec(space, pop, seed, round_, cand_base, m, cr, n_cross=1, best=N
     driver's best config as a value row [ncols] (None: no result yet, the pool
     is the population only)."""
     ncols, npop = pop.shape
-    P = len(space)
-    starts, _ = columns(space)
     g = np.arange(cand_base, cand_base + m, dtype=np.uint64)
     share = information_sharing if best is not None else 0
     t, d1, d2, d3 = donors(g, npop, seed, round_, share)
     if share:   # the best config as an extra population column npop
         pop = np.concatenate([pop, np.asarray(best, dtype=np.float64).reshape(ncols, 1)], axis=1)
         d1, d2, d3 = (np.where(d < 0, npop, d) for d in (d1, d2, d3))
+    return _trials(space, pop, g, t, d1, d2, d3, seed, round_, cr, n_cross)
+
+
+def propose_de_at(space, g, npop, seed, round_, cr, n_cross=1):
+    """The trials of explicit global candidate indices g of a round over the
+    op1_randomize population of npop members (no best config yet), computing
+    only the members those trials read (target + 3 donors): the bench's parity
+    check of a full-size round's selections.  = propose_de_vec(...)[:, g]."""
+    g = np.asarray(g, dtype=np.uint64)
+    t, d1, d2, d3 = donors(g, npop, seed, round_, 0)
+    members = np.unique(np.concatenate([t, d1, d2, d3]))
+    pop = population_init(space, npop, seed, members=members)
+    t, d1, d2, d3 = (np.searchsorted(members, d) for d in (t, d1, d2, d3))
+    return _trials(space, pop, g, t, d1, d2, d3, seed, round_, cr, n_cross)
+
+
+def _trials(space, pop, g, t, d1, d2, d3, seed, round_, cr, n_cross):
+    """the DE trial of every candidate g: target column t, donor columns d1-d3 of pop"""
+    ncols = pop.shape[0]
+    m = g.size
+    P = len(space)
+    starts, _ = columns(space)
     F = use_f(g, seed, round_)
     forced = forced_mask(g, P, n_cross, seed, round_)
     crt = cr_tests(g, P, cr, seed, round_)
@@ -178,10 +198,12 @@ def propose_de_scalar(space, pop_cfgs, seed, round_, g, cr, n_cross=1, best_cfg=
     return cfg
 
 
-def population_init(space, npop, seed, round_=0):
-    """op1_randomize every member (manipulator.py:171-176) -> SoA [ncols][npop]"""
+def population_init(space, npop, seed, round_=0, members=None):
+    """op1_randomize every member (manipulator.py:171-176) -> SoA [ncols][npop]
+    (members: only those member indices, in that order -> [ncols][len(members)])"""
     from .space import to_f64
-    g = np.arange(npop, dtype=np.uint64)
+    g = np.arange(npop, dtype=np.uint64) if members is None else np.asarray(members, dtype=np.uint64)
+    npop = g.size
     starts, nc = columns(space)
     out = np.empty((nc, npop), dtype=np.float64)
     for p, prm in enumerate(space):
@@ -189,7 +211,7 @@ def population_init(space, npop, seed, round_=0):
         if prm.kind == PERM:   # seed_value() = list(items), then shuffle
             S = width(prm)
             for j in range(npop):
-                out[c0:c0 + S, j] = pm.randomized(pm.identity(S), pm.Words(seed, j, p, round_, ph.OP_INIT))
+                out[c0:c0 + S, j] = pm.randomized(pm.identity(S), pm.Words(seed, int(g[j]), p, round_, ph.OP_INIT))
             continue
         x, y, z, w = ph.draw(seed, g, p, round_, ph.OP_INIT)
         if prm.kind == 0:  # FLOAT, vectorised: lo + (hi - lo) * u

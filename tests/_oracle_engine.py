@@ -30,6 +30,7 @@ class OracleEngine:
         self._slots = {}
         self._hist = set()
         self.gp = None
+        self.gp_ok = False
         self.forest = None
         self.calls = {"hash": 0, "gp_fit": 0, "gp_score": 0}
 
@@ -125,8 +126,18 @@ class OracleEngine:
         pass
 
     def gp_fit(self, X, y, lengthscale, sigma_f2=1.0, sigma_n2=1e-6, jitter=0.0, wait=True):
+        """as ut_gp_fit_async: a kernel matrix that is not positive definite
+        does not raise; scores are NaN until a fit succeeds (gp_fit_ok)"""
         self.calls["gp_fit"] += 1
-        self.gp = ogp.GP(X, y, lengthscale=lengthscale, sigma_f2=sigma_f2, sigma_n2=sigma_n2, jitter=jitter)
+        self.calls.setdefault("jitter", []).append(jitter)
+        try:
+            self.gp = ogp.GP(X, y, lengthscale=lengthscale, sigma_f2=sigma_f2, sigma_n2=sigma_n2, jitter=jitter)
+            self.gp_ok = True
+        except np.linalg.LinAlgError:
+            self.gp_ok = False
+
+    def gp_fit_ok(self):
+        return self.gp_ok
 
     @staticmethod
     def acq(kind="ei", xi=0.0, kappa=2.0):
@@ -135,6 +146,9 @@ class OracleEngine:
     def gp_score(self, feat, m=None, acq=None, dup=None):
         self.calls["gp_score"] += 1
         kind, xi, kappa = acq or ("ei", 0.0, 2.0)
+        if not self.gp_ok:
+            nan = torch.full((feat.shape[1],), float("nan"), dtype=torch.float64)
+            return nan, nan.clone(), nan.clone()
         mu, var = self.gp.posterior(feat.numpy().T)
         sc = ogp.acquisition(mu, var, self.gp.f_best, kind=kind, xi=xi, kappa=kappa)
         if dup is not None:

@@ -46,7 +46,9 @@ def _worker(rank, world, port, k, q):
     li = torch.tensor(loc, dtype=torch.int64)
     ls = torch.tensor([scores[g] if g >= 0 else float("-inf") for g in loc], dtype=torch.float64)
     ld = torch.tensor(np.stack([dig[g] if g >= 0 else np.zeros(8, np.int32) for g in loc]), dtype=torch.int32)
-    gi, gs = allgather_topk(li, ls, ld, k)
+    gi, gs, gd, _ = allgather_topk(li, ls, ld, k)
+    # the merged digests are the selected candidates' (zero for empty slots)
+    assert all((gd[j].numpy() == (dig[g] if g >= 0 else 0)).all() for j, g in enumerate(gi.tolist()))
     X = torch.arange(12, dtype=torch.float64).reshape(3, 4) if rank == 0 else None
     y = torch.tensor([1.0, 2.0, 3.0]) if rank == 0 else None
     dd = torch.arange(24, dtype=torch.int32).reshape(3, 8) if rank == 0 else None

@@ -1,4 +1,6 @@
-"""The RCCL ("nccl" backend) path of uptune_amd.dist with DEVICE tensors.
+"""The RCCL ("nccl" backend) path of uptune_amd.dist with DEVICE tensors:
+on an RCCL group every exchange goes through libuthot's own communicator
+(ut_comm_*, bootstrapped over the torch group) and the HIP merge kernel.
 
 The one-GPU boxes cannot run two RCCL ranks (RCCL refuses two ranks on one
 device), so this runs the nccl code paths at world size 1 in a spawned
@@ -41,7 +43,9 @@ def _worker(port, q):
         idx = torch.tensor([5, 2, -1, 9], dtype=torch.int64, device=dev)
         sc = torch.tensor([3.0, 7.0, float("-inf"), 7.0], dtype=torch.float64, device=dev)
         dig = torch.arange(32, dtype=torch.int32, device=dev).reshape(4, 8)
-        mi, ms = allgather_topk(idx, sc, dig, 4)
+        mi, ms, md, _ = allgather_topk(idx, sc, dig, 4)
+        from uptune_amd import dist as D
+        out["via"] = sorted(type(c).__name__ for c in D._COMMS.values())
         out["topk"] = (mi.device.type, mi.cpu().tolist(), ms.cpu().tolist())
         rows = torch.arange(12, dtype=torch.float64, device=dev).reshape(3, 4)
         si, ss, sr, sd = allgather_selection(idx, sc, dig, rows, 4, with_digests=True)
@@ -61,6 +65,7 @@ def _worker(port, q):
             return sum((c["x%d" % i] - 0.5) ** 2 for i in range(6))
         drv.main(f, test_limit=40)
         out["loop"] = (drv.test_count, len(drv.results_query()), drv.best_result.time)
+        D.release_comms()
         dist.destroy_process_group()
     except Exception as ex:  # reported to the parent
         out["error"] = repr(ex)
@@ -79,6 +84,7 @@ def test_rccl_collectives_and_loop_world1():
     p.join(timeout=60)
     assert "error" not in out, out.get("error")
     assert out["backend"] == "nccl"
+    assert out["via"] == ["DeviceComm"]       # the C-ABI communicator carried the exchange
     dev, mi, ms = out["topk"]
     assert dev == "cuda" and mi == [2, 9, 5, -1] and ms[:3] == [7.0, 7.0, 3.0]
     si, rdev, rows, nd = out["sel"]

@@ -253,3 +253,20 @@ def test_scaled_kinds_pso_ga_legal():
         assert np.all((out[0] >= 1) & (out[0] <= 1000)) and np.all(out[0] == np.round(out[0]))
         assert np.all((out[1] >= 0) & (out[1] <= 1 << 30))
         assert np.all(np.frexp(out[2])[0] == 0.5) and np.all((out[2] >= 1) & (out[2] <= 1 << 20))
+
+
+def test_de_at_equals_vectorised():
+    """propose_de_at (the bench's parity check: only the members a trial reads)
+    equals the full vectorised round at those global indices, on the HPL-64
+    mixed space and a permutation space"""
+    from tests._spaces import oracle_space
+    from uptune_amd import spaces
+    for manip in (spaces.hpl64(), spaces.perm_mixed()):
+        space = oracle_space(manip)
+        npop, m = 300, 700
+        pop = ode.population_init(space, npop, 5)
+        full = ode.propose_de_vec(space, pop, 5, 3, 0, m, 0.2, 1)
+        g = np.array([0, 1, 299, 300, 301, 512, 699])
+        assert np.array_equal(ode.propose_de_at(space, g, npop, 5, 3, 0.2, 1), full[:, g])
+        mem = np.array([0, 1, 299, 7])
+        assert np.array_equal(ode.population_init(space, npop, 5, members=mem), pop[:, mem])

@@ -165,3 +165,25 @@ def test_round_failure_on_one_rank_is_collective():
     with round 3 -- nobody hangs in a collective the other rank skipped"""
     out = _spmd(_fail_worker)
     assert out[0][1] == out[1][1] == [False, True, False]
+
+
+def test_failed_async_fit_is_detected_and_refit(caplog):
+    """a GP fit enqueued without a host wait whose kernel matrix is
+    not positive definite must not poison later rounds silently: the next
+    round checks it (gp_fit_ok), logs, and refits with more jitter"""
+    import logging
+
+    from uptune_amd.driver import SearchDriver
+    mirror = _mirror()
+    # lengthscale 1e3, no noise, no jitter: K ~ all ones, singular
+    sm = T.SharedModel(seed=3, lengthscale=1e3, min_train=4, sigma_n2=0.0, jitter=0.0, engine_factory=OracleEngine)
+    de = T.GpuDifferentialEvolution(name="de", pool=256, batch=4, population=64, seed=3, shared=sm)
+    drv = SearchDriver(mirror, de, parallelism=4)
+    with caplog.at_level(logging.WARNING, logger="uptune_amd.technique"):
+        drv.main(_obj, test_limit=40, max_generations=10)
+    eng = drv.root_technique.model.engine     # the driver's (deep) copy of the technique
+    js = eng.calls["jitter"]
+    assert js[0] == 0.0 and max(js) >= 1e-8            # escalated after the failed fit
+    assert any("not positive definite" in r.message for r in caplog.records)
+    assert eng.gp_fit_ok()                             # the refit succeeded
+    assert drv.test_count >= 24                        # rounds kept producing configurations

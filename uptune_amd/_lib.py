@@ -15,13 +15,15 @@ LIB_PATH = os.environ.get("UTHOT_LIB", os.path.join(_HERE, "libuthot.so"))
 
 UT_FLOAT, UT_INT, UT_LOGINT, UT_POW2, UT_BOOL, UT_ENUM, UT_PERM = range(7)
 UT_ACQ_EI, UT_ACQ_UCB = 0, 1
+UT_RED_SUM, UT_RED_MAX, UT_RED_MIN = 0, 1, 2
+UT_COMM_ID_BYTES = 128
 # permutation crossover operators (op3_cross_*, manipulator.py:1179-1353)
 UT_X_NONE, UT_X_OX1, UT_X_OX3, UT_X_PX, UT_X_CX, UT_X_PMX = range(6)
 CROSSOVERS = {"op3_cross_OX1": UT_X_OX1, "op3_cross_OX3": UT_X_OX3, "op3_cross_PX": UT_X_PX,
               "op3_cross_CX": UT_X_CX, "op3_cross_PMX": UT_X_PMX}
 
 ERRORS = {
-    -1: "UT_EINVAL", -2: "UT_EHIP", -3: "UT_ENOSPACE", -4: "UT_EUNSUPPORTED", -5: "UT_ENOTPD", -6: "UT_ENOMEM",
+    -1: "UT_EINVAL", -2: "UT_EHIP", -3: "UT_ENOSPACE", -4: "UT_EUNSUPPORTED", -5: "UT_ENOTPD", -6: "UT_ENOMEM", -7: "UT_ECOMM",
 }
 
 
@@ -126,12 +128,23 @@ SIGNATURES = {
     "ut_gp_score": (C.c_int, [P, P, I64, I64, C.POINTER(Acq), P, P, P, P]),
     "ut_gp_score_values": (C.c_int, [P, P, I64, I64, C.POINTER(Acq), P, P, P, P]),
     "ut_gp_set_precision": (C.c_int, [P, I32]),
+    "ut_gp_fit_status": (C.c_int, [P, C.POINTER(I32)]),
     "ut_gp_stats": (C.c_int, [P, C.POINTER(D), C.POINTER(D), C.POINTER(D)]),
     "ut_topk": (C.c_int, [P, P, P, I64, I64, I32, P, P]),
     "ut_score_round_de": (C.c_int, [P, C.POINTER(DeParams), C.POINTER(Acq), U32, I64, I64, I32,
                                     C.POINTER(RoundOut)]),
     "ut_round_buffers": (C.c_int, [P, C.POINTER(P), C.POINTER(P), C.POINTER(P), C.POINTER(P), C.POINTER(P),
                                    C.POINTER(P), C.POINTER(P), C.POINTER(I64)]),
+    "ut_comm_unique_id": (C.c_int, [P]),
+    "ut_comm_init": (C.c_int, [P, I32, I32, P]),
+    "ut_comm_destroy": (C.c_int, [P]),
+    "ut_comm_info": (C.c_int, [P, C.POINTER(I32), C.POINTER(I32)]),
+    "ut_comm_allgather_topk": (C.c_int, [P, I32, P, P, P, P, I64, I32, P, P, P, P, I64]),
+    "ut_topk_merge": (C.c_int, [P, I64, I32, P, P, P, P, I64, I32, P, P, P, P, I64]),
+    "ut_comm_bcast_results": (C.c_int, [P, I32, I64, P, P, I64, C.POINTER(I64)]),
+    "ut_comm_bcast": (C.c_int, [P, P, I64, I32]),
+    "ut_comm_allreduce_f64": (C.c_int, [P, P, I64, I32]),
+    "ut_comm_barrier": (C.c_int, [P]),
     "ut_set_timing": (C.c_int, [P, I32]),
     "ut_stage_time": (C.c_int, [P, C.c_char_p, C.POINTER(D)]),
 }

@@ -26,8 +26,12 @@ HOSTLIB = os.path.join(HERE, "libuthot_hostcheck.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("UT_OFFLOAD_ARCH", "gfx950")
 
-SOURCES = ["api.hip", "propose.hip", "hash.hip", "dedup.hip", "gp.hip", "gp_gemm.hip", "topk.hip", "forest.hip"]
+SOURCES = ["api.hip", "propose.hip", "hash.hip", "dedup.hip", "gp.hip", "gp_gemm.hip", "topk.hip", "forest.hip", "comm.hip"]
 HEADERS = ["ut_core.h", "ut_internal.h", "ut_param.h", "ut_perm.h", "ryu_tables.h", "libm_log_data.h", os.path.join("..", "..", "include", "uthot.h")]
+
+# RCCL for the multi-GPU exchange (comm.hip); the soname (librccl.so.1) is the
+# one torch loads too, so a process that imported torch first shares its copy
+LINK_LIBS = ["-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib"]
 
 HIP_FLAGS = [
     "-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}",
@@ -72,7 +76,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
         objs = list(ex.map(lambda s: _compile(s, force), SOURCES))
     if force or _mtime(LIB) < max(_mtime(o) for o in objs):
         tmp = LIB + ".tmp"
-        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", tmp]
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", tmp, *LINK_LIBS]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")

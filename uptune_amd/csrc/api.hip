@@ -200,6 +200,7 @@ int ut_ctx_destroy(ut_ctx* c) {
   if (!c) return UT_EINVAL;
   hipSetDevice(c->device);
   if (c->stream) ut::sync_all(c);
+  ut::comm_release(c);
   free_space(c->space);
   auto fr = [](void* p) { if (p) hipFree(p); };
   fr(c->pop); fr(c->pso_vel); fr(c->pso_best);
@@ -222,6 +223,7 @@ int ut_ctx_destroy(ut_ctx* c) {
   fr(c->r_dup.p); fr(c->tk_score[0].p); fr(c->tk_score[1].p); fr(c->tk_idx[0].p); fr(c->tk_idx[1].p);
   fr(c->r_topk_idx.p); fr(c->r_topk_score.p); fr(c->perm_ws.p); fr(c->perm_dig.p);
   fr(c->forest_nodes); fr(c->forest_roots); fr(c->r_topk_vals.p);
+  fr(c->cm_send.p); fr(c->cm_recv.p); fr(c->cm_keep.p); fr(c->cm_pay.p); fr(c->cm_cnt.p);
   for (auto& m : c->timing.marks) hipEventDestroy(m.ev);
   for (hipEvent_t e : {c->ev_fork, c->ev_join, c->ev_fit, c->ev_prefit, c->ev_fit_x})
     if (e) hipEventDestroy(e);
@@ -698,6 +700,15 @@ int ut_gp_set_precision(ut_ctx* c, int32_t bits) {
   if (!c) return UT_EINVAL;
   UT_CHECK(c, bits == 64 || bits == 32 || bits == 16, UT_EINVAL, "gp precision must be 64, 32 or 16 (f16x3)");
   c->gp_prec = bits;
+  return 0;
+}
+
+int ut_gp_fit_status(ut_ctx* c, int32_t* ok) {
+  if (!c || !ok) return UT_EINVAL;
+  UT_CHECK(c, c->gp_ready || c->fit_pending, UT_EINVAL, "gp_fit_status: no fit");
+  const int rc = gp_wait_fit(c);
+  if (rc != 0 && rc != UT_ENOTPD) return rc;
+  *ok = rc == 0 ? 1 : 0;
   return 0;
 }
 

@@ -287,6 +287,15 @@ struct ut_ctx {
   int32_t forest_trees = 0, forest_rule = 0;
   double forest_base = 0.0, forest_scale = 1.0, forest_div = 1.0;
 
+  // multi-GPU exchange (comm.hip): the RCCL communicator of this context's
+  // rank and the packed top-k records of the all-gather / merge
+  void* comm = nullptr;               // ncclComm_t
+  int32_t comm_rank = 0, comm_size = 1;
+  ut::DevBuf<uint64_t> cm_send, cm_recv;   // [k][W] / [R k][W] records (W = 6 + payload columns)
+  ut::DevBuf<uint8_t> cm_keep;             // [R k] record survives the digest dedup
+  ut::DevBuf<double> cm_pay;               // [n][5] broadcast payload (value + digest)
+  ut::DevBuf<int64_t> cm_cnt;              // [1] broadcast count
+
   ut::Timing timing;
 };
 
@@ -425,6 +434,8 @@ constexpr int VAR_BM = 128, VAR_BN = 256;  // variance-contraction tile (rows of
 int launch_to_f32(ut_ctx* c, const double* src, float* dst, int64_t n);
 int launch_gather_rows(ut_ctx* c, const double* values, int64_t ld, const int64_t* idx, int64_t cand_base,
                        int32_t k, double* out, int64_t ldo, const uint32_t* dig, uint32_t* out_dig);
+// comm.hip: release the context's communicator (ut_ctx_destroy)
+void comm_release(ut_ctx* c);
 
 inline unsigned grid1(int64_t n, int bs) { return (unsigned)((n + bs - 1) / bs); }
 

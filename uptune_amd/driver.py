@@ -161,7 +161,11 @@ class SearchDriver:
     def configuration_from_digest(self, cfg, hashv: str) -> Configuration:
         """get_configuration for a config whose hash_config digest the device
         already computed (the GPU techniques hand their selections over this
-        way, so a request costs no second hash)"""
+        way, so a request costs no second hash).  A driver built with a custom
+        hash_fn keys every configuration by it, so the digest is not used then
+        (one Configuration row per configuration, whoever requests it)."""
+        if self._hash_fn is not None:
+            return self.get_configuration(cfg)
         return self._intern(cfg, hashv)
 
     def has_results(self, config) -> bool:
@@ -376,16 +380,12 @@ class TuningRunManager:
 # SPMD over torch.distributed
 # ---------------------------------------------------------------------------
 def agree(ok: bool, group=None, device=None) -> bool:
-    """True iff every rank of the group passes ok=True (one all_reduce MIN).
+    """True iff every rank of the group passes ok=True (dist.agree: one
+    all-reduce MIN over this rank's RCCL communicator, or gloo on the CPU).
     Every rank takes the same branch afterwards, so a failure on one rank
     never leaves the others waiting inside a later collective."""
-    import torch
-    import torch.distributed as dist
-    from .dist import _comm_device
-    cd = _comm_device(group, device if device is not None else torch.device("cpu"))
-    t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=cd)
-    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
-    return bool(int(t.item()))
+    from .dist import agree as _agree
+    return _agree(ok, group, device)
 
 
 class DistributedSearchDriver(SearchDriver):

@@ -284,6 +284,13 @@ class BatchEngine:
         fn = self.lib.ut_gp_fit if wait else self.lib.ut_gp_fit_async
         L.check(self.ctx, fn(self.ctx, X.ctypes.data, y.ctypes.data, n, d, C.byref(h)), "ut_gp_fit")
 
+    def gp_fit_ok(self) -> bool:
+        """ut_gp_fit_status: waits for the last fit; False = its kernel matrix
+        was not positive definite (scores are NaN until a fit succeeds)"""
+        ok = C.c_int32()
+        L.check(self.ctx, self.lib.ut_gp_fit_status(self.ctx, C.byref(ok)), "ut_gp_fit_status")
+        return bool(ok.value)
+
     def gp_set_fit_append(self, enable: bool):
         """incremental fits when the training set only grows (on by default)"""
         L.check(self.ctx, self.lib.ut_gp_set_fit_append(self.ctx, int(bool(enable))), "ut_gp_set_fit_append")

@@ -292,6 +292,7 @@ class SharedModel:
         self._X = None
         self._y: List[float] = []
         self._fit_key = None
+        self._fit_unverified = False
         self.fits = 0
         # list drivers (append-only results table): the usable rows found so
         # far and how far the table has been scanned
@@ -367,6 +368,16 @@ class SharedModel:
             ids = [getattr(r, "id", i) for i, r in enumerate(rows)]
         if len(rows) < self.min_train:
             return False
+        if self._fit_unverified and self._fit_key is not None:
+            # the previous fit ran asynchronously (no host wait when it was
+            # enqueued): a kernel matrix that was not positive definite would
+            # leave every score NaN, so check it once, before reusing it
+            self._fit_unverified = False
+            if not self.engine.gp_fit_ok():
+                self.hyper["jitter"] = max(10.0 * self.hyper.get("jitter", 0.0), 1e-8)
+                log.warning("GP fit on %d results was not positive definite: refitting with jitter %g",
+                            self._fit_key[0], self.hyper["jitter"])
+                self._fit_key = None
         key = (len(rows), ids[-1])
         if key == self._fit_key:
             return True
@@ -380,6 +391,7 @@ class SharedModel:
             self._res_ids = list(ids)   # a copy: the scan list keeps growing
         self.engine.gp_fit(self._X, np.asarray(self._y), lengthscale=self.lengthscale, wait=False, **self.hyper)
         self._fit_key = key
+        self._fit_unverified = True
         self.fits += 1
         return True
 
@@ -400,7 +412,7 @@ class GpuBatchTechnique(SearchTechnique):
     def __init__(self, pool: int = 1 << 14, batch: int = 8, population: int = 1024, device: int = 0,
                  seed: int = 0, lengthscale: float = 0.3, min_train: int = 4, acq: str = "ei",
                  group=None, surrogate=None, shared: Optional[SharedModel] = None, engine_factory=None,
-                 prune_rows: int = 0, *pargs, **kwargs):
+                 prune_rows: int = 0, precision: int = 64, *pargs, **kwargs):
         super().__init__(*pargs, **kwargs)
         # prune_rows > 0: score rounds with ut_gp_topk_pruned (selection-exact EI
         # bound from the first prune_rows rows of L^-1 k*; fp64 fits, EI / UCB):
@@ -412,8 +424,11 @@ class GpuBatchTechnique(SearchTechnique):
         # forest.Forest) ranking candidates by predicted objective (minimised),
         # the multi-stage tuner's model scoring (multi_stage.py:8-22, :109-123)
         self.surrogate = surrogate
+        # precision: the GP contractions of a private model (64 / 32 / 16 = f16x3);
+        # a shared model (the bandit's) carries its own
         self.model = shared if shared is not None else SharedModel(device=device, seed=seed,
                                                                    lengthscale=lengthscale, min_train=min_train,
+                                                                   precision=precision,
                                                                    engine_factory=engine_factory)
         # multi-GPU: with torch.distributed initialised and
         # world > 1, rank r scores candidates [base + r*pool, base + (r+1)*pool)
@@ -520,7 +535,10 @@ class GpuBatchTechnique(SearchTechnique):
                 vals, idx, top, dig, rows = self._local_round()
             except Exception as ex:   # noqa: BLE001 -- re-raised below on every rank
                 err = ex
-            dev = None if err is not None else idx.device
+            # the vote travels on the technique's GPU whether or not the round
+            # failed (a failed rank must use the same communicator as the others)
+            import torch
+            dev = idx.device if err is None else torch.device("cuda", self.model.device)
             if not agree(err is None, self.group, dev):
                 raise RuntimeError(f"{self.name}: scoring round failed on "
                                    f"{'this rank: ' + repr(err) if err is not None else 'another rank'}")
@@ -659,7 +677,7 @@ class GpuGGA(GpuGA):
 
 def _shared_model(kw) -> SharedModel:
     return SharedModel(device=kw.get("device", 0), seed=kw.get("seed", 0), lengthscale=kw.get("lengthscale", 0.3),
-                       min_train=kw.get("min_train", 4), precision=kw.pop("precision", 64),
+                       min_train=kw.get("min_train", 4), precision=kw.get("precision", 64),
                        engine_factory=kw.pop("engine_factory", None))
 
 
@@ -706,7 +724,8 @@ def reference_registry(wrap=None, bandit_cls=None, **kw) -> List[SearchTechnique
     W = wrap or (lambda c: c)
     kw = dict(kw)
     ef = kw.get("engine_factory")
-    sm = _shared_model(kw)          # the bandit's children share one model (pops precision / engine_factory)
+    sm = _shared_model(kw)          # the bandit's children share one model (pops engine_factory; every
+    #                                 technique, stand-alone or not, gets the requested precision)
     if ef is not None:
         kw["engine_factory"] = ef   # ... while each stand-alone technique builds its own
     DE, PSO, GA, GGA = W(GpuDifferentialEvolution), W(GpuPSO), W(GpuGA), W(GpuGGA)
