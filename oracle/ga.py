@@ -73,10 +73,12 @@ def _perm_rand(S, seed, g, stream, round_, op):
 
 def propose_ga_vec(space, parent1, parent2, seed, round_, cand_base, m, mutation_rate=0.1, must_mutate_count=1,
                    normal=False, sigma=0.1, crossover_rate=0.0, crossover_strength=0.0, max_retries=10,
-                   op=ph.OP_GA, crossover=pm.X_NONE):
+                   op=ph.OP_GA, crossover=pm.X_NONE, g=None):
+    """g: explicit global candidate indices (then cand_base / m are ignored)"""
     P = len(space)
     starts, nc = columns(space)
-    g = np.arange(cand_base, cand_base + m, dtype=np.uint64)
+    g = np.arange(cand_base, cand_base + m, dtype=np.uint64) if g is None else np.asarray(g, dtype=np.uint64)
+    m = g.size
     x, y, _, _ = ph.draw(seed, g, ph.STREAM_CAND | 0, round_, op)
     two = ph.u01(x, y) < crossover_rate
     P1 = np.empty((nc, m))
