@@ -220,8 +220,10 @@ class SearchDriver:
             self.report(dr, t)
         self.process_new_results()
 
-    def seed_results(self, cfgs, evaluate) -> None:
-        self.record_seed(cfgs, [evaluate(c) for c in cfgs])
+    def seed_results(self, cfgs, evaluate, keys=None) -> None:
+        """evaluate an initial design and record it (keys: the configurations'
+        hash_config digests when the caller already has them)"""
+        self.record_seed(cfgs, [evaluate(c) for c in cfgs], keys)
 
     # -- generation loop ---------------------------------------------------
     def _add_request(self, dr: DesiredResult) -> DesiredResult:
@@ -429,10 +431,10 @@ class DistributedSearchDriver(SearchDriver):
                                f"{self.src} (this rank {'agrees' if same else 'differs'})")
         return y.cpu().tolist()
 
-    def seed_results(self, cfgs, evaluate) -> None:
+    def seed_results(self, cfgs, evaluate, keys=None) -> None:
         """rank `src` evaluates the initial design; values + digests are broadcast"""
         import torch.distributed as dist
-        keys = self.config_keys(cfgs)
+        keys = keys if keys is not None else self.config_keys(cfgs)
         src = dist.get_rank(self.group) == self.src
         y = self._exchange(keys, [evaluate(c) for c in cfgs] if src else None)
         self.record_seed(cfgs, y, keys)

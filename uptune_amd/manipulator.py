@@ -27,6 +27,7 @@ from __future__ import annotations
 
 import hashlib
 import math
+import operator
 from dataclasses import dataclass, field
 from typing import Any, Dict, List, Sequence
 
@@ -269,27 +270,63 @@ class SpaceSpec:
         return [p.name for p in self.params]
 
     def encode_configs(self, cfgs: Sequence[Dict[Any, Any]]) -> np.ndarray:
-        """configs -> SoA [ncols][n] float64"""
-        # columns are laid out in parameter order (compile_space): one Python
-        # row per config, one array conversion (per-element numpy stores cost
-        # ~0.4 s for a 4096 x 64 seed design)
-        ps_list = self.params
-        rows = []
-        for cfg in cfgs:
-            row = []
-            for ps in ps_list:
-                row.extend(ps.to_columns(cfg[ps.name]))
-            rows.append(row)
-        out = np.empty((self.ncols, len(rows)), dtype=np.float64)   # canonical strides (ld = n)
-        if rows:
-            out[:] = np.array(rows, dtype=np.float64).T
+        """configs -> SoA [ncols][n] float64 (ParamSpec.to_columns, column by
+        column: one C-level conversion per parameter instead of one Python call
+        per value -- a 4096 x 64 seed design in ~10 ms instead of ~0.2 s)"""
+        n = len(cfgs)
+        out = np.empty((self.ncols, n), dtype=np.float64)   # canonical strides (ld = n)
+        if n == 0:
+            return out
+        # rows of values in parameter order, transposed to columns (C-level loops)
+        get = operator.itemgetter(*self.names())
+        cols = list(zip(*map(get, cfgs))) if self.P > 1 else [tuple(map(get, cfgs))]
+        for ps, col in zip(self.params, cols):
+            c0 = ps.col
+            if ps.kind == L.UT_FLOAT:
+                out[c0] = np.fromiter(map(float, col), dtype=np.float64, count=n)
+            elif ps.kind in (L.UT_INT, L.UT_LOGINT, L.UT_POW2):
+                out[c0] = np.fromiter(map(int, col), dtype=np.int64, count=n)
+            elif ps.kind == L.UT_BOOL:
+                out[c0] = np.fromiter(map(bool, col), dtype=bool, count=n)
+            elif ps.kind == L.UT_ENUM:
+                out[c0] = _enum_indices(ps.options, col)
+            else:   # PERM: a value per item
+                for j, v in enumerate(col):
+                    out[c0:c0 + ps.width, j] = ps.to_columns(v)
         return out
 
     def decode_values(self, values: np.ndarray) -> List[Dict[Any, Any]]:
-        """SoA [ncols][n] -> configs"""
-        rows = np.ascontiguousarray(np.asarray(values, dtype=np.float64).T).tolist()
-        named = [(ps.name, ps, ps.col, ps.col + ps.width) for ps in self.params]
-        return [{name: ps.from_columns(r[a:b]) for name, ps, a, b in named} for r in rows]
+        """SoA [ncols][n] -> configs (ParamSpec.from_columns, column by column)"""
+        v = np.asarray(values, dtype=np.float64)
+        cols = []
+        for ps in self.params:
+            x = v[ps.col]
+            if ps.kind == L.UT_FLOAT:
+                cols.append(x.tolist())
+            elif ps.kind in (L.UT_INT, L.UT_LOGINT, L.UT_POW2):
+                cols.append(x.astype(np.int64).tolist())
+            elif ps.kind == L.UT_BOOL:
+                cols.append((x != 0.0).tolist())
+            elif ps.kind == L.UT_ENUM:
+                opts = ps.options
+                cols.append([opts[i] for i in x.astype(np.int64).tolist()])
+            else:
+                cols.append([ps.from_columns(r) for r in v[ps.col:ps.col + ps.width].T.tolist()])
+        names = self.names()
+        return [dict(zip(names, vals)) for vals in zip(*cols)]
+
+
+def _enum_indices(options, col) -> np.ndarray:
+    """[options.index(v) for v in col]: one C-level dict lookup per value when
+    every option and value is hashable (first occurrence, the same equality),
+    else the list method (which raises ValueError for an unknown value)"""
+    try:
+        d = {}
+        for i, o in enumerate(options):
+            d.setdefault(o, i)
+        return np.fromiter(map(d.__getitem__, col), dtype=np.int64, count=len(col))
+    except (KeyError, TypeError):
+        return np.fromiter(map(options.index, col), dtype=np.int64, count=len(col))
 
 
 def unit_bounds(kind: int, lo, hi):

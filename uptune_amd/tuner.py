@@ -19,13 +19,17 @@ from .driver import DistributedSearchDriver, SearchDriver
 from .technique import pso_ga_de_bandit
 
 
-def random_configs(manipulator, n: int, seed: int, device: int = 0):
-    """n configurations drawn by op1_randomize on the device (manipulator.random())"""
-    from .engine import BatchEngine
+def random_configs(manipulator, n: int, seed: int, device: int = 0, with_keys: bool = False):
+    """n configurations drawn by op1_randomize on the device (manipulator.random());
+    with_keys: also their hash_config hex digests, hashed on the device from the
+    drawn values (no host re-encoding)"""
+    from .engine import BatchEngine, digests_to_hex
     eng = BatchEngine(manipulator, device=device, seed=seed)
     try:
         eng.population_init(max(n, 4), round_=0)
-        return eng.decode(eng.population_get()[:, :n])
+        vals = eng.population_get()[:, :n].contiguous()
+        cfgs = eng.decode(vals)
+        return (cfgs, digests_to_hex(eng.hash(vals))) if with_keys else cfgs
     finally:
         eng.close()
 
@@ -52,7 +56,8 @@ def tune_bandit(manipulator, objective: Callable[[Dict[Any, Any]], float], gener
     import time
     t0 = time.perf_counter()
     if n_init:
-        drv.seed_results(random_configs(manipulator, n_init, seed + 7919, device), objective)
+        cfgs, keys = random_configs(manipulator, n_init, seed + 7919, device, with_keys=True)
+        drv.seed_results(cfgs, objective, keys=keys)
     drv.seed_s = time.perf_counter() - t0    # initial design: draw, evaluate, record (host)
     drv.main(objective, test_limit=generations * parallelism, max_generations=generations)
     return drv
