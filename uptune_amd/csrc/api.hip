@@ -189,9 +189,11 @@ int ut_ctx_create(int device, uint64_t seed, ut_ctx** out) {
   if (const char* e = getenv("UT_JOIN_BEFORE_VAR")) c->join_before_var = atoi(e) != 0;
   if (const char* e = getenv("UT_VAR_KERNEL")) c->var_kernel = atoi(e);
   if (const char* e = getenv("UT_VAR_SPLIT")) c->var_split = atoi(e) != 0;
+  if (const char* e = getenv("UT_H3_KERNEL")) c->h3_kernel = atoi(e);
   if (const char* e = getenv("UT_FIT_APPEND")) c->fit_append = atoi(e) != 0;
   if (const char* e = getenv("UT_DE_AOS")) c->de_aos = atoi(e) != 0;
   if (const char* e = getenv("UT_HASH_AFTER_FIT")) c->hash_after_fit = atoi(e);
+  if (const char* e = getenv("UT_HASH_HOLD_LOWPREC")) c->hash_hold_lowprec = atoi(e) != 0;
   *out = c;
   return 0;
 }
@@ -784,7 +786,7 @@ static int score_round_de_impl(ut_ctx* c, const ut_de_params* de, const ut_acq* 
   {
     StreamScope on_side(c, c->side);
     mark(c, "");
-    c->round_hash_hold = (prune_rows == 0 && c->gp_fit_prec == 64) ? c->hash_after_fit : 0;
+    c->round_hash_hold = (prune_rows == 0 && (c->gp_fit_prec == 64 || c->hash_hold_lowprec)) ? c->hash_after_fit : 0;
     rc = launch_hash_de(c, c->r_values.p, ld, m, cand_base, c->r_digest.p, true);
     c->round_hash_hold = 0;
     if (rc) return rc;

@@ -806,15 +806,17 @@ __global__ __launch_bounds__(1024) void k_var_split_red(const double* __restrict
 // LDS image: 64-B operand rows, 16-B chunk c of row r at position c ^ ((r>>2)&3):
 // conflict-free for the ds_read_b128 lane groups of the 32x32x16 fragments.
 // ---------------------------------------------------------------------------
-// H3Cfg<BK, NS>: BK k per stage (64-B or 32-B operand rows), NS ring slots;
-// NS - 2 stages stay in flight behind the one being consumed.
-template <int BK, int NS>
+// H3Cfg<BK, NS, BN>: BK k per stage (64-, 32- or 16-B... operand rows of BK
+// fp16), NS ring slots (NS - 2 stages stay in flight behind the one being
+// consumed), BN candidates per tile.
+template <int BK, int NS, int BN = VAR_BN>
 struct H3Cfg {
-  static constexpr int SA = VAR_BM * BK, SB = VAR_BN * BK;  // fp16 elements per plane
+  static constexpr int SA = VAR_BM * BK, SB = BN * BK;  // fp16 elements per plane
   static constexpr int STAGE = 2 * SA + 2 * SB;
-  static constexpr int CH = BK / 8;                          // 16-B chunks per operand row
-  static constexpr int RPI = 64 / CH;                        // operand rows per glds wave-instruction
-  static constexpr int PER_WAVE = 2 * (VAR_BM + VAR_BN) / RPI / 8;  // glds per wave per stage
+  static constexpr int CH = BK / 8;                     // 16-B chunks per operand row
+  static constexpr int RPI = 64 / CH;                   // operand rows per glds wave-instruction
+  template <int NI>
+  static constexpr int per_wave() { return 2 * (VAR_BM + BN) / RPI / NI; }  // glds per wave per stage, NI waves
   // conflict-free position of chunk c in row r for the ds_read_b128 groups
   static __device__ __forceinline__ int swz(int r, int c) {
     return BK == 32 ? c ^ ((r >> 2) & 3) : c ^ ((r >> 3) & 1);
@@ -833,20 +835,25 @@ template <int BK, int NS>
 __device__ __forceinline__ void h3_glds(const _Float16* __restrict__ src, int64_t ld, int32_t rb, int32_t k0,
                                         _Float16* plane, int lane) {
   using C = H3Cfg<BK, NS>;
-  const int r = rb + lane / C::CH;
-  const int ch = C::swz(r, lane % C::CH);  // data chunk held by this lane's LDS slot (swz is an involution)
-  __builtin_amdgcn_global_load_lds(src + (int64_t)r * ld + k0 + ch * 8,
-                                   (__attribute__((address_space(3))) void*)(plane + rb * BK), 16, 0, 0);
+  const int rl = lane / C::CH;
+  const int ch = C::swz(rb + rl, lane % C::CH);  // data chunk held by this lane's LDS slot (swz is an involution)
+  // a wave-uniform 64-bit base and a 32-bit lane offset (SGPR base + VGPR
+  // offset addressing; rb is a multiple of RPI, so the offset is the same in
+  // every call and no per-instruction 64-bit address stays live in VGPRs)
+  const _Float16* base = src + (int64_t)rb * ld + k0;
+  const uint32_t loff = (uint32_t)rl * (uint32_t)ld + (uint32_t)(ch * 8);
+  __builtin_amdgcn_global_load_lds(base + loff, (__attribute__((address_space(3))) void*)(plane + rb * BK), 16, 0, 0);
 }
 
 // PART: 3 = the whole stage, 1 = its A planes only, 2 = its B planes only
-template <int BK, int NS, int NW, int PART = 3>
+template <int BK, int NS, int NW, int BN, int PART = 3>
 __device__ __forceinline__ void h3_issue(const _Float16* __restrict__ A, int64_t a_lo, const _Float16* __restrict__ B,
                                          int64_t b_lo, int64_t ld, int32_t k0, _Float16* st, int w, int lane) {
   // A / B already at row0 / col0.  Per wave: A rows [w*128/NW, +128/NW) of each plane,
-  // B rows [w*256/NW, +256/NW) of each plane, RPI rows per instruction.
-  using C = H3Cfg<BK, NS>;
-  constexpr int AR = VAR_BM / NW, BR = VAR_BN / NW;  // rows per wave
+  // B rows [w*BN/NW, +BN/NW) of each plane, RPI rows per instruction.
+  using C = H3Cfg<BK, NS, BN>;
+  constexpr int AR = VAR_BM / NW, BR = BN / NW;  // rows per wave
+  static_assert(BR % C::RPI == 0, "B rows per wave");
   if constexpr (!(PART & 1)) {
   } else if constexpr (AR >= C::RPI) {
 #pragma unroll
@@ -872,20 +879,22 @@ __device__ __forceinline__ vh8 h3_frag(const _Float16* plane, int r, int c) {
 
 // mid(): called between the first and second k16 sub-steps (the B half of the
 // next stage's glds goes there, behind this stage's first MFMAs)
-template <int BK, int NS, int JB, class Mid>
+template <int BK, int NS, int JB, int BN, class Mid>
 __device__ __forceinline__ void var_step_h3(const _Float16* st, int wm, int wn, int lane, int imin,
                                             vf16 (&acc)[2][JB], Mid&& mid) {
-  using C = H3Cfg<BK, NS>;
+  using C = H3Cfg<BK, NS, BN>;
   const _Float16* ah = st;
   const _Float16* al = st + C::SA;
   const _Float16* bh = st + 2 * C::SA;
   const _Float16* bl = bh + C::SB;
 #pragma unroll
   for (int s = 0; s < BK / 16; ++s) {
-    if (s == 1) {
-      __builtin_amdgcn_sched_barrier(0);
-      mid();
-      __builtin_amdgcn_sched_barrier(0);
+    if (s == (BK / 16 > 1 ? 1 : 0)) {
+      if constexpr (BK / 16 > 1) {
+        __builtin_amdgcn_sched_barrier(0);
+        mid();
+        __builtin_amdgcn_sched_barrier(0);
+      }
     }
     const int c = 2 * s + (lane >> 5);
     vh8 fbh[JB], fbl[JB];
@@ -914,19 +923,24 @@ __device__ __forceinline__ int h3_linv_exp(const unsigned long long* amax_bits) 
   return H3_KSCALE_EXP - ilogb(__longlong_as_double((long long)*amax_bits));
 }
 
-// NW = 8: one 512-thread workgroup per CU, waves 2 x 4 of 64 x 64;
-// NW = 4: 256-thread workgroups, waves 2 x 2 of 64 x 128, two per CU (their
-// barriers do not align, so one's glds issue and barrier overlap the other's MFMAs)
-template <int BK, int NS, int NW>
+// Tiles of 128 rows of L^-1 x BN candidates, waves 2 x NW/2 of 64 x (2 BN / NW).
+//   NW = 8, BN = 256: one 512-thread workgroup per CU (144 KiB ring), the default;
+//   NW = 4, BN = 128: two 256-thread workgroups per CU (64 KiB ring each), whose
+//     barriers do not align, so one's barrier wait and pipeline fill overlap the
+//     other's MFMAs -- the fp64 k_gp_var_pp arrangement.  The XCD's 64 resident
+//     workgroups then cover two 128-wide strips, the same 4 MiB of K* in its L2
+//     as one 256-wide strip (UT_H3_KERNEL=1 / 2: BK 32 x 2 slots / BK 16 x 4 slots).
+template <int BK, int NS, int NW, int BN>
 __global__ __launch_bounds__(NW * 64, 8 / NW) void k_gp_var_h3(const _Float16* __restrict__ A, int64_t a_lo,
                                                         const _Float16* __restrict__ B, int64_t b_lo, int64_t ld,
                                                         int32_t K, int32_t RT, int32_t CT, int64_t m,
                                                         int32_t* __restrict__ ticket, double* __restrict__ part,
                                                         int64_t ldp, const unsigned long long* __restrict__ amax_bits,
                                                         int32_t kexp) {
-  using C = H3Cfg<BK, NS>;
+  using C = H3Cfg<BK, NS, BN>;
   static_assert(NS * C::STAGE * 2 <= (160 * 1024 - 128) / (8 / NW), "LDS");
-  constexpr int JB = VAR_BN / (NW / 2) / 32;  // 32-column blocks per wave
+  static_assert(NS * C::STAGE * 2 >= 2 * BN * 8, "epilogue reduction buffer");
+  constexpr int JB = BN / (NW / 2) / 32;  // 32-column blocks per wave
   __shared__ __attribute__((aligned(16))) _Float16 lds[NS * C::STAGE + 8];
   int32_t& s_item = *reinterpret_cast<int32_t*>(lds + NS * C::STAGE);
   const int t = threadIdx.x, lane = t & 63;
@@ -942,7 +956,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void k_gp_var_h3(const _Float16* _
     const int32_t ct = (j / RT) * 8 + xcd;
     if (ct >= CT) break;
     const int32_t rt = RT - 1 - (j % RT);
-    const int64_t col0 = (int64_t)ct * VAR_BN;
+    const int64_t col0 = (int64_t)ct * BN;
     const int32_t row0 = rt * VAR_BM;
     const int32_t nk = min(K, row0 + VAR_BM) / BK;
     const _Float16* At = A + (int64_t)row0 * ld;
@@ -959,43 +973,44 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void k_gp_var_h3(const _Float16* _
     // prologue: stages 0 .. NS-2 in flight (nk >= 4 always: K and row0 + 128 are multiples of 128)
 #pragma unroll
     for (int q = 0; q < NS - 1; ++q)
-      if (q < nk) h3_issue<BK, NS, NW>(At, a_lo, Bt, b_lo, ld, q * BK, lds + q * C::STAGE, w, lane);
+      if (q < nk) h3_issue<BK, NS, NW, BN>(At, a_lo, Bt, b_lo, ld, q * BK, lds + q * C::STAGE, w, lane);
     // retire stage kt (NS - 2 younger stages may stay in flight), then refill
-    // the slot of stage kt - 1 with stage kt + NS - 1
-    // the refill of stage kt + NS - 1 is split: A planes right after the
-    // barrier, B planes between the stage's two k16 sub-steps (spreads the glds
-    // issue cost over the MFMAs; the vmcnt count per stage is unchanged)
+    // the slot of stage kt - 1 with stage kt + NS - 1.  With two k16 sub-steps
+    // per stage the refill is split: A planes right after the barrier, B planes
+    // between the sub-steps (spreads the glds issue cost over the MFMAs; the
+    // vmcnt count per stage is unchanged); with one it is issued whole.
+    constexpr bool SPLIT = BK / 16 > 1;
     auto pipe = [&](int32_t kt) -> const _Float16* {
       if (kt + NS - 2 < nk)
-        wait_vmcnt<C::PER_WAVE * (NS - 2)>();
+        wait_vmcnt<C::template per_wave<NW>() * (NS - 2)>();
       else
         wait_vmcnt<0>();
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
       if (kt + NS - 1 < nk)
-        h3_issue<BK, NS, NW, 1>(At, a_lo, Bt, b_lo, ld, (kt + NS - 1) * BK, lds + ((kt + NS - 1) % NS) * C::STAGE, w,
-                                lane);
+        h3_issue<BK, NS, NW, BN, (SPLIT ? 1 : 3)>(At, a_lo, Bt, b_lo, ld, (kt + NS - 1) * BK,
+                                                 lds + ((kt + NS - 1) % NS) * C::STAGE, w, lane);
       return lds + (kt % NS) * C::STAGE;
     };
     auto refill_b = [&](int32_t kt) {
       return [&, kt]() {
-        if (kt + NS - 1 < nk)
-          h3_issue<BK, NS, NW, 2>(At, a_lo, Bt, b_lo, ld, (kt + NS - 1) * BK, lds + ((kt + NS - 1) % NS) * C::STAGE,
-                                  w, lane);
+        if (SPLIT && kt + NS - 1 < nk)
+          h3_issue<BK, NS, NW, BN, 2>(At, a_lo, Bt, b_lo, ld, (kt + NS - 1) * BK,
+                                      lds + ((kt + NS - 1) % NS) * C::STAGE, w, lane);
       };
     };
     const int32_t nfull = min(nk, row0 / BK);
-    for (int32_t kt = 0; kt < nfull; ++kt) var_step_h3<BK, NS, JB>(pipe(kt), wm, wn, lane, 0, acc, refill_b(kt));
+    for (int32_t kt = 0; kt < nfull; ++kt) var_step_h3<BK, NS, JB, BN>(pipe(kt), wm, wn, lane, 0, acc, refill_b(kt));
     for (int32_t kt = nfull; kt < nk; ++kt) {
       const _Float16* st = pipe(kt);
       const int kd = ((kt - nfull) * BK) / 32 - 2 * wm;  // 32-row blocks of this wave entirely above the diagonal
       const int imin = kd < 0 ? 0 : kd;
-      if (imin < 2) var_step_h3<BK, NS, JB>(st, wm, wn, lane, imin, acc, refill_b(kt));
+      if (imin < 2) var_step_h3<BK, NS, JB, BN>(st, wm, wn, lane, imin, acc, refill_b(kt));
       else refill_b(kt)();
     }
 
     __syncthreads();
-    double* red = reinterpret_cast<double*>(lds);  // [2][256]
+    double* red = reinterpret_cast<double*>(lds);  // [2][BN]
 #pragma unroll
     for (int jj = 0; jj < JB; ++jj) {
       const int cl = wn * (32 * JB) + jj * 32 + (lane & 31);
@@ -1005,12 +1020,12 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void k_gp_var_h3(const _Float16* _
 #pragma unroll
         for (int r = 0; r < 16; ++r) s += (double)acc[i][jj][r] * (double)acc[i][jj][r];
       s += __shfl_xor(s, 32);
-      if ((lane >> 5) == 0) red[wm * VAR_BN + cl] = s;
+      if ((lane >> 5) == 0) red[wm * BN + cl] = s;
     }
     __syncthreads();
-    for (int u = t; u < VAR_BN; u += NW * 64) {
+    for (int u = t; u < BN; u += NW * 64) {
       const int64_t col = col0 + u;
-      if (col < m) part[(int64_t)rt * ldp + col] = (red[u] + red[VAR_BN + u]) * unscale2;
+      if (col < m) part[(int64_t)rt * ldp + col] = (red[u] + red[BN + u]) * unscale2;
     }
   }
 }
@@ -1071,10 +1086,25 @@ int launch_gemm_var(ut_ctx* c, int prec, const void* LinvT, int64_t lda, const v
     // slower: 16 k x 6 slots (C3 var 95.8 -> 118.5 ms: twice the barriers per
     // flop) and two 4-wave workgroups per CU (C3 var 96.7 -> 164.0 ms: two
     // K* strips per XCD no longer fit its L2)
-    hipLaunchKernelGGL((k_gp_var_h3<32, 3, 8>), dim3(nb), dim3(V_NT), 0, c->stream, (const _Float16*)LinvT,
-                       lda * (int64_t)npad,
-                       (const _Float16*)kst, ldk * (int64_t)npad, (int64_t)npad, npad, RT, CT, m, c->gp_ctr, part, ldk,
-                       reinterpret_cast<const unsigned long long*>(c->gp_ctr + 16), h3_kstar_exp(c->gp_sf2));
+    const _Float16* Ah = (const _Float16*)LinvT;
+    const _Float16* Bh = (const _Float16*)kst;
+    const unsigned long long* amax = reinterpret_cast<const unsigned long long*>(c->gp_ctr + 16);
+    const int32_t kx = h3_kstar_exp(c->gp_sf2);
+    if (c->h3_kernel == 0) {
+      hipLaunchKernelGGL((k_gp_var_h3<32, 3, 8, 256>), dim3(nb), dim3(V_NT), 0, c->stream, Ah, lda * (int64_t)npad,
+                         Bh, ldk * (int64_t)npad, (int64_t)npad, npad, RT, CT, m, c->gp_ctr, part, ldk, amax, kx);
+    } else {   // two 4-wave workgroups per CU on 128-candidate strips
+      const int32_t CT2 = (int32_t)((m + 127) / 128);
+      const int64_t items2 = (int64_t)RT * CT2;
+      int32_t nb2 = 2 * (c->n_cu / 8) * 8;
+      if (items2 < nb2) nb2 = (int32_t)(((items2 + 7) / 8) * 8);
+      if (c->h3_kernel == 1)
+        hipLaunchKernelGGL((k_gp_var_h3<32, 2, 4, 128>), dim3(nb2), dim3(256), 0, c->stream, Ah, lda * (int64_t)npad,
+                           Bh, ldk * (int64_t)npad, (int64_t)npad, npad, RT, CT2, m, c->gp_ctr, part, ldk, amax, kx);
+      else
+        hipLaunchKernelGGL((k_gp_var_h3<16, 4, 4, 128>), dim3(nb2), dim3(256), 0, c->stream, Ah, lda * (int64_t)npad,
+                           Bh, ldk * (int64_t)npad, (int64_t)npad, npad, RT, CT2, m, c->gp_ctr, part, ldk, amax, kx);
+    }
   }
   else if (fp32)
     hipLaunchKernelGGL(k_gp_var<float>, dim3(nb), dim3(V_NT), 0, c->stream, (const float*)LinvT, lda,

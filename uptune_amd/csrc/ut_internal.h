@@ -137,6 +137,10 @@ struct ut_ctx {
   // fp64 variance with few candidate strips: 1 = split the k loops
   // (k_gp_var_pp<true> + k_var_split_red), 0 = one item per row tile; UT_VAR_SPLIT
   int32_t var_split = 1;
+  // f16x3 variance kernel (UT_H3_KERNEL): 0 = one 8-wave workgroup per CU on
+  // 128 x 256 tiles; 1 / 2 = two 4-wave workgroups per CU on 128 x 128 tiles
+  // (BK 32 x 2 ring slots / BK 16 x 4 slots)
+  int32_t h3_kernel = 0;
   double* fit_host = nullptr;        // pinned staging of X, y, 1/ell for the asynchronous fit
   size_t fit_host_n = 0;
   std::string err;
@@ -182,6 +186,9 @@ struct ut_ctx {
   // 26.10-26.12 ms per round (2), 26.32-26.34 (1), 26.54-26.80 (0).
   int32_t hash_after_fit = 2;
   int32_t round_hash_hold = 0;   // the value in force for the round being enqueued
+  // 1: fp32 / f16x3 dense rounds hold the hash for an in-flight fit as well
+  // (their K* waits for the whole fit anyway); UT_HASH_HOLD_LOWPREC
+  int32_t hash_hold_lowprec = 0;
 
   struct PopSlot {
     double* pop = nullptr;
