@@ -194,6 +194,7 @@ int ut_ctx_create(int device, uint64_t seed, ut_ctx** out) {
   if (const char* e = getenv("UT_DE_AOS")) c->de_aos = atoi(e) != 0;
   if (const char* e = getenv("UT_HASH_AFTER_FIT")) c->hash_after_fit = atoi(e);
   if (const char* e = getenv("UT_HASH_HOLD_LOWPREC")) c->hash_hold_lowprec = atoi(e) != 0;
+  if (const char* e = getenv("UT_HASH_AFTER_KSTAR")) c->hash_after_kstar = atoi(e) != 0;
   *out = c;
   return 0;
 }
@@ -781,20 +782,24 @@ static int score_round_de_impl(ut_ctx* c, const ut_de_params* de, const ut_acq* 
   if ((rc = launch_de(c, de, round_, cand_base, m, c->r_values.p, ld, true))) return rc;
   mark(c, "propose");
   // fork: hash_config + dedup on the side stream, beside encode + GP scoring
-  UT_HIP(c, hipEventRecord(c->ev_fork, c->stream));
-  UT_HIP(c, hipStreamWaitEvent(c->side, c->ev_fork, 0));
-  {
+  // (low-precision dense rounds with hash_after_kstar: forked after K*)
+  auto fork_hash = [&]() -> int {
+    UT_HIP(c, hipEventRecord(c->ev_fork, c->stream));
+    UT_HIP(c, hipStreamWaitEvent(c->side, c->ev_fork, 0));
     StreamScope on_side(c, c->side);
     mark(c, "");
     c->round_hash_hold = (prune_rows == 0 && (c->gp_fit_prec == 64 || c->hash_hold_lowprec)) ? c->hash_after_fit : 0;
-    rc = launch_hash_de(c, c->r_values.p, ld, m, cand_base, c->r_digest.p, true);
+    int r = launch_hash_de(c, c->r_values.p, ld, m, cand_base, c->r_digest.p, true);
     c->round_hash_hold = 0;
-    if (rc) return rc;
+    if (r) return r;
     mark(c, "hash");
-    if ((rc = launch_dedup(c, c->r_digest.p, m, c->r_dup.p))) return rc;
+    if ((r = launch_dedup(c, c->r_digest.p, m, c->r_dup.p))) return r;
     mark(c, "dedup");
     UT_HIP(c, hipEventRecord(c->ev_join, c->side));
-  }
+    return 0;
+  };
+  const bool late_hash = prune_rows == 0 && c->gp_fit_prec != 64 && c->hash_after_kstar;
+  if (!late_hash && (rc = fork_hash())) return rc;
   // dense rounds encode straight into the K* operand (features * 1/ell and
   // their norms); the pruned round keeps the features, which it gathers for
   // its threshold set and survivors
@@ -814,9 +819,12 @@ static int score_round_de_impl(ut_ctx* c, const ut_de_params* de, const ut_acq* 
       return rc;
   } else {
     // join before the finalize kernel, which masks duplicates
-    if ((rc = gp_score_impl(c, nullptr, ld, m, acq, c->r_dup.p, c->r_mu.p, c->r_var.p, c->r_score.p,
-                            c->ev_join)))
-      return rc;
+    if (late_hash)
+      rc = gp_score_impl(c, nullptr, ld, m, acq, c->r_dup.p, c->r_mu.p, c->r_var.p, c->r_score.p, c->ev_join,
+                         fork_hash, false);
+    else
+      rc = gp_score_impl(c, nullptr, ld, m, acq, c->r_dup.p, c->r_mu.p, c->r_var.p, c->r_score.p, c->ev_join);
+    if (rc) return rc;
     if ((rc = topk_impl(c, c->r_score.p, c->r_dup.p, m, cand_base, k, c->r_topk_idx.p, c->r_topk_score.p)))
       return rc;
     mark(c, "topk");

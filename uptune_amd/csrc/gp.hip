@@ -777,7 +777,8 @@ int gp_encode_scaled(ut_ctx* c, const double* values, int64_t ld, int64_t m) {
 }
 
 int gp_score_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, const ut_acq* acq, const uint8_t* dup,
-                  double* mu, double* var, double* score, hipEvent_t dup_ready) {
+                  double* mu, double* var, double* score, hipEvent_t dup_ready, const std::function<int()>& mid,
+                  bool var_joins) {
   UT_CHECK(c, c->gp_ready, UT_EINVAL, "gp_score: call ut_gp_fit first");
   UT_CHECK(c, acq != nullptr, UT_EINVAL, "gp_score: acq is NULL");
   if (m <= 0) return 0;
@@ -810,8 +811,9 @@ int gp_score_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, const ut
                               fp32 ? c->mu_part.p : nullptr)))
     return rc;
   mark(c, "kstar");
+  if (mid && (rc = mid())) return rc;
   if (c->fit_pending && !fp32) UT_HIP(c, hipStreamWaitEvent(c->stream, c->ev_fit, 0));
-  if (dup_ready && c->join_before_var) UT_HIP(c, hipStreamWaitEvent(c->stream, dup_ready, 0));
+  if (dup_ready && c->join_before_var && var_joins) UT_HIP(c, hipStreamWaitEvent(c->stream, dup_ready, 0));
   mark(c, "");  // the wait for the fit is not variance time
   if ((rc = launch_gemm_var(c, prec, fp32 ? (const void*)c->gp_LinvT_f : (const void*)c->gp_LinvT, npad, c->kst.p,
                             ldk, npad, m, c->var_part.p, fp32 ? nullptr : c->gp_beta,

@@ -3,6 +3,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <functional>
 #include <initializer_list>
 #include <string>
 #include <vector>
@@ -189,6 +190,10 @@ struct ut_ctx {
   // 1: fp32 / f16x3 dense rounds hold the hash for an in-flight fit as well
   // (their K* waits for the whole fit anyway); UT_HASH_HOLD_LOWPREC
   int32_t hash_hold_lowprec = 0;
+  // 1: fp32 / f16x3 dense rounds enqueue the hash after K* (their K* waits for
+  // the whole fit, which the hash would otherwise crowd out of the CUs) and the
+  // variance GEMM runs beside it; UT_HASH_AFTER_KSTAR
+  int32_t hash_after_kstar = 0;
 
   struct PopSlot {
     double* pop = nullptr;
@@ -407,8 +412,12 @@ int launch_hist_rehash(ut_ctx* c, const uint32_t* okeys, const uint32_t* ostate,
 int launch_dedup(ut_ctx* c, const uint32_t* dig, int64_t m, uint8_t* dup);
 // feat == nullptr: the candidates' scaled features and norms are already in
 // c->ucand / c->cnorm (gp_encode_scaled)
+// mid (optional): enqueued work between K* and the variance GEMM (the round's
+// hash when it runs after K*); var_joins = false: the variance GEMM does not
+// wait for dup_ready (only the finalize does)
 int gp_score_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, const ut_acq* acq, const uint8_t* dup,
-                  double* mu, double* var, double* score, hipEvent_t dup_ready = nullptr);
+                  double* mu, double* var, double* score, hipEvent_t dup_ready = nullptr,
+                  const std::function<int()>& mid = nullptr, bool var_joins = true);
 // encode + scale in one pass into c->ucand / c->cnorm (sized for m), for gp_score_impl(feat = nullptr)
 int gp_encode_scaled(ut_ctx* c, const double* values, int64_t ld, int64_t m);
 int launch_encode_scaled(ut_ctx* c, const double* values, int64_t ld, int64_t m, double* u, int32_t dpad, int64_t ldu,
