@@ -283,6 +283,35 @@ def parity_de_round(eng, space, idx, top, dig, npop, seed, round_, X, y, ell, ji
              "digests_equal": bool(ghex == hexes), "ei_max_rel_err": rel, "round": int(round_)}, want, ei)
 
 
+def parity_ga_round(eng, space, idx, top, dig, parent, seed, round_, X, y, ell, jitter):
+    """The checker for a C4 GA round (outside the timed region): the oracle's
+    UniformGreedyMutation children at the selected global indices
+    (evolutionarytechniques.py:29-61 restated in oracle/ga.py) equal the
+    device's, their hash_config digests equal the round's, and the scores equal
+    the oracle GP's EI within 1e-5 relative."""
+    import torch
+    from oracle import ga as oga
+    from oracle import gp as ogp
+    from oracle import hashing as oh
+    from oracle.space import features, from_f64
+    from uptune_amd.engine import digests_to_hex
+    ii = idx.cpu().numpy()
+    sel = np.flatnonzero(ii >= 0)
+    g = ii[sel]
+    want, winv = oga.propose_ga_vec(space, parent, None, seed, round_, 0, 0, mutation_rate=0.1, g=g)
+    got = torch.cat([eng.propose_ga(1, parent1=parent, round_=round_, cand_base=int(j), mutation_rate=0.1)[0]
+                     for j in g], dim=1).cpu().numpy() if len(g) else np.zeros_like(want)
+    hexes = [oh.hash_config(space, [from_f64(p, want[c, j]) for c, p in enumerate(space)]) for j in range(len(g))]
+    ghex = digests_to_hex(dig[torch.as_tensor(sel, device=dig.device)]) if len(g) else []
+    gp = ogp.GP(X, y, lengthscale=ell, sigma_f2=1.0, sigma_n2=1e-6, jitter=jitter)
+    mu, var = gp.posterior(features(space, want).T)
+    ei = ogp.acquisition(mu, var, gp.f_best)
+    s = top.cpu().numpy()[sel]
+    rel = float(np.max(np.abs(s - ei) / np.maximum(np.abs(ei), 1e-300))) if len(g) else 0.0
+    return {"rows": int(len(g)), "trials_equal": bool(np.array_equal(got, want)), "valid": bool(not winv.any()),
+            "digests_equal": bool(ghex == hexes), "ei_max_rel_err": rel, "round": int(round_)}
+
+
 def main():
     if "WORLD_SIZE" not in os.environ:
         pre = argparse.ArgumentParser(add_help=False)
@@ -479,7 +508,12 @@ def main():
 
     # ---- the checker, outside the timed region ------------------------------
     parity = None
-    if not args.no_parity and args.config in ("c2", "c3") and not args.prune:
+    if not args.no_parity and args.config == "c4" and rank == 0:
+        rep = parity_ga_round(eng, oracle_space_of(manip), idx, top, sdig, parent, 1, args.warmup + args.steps - 1,
+                              X, y, ell, 1e-8)
+        parity = {"last_round": rep, "all_ok": rep["trials_equal"] and rep["valid"] and rep["digests_equal"] and
+                  rep["ei_max_rel_err"] <= 1e-5}
+    if not args.no_parity and args.config in ("c2", "c3"):
         r_last = args.warmup + args.steps - 1
         space = oracle_space_of(manip)
         jit = 0.0

@@ -194,7 +194,7 @@ int ut_ctx_create(int device, uint64_t seed, ut_ctx** out) {
   if (const char* e = getenv("UT_DE_AOS")) c->de_aos = atoi(e) != 0;
   if (const char* e = getenv("UT_HASH_AFTER_FIT")) c->hash_after_fit = atoi(e);
   if (const char* e = getenv("UT_HASH_HOLD_LOWPREC")) c->hash_hold_lowprec = atoi(e) != 0;
-  if (const char* e = getenv("UT_HASH_AFTER_KSTAR")) c->hash_after_kstar = atoi(e) != 0;
+  if (const char* e = getenv("UT_HASH_AFTER_KSTAR")) c->hash_after_kstar = atoi(e);
   *out = c;
   return 0;
 }
@@ -798,7 +798,8 @@ static int score_round_de_impl(ut_ctx* c, const ut_de_params* de, const ut_acq* 
     UT_HIP(c, hipEventRecord(c->ev_join, c->side));
     return 0;
   };
-  const bool late_hash = prune_rows == 0 && c->gp_fit_prec != 64 && c->hash_after_kstar;
+  const bool late_hash = prune_rows == 0 && c->gp_fit_prec != 64 &&
+                         (c->hash_after_kstar > 0 || (c->hash_after_kstar < 0 && c->gp_n >= 2048));
   if (!late_hash && (rc = fork_hash())) return rc;
   // dense rounds encode straight into the K* operand (features * 1/ell and
   // their norms); the pruned round keeps the features, which it gathers for

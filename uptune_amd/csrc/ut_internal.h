@@ -190,10 +190,13 @@ struct ut_ctx {
   // 1: fp32 / f16x3 dense rounds hold the hash for an in-flight fit as well
   // (their K* waits for the whole fit anyway); UT_HASH_HOLD_LOWPREC
   int32_t hash_hold_lowprec = 0;
-  // 1: fp32 / f16x3 dense rounds enqueue the hash after K* (their K* waits for
-  // the whole fit, which the hash would otherwise crowd out of the CUs) and the
-  // variance GEMM runs beside it; UT_HASH_AFTER_KSTAR
-  int32_t hash_after_kstar = 0;
+  // fp32 / f16x3 dense rounds: 1 = enqueue the hash after K* (their K* waits
+  // for the whole fit, which the hash would otherwise crowd out of the CUs: at
+  // n = 4096 the refit stretches from ~6 to ~14 ms beside it) and let the
+  // variance GEMM run beside it; 0 = fork it before encode; -1 (default) = 1
+  // for fits of n >= 2048.  Measured, f16x3: C3 (n 4096) 149.2 vs 153.0 ms per
+  // round; C2 (n 1024) 12.9-13.1 vs 12.8 ms.  UT_HASH_AFTER_KSTAR
+  int32_t hash_after_kstar = -1;
 
   struct PopSlot {
     double* pop = nullptr;
