@@ -432,8 +432,19 @@ def main():
     ell = {"c2": 0.2, "c3": 1.0, "c4": 2.0}[args.config]
 
     comm = None
+    exchange_note = None
     if world > 1 and backend == "nccl":
-        comm = DeviceComm.from_group(None, eng.device)   # libuthot's RCCL communicator (id over gloo)
+        try:
+            comm = DeviceComm.from_group(None, eng.device)   # libuthot's RCCL communicator (id over gloo)
+        except Exception as ex:   # keep the run: records over gloo, the merge still on the device
+            exchange_note = f"RCCL communicator init failed ({ex!r}); records over gloo + HIP merge"
+            print(f"bench rank {rank}: {exchange_note}", file=sys.stderr, flush=True)
+        ok = torch.tensor([0 if comm is None else 1], dtype=torch.int32)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)   # every rank takes the same exchange path
+        if int(ok.item()) == 0 and comm is not None:
+            comm.close()
+            comm = None
+            exchange_note = exchange_note or "another rank's RCCL init failed; records over gloo + HIP merge"
 
     def exchange(idx, top, dig):
         """merged top-k of every rank (identical on all ranks); world 1: the local list"""
@@ -627,7 +638,7 @@ def main():
         "config": {"workload": workload, "candidates_per_gpu": m, "gp_n": n, "dims": d, "k": k,
                    "parallelism": f"dp{world}",
                    "exchange": (None if world == 1 else "libuthot RCCL (ut_comm_allgather_topk + HIP merge)"
-                                if comm is not None else "gloo records + HIP merge (rehearsal)")},
+                                if comm is not None else (exchange_note or "gloo records + HIP merge (rehearsal)"))},
         "parity": parity,
         "stage_ms": stages,
         "kernels": (kernel_table(m, n, d, eng.space_info()[1]) if profiled else None),
