@@ -189,7 +189,6 @@ int ut_ctx_create(int device, uint64_t seed, ut_ctx** out) {
   if (const char* e = getenv("UT_JOIN_BEFORE_VAR")) c->join_before_var = atoi(e) != 0;
   if (const char* e = getenv("UT_VAR_KERNEL")) c->var_kernel = atoi(e);
   if (const char* e = getenv("UT_VAR_SPLIT")) c->var_split = atoi(e) != 0;
-  if (const char* e = getenv("UT_H3_KERNEL")) c->h3_kernel = atoi(e);
   if (const char* e = getenv("UT_FIT_APPEND")) c->fit_append = atoi(e) != 0;
   if (const char* e = getenv("UT_DE_AOS")) c->de_aos = atoi(e) != 0;
   if (const char* e = getenv("UT_HASH_AFTER_FIT")) c->hash_after_fit = atoi(e);

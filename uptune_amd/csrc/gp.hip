@@ -591,7 +591,8 @@ static int gp_alloc(ut_ctx* c, int32_t npad, int32_t d) {
   UT_HIP(c, hipMalloc((void**)&c->gp_T, sizeof(double) * npad * npad));
   UT_HIP(c, hipMalloc((void**)&c->gp_Xs_f, sizeof(float) * npad * d));
   UT_HIP(c, hipMalloc((void**)&c->gp_LinvT, sizeof(double) * npad * npad));
-  UT_HIP(c, hipMalloc((void**)&c->gp_LinvT_f, sizeof(float) * npad * npad));
+  // fp32: (L^-1)^T; h3: the blocked fp16 hi / lo planes, rows padded to 256
+  UT_HIP(c, hipMalloc((void**)&c->gp_LinvT_f, sizeof(float) * (((npad + 255) / 256) * 256) * npad));
   UT_HIP(c, hipMalloc((void**)&c->gp_ctr, sizeof(int32_t) * 32));
   UT_HIP(c, hipMalloc((void**)&c->gp_XsT, sizeof(double) * npad * (((d + 15) / 16) * 16)));
   c->gp_cap_n = npad;
@@ -821,7 +822,9 @@ int gp_score_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, const ut
     return rc;
   mark(c, "var");
   if (dup_ready) UT_HIP(c, hipStreamWaitEvent(c->stream, dup_ready, 0));
-  hipLaunchKernelGGL(k_gp_finalize, dim3(grid1(m, 256)), dim3(256), 0, c->stream, m, RT, RT, c->mu_part.p,
+  // h3's variance partials come per 256-row tile
+  const int32_t RTv = prec == 16 ? (npad + 255) / 256 : RT;
+  hipLaunchKernelGGL(k_gp_finalize, dim3(grid1(m, 256)), dim3(256), 0, c->stream, m, RT, RTv, c->mu_part.p,
                      c->var_part.p, ldk, c->gp_sf2, c->gp_stats, c->gp_flag, acq->kind, acq->xi, acq->kappa, dup,
                      mu, var, score);
   UT_LAUNCH_CHECK(c);

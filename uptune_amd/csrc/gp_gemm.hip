@@ -30,7 +30,29 @@ __global__ void k_to_f32(const double* __restrict__ src, float* __restrict__ dst
 //   columns >= m zero; written by k_gp_prep_cand)
 // ---------------------------------------------------------------------------
 constexpr int K_NT = 256, K_BM = 128, K_BN = 128, K_BK = 16;
-constexpr int KSTAR_SPARE_PER_XCD = 2;  // CUs left to an in-flight GP fit (launch_gemm_kstar)
+// fp64 K* store form (measurements, scripts/exp/kstar_ab.sh): 0 = one 8-B store
+// per element from the MFMA layout, 1 = none (timing floor), 2 = the same with a
+// per-item wave-uniform base + 32-bit offsets, 3 = 16-row bands transposed
+// through LDS and stored as 16-B row pieces
+#ifndef UT_KSTAR_ST
+#define UT_KSTAR_ST 0
+#endif
+constexpr int KSTAR_SPARE_PER_XCD = 2;
+
+// f16x3 operand layout (k_gp_var_h3): 256-row x 32-k blocks of 16 KiB per
+// plane, pre-swizzled into the variance kernel's LDS image
+constexpr int H3_BM = 256, H3_BN = 256, H3_BK = 32;
+constexpr int H3_BLK = H3_BM * H3_BK;          // fp16 elements per block (16 KiB)
+constexpr int H3_STAGE = 4 * H3_BLK;           // A hi, A lo, B hi, B lo
+constexpr int H3_NS = 2;                       // ring slots (128 KiB)
+typedef _Float16 vh8 __attribute__((ext_vector_type(8)));
+
+// element offset of (r, k) inside a blocked plane with K columns
+__device__ __forceinline__ int64_t h3_blk_off(int64_t r, int32_t k, int32_t K) {
+  const int rr = (int)(r & (H3_BM - 1)), c = (k & (H3_BK - 1)) >> 3;
+  return ((r >> 8) * (K / H3_BK) + (k >> 5)) * H3_BLK + rr * H3_BK + ((c ^ ((rr >> 2) & 3)) << 3) + (k & 7);
+}
+  // CUs left to an in-flight GP fit (launch_gemm_kstar)
 
 // sf2 * exp(x) for x in [-1000, 0], table-driven: x = (256 k' + j) ln2/256 + r,
 // |r| <= ln2/512, so exp(x) = 2^k' * 2^(j/256) * e^r with a degree-4 polynomial
@@ -91,8 +113,8 @@ __global__ __launch_bounds__(K_NT, 2) void k_gp_kstar(const double* __restrict__
   // part2 (MU, fp64/fp32 only; pruned scoring): the column partial sum_r k*_r^2
   // as well, for the tail bound of the variance (gp.hip k_prune_bound)
   // TS = _Float16 (h3): k* * kscale split into fp16 hi + lo, stored candidate-major
-  // [col][row] (ld = npad = RT * K_BM) so the variance MFMA reads k-contiguous
-  // fragments; the lo plane starts lo_off elements after the hi plane
+  // in the blocked layout of k_gp_var_h3 (K = npad = RT * K_BM; ldk % 256 == 0);
+  // the lo plane starts lo_off elements after the hi plane
   constexpr bool H3 = sizeof(TS) == 2;
   // one __shared__ object (see k_gp_var): the 2-stage ring, the exp table,
   // then the ticket slot
@@ -178,6 +200,10 @@ __global__ __launch_bounds__(K_NT, 2) void k_gp_kstar(const double* __restrict__
       hc[jj] = col0 + cl < m ? -0.5 * rowop[2 * K_BM + cl] : -1e300;
     }
     const bool want2 = !H3 && MU && part2 != nullptr;
+    TS* const kbase = kst + (int64_t)row0 * ldk + col0;   // UT_KSTAR_ST 2 / 3
+    double* const band = lds + RED_OFF + 4 * K_BN + w * 1024;   // UT_KSTAR_ST 3: 8 KiB per wave
+    (void)kbase;
+    (void)band;
     double s[4] = {0.0, 0.0, 0.0, 0.0}, s2[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -201,11 +227,29 @@ __global__ __launch_bounds__(K_NT, 2) void k_gp_kstar(const double* __restrict__
             const int o = cl * T_PITCH + rl;
             timg[o] = hi;
             timg[K_BN * T_PITCH + o] = (_Float16)(float)(xs - (double)hi);
-          } else {
+          } else if constexpr (UT_KSTAR_ST == 0) {
             if (rt < store_rt) kst[(int64_t)row * ldk + col] = (TS)ks;   // pruned scoring stores the bound rows only
+          } else if constexpr (UT_KSTAR_ST == 2) {
+            if (rt < store_rt) kbase[(uint32_t)rl * (uint32_t)ldk + (uint32_t)cl] = (TS)ks;
+          } else if constexpr (UT_KSTAR_ST == 3) {
+            band[((lane >> 4) + 4 * r) * 64 + jj * 16 + (lane & 15)] = ks;
           }
           if constexpr (MU) s[jj] += al * ks;
           if constexpr (MU && !H3) s2[jj] += ks * ks;
+        }
+      }
+      if constexpr (!H3 && UT_KSTAR_ST == 3) {
+        // this wave's 16 x 64 band: two 512-B row pieces per store instruction
+        __builtin_amdgcn_wave_barrier();
+        if (rt < store_rt) {
+          typedef double d2 __attribute__((ext_vector_type(2)));
+#pragma unroll 2
+          for (int q = 0; q < 8; ++q) {
+            const int lr = 2 * q + (lane >> 5);
+            const d2 v = *reinterpret_cast<const d2*>(band + lr * 64 + 2 * (lane & 31));
+            *reinterpret_cast<d2*>(kbase + (uint32_t)(wm * 64 + i * 16 + lr) * (uint32_t)ldk + wn * 64 +
+                                   2 * (lane & 31)) = v;
+          }
         }
       }
     }
@@ -236,15 +280,19 @@ __global__ __launch_bounds__(K_NT, 2) void k_gp_kstar(const double* __restrict__
       }
     }
     if constexpr (H3) {
-      // 2 planes x 128 candidate rows of 256 B: a wave instruction stores two rows
-      const int64_t npad = (int64_t)RT * K_BM;
-      const int half = lane >> 5, q = lane & 31;
+      // into the blocked layout: a wave instruction stores 16 candidates' 64-B
+      // pieces of one 32-k block, 1 KiB contiguous (2 planes x 4 k-blocks x 8
+      // candidate groups = 64 instructions per tile)
+      const int32_t npad = RT * K_BM;
+      const int ch = lane & 3;
 #pragma unroll 4
-      for (int it = 0; it < 2 * K_BN / 8; ++it) {
-        const int u = it * 8 + w * 2 + half;  // plane * 128 + column
-        const int pl = u / K_BN, cl = u % K_BN;
-        const uint2 v = *reinterpret_cast<const uint2*>(timg + (pl * K_BN + cl) * T_PITCH + q * 4);
-        *reinterpret_cast<uint2*>(kst + pl * lo_off + (col0 + cl) * npad + row0 + q * 4) = v;
+      for (int it = 0; it < 16; ++it) {
+        const int u = it * 4 + w;
+        const int pl = u >> 5, kb = (u >> 3) & 3, cl = (u & 7) * 16 + (lane >> 2);
+        const _Float16* src = timg + (pl * K_BN + cl) * T_PITCH + kb * 32 + ch * 8;
+        const uint2 v0 = *reinterpret_cast<const uint2*>(src), v1 = *reinterpret_cast<const uint2*>(src + 4);
+        *reinterpret_cast<uint4*>(kst + pl * lo_off + h3_blk_off(col0 + cl, row0 + kb * 32 + ch * 8, npad)) =
+            make_uint4(v0.x, v0.y, v1.x, v1.y);
       }
     }
   }
@@ -799,30 +847,19 @@ __global__ __launch_bounds__(1024) void k_var_split_red(const double* __restrict
 // normal range: K* (<= sf2) by 2^h3_kstar_exp(sf2), L^-1 by 2^(14 - ilogb max|L^-1|)
 // (from the device-side max), so hi < 2^15 and lo's subnormal floor sits ~2^-40
 // below the largest element.  The epilogue unscales the f32 column sums.
-//   A = L^-1 [row][k] (fp16 hi, lo planes; ld npad)      -- k-contiguous fragments
-//   B = K* [col][k]   (fp16 hi, lo planes; ld npad)      -- written so by K* (h3)
-// Tiles, tickets, the 3-deep glds ring and the triangular skip are k_gp_var's;
-// a stage is 32 k x (128 A rows + 256 B rows) x {hi, lo} = 48 KiB, 6 glds per wave.
-// LDS image: 64-B operand rows, 16-B chunk c of row r at position c ^ ((r>>2)&3):
-// conflict-free for the ds_read_b128 lane groups of the 32x32x16 fragments.
+//
+// Operands in HBM, "blocked" (round 3): each plane is cut into 256-row x 32-k
+// blocks of 16 KiB, block (rb, kb) at element (rb * K/32 + kb) * 8192, and
+// inside a block row r's 16-B chunk c sits at r * 32 + ((c ^ ((r >> 2) & 3)) << 3)
+// -- exactly the LDS image the MFMA fragments read conflict-free
+// (ds_read_b128 lane groups of the 32x32x16 layout), so a ring stage is two
+// contiguous 16-KiB copies per operand, 1 KiB per global_load_lds.
+//   A = L^-1 [row][k]: rows padded with zeros to a multiple of 256 (k_split_h3)
+//   B = K*   [cand][k]: written blocked by k_gp_kstar<_Float16> (ldk % 256 == 0)
+// Measured against the row-major 128 x 256-tile kernel it replaces
+// (scripts/exp/h3_probe.hip, random operands, one MI355X): C3 shape 100.5 ->
+// 89.6 ms, C2 shape 3.61 -> 3.13 ms.
 // ---------------------------------------------------------------------------
-// H3Cfg<BK, NS, BN>: BK k per stage (64-, 32- or 16-B... operand rows of BK
-// fp16), NS ring slots (NS - 2 stages stay in flight behind the one being
-// consumed), BN candidates per tile.
-template <int BK, int NS, int BN = VAR_BN>
-struct H3Cfg {
-  static constexpr int SA = VAR_BM * BK, SB = BN * BK;  // fp16 elements per plane
-  static constexpr int STAGE = 2 * SA + 2 * SB;
-  static constexpr int CH = BK / 8;                     // 16-B chunks per operand row
-  static constexpr int RPI = 64 / CH;                   // operand rows per glds wave-instruction
-  template <int NI>
-  static constexpr int per_wave() { return 2 * (VAR_BM + BN) / RPI / NI; }  // glds per wave per stage, NI waves
-  // conflict-free position of chunk c in row r for the ds_read_b128 groups
-  static __device__ __forceinline__ int swz(int r, int c) {
-    return BK == 32 ? c ^ ((r >> 2) & 3) : c ^ ((r >> 3) & 1);
-  }
-};
-typedef _Float16 vh8 __attribute__((ext_vector_type(8)));
 
 // s_waitcnt vmcnt(N) (N < 64), lgkmcnt / expcnt left alone
 template <int N>
@@ -831,86 +868,65 @@ __device__ __forceinline__ void wait_vmcnt() {
   __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
 }
 
-template <int BK, int NS>
-__device__ __forceinline__ void h3_glds(const _Float16* __restrict__ src, int64_t ld, int32_t rb, int32_t k0,
-                                        _Float16* plane, int lane) {
-  using C = H3Cfg<BK, NS>;
-  const int rl = lane / C::CH;
-  const int ch = C::swz(rb + rl, lane % C::CH);  // data chunk held by this lane's LDS slot (swz is an involution)
-  // a wave-uniform 64-bit base and a 32-bit lane offset (SGPR base + VGPR
-  // offset addressing; rb is a multiple of RPI, so the offset is the same in
-  // every call and no per-instruction 64-bit address stays live in VGPRs)
-  const _Float16* base = src + (int64_t)rb * ld + k0;
-  const uint32_t loff = (uint32_t)rl * (uint32_t)ld + (uint32_t)(ch * 8);
-  __builtin_amdgcn_global_load_lds(base + loff, (__attribute__((address_space(3))) void*)(plane + rb * BK), 16, 0, 0);
-}
-
-// PART: 3 = the whole stage, 1 = its A planes only, 2 = its B planes only
-template <int BK, int NS, int NW, int BN, int PART = 3>
-__device__ __forceinline__ void h3_issue(const _Float16* __restrict__ A, int64_t a_lo, const _Float16* __restrict__ B,
-                                         int64_t b_lo, int64_t ld, int32_t k0, _Float16* st, int w, int lane) {
-  // A / B already at row0 / col0.  Per wave: A rows [w*128/NW, +128/NW) of each plane,
-  // B rows [w*BN/NW, +BN/NW) of each plane, RPI rows per instruction.
-  using C = H3Cfg<BK, NS, BN>;
-  constexpr int AR = VAR_BM / NW, BR = BN / NW;  // rows per wave
-  static_assert(BR % C::RPI == 0, "B rows per wave");
-  if constexpr (!(PART & 1)) {
-  } else if constexpr (AR >= C::RPI) {
+// one stage: this wave's two 1-KiB pieces of each 16-KiB block.  PART: 1 = A
+// planes, 2 = B planes, 3 = both
+template <int PART>
+__device__ __forceinline__ void h3_issue(const _Float16* __restrict__ Ab, int64_t a_lo, const _Float16* __restrict__ Bb,
+                                         int64_t b_lo, _Float16* st, int w, int lane) {
 #pragma unroll
-    for (int u = 0; u < AR / C::RPI; ++u) {
-      h3_glds<BK, NS>(A, ld, w * AR + u * C::RPI, k0, st, lane);
-      h3_glds<BK, NS>(A + a_lo, ld, w * AR + u * C::RPI, k0, st + C::SA, lane);
+  for (int u = 0; u < 2; ++u) {
+    const int off = w * 1024 + u * 512;
+    if constexpr (PART & 1) {
+      __builtin_amdgcn_global_load_lds(Ab + off + lane * 8, (__attribute__((address_space(3))) void*)(st + off), 16,
+                                       0, 0);
+      __builtin_amdgcn_global_load_lds(Ab + a_lo + off + lane * 8,
+                                       (__attribute__((address_space(3))) void*)(st + H3_BLK + off), 16, 0, 0);
     }
-  } else {  // one instruction covers the A rows of two waves: even waves hi, odd waves lo
-    const int rb = (w >> 1) * C::RPI;
-    h3_glds<BK, NS>(A + (w & 1) * a_lo, ld, rb, k0, st + (w & 1) * C::SA, lane);
-  }
-#pragma unroll
-  for (int u = 0; u < ((PART & 2) ? BR / C::RPI : 0); ++u) {
-    h3_glds<BK, NS>(B, ld, w * BR + u * C::RPI, k0, st + 2 * C::SA, lane);
-    h3_glds<BK, NS>(B + b_lo, ld, w * BR + u * C::RPI, k0, st + 2 * C::SA + C::SB, lane);
+    if constexpr (PART & 2) {
+      __builtin_amdgcn_global_load_lds(Bb + off + lane * 8,
+                                       (__attribute__((address_space(3))) void*)(st + 2 * H3_BLK + off), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(Bb + b_lo + off + lane * 8,
+                                       (__attribute__((address_space(3))) void*)(st + 3 * H3_BLK + off), 16, 0, 0);
+    }
   }
 }
 
-template <int BK, int NS>
 __device__ __forceinline__ vh8 h3_frag(const _Float16* plane, int r, int c) {
-  return *reinterpret_cast<const vh8*>(plane + r * BK + (H3Cfg<BK, NS>::swz(r, c) << 3));
+  return *reinterpret_cast<const vh8*>(plane + r * H3_BK + ((c ^ ((r >> 2) & 3)) << 3));
 }
 
-// mid(): called between the first and second k16 sub-steps (the B half of the
-// next stage's glds goes there, behind this stage's first MFMAs)
-template <int BK, int NS, int JB, int BN, class Mid>
-__device__ __forceinline__ void var_step_h3(const _Float16* st, int wm, int wn, int lane, int imin,
-                                            vf16 (&acc)[2][JB], Mid&& mid) {
-  using C = H3Cfg<BK, NS, BN>;
+// one 32-k stage of a wave's 64 x 128 sub-tile (2 x 4 blocks of 32 x 32); mid()
+// runs between the two k16 sub-steps (the B half of the next stage's refill
+// goes there, behind this stage's first MFMAs)
+template <class Mid>
+__device__ __forceinline__ void var_step_h3(const _Float16* st, int wm, int wn, int lane, int imin, vf16 (&acc)[2][4],
+                                            Mid&& mid) {
   const _Float16* ah = st;
-  const _Float16* al = st + C::SA;
-  const _Float16* bh = st + 2 * C::SA;
-  const _Float16* bl = bh + C::SB;
+  const _Float16* al = st + H3_BLK;
+  const _Float16* bh = st + 2 * H3_BLK;
+  const _Float16* bl = st + 3 * H3_BLK;
 #pragma unroll
-  for (int s = 0; s < BK / 16; ++s) {
-    if (s == (BK / 16 > 1 ? 1 : 0)) {
-      if constexpr (BK / 16 > 1) {
-        __builtin_amdgcn_sched_barrier(0);
-        mid();
-        __builtin_amdgcn_sched_barrier(0);
-      }
+  for (int s = 0; s < H3_BK / 16; ++s) {
+    if (s == 1) {
+      __builtin_amdgcn_sched_barrier(0);
+      mid();
+      __builtin_amdgcn_sched_barrier(0);
     }
     const int c = 2 * s + (lane >> 5);
-    vh8 fbh[JB], fbl[JB];
+    vh8 fbh[4], fbl[4];
 #pragma unroll
-    for (int jj = 0; jj < JB; ++jj) {
-      const int r = wn * (32 * JB) + jj * 32 + (lane & 31);
-      fbh[jj] = h3_frag<BK, NS>(bh, r, c);
-      fbl[jj] = h3_frag<BK, NS>(bl, r, c);
+    for (int jj = 0; jj < 4; ++jj) {
+      const int r = wn * 128 + jj * 32 + (lane & 31);
+      fbh[jj] = h3_frag(bh, r, c);
+      fbl[jj] = h3_frag(bl, r, c);
     }
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       if (i < imin) continue;
       const int r = wm * 64 + i * 32 + (lane & 31);
-      const vh8 fah = h3_frag<BK, NS>(ah, r, c), fal = h3_frag<BK, NS>(al, r, c);
+      const vh8 fah = h3_frag(ah, r, c), fal = h3_frag(al, r, c);
 #pragma unroll
-      for (int jj = 0; jj < JB; ++jj) {
+      for (int jj = 0; jj < 4; ++jj) {
         acc[i][jj] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fal, fbh[jj], acc[i][jj], 0, 0, 0);
         acc[i][jj] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fah, fbl[jj], acc[i][jj], 0, 0, 0);
         acc[i][jj] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fah, fbh[jj], acc[i][jj], 0, 0, 0);
@@ -923,109 +939,93 @@ __device__ __forceinline__ int h3_linv_exp(const unsigned long long* amax_bits) 
   return H3_KSCALE_EXP - ilogb(__longlong_as_double((long long)*amax_bits));
 }
 
-// Tiles of 128 rows of L^-1 x BN candidates, waves 2 x NW/2 of 64 x (2 BN / NW).
-//   NW = 8, BN = 256: one 512-thread workgroup per CU (144 KiB ring), the default;
-//   NW = 4, BN = 128: two 256-thread workgroups per CU (64 KiB ring each), whose
-//     barriers do not align, so one's barrier wait and pipeline fill overlap the
-//     other's MFMAs -- the fp64 k_gp_var_pp arrangement.  The XCD's 64 resident
-//     workgroups then cover two 128-wide strips, the same 4 MiB of K* in its L2
-//     as one 256-wide strip (UT_H3_KERNEL=1 / 2: BK 32 x 2 slots / BK 16 x 4 slots).
-template <int BK, int NS, int NW, int BN>
-__global__ __launch_bounds__(NW * 64, 8 / NW) void k_gp_var_h3(const _Float16* __restrict__ A, int64_t a_lo,
-                                                        const _Float16* __restrict__ B, int64_t b_lo, int64_t ld,
-                                                        int32_t K, int32_t RT, int32_t CT, int64_t m,
-                                                        int32_t* __restrict__ ticket, double* __restrict__ part,
-                                                        int64_t ldp, const unsigned long long* __restrict__ amax_bits,
-                                                        int32_t kexp) {
-  using C = H3Cfg<BK, NS, BN>;
-  static_assert(NS * C::STAGE * 2 <= (160 * 1024 - 128) / (8 / NW), "LDS");
-  static_assert(NS * C::STAGE * 2 >= 2 * BN * 8, "epilogue reduction buffer");
-  constexpr int JB = BN / (NW / 2) / 32;  // 32-column blocks per wave
-  __shared__ __attribute__((aligned(16))) _Float16 lds[NS * C::STAGE + 8];
-  int32_t& s_item = *reinterpret_cast<int32_t*>(lds + NS * C::STAGE);
+// Persistent, one 512-thread workgroup per CU (the 128 KiB ring allows no
+// more), per-XCD work tickets, 256 x 256 tiles: item (rt, ct) = rows
+// [256 rt, +256) of L^-1 against candidates [256 ct, +256); its k loop stops
+// at the diagonal.  Waves are 4 row groups x 2 column halves of 64 x 128; waves
+// w and w + 4 share a SIMD and get row groups wm and 3 - wm, so the diagonal
+// block's skipped 32-row blocks balance per SIMD.  A 2-slot ring: stage kt + 1
+// is issued right after the barrier that retires stage kt - 1 (its A planes)
+// and between stage kt's two k16 sub-steps (its B planes), and lands while
+// stage kt's 48 MFMAs per wave run.  part[rt][col] gets the column partial
+// sum_{r in tile} V[r][col]^2 (RT2 = rows / 256 of them).
+__global__ __launch_bounds__(512, 2) void k_gp_var_h3(const _Float16* __restrict__ A, int64_t a_lo,
+                                                      const _Float16* __restrict__ B, int64_t b_lo, int32_t K,
+                                                      int32_t RT2, int32_t CT, int64_t m, int32_t* __restrict__ ticket,
+                                                      double* __restrict__ part, int64_t ldp,
+                                                      const unsigned long long* __restrict__ amax_bits, int32_t kexp) {
+  __shared__ __attribute__((aligned(16))) _Float16 lds[H3_NS * H3_STAGE + 8];
+  int32_t& s_item = *reinterpret_cast<int32_t*>(lds + H3_NS * H3_STAGE);
   const int t = threadIdx.x, lane = t & 63;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
-  const int wm = w / (NW / 2), wn = w % (NW / 2);
+  const int wm = w < 4 ? w : 7 - w, wn = w < 4 ? 0 : 1;
   const int32_t xcd = blockIdx.x & 7;
+  const int32_t KB = K / H3_BK;
   const double unscale2 = __builtin_ldexp(1.0, -2 * (h3_linv_exp(amax_bits) + kexp));
 
   for (;;) {
     if (t == 0) s_item = atomicAdd(&ticket[xcd], 1);
     __syncthreads();
     const int32_t j = s_item;
-    const int32_t ct = (j / RT) * 8 + xcd;
+    const int32_t ct = (j / RT2) * 8 + xcd;
     if (ct >= CT) break;
-    const int32_t rt = RT - 1 - (j % RT);
-    const int64_t col0 = (int64_t)ct * BN;
-    const int32_t row0 = rt * VAR_BM;
-    const int32_t nk = min(K, row0 + VAR_BM) / BK;
-    const _Float16* At = A + (int64_t)row0 * ld;
-    const _Float16* Bt = B + col0 * ld;
+    const int32_t rt = RT2 - 1 - (j % RT2);
+    const int32_t row0 = rt * H3_BM;
+    const int32_t nk = min(K, row0 + H3_BM) / H3_BK;
+    const _Float16* Ab = A + (int64_t)rt * KB * H3_BLK;
+    const _Float16* Bb = B + (int64_t)ct * KB * H3_BLK;
 
-    vf16 acc[2][JB];
+    vf16 acc[2][4];
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
-      for (int jj = 0; jj < JB; ++jj)
+      for (int jj = 0; jj < 4; ++jj)
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[i][jj][r] = 0.0f;
 
-    // prologue: stages 0 .. NS-2 in flight (nk >= 4 always: K and row0 + 128 are multiples of 128)
-#pragma unroll
-    for (int q = 0; q < NS - 1; ++q)
-      if (q < nk) h3_issue<BK, NS, NW, BN>(At, a_lo, Bt, b_lo, ld, q * BK, lds + q * C::STAGE, w, lane);
-    // retire stage kt (NS - 2 younger stages may stay in flight), then refill
-    // the slot of stage kt - 1 with stage kt + NS - 1.  With two k16 sub-steps
-    // per stage the refill is split: A planes right after the barrier, B planes
-    // between the sub-steps (spreads the glds issue cost over the MFMAs; the
-    // vmcnt count per stage is unchanged); with one it is issued whole.
-    constexpr bool SPLIT = BK / 16 > 1;
+    h3_issue<3>(Ab, a_lo, Bb, b_lo, lds, w, lane);   // stage 0 (nk >= 4: K and row0 + 256 are multiples of 128)
     auto pipe = [&](int32_t kt) -> const _Float16* {
-      if (kt + NS - 2 < nk)
-        wait_vmcnt<C::template per_wave<NW>() * (NS - 2)>();
-      else
-        wait_vmcnt<0>();
-      __builtin_amdgcn_s_barrier();
+      wait_vmcnt<0>();
+      __builtin_amdgcn_s_barrier();   // stage kt landed everywhere; stage kt - 1 fully read
       asm volatile("" ::: "memory");
-      if (kt + NS - 1 < nk)
-        h3_issue<BK, NS, NW, BN, (SPLIT ? 1 : 3)>(At, a_lo, Bt, b_lo, ld, (kt + NS - 1) * BK,
-                                                 lds + ((kt + NS - 1) % NS) * C::STAGE, w, lane);
-      return lds + (kt % NS) * C::STAGE;
+      if (kt + 1 < nk)
+        h3_issue<1>(Ab + (int64_t)(kt + 1) * H3_BLK, a_lo, nullptr, 0, lds + ((kt + 1) & 1) * H3_STAGE, w, lane);
+      return lds + (kt & 1) * H3_STAGE;
     };
     auto refill_b = [&](int32_t kt) {
       return [&, kt]() {
-        if (SPLIT && kt + NS - 1 < nk)
-          h3_issue<BK, NS, NW, BN, 2>(At, a_lo, Bt, b_lo, ld, (kt + NS - 1) * BK,
-                                      lds + ((kt + NS - 1) % NS) * C::STAGE, w, lane);
+        if (kt + 1 < nk)
+          h3_issue<2>(nullptr, 0, Bb + (int64_t)(kt + 1) * H3_BLK, b_lo, lds + ((kt + 1) & 1) * H3_STAGE, w, lane);
       };
     };
-    const int32_t nfull = min(nk, row0 / BK);
-    for (int32_t kt = 0; kt < nfull; ++kt) var_step_h3<BK, NS, JB, BN>(pipe(kt), wm, wn, lane, 0, acc, refill_b(kt));
+    const int32_t nfull = min(nk, row0 / H3_BK);
+    for (int32_t kt = 0; kt < nfull; ++kt) var_step_h3(pipe(kt), wm, wn, lane, 0, acc, refill_b(kt));
     for (int32_t kt = nfull; kt < nk; ++kt) {
       const _Float16* st = pipe(kt);
-      const int kd = ((kt - nfull) * BK) / 32 - 2 * wm;  // 32-row blocks of this wave entirely above the diagonal
+      const int kd = kt - nfull - 2 * wm;   // 32-row blocks of this wave entirely above the diagonal
       const int imin = kd < 0 ? 0 : kd;
-      if (imin < 2) var_step_h3<BK, NS, JB, BN>(st, wm, wn, lane, imin, acc, refill_b(kt));
+      if (imin < 2) var_step_h3(st, wm, wn, lane, imin, acc, refill_b(kt));
       else refill_b(kt)();
     }
 
     __syncthreads();
-    double* red = reinterpret_cast<double*>(lds);  // [2][BN]
+    double* red = reinterpret_cast<double*>(lds);  // [4][256]
 #pragma unroll
-    for (int jj = 0; jj < JB; ++jj) {
-      const int cl = wn * (32 * JB) + jj * 32 + (lane & 31);
+    for (int jj = 0; jj < 4; ++jj) {
+      const int cl = wn * 128 + jj * 32 + (lane & 31);
       double s = 0.0;
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int r = 0; r < 16; ++r) s += (double)acc[i][jj][r] * (double)acc[i][jj][r];
       s += __shfl_xor(s, 32);
-      if ((lane >> 5) == 0) red[wm * BN + cl] = s;
+      if ((lane >> 5) == 0) red[wm * H3_BN + cl] = s;
     }
     __syncthreads();
-    for (int u = t; u < BN; u += NW * 64) {
-      const int64_t col = col0 + u;
-      if (col < m) part[(int64_t)rt * ldp + col] = (red[u] + red[BN + u]) * unscale2;
+    if (t < H3_BN) {
+      const int64_t col = (int64_t)ct * H3_BN + t;
+      if (col < m)
+        part[(int64_t)rt * ldp + col] = ((red[t] + red[H3_BN + t]) + (red[2 * H3_BN + t] + red[3 * H3_BN + t])) * unscale2;
     }
   }
 }
@@ -1046,22 +1046,30 @@ __global__ __launch_bounds__(256) void k_absmax(const double* __restrict__ x, in
   }
 }
 
-__global__ void k_split_h3(const double* __restrict__ x, int64_t cnt, const unsigned long long* __restrict__ amax_bits,
-                           _Float16* __restrict__ dst) {
+// L^-1 [row][k] (n x n fp64) -> scaled hi / lo planes in the blocked layout,
+// rows padded with zeros to n256 = n rounded up to 256 (one element per thread;
+// the lo plane n256 * n elements after the hi plane)
+__global__ void k_split_h3(const double* __restrict__ x, int32_t n, int32_t n256,
+                           const unsigned long long* __restrict__ amax_bits, _Float16* __restrict__ dst) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= cnt) return;
-  const double xs = __builtin_ldexp(x[i], h3_linv_exp(amax_bits));
+  if (i >= (int64_t)n256 * n) return;
+  const int64_t r = i / n;
+  const int32_t k = (int32_t)(i - r * n);
+  const double xs = r < n ? __builtin_ldexp(x[i], h3_linv_exp(amax_bits)) : 0.0;
   const _Float16 hi = (_Float16)(float)xs;
-  dst[i] = hi;
-  dst[cnt + i] = (_Float16)(float)(xs - (double)hi);
+  const int64_t o = h3_blk_off(r, k, n);
+  dst[o] = hi;
+  dst[(int64_t)n256 * n + o] = (_Float16)(float)(xs - (double)hi);
 }
 
 int launch_split_h3(ut_ctx* c, const double* Linv, int32_t n, _Float16* dst) {
   const int64_t cnt = (int64_t)n * n;
+  const int32_t n256 = ((n + H3_BM - 1) / H3_BM) * H3_BM;
   unsigned long long* amax = reinterpret_cast<unsigned long long*>(c->gp_ctr + 16);
   UT_HIP(c, hipMemsetAsync(amax, 0, sizeof(unsigned long long), c->stream));
   hipLaunchKernelGGL(k_absmax, dim3(1024), dim3(256), 0, c->stream, Linv, cnt, amax);
-  hipLaunchKernelGGL(k_split_h3, dim3(grid1(cnt, 256)), dim3(256), 0, c->stream, Linv, cnt, amax, dst);
+  hipLaunchKernelGGL(k_split_h3, dim3(grid1((int64_t)n256 * n, 256)), dim3(256), 0, c->stream, Linv, n, n256, amax,
+                     dst);
   UT_LAUNCH_CHECK(c);
   return 0;
 }
@@ -1081,30 +1089,17 @@ int launch_gemm_var(ut_ctx* c, int prec, const void* LinvT, int64_t lda, const v
   int32_t nb = (c->n_cu / 8) * 8;
   if (items < nb) nb = (int32_t)(((items + 7) / 8) * 8);
   UT_HIP(c, hipMemsetAsync(c->gp_ctr, 0, sizeof(int32_t) * 8, c->stream));
-  if (prec == 16) {  // LinvT: L^-1 [row][k] hi/lo planes; kst: K* [col][row] hi/lo planes (see k_gp_var_h3)
-    // 32 k x 3 slots (48-KiB stages), one 8-wave workgroup per CU.  Measured
-    // slower: 16 k x 6 slots (C3 var 95.8 -> 118.5 ms: twice the barriers per
-    // flop) and two 4-wave workgroups per CU (C3 var 96.7 -> 164.0 ms: two
-    // K* strips per XCD no longer fit its L2)
-    const _Float16* Ah = (const _Float16*)LinvT;
-    const _Float16* Bh = (const _Float16*)kst;
+  if (prec == 16) {  // LinvT / kst: the blocked hi / lo planes of L^-1 and K* (see k_gp_var_h3)
+    UT_CHECK(c, ldk % H3_BN == 0, UT_EINVAL, "gemm_var: h3 needs 256-candidate padding");
+    const int32_t n256 = ((npad + H3_BM - 1) / H3_BM) * H3_BM;
+    const int32_t RT2 = n256 / H3_BM, CT2 = (int32_t)(ldk / H3_BN);
+    const int64_t items2 = (int64_t)RT2 * CT2;
+    int32_t nb2 = (c->n_cu / 8) * 8;
+    if (items2 < nb2) nb2 = (int32_t)(((items2 + 7) / 8) * 8);
     const unsigned long long* amax = reinterpret_cast<const unsigned long long*>(c->gp_ctr + 16);
-    const int32_t kx = h3_kstar_exp(c->gp_sf2);
-    if (c->h3_kernel == 0) {
-      hipLaunchKernelGGL((k_gp_var_h3<32, 3, 8, 256>), dim3(nb), dim3(V_NT), 0, c->stream, Ah, lda * (int64_t)npad,
-                         Bh, ldk * (int64_t)npad, (int64_t)npad, npad, RT, CT, m, c->gp_ctr, part, ldk, amax, kx);
-    } else {   // two 4-wave workgroups per CU on 128-candidate strips
-      const int32_t CT2 = (int32_t)((m + 127) / 128);
-      const int64_t items2 = (int64_t)RT * CT2;
-      int32_t nb2 = 2 * (c->n_cu / 8) * 8;
-      if (items2 < nb2) nb2 = (int32_t)(((items2 + 7) / 8) * 8);
-      if (c->h3_kernel == 1)
-        hipLaunchKernelGGL((k_gp_var_h3<32, 2, 4, 128>), dim3(nb2), dim3(256), 0, c->stream, Ah, lda * (int64_t)npad,
-                           Bh, ldk * (int64_t)npad, (int64_t)npad, npad, RT, CT2, m, c->gp_ctr, part, ldk, amax, kx);
-      else
-        hipLaunchKernelGGL((k_gp_var_h3<16, 4, 4, 128>), dim3(nb2), dim3(256), 0, c->stream, Ah, lda * (int64_t)npad,
-                           Bh, ldk * (int64_t)npad, (int64_t)npad, npad, RT, CT2, m, c->gp_ctr, part, ldk, amax, kx);
-    }
+    hipLaunchKernelGGL(k_gp_var_h3, dim3(nb2), dim3(512), 0, c->stream, (const _Float16*)LinvT, (int64_t)n256 * npad,
+                       (const _Float16*)kst, ldk * (int64_t)npad, npad, RT2, (int32_t)((m + H3_BN - 1) / H3_BN), m,
+                       c->gp_ctr, part, ldk, amax, h3_kstar_exp(c->gp_sf2));
   }
   else if (fp32)
     hipLaunchKernelGGL(k_gp_var<float>, dim3(nb), dim3(V_NT), 0, c->stream, (const float*)LinvT, lda,

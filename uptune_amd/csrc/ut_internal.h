@@ -138,10 +138,6 @@ struct ut_ctx {
   // fp64 variance with few candidate strips: 1 = split the k loops
   // (k_gp_var_pp<true> + k_var_split_red), 0 = one item per row tile; UT_VAR_SPLIT
   int32_t var_split = 1;
-  // f16x3 variance kernel (UT_H3_KERNEL): 0 = one 8-wave workgroup per CU on
-  // 128 x 256 tiles; 1 / 2 = two 4-wave workgroups per CU on 128 x 128 tiles
-  // (BK 32 x 2 ring slots / BK 16 x 4 slots)
-  int32_t h3_kernel = 0;
   double* fit_host = nullptr;        // pinned staging of X, y, 1/ell for the asynchronous fit
   size_t fit_host_n = 0;
   std::string err;
@@ -446,7 +442,7 @@ int launch_xs_t(ut_ctx* c, const double* Xs, int32_t npad, int32_t d, int32_t dp
 int launch_gemm_var(ut_ctx* c, int prec, const void* LinvT, int64_t lda, const void* kst, int64_t ldk, int32_t npad,
                     int64_t m, double* part, const double* beta, double* mpart);
 int launch_transpose(ut_ctx* c, const double* src, int32_t n, double* dst, float* dst_f);
-// L^-1 [row][k] (n x n, fp64) -> scaled fp16 hi/lo planes [row][k] (h3 A operand);
+// L^-1 [row][k] (n x n, fp64) -> scaled fp16 hi/lo planes, blocked (h3 A operand, rows padded to 256);
 // the scale exponent is derived on the device from max|L^-1| (kept in gp_ctr[16..17])
 int launch_split_h3(ut_ctx* c, const double* Linv, int32_t n, _Float16* dst);
 constexpr int VAR_BM = 128, VAR_BN = 256;  // variance-contraction tile (rows of L^-1 x candidates)
