@@ -300,6 +300,12 @@ int ut_gp_topk_pruned(ut_ctx* ctx, const double* features, int64_t ld, int64_t m
  * K*, f32 accumulate (fp32-class, the same 1e-3 parity tier).  The fit itself
  * is always fp64. */
 int ut_gp_set_precision(ut_ctx* ctx, int32_t bits);
+/* order everything enqueued on ctx's stream after this call behind the
+ * in-flight fit (a stream wait on its event; no host wait).  Scoring that
+ * needs the whole fit (pruned, fp32, f16x3) then starts with the fit done, and
+ * the proposal / hash stages before it no longer share the CUs with the fit's
+ * chain of small kernels. */
+int ut_gp_join_fit(ut_ctx* ctx);
 /* wait for the last (possibly asynchronous) fit and report whether its kernel
  * matrix was positive definite (*ok = 1) or not (*ok = 0: later scoring
  * yields NaN scores until a new fit succeeds); not an error either way */

@@ -97,6 +97,26 @@ def main():
         torch.cuda.synchronize()
         rr.append(time.perf_counter() - t1)
     round_rate = args.pool / min(rr)
+    # the stand-alone rate of the loop's own technique mix: each technique's
+    # round (_local_round: propose, hash, dedup, score, local top-k) timed at the
+    # final model, weighted by how many rounds the bandit gave it (the DE round
+    # above is the cheapest kind; PSO rounds move only the swarm)
+    mix_s, mix_c, per_tech = 0.0, 0, {}
+    for t in techs:
+        if t.round == 0:
+            continue
+        cands = t.pool if t.sharded else min(t.pool, t.population)
+        ts = []
+        for _ in range(3):
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            t._local_round()
+            torch.cuda.synchronize()
+            ts.append(time.perf_counter() - t1)
+        per_tech[t.name] = {"rounds": t.round, "candidates": cands, "ms": min(ts) * 1e3}
+        mix_s += t.round * min(ts)
+        mix_c += t.round * cands
+    mix_rate = mix_c / mix_s if mix_s else None
     n_train = len(drv.results_query())
     out = {"config": "C5 AUC bandit over GPU DE+PSO+GA+GGA, shared GP, Rosenbrock-64"
                      + (f", EI-bound pruned ({args.prune} rows)" if args.prune else ""), "n_gpus": world,
@@ -109,6 +129,9 @@ def main():
            "seed_s": drv.seed_s, "loop_candidates_scored_per_s": scored / (wall - drv.seed_s),
            "round_rate_candidates_per_s": round_rate * (world if world > 1 else 1),
            "end_to_end_vs_round": (scored / wall) / (round_rate * (world if world > 1 else 1)),
+           "technique_round_ms": per_tech,
+           "mix_round_rate_candidates_per_s": mix_rate * (world if world > 1 else 1) if mix_rate else None,
+           "end_to_end_vs_mix": (scored / wall) / (mix_rate * (world if world > 1 else 1)) if mix_rate else None,
            "bandit_uses": dict(drv.root_technique.bandit.use_counts)}
     if rank == 0:
         print(json.dumps(out), flush=True)

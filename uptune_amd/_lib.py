@@ -129,6 +129,7 @@ SIGNATURES = {
     "ut_gp_score_values": (C.c_int, [P, P, I64, I64, C.POINTER(Acq), P, P, P, P]),
     "ut_gp_set_precision": (C.c_int, [P, I32]),
     "ut_gp_fit_status": (C.c_int, [P, C.POINTER(I32)]),
+    "ut_gp_join_fit": (C.c_int, [P]),
     "ut_gp_stats": (C.c_int, [P, C.POINTER(D), C.POINTER(D), C.POINTER(D)]),
     "ut_topk": (C.c_int, [P, P, P, I64, I64, I32, P, P]),
     "ut_score_round_de": (C.c_int, [P, C.POINTER(DeParams), C.POINTER(Acq), U32, I64, I64, I32,

@@ -647,6 +647,12 @@ int ut_gp_fit_async(ut_ctx* c, const double* X, const double* y, int32_t n, int3
   return gp_fit_enqueue(c, X, y, n, d, h);
 }
 
+int ut_gp_join_fit(ut_ctx* c) {
+  if (!c) return UT_EINVAL;
+  if (c->fit_pending) UT_HIP(c, hipStreamWaitEvent(c->stream, c->ev_fit, 0));
+  return 0;
+}
+
 int ut_gp_set_fit_append(ut_ctx* c, int32_t enable) {
   if (!c) return UT_EINVAL;
   c->fit_append = enable != 0;

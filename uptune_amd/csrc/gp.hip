@@ -645,7 +645,11 @@ int gp_fit_enqueue(ut_ctx* c, const double* X, const double* y, int32_t n, int32
   double* hX = c->fit_host;
   double* hy = hX + (size_t)n * d;
   double* hinv = hy + n;
-  std::memcpy(hX, X, sizeof(double) * n * d);
+  // an append stages and copies only the new rows: the staging prefix was just
+  // compared equal to X's, and the device staging (gp_tmp, same npad) still
+  // holds the previous fit's rows
+  const int32_t xr0 = app ? n0 : 0;
+  std::memcpy(hX + (size_t)xr0 * d, X + (size_t)xr0 * d, sizeof(double) * (size_t)(n - xr0) * d);
   std::memcpy(hy, y, sizeof(double) * n);
   for (int32_t k = 0; k < d; ++k) hinv[k] = 1.0 / h->lengthscale_host[k];
   UT_HIP(c, hipEventRecord(c->ev_prefit, c->stream));
@@ -656,7 +660,8 @@ int gp_fit_enqueue(ut_ctx* c, const double* X, const double* y, int32_t n, int32
   double* dX = c->gp_tmp;           // [n][d] staging (gp_tmp holds npad*(d+1))
   double* dy = c->gp_tmp + (int64_t)npad * d;
   UT_HIP(c, hipMemcpyAsync(c->gp_inv_ell, hinv, sizeof(double) * d, hipMemcpyHostToDevice, c->stream));
-  UT_HIP(c, hipMemcpyAsync(dX, hX, sizeof(double) * n * d, hipMemcpyHostToDevice, c->stream));
+  UT_HIP(c, hipMemcpyAsync(dX + (size_t)xr0 * d, hX + (size_t)xr0 * d, sizeof(double) * (size_t)(n - xr0) * d,
+                           hipMemcpyHostToDevice, c->stream));
   UT_HIP(c, hipMemcpyAsync(dy, hy, sizeof(double) * n, hipMemcpyHostToDevice, c->stream));
   if (!app) UT_HIP(c, hipMemsetAsync(c->gp_flag, 0, sizeof(int32_t), c->stream));
   hipLaunchKernelGGL(k_gp_prep_train, dim3(grid1(npad, 256)), dim3(256), 0, c->stream, dX, n, npad, d,

@@ -30,13 +30,6 @@ __global__ void k_to_f32(const double* __restrict__ src, float* __restrict__ dst
 //   columns >= m zero; written by k_gp_prep_cand)
 // ---------------------------------------------------------------------------
 constexpr int K_NT = 256, K_BM = 128, K_BN = 128, K_BK = 16;
-// fp64 K* store form (measurements, scripts/exp/kstar_ab.sh): 0 = one 8-B store
-// per element from the MFMA layout, 1 = none (timing floor), 2 = the same with a
-// per-item wave-uniform base + 32-bit offsets, 3 = 16-row bands transposed
-// through LDS and stored as 16-B row pieces
-#ifndef UT_KSTAR_ST
-#define UT_KSTAR_ST 0
-#endif
 constexpr int KSTAR_SPARE_PER_XCD = 2;
 
 // f16x3 operand layout (k_gp_var_h3): 256-row x 32-k blocks of 16 KiB per
@@ -200,10 +193,6 @@ __global__ __launch_bounds__(K_NT, 2) void k_gp_kstar(const double* __restrict__
       hc[jj] = col0 + cl < m ? -0.5 * rowop[2 * K_BM + cl] : -1e300;
     }
     const bool want2 = !H3 && MU && part2 != nullptr;
-    TS* const kbase = kst + (int64_t)row0 * ldk + col0;   // UT_KSTAR_ST 2 / 3
-    double* const band = lds + RED_OFF + 4 * K_BN + w * 1024;   // UT_KSTAR_ST 3: 8 KiB per wave
-    (void)kbase;
-    (void)band;
     double s[4] = {0.0, 0.0, 0.0, 0.0}, s2[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -227,29 +216,11 @@ __global__ __launch_bounds__(K_NT, 2) void k_gp_kstar(const double* __restrict__
             const int o = cl * T_PITCH + rl;
             timg[o] = hi;
             timg[K_BN * T_PITCH + o] = (_Float16)(float)(xs - (double)hi);
-          } else if constexpr (UT_KSTAR_ST == 0) {
+          } else {
             if (rt < store_rt) kst[(int64_t)row * ldk + col] = (TS)ks;   // pruned scoring stores the bound rows only
-          } else if constexpr (UT_KSTAR_ST == 2) {
-            if (rt < store_rt) kbase[(uint32_t)rl * (uint32_t)ldk + (uint32_t)cl] = (TS)ks;
-          } else if constexpr (UT_KSTAR_ST == 3) {
-            band[((lane >> 4) + 4 * r) * 64 + jj * 16 + (lane & 15)] = ks;
           }
           if constexpr (MU) s[jj] += al * ks;
           if constexpr (MU && !H3) s2[jj] += ks * ks;
-        }
-      }
-      if constexpr (!H3 && UT_KSTAR_ST == 3) {
-        // this wave's 16 x 64 band: two 512-B row pieces per store instruction
-        __builtin_amdgcn_wave_barrier();
-        if (rt < store_rt) {
-          typedef double d2 __attribute__((ext_vector_type(2)));
-#pragma unroll 2
-          for (int q = 0; q < 8; ++q) {
-            const int lr = 2 * q + (lane >> 5);
-            const d2 v = *reinterpret_cast<const d2*>(band + lr * 64 + 2 * (lane & 31));
-            *reinterpret_cast<d2*>(kbase + (uint32_t)(wm * 64 + i * 16 + lr) * (uint32_t)ldk + wn * 64 +
-                                   2 * (lane & 31)) = v;
-          }
         }
       }
     }

@@ -284,6 +284,11 @@ class BatchEngine:
         fn = self.lib.ut_gp_fit if wait else self.lib.ut_gp_fit_async
         L.check(self.ctx, fn(self.ctx, X.ctypes.data, y.ctypes.data, n, d, C.byref(h)), "ut_gp_fit")
 
+    def gp_join_fit(self):
+        """ut_gp_join_fit: later work on the engine's stream waits for the
+        in-flight fit on the device (no host wait)"""
+        L.check(self.ctx, self.lib.ut_gp_join_fit(self.ctx), "ut_gp_join_fit")
+
     def gp_fit_ok(self) -> bool:
         """ut_gp_fit_status: waits for the last fit; False = its kernel matrix
         was not positive definite (scores are NaN until a fit succeeds)"""

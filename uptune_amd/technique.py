@@ -25,6 +25,7 @@ from __future__ import annotations
 import copy
 import logging
 import math
+import os
 import random
 from collections import deque
 from typing import Any, Dict, List, Optional
@@ -499,6 +500,17 @@ class GpuBatchTechnique(SearchTechnique):
         import torch
         eng = self._ensure_engine()
         self.model.sync_history(self.driver)
+        # the fit first: its new training rows are encoded through the device
+        # (one host round trip) while the queue is still empty.  Pruned scoring
+        # needs the whole fit before its K*, so the round's stages queue behind
+        # it (ut_gp_join_fit): the fit's chain of small kernels runs alone
+        # instead of starving beside the hash, and no host wait sits between the
+        # hash and the fit (the proposals never read the GP).  Dense fp64 rounds
+        # keep the fit beside their K* (only the variance GEMM waits for it).
+        fit_first = os.environ.get("UT_FIT_FIRST", "1") != "0"
+        have_model = fit_first and self.surrogate is None and self.model.fit(self.driver)
+        if have_model and self.prune_rows > 0 and self.model.precision == 64 and os.environ.get("UT_JOIN_FIT", "1") != "0":
+            eng.gp_join_fit()
         base = self.round_base()
         vals, invalid = self.propose(self.pool)
         dig = self.hash_proposals(vals, base)
@@ -509,7 +521,7 @@ class GpuBatchTechnique(SearchTechnique):
             if getattr(eng, "forest", None) is None:
                 eng.forest_set(self.surrogate)
             _, score = eng.forest_predict(eng.encode(vals), dup=dup)
-        elif self.model.fit(self.driver):
+        elif have_model or (not fit_first and self.model.fit(self.driver)):
             if self.prune_rows > 0 and self.model.precision == 64:
                 idx, top, _ = eng.gp_topk_pruned(eng.encode(vals), self.batch, acq=eng.acq(self.acq_kind), dup=dup,
                                                  cand_base=base, bound_rows=self.prune_rows)
