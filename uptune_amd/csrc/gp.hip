@@ -635,20 +635,24 @@ int gp_fit_enqueue(ut_ctx* c, const double* X, const double* y, int32_t n, int32
   if (rc) return rc;
   c->pr_f2_valid = false;   // |L^-1|_F^2 (pruned scoring) belongs to the previous factor
   const size_t need = (size_t)n * d + n + d;
+  bool fresh = false;   // a new staging buffer holds no previous rows
   if (c->fit_host_n < need) {
     if (c->fit_host) hipHostFree(c->fit_host);
     c->fit_host = nullptr;
     c->fit_host_n = 0;
-    UT_HIP(c, hipHostMalloc((void**)&c->fit_host, sizeof(double) * need, hipHostMallocDefault));
-    c->fit_host_n = need;
+    // room for growth: the tuning loop appends a few rows per fit
+    const size_t cap = need + need / 4 + 4096;
+    UT_HIP(c, hipHostMalloc((void**)&c->fit_host, sizeof(double) * cap, hipHostMallocDefault));
+    c->fit_host_n = cap;
+    fresh = true;
   }
   double* hX = c->fit_host;
   double* hy = hX + (size_t)n * d;
   double* hinv = hy + n;
   // an append stages and copies only the new rows: the staging prefix was just
-  // compared equal to X's, and the device staging (gp_tmp, same npad) still
-  // holds the previous fit's rows
-  const int32_t xr0 = app ? n0 : 0;
+  // compared equal to X's (unless the staging buffer was just reallocated), and
+  // the device staging (gp_tmp, same npad) still holds the previous fit's rows
+  const int32_t xr0 = app && !fresh ? n0 : 0;
   std::memcpy(hX + (size_t)xr0 * d, X + (size_t)xr0 * d, sizeof(double) * (size_t)(n - xr0) * d);
   std::memcpy(hy, y, sizeof(double) * n);
   for (int32_t k = 0; k < d; ++k) hinv[k] = 1.0 / h->lengthscale_host[k];

@@ -25,7 +25,6 @@ from __future__ import annotations
 import copy
 import logging
 import math
-import os
 import random
 from collections import deque
 from typing import Any, Dict, List, Optional
@@ -507,9 +506,8 @@ class GpuBatchTechnique(SearchTechnique):
         # instead of starving beside the hash, and no host wait sits between the
         # hash and the fit (the proposals never read the GP).  Dense fp64 rounds
         # keep the fit beside their K* (only the variance GEMM waits for it).
-        fit_first = os.environ.get("UT_FIT_FIRST", "1") != "0"
-        have_model = fit_first and self.surrogate is None and self.model.fit(self.driver)
-        if have_model and self.prune_rows > 0 and self.model.precision == 64 and os.environ.get("UT_JOIN_FIT", "1") != "0":
+        have_model = self.surrogate is None and self.model.fit(self.driver)
+        if have_model and self.prune_rows > 0 and self.model.precision == 64:
             eng.gp_join_fit()
         base = self.round_base()
         vals, invalid = self.propose(self.pool)
@@ -521,7 +519,7 @@ class GpuBatchTechnique(SearchTechnique):
             if getattr(eng, "forest", None) is None:
                 eng.forest_set(self.surrogate)
             _, score = eng.forest_predict(eng.encode(vals), dup=dup)
-        elif have_model or (not fit_first and self.model.fit(self.driver)):
+        elif have_model:
             if self.prune_rows > 0 and self.model.precision == 64:
                 idx, top, _ = eng.gp_topk_pruned(eng.encode(vals), self.batch, acq=eng.acq(self.acq_kind), dup=dup,
                                                  cand_base=base, bound_rows=self.prune_rows)
