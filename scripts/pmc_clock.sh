@@ -3,7 +3,7 @@
 # clock = GRBM_GUI_ACTIVE / 8 / duration; MFMA util = SQ_VALU_MFMA_BUSY_CYCLES / (cycles * CUs)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-OUT=gpurun_out/clk
+OUT=${PROF_OUT:-gpurun_out/clk}
 mkdir -p $OUT
 ARGS=${BENCH_ARGS:---steps 3 --warmup 1 --no-cpu-baseline}
 timeout -k 10 600 rocprofv3 --kernel-trace --pmc GRBM_GUI_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CU_CYCLES -d $OUT -o run --output-format csv -- \

@@ -2,7 +2,7 @@
 # rocprofv3 kernel trace + stats, then HBM byte counters in separate passes.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-OUT=gpurun_out/prof
+OUT=${PROF_OUT:-gpurun_out/prof}
 mkdir -p $OUT
 ARGS=${BENCH_ARGS:---steps 3 --warmup 1 --no-cpu-baseline}
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- \
