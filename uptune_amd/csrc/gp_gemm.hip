@@ -128,7 +128,11 @@ __global__ __launch_bounds__(K_NT, 2) void k_gp_kstar(const double* __restrict__
   double* const rowop = lds + MAIN + EXP_TAB + 2;   // [xnorm 128][alpha 128][cnorm 128]
   _Float16* timg = reinterpret_cast<_Float16*>(lds);
   const int t = threadIdx.x, lane = t & 63;
-  if (t < EXP_TAB) etab[t] = sf2 * exp2((double)t / EXP_TAB);  // published by the first ticket barrier
+  // h3: the table carries the split's power-of-two scale, so ks below is
+  // k* * kscale exactly (and the mean's alpha is divided by it: the product is
+  // unchanged bit for bit)
+  if (t < EXP_TAB) etab[t] = (sf2 * exp2((double)t / EXP_TAB)) * (H3 ? kscale : 1.0);  // published by the first ticket barrier
+  const double ikscale = 1.0 / kscale;   // a power of two
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
   const int wm = w >> 1, wn = w & 1;
   const int32_t xcd = blockIdx.x & 7;
@@ -202,7 +206,7 @@ __global__ __launch_bounds__(K_NT, 2) void k_gp_kstar(const double* __restrict__
         const int32_t row = row0 + rl;
         const double hx = row < n ? -0.5 * rowop[rl] : -1e300;
         double al = 0.0;
-        if constexpr (MU) al = rowop[K_BM + rl];
+        if constexpr (MU) al = H3 ? rowop[K_BM + rl] * ikscale : rowop[K_BM + rl];
 #pragma unroll
         for (int jj = 0; jj < 4; ++jj) {
           const int cl = wn * 64 + jj * 16 + (lane & 15);
@@ -211,11 +215,13 @@ __global__ __launch_bounds__(K_NT, 2) void k_gp_kstar(const double* __restrict__
           const double x = __builtin_fmax(__builtin_fmin((acc[i][jj][r] + hx) + hc[jj], 0.0), -1000.0);
           const double ks = sf2_exp_nonpos(x, etab);
           if constexpr (H3) {
-            const double xs = ks * kscale;
-            const _Float16 hi = (_Float16)(float)xs;
+            // ks = k* * kscale (< 2^15): hi = fp16(ks), lo = fp16 of the rest,
+            // the rest taken in f32 (exact there: hi is within 2^-11 of xf)
+            const float xf = (float)ks;
+            const _Float16 hi = (_Float16)xf;
             const int o = cl * T_PITCH + rl;
             timg[o] = hi;
-            timg[K_BN * T_PITCH + o] = (_Float16)(float)(xs - (double)hi);
+            timg[K_BN * T_PITCH + o] = (_Float16)(xf - (float)hi);
           } else {
             if (rt < store_rt) kst[(int64_t)row * ldk + col] = (TS)ks;   // pruned scoring stores the bound rows only
           }
