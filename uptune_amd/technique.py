@@ -291,6 +291,10 @@ class SharedModel:
         self._res_ids: List[Any] = []
         self._X = None
         self._y: List[float] = []
+        # the fit's row order (a permutation of the results): best y first as of
+        # the last refit, the results since appended in arrival order
+        self._perm = None
+        self._perm_npad = 0
         self._fit_key = None
         self._fit_unverified = False
         self.fits = 0
@@ -384,12 +388,31 @@ class SharedModel:
         k = len(self._res_ids)
         if self._X is None or ids[:k] != self._res_ids:      # not an append: re-encode everything
             self._X, self._y, self._res_ids, k = np.zeros((0, self.engine.spec.n_features)), [], [], 0
+            self._perm = None
         new = rows[k:]
         if new:
             self._X = np.vstack([self._X, self.engine.features_host([r.configuration.data for r in new])])
             self._y += [float(r.time) for r in new]
             self._res_ids = list(ids)   # a copy: the scan list keeps growing
-        self.engine.gp_fit(self._X, np.asarray(self._y), lengthscale=self.lengthscale, wait=False, **self.hyper)
+        # Row order.  The GP posterior does not depend on it, but the EI bound of
+        # pruned scoring (ut_gp_topk_pruned) comes from the first rows of L^-1:
+        # with the best results first it sees the neighbourhood that GA / GGA
+        # children (mutations of the best configuration) live in (the C5 GGA
+        # round: 262,144 survivors -> 8, 75 -> 5 ms; a GA round: 2,459 -> 8,
+        # scripts/exp/gga_prune_probe.py).  The rows are re-sorted only where
+        # the device refits anyway (a new padded size, gp.hip NPAD = 128, or a
+        # re-encode); in between the new results are appended, so the
+        # incremental fit still applies.
+        y = np.asarray(self._y)
+        n = len(y)
+        npad = -(-n // 128) * 128
+        if self._perm is None or npad != self._perm_npad or len(self._perm) > n:
+            self._perm = np.argsort(y, kind="stable")
+            self._perm_npad = npad
+        elif len(self._perm) < n:
+            self._perm = np.concatenate([self._perm, np.arange(len(self._perm), n)])
+        self.engine.gp_fit(self._X[self._perm], y[self._perm], lengthscale=self.lengthscale, wait=False,
+                           **self.hyper)
         self._fit_key = key
         self._fit_unverified = True
         self.fits += 1
