@@ -73,6 +73,7 @@ class BatchEngine:
     # -- plumbing ----------------------------------------------------------
     def _bind_stream(self):
         s = torch.cuda.current_stream(self.device)
+        self._stream = s
         L.check(self.ctx, self.lib.ut_set_stream(self.ctx, C.c_void_p(s.cuda_stream)), "ut_set_stream")
 
     def close(self):
@@ -162,7 +163,12 @@ class BatchEngine:
             return None
         if isinstance(r, torch.Tensor):
             return r.to(self.device, torch.float64).contiguous()
-        return torch.as_tensor(np.asarray(r, dtype=np.float64), device=self.device)
+        # through pinned memory, asynchronously on the engine's stream (the
+        # library's stream, _bind_stream): a pageable copy would wait for every
+        # kernel already queued (the fit, the previous stages) before returning
+        h = torch.from_numpy(np.ascontiguousarray(r, dtype=np.float64)).pin_memory()
+        with torch.cuda.stream(self._stream):
+            return h.to(self.device, non_blocking=True)
 
     def propose_pso(self, gbest, m: int, round_: int = 0, cand_base: int = 0, omega: float = 0.5,
                     phi_l: float = 0.5, phi_g: float = 0.5, sigma: float = 0.2, alias_pbest: bool = True,
