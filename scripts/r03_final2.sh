@@ -7,7 +7,7 @@
 # failure ends the script.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-O=gpurun_out/final2
+O=${FINAL_OUT:-gpurun_out/final2}
 mkdir -p $O
 run() { local t=$1 name=$2; shift 2; timeout -k 10 $t "$@" > $O/$name.log 2>&1; local rc=$?;
         echo "$name rc=$rc"; tail -c 300 $O/$name.log; echo; [ $rc -eq 0 ] || exit $rc; }
