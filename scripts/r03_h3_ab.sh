@@ -1,4 +1,6 @@
 #!/bin/bash
+# (historical: UT_H3_KERNEL and these variants were removed in round 3, when the
+# blocked 256 x 256-tile kernel replaced them; see DESIGN.md "Round 3: the f16x3 variance kernel")
 # round 3: f16x3 variance kernel A/B (UT_H3_KERNEL = 0: one 8-wave workgroup
 # per CU on 128 x 256 tiles; 1 / 2: two 4-wave workgroups per CU on 128 x 128
 # tiles, BK 32 x 2 slots / BK 16 x 4 slots): parity at each, then the C2 / C3
