@@ -1,6 +1,6 @@
 // Experiment (round 3): what bounds the f16x3 variance contraction, and a
 // 256 x 256-tile variant.  Standalone; includes the library kernels.
-//   base      the library's k_gp_var_h3<32, 3, 8, 256> (128 x 256 tiles)
+//   base      the library's k_gp_var_h3 (blocked operands; round 3's shipped form)
 //   w3<BK,NS,MODE>  256 x 256 tiles, 8 waves of 64 rows x 128 columns, NS-slot
 //             glds ring of BK-k stages (2 x 64 KiB at BK 32, 4 x 32 KiB at BK 16)
 //     MODE 0  as it would ship
@@ -9,8 +9,8 @@
 //     MODE 3  MODE 2 + A from row tile 0
 //   hipcc -O3 -std=c++17 --offload-arch=gfx950 -I uptune_amd/csrc scripts/exp/h3_probe.hip -o gpurun_tmp/h3_probe
 //   gpurun_tmp/h3_probe NPAD M REPS
-// Builds against the library at commit 169f49e (its row-major k_gp_var_h3 is
-// the "base" here; the library now ships the blocked 256 x 256 form).
+// "base" is the library's shipped kernel (blocked operands, 256 x 256 tiles);
+// the w3 kernels below read row-major planes or the blocked copies.
 #include "../../uptune_amd/csrc/gp_gemm.hip"
 
 #include <algorithm>
@@ -21,6 +21,25 @@
 #include <type_traits>
 
 namespace ut {
+
+
+// row-major-plane helpers (the round-2 kernel's, kept here for the w3 variants)
+template <int BK>
+__device__ __forceinline__ int p_swz(int r, int c) { return BK == 32 ? c ^ ((r >> 2) & 3) : c ^ ((r >> 3) & 1); }
+template <int BK>
+__device__ __forceinline__ void p_glds(const _Float16* __restrict__ src, int64_t ld, int32_t rb, int32_t k0,
+                                       _Float16* plane, int lane) {
+  constexpr int CH = BK / 8;
+  const int rl = lane / CH;
+  const int ch = p_swz<BK>(rb + rl, lane % CH);
+  const _Float16* base = src + (int64_t)rb * ld + k0;
+  const uint32_t loff = (uint32_t)rl * (uint32_t)ld + (uint32_t)(ch * 8);
+  __builtin_amdgcn_global_load_lds(base + loff, (__attribute__((address_space(3))) void*)(plane + rb * BK), 16, 0, 0);
+}
+template <int BK>
+__device__ __forceinline__ vh8 p_frag(const _Float16* plane, int r, int c) {
+  return *reinterpret_cast<const vh8*>(plane + r * BK + (p_swz<BK>(r, c) << 3));
+}
 
 template <int BK>
 struct W3 {
@@ -38,15 +57,15 @@ __device__ __forceinline__ void w3_issue(const _Float16* __restrict__ A, int64_t
   if constexpr (PART & 1) {
 #pragma unroll
     for (int u = 0; u < R / C::RPI; ++u) {
-      h3_glds<BK, NS>(A, ld, w * R + u * C::RPI, k0, st, lane);
-      h3_glds<BK, NS>(A + a_lo, ld, w * R + u * C::RPI, k0, st + C::SA, lane);
+      p_glds<BK>(A, ld, w * R + u * C::RPI, k0, st, lane);
+      p_glds<BK>(A + a_lo, ld, w * R + u * C::RPI, k0, st + C::SA, lane);
     }
   }
   if constexpr (PART & 2) {
 #pragma unroll
     for (int u = 0; u < R / C::RPI; ++u) {
-      h3_glds<BK, NS>(B, ld, w * R + u * C::RPI, k0, st + 2 * C::SA, lane);
-      h3_glds<BK, NS>(B + b_lo, ld, w * R + u * C::RPI, k0, st + 3 * C::SA, lane);
+      p_glds<BK>(B, ld, w * R + u * C::RPI, k0, st + 2 * C::SA, lane);
+      p_glds<BK>(B + b_lo, ld, w * R + u * C::RPI, k0, st + 3 * C::SA, lane);
     }
   }
 }
@@ -99,14 +118,14 @@ __device__ __forceinline__ void w3_step(const _Float16* st, int wm, int wn, int 
 #pragma unroll
     for (int jj = 0; jj < 4; ++jj) {
       const int r = wn * 128 + jj * 32 + (lane & 31);
-      fbh[jj] = h3_frag<BK, NS>(bh, r, c);
-      fbl[jj] = h3_frag<BK, NS>(bl, r, c);
+      fbh[jj] = p_frag<BK>(bh, r, c);
+      fbl[jj] = p_frag<BK>(bl, r, c);
     }
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       if (i < imin) continue;
       const int r = wm * 64 + i * 32 + (lane & 31);
-      const vh8 fah = h3_frag<BK, NS>(ah, r, c), fal = h3_frag<BK, NS>(al, r, c);
+      const vh8 fah = p_frag<BK>(ah, r, c), fal = p_frag<BK>(al, r, c);
 #pragma unroll
       for (int jj = 0; jj < 4; ++jj) {
         acc[i][jj] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fal, fbh[jj], acc[i][jj], 0, 0, 0);
@@ -332,11 +351,6 @@ int main(int argc, char** argv) {
     CK(hipMemcpy(dst.data(), cs, sizeof(double) * m, hipMemcpyDeviceToHost));
   };
   const int CT = (int)(ldk / 256);
-  timeit("base k_gp_var_h3<32,3,8,256>", [&] {
-    hipLaunchKernelGGL((k_gp_var_h3<32, 3, 8, 256>), dim3(ncu), dim3(512), 0, 0, A, na, B, nb, (int64_t)npad, npad, RT,
-                       CT, m, ticket, part, ldk, amax, -14);
-  });
-  colsum(RT, ref);
   auto cmp = [&](const char* what) {
     double md = 0;
     for (int64_t q = 0; q < m; ++q) md = std::max(md, std::abs(ref[q] - got[q]) / (std::abs(ref[q]) + 1e-30));
@@ -348,16 +362,21 @@ int main(int argc, char** argv) {
     hipLaunchKernelGGL((k_h3w<BK, NS, MODE>), dim3(ncu), dim3(512), 0, 0, A, na, B, nb, (int64_t)npad, npad, RT2, \
                        CT, m, ticket, part, ldk, 1.0);                                                          \
   })
-  W3RUN(32, 2, 0, "w3 BK32 NS2");
+  _Float16 *Ab, *Bb;
+  CK(hipMalloc(&Ab, sizeof(_Float16) * 2 * na));
+  CK(hipMalloc(&Bb, sizeof(_Float16) * 2 * nb));
+  k_to_blk<<<65536, 256>>>(A, na, Ab, na, npad, npad);
+  k_to_blk<<<65536, 256>>>(B, nb, Bb, nb, ldk, npad);
+  CK(hipDeviceSynchronize());
+  timeit("base: library k_gp_var_h3 (blocked)", [&] {
+    hipLaunchKernelGGL(k_gp_var_h3, dim3(ncu), dim3(512), 0, 0, Ab, na, Bb, nb, npad, RT2, CT, m, ticket, part, ldk,
+                       amax, -14);
+  });
+  colsum(RT2, ref);
+  W3RUN(32, 2, 0, "w3 BK32 NS2 (row-major planes)");
   colsum(RT2, got);
   cmp("w3 BK32 NS2");
   {
-    _Float16 *Ab, *Bb;
-    CK(hipMalloc(&Ab, sizeof(_Float16) * 2 * na));
-    CK(hipMalloc(&Bb, sizeof(_Float16) * 2 * nb));
-    k_to_blk<<<65536, 256>>>(A, na, Ab, na, npad, npad);
-    k_to_blk<<<65536, 256>>>(B, nb, Bb, nb, ldk, npad);
-    CK(hipDeviceSynchronize());
     timeit("w3 BK32 NS2 blocked", [&] {
       hipLaunchKernelGGL((k_h3w<32, 2, 0, true>), dim3(ncu), dim3(512), 0, 0, Ab, na, Bb, nb, (int64_t)npad, npad, RT2,
                          CT, m, ticket, part, ldk, 1.0);
@@ -372,9 +391,9 @@ int main(int argc, char** argv) {
       hipLaunchKernelGGL((k_h3w<32, 2, 2, true>), dim3(ncu), dim3(512), 0, 0, Ab, na, Bb, nb, (int64_t)npad, npad, RT2,
                          CT, m, ticket, part, ldk, 1.0);
     });
-    CK(hipFree(Ab));
-    CK(hipFree(Bb));
   }
+  CK(hipFree(Ab));
+  CK(hipFree(Bb));
   W3RUN(16, 4, 0, "w3 BK16 NS4");
   colsum(RT2, got);
   cmp("w3 BK16 NS4");
