@@ -246,6 +246,120 @@ __global__ __launch_bounds__(512, 2) void k_h3w(const _Float16* __restrict__ A, 
   }
 }
 
+
+// q4: one wave per SIMD (a 4-wave workgroup, up to 512 VGPRs per lane), 256 x 256
+// tiles on the blocked operands, each wave 128 rows x 128 columns (4 x 4 blocks
+// of 32 x 32: 256 accumulator registers); 16 ds_read_b128 per 48 MFMAs (0.33
+// per MFMA against 0.5 at 8 waves); each wave issues 16 of a stage's 64 glds,
+// four between every k16 sub-step's MFMA groups.
+//   MODE 0 as it would ship, 1 no refills
+template <int MODE>
+__global__ __launch_bounds__(256, 1) void k_h3q(const _Float16* __restrict__ A, int64_t a_lo,
+                                                const _Float16* __restrict__ B, int64_t b_lo, int32_t K, int32_t RT2,
+                                                int32_t CT, int64_t m, int32_t* __restrict__ ticket,
+                                                double* __restrict__ part, int64_t ldp, double unscale2) {
+  __shared__ __attribute__((aligned(16))) _Float16 lds[H3_NS * H3_STAGE + 8];
+  int32_t& s_item = *reinterpret_cast<int32_t*>(lds + H3_NS * H3_STAGE);
+  const int t = threadIdx.x, lane = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wm = w >> 1, wn = w & 1;
+  const int32_t xcd = blockIdx.x & 7;
+  const int32_t KB = K / H3_BK;
+  // this wave's 16 pieces of a stage: plane p (0 A hi, 1 A lo, 2 B hi, 3 B lo), pieces 4w .. 4w+3 of 16 per plane
+  auto issue_part = [&](const _Float16* Ab, const _Float16* Bb, _Float16* st, int part_) {
+    // part_ 0..3: plane part_
+    const _Float16* src = part_ == 0 ? Ab : part_ == 1 ? Ab + a_lo : part_ == 2 ? Bb : Bb + b_lo;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int off = (w * 4 + u) * 512;
+      __builtin_amdgcn_global_load_lds(src + off + lane * 8,
+                                       (__attribute__((address_space(3))) void*)(st + part_ * H3_BLK + off), 16, 0, 0);
+    }
+  };
+  for (;;) {
+    if (t == 0) s_item = atomicAdd(&ticket[xcd], 1);
+    __syncthreads();
+    const int32_t j = s_item;
+    const int32_t ct = (j / RT2) * 8 + xcd;
+    if (ct >= CT) break;
+    const int32_t rt = RT2 - 1 - (j % RT2);
+    const int32_t row0 = rt * H3_BM;
+    const int32_t nk = min(K, row0 + H3_BM) / H3_BK;
+    const _Float16* Ab = A + (int64_t)rt * KB * H3_BLK;
+    const _Float16* Bb = B + (int64_t)ct * KB * H3_BLK;
+    vf16 acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][jj][r] = 0.0f;
+    for (int q = 0; q < 4; ++q) issue_part(Ab, Bb, lds, q);
+    const int32_t nfull = min(nk, row0 / H3_BK);
+    for (int32_t kt = 0; kt < nk; ++kt) {
+      if (MODE != 1) wait_vmcnt<0>();
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      const bool nxt = MODE != 1 && kt + 1 < nk;
+      _Float16* nst = lds + ((kt + 1) & 1) * H3_STAGE;
+      const _Float16* st = lds + (kt & 1) * H3_STAGE;
+      const _Float16* ah = st;
+      const _Float16* al = st + H3_BLK;
+      const _Float16* bh = st + 2 * H3_BLK;
+      const _Float16* bl = st + 3 * H3_BLK;
+      const int kd = kt < nfull ? -100 : (kt - nfull) - 4 * wm;   // 32-row blocks above the diagonal
+      const int imin = kd < 0 ? 0 : kd;
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const int c = 2 * s2 + (lane >> 5);
+        vh8 fbh[4], fbl[4];
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          const int r = wn * 128 + jj * 32 + (lane & 31);
+          fbh[jj] = h3_frag(bh, r, c);
+          fbl[jj] = h3_frag(bl, r, c);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          if (nxt && (i & 1) == 0) {
+            __builtin_amdgcn_sched_barrier(0);
+            issue_part(Ab + (int64_t)(kt + 1) * H3_BLK, Bb + (int64_t)(kt + 1) * H3_BLK, nst, 2 * s2 + (i >> 1));
+            __builtin_amdgcn_sched_barrier(0);
+          }
+          if (i < imin) continue;
+          const int r = wm * 128 + i * 32 + (lane & 31);
+          const vh8 fah = h3_frag(ah, r, c), fal = h3_frag(al, r, c);
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj) {
+            acc[i][jj] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fal, fbh[jj], acc[i][jj], 0, 0, 0);
+            acc[i][jj] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fah, fbl[jj], acc[i][jj], 0, 0, 0);
+            acc[i][jj] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fah, fbh[jj], acc[i][jj], 0, 0, 0);
+          }
+        }
+      }
+    }
+    if (MODE == 1) wait_vmcnt<0>();
+    __syncthreads();
+    double* red = reinterpret_cast<double*>(lds);  // [2][256]
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+      const int cl = wn * 128 + jj * 32 + (lane & 31);
+      double sum = 0.0;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) sum += (double)acc[i][jj][r] * (double)acc[i][jj][r];
+      sum += __shfl_xor(sum, 32);
+      if ((lane >> 5) == 0) red[wm * 256 + cl] = sum;
+    }
+    __syncthreads();
+    {
+      const int64_t col = (int64_t)ct * 256 + t;
+      if (col < m) part[(int64_t)rt * ldp + col] = (red[t] + red[256 + t]) * unscale2;
+    }
+  }
+}
+
 }  // namespace ut
 
 using namespace ut;
@@ -373,6 +487,14 @@ int main(int argc, char** argv) {
                        amax, -14);
   });
   colsum(RT2, ref);
+  timeit("q4: one wave per SIMD, 128 x 128 per wave", [&] {
+    hipLaunchKernelGGL((k_h3q<0>), dim3(ncu), dim3(256), 0, 0, Ab, na, Bb, nb, npad, RT2, CT, m, ticket, part, ldk, 1.0);
+  });
+  colsum(RT2, got);
+  cmp("q4");
+  timeit("q4 no refills", [&] {
+    hipLaunchKernelGGL((k_h3q<1>), dim3(ncu), dim3(256), 0, 0, Ab, na, Bb, nb, npad, RT2, CT, m, ticket, part, ldk, 1.0);
+  });
   W3RUN(32, 2, 0, "w3 BK32 NS2 (row-major planes)");
   colsum(RT2, got);
   cmp("w3 BK32 NS2");
