@@ -25,7 +25,7 @@ def make_spy(cls, key, at_round):
     def spy(self):
         out = orig(self)
         if key not in cap and self.round >= at_round:
-            cap[key] = dict(vals=out[0].clone(), X=self.model._X.copy(), y=np.asarray(self.model._y).copy(),
+            cap[key] = dict(vals=out[0].clone(), X=self.model._Xa[:self.model._n].copy(), y=self.model._ya[:self.model._n].copy(),
                             eng=self.engine, round=self.round)
         return out
     cls._local_round = spy

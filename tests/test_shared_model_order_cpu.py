@@ -66,3 +66,71 @@ def test_rows_best_first_at_refit_appended_between():
     # no change -> no new fit
     n = len(m.engine.fits)
     assert m.fit(d) and len(m.engine.fits) == n
+
+
+def test_selection_features_equal_features_host():
+    """the features a round encodes beside its selections (GpuBatchTechnique._round,
+    SharedModel.remember_features) are bitwise the ones features_host gives the
+    results' configurations (an enum option listed twice included: proposals
+    carry its first index, as encode_configs does)"""
+    from _oracle_engine import OracleEngine
+    from uptune_amd import technique as T
+    from uptune_amd.driver import SearchDriver
+    from uptune_amd.manipulator import (BooleanParameter, ConfigurationManipulator, EnumParameter, FloatParameter,
+                                        IntegerParameter)
+
+    class Counting(OracleEngine):
+        rows_host = 0
+
+        def features_host(self, cfgs):
+            Counting.rows_host += len(cfgs)
+            return super().features_host(cfgs)
+
+    space = ConfigurationManipulator([FloatParameter("x", -2.0, 2.0), IntegerParameter("n", 0, 50),
+                                      EnumParameter("e", ["a", "b", "a", "c"]), BooleanParameter("b")])
+
+    def obj(c):
+        return (c["x"] - 0.3) ** 2 + 0.01 * c["n"] + (-0.5 if c["e"] == "a" else 0.0) + (0.1 if c["b"] else 0.0)
+
+    drv = SearchDriver(space, T.GpuGA(name="ga", pool=256, batch=4, population=32, seed=5, lengthscale=0.5,
+                                      engine_factory=Counting), parallelism=4)
+    drv.main(obj, test_limit=48, max_generations=12)
+    sm = drv.root_technique.model
+    assert sm.fits >= 5 and sm._n >= 24
+    res = drv.results_query()[:sm._n]
+    want = sm.engine.features_host([r.configuration.data for r in res])
+    assert np.array_equal(sm._Xa[:sm._n].view(np.int64), want.view(np.int64))
+    assert np.array_equal(sm._ya[:sm._n], [r.time for r in res])
+    Counting.rows_host -= len(res)            # the check above
+    assert Counting.rows_host < sm._n         # most rows came from the rounds' encodings
+
+
+def test_selection_with_two_encodings_is_not_cached():
+    """a selected value column that does not re-encode to the same bits (an enum
+    option listed twice, at its second index) keeps no round encoding: its
+    result is encoded by features_host"""
+    import torch
+    from _oracle_engine import OracleEngine
+    from uptune_amd import technique as T
+    from uptune_amd.driver import SearchDriver
+    from uptune_amd.manipulator import ConfigurationManipulator, EnumParameter, FloatParameter
+
+    class Fixed(T.GpuGA):
+        def _local_round(self):
+            eng = self._ensure_engine()
+            rows = torch.zeros((eng.spec.ncols, 2), dtype=torch.float64)
+            for ps in eng.spec.params:
+                rows[ps.col] = torch.tensor([0.25, -0.5] if ps.name == "x" else [2.0, 1.0])   # e: "a" (2nd), "b"
+            return rows, torch.tensor([0, 1]), torch.zeros(2, dtype=torch.float64), eng.hash(rows), rows
+
+    space = ConfigurationManipulator([FloatParameter("x", -2.0, 2.0), EnumParameter("e", ["a", "b", "a", "c"])])
+    drv = SearchDriver(space, Fixed(name="ga", pool=16, batch=2, population=8, seed=1, engine_factory=OracleEngine),
+                       parallelism=2)
+    t = drv.root_technique
+    t._round()
+    cache = t.model._feat_cache
+    (c0, h0), (c1, h1) = t.queue
+    assert c0["e"] == "a" and c1["e"] == "b"
+    assert h0 not in cache and h1 in cache
+    want = t.engine.features_host([c1])[0]
+    assert np.array_equal(cache[h1].view(np.int64), want.view(np.int64))

@@ -562,8 +562,13 @@ __global__ void k_gp_finalize(int64_t m, int32_t RT1, int32_t RT2, const double*
 // ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
-static int gp_alloc(ut_ctx* c, int32_t npad, int32_t d) {
-  if (c->gp_cap_n >= npad && c->gp_d == d && c->gp_Xs) return 0;
+static int gp_alloc(ut_ctx* c, int32_t npad_need, int32_t d) {
+  if (c->gp_cap_n >= npad_need && c->gp_d == d && c->gp_Xs) return 0;
+  // room for a growing training set (the tuning loop adds a few rows per fit):
+  // a new padded size then reuses the buffers instead of freeing and
+  // allocating ~5 n^2 doubles behind a device-wide sync (2.5-10 ms per 128
+  // rows in the C5 loop).  Every kernel indexes with the fit's own npad.
+  const int64_t npad = ((npad_need + npad_need / 4 + NPAD - 1) / NPAD) * NPAD;
   if (c->gp_Xs_f) {
     UT_HIP(c, ut::sync_all(c));
     hipFree(c->gp_Xs_f); hipFree(c->gp_LinvT); hipFree(c->gp_LinvT_f); hipFree(c->gp_T); hipFree(c->gp_ctr);

@@ -3,6 +3,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <algorithm>
 #include <functional>
 #include <initializer_list>
 #include <string>
@@ -355,18 +356,25 @@ struct StreamScope {
 template <class T>
 int ensure(ut_ctx* c, DevBuf<T>& b, size_t n) {
   if (b.n >= n && b.p) return 0;
+  // a buffer that has to grow again (sizes that follow a growing training
+  // set) gets headroom, up to 2 GiB: every regrowth costs a device-wide sync
+  size_t want = n;
   if (b.p) {
+    want = n + std::min(n / 4, ((size_t)2 << 30) / sizeof(T));
     hipError_t e = ut::sync_all(c);
     (void)e;
     (void)hipFree(b.p);
     b.p = nullptr;
     b.n = 0;
   }
-  size_t bytes = n * sizeof(T);
-  if (bytes == 0) bytes = sizeof(T);
-  hipError_t e = hipMalloc((void**)&b.p, bytes);
+  hipError_t e = hipMalloc((void**)&b.p, (want ? want : 1) * sizeof(T));
+  if (e != hipSuccess && want > n) {   // no room for the headroom: exactly n
+    (void)hipGetLastError();
+    want = n;
+    e = hipMalloc((void**)&b.p, (want ? want : 1) * sizeof(T));
+  }
   if (e != hipSuccess) return set_err(c, UT_ENOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
-  b.n = n;
+  b.n = want;
   return 0;
 }
 

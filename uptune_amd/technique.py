@@ -289,12 +289,22 @@ class SharedModel:
         self._req_seen = 0          # requests_query() rows pushed to the device set (list drivers)
         self._hist = set()          # digests pushed (any driver)
         self._res_ids: List[Any] = []
-        self._X = None
-        self._y: List[float] = []
-        # the fit's row order (a permutation of the results): best y first as of
-        # the last refit, the results since appended in arrival order
-        self._perm = None
+        # training rows in arrival order (features, objective): the first _n
+        # rows of capacity-grown buffers, so a fit that appends a few results
+        # copies only those
+        self._n = 0
+        self._Xa = np.zeros((0, 0))
+        self._ya = np.zeros(0)
+        # the same rows in the fit's order (what gp_fit receives): best y first
+        # as of the last refit, the results since appended in arrival order
+        self._Xf = np.zeros((0, 0))
+        self._yf = np.zeros(0)
+        self._nf = 0
         self._perm_npad = 0
+        # features of the rounds' selections, encoded on the device beside
+        # them (GpuBatchTechnique._round), by hash_config digest: a result of a
+        # selected configuration needs no second encode round trip
+        self._feat_cache: Dict[str, np.ndarray] = {}
         self._fit_key = None
         self._fit_unverified = False
         self.fits = 0
@@ -385,14 +395,16 @@ class SharedModel:
         key = (len(rows), ids[-1])
         if key == self._fit_key:
             return True
-        k = len(self._res_ids)
-        if self._X is None or ids[:k] != self._res_ids:      # not an append: re-encode everything
-            self._X, self._y, self._res_ids, k = np.zeros((0, self.engine.spec.n_features)), [], [], 0
-            self._perm = None
+        k = self._n
+        if k == 0 or ids[:k] != self._res_ids:      # not an append: re-encode everything
+            k = self._n = self._nf = 0
         new = rows[k:]
         if new:
-            self._X = np.vstack([self._X, self.engine.features_host([r.configuration.data for r in new])])
-            self._y += [float(r.time) for r in new]
+            n = k + len(new)
+            self._Xa, self._ya = _rows_room(self._Xa, self._ya, k, n, self.engine.spec.n_features)
+            self._Xa[k:n] = self._features(new)
+            self._ya[k:n] = [float(r.time) for r in new]
+            self._n = n
             self._res_ids = list(ids)   # a copy: the scan list keeps growing
         # Row order.  The GP posterior does not depend on it, but the EI bound of
         # pruned scoring (ut_gp_topk_pruned) comes from the first rows of L^-1:
@@ -403,20 +415,57 @@ class SharedModel:
         # the device refits anyway (a new padded size, gp.hip NPAD = 128, or a
         # re-encode); in between the new results are appended, so the
         # incremental fit still applies.
-        y = np.asarray(self._y)
-        n = len(y)
+        n = self._n
         npad = -(-n // 128) * 128
-        if self._perm is None or npad != self._perm_npad or len(self._perm) > n:
-            self._perm = np.argsort(y, kind="stable")
+        self._Xf, self._yf = _rows_room(self._Xf, self._yf, self._nf, n, self._Xa.shape[1])
+        if self._nf == 0 or npad != self._perm_npad or self._nf > n:
+            perm = np.argsort(self._ya[:n], kind="stable")
+            self._Xf[:n] = self._Xa[perm]
+            self._yf[:n] = self._ya[perm]
             self._perm_npad = npad
-        elif len(self._perm) < n:
-            self._perm = np.concatenate([self._perm, np.arange(len(self._perm), n)])
-        self.engine.gp_fit(self._X[self._perm], y[self._perm], lengthscale=self.lengthscale, wait=False,
-                           **self.hyper)
+        else:
+            self._Xf[self._nf:n] = self._Xa[self._nf:n]
+            self._yf[self._nf:n] = self._ya[self._nf:n]
+        self._nf = n
+        self.engine.gp_fit(self._Xf[:n], self._yf[:n], lengthscale=self.lengthscale, wait=False, **self.hyper)
         self._fit_key = key
         self._fit_unverified = True
         self.fits += 1
         return True
+
+    def remember_features(self, hexes, feat) -> None:
+        """features [k][F] of configurations selected this round, by digest"""
+        if len(self._feat_cache) > (1 << 16):   # selections never evaluated: bounded
+            self._feat_cache.clear()
+        for hx, f in zip(hexes, feat):
+            self._feat_cache[hx] = f
+
+    def _features(self, results) -> np.ndarray:
+        """GP features of results: the round's device encoding where the result's
+        configuration is one of the selections, else encoded now"""
+        out = np.empty((len(results), self.engine.spec.n_features))
+        miss = []
+        for i, r in enumerate(results):
+            f = self._feat_cache.pop(getattr(r.configuration, "hash", None), None)
+            if f is None:
+                miss.append(i)
+            else:
+                out[i] = f
+        if miss:
+            out[miss] = self.engine.features_host([results[i].configuration.data for i in miss])
+        return out
+
+
+def _rows_room(X, y, used, n, d):
+    """(X, y) with room for n rows of d features, the first `used` rows kept"""
+    if X.shape[0] >= n and X.shape[1] == d:
+        return X, y
+    cap = max(n + n // 2, 256)
+    X2, y2 = np.empty((cap, d)), np.empty(cap)
+    used = min(used, n, X.shape[0])
+    if used and X.shape[1] == d:
+        X2[:used], y2[:used] = X[:used], y[:used]
+    return X2, y2
 
 
 class GpuBatchTechnique(SearchTechnique):
@@ -580,11 +629,33 @@ class GpuBatchTechnique(SearchTechnique):
                                                       with_digests=True)
         else:
             vals, idx, top, dig, rows = self._local_round()
-        keep = (idx >= 0)
-        idx, rows, dig = idx[keep], rows[:, keep], dig[keep]
-        cfgs = self.engine.decode(rows)
-        self.queue.extend(zip(cfgs, digests_to_hex(dig)))
-        self.after_round(idx, digests_to_hex(dig))
+        import torch
+        eng = self.engine
+        # the selections (and, for the GP's next fit, their features) reach the
+        # host in ONE copy: global indices, value rows, digests, features
+        feat = eng.encode(rows) if self.surrogate is None else None
+        parts = [idx.contiguous().view(torch.float64), rows.contiguous().reshape(-1),
+                 dig.to(torch.int32).contiguous().view(torch.float64).reshape(-1)]
+        if feat is not None:
+            parts.append(feat.contiguous().reshape(-1))
+        host = torch.cat(parts).cpu().numpy()
+        k, ncol = idx.numel(), rows.shape[0]
+        o1, o2 = k + ncol * k, k + ncol * k + 4 * k
+        keep = host[:k].view(np.int64) >= 0
+        idx_h = host[:k].view(np.int64)[keep]
+        rows_h = host[k:o1].reshape(ncol, k)[:, keep]
+        hexes = digests_to_hex(host[o1:o2].view(np.int32).reshape(k, 8)[keep])
+        cfgs = eng.spec.decode_values(rows_h)
+        self.queue.extend(zip(cfgs, hexes))
+        if feat is not None:
+            # a result's features are what features_host(config) encodes: keep
+            # those of selections whose config re-encodes to the same value
+            # bits (always, unless a value has two encodings, e.g. an enum
+            # option listed twice)
+            same = (eng.spec.encode_configs(cfgs).view(np.int64) == rows_h.view(np.int64)).all(axis=0)
+            ft = host[o2:].reshape(-1, k)[:, keep].T
+            self.model.remember_features([h for h, s in zip(hexes, same) if s], ft[same])
+        self.after_round(idx_h, hexes)
         self.round += 1
         self.cand_base += (world if self.sharded else 1) * self.pool
 
@@ -631,7 +702,7 @@ class GpuDifferentialEvolution(GpuBatchTechnique):
 
     def after_round(self, idx, hexes):
         npop = self.engine.npop
-        for g, hx in zip(idx.cpu().numpy().tolist(), hexes):   # global index g targets member g % npop
+        for g, hx in zip(np.asarray(idx).tolist(), hexes):   # global index g targets member g % npop
             self._pending[hx] = g % npop
 
     def handle_requested_result(self, result):
