@@ -599,7 +599,7 @@ static int gp_alloc(ut_ctx* c, int32_t npad_need, int32_t d) {
   // fp32: (L^-1)^T; h3: the blocked fp16 hi / lo planes, rows padded to 256
   UT_HIP(c, hipMalloc((void**)&c->gp_LinvT_f, sizeof(float) * (((npad + 255) / 256) * 256) * npad));
   UT_HIP(c, hipMalloc((void**)&c->gp_ctr, sizeof(int32_t) * 32));
-  UT_HIP(c, hipMalloc((void**)&c->gp_XsT, sizeof(double) * npad * (((d + 15) / 16) * 16)));
+  UT_HIP(c, hipMalloc((void**)&c->gp_XsT, sizeof(double) * npad * kstar_dpad(d)));
   c->gp_cap_n = npad;
   c->gp_d = d;
   return 0;
@@ -677,7 +677,7 @@ int gp_fit_enqueue(ut_ctx* c, const double* X, const double* y, int32_t n, int32
                      c->gp_inv_ell, c->gp_Xs, c->gp_xnorm);
   // the candidate side of K* needs only the scaled inputs: fp64 scoring starts
   // its K* here while the factorisation below is still running
-  if ((rc = launch_xs_t(c, c->gp_Xs, npad, d, ((d + 15) / 16) * 16, c->gp_XsT))) return rc;
+  if ((rc = launch_xs_t(c, c->gp_Xs, npad, d, kstar_dpad(d), c->gp_XsT))) return rc;
   UT_HIP(c, hipEventRecord(c->ev_fit_x, c->stream));
   const double diag = h->sigma_n2 + h->jitter;
   if (app) {
@@ -783,7 +783,7 @@ int gp_encode_scaled(ut_ctx* c, const double* values, int64_t ld, int64_t m) {
   if (m <= 0) return 0;
   // 1/ell comes with the fit's scaled training inputs
   if (c->fit_pending) UT_HIP(c, hipStreamWaitEvent(c->stream, c->ev_fit_x, 0));
-  const int32_t dpad = ((c->gp_d + 15) / 16) * 16;
+  const int32_t dpad = kstar_dpad(c->gp_d);
   const int64_t ldk = ((m + VAR_BN - 1) / VAR_BN) * VAR_BN;   // as gp_score_impl
   int rc;
   if ((rc = ensure(c, c->cnorm, (size_t)ldk))) return rc;
@@ -807,7 +807,7 @@ int gp_score_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, const ut
   if (c->fit_pending) UT_HIP(c, hipStreamWaitEvent(c->stream, fp32 ? c->ev_fit : c->ev_fit_x, 0));
   const int32_t n = c->gp_n, d = c->gp_d;
   const int32_t npad = ((n + NPAD - 1) / NPAD) * NPAD;
-  const int32_t dpad = ((d + 15) / 16) * 16;
+  const int32_t dpad = kstar_dpad(d);
   // K* rows padded to whole variance column tiles: the variance kernel reads
   // full 256-candidate strips (the K* kernel writes zeros past m)
   const int64_t ldk = ((m + VAR_BN - 1) / VAR_BN) * VAR_BN;
@@ -1012,7 +1012,7 @@ int gp_topk_pruned_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, co
   if (c->fit_pending) UT_HIP(c, hipStreamWaitEvent(c->stream, c->ev_fit, 0));   // K* takes mu = k* . alpha
   const int32_t n = c->gp_n, d = c->gp_d;
   const int32_t npad = ((n + NPAD - 1) / NPAD) * NPAD;
-  const int32_t dpad = ((d + 15) / 16) * 16;
+  const int32_t dpad = kstar_dpad(d);
   const int32_t RT = npad / NPAD;
   int32_t R = (bound_rows + NPAD - 1) / NPAD;
   R = R < 1 ? 1 : (R > RT ? RT : R);

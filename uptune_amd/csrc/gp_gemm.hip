@@ -76,8 +76,11 @@ constexpr int K_SA = K_BK * K_BM, K_SB = K_BK * K_BN, K_STAGE = K_SA + K_SB;
 
 __device__ __forceinline__ void kstar_issue(const double* __restrict__ AT, int64_t lda, const double* __restrict__ B,
                                             int64_t ldb, int32_t row0, int64_t col0, int32_t k0, double* st, int w,
-                                            int lane) {
-  // 16 KiB of A and 16 KiB of B per stage = 32 wave-instructions, 8 per wave
+                                            int lane, int32_t dpad) {
+  // 16 KiB of A and 16 KiB of B per stage = 32 wave-instructions, 8 per wave;
+  // wave w loads k rows 4w .. 4w+3, none past dpad (a multiple of 4: the last
+  // stage of a dpad that is not a multiple of 16 is partial)
+  if (k0 + 4 * w >= dpad) return;
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
     const int q = 4 * w + u;  // 0..15: A tile row k = q (128 doubles = 1 KiB)
@@ -91,6 +94,8 @@ __device__ __forceinline__ void kstar_issue(const double* __restrict__ AT, int64
     __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(st + K_SA + q * 128), 16, 0, 0);
   }
 }
+
+typedef double kd4 __attribute__((ext_vector_type(4)));
 
 // MU: also the column partial of the mean, sum_r alpha_r k*_r (fp32 scoring;
 // fp64 takes the mean from the variance epilogue instead)
@@ -136,8 +141,10 @@ __global__ __launch_bounds__(K_NT, 2) void k_gp_kstar(const double* __restrict__
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
   const int wm = w >> 1, wn = w & 1;
   const int32_t xcd = blockIdx.x & 7;
-  const int32_t nk = dpad / K_BK;
-  typedef double d4 __attribute__((ext_vector_type(4)));
+  // dpad % 4 == 0: whole 16-k stages, then one stage of k_rem k4 steps
+  const int32_t nk_full = dpad / K_BK, k_rem = (dpad % K_BK) / 4;
+  const int32_t nk = nk_full + (k_rem ? 1 : 0);
+  typedef kd4 d4;
 
   for (;;) {
     if (t == 0) s_item = atomicAdd(&ticket[xcd], 1);
@@ -155,7 +162,7 @@ __global__ __launch_bounds__(K_NT, 2) void k_gp_kstar(const double* __restrict__
 #pragma unroll
       for (int jj = 0; jj < 4; ++jj) acc[i][jj] = (d4){0.0, 0.0, 0.0, 0.0};
 
-    kstar_issue(AT, lda, B, ldb, row0, col0, 0, lds, w, lane);
+    kstar_issue(AT, lda, B, ldb, row0, col0, 0, lds, w, lane, dpad);
     {  // one 1-KiB glds per operand (rows < npad, columns < ldk are in range)
       const double* src = w == 0 ? xnorm + row0 : (w == 1 ? alpha + row0 : cnorm + col0);
       if (w < 3 && (MU || w != 1))
@@ -166,11 +173,15 @@ __global__ __launch_bounds__(K_NT, 2) void k_gp_kstar(const double* __restrict__
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();  // stage kt landed everywhere; stage kt-1 fully read
       asm volatile("" ::: "memory");
-      if (kt + 1 < nk) kstar_issue(AT, lda, B, ldb, row0, col0, (kt + 1) * K_BK, lds + ((kt + 1) & 1) * K_STAGE, w, lane);
+      if (kt + 1 < nk)
+        kstar_issue(AT, lda, B, ldb, row0, col0, (kt + 1) * K_BK, lds + ((kt + 1) & 1) * K_STAGE, w, lane, dpad);
       const double* as = lds + (kt & 1) * K_STAGE;
       const double* bs = as + K_SA;
+      // the last stage of a dpad that is not a multiple of 16 has k_rem k4 steps
+      const int nks = kt < nk_full ? K_BK / 4 : k_rem;
 #pragma unroll
       for (int ks = 0; ks < K_BK / 4; ++ks) {
+        if (ks >= nks) break;
         const int kr = ks * 4 + (lane >> 4);
         double af[4], bf[4];
 #pragma unroll
@@ -280,7 +291,7 @@ int h3_kstar_exp(double sf2) { return H3_KSCALE_EXP - ilogb(sf2); }  // sf2 * 2^
 int launch_gemm_kstar(ut_ctx* c, int prec, const double* XsT, int32_t npad, const double* ucand, int32_t dpad,
                       int64_t m, void* kst, int64_t ldk, double* part, int32_t store_rows, const double* cn,
                       double* part2) {
-  UT_CHECK(c, npad % K_BM == 0 && dpad % K_BK == 0 && ldk % K_BN == 0 && ldk >= m, UT_EINVAL,
+  UT_CHECK(c, npad % K_BM == 0 && dpad % 4 == 0 && dpad >= 4 && ldk % K_BN == 0 && ldk >= m, UT_EINVAL,
            "gemm_kstar: bad padding");
   UT_CHECK(c, prec == 64 || prec == 32 || prec == 16, UT_EINVAL, "gemm_kstar: bad precision");
   UT_CHECK(c, part != nullptr || prec == 64, UT_EINVAL,

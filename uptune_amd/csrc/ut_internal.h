@@ -353,6 +353,9 @@ struct StreamScope {
       return ::ut::set_err((ctx), UT_EHIP, std::string("launch: ") + hipGetErrorString(e_)); \
   } while (0)
 
+// feature rows of the K* operands (Xs^T, U'): d rounded up to the f64 MFMA's k = 4
+inline int32_t kstar_dpad(int32_t d) { return ((d + 3) / 4) * 4; }
+
 template <class T>
 int ensure(ut_ctx* c, DevBuf<T>& b, size_t n) {
   if (b.n >= n && b.p) return 0;
