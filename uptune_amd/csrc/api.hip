@@ -213,6 +213,7 @@ int ut_ctx_destroy(ut_ctx* c) {
     fr(c->pop_slots[s].pop_aos);
   }
   fr(c->r_mask.p); fr(c->r_fresh.p); fr(c->r_pairs.p); fr(c->r_npairs.p); fr(c->de_xbits.p); fr(c->par_dig.p);
+  fr(c->hs_mask.p); fr(c->hs_fresh.p);
   fr(c->pr_mu.p); fr(c->pr_ub.p); fr(c->pr_score.p); fr(c->pr_mpart.p); fr(c->pr_kst.p); fr(c->pr_vpart.p);
   fr(c->pr_idx.p); fr(c->pr_count.p); fr(c->pr_ucand.p); fr(c->pr_cnorm.p);
   fr(c->pr_k2.p); fr(c->pr_f2.p); fr(c->pr_exact.p); fr(c->app_ws.p); fr(c->var_vbuf.p);

@@ -276,6 +276,8 @@ struct ut_ctx {
   ut::DevBuf<int64_t> r_npairs;     // [1] their count
   ut::DevBuf<uint32_t> de_xbits;    // k_de's cr-test bits when they outgrow LDS (> 2048 params)
   ut::DevBuf<uint32_t> par_dig;     // [n_comp][16]: hex inner digests of ut_hash_parent's parent row
+  ut::DevBuf<uint32_t> hs_mask;     // small-m ut_hash: all-ones reuse mask [ceil(n_comp / 32)][ld]
+  ut::DevBuf<uint32_t> hs_fresh;    // small-m ut_hash: every inner digest, hex [n_comp][ld][16]
   // EI-bound pruned scoring (gp.hip ut_gp_topk_pruned)
   ut::DevBuf<double> pr_mu, pr_ub, pr_score;   // [ld] exact mean, score bound, exact scores (-inf if pruned)
   ut::DevBuf<double> pr_mpart;                 // [RT][ldk] unused mean partials of the bound / survivor GEMMs
