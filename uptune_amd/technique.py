@@ -433,6 +433,16 @@ class SharedModel:
         self.fits += 1
         return True
 
+    def note_selections(self, hexes) -> None:
+        """a round's selections are requests the driver has not made yet: they
+        join the dedup set now, so no technique sharing this model selects one
+        of them again while it waits in a queue (a bandit runs other techniques'
+        rounds between the requests of one round's batch)"""
+        new = [h for h in hexes if h not in self._hist]
+        if new:
+            self._hist.update(new)
+            self.engine.history_add(new)
+
     def remember_features(self, hexes, feat) -> None:
         """features [k][F] of configurations selected this round, by digest"""
         if len(self._feat_cache) > (1 << 16):   # selections never evaluated: bounded
@@ -647,6 +657,7 @@ class GpuBatchTechnique(SearchTechnique):
         hexes = digests_to_hex(host[o1:o2].view(np.int32).reshape(k, 8)[keep])
         cfgs = eng.spec.decode_values(rows_h)
         self.queue.extend(zip(cfgs, hexes))
+        self.model.note_selections(hexes)
         if feat is not None:
             # a result's features are what features_host(config) encodes: keep
             # those of selections whose config re-encodes to the same value
