@@ -134,3 +134,28 @@ def test_selection_with_two_encodings_is_not_cached():
     assert h0 not in cache and h1 in cache
     want = t.engine.features_host([c1])[0]
     assert np.array_equal(cache[h1].view(np.int64), want.view(np.int64))
+
+
+def test_queued_selections_are_in_the_dedup_set():
+    """two techniques sharing one model: the second round, run before any of the
+    first round's selections is requested, selects none of them (the same
+    technique twice proposes the same candidates, so without the round-time
+    dedup entries the two queues would be equal)"""
+    from _oracle_engine import OracleEngine
+    from uptune_amd import technique as T
+    from uptune_amd.driver import SearchDriver
+    from uptune_amd.manipulator import ConfigurationManipulator, FloatParameter, IntegerParameter
+
+    space = ConfigurationManipulator([FloatParameter("x", -2.0, 2.0), IntegerParameter("n", 0, 50)])
+    sm = T.SharedModel(seed=4, engine_factory=OracleEngine)
+    kw = dict(pool=64, batch=4, population=16, seed=4, shared=sm)
+    drv = SearchDriver(space, T.MetaSearchTechnique([T.GpuGA(name="a", **kw), T.GpuGA(name="b", **kw)]),
+                       parallelism=4)
+    a, b = drv.root_technique.techniques
+    assert a.model is b.model
+    a._round()
+    b._round()
+    ha = {h for _, h in a.queue}
+    hb = {h for _, h in b.queue}
+    assert len(ha) == 4 and len(hb) == 4 and not (ha & hb)
+    assert ha | hb <= a.model._hist
