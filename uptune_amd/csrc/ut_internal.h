@@ -187,6 +187,11 @@ struct ut_ctx {
   // 1: fp32 / f16x3 dense rounds hold the hash for an in-flight fit as well
   // (their K* waits for the whole fit anyway); UT_HASH_HOLD_LOWPREC
   int32_t hash_hold_lowprec = 0;
+  // pruned rounds: the hash also waits for an in-flight fit (UT_HASH_HOLD_PRUNED)
+  int32_t hash_hold_pruned = 0;
+  // the side stream (hash + dedup) on all CUs but a few per XCD, left to the fit's
+  // latency-bound chain of small kernels (UT_SIDE_CU_MASK)
+  int32_t side_cu_mask = 0;
   // fp32 / f16x3 dense rounds: 1 = enqueue the hash after K* (their K* waits
   // for the whole fit, which the hash would otherwise crowd out of the CUs: at
   // n = 4096 the refit stretches from ~6 to ~14 ms beside it) and let the
