@@ -12,10 +12,10 @@ one() { local tag=$1 envs=$2; shift 2
   python3 -c "import json; d=json.loads([l for l in open('$O/x.log') if l.startswith('{')][-1]); print('$tag', '$envs', round(d['ms_per_step'],2), {k: round(v,2) for k,v in d['stage_ms'].items() if k in ('hash','kstar','var','dedup')})"
 }
 for rep in 1 2; do
-  for e in "X=0" "UT_SIDE_CU_MASK=1" "UT_HASH_HOLD_PRUNED=1" "UT_SIDE_CU_MASK=1 UT_HASH_HOLD_PRUNED=1"; do
+  for e in "X=0" "UT_CHOL_FUSE=1" "UT_SIDE_CU_MASK=1" "UT_HASH_HOLD_PRUNED=1" "UT_CHOL_FUSE=1 UT_SIDE_CU_MASK=1"; do
     one c3p "$e" --config c3 --prune 256 --steps 5 --warmup 2
   done
-  for e in "X=0" "UT_SIDE_CU_MASK=1"; do
+  for e in "X=0" "UT_CHOL_FUSE=1" "UT_SIDE_CU_MASK=1"; do
     one c3h "$e" --config c3 --precision 16 --steps 5 --warmup 2
     one c2 "$e" --steps 20 --warmup 3
   done

@@ -200,6 +200,7 @@ int ut_ctx_create(int device, uint64_t seed, ut_ctx** out) {
     }
   }
   if (const char* e = getenv("UT_HASH_HOLD_PRUNED")) c->hash_hold_pruned = atoi(e) != 0;
+  if (const char* e = getenv("UT_CHOL_FUSE")) c->chol_fuse = atoi(e) != 0;
   if (const char* e = getenv("UT_JOIN_BEFORE_VAR")) c->join_before_var = atoi(e) != 0;
   if (const char* e = getenv("UT_VAR_KERNEL")) c->var_kernel = atoi(e);
   if (const char* e = getenv("UT_VAR_SPLIT")) c->var_split = atoi(e) != 0;

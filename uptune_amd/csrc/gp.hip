@@ -155,18 +155,15 @@ __device__ __forceinline__ double readlane_f64(double v, int lane) {
   return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
 }
 
-__global__ __launch_bounds__(256) void k_chol_diag(double* __restrict__ K, double* __restrict__ Li, int32_t npad,
-                                                   int32_t kb, int32_t* flag) {
-  __shared__ double col[2][NB];
-  __shared__ double Ls[NB * (NB + 1)];
-  __shared__ double invd[NB];
+// the diagonal block kb from a[] (thread t: row t & 63, columns 16 (t >> 6) ..
+// + 15 of the updated block); col [2][NB], Ls [NB][NB + 1], invd [NB] in LDS
+__device__ __forceinline__ void chol_diag_core(double (&a)[16], double* __restrict__ K, double* __restrict__ Li,
+                                               int32_t npad, int32_t kb, int32_t* flag, double (*col)[NB],
+                                               double* Ls, double* invd) {
   const int t = threadIdx.x, r = t & 63;
   const int g = __builtin_amdgcn_readfirstlane(t >> 6);
   const int64_t base = (int64_t)kb * NB;
   double* rowp = K + (base + r) * npad + base + 16 * g;
-  double a[16];
-#pragma unroll
-  for (int j = 0; j < 16; ++j) a[j] = rowp[j];
   for (int cb = 0; cb < NB / 16; ++cb) {
 #pragma unroll
     for (int cc = 0; cc < 16; ++cc) {
@@ -213,6 +210,21 @@ __global__ __launch_bounds__(256) void k_chol_diag(double* __restrict__ K, doubl
   for (int j = 0; j < 16; ++j) lip[j] = b[j] * ir;
 }
 
+__global__ __launch_bounds__(256) void k_chol_diag(double* __restrict__ K, double* __restrict__ Li, int32_t npad,
+                                                   int32_t kb, int32_t* flag) {
+  __shared__ double col[2][NB];
+  __shared__ double Ls[NB * (NB + 1)];
+  __shared__ double invd[NB];
+  const int t = threadIdx.x, r = t & 63;
+  const int g = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int64_t base = (int64_t)kb * NB;
+  const double* rowp = K + (base + r) * npad + base + 16 * g;
+  double a[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) a[j] = rowp[j];
+  chol_diag_core(a, K, Li, npad, kb, flag, col, Ls, invd);
+}
+
 // Panel kb, step 2: row block i > kb:  L_ik = A_ik * inv(L_kk)^T  (NT product)
 __global__ __launch_bounds__(256) void k_chol_rows(double* __restrict__ K, const double* __restrict__ Li,
                                                    int32_t npad, int32_t kb) {
@@ -254,6 +266,59 @@ __global__ __launch_bounds__(256) void k_chol_update(double* __restrict__ K, int
     for (int b = 0; b < 2; ++b)
 #pragma unroll
       for (int r = 0; r < 4; ++r) K[(ib + tile_row(a, r)) * npad + jb + tile_col(b)] -= acc[a][b][r];
+}
+
+// k_chol_update with the next panel's diagonal block factored in the same
+// launch: the workgroup that updates block (kb + 1, kb + 1) keeps it in LDS
+// and runs k_chol_diag's steps on it while the others update the rest, so the
+// fit's serial chain loses one launch per level (UT_CHOL_FUSE)
+__global__ __launch_bounds__(256) void k_chol_update_diag(double* __restrict__ K, double* __restrict__ Li,
+                                                          int32_t npad, int32_t kb, int32_t* flag) {
+  // As / Bs of the tile product, then (workgroup 0) Ls, col, invd of the diagonal block
+  __shared__ double sm[NB * (NB + 1) + 2 * NB + NB];
+  double* As = sm;
+  double* Bs = sm + 16 * 80;
+  const int32_t tid = blockIdx.x;
+  int32_t i = 0;
+  while ((i + 1) * (i + 2) / 2 <= tid) ++i;
+  const int32_t j = tid - i * (i + 1) / 2;
+  const int64_t ib = (int64_t)(kb + 1 + i) * NB, jb = (int64_t)(kb + 1 + j) * NB, cb = (int64_t)kb * NB;
+  fd4 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) acc[a][b] = (fd4){0.0, 0.0, 0.0, 0.0};
+  tile64_nt(K + ib * npad + cb, npad, K + jb * npad + cb, npad, NB, As, Bs, acc);
+  if (tid != 0) {
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) K[(ib + tile_row(a, r)) * npad + jb + tile_col(b)] -= acc[a][b][r];
+    return;
+  }
+  // block (kb + 1, kb + 1): the updated values (the same arithmetic as the
+  // store above) into LDS, then the diagonal steps on them
+  double* Ls = sm;
+  double(*col)[NB] = reinterpret_cast<double(*)[NB]>(sm + NB * (NB + 1));
+  double* invd = sm + NB * (NB + 1) + 2 * NB;
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int tr = tile_row(a, r), tc = tile_col(b);
+        Ls[tr * (NB + 1) + tc] = K[(ib + tr) * npad + jb + tc] - acc[a][b][r];
+      }
+  __syncthreads();
+  const int t = threadIdx.x, rr = t & 63, g = t >> 6;
+  double av[16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) av[q] = Ls[rr * (NB + 1) + 16 * g + q];
+  __syncthreads();   // Ls is rewritten by the substitution's setup
+  chol_diag_core(av, K, Li, npad, kb + 1, flag, col, Ls, invd);
 }
 
 // K = sf2 exp(-0.5 |xs_i - xs_j|^2) + diag I, 64 x 64 tiles on fp64 MFMA;
@@ -721,11 +786,17 @@ int gp_fit_enqueue(ut_ctx* c, const double* X, const double* y, int32_t n, int32
     const int32_t nb = npad / NB;
     UT_HIP(c, hipMemsetAsync(c->gp_Linv, 0, sizeof(double) * npad * npad, c->stream));
     for (int32_t kb = 0; kb < nb; ++kb) {
-      hipLaunchKernelGGL(k_chol_diag, dim3(1), dim3(256), 0, c->stream, c->gp_K, c->gp_Linv, npad, kb, c->gp_flag);
+      // (fused: diagonal blocks after the first come from the previous update)
+      if (!c->chol_fuse || kb == 0)
+        hipLaunchKernelGGL(k_chol_diag, dim3(1), dim3(256), 0, c->stream, c->gp_K, c->gp_Linv, npad, kb, c->gp_flag);
       const int32_t T = nb - kb - 1;
       if (T > 0) {
         hipLaunchKernelGGL(k_chol_rows, dim3(T), dim3(256), 0, c->stream, c->gp_K, c->gp_Linv, npad, kb);
-        hipLaunchKernelGGL(k_chol_update, dim3(T * (T + 1) / 2), dim3(256), 0, c->stream, c->gp_K, npad, kb);
+        if (c->chol_fuse)
+          hipLaunchKernelGGL(k_chol_update_diag, dim3(T * (T + 1) / 2), dim3(256), 0, c->stream, c->gp_K, c->gp_Linv,
+                             npad, kb, c->gp_flag);
+        else
+          hipLaunchKernelGGL(k_chol_update, dim3(T * (T + 1) / 2), dim3(256), 0, c->stream, c->gp_K, npad, kb);
       }
     }
     UT_LAUNCH_CHECK(c);

@@ -192,6 +192,8 @@ struct ut_ctx {
   // the side stream (hash + dedup) on all CUs but a few per XCD, left to the fit's
   // latency-bound chain of small kernels (UT_SIDE_CU_MASK)
   int32_t side_cu_mask = 0;
+  // refit: the next diagonal block factored inside the trailing update (UT_CHOL_FUSE)
+  int32_t chol_fuse = 0;
   // fp32 / f16x3 dense rounds: 1 = enqueue the hash after K* (their K* waits
   // for the whole fit, which the hash would otherwise crowd out of the CUs: at
   // n = 4096 the refit stretches from ~6 to ~14 ms beside it) and let the
