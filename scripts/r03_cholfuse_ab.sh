@@ -5,6 +5,8 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 O=gpurun_out/cholfuse
 mkdir -p $O
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > $O/pytest_default.log 2>&1
+rc=$?; echo "pytest (default) rc=$rc"; tail -3 $O/pytest_default.log; [ $rc -eq 0 ] || exit $rc
 UT_CHOL_FUSE=1 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > $O/pytest.log 2>&1
 rc=$?; echo "pytest (fused) rc=$rc"; tail -3 $O/pytest.log; [ $rc -eq 0 ] || exit $rc
 for f in 0 1; do
