@@ -186,21 +186,7 @@ int ut_ctx_create(int device, uint64_t seed, ut_ctx** out) {
     return UT_EHIP;
   }
   c->stream = c->own_stream;
-  if (const char* e = getenv("UT_SIDE_CU_MASK")) c->side_cu_mask = atoi(e) != 0;
-  if (c->side_cu_mask) {
-    // CUs i < 8 and i % 32 == 0 stay off the side stream: at least one per XCD
-    // whichever way the mask bits map onto the XCDs (interleaved or XCD-major)
-    std::vector<uint32_t> mask((c->n_cu + 31) / 32, 0u);
-    for (int i = 0; i < c->n_cu; ++i)
-      if (!(i < 8 || i % 32 == 0)) mask[i / 32] |= 1u << (i % 32);
-    hipStream_t s2 = nullptr;
-    if (hipExtStreamCreateWithCUMask(&s2, (uint32_t)mask.size(), mask.data()) == hipSuccess) {
-      hipStreamDestroy(c->side);
-      c->side = s2;
-    }
-  }
-  if (const char* e = getenv("UT_HASH_HOLD_PRUNED")) c->hash_hold_pruned = atoi(e) != 0;
-  if (const char* e = getenv("UT_CHOL_FUSE")) c->chol_fuse = atoi(e) != 0;
+  if (const char* e = getenv("UT_CHOL_FUSE")) c->chol_fuse = atoi(e);
   if (const char* e = getenv("UT_JOIN_BEFORE_VAR")) c->join_before_var = atoi(e) != 0;
   if (const char* e = getenv("UT_VAR_KERNEL")) c->var_kernel = atoi(e);
   if (const char* e = getenv("UT_VAR_SPLIT")) c->var_split = atoi(e) != 0;
@@ -809,10 +795,7 @@ static int score_round_de_impl(ut_ctx* c, const ut_de_params* de, const ut_acq* 
     UT_HIP(c, hipStreamWaitEvent(c->side, c->ev_fork, 0));
     StreamScope on_side(c, c->side);
     mark(c, "");
-    c->round_hash_hold = ((prune_rows == 0 && (c->gp_fit_prec == 64 || c->hash_hold_lowprec)) ||
-                          (prune_rows > 0 && c->hash_hold_pruned))
-                             ? c->hash_after_fit
-                             : 0;
+    c->round_hash_hold = (prune_rows == 0 && (c->gp_fit_prec == 64 || c->hash_hold_lowprec)) ? c->hash_after_fit : 0;
     int r = launch_hash_de(c, c->r_values.p, ld, m, cand_base, c->r_digest.p, true);
     c->round_hash_hold = 0;
     if (r) return r;

@@ -271,7 +271,7 @@ __global__ __launch_bounds__(256) void k_chol_update(double* __restrict__ K, int
 // k_chol_update with the next panel's diagonal block factored in the same
 // launch: the workgroup that updates block (kb + 1, kb + 1) keeps it in LDS
 // and runs k_chol_diag's steps on it while the others update the rest, so the
-// fit's serial chain loses one launch per level (UT_CHOL_FUSE)
+// fit's serial chain loses one launch per level (ut_ctx::chol_fuse)
 __global__ __launch_bounds__(256) void k_chol_update_diag(double* __restrict__ K, double* __restrict__ Li,
                                                           int32_t npad, int32_t kb, int32_t* flag) {
   // As / Bs of the tile product, then (workgroup 0) Ls, col, invd of the diagonal block
@@ -785,14 +785,15 @@ int gp_fit_enqueue(ut_ctx* c, const double* X, const double* y, int32_t n, int32
     UT_LAUNCH_CHECK(c);
     const int32_t nb = npad / NB;
     UT_HIP(c, hipMemsetAsync(c->gp_Linv, 0, sizeof(double) * npad * npad, c->stream));
+    const bool fuse = c->chol_fuse > 0 || (c->chol_fuse < 0 && npad >= 2048);
     for (int32_t kb = 0; kb < nb; ++kb) {
       // (fused: diagonal blocks after the first come from the previous update)
-      if (!c->chol_fuse || kb == 0)
+      if (!fuse || kb == 0)
         hipLaunchKernelGGL(k_chol_diag, dim3(1), dim3(256), 0, c->stream, c->gp_K, c->gp_Linv, npad, kb, c->gp_flag);
       const int32_t T = nb - kb - 1;
       if (T > 0) {
         hipLaunchKernelGGL(k_chol_rows, dim3(T), dim3(256), 0, c->stream, c->gp_K, c->gp_Linv, npad, kb);
-        if (c->chol_fuse)
+        if (fuse)
           hipLaunchKernelGGL(k_chol_update_diag, dim3(T * (T + 1) / 2), dim3(256), 0, c->stream, c->gp_K, c->gp_Linv,
                              npad, kb, c->gp_flag);
         else

@@ -187,13 +187,11 @@ struct ut_ctx {
   // 1: fp32 / f16x3 dense rounds hold the hash for an in-flight fit as well
   // (their K* waits for the whole fit anyway); UT_HASH_HOLD_LOWPREC
   int32_t hash_hold_lowprec = 0;
-  // pruned rounds: the hash also waits for an in-flight fit (UT_HASH_HOLD_PRUNED)
-  int32_t hash_hold_pruned = 0;
-  // the side stream (hash + dedup) on all CUs but a few per XCD, left to the fit's
-  // latency-bound chain of small kernels (UT_SIDE_CU_MASK)
-  int32_t side_cu_mask = 0;
-  // refit: the next diagonal block factored inside the trailing update (UT_CHOL_FUSE)
-  int32_t chol_fuse = 0;
+  // refit: the next diagonal block factored inside the trailing update
+  // (k_chol_update_diag). -1 = from 2048 padded rows on: the fit alone 6.5 ->
+  // 5.7 ms at n = 4096, C3 pruned 60.1 -> 59.2 ms; at C2 (n = 1024, the fit
+  // beside K*) the heavier update workgroups cost the round 0.25 ms. UT_CHOL_FUSE
+  int32_t chol_fuse = -1;
   // fp32 / f16x3 dense rounds: 1 = enqueue the hash after K* (their K* waits
   // for the whole fit, which the hash would otherwise crowd out of the CUs: at
   // n = 4096 the refit stretches from ~6 to ~14 ms beside it) and let the
