@@ -15,13 +15,19 @@ top-k (+ all-gather merge of the local top-k over RCCL when N > 1).
 N > 1: one process per GPU.  Under torch.distributed.run (WORLD_SIZE set)
 each process is one rank; run directly with --gpus N, the script starts the N
 rank processes itself (before anything touches a GPU) and relays rank 0's line.
-Each rank scores its own shard of global candidate indices (weak scaling: m
-per GPU is fixed); the local top-k lists travel through libuthot's own RCCL
-communicator (ut_comm_allgather_topk: all-gather + HIP merge kernel) and the
-merged selections join every rank's history, so every rank -- and every N --
-selects the same candidates.  torch.distributed (gloo) only bootstraps the
-communicator and carries the barriers.  UT_DIST_BACKEND=gloo rehearses N ranks
-on fewer GPUs (records over gloo, merge on the device).
+Each rank scores its own shard of global candidate indices: --scaling weak
+(default) fixes m per GPU (global pool N*m), --scaling strong fixes the global
+pool m (rank r scores [r*m/N, (r+1)*m/N)).  The local top-k lists travel
+through libuthot's own RCCL communicator (ut_comm_allgather_topk: all-gather +
+HIP merge kernel) and the merged selections join every rank's history, so
+every rank selects the same candidates, and `selection_sha` (the last timed
+round's merged (index, digest) list) is the same at every N for one global
+pool: strong lines at N = 1, 2, 4, 8 carry equal shas, and a weak line at N
+equals the one-rank line of --m N*m.  torch.distributed (gloo) only bootstraps
+the communicator and carries the barriers.  UT_DIST_BACKEND=gloo rehearses N
+ranks on fewer GPUs (records over gloo, merge on the device).
+`hbm_bytes_per_rank` is the device memory libuthot holds per rank (max over
+ranks; each rank caches inner digests for its own shard's DE targets only).
 
 After the timed rounds (outside the timed region) rank 0 checks the last
 round's selections against the oracle (`parity`: DE trials, hash_config
@@ -323,7 +329,14 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--m", "--candidates", dest="m", type=int, default=1 << 20, help="candidates per GPU per round")
+    ap.add_argument("--m", "--candidates", dest="m", type=int, default=1 << 20,
+                    help="candidates per GPU per round (--scaling weak) or the global pool of a round "
+                         "(--scaling strong)")
+    ap.add_argument("--scaling", default="weak", choices=("weak", "strong"),
+                    help="weak: every rank scores m candidates of a global pool of N*m (the population has N*m "
+                         "members); strong: the global pool is m (population m) and rank r scores "
+                         "[r*m/N, (r+1)*m/N) -- the same workload, and the same selections (selection_sha), "
+                         "at every N")
     ap.add_argument("--n", type=int, default=1024, help="GP training points")
     ap.add_argument("--d", type=int, default=64)
     ap.add_argument("--k", type=int, default=256)
@@ -379,7 +392,20 @@ def main():
     from uptune_amd.engine import BatchEngine
     from uptune_amd.manipulator import ConfigurationManipulator, FloatParameter
 
-    m, n, d, k = args.m, args.n, args.d, args.k
+    n, d, k = args.n, args.d, args.k
+    # the shard of global candidate indices this rank scores:
+    # weak scaling fixes the per-rank m (global pool N*m), strong scaling the
+    # global pool (rank r: [r*M/N, (r+1)*M/N))
+    if args.scaling == "strong":
+        npop = args.m
+        if npop < world:
+            ap.error(f"--scaling strong needs --m >= the {world} ranks")
+        cand_base = rank * npop // world
+        m = (rank + 1) * npop // world - cand_base
+    else:
+        m = args.m
+        npop = m * world                   # replicated population, deterministic init on every rank
+        cand_base = rank * m
     if args.config == "c3":
         from uptune_amd import spaces
         manip = spaces.hpl64()
@@ -389,7 +415,6 @@ def main():
     else:
         manip = ConfigurationManipulator([FloatParameter(i, -1000.0, 1000.0) for i in range(d)])
     eng = BatchEngine(manip, device=local, seed=1)
-    npop = m * world                       # replicated population, deterministic init on every rank
     eng.gp_set_precision(args.precision)
     eng.population_init(npop)
     # the results history holds the evaluated configurations: the n training
@@ -427,7 +452,6 @@ def main():
         X, y = training_set(n, d, 101)
         hv = torch.from_numpy(np.ascontiguousarray((X * 2000.0 - 1000.0).T)).to(eng.device)   # decoded configs
         eng.history_add(eng.hash(hv))
-    cand_base = rank * m
     acq = eng.acq("ei", xi=0.0)
     ell = {"c2": 0.2, "c3": 1.0, "c4": 2.0}[args.config]
 
@@ -562,8 +586,21 @@ def main():
             parity["all_ok"] = all(v["trials_equal"] and v["digests_equal"] and v["ei_max_rel_err"] <= 1e-5 and
                                    v.get("topk_beats_sample", True) for v in legs)
 
+    # the last timed round's merged selections, as one digest comparable across
+    # N (strong scaling: the same at every N; weak: equal to a one-rank run
+    # with --m N*m) -- computed outside the timed region
+    import hashlib
+    sel_sha = hashlib.sha256(idx.detach().cpu().numpy().astype("<i8").tobytes() +
+                             sdig.detach().cpu().numpy().view(np.uint32).astype(">u4").tobytes()).hexdigest()
+    # device memory per rank: what libuthot holds on the rank's GPU (max over ranks)
+    mem = torch.tensor([float(eng.device_bytes())], dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(mem, op=dist.ReduceOp.MAX)
+    hbm_rank = int(mem.item())
+    free_b, total_b = torch.cuda.mem_get_info(eng.device)
+
     ms_per_step = elapsed * 1000.0 / args.steps
-    value = world * m / (elapsed / args.steps)
+    value = npop / (elapsed / args.steps)   # every candidate of the global pool, all ranks together
     stages = {st: float(np.mean(v)) for st, v in stage_ms.items()}
     # dominant kernel: the variance GEMM  V = L^-1 K*^T  (fp64 MFMA); at C4 (707
     # features) the K* contraction (2 n d flops per candidate) carries more flops
@@ -629,17 +666,21 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": ms_per_step,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": args.scaling,
         "vs_baseline": None,
-        "dtype": {64: "f64", 32: "f32 (K*, L^-1 K* MFMA; fit/EI f64)",
+        "dtype": {64: "f64", 32: "f32 (variance L^-1 K*^T on fp32 MFMA; K* contracted in fp64, stored f32; "
+                      "fit/mean/EI f64)",
                   16: "f32-tier f16x3 (L^-1 K*^T as hi*hi + hi*lo + lo*hi fp16 MFMA, f32 accumulate; "
                       "K*/fit/EI f64)"}[args.precision],
         "data": data,
-        "config": {"workload": workload, "candidates_per_gpu": m, "gp_n": n, "dims": d, "k": k,
-                   "parallelism": f"dp{world}",
+        "config": {"workload": workload, "candidates_per_gpu": m, "global_pool": npop, "gp_n": n, "dims": d,
+                   "k": k, "parallelism": f"dp{world}", "scaling": args.scaling,
                    "exchange": (None if world == 1 else "libuthot RCCL (ut_comm_allgather_topk + HIP merge)"
                                 if comm is not None else (exchange_note or "gloo records + HIP merge (rehearsal)"))},
         "parity": parity,
+        "selection_sha": sel_sha,
+        "hbm_bytes_per_rank": hbm_rank,
+        "hbm_device_used_bytes": int(total_b - free_b),
         "stage_ms": stages,
         "kernels": (kernel_table(m, n, d, eng.space_info()[1]) if profiled else None),
         "prune": prune_info,

@@ -132,6 +132,10 @@ const char* ut_last_error(ut_ctx* ctx);
 int ut_set_stream(ut_ctx* ctx, void* hip_stream);
 int ut_sync(ut_ctx* ctx);
 int ut_version(void);
+/* device memory (bytes) the library currently holds on `device` in this
+ * process, over all its contexts (RCCL's own buffers not included): one rank
+ * per process and GPU makes this the rank's HBM footprint */
+int ut_device_bytes(int32_t device, int64_t* bytes_host);
 
 /* ---- search space (ConfigurationManipulator, manipulator.py:129-272) ---- */
 /* py2_layout: 1 = OpenTuner/Python-2 hash layout (no b'' around primitive
@@ -401,7 +405,10 @@ int ut_topk_merge(ut_ctx* ctx, int64_t n, int32_t k, const int64_t* idx, const d
  * [n][8] (device buffers of capacity `cap` on every rank).  The root's n goes
  * first, so every rank learns it (*n_out_host) and takes part in the payload
  * broadcast even when its own n differs; n > cap is UT_EINVAL after the
- * collective (rows beyond cap are dropped). */
+ * collective (rows beyond cap are dropped).  No rank is left inside a
+ * collective when another fails: a root whose own arguments are bad sends a
+ * sentinel count and every rank returns UT_EINVAL; the ranks agree on the
+ * payload allocation before the payload broadcast (UT_ENOMEM on all). */
 int ut_comm_bcast_results(ut_ctx* ctx, int32_t root, int64_t n, double* y, uint32_t* digest, int64_t cap,
                           int64_t* n_out_host);
 /* raw broadcast of `bytes` bytes of a device buffer from `root` */

@@ -120,6 +120,13 @@ def test_rccl_c_abi_world1():
         assert y.cpu().tolist() == [1.5, 2.5] and torch.equal(d, dg[:2])
         y, d = comm.bcast_results(torch.zeros(0, dtype=torch.float64), dg[:0], 0, src=0)
         assert y.numel() == 0 and d.shape == (0, 8)
+        # a source whose rows do not match n enters the collective with the
+        # failure sentinel and raises (no rank is left waiting), and the
+        # communicator stays usable
+        with pytest.raises(L.UthotError):
+            comm.bcast_results(torch.tensor([1.5, 2.5], dtype=torch.float64), dg[:2], 3, src=0)
+        y, d = comm.bcast_results(torch.tensor([4.5], dtype=torch.float64), dg[:1], 1, src=0)
+        assert y.cpu().tolist() == [4.5] and torch.equal(d, dg[:1])
         t = torch.tensor([3.0, -1.0], dtype=torch.float64, device=dev)
         assert comm.allreduce_(t, L.UT_RED_MAX).cpu().tolist() == [3.0, -1.0]
         assert comm.agree(True) and not comm.agree(False)

@@ -203,6 +203,35 @@ def test_hash_de_reuses_population_digests(which):
         assert hexes(e.hash_de(trial3, 0)) == hexes(e.hash(trial3))
 
 
+@pytest.mark.parametrize("which", ["r64", "hpl"])
+def test_hash_de_shard_window(which):
+    """ut_hash_de caches the inner digests of the calling shard's targets only
+    (members [cand_base, cand_base + m)): a call for another shard rebuilds the
+    window, ut_population_replace patches the rows inside it and skips the
+    others, and every digest still equals ut_hash's"""
+    space = {"r64": r64_space, "hpl": hpl_space}[which]()
+    e = engine(space, seed=37)
+    e.population_init(4000, round_=1)
+    other = torch.from_numpy(ode.population_init(space, 8, seed=98)).cuda()
+    for r, (base, m) in enumerate([(1000, 1000), (1000, 600), (2500, 1000), (1200, 300), (3900, 200)]):
+        trial = e.propose_de(m, round_=r, cand_base=base, cr=0.2)
+        assert hexes(e.hash_de(trial, base)) == hexes(e.hash(trial)), (base, m)
+        if r == 2:   # rows inside ([2500, 3500)) and outside the cached window
+            e.population_replace(other[:, :4].contiguous(), torch.tensor([2600, 10, 3499, 3600], device="cuda"))
+            trial = e.propose_de(m, round_=9, cand_base=base, cr=0.2)
+            assert hexes(e.hash_de(trial, base)) == hexes(e.hash(trial))
+
+
+def test_hash_small_m_of_a_wide_array():
+    """a few columns of a wide SoA array (ld much larger than m): the small-m
+    path sizes its scratch by m, not by ld, and the digests equal
+    those of a contiguous copy"""
+    space = r64_space()
+    e = engine(space, seed=5)
+    wide = torch.from_numpy(ode.population_init(space, 1 << 20, seed=4)).cuda()   # [64][2^20]: ld = 2^20
+    assert hexes(e.hash(wide, m=100)) == hexes(e.hash(wide[:, :100].contiguous()))
+
+
 def test_de_golden(golden_dir):
     z = np.load(os.path.join(golden_dir, "de_mixed.npz"))
     e = engine(mixed_space(), seed=11)

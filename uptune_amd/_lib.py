@@ -89,6 +89,7 @@ I32, I64, U32, U64, D = C.c_int32, C.c_int64, C.c_uint32, C.c_uint64, C.c_double
 # name -> (restype, argtypes); every symbol declared in include/uthot.h
 SIGNATURES = {
     "ut_version": (C.c_int, []),
+    "ut_device_bytes": (C.c_int, [I32, C.POINTER(I64)]),
     "ut_ctx_create": (C.c_int, [C.c_int, U64, C.POINTER(P)]),
     "ut_ctx_destroy": (C.c_int, [P]),
     "ut_last_error": (C.c_char_p, [P]),

@@ -3,7 +3,9 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <mutex>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "ut_internal.h"
@@ -13,6 +15,37 @@ namespace ut {
 int set_err(ut_ctx* c, int code, const std::string& msg) {
   if (c) c->err = msg;
   return code;
+}
+
+// device allocation accounting: pointer -> (bytes, device), process-wide
+namespace {
+std::mutex g_mem_mu;
+std::unordered_map<void*, std::pair<size_t, int>> g_mem_ptrs;
+std::unordered_map<int, int64_t> g_mem_bytes;
+}  // namespace
+
+hipError_t dmalloc(void** p, size_t bytes) {
+  const hipError_t e = hipMalloc(p, bytes);
+  if (e != hipSuccess) return e;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  std::lock_guard<std::mutex> g(g_mem_mu);
+  g_mem_ptrs[*p] = {bytes, dev};
+  g_mem_bytes[dev] += (int64_t)bytes;
+  return e;
+}
+
+hipError_t dfree(void* p) {
+  if (!p) return hipSuccess;
+  {
+    std::lock_guard<std::mutex> g(g_mem_mu);
+    auto it = g_mem_ptrs.find(p);
+    if (it != g_mem_ptrs.end()) {
+      g_mem_bytes[it->second.second] -= (int64_t)it->second.first;
+      g_mem_ptrs.erase(it);
+    }
+  }
+  return hipFree(p);
 }
 
 void mark(ut_ctx* c, const char* name) {
@@ -62,16 +95,16 @@ static int timing_collect(ut_ctx* c, bool keep) {
 }
 
 static void free_space(Space& s) {
-  if (s.d_params) hipFree(s.d_params);
-  if (s.d_order) hipFree(s.d_order);
-  if (s.d_words) hipFree(s.d_words);
-  if (s.d_block_last) hipFree(s.d_block_last);
-  if (s.d_lut) hipFree(s.d_lut);
-  if (s.d_vtab) hipFree(s.d_vtab);
+  if (s.d_params) ut::dfree(s.d_params);
+  if (s.d_order) ut::dfree(s.d_order);
+  if (s.d_words) ut::dfree(s.d_words);
+  if (s.d_block_last) ut::dfree(s.d_block_last);
+  if (s.d_lut) ut::dfree(s.d_lut);
+  if (s.d_vtab) ut::dfree(s.d_vtab);
   for (void* q : {(void*)s.d_order_col, (void*)s.d_perm_params, (void*)s.d_perm_bytes, (void*)s.d_perm_off,
                   (void*)s.d_perm_offbase, (void*)s.d_perm_len, (void*)s.d_comp,
                   (void*)s.d_col_param})
-    if (q) hipFree(q);
+    if (q) ut::dfree(q);
   s = Space();
 }
 
@@ -131,9 +164,9 @@ static int compile_hash_layout(ut_ctx* c, const std::vector<std::string>& names,
   }
   s.outer_len = L;
   s.outer_blocks = NBLK;
-  UT_HIP(c, hipMalloc((void**)&s.d_words, sizeof(HashWord) * words.size()));
+  UT_HIP(c, ut::dmalloc((void**)&s.d_words, sizeof(HashWord) * words.size()));
   UT_HIP(c, hipMemcpy(s.d_words, words.data(), sizeof(HashWord) * words.size(), hipMemcpyHostToDevice));
-  UT_HIP(c, hipMalloc((void**)&s.d_block_last, sizeof(int32_t) * block_last.size()));
+  UT_HIP(c, ut::dmalloc((void**)&s.d_block_last, sizeof(int32_t) * block_last.size()));
   UT_HIP(c, hipMemcpy(s.d_block_last, block_last.data(), sizeof(int32_t) * block_last.size(), hipMemcpyHostToDevice));
   return 0;
 }
@@ -143,11 +176,11 @@ static int history_alloc(ut_ctx* c, int64_t cap) {
   while (p2 < cap) p2 <<= 1;
   if (c->hist_keys) {
     UT_HIP(c, ut::sync_all(c));
-    hipFree(c->hist_keys);
-    hipFree(c->hist_state);
+    ut::dfree(c->hist_keys);
+    ut::dfree(c->hist_state);
   }
-  UT_HIP(c, hipMalloc((void**)&c->hist_keys, sizeof(uint32_t) * 8 * p2));
-  UT_HIP(c, hipMalloc((void**)&c->hist_state, sizeof(uint32_t) * p2));
+  UT_HIP(c, ut::dmalloc((void**)&c->hist_keys, sizeof(uint32_t) * 8 * p2));
+  UT_HIP(c, ut::dmalloc((void**)&c->hist_state, sizeof(uint32_t) * p2));
   UT_HIP(c, hipMemsetAsync(c->hist_state, 0, sizeof(uint32_t) * p2, c->stream));
   c->hist_cap = p2;
   c->hist_count = 0;
@@ -161,6 +194,14 @@ using namespace ut;
 extern "C" {
 
 int ut_version(void) { return 1; }
+
+int ut_device_bytes(int32_t device, int64_t* bytes) {
+  if (!bytes) return UT_EINVAL;
+  std::lock_guard<std::mutex> g(g_mem_mu);
+  auto it = g_mem_bytes.find(device);
+  *bytes = it == g_mem_bytes.end() ? 0 : it->second;
+  return 0;
+}
 
 int ut_ctx_create(int device, uint64_t seed, ut_ctx** out) {
   if (!out) return UT_EINVAL;
@@ -205,7 +246,7 @@ int ut_ctx_destroy(ut_ctx* c) {
   if (c->stream) ut::sync_all(c);
   ut::comm_release(c);
   free_space(c->space);
-  auto fr = [](void* p) { if (p) hipFree(p); };
+  auto fr = [](void* p) { if (p) ut::dfree(p); };
   fr(c->pop); fr(c->pso_vel); fr(c->pso_best);
   fr(c->pop_dig); fr(c->pop_aos);
   for (size_t s = 0; s < c->pop_slots.size(); ++s) {
@@ -375,30 +416,30 @@ int ut_space_define(ut_ctx* c, int32_t P, const ut_param_desc* params, int32_t p
   }
   s.n_feat = feat;
   s.ncols = col;
-  UT_HIP(c, hipMalloc((void**)&s.d_params, sizeof(DevParam) * P));
+  UT_HIP(c, ut::dmalloc((void**)&s.d_params, sizeof(DevParam) * P));
   UT_HIP(c, hipMemcpy(s.d_params, s.host_params.data(), sizeof(DevParam) * P, hipMemcpyHostToDevice));
-  UT_HIP(c, hipMalloc((void**)&s.d_order, sizeof(int32_t) * P));
+  UT_HIP(c, ut::dmalloc((void**)&s.d_order, sizeof(int32_t) * P));
   UT_HIP(c, hipMemcpy(s.d_order, s.host_order.data(), sizeof(int32_t) * P, hipMemcpyHostToDevice));
   if (lut.empty()) lut.resize(8, 0u);
   {  // the device LUT holds each digest as its 64 hex characters (16 big-endian
      // words, what the outer message holds): k_hash copies them into its hex slot
     std::vector<uint32_t> luthex(lut.size() * 2);
     for (size_t e = 0; e < lut.size() / 8; ++e) ut::digest_hex(&lut[8 * e], &luthex[16 * e]);
-    UT_HIP(c, hipMalloc((void**)&s.d_lut, sizeof(uint32_t) * luthex.size()));
+    UT_HIP(c, ut::dmalloc((void**)&s.d_lut, sizeof(uint32_t) * luthex.size()));
     UT_HIP(c, hipMemcpy(s.d_lut, luthex.data(), sizeof(uint32_t) * luthex.size(), hipMemcpyHostToDevice));
   }
   if (vtab.empty()) vtab.resize(1, 0.0);
-  UT_HIP(c, hipMalloc((void**)&s.d_vtab, sizeof(double) * vtab.size()));
+  UT_HIP(c, ut::dmalloc((void**)&s.d_vtab, sizeof(double) * vtab.size()));
   UT_HIP(c, hipMemcpy(s.d_vtab, vtab.data(), sizeof(double) * vtab.size(), hipMemcpyHostToDevice));
   {
     std::vector<int32_t> order_col(P);
     for (int32_t j = 0; j < P; ++j) order_col[j] = s.host_params[s.host_order[j]].col;
-    UT_HIP(c, hipMalloc((void**)&s.d_order_col, sizeof(int32_t) * P));
+    UT_HIP(c, ut::dmalloc((void**)&s.d_order_col, sizeof(int32_t) * P));
     UT_HIP(c, hipMemcpy(s.d_order_col, order_col.data(), sizeof(int32_t) * P, hipMemcpyHostToDevice));
   }
   if (s.n_perm > 0) {
     auto up = [&](auto*& dst, const auto& v) -> hipError_t {
-      hipError_t e = hipMalloc((void**)&dst, sizeof(v[0]) * v.size());
+      hipError_t e = ut::dmalloc((void**)&dst, sizeof(v[0]) * v.size());
       if (e != hipSuccess) return e;
       return hipMemcpy(dst, v.data(), sizeof(v[0]) * v.size(), hipMemcpyHostToDevice);
     };
@@ -409,14 +450,14 @@ int ut_space_define(ut_ctx* c, int32_t P, const ut_param_desc* params, int32_t p
     UT_HIP(c, up(s.d_perm_len, perm_len));
   }
   if (s.n_comp > 0) {
-    UT_HIP(c, hipMalloc((void**)&s.d_comp, sizeof(int32_t) * comp.size()));
+    UT_HIP(c, ut::dmalloc((void**)&s.d_comp, sizeof(int32_t) * comp.size()));
     UT_HIP(c, hipMemcpy(s.d_comp, comp.data(), sizeof(int32_t) * comp.size(), hipMemcpyHostToDevice));
   }
   {
     std::vector<int32_t> col_param(s.ncols > 0 ? s.ncols : 1, -1);
     for (int32_t j = 0; j < P; ++j)
       if (s.host_params[j].kind != UT_PERM) col_param[s.host_params[j].col] = j;
-    UT_HIP(c, hipMalloc((void**)&s.d_col_param, sizeof(int32_t) * col_param.size()));
+    UT_HIP(c, ut::dmalloc((void**)&s.d_col_param, sizeof(int32_t) * col_param.size()));
     UT_HIP(c, hipMemcpy(s.d_col_param, col_param.data(), sizeof(int32_t) * col_param.size(), hipMemcpyHostToDevice));
   }
   int rc = compile_hash_layout(c, names, primitive);
@@ -424,7 +465,7 @@ int ut_space_define(ut_ctx* c, int32_t P, const ut_param_desc* params, int32_t p
   c->has_space = true;
   // a new space invalidates the population (and its digest cache)
   if (c->pop) {
-    hipFree(c->pop);
+    ut::dfree(c->pop);
     c->pop = nullptr;
     c->npop = 0;
     c->pop_cap = 0;
@@ -459,9 +500,9 @@ static int pop_alloc(ut_ctx* c, int64_t npop) {
   }
   if (c->pop) {
     UT_HIP(c, ut::sync_all(c));
-    hipFree(c->pop);
+    ut::dfree(c->pop);
   }
-  UT_HIP(c, hipMalloc((void**)&c->pop, sizeof(double) * need));
+  UT_HIP(c, ut::dmalloc((void**)&c->pop, sizeof(double) * need));
   c->pop_cap = need;
   c->npop = npop;
   return 0;
@@ -504,11 +545,13 @@ int ut_population_select(ut_ctx* c, int32_t slot) {
   cur.pop = c->pop; cur.npop = c->npop; cur.pop_cap = c->pop_cap;
   cur.pso_vel = c->pso_vel; cur.pso_best = c->pso_best; cur.pso_cap = c->pso_cap;
   cur.pop_dig = c->pop_dig; cur.pop_dig_cap = c->pop_dig_cap; cur.pop_dig_valid = c->pop_dig_valid;
+  cur.pop_dig_lo = c->pop_dig_lo; cur.pop_dig_n = c->pop_dig_n;
   cur.pop_aos = c->pop_aos; cur.pop_aos_cap = c->pop_aos_cap; cur.pop_aos_valid = c->pop_aos_valid;
   const ut_ctx::PopSlot& nx = c->pop_slots[slot];
   c->pop = nx.pop; c->npop = nx.npop; c->pop_cap = nx.pop_cap;
   c->pso_vel = nx.pso_vel; c->pso_best = nx.pso_best; c->pso_cap = nx.pso_cap;
   c->pop_dig = nx.pop_dig; c->pop_dig_cap = nx.pop_dig_cap; c->pop_dig_valid = nx.pop_dig_valid;
+  c->pop_dig_lo = nx.pop_dig_lo; c->pop_dig_n = nx.pop_dig_n;
   c->pop_aos = nx.pop_aos; c->pop_aos_cap = nx.pop_aos_cap; c->pop_aos_valid = nx.pop_aos_valid;
   c->pop_slot = slot;
   return 0;
@@ -596,16 +639,16 @@ int ut_history_add(ut_ctx* c, const uint32_t* dig, int64_t n) {
     int64_t want = (old_count + n) * 4;
     int64_t p2 = 1024;
     while (p2 < want) p2 <<= 1;
-    UT_HIP(c, hipMalloc((void**)&c->hist_keys, sizeof(uint32_t) * 8 * p2));
-    UT_HIP(c, hipMalloc((void**)&c->hist_state, sizeof(uint32_t) * p2));
+    UT_HIP(c, ut::dmalloc((void**)&c->hist_keys, sizeof(uint32_t) * 8 * p2));
+    UT_HIP(c, ut::dmalloc((void**)&c->hist_state, sizeof(uint32_t) * p2));
     UT_HIP(c, hipMemsetAsync(c->hist_state, 0, sizeof(uint32_t) * p2, c->stream));
     c->hist_cap = p2;
     c->hist_count = 0;
     if (old_keys) {
       int rc = launch_hist_rehash(c, old_keys, old_state, old_cap);
       UT_HIP(c, ut::sync_all(c));
-      hipFree(old_keys);
-      hipFree(old_state);
+      ut::dfree(old_keys);
+      ut::dfree(old_state);
       if (rc) return rc;
       c->hist_count = old_count;
     }
@@ -621,11 +664,11 @@ int ut_history_add_host(ut_ctx* c, const uint32_t* dig, int64_t n) {
   if (n <= 0) return 0;
   UT_CHECK(c, dig != nullptr, UT_EINVAL, "history_add_host: NULL digests");
   uint32_t* tmp = nullptr;
-  UT_HIP(c, hipMalloc((void**)&tmp, sizeof(uint32_t) * 8 * n));
+  UT_HIP(c, ut::dmalloc((void**)&tmp, sizeof(uint32_t) * 8 * n));
   UT_HIP(c, hipMemcpyAsync(tmp, dig, sizeof(uint32_t) * 8 * n, hipMemcpyHostToDevice, c->stream));
   int rc = ut_history_add(c, tmp, n);
   UT_HIP(c, ut::sync_all(c));
-  hipFree(tmp);
+  ut::dfree(tmp);
   return rc;
 }
 

@@ -243,6 +243,10 @@ int ut_comm_init(ut_ctx* c, int32_t rank, int32_t nranks, const uint8_t* id_host
   ncclUniqueId id;
   memcpy(&id, id_host, sizeof(id));
   ncclComm_t comm = nullptr;
+  // the count / agreement words of ut_comm_bcast_results, allocated here so
+  // that no allocation can fail between a rank's entry and its first collective
+  int rc;
+  if ((rc = ensure(c, c->cm_cnt, 2))) return rc;
   UT_RCCL(c, ncclCommInitRank(&comm, nranks, id, rank));
   c->comm = comm;
   c->comm_rank = rank;
@@ -304,26 +308,46 @@ int ut_comm_allgather_topk(ut_ctx* c, int32_t k, const int64_t* idx, const doubl
   return merge_records(c, n, W, k, ncols, out_idx, out_score, out_digest, out_rows, ld_out);
 }
 
+// Every rank takes part in every collective of this call whatever fails
+// locally, so no rank is ever left waiting inside one (dist.py's design goal):
+//   1. the root broadcasts its count, or -2 when its own arguments are bad
+//      (n > cap, missing buffers): every rank then returns UT_EINVAL;
+//   2. every rank sizes its payload buffer and the ranks agree on success (an
+//      all-reduce MIN of an ok flag): a rank that could not allocate makes
+//      all of them return UT_ENOMEM before the payload broadcast;
+//   3. the payload broadcast.
 int ut_comm_bcast_results(ut_ctx* c, int32_t root, int64_t n, double* y, uint32_t* digest, int64_t cap,
                           int64_t* n_out_host) {
   if (!c) return UT_EINVAL;
-  int rc;
-  UT_CHECK(c, c->comm != nullptr, UT_EINVAL, "comm_bcast_results: call ut_comm_init first");
-  UT_CHECK(c, root >= 0 && root < c->comm_size && cap >= 0, UT_EINVAL, "comm_bcast_results: bad root / cap");
+  UT_CHECK(c, c->comm != nullptr && c->cm_cnt.p != nullptr, UT_EINVAL, "comm_bcast_results: call ut_comm_init first");
+  UT_CHECK(c, root >= 0 && root < c->comm_size, UT_EINVAL, "comm_bcast_results: bad root");
   const bool is_root = c->comm_rank == root;
-  UT_CHECK(c, !is_root || (n >= 0 && n <= cap && (n == 0 || (y && digest))), UT_EINVAL,
-           "comm_bcast_results: the root needs n <= cap and its y / digest buffers");
+  const bool root_ok = !is_root || (n >= 0 && cap >= 0 && n <= cap && (n == 0 || (y && digest)));
   UT_HIP(c, hipSetDevice(c->device));
-  if ((rc = ensure(c, c->cm_cnt, 1))) return rc;
-  // the root's count first: every rank takes part in the payload broadcast
-  int64_t cnt = is_root ? n : -1;
+  // 1. the root's count (or the failure sentinel) first
+  int64_t cnt = is_root ? (root_ok ? n : -2) : -1;
   UT_HIP(c, hipMemcpyAsync(c->cm_cnt.p, &cnt, sizeof(cnt), hipMemcpyHostToDevice, c->stream));
   UT_RCCL(c, ncclBroadcast(c->cm_cnt.p, c->cm_cnt.p, 1, ncclInt64, root, (ncclComm_t)c->comm, c->stream));
   UT_HIP(c, hipMemcpyAsync(&cnt, c->cm_cnt.p, sizeof(cnt), hipMemcpyDeviceToHost, c->stream));
   UT_HIP(c, hipStreamSynchronize(c->stream));
+  if (cnt == -2) {
+    if (n_out_host) *n_out_host = 0;
+    return set_err(c, UT_EINVAL, is_root ? "comm_bcast_results: the root needs n <= cap and its y / digest buffers"
+                                         : "comm_bcast_results: the root's arguments were rejected");
+  }
   if (n_out_host) *n_out_host = cnt;
   if (cnt <= 0) return 0;
-  if ((rc = ensure(c, c->cm_pay, (size_t)cnt * 5))) return rc;
+  // 2. payload buffers on every rank, then agreement
+  const bool have = ensure(c, c->cm_pay, (size_t)cnt * 5) == 0;
+  int64_t ok = have ? 1 : 0;
+  UT_HIP(c, hipMemcpyAsync(c->cm_cnt.p + 1, &ok, sizeof(ok), hipMemcpyHostToDevice, c->stream));
+  UT_RCCL(c, ncclAllReduce(c->cm_cnt.p + 1, c->cm_cnt.p + 1, 1, ncclInt64, ncclMin, (ncclComm_t)c->comm, c->stream));
+  UT_HIP(c, hipMemcpyAsync(&ok, c->cm_cnt.p + 1, sizeof(ok), hipMemcpyDeviceToHost, c->stream));
+  UT_HIP(c, hipStreamSynchronize(c->stream));
+  if (!ok)
+    return set_err(c, UT_ENOMEM, have ? "comm_bcast_results: another rank could not allocate the payload"
+                                      : "comm_bcast_results: no memory for the payload");
+  // 3. the payload
   uint64_t* pay = reinterpret_cast<uint64_t*>(c->cm_pay.p);
   if (is_root) {
     hipLaunchKernelGGL(k_pack_results, dim3(grid1(cnt, 256)), dim3(256), 0, c->stream, cnt, y, digest, pay);

@@ -70,13 +70,13 @@ extern "C" int ut_forest_set(ut_ctx* c, int32_t n_trees, const int32_t* roots_ho
   }
   UT_HIP(c, hipSetDevice(c->device));
   UT_HIP(c, ut::sync_all(c));
-  if (c->forest_nodes) hipFree(c->forest_nodes);
-  if (c->forest_roots) hipFree(c->forest_roots);
+  if (c->forest_nodes) ut::dfree(c->forest_nodes);
+  if (c->forest_roots) ut::dfree(c->forest_roots);
   c->forest_nodes = nullptr;
   c->forest_roots = nullptr;
   c->forest_trees = 0;
-  UT_HIP(c, hipMalloc((void**)&c->forest_nodes, sizeof(ut_tree_node) * n_nodes));
-  UT_HIP(c, hipMalloc((void**)&c->forest_roots, sizeof(int32_t) * n_trees));
+  UT_HIP(c, ut::dmalloc((void**)&c->forest_nodes, sizeof(ut_tree_node) * n_nodes));
+  UT_HIP(c, ut::dmalloc((void**)&c->forest_roots, sizeof(int32_t) * n_trees));
   UT_HIP(c, hipMemcpy(c->forest_nodes, nodes_host, sizeof(ut_tree_node) * n_nodes, hipMemcpyHostToDevice));
   UT_HIP(c, hipMemcpy(c->forest_roots, roots_host, sizeof(int32_t) * n_trees, hipMemcpyHostToDevice));
   c->forest_trees = n_trees;

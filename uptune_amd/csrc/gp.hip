@@ -636,35 +636,35 @@ static int gp_alloc(ut_ctx* c, int32_t npad_need, int32_t d) {
   const int64_t npad = ((npad_need + npad_need / 4 + NPAD - 1) / NPAD) * NPAD;
   if (c->gp_Xs_f) {
     UT_HIP(c, ut::sync_all(c));
-    hipFree(c->gp_Xs_f); hipFree(c->gp_LinvT); hipFree(c->gp_LinvT_f); hipFree(c->gp_T); hipFree(c->gp_ctr);
-    hipFree(c->gp_XsT);
+    ut::dfree(c->gp_Xs_f); ut::dfree(c->gp_LinvT); ut::dfree(c->gp_LinvT_f); ut::dfree(c->gp_T); ut::dfree(c->gp_ctr);
+    ut::dfree(c->gp_XsT);
     c->gp_Xs_f = nullptr; c->gp_LinvT = nullptr; c->gp_LinvT_f = nullptr; c->gp_T = nullptr; c->gp_ctr = nullptr;
     c->gp_XsT = nullptr;
   }
   if (c->gp_Xs) {
     UT_HIP(c, ut::sync_all(c));
-    hipFree(c->gp_Xs); hipFree(c->gp_xnorm); hipFree(c->gp_K); hipFree(c->gp_Linv);
-    hipFree(c->gp_y); hipFree(c->gp_tmp); hipFree(c->gp_alpha); hipFree(c->gp_beta); hipFree(c->gp_inv_ell);
-    hipFree(c->gp_stats); hipFree(c->gp_flag);
+    ut::dfree(c->gp_Xs); ut::dfree(c->gp_xnorm); ut::dfree(c->gp_K); ut::dfree(c->gp_Linv);
+    ut::dfree(c->gp_y); ut::dfree(c->gp_tmp); ut::dfree(c->gp_alpha); ut::dfree(c->gp_beta); ut::dfree(c->gp_inv_ell);
+    ut::dfree(c->gp_stats); ut::dfree(c->gp_flag);
   }
-  UT_HIP(c, hipMalloc((void**)&c->gp_Xs, sizeof(double) * npad * d));
-  UT_HIP(c, hipMalloc((void**)&c->gp_xnorm, sizeof(double) * npad));
-  UT_HIP(c, hipMalloc((void**)&c->gp_K, sizeof(double) * npad * npad));
-  UT_HIP(c, hipMalloc((void**)&c->gp_Linv, sizeof(double) * npad * npad));
-  UT_HIP(c, hipMalloc((void**)&c->gp_y, sizeof(double) * npad));
-  UT_HIP(c, hipMalloc((void**)&c->gp_tmp, sizeof(double) * npad * (d + 1)));
-  UT_HIP(c, hipMalloc((void**)&c->gp_alpha, sizeof(double) * npad));
-  UT_HIP(c, hipMalloc((void**)&c->gp_beta, sizeof(double) * npad));
-  UT_HIP(c, hipMalloc((void**)&c->gp_inv_ell, sizeof(double) * d));
-  UT_HIP(c, hipMalloc((void**)&c->gp_stats, sizeof(double) * 4));
-  UT_HIP(c, hipMalloc((void**)&c->gp_flag, sizeof(int32_t)));
-  UT_HIP(c, hipMalloc((void**)&c->gp_T, sizeof(double) * npad * npad));
-  UT_HIP(c, hipMalloc((void**)&c->gp_Xs_f, sizeof(float) * npad * d));
-  UT_HIP(c, hipMalloc((void**)&c->gp_LinvT, sizeof(double) * npad * npad));
+  UT_HIP(c, ut::dmalloc((void**)&c->gp_Xs, sizeof(double) * npad * d));
+  UT_HIP(c, ut::dmalloc((void**)&c->gp_xnorm, sizeof(double) * npad));
+  UT_HIP(c, ut::dmalloc((void**)&c->gp_K, sizeof(double) * npad * npad));
+  UT_HIP(c, ut::dmalloc((void**)&c->gp_Linv, sizeof(double) * npad * npad));
+  UT_HIP(c, ut::dmalloc((void**)&c->gp_y, sizeof(double) * npad));
+  UT_HIP(c, ut::dmalloc((void**)&c->gp_tmp, sizeof(double) * npad * (d + 1)));
+  UT_HIP(c, ut::dmalloc((void**)&c->gp_alpha, sizeof(double) * npad));
+  UT_HIP(c, ut::dmalloc((void**)&c->gp_beta, sizeof(double) * npad));
+  UT_HIP(c, ut::dmalloc((void**)&c->gp_inv_ell, sizeof(double) * d));
+  UT_HIP(c, ut::dmalloc((void**)&c->gp_stats, sizeof(double) * 4));
+  UT_HIP(c, ut::dmalloc((void**)&c->gp_flag, sizeof(int32_t)));
+  UT_HIP(c, ut::dmalloc((void**)&c->gp_T, sizeof(double) * npad * npad));
+  UT_HIP(c, ut::dmalloc((void**)&c->gp_Xs_f, sizeof(float) * npad * d));
+  UT_HIP(c, ut::dmalloc((void**)&c->gp_LinvT, sizeof(double) * npad * npad));
   // fp32: (L^-1)^T; h3: the blocked fp16 hi / lo planes, rows padded to 256
-  UT_HIP(c, hipMalloc((void**)&c->gp_LinvT_f, sizeof(float) * (((npad + 255) / 256) * 256) * npad));
-  UT_HIP(c, hipMalloc((void**)&c->gp_ctr, sizeof(int32_t) * 32));
-  UT_HIP(c, hipMalloc((void**)&c->gp_XsT, sizeof(double) * npad * kstar_dpad(d)));
+  UT_HIP(c, ut::dmalloc((void**)&c->gp_LinvT_f, sizeof(float) * (((npad + 255) / 256) * 256) * npad));
+  UT_HIP(c, ut::dmalloc((void**)&c->gp_ctr, sizeof(int32_t) * 32));
+  UT_HIP(c, ut::dmalloc((void**)&c->gp_XsT, sizeof(double) * npad * kstar_dpad(d)));
   c->gp_cap_n = npad;
   c->gp_d = d;
   return 0;

@@ -166,23 +166,27 @@ __global__ __launch_bounds__(PD_NT) void k_perm_digest(const DevParam* __restric
 //                 wave has a lane crossing every parameter),
 //   k_hash        reads each inner digest from the cache or the fresh buffer.
 // ---------------------------------------------------------------------------
+// The cache covers the members [lo, lo + wn): a context caches the targets of
+// its own candidates (a rank's shard), not the whole replicated population.
+// rows == nullptr: rebuild every member of the window; else patch the members
+// rows[0..nrows) that fall inside it.
 __global__ __launch_bounds__(HASH_NT) void k_pop_digests(const DevParam* __restrict__ params,
                                                          const int32_t* __restrict__ comp, int32_t n_comp,
                                                          const double* __restrict__ pop, int64_t npop,
                                                          const int64_t* __restrict__ rows, int64_t nrows,
-                                                         uint4* __restrict__ cache) {
+                                                         int64_t lo, int64_t wn, uint4* __restrict__ cache) {
   __shared__ uint32_t lds[SCR_WORDS * HASH_NT];
   const int lane = threadIdx.x;
   const int32_t s = blockIdx.y;
   const int64_t r = (int64_t)blockIdx.x * HASH_NT + lane;
-  const int64_t n = rows ? nrows : npop;
+  const int64_t n = rows ? nrows : wn;
   if (s >= n_comp || r >= n) return;   // no barriers below: every lane owns its LDS column
-  int64_t j = rows ? rows[r] : r;
-  j = j < 0 ? 0 : (j >= npop ? npop - 1 : j);
+  const int64_t j = rows ? rows[r] : lo + r;
+  if (j < lo || j >= lo + wn || j >= npop) return;   // outside the cached window
   const DevParam pr = params[comp[s]];
   uint32_t D[8];
   repr_digest(pr, pop[(int64_t)pr.col * npop + j], lds, lane, D);
-  store_hex(cache + 4 * ((int64_t)s * npop + j), D);
+  store_hex(cache + 4 * ((int64_t)s * wn + (j - lo)), D);
 }
 
 constexpr int DIFF_NT = 256;
@@ -273,7 +277,7 @@ __global__ __launch_bounds__(HASH_NT) void k_inner_all(const DevParam* __restric
     const DevParam pr = params[comp[s]];
     uint32_t D[8];
     repr_digest(pr, values[(int64_t)pr.col * ld + i], lds, lane, D);
-    store_hex(fresh + 4 * ((int64_t)s * ld + i), D);
+    store_hex(fresh + 4 * ((int64_t)s * m + i), D);
   }
 }
 
@@ -281,10 +285,13 @@ __global__ __launch_bounds__(HASH_NT) void k_inner_all(const DevParam* __restric
 // rounds), kept as their 64 hex characters (16 big-endian words: what the
 // outer message holds), so k_hash moves them into its hex slot as they are
 struct InnerRef {
-  const uint32_t* mask;   // [ceil(n_comp / 32)][ld]
-  const uint4* fresh;     // [n_comp][ld][16 hex words]
-  const uint4* cache;     // [n_comp][npop][16 hex words]; nullptr = compute every inner digest in k_hash
+  const uint32_t* mask;   // [ceil(n_comp / 32)][ldf]
+  const uint4* fresh;     // [n_comp][ldf][16 hex words]
+  const uint4* cache;     // [n_comp][wn][16 hex words] of members [wlo, wlo + wn); nullptr = compute every
+                          // inner digest in k_hash
   int64_t npop, cand_base;
+  int64_t wlo, wn;        // the cache's member window (every target (cand_base + i) % npop lies in it)
+  int64_t ldf;            // leading dimension of mask / fresh
 };
 
 // REF: every computed inner digest comes from ref (cache / fresh) and the
@@ -355,9 +362,10 @@ __global__ __launch_bounds__(HASH_NT, MINW) void k_hash(const DevParam* __restri
         } else if constexpr (REF) {
           // the target's cached hex digest, or this trial's fresh one (k_inner_pairs),
           // straight into the hex slot
-          const uint32_t mw = ref.mask[(int64_t)(pr.cslot >> 5) * ld + i];
-          const uint4* src = ((mw >> (pr.cslot & 31)) & 1u) ? ref.fresh + 4 * ((int64_t)pr.cslot * ld + i)
-                                                             : ref.cache + 4 * ((int64_t)pr.cslot * ref.npop + t);
+          const uint32_t mw = ref.mask[(int64_t)(pr.cslot >> 5) * ref.ldf + i];
+          const uint4* src = ((mw >> (pr.cslot & 31)) & 1u)
+                                 ? ref.fresh + 4 * ((int64_t)pr.cslot * ref.ldf + i)
+                                 : ref.cache + 4 * ((int64_t)pr.cslot * ref.wn + (t - ref.wlo));
           const uint4 q0 = src[0], q1 = src[1], q2 = src[2], q3 = src[3];
           if (next + 1 < P) vnext = values[(int64_t)order_col[next + 1] * ld + i];
           put_hex(HX, next & 1, q0, q1, q2, q3);
@@ -443,9 +451,11 @@ int launch_hash(ut_ctx* c, const double* values, int64_t ld, int64_t m, uint32_t
   if (s.n_comp > 0 && m > 0 && m <= HASH_SMALL_M) {
     const int32_t nw = (s.n_comp + 31) / 32;
     int rc;
-    if ((rc = ensure(c, c->hs_mask, (size_t)nw * ld))) return rc;
-    if ((rc = ensure(c, c->hs_fresh, (size_t)s.n_comp * ld * 16))) return rc;
-    UT_HIP(c, hipMemsetAsync(c->hs_mask.p, 0xFF, sizeof(uint32_t) * nw * ld, c->stream));
+    // the fresh digests and the mask are indexed with leading dimension m, not
+    // ld (a few columns of a wide SoA array must not size them by its ld)
+    if ((rc = ensure(c, c->hs_mask, (size_t)nw * m))) return rc;
+    if ((rc = ensure(c, c->hs_fresh, (size_t)s.n_comp * m * 16))) return rc;
+    UT_HIP(c, hipMemsetAsync(c->hs_mask.p, 0xFF, sizeof(uint32_t) * nw * m, c->stream));
     const int64_t want = ((int64_t)s.n_comp * m + HASH_NT - 1) / HASH_NT;
     const unsigned grid = (unsigned)std::min<int64_t>(want, (int64_t)c->n_cu * 8);
     hipLaunchKernelGGL(k_inner_all, dim3(grid), dim3(HASH_NT), 0, c->stream, s.d_params, s.d_comp, s.n_comp, values,
@@ -454,35 +464,45 @@ int launch_hash(ut_ctx* c, const double* values, int64_t ld, int64_t m, uint32_t
     // every mask bit set: k_hash reads each computed digest from hs_fresh (the
     // "cache" operand is never read)
     const uint4* fr = reinterpret_cast<const uint4*>(c->hs_fresh.p);
-    return launch_hash_impl(c, values, ld, m, out, InnerRef{c->hs_mask.p, fr, fr, 1, 0});
+    return launch_hash_impl(c, values, ld, m, out, InnerRef{c->hs_mask.p, fr, fr, 1, 0, 0, 1, m});
   }
-  return launch_hash_impl(c, values, ld, m, out, InnerRef{nullptr, nullptr, nullptr, 1, 0});
+  return launch_hash_impl(c, values, ld, m, out, InnerRef{nullptr, nullptr, nullptr, 1, 0, 0, 1, ld});
+}
+
+int launch_pop_digests_window(ut_ctx* c, int64_t lo, int64_t wn) {
+  const Space& s = c->space;
+  if (s.n_comp == 0 || c->npop == 0) return 0;
+  lo = std::max<int64_t>(0, std::min(lo, c->npop - 1));
+  wn = std::max<int64_t>(1, std::min(wn, c->npop - lo));
+  const int64_t need = (int64_t)s.n_comp * wn * 16;   // 64 hex characters per digest
+  if (c->pop_dig_cap < need) {
+    if (c->pop_dig) {
+      UT_HIP(c, sync_all(c));
+      ut::dfree(c->pop_dig);
+      c->pop_dig = nullptr;
+      c->pop_dig_cap = 0;
+    }
+    const hipError_t e = ut::dmalloc((void**)&c->pop_dig, sizeof(uint32_t) * need);
+    if (e != hipSuccess) return set_err(c, UT_ENOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
+    c->pop_dig_cap = need;
+  }
+  hipLaunchKernelGGL(k_pop_digests, dim3(grid1(wn, HASH_NT), (unsigned)s.n_comp), dim3(HASH_NT), 0, c->stream,
+                     s.d_params, s.d_comp, s.n_comp, c->pop, c->npop, (const int64_t*)nullptr, (int64_t)0, lo, wn,
+                     reinterpret_cast<uint4*>(c->pop_dig));
+  UT_LAUNCH_CHECK(c);
+  c->pop_dig_lo = lo;
+  c->pop_dig_n = wn;
+  c->pop_dig_valid = true;
+  return 0;
 }
 
 int launch_pop_digests(ut_ctx* c, const int64_t* idx, int64_t n) {
   const Space& s = c->space;
-  if (s.n_comp == 0 || c->npop == 0) return 0;
-  if (!idx) {  // full rebuild
-    const int64_t need = (int64_t)s.n_comp * c->npop * 16;   // 64 hex characters per digest
-    if (c->pop_dig_cap < need) {
-      if (c->pop_dig) {
-        UT_HIP(c, sync_all(c));
-        hipFree(c->pop_dig);
-        c->pop_dig = nullptr;
-        c->pop_dig_cap = 0;
-      }
-      const hipError_t e = hipMalloc((void**)&c->pop_dig, sizeof(uint32_t) * need);
-      if (e != hipSuccess) return set_err(c, UT_ENOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
-      c->pop_dig_cap = need;
-    }
-    n = c->npop;
-  }
-  if (n <= 0) return 0;
+  if (s.n_comp == 0 || c->npop == 0 || !c->pop_dig_valid || n <= 0) return 0;
   hipLaunchKernelGGL(k_pop_digests, dim3(grid1(n, HASH_NT), (unsigned)s.n_comp), dim3(HASH_NT), 0, c->stream,
-                     s.d_params, s.d_comp, s.n_comp, c->pop, c->npop, idx, idx ? n : 0,
+                     s.d_params, s.d_comp, s.n_comp, c->pop, c->npop, idx, n, c->pop_dig_lo, c->pop_dig_n,
                      reinterpret_cast<uint4*>(c->pop_dig));
   UT_LAUNCH_CHECK(c);
-  if (!idx) c->pop_dig_valid = true;
   return 0;
 }
 
@@ -501,7 +521,12 @@ int launch_hash_de(ut_ctx* c, const double* values, int64_t ld, int64_t m, int64
   const Space& s = c->space;
   if (s.n_comp == 0 || m <= 0) return launch_hash(c, values, ld, m, out);
   int rc;
-  if (!c->pop_dig_valid && (rc = launch_pop_digests(c, nullptr, 0))) return rc;
+  // the targets of this call: members (cand_base + i) % npop, i < m -- one
+  // contiguous range unless it wraps around the population (then all of it)
+  int64_t tlo = (int64_t)((uint64_t)cand_base % (uint64_t)c->npop), tn = m;
+  if (tlo + tn > c->npop) tlo = 0, tn = c->npop;
+  const bool covered = c->pop_dig_valid && tlo >= c->pop_dig_lo && tlo + tn <= c->pop_dig_lo + c->pop_dig_n;
+  if (!covered && (rc = launch_pop_digests_window(c, tlo, tn))) return rc;
   if ((rc = ensure_de_diff(c, ld))) return rc;
   unsigned long long* np = reinterpret_cast<unsigned long long*>(c->r_npairs.p);
   if (!have_diff) {
@@ -520,7 +545,8 @@ int launch_hash_de(ut_ctx* c, const double* values, int64_t ld, int64_t m, int64
   if (hold && c->round_hash_hold == 1) UT_HIP(c, hipStreamWaitEvent(c->stream, c->ev_fit, 0));
   return launch_hash_impl(c, values, ld, m, out,
                           InnerRef{c->r_mask.p, reinterpret_cast<const uint4*>(c->r_fresh.p),
-                                   reinterpret_cast<const uint4*>(c->pop_dig), c->npop, cand_base});
+                                   reinterpret_cast<const uint4*>(c->pop_dig), c->npop, cand_base, c->pop_dig_lo,
+                                   c->pop_dig_n, ld});
 }
 
 int launch_hash_parent(ut_ctx* c, const double* values, int64_t ld, int64_t m, const double* parent, uint32_t* out) {
@@ -531,7 +557,7 @@ int launch_hash_parent(ut_ctx* c, const double* values, int64_t ld, int64_t m, c
   if ((rc = ensure_de_diff(c, ld))) return rc;
   // the parent's hex inner digests: a population of one member (column p at parent[col])
   hipLaunchKernelGGL(k_pop_digests, dim3(1, (unsigned)s.n_comp), dim3(HASH_NT), 0, c->stream, s.d_params, s.d_comp,
-                     s.n_comp, parent, (int64_t)1, (const int64_t*)nullptr, (int64_t)0,
+                     s.n_comp, parent, (int64_t)1, (const int64_t*)nullptr, (int64_t)0, (int64_t)0, (int64_t)1,
                      reinterpret_cast<uint4*>(c->par_dig.p));
   UT_LAUNCH_CHECK(c);
   // which computed-digest values differ from the parent's: every child "targets" member 0
@@ -547,7 +573,7 @@ int launch_hash_parent(ut_ctx* c, const double* values, int64_t ld, int64_t m, c
   UT_LAUNCH_CHECK(c);
   return launch_hash_impl(c, values, ld, m, out,
                           InnerRef{c->r_mask.p, reinterpret_cast<const uint4*>(c->r_fresh.p),
-                                   reinterpret_cast<const uint4*>(c->par_dig.p), 1, 0});
+                                   reinterpret_cast<const uint4*>(c->par_dig.p), 1, 0, 0, 1, ld});
 }
 
 }  // namespace ut

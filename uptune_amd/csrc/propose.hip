@@ -748,12 +748,12 @@ int ensure_pop_aos(ut_ctx* c) {
   if (c->pop_aos_cap < need) {
     if (c->pop_aos) {
       UT_HIP(c, sync_all(c));
-      (void)hipFree(c->pop_aos);
+      (void)ut::dfree(c->pop_aos);
       c->pop_aos = nullptr;
       c->pop_aos_cap = 0;
     }
-    const hipError_t e = hipMalloc((void**)&c->pop_aos, sizeof(double) * need);
-    if (e != hipSuccess) return set_err(c, UT_ENOMEM, std::string("hipMalloc(pop_aos): ") + hipGetErrorString(e));
+    const hipError_t e = ut::dmalloc((void**)&c->pop_aos, sizeof(double) * need);
+    if (e != hipSuccess) return set_err(c, UT_ENOMEM, std::string("ut::dmalloc(pop_aos): ") + hipGetErrorString(e));
     c->pop_aos_cap = need;
   }
   hipLaunchKernelGGL(k_pop_to_aos, dim3(grid1(c->npop, 64), (unsigned)(lda / 16)), dim3(256), 0, c->stream,
@@ -910,11 +910,11 @@ extern "C" int ut_pso_reset(ut_ctx* c) {
   if (c->pso_cap < need) {
     if (c->pso_vel) {
       UT_HIP(c, ut::sync_all(c));
-      hipFree(c->pso_vel);
-      hipFree(c->pso_best);
+      ut::dfree(c->pso_vel);
+      ut::dfree(c->pso_best);
     }
-    UT_HIP(c, hipMalloc((void**)&c->pso_vel, sizeof(double) * need));
-    UT_HIP(c, hipMalloc((void**)&c->pso_best, sizeof(double) * need));
+    UT_HIP(c, ut::dmalloc((void**)&c->pso_vel, sizeof(double) * need));
+    UT_HIP(c, ut::dmalloc((void**)&c->pso_best, sizeof(double) * need));
     c->pso_cap = need;
   }
   UT_HIP(c, hipMemsetAsync(c->pso_vel, 0, sizeof(double) * need, c->stream));

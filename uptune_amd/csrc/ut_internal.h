@@ -165,6 +165,10 @@ struct ut_ctx {
   uint32_t* pop_dig = nullptr;
   int64_t pop_dig_cap = 0;
   bool pop_dig_valid = false;
+  // the cache covers members [pop_dig_lo, pop_dig_lo + pop_dig_n) only: the
+  // targets of this context's candidates (a rank's shard of the global pool,
+  // cand_base .. cand_base + m), not the whole replicated population
+  int64_t pop_dig_lo = 0, pop_dig_n = 0;
   // member-major donor copy of the selected population ([npop + 1][ld], ld =
   // ncols rounded up to 16 columns = whole 128-B lines), primitive params
   // stored as their unit values (unit_of), the others raw: k_de gathers its
@@ -209,6 +213,7 @@ struct ut_ctx {
     uint32_t* pop_dig = nullptr;
     int64_t pop_dig_cap = 0;
     bool pop_dig_valid = false;
+    int64_t pop_dig_lo = 0, pop_dig_n = 0;
     double* pop_aos = nullptr;
     int64_t pop_aos_cap = 0;
     bool pop_aos_valid = false;
@@ -313,7 +318,7 @@ struct ut_ctx {
   ut::DevBuf<uint64_t> cm_send, cm_recv;   // [k][W] / [R k][W] records (W = 6 + payload columns)
   ut::DevBuf<uint8_t> cm_keep;             // [R k] record survives the digest dedup
   ut::DevBuf<double> cm_pay;               // [n][5] broadcast payload (value + digest)
-  ut::DevBuf<int64_t> cm_cnt;              // [1] broadcast count
+  ut::DevBuf<int64_t> cm_cnt;              // [2] broadcast count + agreement flag (allocated by ut_comm_init)
 
   ut::Timing timing;
 };
@@ -321,6 +326,12 @@ struct ut_ctx {
 namespace ut {
 
 int set_err(ut_ctx* c, int code, const std::string& msg);
+
+// every device allocation of the library goes through these two (api.hip):
+// the bytes held per device are what ut_device_bytes reports (a rank's HBM
+// footprint in the bench line)
+hipError_t dmalloc(void** p, size_t bytes);
+hipError_t dfree(void* p);
 
 // wait for every stream of the context (before freeing or reusing buffers)
 inline hipError_t sync_all(ut_ctx* c) {
@@ -373,15 +384,15 @@ int ensure(ut_ctx* c, DevBuf<T>& b, size_t n) {
     want = n + std::min(n / 4, ((size_t)2 << 30) / sizeof(T));
     hipError_t e = ut::sync_all(c);
     (void)e;
-    (void)hipFree(b.p);
+    (void)ut::dfree(b.p);
     b.p = nullptr;
     b.n = 0;
   }
-  hipError_t e = hipMalloc((void**)&b.p, (want ? want : 1) * sizeof(T));
+  hipError_t e = ut::dmalloc((void**)&b.p, (want ? want : 1) * sizeof(T));
   if (e != hipSuccess && want > n) {   // no room for the headroom: exactly n
     (void)hipGetLastError();
     want = n;
-    e = hipMalloc((void**)&b.p, (want ? want : 1) * sizeof(T));
+    e = ut::dmalloc((void**)&b.p, (want ? want : 1) * sizeof(T));
   }
   if (e != hipSuccess) return set_err(c, UT_ENOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
   b.n = want;
@@ -415,8 +426,11 @@ int launch_hash_de(ut_ctx* c, const double* values, int64_t ld, int64_t m, int64
 int launch_hash_parent(ut_ctx* c, const double* values, int64_t ld, int64_t m, const double* parent, uint32_t* out);
 // the DE-diff buffers for m candidates (ld): r_mask, r_fresh, r_pairs, r_npairs
 int ensure_de_diff(ut_ctx* c, int64_t ld);
-// population cache maintenance: full rebuild, or the rows idx[0..n) after a replace
+// population cache maintenance: the rows idx[0..n) after a replace (rows
+// outside the cached window are skipped)
 int launch_pop_digests(ut_ctx* c, const int64_t* idx, int64_t n);
+// full rebuild of the cache for the members [lo, lo + wn)
+int launch_pop_digests_window(ut_ctx* c, int64_t lo, int64_t wn);
 // the member-major population copy: rebuilt if stale (ensure), or the rows
 // idx[0..n) patched from trial after a replace
 int ensure_pop_aos(ut_ctx* c);

@@ -200,15 +200,21 @@ class DeviceComm(DeviceCtx):
         a rank whose own n differs still receives src's rows (check the length)"""
         is_src = self.rank == src
         cap = max(int(n), 1)
-        if is_src:
+        # a source whose rows do not match n still enters the collective (with
+        # n = -1: the library sends the failure sentinel, so every rank raises
+        # instead of waiting for a payload that never comes; ADVICE r3)
+        bad = is_src and (y is None or digests is None or int(y.numel()) != int(n) or
+                          tuple(digests.reshape(-1, 8).shape) != (int(n), 8))
+        if is_src and not bad:
             yb = y.to(self.device, torch.float64).contiguous().reshape(-1)
             db = digests.to(self.device, torch.int32).contiguous().reshape(-1, 8)
         else:
             yb = torch.empty(cap, dtype=torch.float64, device=self.device)
             db = torch.empty((cap, 8), dtype=torch.int32, device=self.device)
         got = C.c_int64()
-        rc = self.lib.ut_comm_bcast_results(self.ctx, int(src), int(n) if is_src else 0, _ptr(yb), _ptr(db),
-                                            yb.numel() if is_src else cap, C.byref(got))
+        n_arg = (-1 if bad else int(n)) if is_src else 0
+        rc = self.lib.ut_comm_bcast_results(self.ctx, int(src), n_arg, _ptr(yb), _ptr(db),
+                                            yb.numel() if is_src and not bad else cap, C.byref(got))
         ns = max(int(got.value), 0)
         if rc == -1 and ns > cap and not is_src:
             # src sent more rows than this rank expected (the collective completed;

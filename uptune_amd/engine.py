@@ -95,6 +95,13 @@ class BatchEngine:
     def sync(self):
         L.check(self.ctx, self.lib.ut_sync(self.ctx), "ut_sync")
 
+    def device_bytes(self) -> int:
+        """ut_device_bytes: device memory libuthot holds on this engine's GPU in
+        this process (every context; one rank per GPU makes it the rank's footprint)"""
+        b = C.c_int64()
+        L.check(self.ctx, self.lib.ut_device_bytes(self.device.index, C.byref(b)), "ut_device_bytes")
+        return int(b.value)
+
     def space_info(self) -> Tuple[int, int, int]:
         a, b, c = C.c_int64(), C.c_int64(), C.c_int32()
         L.check(self.ctx, self.lib.ut_space_info(self.ctx, C.byref(a), C.byref(b), C.byref(c)), "ut_space_info")
