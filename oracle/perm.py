@@ -15,7 +15,11 @@ A permutation value is a list of item indices (0..S-1 into the parameter's
     randbelow(word, n)     =  (word * n) >> 32
     random() < p           -> word * 2**-32 < p
 
-which is exactly uptune_amd/csrc/ut_perm.h.  Operators and their reference lines:
+which is exactly uptune_amd/csrc/ut_perm.h.  The crossovers take their
+randint calls from `ints(W)`: a word stream (the counter form above, call k
+reads word k) or any object with randint(a, b) -- CPython's random.Random,
+so the same code consumes the reference's MT19937 stream call for call
+(oracle/replay.py MTDraws).  Operators and their reference lines:
 
     op1_randomize            random.shuffle (CPython Fisher-Yates, i = S-1 .. 1)  :1057-1064
     op1_small_random_change  swap (i-1, i) with probability p                    :1066-1079
@@ -68,6 +72,26 @@ def randint(word, a, b):
     return a + randbelow(word, b - a + 1)
 
 
+class WordInts:
+    """random.randint(a, b) calls answered from consecutive words of a draw
+    site (call k -> word k), the counter form of the crossovers' randint"""
+
+    def __init__(self, W):
+        self.W, self.k = W, 0
+
+    def randint(self, a, b):
+        v = randint(self.W[self.k], a, b)
+        self.k += 1
+        return v
+
+
+def ints(W):
+    """the crossovers' randint source: an object with randint(a, b) (e.g.
+    CPython's random.Random: the reference's MT19937 stream, in call order) is
+    used as it is; a word stream is read one word per call"""
+    return W if hasattr(W, "randint") else WordInts(W)
+
+
 def shuffle(x, W):
     """random.shuffle(x) in place: for i in reversed(range(1, len(x))): j = randbelow(i + 1)"""
     for s, i in enumerate(reversed(range(1, len(x)))):
@@ -86,7 +110,7 @@ def cross_PX(p1, p2, d, W):
     S = len(p1)
     if S < 2:
         return list(p1)
-    c1 = randint(W[0], 2, S)
+    c1 = ints(W).randint(2, S)
     return sorted(p1[:c1], key=lambda x: p2.index(x)) + p1[c1:]
 
 
@@ -98,7 +122,7 @@ def cross_PMX(p1, p2, d, W):
         return list(p1)
     p1 = p1[:]
     p2 = p2[:]
-    r = randint(W[0], 0, S - d)
+    r = ints(W).randint(0, S - d)
     c1 = p1[r:r + d]
     c2 = p2[r:r + d]
     pnew = p1[:]
@@ -131,7 +155,7 @@ def cross_PMX(p1, p2, d, W):
 def cross_CX(p1, p2, d, W):
     S = len(p1)
     p = p1[:]
-    s = randint(W[0], 0, S - 1)
+    s = ints(W).randint(0, S - 1)
     i = s
     indices = set()
     while len(indices) < S:
@@ -156,7 +180,7 @@ def cross_OX1(p1, p2, d, W):
     if d > S:
         return list(p1)
     c1 = p1[:]
-    r = randint(W[0], 0, S - d)
+    r = ints(W).randint(0, S - d)
     for i in p2[r:r + d]:
         c1.remove(i)
     return c1[:r] + p2[r:r + d] + c1[r:]
@@ -169,8 +193,9 @@ def cross_OX3(p1, p2, d, W):
     if d > S:
         return list(p1)
     c1 = p1[:]
-    r1 = randint(W[0], 0, S - d)
-    r2 = randint(W[1], 0, S - d)
+    R = ints(W)
+    r1 = R.randint(0, S - d)
+    r2 = R.randint(0, S - d)
     for i in p2[r2:r2 + d]:
         c1.remove(i)
     return c1[:r1] + p2[r2:r2 + d] + c1[r1:]

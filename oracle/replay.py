@@ -35,6 +35,16 @@ reference's RNG, it is not compared with the reference's own output.
 The PSO sigmoid's numpy.exp is part of the draw source: MTDraws uses
 numpy.exp (the reference), CounterDraws the build's ut_exp (oracle/mathx.py,
 = the device's), the one non-random substitution.
+
+MT mode covers every random call of the path: the permutation crossovers
+op3_cross_{OX1,OX3,PX,CX,PMX} (manipulator.py:1179-1353; PSO's permutation
+op3_swarm :1115-1140 and CrossoverMixin :123-134) draw their random.randint
+calls from the stream in the reference's order (oracle/perm.py `ints`), and
+MTDraws.params keeps the manipulator's ONE shared params list that GA / GGA
+shuffle in place: seed_config, random(), the next mutation,
+CrossoverMixin and HybridParticle.move iterate the order the last shuffle
+left, across calls.  (The counter form keys each draw by param index, so the
+order does not change its output.)
 """
 import random
 
@@ -56,11 +66,23 @@ class MTDraws:
 
     def __init__(self, rng: random.Random):
         self.rng = rng
+        self._params = {}
 
     exp = staticmethod(np.exp)
 
     def site(self, *key):
         return self
+
+    def params(self, P):
+        """manipulator.parameters(cfg) / manipulator.params: ONE shared list
+        (manipulator.py:178-185) that GA / GGA shuffle in place
+        (evolutionarytechniques.py:55-56, globalGA.py:54-56,71-72):
+        every later iteration -- seed_config, random(), the next mutation's
+        shuffle, CrossoverMixin, HybridParticle.move -- sees the order the last
+        shuffle left.  Persistent across calls on this draw source."""
+        if P not in self._params:
+            self._params[P] = list(range(P))
+        return self._params[P]
 
     def random(self):
         return self.rng.random()
@@ -114,7 +136,11 @@ class MTDraws:
         return v
 
     def cross(self, xop, p1, p2, d):
-        raise NotImplementedError("MT replay of the op3_cross_* operators is not restated")
+        """op3_cross_<xop> (manipulator.py:1179-1353) on the MT stream: each
+        operator's random.randint calls, in the reference's order (PX: the cut
+        point; PMX, OX1: the section start; CX: the start index; OX3: r1 then
+        r2), through the same list code as the counter form (oracle/perm.py)"""
+        return pm.cross(xop, list(p1), list(p2), d, self.rng)
 
 
 class _Queue:
@@ -147,6 +173,12 @@ class CounterDraws:
         self.ga = np.array([self.g], dtype=np.uint64)
 
     exp = staticmethod(ut_exp)
+
+    @staticmethod
+    def params(P):
+        """the batch form keys every draw by parameter index, so the order of
+        the manipulator's shared list does not matter: a fresh list"""
+        return list(range(P))
 
     def _blk(self, stream):
         return [int(v[0]) for v in ph.draw(self.seed, self.ga, stream & 0xFFFFFFFF, self.round_, self.op)]
@@ -311,7 +343,8 @@ def pso_move_scalar(space, position, velocity, best, global_best, draws, omega=0
     c1=phi_g, c2=phi_l, xchoice, velocity=velocity[p]).  Stored-value rows
     (PERM: item-index lists).  -> (new position, new velocity)"""
     pos, vel = list(position), list(velocity)
-    for i, prm in enumerate(space):
+    for i in draws.params(len(space)):                  # for p in m.params (the shared list's order)
+        prm = space[i]
         d = draws.site("pso", i, prm.kind)
         pos[i], nv = op3_swarm(prm, d, pos[i], global_best[i], best[i], omega, phi_g, phi_l, vel[i], sigma,
                                xchoice)
@@ -325,8 +358,13 @@ def pso_move_scalar(space, position, velocity, best, global_best, draws, omega=0
 def _manip_random(space, draws, which):
     """manipulator.random() (manipulator.py:171-176): seed_config, then
     op1_randomize of every param"""
-    cfg = [draws.site("parent", which, i).seed_value(p) for i, p in enumerate(space)]
-    return [draws.site("parent", which, i).op1_randomize(p, cfg[i]) for i, p in enumerate(space)]
+    order = list(draws.params(len(space)))              # seed_config / random() iterate self.params
+    cfg = [None] * len(space)
+    for i in order:
+        cfg[i] = draws.site("parent", which, i).seed_value(space[i])
+    for i in order:
+        cfg[i] = draws.site("parent", which, i).op1_randomize(space[i], cfg[i])
+    return cfg
 
 
 def _key(space, cfg):
@@ -370,13 +408,14 @@ def _crossover(space, draws, parents, crossover_strength, crossover):
     cfg1, cfg2 = parents
     new = list(cfg1)                                              # manipulator.copy(cfg1)
     if crossover_strength > 0:                                    # GlobalEvolutionaryTechnique.crossover
-        params = list(range(len(space)))
+        params = draws.params(len(space))                         # the shared list, shuffled in place
         d = int(crossover_strength * len(params))
         draws.site("gga", d, len(space)).shuffle(params)
         for i in params[:d]:
             new[i] = cfg2[i]                                      # set_value(new, get_value(cfg2))
         return new
-    for i, prm in enumerate(space):                               # CrossoverMixin.crossover
+    for i in list(draws.params(len(space))):                      # CrossoverMixin.crossover
+        prm = space[i]
         if crossover != pm.X_NONE and prm.kind == PERM and len(prm.options) > 6:
             new[i] = draws.site("xmix", i).cross(crossover, list(cfg1[i]), list(cfg2[i]), len(prm.options) // 3)
     return new
@@ -384,12 +423,12 @@ def _crossover(space, draws, parents, crossover_strength, crossover):
 
 def _mutation(space, draws, cfg, z, mutation_rate, must_mutate_count, normal, sigma, P):
     """EvolutionaryTechnique.mutation (:51-61), in place"""
-    params = list(range(P))
+    params = draws.params(P)                                      # the shared list, shuffled in place
     site = draws.site("mutation", z, must_mutate_count, P)
     site.shuffle(params)
-    for i in params[:must_mutate_count]:
+    for i in list(params[:must_mutate_count]):
         _mutate_param(space[i], draws.site("mutate", z, i), cfg, i, normal, sigma)
-    for i in params[must_mutate_count:]:
+    for i in list(params[must_mutate_count:]):
         if site.random() < mutation_rate:
             _mutate_param(space[i], draws.site("mutate", z, i), cfg, i, normal, sigma)
 

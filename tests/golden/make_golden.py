@@ -13,6 +13,9 @@ Inputs read as DATA from the reference:
     the BLOCK_SIZE whose Python-2-layout hash_config reproduces it.
   * samples/gcc-options/matmul-record.csv  -- recorded gcc-flag configs
     (enum codes 1..3 decoded with the sorted mapping of api.py:296-300).
+  * samples/gcc-options/raytracer-record.csv  -- 2,269 more recorded configs
+    of the same 339-param space (same header), tuned on another program: the
+    second C4 history fixture.
   * samples/gcc-options/params.def  -- text; the DEFPARAM(name, desc,
     default, min, max) records give the integer --param ranges exactly as
     tune_gcc.py:136-158 extracts them (the same regex, the same three textual
@@ -133,6 +136,37 @@ def gcc_space_and_rows(nrows=512, nhash=64):
                    "hashes_py3": hashes}, f)
 
 
+def gcc_raytracer_history(nhash=64):
+    """samples/gcc-options/raytracer-record.csv, decoded like the matmul record
+    into the gcc_space.json space: every row as SoA f64 values (enum -> option
+    index) + its recorded qor, and the oracle's hash_config of the first rows"""
+    path = os.path.join(REF, "samples/gcc-options/raytracer-record.csv")
+    with open(path) as f:
+        r = csv.reader(f)
+        header = next(r)
+        rows = [row for row in r]
+    sp = json.load(open(os.path.join(HERE, "gcc_space.json")))
+    cols = [c for c in header if c not in ("time", "build_time", "qor", "is_best")]
+    assert cols == [q[1] for q in sp["params"]], "raytracer record: not the matmul record's space"
+    code = {int(k): v for k, v in sp["enum_code"].items()}
+    opts = ["on", "off", "default"]
+    params = []
+    for kind, name, rng in sp["params"]:
+        params.append(Param(name, ENUM, options=list(opts)) if kind == "EnumParameter" else Param(name, INT, *rng))
+    idx = [header.index(c) for c in cols]
+    data = np.array([[int(float(row[i])) for i in idx] for row in rows], dtype=np.int64)
+    for j, p in enumerate(params):
+        if p.kind == INT:
+            assert p.lo <= data[:, j].min() and data[:, j].max() <= p.hi, (p.name, p.lo, p.hi)
+    allv = np.array([[float(opts.index(code[int(v)])) if p.kind == ENUM else float(v) for p, v in zip(params, row)]
+                     for row in data]).T
+    qor = np.array([float(row[header.index("qor")]) for row in rows])
+    cfgs = [[code[int(v)] if p.kind == ENUM else int(v) for p, v in zip(params, row)] for row in data[:nhash]]
+    hashes = [oh.hash_config(params, c) for c in cfgs]
+    np.savez_compressed(os.path.join(HERE, "gcc_raytracer_history.npz"), values=allv.astype(np.float64), qor=qor,
+                        hashes_py3=np.array(hashes))
+
+
 def r64():
     rng = np.random.default_rng(7)
     space = [Param(d, FLOAT, -1000.0, 1000.0) for d in range(64)]
@@ -176,6 +210,7 @@ def gp_golden():
 if __name__ == "__main__":
     tutorial_db()
     gcc_space_and_rows()
+    gcc_raytracer_history()
     r64()
     de_golden()
     gp_golden()

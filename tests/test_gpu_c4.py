@@ -162,3 +162,55 @@ def test_c4_pso_round(c4):
     dup = e.dedup(dig).cpu().numpy().tolist()
     assert dup == osel.dedup(hx, c4["hist_hex"])
     _score_and_check(c4, wx, dup, k=32)
+
+
+def test_c4_second_history_raytracer(c4, golden_dir):
+    """the second recorded history of the same space
+    (samples/gcc-options/raytracer-record.csv, 2,269 configs:
+    tests/golden/gcc_raytracer_history.npz): every recorded config hashes on
+    the device as the oracle hashes it (the committed oracle digests of its
+    first rows too); deduplicated against the matmul history the mask is the
+    oracle's set membership; then both histories together are the dedup set
+    of a GA round from the raytracer's best config, scored by a GP on the
+    raytracer's recorded qor"""
+    e, space, H = c4["e"], c4["space"], c4["H"]
+    from uptune_amd.engine import digests_to_hex
+    z = np.load(os.path.join(golden_dir, "gcc_raytracer_history.npz"))
+    rv, rq = z["values"], z["qor"]
+    assert rv.shape == (339, 2269)
+    dig = e.hash(torch.from_numpy(np.ascontiguousarray(rv)).cuda())
+    hx = digests_to_hex(dig)
+    assert hx[:len(z["hashes_py3"])] == list(z["hashes_py3"])
+    assert hx == H(rv)
+    dup = e.dedup(dig).cpu().numpy().tolist()
+    assert dup == osel.dedup(hx, c4["hist_hex"])      # matmul history + repeats inside the raytracer record
+    # a fresh engine: both recorded histories are the dedup set
+    from uptune_amd import spaces
+    from uptune_amd.engine import BatchEngine
+    e2 = BatchEngine(spaces.gcc(), device=0, seed=45)
+    e2.history_reset(0)
+    e2.history_add(e.hash(torch.from_numpy(np.ascontiguousarray(c4["hist"])).cuda()))
+    e2.history_add(dig)
+    best = rv[:, int(np.argmin(rq))].copy()
+    vals, inv = e2.propose_ga(M, parent1=best, round_=5, cand_base=3, mutation_rate=0.05)
+    wv, winv = oga.propose_ga_vec(space, best, None, 45, 5, 3, M, mutation_rate=0.05)
+    np.testing.assert_array_equal(vals.cpu().numpy(), wv)
+    np.testing.assert_array_equal(inv.cpu().numpy().astype(bool), winv)
+    allv = np.ascontiguousarray(np.concatenate([wv, rv[:, :100], c4["hist"][:, :100]], axis=1))
+    d2 = e2.hash_parent(torch.from_numpy(allv).cuda(), best)
+    h2 = digests_to_hex(d2)
+    assert h2 == H(allv)
+    m2 = e2.dedup(d2).cpu().numpy().tolist()
+    assert m2 == osel.dedup(h2, c4["hist_hex"] | set(hx))
+    assert all(m2[M:])
+    ok = np.flatnonzero(np.isfinite(rq))[:1024]
+    X = features(space, rv[:, ok]).T
+    y = rq[ok].astype(np.float64)
+    e2.gp_fit(X, y, lengthscale=2.0, sigma_f2=1.0, sigma_n2=1e-6, jitter=1e-8)
+    mu, var, score = e2.gp_score_values(torch.from_numpy(allv).cuda(), acq=e2.acq("ei"),
+                                        dup=torch.tensor(m2, dtype=torch.uint8, device="cuda"))
+    g = ogp.GP(X, y, lengthscale=2.0, sigma_f2=1.0, sigma_n2=1e-6, jitter=1e-8)
+    wmu, wvar = g.posterior(features(space, allv).T)
+    np.testing.assert_allclose(mu.cpu().numpy(), wmu, rtol=1e-5, atol=1e-9)
+    np.testing.assert_allclose(var.cpu().numpy(), wvar, rtol=1e-5, atol=1e-9)
+    e2.close()

@@ -270,3 +270,25 @@ def test_de_at_equals_vectorised():
         assert np.array_equal(ode.propose_de_at(space, g, npop, 5, 3, 0.2, 1), full[:, g])
         mem = np.array([0, 1, 299, 7])
         assert np.array_equal(ode.population_init(space, npop, 5, members=mem), pop[:, mem])
+
+
+def test_raytracer_history_fixture(golden_dir):
+    """the second C4 history (samples/gcc-options/raytracer-record.csv decoded
+    into the gcc_space.json space): values inside the params.def ranges, and
+    the committed digests are the oracle's hash_config of its first rows"""
+    import json
+    z = np.load(os.path.join(golden_dir, "gcc_raytracer_history.npz"))
+    sp = json.load(open(os.path.join(golden_dir, "gcc_space.json")))
+    v = z["values"]
+    assert v.shape == (len(sp["params"]), 2269) and z["qor"].shape == (2269,)
+    from oracle.space import ENUM, INT, Param, from_f64
+    from oracle import hashing as oh
+    space = [Param(n, ENUM, options=["on", "off", "default"]) if k == "EnumParameter" else Param(n, INT, *r)
+             for k, n, r in sp["params"]]
+    for j, p in enumerate(space):
+        if p.kind == INT:
+            assert p.lo <= v[j].min() and v[j].max() <= p.hi
+        else:
+            assert set(np.unique(v[j])) <= {0.0, 1.0, 2.0}
+    for c in range(8):
+        assert oh.hash_config(space, [from_f64(p, v[i, c]) for i, p in enumerate(space)]) == z["hashes_py3"][c]
