@@ -1122,3 +1122,52 @@ def test_gp_score_values_equals_score_of_encoded(which, prec):
     tol = (RTOL, ATOL) if prec == 64 else (1e-3, 1e-3)
     np.testing.assert_allclose(mu1.cpu().numpy(), mu, rtol=tol[0], atol=tol[1])
     np.testing.assert_allclose(var1.cpu().numpy(), var, rtol=tol[0], atol=tol[1])
+
+
+def test_chol_fused_refit_bitwise_and_not_pd():
+    """the fused refit (k_chol_update_diag factors the next diagonal block
+    inside the trailing update; default from 2048 padded rows) gives bitwise
+    the factor of the unfused chain (UT_CHOL_FUSE=0 vs 1: the posterior and
+    EI of a batch are bitwise equal), and a kernel matrix that is not positive
+    definite in a block the fused kernel factors is flagged (gp_fit_ok() is
+    False, every score NaN, nothing selected) -- ADVICE r3"""
+    _require_gpu()
+    rng = np.random.default_rng(41)
+    n, d = 2200, 6
+    X = rng.uniform(size=(n, d))
+    y = np.sum((X - 0.4) ** 2, axis=1)
+    U = torch.from_numpy(np.ascontiguousarray(rng.uniform(size=(d, 3000)))).cuda()
+    U[:, :5] = torch.from_numpy(np.ascontiguousarray(X[:5].T)).cuda()
+    space = [Param("f%d" % i, FLOAT, 0.0, 1.0) for i in range(d)]
+    old = os.environ.get("UT_CHOL_FUSE")
+    outs = []
+    try:
+        for fuse in ("0", "1"):
+            os.environ["UT_CHOL_FUSE"] = fuse
+            e = engine(space, seed=2)
+            e.gp_fit(X, y, lengthscale=0.3, sigma_f2=1.0, sigma_n2=1e-6, jitter=1e-8)
+            outs.append([t.cpu() for t in e.gp_score(U, acq=e.acq("ei"))])
+            e.close()
+        for a, b in zip(*outs):
+            assert torch.equal(a, b)
+        # not PD from block row 2100 on: rows 2100.. repeat rows 0..99 (the Schur
+        # complement there is ~0) and the diagonal carries -0.5
+        X2 = X.copy()
+        X2[2100:] = X[:100]
+        os.environ["UT_CHOL_FUSE"] = "1"
+        e = engine(space, seed=2)
+        e.gp_fit(X2, y, lengthscale=0.05, sigma_f2=1.0, sigma_n2=-0.5, jitter=0.0, wait=False)
+        assert not e.gp_fit_ok()
+        _, _, score = e.gp_score(U, acq=e.acq("ei"))
+        assert torch.isnan(score).all()
+        idx, _ = e.topk(score, 8)
+        assert idx.cpu().tolist() == [-1] * 8
+        # the same matrix with its duplicates removed is PD on the fused path
+        e.gp_fit(X2[:2100], y[:2100], lengthscale=0.05, sigma_f2=1.0, sigma_n2=-0.5, jitter=0.0, wait=False)
+        assert e.gp_fit_ok()
+        e.close()
+    finally:
+        if old is None:
+            os.environ.pop("UT_CHOL_FUSE", None)
+        else:
+            os.environ["UT_CHOL_FUSE"] = old

@@ -116,3 +116,16 @@ def test_compile_space_scaled_kinds():
     assert arr[[i for i, ps in enumerate(spec.params) if ps.name == "logint_2"][0]].vtab_count == 65521
     cfg = {"pow2_1": 1 << 9, "logint_2": 300}
     assert by["pow2_1"].to_value(cfg["pow2_1"]) == 512.0 and by["logint_2"].from_value(300.0) == 300
+
+
+def test_encode_decode_ints_beyond_int64():
+    """INT values of magnitude >= 2^63 take the per-value float(int(v)) /
+    int(x) path: no OverflowError on encode, no int64 wrap on decode"""
+    m = ConfigurationManipulator([IntegerParameter("big", -(1 << 70), 1 << 70), FloatParameter("x", 0.0, 1.0)])
+    spec = compile_space(m)
+    cfgs = [{"big": 1 << 65, "x": 0.5}, {"big": -(1 << 64) - 12345, "x": 0.25}, {"big": 7, "x": 1.0}]
+    vals = spec.encode_configs(cfgs)
+    assert vals[0].tolist() == [float(1 << 65), float(-(1 << 64) - 12345), 7.0]
+    back = spec.decode_values(vals)
+    assert [c["big"] for c in back] == [int(float(1 << 65)), int(float(-(1 << 64) - 12345)), 7]
+    assert [c["x"] for c in back] == [0.5, 0.25, 1.0]

@@ -285,7 +285,10 @@ class SpaceSpec:
             if ps.kind == L.UT_FLOAT:
                 out[c0] = np.fromiter(map(float, col), dtype=np.float64, count=n)
             elif ps.kind in (L.UT_INT, L.UT_LOGINT, L.UT_POW2):
-                out[c0] = np.fromiter(map(int, col), dtype=np.int64, count=n)
+                try:
+                    out[c0] = np.fromiter(map(int, col), dtype=np.int64, count=n)
+                except OverflowError:   # |v| >= 2^63: float(int(v)) per value, as to_value does
+                    out[c0] = np.fromiter(map(ps.to_value, col), dtype=np.float64, count=n)
             elif ps.kind == L.UT_BOOL:
                 out[c0] = np.fromiter(map(bool, col), dtype=bool, count=n)
             elif ps.kind == L.UT_ENUM:
@@ -304,7 +307,10 @@ class SpaceSpec:
             if ps.kind == L.UT_FLOAT:
                 cols.append(x.tolist())
             elif ps.kind in (L.UT_INT, L.UT_LOGINT, L.UT_POW2):
-                cols.append(x.astype(np.int64).tolist())
+                if x.size and not (np.all(np.abs(x) < 2.0 ** 63)):   # int64 would wrap: int(x) per value
+                    cols.append([ps.from_value(a) for a in x.tolist()])
+                else:
+                    cols.append(x.astype(np.int64).tolist())
             elif ps.kind == L.UT_BOOL:
                 cols.append((x != 0.0).tolist())
             elif ps.kind == L.UT_ENUM:
