@@ -5,7 +5,7 @@
 # a failure ends the script.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 set -e
-bash scripts/r02_prof.sh
+bash scripts/ab/r02_prof.sh
 bash scripts/pmc_clock.sh
 python3 scripts/clock_summary.py gpurun_out/clk > gpurun_out/clock.json
 if [ -z "$NO_BENCH" ]; then

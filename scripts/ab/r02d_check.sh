@@ -5,7 +5,7 @@
 # limit; a failure ends the script.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
-SKIP_C4=1 bash scripts/r02_check.sh || exit $?
+SKIP_C4=1 bash scripts/ab/r02_check.sh || exit $?
 timeout -k 10 300 python bench.py --config c4 --steps 5 --warmup 2 > gpurun_out/bench_c4.log 2>&1 || exit 1
 tail -1 gpurun_out/bench_c4.log | cut -c1-120
 timeout -k 10 200 python scripts/c5_bandit.py --prune 256 > /dev/null 2>&1 || exit 1

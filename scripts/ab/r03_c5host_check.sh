@@ -12,4 +12,4 @@ run() { local t=$1 name=$2; shift 2; timeout -k 10 $t "$@" > $O/$name.log 2>&1; 
 run 300 c5_dense python scripts/c5_bandit.py --generations 100
 run 300 c5_prune python scripts/c5_bandit.py --generations 100 --prune 256
 run 300 c5_prune2 python scripts/c5_bandit.py --generations 100 --prune 256
-bash scripts/r03_c5_trace.sh
+bash scripts/ab/r03_c5_trace.sh

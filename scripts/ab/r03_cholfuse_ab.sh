@@ -13,4 +13,4 @@ for f in 0 1; do
   UT_CHOL_FUSE=$f timeout -k 10 300 python scripts/exp/fit_alone.py > $O/fa.log 2>&1 || { echo "fit_alone rc=$?"; tail -5 $O/fa.log; exit 1; }
   echo "fuse=$f"; cat $O/fa.log | grep "n="
 done
-bash scripts/r03_fitsched_ab.sh
+bash scripts/ab/r03_fitsched_ab.sh
