@@ -1157,11 +1157,14 @@ def test_chol_fused_refit_bitwise_and_not_pd():
         os.environ["UT_CHOL_FUSE"] = "1"
         e = engine(space, seed=2)
         e.gp_fit(X2, y, lengthscale=0.05, sigma_f2=1.0, sigma_n2=-0.5, jitter=0.0, wait=False)
-        assert not e.gp_fit_ok()
-        _, _, score = e.gp_score(U, acq=e.acq("ei"))
-        assert torch.isnan(score).all()
+        _, _, score = e.gp_score(U, acq=e.acq("ei"))       # enqueued behind the failing fit: NaN
         idx, _ = e.topk(score, 8)
+        assert torch.isnan(score).all()
         assert idx.cpu().tolist() == [-1] * 8
+        assert not e.gp_fit_ok()
+        from uptune_amd._lib import UthotError
+        with pytest.raises(UthotError):                     # no usable fit until a new one succeeds
+            e.gp_score(U, acq=e.acq("ei"))
         # the same matrix with its duplicates removed is PD on the fused path
         e.gp_fit(X2[:2100], y[:2100], lengthscale=0.05, sigma_f2=1.0, sigma_n2=-0.5, jitter=0.0, wait=False)
         assert e.gp_fit_ok()

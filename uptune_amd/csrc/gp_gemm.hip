@@ -937,11 +937,22 @@ __device__ __forceinline__ int h3_linv_exp(const unsigned long long* amax_bits) 
 // and between stage kt's two k16 sub-steps (its B planes), and lands while
 // stage kt's 48 MFMAs per wave run.  part[rt][col] gets the column partial
 // sum_{r in tile} V[r][col]^2 (RT2 = rows / 256 of them).
+//
+// Item order (sched): 0 = per XCD, strip-major (a strip's row tiles, longest
+// first, then the next strip); 1 = "paired groups": an item is the row-tile
+// pair (RT2 - 1 - p, p) of one strip (every pair the same length, RT2 + 1
+// tiles of k), and an XCD's W workgroups take W items at once as P pairs x
+// S strips (P = ceil(RT2 / 2), S = W / P).  Equal lengths keep a group in
+// step, so the S workgroups of a pair read each L^-1 stage at about the same
+// time (one fetch from the Infinity Cache, S - 1 L2 hits) and the P
+// workgroups of a strip share its long-tile K* stages -- where sched 0 reads
+// the whole L^-1 triangle per strip from the Infinity Cache.
 __global__ __launch_bounds__(512, 2) void k_gp_var_h3(const _Float16* __restrict__ A, int64_t a_lo,
                                                       const _Float16* __restrict__ B, int64_t b_lo, int32_t K,
                                                       int32_t RT2, int32_t CT, int64_t m, int32_t* __restrict__ ticket,
                                                       double* __restrict__ part, int64_t ldp,
-                                                      const unsigned long long* __restrict__ amax_bits, int32_t kexp) {
+                                                      const unsigned long long* __restrict__ amax_bits, int32_t kexp,
+                                                      int32_t sched, int32_t S) {
   __shared__ __attribute__((aligned(16))) _Float16 lds[H3_NS * H3_STAGE + 8];
   int32_t& s_item = *reinterpret_cast<int32_t*>(lds + H3_NS * H3_STAGE);
   const int t = threadIdx.x, lane = t & 63;
@@ -951,13 +962,27 @@ __global__ __launch_bounds__(512, 2) void k_gp_var_h3(const _Float16* __restrict
   const int32_t KB = K / H3_BK;
   const double unscale2 = __builtin_ldexp(1.0, -2 * (h3_linv_exp(amax_bits) + kexp));
 
+  const int32_t P = (RT2 + 1) / 2;
   for (;;) {
     if (t == 0) s_item = atomicAdd(&ticket[xcd], 1);
     __syncthreads();
     const int32_t j = s_item;
-    const int32_t ct = (j / RT2) * 8 + xcd;
+    int32_t ct, rts[2], nrt;
+    if (sched == 1) {
+      const int32_t G = j / (P * S), q = j % (P * S), p = q % P;
+      ct = (G * S + q / P) * 8 + xcd;
+      rts[0] = RT2 - 1 - p;
+      rts[1] = p;
+      nrt = rts[1] == rts[0] ? 1 : 2;
+    } else {
+      ct = (j / RT2) * 8 + xcd;
+      rts[0] = RT2 - 1 - (j % RT2);
+      nrt = 1;
+    }
     if (ct >= CT) break;
-    const int32_t rt = RT2 - 1 - (j % RT2);
+    for (int32_t ri = 0; ri < nrt; ++ri) {
+    if (ri > 0) __syncthreads();   // the previous tile's reduction buffer (LDS ring) fully read
+    const int32_t rt = rts[ri];
     const int32_t row0 = rt * H3_BM;
     const int32_t nk = min(K, row0 + H3_BM) / H3_BK;
     const _Float16* Ab = A + (int64_t)rt * KB * H3_BLK;
@@ -1014,6 +1039,7 @@ __global__ __launch_bounds__(512, 2) void k_gp_var_h3(const _Float16* __restrict
       const int64_t col = (int64_t)ct * H3_BN + t;
       if (col < m)
         part[(int64_t)rt * ldp + col] = ((red[t] + red[H3_BN + t]) + (red[2 * H3_BN + t] + red[3 * H3_BN + t])) * unscale2;
+    }
     }
   }
 }
@@ -1085,9 +1111,12 @@ int launch_gemm_var(ut_ctx* c, int prec, const void* LinvT, int64_t lda, const v
     int32_t nb2 = (c->n_cu / 8) * 8;
     if (items2 < nb2) nb2 = (int32_t)(((items2 + 7) / 8) * 8);
     const unsigned long long* amax = reinterpret_cast<const unsigned long long*>(c->gp_ctr + 16);
+    // paired groups: S strips per group so that P x S items fill an XCD's workgroups
+    const int32_t P2 = (RT2 + 1) / 2, W = nb2 / 8;
+    const int32_t S2 = W / P2 > 1 ? W / P2 : 1;
     hipLaunchKernelGGL(k_gp_var_h3, dim3(nb2), dim3(512), 0, c->stream, (const _Float16*)LinvT, (int64_t)n256 * npad,
                        (const _Float16*)kst, ldk * (int64_t)npad, npad, RT2, (int32_t)((m + H3_BN - 1) / H3_BN), m,
-                       c->gp_ctr, part, ldk, amax, h3_kstar_exp(c->gp_sf2));
+                       c->gp_ctr, part, ldk, amax, h3_kstar_exp(c->gp_sf2), c->h3_sched, S2);
   }
   else if (fp32)
     hipLaunchKernelGGL(k_gp_var<float>, dim3(nb), dim3(V_NT), 0, c->stream, (const float*)LinvT, lda,

@@ -203,6 +203,9 @@ struct ut_ctx {
   // for fits of n >= 2048.  Measured, f16x3: C3 (n 4096) 149.2 vs 153.0 ms per
   // round; C2 (n 1024) 12.9-13.1 vs 12.8 ms.  UT_HASH_AFTER_KSTAR
   int32_t hash_after_kstar = -1;
+  // k_gp_var_h3 item order: 0 = strip-major, 1 = paired row tiles in XCD
+  // groups (L^-1 stages shared in L2 by the group's workgroups); UT_H3_SCHED
+  int32_t h3_sched = 1;
 
   struct PopSlot {
     double* pop = nullptr;
