@@ -637,7 +637,7 @@ __global__ __launch_bounds__(VP_NT, 2) void k_gp_var_pp(const double* __restrict
                                                         int32_t* __restrict__ ticket, double* __restrict__ part,
                                                         int64_t ldp, const double* __restrict__ beta,
                                                         double* __restrict__ mpart, int32_t kcs, int32_t per_strip,
-                                                        double* __restrict__ vbuf) {
+                                                        double* __restrict__ vbuf, int32_t sched, int32_t S) {
   // one __shared__ object (see k_gp_var): ring, reduction buffer, ticket slot
   __shared__ __attribute__((aligned(16))) double lds[VP_ST * VP_STAGE + 4 * VP_BN + VAR_BM + 2];
   double* red = lds + VP_ST * VP_STAGE;  // [2][128] squares, [2][128] mean
@@ -663,11 +663,13 @@ __global__ __launch_bounds__(VP_NT, 2) void k_gp_var_pp(const double* __restrict
                                        (__attribute__((address_space(3))) void*)(st + VP_SA + q * VP_BN), 16, 0, 0);
     }
   };
+  const int32_t P = (RT + 1) / 2;
   for (;;) {
     if (t == 0) s_item = atomicAdd(&ticket[xcd], 1);
     __syncthreads();  // also: the previous item's epilogue is done with `red`
     const int32_t j = s_item;
     int32_t ct, rt, kt0, kt1, g = 0;
+    int32_t rt2 = -1;   // sched 1: the pair's second (short) row tile
     if constexpr (SPLIT) {
       g = j * 8 + xcd;
       if (g >= CT * per_strip) break;
@@ -682,6 +684,17 @@ __global__ __launch_bounds__(VP_NT, 2) void k_gp_var_pp(const double* __restrict
       }
       kt0 = rem * kcs;
       kt1 = min(var_nk(K, rt), kt0 + kcs);
+    } else if (sched == 1) {
+      // paired groups (as k_gp_var_h3): item = row tiles (RT - 1 - p, p) of one
+      // strip, every item the same length; an XCD's workgroups take P pairs x S
+      // strips at once, so a group shares each L^-1 stage through L2
+      const int32_t G = j / (P * S), q = j % (P * S), p = q % P;
+      ct = (G * S + q / P) * 8 + xcd;
+      if (ct >= CT) break;
+      rt = RT - 1 - p;
+      rt2 = p != rt ? p : -1;
+      kt0 = 0;
+      kt1 = var_nk(K, rt);
     } else {
       ct = (j / RT) * 8 + xcd;
       if (ct >= CT) break;  // uniform: every wave of the block leaves together
@@ -689,6 +702,7 @@ __global__ __launch_bounds__(VP_NT, 2) void k_gp_var_pp(const double* __restrict
       kt0 = 0;
       kt1 = var_nk(K, rt);
     }
+    for (;;) {   // the item's row tiles (one, or sched 1's pair)
     const int64_t col0 = (int64_t)ct * VP_BN;
     const int32_t row0 = rt * VAR_BM;
     vd4 acc[4][4];
@@ -746,7 +760,7 @@ __global__ __launch_bounds__(VP_NT, 2) void k_gp_var_pp(const double* __restrict
 #pragma unroll
           for (int r = 0; r < 4; ++r)
             vt[((2 * i + wm) * 16 + (lane >> 4) + 4 * r) * VP_BN + wn * 64 + jj * 16 + (lane & 15)] = acc[i][jj][r];
-      continue;   // the next ticket's barrier orders the LDS ring's reuse
+      break;   // to the next ticket, whose barrier orders the LDS ring's reuse
     }
     // epilogue: column sums of squares over the tile's 128 rows and the mean
     // partial sum_r V[r][c] beta_r (beta = L^-1 y)
@@ -778,6 +792,12 @@ __global__ __launch_bounds__(VP_NT, 2) void k_gp_var_pp(const double* __restrict
         part[(int64_t)rt * ldp + col] = red[t] + red[VP_BN + t];
         mpart[(int64_t)rt * ldp + col] = red[2 * VP_BN + t] + red[3 * VP_BN + t];
       }
+    }
+    if (SPLIT || rt2 < 0) break;
+    rt = rt2;
+    rt2 = -1;
+    kt1 = var_nk(K, rt);
+    __syncthreads();   // red / sbeta read; the ring is reused by the next tile
     }
   }
 }
@@ -1144,13 +1164,16 @@ int launch_gemm_var(ut_ctx* c, int prec, const void* LinvT, int64_t lda, const v
       if (items_s < nbp) nbp = (int32_t)(((items_s + 7) / 8) * 8);
       hipLaunchKernelGGL(k_gp_var_pp<true>, dim3(nbp), dim3(VP_NT), 0, c->stream, (const double*)LinvT, lda,
                          (const double*)kst, ldk, npad, RT, CTp, m, c->gp_ctr, part, ldk, beta, mpart, kcs, per_strip,
-                         c->var_vbuf.p);
+                         c->var_vbuf.p, 0, 1);
       hipLaunchKernelGGL(k_var_split_red, dim3(RT, CTp), dim3(1024), 0, c->stream, c->var_vbuf.p, npad, kcs, per_strip,
                          m, beta, part, mpart, ldk);
     } else {
       if (items_p < nbp) nbp = (int32_t)(((items_p + 7) / 8) * 8);
+      const int32_t Pp = (RT + 1) / 2, Wp = nbp / 8;
+      const int32_t Sp = Wp / Pp > 1 ? Wp / Pp : 1;
       hipLaunchKernelGGL(k_gp_var_pp<false>, dim3(nbp), dim3(VP_NT), 0, c->stream, (const double*)LinvT, lda,
-                         (const double*)kst, ldk, npad, RT, CTp, m, c->gp_ctr, part, ldk, beta, mpart, 0, 0, nullptr);
+                         (const double*)kst, ldk, npad, RT, CTp, m, c->gp_ctr, part, ldk, beta, mpart, 0, 0, nullptr,
+                         c->var_sched, Sp);
     }
   }
   UT_LAUNCH_CHECK(c);
