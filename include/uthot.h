@@ -314,6 +314,14 @@ int ut_gp_join_fit(ut_ctx* ctx);
  * matrix was positive definite (*ok = 1) or not (*ok = 0: later scoring
  * yields NaN scores until a new fit succeeds); not an error either way */
 int ut_gp_fit_status(ut_ctx* ctx, int32_t* ok);
+/* the K* contraction the current fit scores with: *categorical = 1 when its
+ * ENUM / BOOL one-hot blocks go through the int8 code product (one lengthscale
+ * over those features, every training row one-hot there; candidates encoded
+ * by the library), 0 = the dense fp64 contraction over every feature.  Both
+ * give the same posterior (the categorical part of |x - u|^2 is exactly
+ * 2 / ell^2 per mismatching ENUM, 1 / ell^2 per BOOL); UT_CAT_KSTAR=0 turns
+ * the categorical form off. */
+int ut_gp_kstar_mode(ut_ctx* ctx, int32_t* categorical);
 /* f_best (min standardised y), y mean/std used for standardisation */
 int ut_gp_stats(ut_ctx* ctx, double* f_best, double* y_mean, double* y_std);
 

@@ -1174,3 +1174,105 @@ def test_chol_fused_refit_bitwise_and_not_pd():
             os.environ.pop("UT_CHOL_FUSE", None)
         else:
             os.environ["UT_CHOL_FUSE"] = old
+
+
+@pytest.mark.parametrize("which", ["hpl", "gcc", "mixed", "perm"])
+@pytest.mark.parametrize("prec", [64, 32, 16])
+def test_categorical_kstar_equals_dense(which, prec):
+    """The categorical K* (ENUM / BOOL one-hot blocks as an int8 code product on
+    v_mfma_i32_16x16x64_i8, the other features on the fp64 contraction) gives
+    the dense contraction's posterior: ut_gp_score_values (categorical, the
+    library's own encoding) against ut_gp_score on the same candidates' feature
+    matrix (dense), and the oracle GP.  fp64 within 1e-11 of the dense path
+    (only the fp summation order of the distances differs), lower tiers at
+    their 1e-3 tolerance against the oracle."""
+    _require_gpu()
+    from uptune_amd import spaces
+    space = {"hpl": hpl_space, "mixed": mixed_space, "perm": perm_space,
+             "gcc": lambda: oracle_space(spaces.gcc())}[which]()
+    e = engine(space, seed=9)
+    e.gp_set_precision(prec)
+    n, m = (700, 5000) if which != "gcc" else (400, 3000)
+    tr = ode.population_init(space, n, seed=8)
+    X = features(space, tr).T
+    y = np.sum((X - 0.35) ** 2, axis=1)
+    ell = {"hpl": 1.0, "gcc": 2.0, "mixed": 0.7, "perm": 0.9}[which]
+    e.gp_fit(X, y, lengthscale=ell, sigma_f2=1.0, sigma_n2=1e-6, jitter=1e-8)
+    assert e.gp_kstar_mode() == "categorical"
+    cand = ode.population_init(space, m, seed=7)
+    cand[:, :20] = tr[:, :20]                  # candidates on training points (var ~ 0)
+    vals = dev(cand)
+    mu_c, var_c, sc_c = [t.cpu().numpy() for t in e.gp_score_values(vals, acq=e.acq("ei"))]
+    mu_d, var_d, sc_d = [t.cpu().numpy() for t in e.gp_score(e.encode(vals), acq=e.acq("ei"))]
+    g = ogp.GP(X, y, lengthscale=ell, sigma_f2=1.0, sigma_n2=1e-6, jitter=1e-8)
+    wmu, wvar = g.posterior(features(space, cand).T)
+    ei = ogp.acquisition(wmu, wvar, g.f_best)
+    if prec == 64:
+        np.testing.assert_allclose(mu_c, mu_d, rtol=1e-11, atol=1e-12)
+        np.testing.assert_allclose(var_c, var_d, rtol=1e-11, atol=1e-12)
+        np.testing.assert_allclose(sc_c, sc_d, rtol=1e-11, atol=1e-12)
+        tol = dict(rtol=RTOL, atol=ATOL)
+    else:
+        tol = dict(rtol=1e-3, atol=1e-5)
+    np.testing.assert_allclose(mu_c, wmu, **tol)
+    np.testing.assert_allclose(var_c, wvar, **tol)
+    np.testing.assert_allclose(sc_c, ei, **tol)
+
+
+def test_categorical_kstar_fallbacks():
+    """the dense contraction when the categorical form does not apply: a
+    training row whose ENUM block is not one-hot, per-feature lengthscales
+    that differ inside the categorical features, UT_CAT_KSTAR=0 -- the
+    posterior is the oracle's either way; a later fit with clean rows goes back
+    to the categorical form, and an appended fit re-checks only its new rows"""
+    _require_gpu()
+    space = hpl_space()
+    e = engine(space, seed=4)
+    tr = ode.population_init(space, 300, seed=3)
+    X = features(space, tr).T
+    y = np.sum((X - 0.5) ** 2, axis=1)
+    cand = dev(ode.population_init(space, 2000, seed=2))
+    F = X.shape[1]
+
+    def check(Xf, ell):
+        g = ogp.GP(Xf, y[:Xf.shape[0]], lengthscale=ell, sigma_f2=1.0, sigma_n2=1e-6, jitter=1e-8)
+        mu, var = g.posterior(features(space, cand.cpu().numpy()).T)
+        m2, v2, _ = e.gp_score_values(cand, acq=e.acq("ei"))
+        np.testing.assert_allclose(m2.cpu().numpy(), mu, rtol=RTOL, atol=ATOL)
+        np.testing.assert_allclose(v2.cpu().numpy(), var, rtol=RTOL, atol=ATOL)
+
+    Xb = X.copy()
+    enum_col = next(p.feat_col for p in e.spec.params if p.kind == 5)
+    Xb[7, enum_col] = 0.5                       # not one-hot
+    e.gp_fit(Xb, y, lengthscale=1.0, sigma_f2=1.0, sigma_n2=1e-6, jitter=1e-8)
+    assert e.gp_kstar_mode() == "dense"
+    check(Xb, 1.0)
+    ell = np.ones(F)
+    ell[enum_col + 1] = 1.5                     # two lengthscales inside the categorical features
+    e.gp_fit(X, y, lengthscale=ell, sigma_f2=1.0, sigma_n2=1e-6, jitter=1e-8)
+    assert e.gp_kstar_mode() == "dense"
+    check(X, ell)
+    e.gp_fit(X[:200], y[:200], lengthscale=1.0, sigma_f2=1.0, sigma_n2=1e-6, jitter=1e-8)
+    assert e.gp_kstar_mode() == "categorical"
+    check(X[:200], 1.0)
+    e.gp_fit(X[:250], y[:250], lengthscale=1.0, sigma_f2=1.0, sigma_n2=1e-6, jitter=1e-8)   # appends
+    assert e.gp_last_fit_kind() == "append" and e.gp_kstar_mode() == "categorical"
+    check(X[:250], 1.0)
+    Xc = X.copy()
+    Xc[280, enum_col] = 0.0                     # an all-zero block in an appended row
+    e.gp_fit(Xc, y, lengthscale=1.0, sigma_f2=1.0, sigma_n2=1e-6, jitter=1e-8)
+    assert e.gp_kstar_mode() == "dense"
+    check(Xc, 1.0)
+    e.close()
+    old = os.environ.get("UT_CAT_KSTAR")
+    os.environ["UT_CAT_KSTAR"] = "0"
+    try:
+        e2 = engine(space, seed=4)
+        e2.gp_fit(X, y, lengthscale=1.0, sigma_f2=1.0, sigma_n2=1e-6, jitter=1e-8)
+        assert e2.gp_kstar_mode() == "dense"
+        e2.close()
+    finally:
+        if old is None:
+            os.environ.pop("UT_CAT_KSTAR", None)
+        else:
+            os.environ["UT_CAT_KSTAR"] = old

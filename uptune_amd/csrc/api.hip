@@ -35,8 +35,8 @@ hipError_t dmalloc(void** p, size_t bytes) {
   return e;
 }
 
-hipError_t dfree(void* p) {
-  if (!p) return hipSuccess;
+void dfree(void* p) {
+  if (!p) return;
   {
     std::lock_guard<std::mutex> g(g_mem_mu);
     auto it = g_mem_ptrs.find(p);
@@ -45,7 +45,7 @@ hipError_t dfree(void* p) {
       g_mem_ptrs.erase(it);
     }
   }
-  return hipFree(p);
+  (void)hipFree(p);
 }
 
 void mark(ut_ctx* c, const char* name) {
@@ -103,7 +103,7 @@ static void free_space(Space& s) {
   if (s.d_vtab) ut::dfree(s.d_vtab);
   for (void* q : {(void*)s.d_order_col, (void*)s.d_perm_params, (void*)s.d_perm_bytes, (void*)s.d_perm_off,
                   (void*)s.d_perm_offbase, (void*)s.d_perm_len, (void*)s.d_comp,
-                  (void*)s.d_col_param})
+                  (void*)s.d_col_param, (void*)s.d_cat_ccol, (void*)s.d_num_feat, (void*)s.d_feat_num})
     if (q) ut::dfree(q);
   s = Space();
 }
@@ -238,6 +238,7 @@ int ut_ctx_create(int device, uint64_t seed, ut_ctx** out) {
   if (const char* e = getenv("UT_HASH_AFTER_KSTAR")) c->hash_after_kstar = atoi(e);
   if (const char* e = getenv("UT_H3_SCHED")) c->h3_sched = atoi(e);
   if (const char* e = getenv("UT_VAR_SCHED")) c->var_sched = atoi(e);
+  if (const char* e = getenv("UT_CAT_KSTAR")) c->cat_enable = atoi(e) != 0;
   *out = c;
   return 0;
 }
@@ -265,6 +266,7 @@ int ut_ctx_destroy(ut_ctx* c) {
   fr(c->gp_Xs); fr(c->gp_xnorm); fr(c->gp_K); fr(c->gp_Linv); fr(c->gp_y); fr(c->gp_tmp);
   fr(c->gp_alpha); fr(c->gp_beta); fr(c->gp_inv_ell); fr(c->gp_stats); fr(c->gp_flag); fr(c->gp_Xs_f); fr(c->gp_T);
   fr(c->gp_LinvT); fr(c->gp_LinvT_f); fr(c->gp_ctr); fr(c->gp_XsT); fr(c->ucand.p);
+  fr(c->gp_XsT_num.p); fr(c->gp_xnorm_num.p); fr(c->gp_acat.p); fr(c->bcat.p); fr(c->pr_bcat.p);
   fr(c->kst.p); fr(c->mu_part.p); fr(c->var_part.p); fr(c->cnorm.p);
   fr(c->r_values.p); fr(c->r_feat.p); fr(c->r_mu.p); fr(c->r_var.p); fr(c->r_score.p); fr(c->r_digest.p);
   fr(c->r_dup.p); fr(c->tk_score[0].p); fr(c->tk_score[1].p); fr(c->tk_idx[0].p); fr(c->tk_idx[1].p);
@@ -461,6 +463,34 @@ int ut_space_define(ut_ctx* c, int32_t P, const ut_param_desc* params, int32_t p
       if (s.host_params[j].kind != UT_PERM) col_param[s.host_params[j].col] = j;
     UT_HIP(c, ut::dmalloc((void**)&s.d_col_param, sizeof(int32_t) * col_param.size()));
     UT_HIP(c, hipMemcpy(s.d_col_param, col_param.data(), sizeof(int32_t) * col_param.size(), hipMemcpyHostToDevice));
+  }
+  {  // categorical K*: ENUM / BOOL code columns, numeric features (gp_gemm.hip)
+    std::vector<int32_t> ccol(P, -1), feat_num(s.n_feat > 0 ? s.n_feat : 1, -1);
+    int32_t kc = 0;
+    for (int32_t p = 0; p < P; ++p) {
+      const DevParam& q = s.host_params[p];
+      if (q.kind == UT_ENUM || q.kind == UT_BOOL) {
+        ccol[p] = kc;
+        kc += q.kind == UT_ENUM ? (int32_t)q.n_opt : 2;
+        s.host_cat.push_back(p);
+      } else {
+        for (int32_t f = 0; f < q.n_feat; ++f) {
+          feat_num[q.feat_col + f] = (int32_t)s.host_num_feat.size();
+          s.host_num_feat.push_back(q.feat_col + f);
+        }
+      }
+    }
+    s.n_cat = (int32_t)s.host_cat.size();
+    s.n_num = (int32_t)s.host_num_feat.size();
+    s.cat_k = (kc + 127) / 128 * 128;
+    std::vector<int32_t> num_feat = s.host_num_feat;
+    if (num_feat.empty()) num_feat.push_back(0);
+    UT_HIP(c, ut::dmalloc((void**)&s.d_cat_ccol, sizeof(int32_t) * P));
+    UT_HIP(c, hipMemcpy(s.d_cat_ccol, ccol.data(), sizeof(int32_t) * P, hipMemcpyHostToDevice));
+    UT_HIP(c, ut::dmalloc((void**)&s.d_num_feat, sizeof(int32_t) * num_feat.size()));
+    UT_HIP(c, hipMemcpy(s.d_num_feat, num_feat.data(), sizeof(int32_t) * num_feat.size(), hipMemcpyHostToDevice));
+    UT_HIP(c, ut::dmalloc((void**)&s.d_feat_num, sizeof(int32_t) * feat_num.size()));
+    UT_HIP(c, hipMemcpy(s.d_feat_num, feat_num.data(), sizeof(int32_t) * feat_num.size(), hipMemcpyHostToDevice));
   }
   int rc = compile_hash_layout(c, names, primitive);
   if (rc) return rc;
@@ -767,6 +797,12 @@ int ut_gp_fit_status(ut_ctx* c, int32_t* ok) {
   return 0;
 }
 
+int ut_gp_kstar_mode(ut_ctx* c, int32_t* categorical) {
+  if (!c || !categorical) return UT_EINVAL;
+  *categorical = c->cat_on ? 1 : 0;
+  return 0;
+}
+
 int ut_gp_stats(ut_ctx* c, double* f_best, double* y_mean, double* y_std) {
   if (!c) return UT_EINVAL;
   UT_CHECK(c, c->gp_ready, UT_EINVAL, "gp_stats: no fitted GP");
@@ -868,7 +904,7 @@ static int score_round_de_impl(ut_ctx* c, const ut_de_params* de, const ut_acq* 
     // pruned: only candidates whose score bound reaches the threshold get the
     // full variance (the bound kernel joins the dup mask first)
     if ((rc = gp_topk_pruned_impl(c, c->r_feat.p, ld, m, acq, c->r_dup.p, cand_base, k, prune_rows, c->r_topk_idx.p,
-                                  c->r_topk_score.p, stats, c->ev_join)))
+                                  c->r_topk_score.p, stats, c->ev_join, true)))
       return rc;
   } else {
     // join before the finalize kernel, which masks duplicates

@@ -130,7 +130,7 @@ int launch_dedup(ut_ctx* c, const uint32_t* dig, int64_t m, uint8_t* dup) {
   if (c->batch_cap < cap) {
     if (c->batch_slots) {
       UT_HIP(c, ut::sync_all(c));
-      UT_HIP(c, ut::dfree(c->batch_slots));
+      ut::dfree(c->batch_slots);
     }
     UT_HIP(c, ut::dmalloc((void**)&c->batch_slots, cap * sizeof(int32_t)));
     c->batch_cap = cap;

@@ -50,6 +50,48 @@ __global__ void k_gp_prep_train(const double* __restrict__ X, int32_t n, int32_t
   xnorm[j] = s;
 }
 
+// categorical K* operands of the training rows (gp_gemm.hip "Categorical K*"):
+// XsT_num [dpad_num][npad] = the numeric features of Xs, transposed, and their
+// norms in feature order; one thread per row
+__global__ void k_gp_num_train(const double* __restrict__ Xs, int32_t npad, int32_t d,
+                               const int32_t* __restrict__ num_feat, int32_t n_num, int32_t dpad_num,
+                               double* __restrict__ XsT_num, double* __restrict__ xnorm_num) {
+  const int32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= npad) return;
+  double s = 0.0;
+  for (int32_t k = 0; k < dpad_num; ++k) {
+    const double v = k < n_num ? Xs[(int64_t)r * d + num_feat[k]] : 0.0;
+    XsT_num[(int64_t)k * npad + r] = v;
+    s += v * v;
+  }
+  xnorm_num[r] = s;
+}
+
+// the training rows' weighted one-hot codes [cat_k / 128][npad][128] (zeroed
+// before): ENUM option o -> 2 at code column ccol + o, BOOL b -> 1 at ccol + b;
+// X (unscaled features, rows < n) was checked one-hot on the host
+__global__ void k_gp_cat_train(const DevParam* __restrict__ params, int32_t P, const int32_t* __restrict__ cat_ccol,
+                               const double* __restrict__ X, int32_t n, int32_t d, int32_t npad,
+                               int8_t* __restrict__ acat) {
+  const int32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= n) return;
+  for (int32_t p = 0; p < P; ++p) {
+    const int32_t cc = cat_ccol[p];
+    if (cc < 0) continue;
+    const DevParam pr = params[p];
+    const double* x = X + (int64_t)r * d + pr.feat_col;
+    int32_t o = 0;
+    if (pr.kind == UT_BOOL) {
+      o = x[0] != 0.0 ? 1 : 0;
+    } else {
+      for (int32_t k = 0; k < (int32_t)pr.n_opt; ++k)
+        if (x[k] == 1.0) { o = k; break; }
+    }
+    const int32_t q = cc + o;
+    acat[((int64_t)(q >> 7) * npad + r) * 128 + (q & 127)] = (int8_t)(pr.kind == UT_BOOL ? 1 : 2);
+  }
+}
+
 // mean / std (ddof=0) / standardise / f_best = min(ys); one workgroup
 __global__ __launch_bounds__(256) void k_gp_ystats(const double* __restrict__ y, int32_t n, int32_t npad,
                                                    double* __restrict__ ys, double* __restrict__ stats) {
@@ -670,6 +712,29 @@ static int gp_alloc(ut_ctx* c, int32_t npad_need, int32_t d) {
   return 0;
 }
 
+// rows [r0, r1) of X [n][d] have exact one-hot ENUM blocks and 0 / 1 BOOL
+// features: the categorical K* reads the training rows as option codes
+static bool cat_rows_ok(const Space& s, const double* X, int32_t d, int32_t r0, int32_t r1) {
+  for (int32_t r = r0; r < r1; ++r) {
+    const double* row = X + (size_t)r * d;
+    for (int32_t p : s.host_cat) {
+      const DevParam& q = s.host_params[p];
+      const double* x = row + q.feat_col;
+      if (q.kind == UT_BOOL) {
+        if (!(x[0] == 0.0 || x[0] == 1.0)) return false;
+        continue;
+      }
+      int32_t ones = 0;
+      for (int32_t k = 0; k < (int32_t)q.n_opt; ++k) {
+        if (x[k] == 1.0) ++ones;
+        else if (x[k] != 0.0) return false;
+      }
+      if (ones != 1) return false;
+    }
+  }
+  return true;
+}
+
 // Enqueue a fit on the fit stream, ordered after everything already enqueued
 // on the caller's stream (earlier rounds read the GP state being replaced).
 // Scoring waits on ev_fit; failure (not positive definite) is reported by
@@ -726,6 +791,32 @@ int gp_fit_enqueue(ut_ctx* c, const double* X, const double* y, int32_t n, int32
   std::memcpy(hX + (size_t)xr0 * d, X + (size_t)xr0 * d, sizeof(double) * (size_t)(n - xr0) * d);
   std::memcpy(hy, y, sizeof(double) * n);
   for (int32_t k = 0; k < d; ++k) hinv[k] = 1.0 / h->lengthscale_host[k];
+  // categorical K*: every ENUM / BOOL feature under one lengthscale and every
+  // training row one-hot there (an append checks only its new rows)
+  const Space& sp = c->space;
+  bool cat = c->cat_enable && c->has_space && sp.n_cat > 0 && d == sp.n_feat;
+  double cinv = 0.0;
+  if (cat) {
+    cinv = hinv[sp.host_params[sp.host_cat[0]].feat_col];
+    for (int32_t p : sp.host_cat) {
+      const DevParam& q = sp.host_params[p];
+      for (int32_t f = 0; f < q.n_feat && cat; ++f) cat = std::memcmp(&hinv[q.feat_col + f], &cinv, sizeof(double)) == 0;
+      if (!cat) break;
+    }
+  }
+  if (cat) {
+    const bool prefix_ok = app && c->cat_x_ok;
+    cat = cat_rows_ok(sp, X, d, prefix_ok ? n0 : 0, n);
+  }
+  c->cat_x_ok = cat;
+  c->cat_on = cat;
+  if (cat) {
+    int32_t pw = 0;
+    for (int32_t p : sp.host_cat) pw += sp.host_params[p].kind == UT_BOOL ? 1 : 2;
+    const double base = cinv * cinv;
+    c->cat_c1 = 0.5 * base;
+    c->cat_c0 = -0.5 * base * (double)pw;
+  }
   UT_HIP(c, hipEventRecord(c->ev_prefit, c->stream));
   UT_HIP(c, hipStreamWaitEvent(c->fit_stream, c->ev_prefit, 0));
   StreamScope on_fit(c, c->fit_stream);
@@ -743,6 +834,18 @@ int gp_fit_enqueue(ut_ctx* c, const double* X, const double* y, int32_t n, int32
   // the candidate side of K* needs only the scaled inputs: fp64 scoring starts
   // its K* here while the factorisation below is still running
   if ((rc = launch_xs_t(c, c->gp_Xs, npad, d, kstar_dpad(d), c->gp_XsT))) return rc;
+  if (c->cat_on) {
+    const int32_t dpn = cat_dpad(c);
+    if ((rc = ensure(c, c->gp_XsT_num, (size_t)(dpn > 0 ? dpn : 1) * npad))) return rc;
+    if ((rc = ensure(c, c->gp_xnorm_num, (size_t)npad))) return rc;
+    if ((rc = ensure(c, c->gp_acat, (size_t)sp.cat_k * npad))) return rc;
+    hipLaunchKernelGGL(k_gp_num_train, dim3(grid1(npad, 256)), dim3(256), 0, c->stream, c->gp_Xs, npad, d,
+                       sp.d_num_feat, sp.n_num, dpn, c->gp_XsT_num.p, c->gp_xnorm_num.p);
+    UT_HIP(c, hipMemsetAsync(c->gp_acat.p, 0, (size_t)sp.cat_k * npad, c->stream));
+    hipLaunchKernelGGL(k_gp_cat_train, dim3(grid1(n, 256)), dim3(256), 0, c->stream, sp.d_params, sp.P, sp.d_cat_ccol,
+                       dX, n, d, npad, c->gp_acat.p);
+    UT_LAUNCH_CHECK(c);
+  }
   UT_HIP(c, hipEventRecord(c->ev_fit_x, c->stream));
   const double diag = h->sigma_n2 + h->jitter;
   if (app) {
@@ -855,12 +958,31 @@ int gp_encode_scaled(ut_ctx* c, const double* values, int64_t ld, int64_t m) {
   if (m <= 0) return 0;
   // 1/ell comes with the fit's scaled training inputs
   if (c->fit_pending) UT_HIP(c, hipStreamWaitEvent(c->stream, c->ev_fit_x, 0));
-  const int32_t dpad = kstar_dpad(c->gp_d);
   const int64_t ldk = ((m + VAR_BN - 1) / VAR_BN) * VAR_BN;   // as gp_score_impl
   int rc;
   if ((rc = ensure(c, c->cnorm, (size_t)ldk))) return rc;
+  if (c->cat_on) {   // numeric U', norms and the one-hot codes (categorical K*)
+    const int32_t dpn = cat_dpad(c);
+    if ((rc = ensure(c, c->ucand, (size_t)(dpn > 0 ? dpn : 1) * ldk))) return rc;
+    if ((rc = ensure(c, c->bcat, (size_t)c->space.cat_k * ldk))) return rc;
+    c->ucand_cat = true;
+    return launch_encode_scaled_cat(c, values, ld, m, c->ucand.p, dpn, ldk, c->cnorm.p, c->bcat.p);
+  }
+  const int32_t dpad = kstar_dpad(c->gp_d);
   if ((rc = ensure(c, c->ucand, (size_t)dpad * ldk))) return rc;
+  c->ucand_cat = false;
   return launch_encode_scaled(c, values, ld, m, c->ucand.p, dpad, ldk, c->cnorm.p);
+}
+
+// the categorical operands of the current fit for launch_gemm_kstar
+static KstarCat kstar_cat(ut_ctx* c, const int8_t* bcat) {
+  KstarCat k;
+  k.acat = c->gp_acat.p;
+  k.bcat = bcat;
+  k.nkc = c->space.cat_k / 128;
+  k.c0 = c->cat_c0;
+  k.c1 = c->cat_c1;
+  return k;
 }
 
 int gp_score_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, const ut_acq* acq, const uint8_t* dup,
@@ -879,7 +1001,11 @@ int gp_score_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, const ut
   if (c->fit_pending) UT_HIP(c, hipStreamWaitEvent(c->stream, fp32 ? c->ev_fit : c->ev_fit_x, 0));
   const int32_t n = c->gp_n, d = c->gp_d;
   const int32_t npad = ((n + NPAD - 1) / NPAD) * NPAD;
-  const int32_t dpad = kstar_dpad(d);
+  // the categorical K* when the candidates came through ut's encoder
+  // (gp_encode_scaled in categorical mode); a caller's feature matrix takes the
+  // dense contraction over every feature
+  const bool cat = !feat && c->cat_on && c->ucand_cat;
+  const int32_t dpad = cat ? cat_dpad(c) : kstar_dpad(d);
   // K* rows padded to whole variance column tiles: the variance kernel reads
   // full 256-candidate strips (the K* kernel writes zeros past m)
   const int64_t ldk = ((m + VAR_BN - 1) / VAR_BN) * VAR_BN;
@@ -889,13 +1015,15 @@ int gp_score_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, const ut
   if ((rc = ensure(c, c->mu_part, (size_t)RT * ldk))) return rc;
   if ((rc = ensure(c, c->var_part, (size_t)RT * ldk))) return rc;
   if ((rc = ensure(c, c->cnorm, (size_t)ldk))) return rc;
-  if ((rc = ensure(c, c->ucand, (size_t)dpad * ldk))) return rc;
+  if ((rc = ensure(c, c->ucand, (size_t)(dpad > 0 ? dpad : 1) * ldk))) return rc;
   if (feat) {
     if ((rc = launch_prep_cand(c, feat, ld, m, d, dpad, c->ucand.p, ldk, c->cnorm.p))) return rc;
+    c->ucand_cat = false;
     mark(c, "cnorm");
   }
-  if ((rc = launch_gemm_kstar(c, prec, c->gp_XsT, npad, c->ucand.p, dpad, m, c->kst.p, ldk,
-                              fp32 ? c->mu_part.p : nullptr)))
+  if ((rc = launch_gemm_kstar(c, prec, cat ? c->gp_XsT_num.p : c->gp_XsT, npad, c->ucand.p, dpad, m, c->kst.p, ldk,
+                              fp32 ? c->mu_part.p : nullptr, -1, nullptr, nullptr,
+                              cat ? kstar_cat(c, c->bcat.p) : KstarCat(), cat ? c->gp_xnorm_num.p : nullptr)))
     return rc;
   mark(c, "kstar");
   if (mid && (rc = mid())) return rc;
@@ -1003,6 +1131,23 @@ __global__ __launch_bounds__(256) void k_sumsq_final(const double* __restrict__ 
   if (threadIdx.x == 0) *out = (red[0] + red[1]) + (red[2] + red[3]);
 }
 
+// the categorical K* codes of gathered candidates: 16-byte pieces of their
+// 128-byte rows, code block blockIdx.y (zeros past n and for empty slots)
+__global__ void k_gather_code_rows(const int8_t* __restrict__ bcat, int64_t ldk, const int64_t* __restrict__ idx,
+                                   int64_t base, int64_t n, int64_t ldo, int8_t* __restrict__ out) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t kb = blockIdx.y;
+  const int64_t j = e >> 3;
+  const int piece = (int)(e & 7);
+  if (j >= ldo) return;
+  uint4 v = make_uint4(0u, 0u, 0u, 0u);
+  if (j < n) {
+    const int64_t q = idx[j];
+    if (q >= 0) v = reinterpret_cast<const uint4*>(bcat + (kb * ldk + (q - base)) * 128)[piece];
+  }
+  reinterpret_cast<uint4*>(out + (kb * ldo + j) * 128)[piece] = v;
+}
+
 __global__ void k_gather_cols(const double* __restrict__ kst, int64_t ldk, const int64_t* __restrict__ idx,
                                   int64_t base, int64_t n, int64_t ldo, double* __restrict__ out) {
   const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1075,7 +1220,7 @@ __global__ void k_fill(double* __restrict__ p, int64_t n, double v) {
 
 int gp_topk_pruned_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, const ut_acq* acq, const uint8_t* dup,
                         int64_t cand_base, int32_t k, int32_t bound_rows, int64_t* out_idx, double* out_score,
-                        ut_prune_stats* stats, hipEvent_t dup_ready) {
+                        ut_prune_stats* stats, hipEvent_t dup_ready, bool feat_ours) {
   UT_CHECK(c, c->gp_ready, UT_EINVAL, "gp_topk_pruned: call ut_gp_fit first");
   UT_CHECK(c, c->gp_fit_prec == 64, UT_EINVAL, "gp_topk_pruned: needs an fp64 fit (ut_gp_set_precision 64)");
   UT_CHECK(c, acq->kind == UT_ACQ_EI || (acq->kind == UT_ACQ_UCB && acq->kappa >= 0.0), UT_EINVAL,
@@ -1084,7 +1229,8 @@ int gp_topk_pruned_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, co
   if (c->fit_pending) UT_HIP(c, hipStreamWaitEvent(c->stream, c->ev_fit, 0));   // K* takes mu = k* . alpha
   const int32_t n = c->gp_n, d = c->gp_d;
   const int32_t npad = ((n + NPAD - 1) / NPAD) * NPAD;
-  const int32_t dpad = kstar_dpad(d);
+  const bool cat = feat_ours && c->cat_on;   // the categorical K* (features from ut's encoder)
+  const int32_t dpad = cat ? cat_dpad(c) : kstar_dpad(d);
   const int32_t RT = npad / NPAD;
   int32_t R = (bound_rows + NPAD - 1) / NPAD;
   R = R < 1 ? 1 : (R > RT ? RT : R);
@@ -1095,7 +1241,8 @@ int gp_topk_pruned_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, co
   if ((rc = ensure(c, c->var_part, (size_t)RT * ldk))) return rc;
   if ((rc = ensure(c, c->pr_mpart, (size_t)RT * ldk))) return rc;
   if ((rc = ensure(c, c->cnorm, (size_t)ldk))) return rc;
-  if ((rc = ensure(c, c->ucand, (size_t)dpad * ldk))) return rc;
+  if ((rc = ensure(c, c->ucand, (size_t)(dpad > 0 ? dpad : 1) * ldk))) return rc;
+  if (cat && (rc = ensure(c, c->bcat, (size_t)c->space.cat_k * ldk))) return rc;
   if ((rc = ensure(c, c->pr_mu, (size_t)ldk))) return rc;
   if ((rc = ensure(c, c->pr_ub, (size_t)ldk))) return rc;
   if ((rc = ensure(c, c->pr_score, (size_t)ldk + 2048))) return rc;   // + the threshold set's two [1024] arrays
@@ -1106,13 +1253,20 @@ int gp_topk_pruned_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, co
   if ((rc = ensure(c, c->pr_exact, (size_t)ldk))) return rc;
   const double* LinvT = c->gp_LinvT;
   // 1. K* with the mean in its epilogue, 2. the first R row tiles of L^-1 K*^T
-  if ((rc = launch_prep_cand(c, feat, ld, m, d, dpad, c->ucand.p, ldk, c->cnorm.p))) return rc;
+  if (cat) {
+    if ((rc = launch_prep_cand_cat(c, feat, ld, m, c->ucand.p, dpad, ldk, c->cnorm.p, c->bcat.p))) return rc;
+  } else if ((rc = launch_prep_cand(c, feat, ld, m, d, dpad, c->ucand.p, ldk, c->cnorm.p))) {
+    return rc;
+  }
+  c->ucand_cat = cat;
+  const double* XsT = cat ? c->gp_XsT_num.p : c->gp_XsT;
+  const double* xn = cat ? c->gp_xnorm_num.p : nullptr;
   // K* stores only the bound rows; the mean sums every row.  The few
   // candidates that need every row (threshold set, survivors) get their K*
   // columns recomputed from their features (recompute_cols below): cheaper than
   // writing and re-reading the whole n x m matrix
-  if ((rc = launch_gemm_kstar(c, 64, c->gp_XsT, npad, c->ucand.p, dpad, m, c->kst.p, ldk, c->mu_part.p, R * NPAD,
-                              nullptr, c->pr_k2.p)))
+  if ((rc = launch_gemm_kstar(c, 64, XsT, npad, c->ucand.p, dpad, m, c->kst.p, ldk, c->mu_part.p, R * NPAD,
+                              nullptr, c->pr_k2.p, cat ? kstar_cat(c, c->bcat.p) : KstarCat(), xn)))
     return rc;
   // |L^-1|_F^2 for the variance tail bound, once per fit
   if (!c->pr_f2_valid) {
@@ -1144,15 +1298,21 @@ int gp_topk_pruned_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, co
     int r2;
     if ((r2 = ensure(c, c->pr_kst, (size_t)npad * ldc))) return r2;
     if ((r2 = ensure(c, c->pr_vpart, (size_t)RT * ldc))) return r2;
-    if ((r2 = ensure(c, c->pr_ucand, (size_t)dpad * ldc))) return r2;
+    if ((r2 = ensure(c, c->pr_ucand, (size_t)(dpad > 0 ? dpad : 1) * ldc))) return r2;
     if ((r2 = ensure(c, c->pr_cnorm, (size_t)ldc))) return r2;
-    hipLaunchKernelGGL(k_gather_cols, dim3(grid1(ldc, 256), (unsigned)dpad), dim3(256), 0, c->stream, c->ucand.p, ldk,
-                       idx, base, nc, ldc, c->pr_ucand.p);
+    if (dpad > 0)
+      hipLaunchKernelGGL(k_gather_cols, dim3(grid1(ldc, 256), (unsigned)dpad), dim3(256), 0, c->stream, c->ucand.p,
+                         ldk, idx, base, nc, ldc, c->pr_ucand.p);
     hipLaunchKernelGGL(k_gather_cols, dim3(grid1(ldc, 256), 1u), dim3(256), 0, c->stream, c->cnorm.p, ldk, idx, base,
                        nc, ldc, c->pr_cnorm.p);
+    if (cat) {   // the gathered candidates' 128-byte code rows, per code block
+      if ((r2 = ensure(c, c->pr_bcat, (size_t)c->space.cat_k * ldc))) return r2;
+      hipLaunchKernelGGL(k_gather_code_rows, dim3(grid1(ldc * 8, 256), (unsigned)(c->space.cat_k / 128)), dim3(256), 0,
+                         c->stream, c->bcat.p, ldk, idx, base, nc, ldc, c->pr_bcat.p);
+    }
     UT_LAUNCH_CHECK(c);
-    return launch_gemm_kstar(c, 64, c->gp_XsT, npad, c->pr_ucand.p, dpad, nc, c->pr_kst.p, ldc, nullptr, -1,
-                             c->pr_cnorm.p);
+    return launch_gemm_kstar(c, 64, XsT, npad, c->pr_ucand.p, dpad, nc, c->pr_kst.p, ldc, nullptr, -1,
+                             c->pr_cnorm.p, nullptr, cat ? kstar_cat(c, c->pr_bcat.p) : KstarCat(), xn);
   };
   const int64_t ldt = ((int64_t)kp + VAR_BN - 1) / VAR_BN * VAR_BN;
   if ((rc = recompute_cols(tset, cand_base, kp, ldt))) return rc;
@@ -1182,7 +1342,9 @@ int gp_topk_pruned_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, co
   const bool dense = ns * 2 > m;
   if (dense) {
     // most candidates survive: the whole K* (this time every row) and the dense variance
-    if ((rc = launch_gemm_kstar(c, 64, c->gp_XsT, npad, c->ucand.p, dpad, m, c->kst.p, ldk, c->mu_part.p))) return rc;
+    if ((rc = launch_gemm_kstar(c, 64, XsT, npad, c->ucand.p, dpad, m, c->kst.p, ldk, c->mu_part.p, -1, nullptr,
+                                nullptr, cat ? kstar_cat(c, c->bcat.p) : KstarCat(), xn)))
+      return rc;
     if ((rc = launch_gemm_var(c, 64, LinvT, npad, c->kst.p, ldk, npad, m, c->var_part.p, c->gp_beta,
                               c->pr_mpart.p)))
       return rc;

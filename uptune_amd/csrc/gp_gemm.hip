@@ -96,10 +96,49 @@ __device__ __forceinline__ void kstar_issue(const double* __restrict__ AT, int64
 }
 
 typedef double kd4 __attribute__((ext_vector_type(4)));
+typedef int32_t ki4 __attribute__((ext_vector_type(4)));
+
+// Categorical K* (CAT): ENUM and BOOL params are one-hot blocks of the GP
+// features (SURVEY.md §8 GP spec: Enum one-hot, Bool {0, 1}), and with one
+// lengthscale ell over those blocks a block contributes to |x - u|^2 exactly
+//   2 / ell^2 (ENUM) or 1 / ell^2 (BOOL)  when the two configurations' options
+//   differ, and 0 when they match.
+// So -|x - u|^2 / 2 over the categorical features is c0 + c1 * M with
+//   M = sum_j w_j [opt_x(j) == opt_u(j)],  w_j = 2 (ENUM), 1 (BOOL),
+//   c1 = 1 / (2 ell^2),  c0 = -c1 * sum_j w_j,
+// and M is the integer dot product of the training rows' weighted one-hot
+// codes with the candidates' 0/1 codes (ENUM: n_opt columns, BOOL: 2).  That
+// product runs on v_mfma_i32_16x16x64_i8 (exact int32, 4x the fp64 MFMA's
+// rate per instruction at 16x the K), ahead of the fp64 contraction over the
+// remaining ("numeric") features, and c0 + c1 M starts the fp64 accumulator.
+// At C3 (HPL-64: 79 of 119 features one-hot / 0-1) the fp64 contraction's K
+// drops 120 -> 40, at C4 (gcc: 552 of 707) 708 -> 156.
+//   int8 stage: 128 code columns x 128 rows (A) / candidates (B) = 16 KiB per
+//   operand, the fp64 stage's footprint; global layout [k / 128][row][128 B],
+//   LDS row r's 16-B chunk c at position c ^ (r & 7) (swizzled through the
+//   glds source address: the fragment reads are at most 2-way conflicted).
+//   The i8 MFMA's C/D rows are 4 (l >> 4) + q where the fp64 MFMA's are
+//   (l >> 4) + 4 q, so the A fragment of MFMA row rho loads tile row
+//   sigma(rho) = (rho >> 2) + 4 (rho & 3): iacc[i][jj][q] then sits where
+//   acc[i][jj][q] does (scripts/exp/i8_mfma_probe.hip checks both maps).
+__device__ __forceinline__ void kcat_issue(const int8_t* __restrict__ Ab, const int8_t* __restrict__ Bb,
+                                           double* st, int w, int lane) {
+  uint8_t* sb = reinterpret_cast<uint8_t*>(st);
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int q = 4 * w + u;                      // rows 8q .. 8q + 7 of the tile (1 KiB)
+    const int r = 8 * q + (lane >> 3);
+    const int cch = (lane & 7) ^ (r & 7);         // the global chunk that lands at position lane & 7
+    __builtin_amdgcn_global_load_lds(Ab + r * 128 + cch * 16, (__attribute__((address_space(3))) void*)(sb + q * 1024),
+                                     16, 0, 0);
+    __builtin_amdgcn_global_load_lds(Bb + r * 128 + cch * 16,
+                                     (__attribute__((address_space(3))) void*)(sb + K_SA * 8 + q * 1024), 16, 0, 0);
+  }
+}
 
 // MU: also the column partial of the mean, sum_r alpha_r k*_r (fp32 scoring;
 // fp64 takes the mean from the variance epilogue instead)
-template <typename TS, bool MU>
+template <typename TS, bool MU, bool CAT>
 __global__ __launch_bounds__(K_NT, 2) void k_gp_kstar(const double* __restrict__ AT, int64_t lda,
                                                       const double* __restrict__ B, int64_t ldb, int32_t dpad,
                                                       int32_t RT, int32_t CT, const double* __restrict__ xnorm,
@@ -107,7 +146,9 @@ __global__ __launch_bounds__(K_NT, 2) void k_gp_kstar(const double* __restrict__
                                                       const double* __restrict__ alpha, double sf2, int32_t n,
                                                       int64_t m, int32_t* __restrict__ ticket, TS* __restrict__ kst,
                                                       int64_t ldk, double* __restrict__ part, double kscale,
-                                                      int64_t lo_off, int32_t store_rt, double* __restrict__ part2) {
+                                                      int64_t lo_off, int32_t store_rt, double* __restrict__ part2,
+                                                      const int8_t* __restrict__ acat, const int8_t* __restrict__ bcat,
+                                                      int32_t nkc, double cat_c0, double cat_c1) {
   // part2 (MU, fp64/fp32 only; pruned scoring): the column partial sum_r k*_r^2
   // as well, for the tail bound of the variance (gp.hip k_prune_bound)
   // TS = _Float16 (h3): k* * kscale split into fp16 hi + lo, stored candidate-major
@@ -144,6 +185,11 @@ __global__ __launch_bounds__(K_NT, 2) void k_gp_kstar(const double* __restrict__
   // dpad % 4 == 0: whole 16-k stages, then one stage of k_rem k4 steps
   const int32_t nk_full = dpad / K_BK, k_rem = (dpad % K_BK) / 4;
   const int32_t nk = nk_full + (k_rem ? 1 : 0);
+  const int32_t ncs = CAT ? nkc : 0;          // int8 stages first, then the fp64 ones
+  const int32_t ntot = ncs + nk;
+  const int npad_a = RT * K_BM;
+  // the i8 MFMA's row rho of A is tile row sigma(rho) (see above)
+  const int sig = ((lane & 15) >> 2) + 4 * (lane & 3);
   typedef kd4 d4;
 
   for (;;) {
@@ -156,26 +202,75 @@ __global__ __launch_bounds__(K_NT, 2) void k_gp_kstar(const double* __restrict__
     const int64_t col0 = (int64_t)ct * K_BN;
     const int32_t row0 = rt * K_BM;
 
-    d4 acc[4][4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int jj = 0; jj < 4; ++jj) acc[i][jj] = (d4){0.0, 0.0, 0.0, 0.0};
-
-    kstar_issue(AT, lda, B, ldb, row0, col0, 0, lds, w, lane, dpad);
+    auto issue_stage = [&](int32_t s2, double* st) {
+      if (CAT && s2 < ncs)
+        kcat_issue(acat + ((int64_t)s2 * npad_a + row0) * 128, bcat + ((int64_t)s2 * ldb + col0) * 128, st, w, lane);
+      else
+        kstar_issue(AT, lda, B, ldb, row0, col0, (s2 - ncs) * K_BK, st, w, lane, dpad);
+    };
+    if (ntot > 0) issue_stage(0, lds);
     {  // one 1-KiB glds per operand (rows < npad, columns < ldk are in range)
       const double* src = w == 0 ? xnorm + row0 : (w == 1 ? alpha + row0 : cnorm + col0);
       if (w < 3 && (MU || w != 1))
         __builtin_amdgcn_global_load_lds(src + lane * 2, (__attribute__((address_space(3))) void*)(rowop + w * K_BM),
                                          16, 0, 0);
     }
-    for (int32_t kt = 0; kt < nk; ++kt) {
+    d4 acc[4][4];
+    if constexpr (CAT) {
+      // the int8 stages: M into int32 accumulators (dead once acc is started)
+      ki4 iacc[4][4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) iacc[i][jj] = (ki4){0, 0, 0, 0};
+      for (int32_t s2 = 0; s2 < ncs; ++s2) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();  // stage s2 landed everywhere; stage s2-1 fully read
+        asm volatile("" ::: "memory");
+        if (s2 + 1 < ntot) issue_stage(s2 + 1, lds + ((s2 + 1) & 1) * K_STAGE);
+        const int8_t* as8 = reinterpret_cast<const int8_t*>(lds + (s2 & 1) * K_STAGE);
+        const int8_t* bs8 = as8 + K_SA * 8;
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+          const int c16 = (lane >> 4) + 4 * kk;
+          ki4 af[4], bf[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int row = wm * 64 + i * 16 + sig;
+            af[i] = *reinterpret_cast<const ki4*>(as8 + row * 128 + ((c16 ^ (row & 7)) << 4));
+          }
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj) {
+            const int col = wn * 64 + jj * 16 + (lane & 15);
+            bf[jj] = *reinterpret_cast<const ki4*>(bs8 + col * 128 + ((c16 ^ (col & 7)) << 4));
+          }
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj)
+              iacc[i][jj] = __builtin_amdgcn_mfma_i32_16x16x64_i8(af[i], bf[jj], iacc[i][jj], 0, 0, 0);
+        }
+      }
+      // c0 + c1 M starts the fp64 accumulators
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[i][jj][r] = __builtin_fma((double)iacc[i][jj][r], cat_c1, cat_c0);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) acc[i][jj] = (d4){0.0, 0.0, 0.0, 0.0};
+    }
+    for (int32_t s2 = ncs; s2 < ntot; ++s2) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();  // stage kt landed everywhere; stage kt-1 fully read
+      __builtin_amdgcn_s_barrier();  // stage s2 landed everywhere; stage s2-1 fully read
       asm volatile("" ::: "memory");
-      if (kt + 1 < nk)
-        kstar_issue(AT, lda, B, ldb, row0, col0, (kt + 1) * K_BK, lds + ((kt + 1) & 1) * K_STAGE, w, lane, dpad);
-      const double* as = lds + (kt & 1) * K_STAGE;
+      if (s2 + 1 < ntot) issue_stage(s2 + 1, lds + ((s2 + 1) & 1) * K_STAGE);
+      const double* as = lds + (s2 & 1) * K_STAGE;
+      const int32_t kt = s2 - ncs;
       const double* bs = as + K_SA;
       // the last stage of a dpad that is not a multiple of 16 has k_rem k4 steps
       const int nks = kt < nk_full ? K_BK / 4 : k_rem;
@@ -195,6 +290,7 @@ __global__ __launch_bounds__(K_NT, 2) void k_gp_kstar(const double* __restrict__
             acc[i][jj] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[i], bf[jj], acc[i][jj], 0, 0, 0);
       }
     }
+    if (ntot == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the epilogue operands
 
     __syncthreads();  // ring free: reuse as the column reduction buffer (and the h3 image)
     double* red = lds + RED_OFF;  // [2][128]
@@ -290,9 +386,11 @@ int h3_kstar_exp(double sf2) { return H3_KSCALE_EXP - ilogb(sf2); }  // sf2 * 2^
 
 int launch_gemm_kstar(ut_ctx* c, int prec, const double* XsT, int32_t npad, const double* ucand, int32_t dpad,
                       int64_t m, void* kst, int64_t ldk, double* part, int32_t store_rows, const double* cn,
-                      double* part2) {
-  UT_CHECK(c, npad % K_BM == 0 && dpad % 4 == 0 && dpad >= 4 && ldk % K_BN == 0 && ldk >= m, UT_EINVAL,
+                      double* part2, const KstarCat& cat, const double* xn) {
+  const bool has_cat = cat.nkc > 0;
+  UT_CHECK(c, npad % K_BM == 0 && dpad % 4 == 0 && (dpad >= 4 || has_cat) && ldk % K_BN == 0 && ldk >= m, UT_EINVAL,
            "gemm_kstar: bad padding");
+  UT_CHECK(c, !has_cat || (cat.acat && cat.bcat), UT_EINVAL, "gemm_kstar: categorical operands missing");
   UT_CHECK(c, prec == 64 || prec == 32 || prec == 16, UT_EINVAL, "gemm_kstar: bad precision");
   UT_CHECK(c, part != nullptr || prec == 64, UT_EINVAL,
            "gemm_kstar: fp32 / h3 mode takes the mean partial here");
@@ -312,23 +410,28 @@ int launch_gemm_kstar(ut_ctx* c, int prec, const double* XsT, int32_t npad, cons
   int32_t nb = 2 * (c->n_cu / 8 - spare) * 8;
   if (items < nb) nb = (int32_t)(((items + 7) / 8) * 8);
   UT_HIP(c, hipMemsetAsync(c->gp_ctr + 8, 0, sizeof(int32_t) * 8, c->stream));
+  const double* xnorm = xn ? xn : c->gp_xnorm;
+  const double* cnorm = cn ? cn : c->cnorm.p;
+#define UT_KSTAR_LAUNCH(TS, MU, CAT, KST, PART, KSCALE, LOOFF, SRT, PART2)                                         \
+  hipLaunchKernelGGL((k_gp_kstar<TS, MU, CAT>), dim3(nb), dim3(K_NT), 0, c->stream, XsT, (int64_t)npad, ucand, ldk, \
+                     dpad, RT, CT, xnorm, cnorm, c->gp_alpha, c->gp_sf2, c->gp_n, m, c->gp_ctr + 8, KST, ldk, PART, \
+                     KSCALE, LOOFF, SRT, PART2, cat.acat, cat.bcat, cat.nkc, cat.c0, cat.c1)
+#define UT_KSTAR_BOTH(TS, MU, ...)                   \
+  do {                                               \
+    if (has_cat) UT_KSTAR_LAUNCH(TS, MU, true, __VA_ARGS__); \
+    else UT_KSTAR_LAUNCH(TS, MU, false, __VA_ARGS__);        \
+  } while (0)
   if (prec == 16)
-    hipLaunchKernelGGL((k_gp_kstar<_Float16, true>), dim3(nb), dim3(K_NT), 0, c->stream, XsT, (int64_t)npad, ucand, ldk,
-                       dpad, RT, CT, c->gp_xnorm, cn ? cn : c->cnorm.p, c->gp_alpha, c->gp_sf2, c->gp_n, m, c->gp_ctr + 8,
-                       (_Float16*)kst, ldk, part, ldexp(1.0, h3_kstar_exp(c->gp_sf2)), ldk * (int64_t)npad, RT,
-                       nullptr);
+    UT_KSTAR_BOTH(_Float16, true, (_Float16*)kst, part, ldexp(1.0, h3_kstar_exp(c->gp_sf2)), ldk * (int64_t)npad, RT,
+                  nullptr);
   else if (prec == 32)
-    hipLaunchKernelGGL((k_gp_kstar<float, true>), dim3(nb), dim3(K_NT), 0, c->stream, XsT, (int64_t)npad, ucand, ldk, dpad,
-                       RT, CT, c->gp_xnorm, cn ? cn : c->cnorm.p, c->gp_alpha, c->gp_sf2, c->gp_n, m, c->gp_ctr + 8,
-                       (float*)kst, ldk, part, 1.0, (int64_t)0, RT, nullptr);
+    UT_KSTAR_BOTH(float, true, (float*)kst, part, 1.0, (int64_t)0, RT, nullptr);
   else if (part)   // fp64 with the mean k* . alpha in the epilogue (pruned scoring: needs the whole fit)
-    hipLaunchKernelGGL((k_gp_kstar<double, true>), dim3(nb), dim3(K_NT), 0, c->stream, XsT, (int64_t)npad, ucand, ldk, dpad,
-                       RT, CT, c->gp_xnorm, cn ? cn : c->cnorm.p, c->gp_alpha, c->gp_sf2, c->gp_n, m, c->gp_ctr + 8,
-                       (double*)kst, ldk, part, 1.0, (int64_t)0, store_rt, part2);
+    UT_KSTAR_BOTH(double, true, (double*)kst, part, 1.0, (int64_t)0, store_rt, part2);
   else
-    hipLaunchKernelGGL((k_gp_kstar<double, false>), dim3(nb), dim3(K_NT), 0, c->stream, XsT, (int64_t)npad, ucand, ldk, dpad,
-                       RT, CT, c->gp_xnorm, cn ? cn : c->cnorm.p, c->gp_alpha, c->gp_sf2, c->gp_n, m, c->gp_ctr + 8,
-                       (double*)kst, ldk, part, 1.0, (int64_t)0, store_rt, nullptr);
+    UT_KSTAR_BOTH(double, false, (double*)kst, part, 1.0, (int64_t)0, store_rt, nullptr);
+#undef UT_KSTAR_BOTH
+#undef UT_KSTAR_LAUNCH
   UT_LAUNCH_CHECK(c);
   return 0;
 }
@@ -352,6 +455,59 @@ int launch_prep_cand(ut_ctx* c, const double* feat, int64_t ld, int64_t m, int32
                      int64_t ldu, double* cn) {
   hipLaunchKernelGGL(k_gp_prep_cand, dim3(grid1(ldu, 256)), dim3(256), 0, c->stream, feat, ld, m, d, dpad,
                      c->gp_inv_ell, u, ldu, cn);
+  UT_LAUNCH_CHECK(c);
+  return 0;
+}
+
+// k_gp_prep_cand for the categorical K*, from a feature matrix made by ut's own
+// encoder (ENUM blocks one-hot, BOOL 0 / 1): numeric U' and norms as
+// k_encode_scaled_cat writes them, codes from the blocks (the first 1.0 of an
+// ENUM block; no 1.0: no code, as for an out-of-range value)
+__global__ void k_gp_prep_cand_cat(const DevParam* __restrict__ params, int32_t P, const double* __restrict__ feat,
+                                   int64_t ld, int64_t m, const int32_t* __restrict__ num_feat, int32_t n_num,
+                                   int32_t dpad, const double* __restrict__ inv_ell,
+                                   const int32_t* __restrict__ cat_ccol, int32_t cat_k, double* __restrict__ u,
+                                   int64_t ldu, double* __restrict__ cn, int8_t* __restrict__ bcat) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= ldu) return;
+  const uint4 z = make_uint4(0u, 0u, 0u, 0u);
+  for (int32_t kb = 0; kb < cat_k / 128; ++kb) {
+    uint4* row = reinterpret_cast<uint4*>(bcat + ((int64_t)kb * ldu + i) * 128);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) row[q] = z;
+  }
+  double s = 0.0;
+  for (int32_t k = 0; k < dpad; ++k) {
+    const int32_t f = k < n_num ? num_feat[k] : 0;
+    const double v = (k < n_num && i < m) ? feat[(int64_t)f * ld + i] * inv_ell[f] : 0.0;
+    u[(int64_t)k * ldu + i] = v;
+    s += v * v;
+  }
+  cn[i] = s;
+  if (i >= m) return;
+  for (int32_t p = 0; p < P; ++p) {
+    const int32_t cc = cat_ccol[p];
+    if (cc < 0) continue;
+    const DevParam pr = params[p];
+    const double* x = feat + (int64_t)pr.feat_col * ld + i;
+    int32_t o = -1;
+    if (pr.kind == UT_BOOL) {
+      o = x[0] != 0.0 ? 1 : 0;
+    } else {
+      for (int32_t k = 0; k < (int32_t)pr.n_opt; ++k)
+        if (x[(int64_t)k * ld] == 1.0) { o = k; break; }
+    }
+    if (o < 0) continue;
+    const int32_t q = cc + o;
+    bcat[((int64_t)(q >> 7) * ldu + i) * 128 + (q & 127)] = 1;
+  }
+}
+
+int launch_prep_cand_cat(ut_ctx* c, const double* feat, int64_t ld, int64_t m, double* u, int32_t dpad, int64_t ldu,
+                         double* cn, int8_t* bcat) {
+  const Space& s = c->space;
+  hipLaunchKernelGGL(k_gp_prep_cand_cat, dim3(grid1(ldu, 256)), dim3(256), 0, c->stream, s.d_params, s.P, feat, ld, m,
+                     s.d_num_feat, s.n_num, dpad, c->gp_inv_ell, s.d_cat_ccol, s.cat_k, u, ldu, cn, bcat);
   UT_LAUNCH_CHECK(c);
   return 0;
 }

@@ -419,6 +419,56 @@ __global__ __launch_bounds__(256) void k_encode_scaled(const DevParam* __restric
   cn[i] = s;
 }
 
+// the categorical K*'s candidate operands in one pass (gp_gemm.hip
+// "Categorical K*"): U'[k][i] = numeric feature k / ell (0 past n_num and for
+// the padding columns), cnorm[i] = |u'_i|^2 over the numeric features in
+// feature order, and the one-hot codes bcat[(q >> 7)][i][q & 127] = 1 at code
+// column q = ccol + option (ENUM), ccol + (value != 0) (BOOL); every code byte
+// of the candidate is written (zeros, then its ones)
+__global__ __launch_bounds__(256) void k_encode_scaled_cat(const DevParam* __restrict__ params, int32_t P,
+                                                           const double* __restrict__ vtab,
+                                                           const double* __restrict__ values, int64_t ld, int64_t m,
+                                                           const int32_t* __restrict__ feat_num, int32_t dpad,
+                                                           const double* __restrict__ inv_ell,
+                                                           const int32_t* __restrict__ cat_ccol, int32_t cat_k,
+                                                           double* __restrict__ u, int64_t ldu, double* __restrict__ cn,
+                                                           int8_t* __restrict__ bcat) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= ldu) return;
+  const uint4 z = make_uint4(0u, 0u, 0u, 0u);
+  for (int32_t kb = 0; kb < cat_k / 128; ++kb) {
+    uint4* row = reinterpret_cast<uint4*>(bcat + ((int64_t)kb * ldu + i) * 128);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) row[q] = z;
+  }
+  for (int32_t k = 0; k < dpad; ++k) u[(int64_t)k * ldu + i] = 0.0;
+  double s = 0.0;
+  if (i < m) {
+    for (int32_t p = 0; p < P; ++p) {
+      const int32_t cc = cat_ccol[p];
+      const DevParam pr = params[p];
+      if (cc >= 0) {
+        const double v = values[(int64_t)pr.col * ld + i];
+        int64_t o = pr.kind == UT_BOOL ? (v != 0.0 ? 1 : 0) : (int64_t)v;
+        if (o < 0 || o >= (pr.kind == UT_BOOL ? 2 : pr.n_opt)) continue;   // no option: no match
+        const int32_t q = cc + (int32_t)o;
+        bcat[((int64_t)(q >> 7) * ldu + i) * 128 + (q & 127)] = 1;
+        continue;
+      }
+      encode_param(pr, values, ld, i, vtab, [&](int32_t c, double f) {
+        const double v = f * inv_ell[c];
+        u[(int64_t)feat_num[c] * ldu + i] = v;
+      });
+    }
+    // the norm in numeric-feature order (= feature order), as k_gp_num_train sums the training side
+    for (int32_t k = 0; k < dpad; ++k) {
+      const double v = u[(int64_t)k * ldu + i];
+      s += v * v;
+    }
+  }
+  cn[i] = s;
+}
+
 __global__ void k_gather_rows(int32_t NC, const double* __restrict__ values, int64_t ld,
                               const int64_t* __restrict__ idx, int64_t cand_base, int32_t k,
                               double* __restrict__ out, int64_t ldo, const uint32_t* __restrict__ dig,
@@ -872,6 +922,15 @@ int launch_encode_scaled(ut_ctx* c, const double* values, int64_t ld, int64_t m,
                          double* cn) {
   hipLaunchKernelGGL(k_encode_scaled, dim3(grid1(ldu, 256)), dim3(256), 0, c->stream, c->space.d_params, c->space.P,
                      c->space.d_vtab, values, ld, m, c->space.n_feat, c->gp_inv_ell, dpad, u, ldu, cn);
+  UT_LAUNCH_CHECK(c);
+  return 0;
+}
+
+int launch_encode_scaled_cat(ut_ctx* c, const double* values, int64_t ld, int64_t m, double* u, int32_t dpad,
+                             int64_t ldu, double* cn, int8_t* bcat) {
+  const Space& s = c->space;
+  hipLaunchKernelGGL(k_encode_scaled_cat, dim3(grid1(ldu, 256)), dim3(256), 0, c->stream, s.d_params, s.P, s.d_vtab,
+                     values, ld, m, s.d_feat_num, dpad, c->gp_inv_ell, s.d_cat_ccol, s.cat_k, u, ldu, cn, bcat);
   UT_LAUNCH_CHECK(c);
   return 0;
 }

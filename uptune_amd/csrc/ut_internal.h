@@ -86,6 +86,18 @@ struct Space {
   int32_t n_comp = 0;                     // params whose inner digest is computed (cslot >= 0)
   int32_t* d_comp = nullptr;              // cslot -> param index
   int32_t* d_col_param = nullptr;         // value column -> its param (first column of a non-PERM param), or -1
+  // categorical K* (gp_gemm.hip): ENUM / BOOL params are one-hot blocks of the
+  // GP features, so their part of |x - u|^2 is (2 or 1) / ell^2 per mismatching
+  // param -- an integer dot product of one-hot codes, taken on the int8 MFMA;
+  // the other ("numeric") features go through the fp64 K* contraction
+  int32_t n_cat = 0;                      // ENUM + BOOL params
+  int32_t cat_k = 0;                      // int8 code columns (ENUM: n_opt, BOOL: 2), padded to 128
+  int32_t n_num = 0;                      // numeric features
+  std::vector<int32_t> host_cat;          // the ENUM / BOOL param indices
+  std::vector<int32_t> host_num_feat;     // numeric k -> feature column
+  int32_t* d_cat_ccol = nullptr;          // per param: first code column (-1: numeric param)
+  int32_t* d_num_feat = nullptr;          // numeric k -> feature column
+  int32_t* d_feat_num = nullptr;          // feature column -> numeric k, or -1 (categorical)
 };
 
 template <class T>
@@ -265,6 +277,19 @@ struct ut_ctx {
   float* gp_Xs_f = nullptr;    // fp32 copies for the fp32 MFMA path
   double* gp_LinvT = nullptr;  // (L^-1)^T [k][row]: the A operand of the variance contraction
   double* gp_XsT = nullptr;    // (X/ell)^T [dpad][npad]: the A operand of the K* contraction
+  // categorical K* of the current fit (cat_on): numeric-feature operands and
+  // the training rows' weighted one-hot codes; c0 + c1 * matches starts the
+  // fp64 accumulator (= -|x_cat - u_cat|^2 / 2)
+  bool cat_on = false;         // this fit scores with the categorical K*
+  bool cat_x_ok = false;       // every training row so far has one-hot ENUM / 0-1 BOOL features
+  int32_t cat_enable = 1;      // UT_CAT_KSTAR
+  double cat_c0 = 0.0, cat_c1 = 0.0;
+  ut::DevBuf<double> gp_XsT_num;    // [dpad_num][npad]
+  ut::DevBuf<double> gp_xnorm_num;  // [npad] |x_num / ell|^2
+  ut::DevBuf<int8_t> gp_acat;       // [cat_k / 128][npad][128] training codes (weights 2 ENUM, 1 BOOL)
+  ut::DevBuf<int8_t> bcat;         // [cat_k / 128][ldk][128] candidate codes (one-hot 0/1)
+  bool ucand_cat = false;          // ucand / cnorm / bcat hold the categorical K*'s operands (encode path)
+  ut::DevBuf<int8_t> pr_bcat;      // pruned scoring: the gathered candidates' codes
   float* gp_LinvT_f = nullptr;  // fp32 (L^-1)^T; in h3 mode the fp16 hi/lo planes of L^-1 [row][k]
   int32_t* gp_ctr = nullptr;   // [32] per-XCD work tickets: [0,8) variance, [8,16) K*; [16,18) max|L^-1| bits (h3)
   int32_t n_cu = 256;
@@ -337,7 +362,7 @@ int set_err(ut_ctx* c, int code, const std::string& msg);
 // the bytes held per device are what ut_device_bytes reports (a rank's HBM
 // footprint in the bench line)
 hipError_t dmalloc(void** p, size_t bytes);
-hipError_t dfree(void* p);
+void dfree(void* p);
 
 // wait for every stream of the context (before freeing or reusing buffers)
 inline hipError_t sync_all(ut_ctx* c) {
@@ -463,19 +488,39 @@ int topk_impl(ut_ctx* c, const double* score, const uint8_t* dup, int64_t m, int
               int64_t* out_idx, double* out_score);
 int topk_pairs_impl(ut_ctx* c, const double* score, const int64_t* idx, int64_t n, int32_t k, int64_t* out_idx,
                     double* out_score);
+// feat_ours: the features come from ut's own encoder (one-hot ENUM blocks),
+// so the categorical K* may read them as codes
 int gp_topk_pruned_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, const ut_acq* acq, const uint8_t* dup,
                         int64_t cand_base, int32_t k, int32_t bound_rows, int64_t* out_idx, double* out_score,
-                        ut_prune_stats* stats, hipEvent_t dup_ready = nullptr);
+                        ut_prune_stats* stats, hipEvent_t dup_ready = nullptr, bool feat_ours = false);
 // prec: 64 (fp64 MFMA), 32 (fp32 MFMA), 16 (f16x3: fp16 hi/lo split operands,
 // three fp16 MFMA products, f32 accumulate -- see gp_gemm.hip)
 constexpr int H3_KSCALE_EXP = 14;  // K* (<= sf2) is scaled by 2^(14 - ceil(log2 sf2)) before the split
 int h3_kstar_exp(double sf2);
+// the K* contraction's categorical operands (nkc = cat_k / 128 int8 stages; 0 = none)
+struct KstarCat {
+  const int8_t* acat = nullptr;
+  const int8_t* bcat = nullptr;
+  int32_t nkc = 0;
+  double c0 = 0.0, c1 = 0.0;
+};
 int launch_gemm_kstar(ut_ctx* c, int prec, const double* XsT, int32_t npad, const double* ucand, int32_t dpad,
                       int64_t m, void* kst, int64_t ldk, double* part, int32_t store_rows = -1,
                       const double* cn = nullptr,    // candidate norms (nullptr: c->cnorm)
-                      double* part2 = nullptr);      // fp64 with part: also sum_r k*_r^2 partials
+                      double* part2 = nullptr,       // fp64 with part: also sum_r k*_r^2 partials
+                      const KstarCat& cat = KstarCat(),
+                      const double* xn = nullptr);   // training norms (nullptr: c->gp_xnorm)
 int launch_prep_cand(ut_ctx* c, const double* feat, int64_t ld, int64_t m, int32_t d, int32_t dpad, double* u,
                      int64_t ldu, double* cn);
+// categorical K*: the K* operands of the candidate side when the fit is in
+// categorical mode -- numeric features / ell (dpad_num rows), their norms, and
+// one-hot codes into c->bcat (from values, or from features made by ut's own
+// encoder)
+inline int32_t cat_dpad(const ut_ctx* c) { return kstar_dpad(c->space.n_num); }
+int launch_encode_scaled_cat(ut_ctx* c, const double* values, int64_t ld, int64_t m, double* u, int32_t dpad,
+                             int64_t ldu, double* cn, int8_t* bcat);
+int launch_prep_cand_cat(ut_ctx* c, const double* feat, int64_t ld, int64_t m, double* u, int32_t dpad, int64_t ldu,
+                         double* cn, int8_t* bcat);
 int launch_xs_t(ut_ctx* c, const double* Xs, int32_t npad, int32_t d, int32_t dpad, double* XsT);
 int launch_gemm_var(ut_ctx* c, int prec, const void* LinvT, int64_t lda, const void* kst, int64_t ldk, int32_t npad,
                     int64_t m, double* part, const double* beta, double* mpart);

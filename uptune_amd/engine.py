@@ -318,6 +318,13 @@ class BatchEngine:
         L.check(self.ctx, self.lib.ut_gp_last_fit_kind(self.ctx, C.byref(k)), "ut_gp_last_fit_kind")
         return "append" if k.value == 1 else "refit"
 
+    def gp_kstar_mode(self) -> str:
+        """ut_gp_kstar_mode: "categorical" (ENUM / BOOL one-hot blocks as an
+        int8 code product beside the fp64 contraction) or "dense" """
+        v = C.c_int32()
+        L.check(self.ctx, self.lib.ut_gp_kstar_mode(self.ctx, C.byref(v)), "ut_gp_kstar_mode")
+        return "categorical" if v.value else "dense"
+
     def gp_stats(self) -> Tuple[float, float, float]:
         a, b, c = C.c_double(), C.c_double(), C.c_double()
         L.check(self.ctx, self.lib.ut_gp_stats(self.ctx, C.byref(a), C.byref(b), C.byref(c)), "ut_gp_stats")
