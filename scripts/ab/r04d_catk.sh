@@ -13,3 +13,7 @@ for cfg in "--config c3 --precision 16" "--config c3 --prune 256" "--config c4";
     UT_CAT_KSTAR=$on run 400 ${tag}_cat$on python bench.py $cfg --steps 3 --warmup 1 --no-cpu-baseline
   done
 done
+# per-rank device memory at N > 1 (gloo rehearsal on one GPU): weak N = 2 at
+# the full C2 m (population 2M), strong N = 8 over the C2 pool (128k per rank)
+UT_DIST_BACKEND=gloo run 400 mem_weak2 python bench.py --gpus 2 --steps 2 --warmup 1 --no-cpu-baseline --no-parity
+UT_DIST_BACKEND=gloo run 400 mem_strong8 python bench.py --gpus 8 --scaling strong --steps 2 --warmup 1 --no-cpu-baseline --no-parity
