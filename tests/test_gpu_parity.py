@@ -1213,11 +1213,21 @@ def test_categorical_kstar_equals_dense(which, prec):
         np.testing.assert_allclose(var_c, var_d, rtol=1e-9, atol=1e-10)
         np.testing.assert_allclose(sc_c, sc_d, rtol=1e-9, atol=1e-10)
         tol = dict(rtol=RTOL, atol=ATOL)
+        np.testing.assert_allclose(mu_c, wmu, **tol)
+        np.testing.assert_allclose(var_c, wvar, **tol)
+        np.testing.assert_allclose(sc_c, ei, **tol)
     else:
-        tol = dict(rtol=1e-3, atol=1e-5)
-    np.testing.assert_allclose(mu_c, wmu, **tol)
-    np.testing.assert_allclose(var_c, wvar, **tol)
-    np.testing.assert_allclose(sc_c, ei, **tol)
+        # the fp32 / f16x3 variance of a candidate ON a training point is a
+        # cancellation 1 - (1 - 1e-6) in f32: the tier's error there is the
+        # dense path's too, so the categorical K* must be as good as dense
+        # (its K* differs from dense only in fp64 summation order, below the
+        # f32 rounding of the stored K*)
+        def err(a, b):
+            return float(np.max(np.abs(a - b) / (1e-5 + 1e-3 * np.abs(b))))
+        for got, dense, want in ((mu_c, mu_d, wmu), (var_c, var_d, wvar), (sc_c, sc_d, ei)):
+            assert err(got, want) <= max(1.0, 1.25 * err(dense, want)), (err(got, want), err(dense, want))
+            far = np.arange(m) >= 20              # away from the training points: the tier's 1e-3
+            np.testing.assert_allclose(got[far], want[far], rtol=1e-3, atol=1e-5)
 
 
 def test_categorical_kstar_fallbacks():
