@@ -5,7 +5,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 O=gpurun_out/r04d; mkdir -p $O
 run() { local t=$1 name=$2; shift 2; timeout -k 10 $t "$@" > $O/$name.log 2>&1; local rc=$?;
         echo "$name rc=$rc"; tail -1 $O/$name.log | cut -c1-250; [ $rc -eq 0 ] || exit $rc; }
-run 300 pytest_cat python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 120 --timeout-method thread -k "categorical"
+run 300 pytest_cat python -u -m pytest tests/test_gpu_parity.py -m gpu -q --timeout 120 --timeout-method thread -k "categorical"
 run 900 pytest python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread
 for cfg in "--config c3 --precision 16" "--config c3 --prune 256" "--config c4"; do
   tag=$(echo $cfg | tr -d ' -')

