@@ -1251,7 +1251,8 @@ def test_categorical_kstar_fallbacks():
         np.testing.assert_allclose(v2.cpu().numpy(), var, rtol=RTOL, atol=ATOL)
 
     Xb = X.copy()
-    enum_col = next(p.feat_col for p in e.spec.params if p.kind == 5)
+    enum_p = next(p for p in e.spec.params if p.kind == 5)
+    enum_col = enum_p.feat_col
     Xb[7, enum_col] = 0.5                       # not one-hot
     e.gp_fit(Xb, y, lengthscale=1.0, sigma_f2=1.0, sigma_n2=1e-6, jitter=1e-8)
     assert e.gp_kstar_mode() == "dense"
@@ -1268,7 +1269,7 @@ def test_categorical_kstar_fallbacks():
     assert e.gp_last_fit_kind() == "append" and e.gp_kstar_mode() == "categorical"
     check(X[:250], 1.0)
     Xc = X.copy()
-    Xc[280, enum_col] = 0.0                     # an all-zero block in an appended row
+    Xc[280, enum_col:enum_col + enum_p.n_feat] = 0.0   # an all-zero block in an appended row
     e.gp_fit(Xc, y, lengthscale=1.0, sigma_f2=1.0, sigma_n2=1e-6, jitter=1e-8)
     assert e.gp_kstar_mode() == "dense"
     check(Xc, 1.0)
