@@ -1176,6 +1176,58 @@ def test_chol_fused_refit_bitwise_and_not_pd():
             os.environ["UT_CHOL_FUSE"] = old
 
 
+@pytest.mark.parametrize("prec", [64, 32, 16])
+def test_early_alpha_equals_inverse_products(prec):
+    """alpha = K^-1 y and beta = L^-1 y by the triangular solves that ride on
+    the refit's panel steps (UT_EARLY_ALPHA=1, the default: scoring that takes
+    the mean in K* starts before the recursive inverse) against the products
+    with L^-1 (UT_EARLY_ALPHA=0): the posterior agrees to fp64 rounding, and
+    both to the oracle; the pruned top-k is the same selection"""
+    _require_gpu()
+    rng = np.random.default_rng(43)
+    n, d = 1500, 8
+    X = rng.uniform(size=(n, d))
+    y = np.sin(3 * X[:, 0]) + np.sum((X - 0.4) ** 2, axis=1)
+    U = np.ascontiguousarray(rng.uniform(size=(d, 5000)))
+    U[:, :4] = X[:4].T
+    space = [Param("f%d" % i, FLOAT, 0.0, 1.0) for i in range(d)]
+    old = os.environ.get("UT_EARLY_ALPHA")
+    outs, sels = [], []
+    try:
+        for early in ("0", "1"):
+            os.environ["UT_EARLY_ALPHA"] = early
+            e = engine(space, seed=2)
+            e.gp_set_precision(prec)
+            e.gp_fit(X, y, lengthscale=0.3, sigma_f2=1.0, sigma_n2=1e-6, jitter=1e-8, wait=False)
+            Ud = torch.from_numpy(U).cuda()
+            outs.append([t.cpu().numpy() for t in e.gp_score(Ud, acq=e.acq("ei"))])
+            if prec == 64:
+                e.gp_fit(X[:1400], y[:1400], lengthscale=0.3, sigma_f2=1.0, sigma_n2=1e-6, jitter=1e-8, wait=False)
+                idx, sc, _ = e.gp_topk_pruned(Ud, 16, acq=e.acq("ei"), bound_rows=256)
+                sels.append(idx.cpu().numpy())
+            e.close()
+    finally:
+        if old is None:
+            os.environ.pop("UT_EARLY_ALPHA", None)
+        else:
+            os.environ["UT_EARLY_ALPHA"] = old
+    (mu0, var0, ei0), (mu1, var1, ei1) = outs
+    assert np.array_equal(var0, var1)          # the variance reads L^-1 only
+    np.testing.assert_allclose(mu1, mu0, rtol=1e-9, atol=1e-12)
+    np.testing.assert_allclose(ei1, ei0, rtol=1e-9, atol=1e-12)
+    g = ogp.GP(X, y, lengthscale=0.3, sigma_f2=1.0, sigma_n2=1e-6, jitter=1e-8)
+    mu_o, var_o = g.posterior(U.T)
+    ei_o = ogp.acquisition(mu_o, var_o, g.f_best)
+    _close(mu1, mu_o)                          # the mean is fp64 in every tier
+    if prec == 64:
+        _close(var1, var_o, atol=1e-8)
+        _close(ei1, ei_o, atol=1e-8)
+        assert (sels[0] == sels[1]).all()
+    else:
+        _close(var1, var_o, rtol=1e-3, atol=1e-5)
+        _close(ei1, ei_o, rtol=1e-3, atol=1e-5)
+
+
 @pytest.mark.parametrize("which", ["hpl", "gcc", "mixed", "perm"])
 @pytest.mark.parametrize("prec", [64, 32, 16])
 def test_categorical_kstar_equals_dense(which, prec):

@@ -221,6 +221,7 @@ int ut_ctx_create(int device, uint64_t seed, ut_ctx** out) {
       hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_fit, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_alpha, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_prefit, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_fit_x, hipEventDisableTiming) != hipSuccess) {
     ut_ctx_destroy(c);
@@ -234,6 +235,7 @@ int ut_ctx_create(int device, uint64_t seed, ut_ctx** out) {
   if (const char* e = getenv("UT_FIT_APPEND")) c->fit_append = atoi(e) != 0;
   if (const char* e = getenv("UT_DE_AOS")) c->de_aos = atoi(e) != 0;
   if (const char* e = getenv("UT_HASH_AFTER_FIT")) c->hash_after_fit = atoi(e);
+  if (const char* e = getenv("UT_EARLY_ALPHA")) c->early_alpha = atoi(e) != 0;
   if (const char* e = getenv("UT_HASH_HOLD_LOWPREC")) c->hash_hold_lowprec = atoi(e) != 0;
   if (const char* e = getenv("UT_HASH_AFTER_KSTAR")) c->hash_after_kstar = atoi(e);
   if (const char* e = getenv("UT_H3_SCHED")) c->h3_sched = atoi(e);
@@ -274,7 +276,7 @@ int ut_ctx_destroy(ut_ctx* c) {
   fr(c->forest_nodes); fr(c->forest_roots); fr(c->r_topk_vals.p);
   fr(c->cm_send.p); fr(c->cm_recv.p); fr(c->cm_keep.p); fr(c->cm_pay.p); fr(c->cm_cnt.p);
   for (auto& m : c->timing.marks) hipEventDestroy(m.ev);
-  for (hipEvent_t e : {c->ev_fork, c->ev_join, c->ev_fit, c->ev_prefit, c->ev_fit_x})
+  for (hipEvent_t e : {c->ev_fork, c->ev_join, c->ev_fit, c->ev_prefit, c->ev_fit_x, c->ev_alpha})
     if (e) hipEventDestroy(e);
   if (c->fit_host) hipHostFree(c->fit_host);
   if (c->flag_host) hipHostFree(c->flag_host);

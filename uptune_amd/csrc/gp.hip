@@ -267,12 +267,34 @@ __global__ __launch_bounds__(256) void k_chol_diag(double* __restrict__ K, doubl
   chol_diag_core(a, K, Li, npad, kb, flag, col, Ls, invd);
 }
 
-// Panel kb, step 2: row block i > kb:  L_ik = A_ik * inv(L_kk)^T  (NT product)
+// w_kb = inv(L_kk) yw_kb: thread t < 64 of the calling workgroup, row t
+__device__ __forceinline__ double fwd_block(const double* __restrict__ Li, int32_t npad, int64_t base,
+                                           const double* __restrict__ yw, int t) {
+  const double* li = Li + (base + t) * npad + base;
+  double s = 0.0;
+  for (int c = 0; c <= t; ++c) s = __builtin_fma(li[c], yw[base + c], s);
+  return s;
+}
+
+// Panel kb, step 2: row block i > kb:  L_ik = A_ik * inv(L_kk)^T  (NT product).
+// yw != NULL: the forward solve L beta = y rides along (the right-looking
+// update of an extra column): every workgroup forms w_kb = inv(L_kk) yw_kb
+// (yw_kb is final: blocks <= kb are not written in this launch), workgroup 0
+// stores it as beta_kb, and each updates its own block, yw_i -= L_ik w_kb.
 __global__ __launch_bounds__(256) void k_chol_rows(double* __restrict__ K, const double* __restrict__ Li,
-                                                   int32_t npad, int32_t kb) {
+                                                   int32_t npad, int32_t kb, double* __restrict__ yw,
+                                                   double* __restrict__ beta) {
   __shared__ double As[16 * 80];
   __shared__ double Bs[16 * 80];
+  __shared__ double Lt[NB * (NB + 1)];
+  __shared__ double wv[NB];
   const int64_t base = (int64_t)kb * NB, rb = (int64_t)(kb + 1 + blockIdx.x) * NB;
+  const int t = threadIdx.x;
+  if (yw && t < NB) {
+    const double w = fwd_block(Li, npad, base, yw, t);
+    wv[t] = w;
+    if (blockIdx.x == 0) beta[base + t] = w;
+  }
   fd4 acc[2][2];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -284,7 +306,46 @@ __global__ __launch_bounds__(256) void k_chol_rows(double* __restrict__ K, const
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) K[(rb + tile_row(i, r)) * npad + base + tile_col(j)] = acc[i][j][r];
+      for (int r = 0; r < 4; ++r) {
+        K[(rb + tile_row(i, r)) * npad + base + tile_col(j)] = acc[i][j][r];
+        if (yw) Lt[tile_row(i, r) * (NB + 1) + tile_col(j)] = acc[i][j][r];
+      }
+  if (!yw) return;
+  __syncthreads();
+  if (t < NB) {
+    double s = 0.0;
+    for (int c = 0; c < NB; ++c) s = __builtin_fma(Lt[t * (NB + 1) + c], wv[c], s);
+    yw[rb + t] -= s;
+  }
+}
+
+// the forward solve's last block (no row block below it): beta_kb = inv(L_kk) yw_kb
+__global__ __launch_bounds__(64) void k_fwd_last(const double* __restrict__ Li, int32_t npad, int32_t kb,
+                                                 const double* __restrict__ yw, double* __restrict__ beta) {
+  const int64_t base = (int64_t)kb * NB;
+  beta[base + threadIdx.x] = fwd_block(Li, npad, base, yw, threadIdx.x);
+}
+
+// Backward solve L^T alpha = beta, right-looking from the last block: launch b
+// forms alpha_b = inv(L_bb)^T z_b (z_b final: only blocks < b are written
+// here), workgroup 0 stores it, and workgroup c < b updates its block,
+// z_c -= L_bc^T alpha_b (row r of L_bc read coalesced).  z starts as beta.
+__global__ __launch_bounds__(64) void k_bwd_step(const double* __restrict__ L, const double* __restrict__ Li,
+                                                 int32_t npad, int32_t b, double* __restrict__ z,
+                                                 double* __restrict__ alpha) {
+  __shared__ double av[NB];
+  const int t = threadIdx.x;
+  const int64_t bb = (int64_t)b * NB;
+  double s = 0.0;
+  for (int j = t; j < NB; ++j) s = __builtin_fma(Li[(bb + j) * npad + bb + t], z[bb + j], s);
+  av[t] = s;
+  if (blockIdx.x == 0) alpha[bb + t] = s;
+  if (b == 0) return;
+  __syncthreads();
+  const int64_t cb = (int64_t)blockIdx.x * NB;
+  double u = 0.0;
+  for (int r = 0; r < NB; ++r) u = __builtin_fma(L[(bb + r) * npad + cb + t], av[r], u);
+  z[cb + t] -= u;
 }
 
 // Trailing update A_ij -= L_i,kb L_j,kb^T for kb < j <= i < nb.
@@ -889,13 +950,21 @@ int gp_fit_enqueue(ut_ctx* c, const double* X, const double* y, int32_t n, int32
     const int32_t nb = npad / NB;
     UT_HIP(c, hipMemsetAsync(c->gp_Linv, 0, sizeof(double) * npad * npad, c->stream));
     const bool fuse = c->chol_fuse > 0 || (c->chol_fuse < 0 && npad >= 2048);
+    // early alpha: beta = L^-1 y by a forward solve riding on the panel steps
+    // and alpha = L^-T beta by a backward solve, both before the inverse, so
+    // the scoring that takes the mean in K* (pruned, fp32, f16x3) starts at
+    // ev_alpha while the recursive inverse is still running.  The work vector
+    // is the inverse's scratch (gp_T), free until then.
+    double* yw = c->early_alpha ? c->gp_T : nullptr;
+    if (yw) UT_HIP(c, hipMemcpyAsync(yw, c->gp_y, sizeof(double) * npad, hipMemcpyDeviceToDevice, c->stream));
     for (int32_t kb = 0; kb < nb; ++kb) {
       // (fused: diagonal blocks after the first come from the previous update)
       if (!fuse || kb == 0)
         hipLaunchKernelGGL(k_chol_diag, dim3(1), dim3(256), 0, c->stream, c->gp_K, c->gp_Linv, npad, kb, c->gp_flag);
       const int32_t T = nb - kb - 1;
       if (T > 0) {
-        hipLaunchKernelGGL(k_chol_rows, dim3(T), dim3(256), 0, c->stream, c->gp_K, c->gp_Linv, npad, kb);
+        hipLaunchKernelGGL(k_chol_rows, dim3(T), dim3(256), 0, c->stream, c->gp_K, c->gp_Linv, npad, kb, yw,
+                           c->gp_beta);
         if (fuse)
           hipLaunchKernelGGL(k_chol_update_diag, dim3(T * (T + 1) / 2), dim3(256), 0, c->stream, c->gp_K, c->gp_Linv,
                              npad, kb, c->gp_flag);
@@ -903,7 +972,15 @@ int gp_fit_enqueue(ut_ctx* c, const double* X, const double* y, int32_t n, int32
           hipLaunchKernelGGL(k_chol_update, dim3(T * (T + 1) / 2), dim3(256), 0, c->stream, c->gp_K, npad, kb);
       }
     }
+    if (yw) {
+      hipLaunchKernelGGL(k_fwd_last, dim3(1), dim3(64), 0, c->stream, c->gp_Linv, npad, nb - 1, yw, c->gp_beta);
+      UT_HIP(c, hipMemcpyAsync(yw, c->gp_beta, sizeof(double) * npad, hipMemcpyDeviceToDevice, c->stream));
+      for (int32_t b = nb - 1; b >= 0; --b)
+        hipLaunchKernelGGL(k_bwd_step, dim3(b > 0 ? b : 1), dim3(64), 0, c->stream, c->gp_K, c->gp_Linv, npad, b, yw,
+                           c->gp_alpha);
+    }
     UT_LAUNCH_CHECK(c);
+    UT_HIP(c, hipEventRecord(c->ev_alpha, c->stream));
     // off-diagonal blocks of L^-1 by recursive doubling (diagonal blocks came from k_chol_diag)
     for (int32_t lv = NB; lv < npad; lv *= 2) {
       const int32_t pairs = (int32_t)((npad - lv + 2 * lv - 1) / (2 * lv));
@@ -913,17 +990,23 @@ int gp_fit_enqueue(ut_ctx* c, const double* X, const double* y, int32_t n, int32
     }
     UT_LAUNCH_CHECK(c);
   }
-  hipLaunchKernelGGL(k_lower_mv, dim3(grid1(npad, 4)), dim3(256), 0, c->stream, c->gp_Linv, npad, c->gp_y,
-                     c->gp_beta);
-  UT_LAUNCH_CHECK(c);
+  const bool solved = !app && c->early_alpha;   // beta and alpha came from the solves above
+  if (!solved) {
+    hipLaunchKernelGGL(k_lower_mv, dim3(grid1(npad, 4)), dim3(256), 0, c->stream, c->gp_Linv, npad, c->gp_y,
+                       c->gp_beta);
+    UT_LAUNCH_CHECK(c);
+  }
   if (c->gp_prec == 32 && (rc = launch_to_f32(c, c->gp_Xs, c->gp_Xs_f, (int64_t)npad * d))) return rc;
   // (an append wrote its rows of LinvT itself)
   if ((!app || c->gp_prec == 32) &&
       (rc = launch_transpose(c, c->gp_Linv, npad, c->gp_LinvT, c->gp_prec == 32 ? c->gp_LinvT_f : nullptr)))
     return rc;
-  hipLaunchKernelGGL(k_upper_mv, dim3(grid1(npad, 4)), dim3(256), 0, c->stream, c->gp_LinvT, npad, c->gp_beta,
-                     c->gp_alpha);
-  UT_LAUNCH_CHECK(c);
+  if (!solved) {
+    hipLaunchKernelGGL(k_upper_mv, dim3(grid1(npad, 4)), dim3(256), 0, c->stream, c->gp_LinvT, npad, c->gp_beta,
+                       c->gp_alpha);
+    UT_LAUNCH_CHECK(c);
+    UT_HIP(c, hipEventRecord(c->ev_alpha, c->stream));
+  }
   if (c->gp_prec == 16 && (rc = launch_split_h3(c, c->gp_Linv, npad, reinterpret_cast<_Float16*>(c->gp_LinvT_f))))
     return rc;
   c->gp_fit_prec = c->gp_prec;
@@ -998,7 +1081,7 @@ int gp_score_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, const ut
   // overlaps the rest of an asynchronous fit and only the variance GEMM waits
   // for L^-1.  fp32 keeps the mean in K*'s fp64 epilogue (k* . alpha, before
   // k* is rounded to fp32) and waits for the whole fit.
-  if (c->fit_pending) UT_HIP(c, hipStreamWaitEvent(c->stream, fp32 ? c->ev_fit : c->ev_fit_x, 0));
+  if (c->fit_pending) UT_HIP(c, hipStreamWaitEvent(c->stream, fp32 ? c->ev_alpha : c->ev_fit_x, 0));
   const int32_t n = c->gp_n, d = c->gp_d;
   const int32_t npad = ((n + NPAD - 1) / NPAD) * NPAD;
   // the categorical K* when the candidates came through ut's encoder
@@ -1027,7 +1110,7 @@ int gp_score_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, const ut
     return rc;
   mark(c, "kstar");
   if (mid && (rc = mid())) return rc;
-  if (c->fit_pending && !fp32) UT_HIP(c, hipStreamWaitEvent(c->stream, c->ev_fit, 0));
+  if (c->fit_pending) UT_HIP(c, hipStreamWaitEvent(c->stream, c->ev_fit, 0));
   if (dup_ready && c->join_before_var && var_joins) UT_HIP(c, hipStreamWaitEvent(c->stream, dup_ready, 0));
   mark(c, "");  // the wait for the fit is not variance time
   if ((rc = launch_gemm_var(c, prec, fp32 ? (const void*)c->gp_LinvT_f : (const void*)c->gp_LinvT, npad, c->kst.p,
@@ -1226,7 +1309,7 @@ int gp_topk_pruned_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, co
   UT_CHECK(c, acq->kind == UT_ACQ_EI || (acq->kind == UT_ACQ_UCB && acq->kappa >= 0.0), UT_EINVAL,
            "gp_topk_pruned: the score must increase with sigma (EI, or UCB with kappa >= 0)");
   UT_CHECK(c, k >= 1 && k <= 1024, UT_EINVAL, "gp_topk_pruned: k must be in [1, 1024]");
-  if (c->fit_pending) UT_HIP(c, hipStreamWaitEvent(c->stream, c->ev_fit, 0));   // K* takes mu = k* . alpha
+  if (c->fit_pending) UT_HIP(c, hipStreamWaitEvent(c->stream, c->ev_alpha, 0));   // K* takes mu = k* . alpha
   const int32_t n = c->gp_n, d = c->gp_d;
   const int32_t npad = ((n + NPAD - 1) / NPAD) * NPAD;
   const bool cat = feat_ours && c->cat_on;   // the categorical K* (features from ut's encoder)
@@ -1268,6 +1351,8 @@ int gp_topk_pruned_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, co
   if ((rc = launch_gemm_kstar(c, 64, XsT, npad, c->ucand.p, dpad, m, c->kst.p, ldk, c->mu_part.p, R * NPAD,
                               nullptr, c->pr_k2.p, cat ? kstar_cat(c, c->bcat.p) : KstarCat(), xn)))
     return rc;
+  // the rest reads L^-1 (K* needed only alpha: ev_alpha above)
+  if (c->fit_pending) UT_HIP(c, hipStreamWaitEvent(c->stream, c->ev_fit, 0));
   // |L^-1|_F^2 for the variance tail bound, once per fit
   if (!c->pr_f2_valid) {
     hipLaunchKernelGGL(k_sumsq_part, dim3(SQ_BLOCKS), dim3(256), 0, c->stream, c->gp_Linv, (int64_t)npad * npad,

@@ -136,6 +136,11 @@ struct ut_ctx {
   hipStream_t side = nullptr;
   hipStream_t fit_stream = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_fit = nullptr, ev_prefit = nullptr;
+  // alpha = K^-1 y (and beta = L^-1 y) ready: a refit solves for them right after
+  // the Cholesky, before the recursive inverse (early_alpha; UT_EARLY_ALPHA=0
+  // takes them from L^-1 as before); an append records it with ev_fit
+  hipEvent_t ev_alpha = nullptr;
+  bool early_alpha = true;
   hipEvent_t ev_fit_x = nullptr;     // fit stream: scaled training inputs ready (K* may start)
   bool fit_pending = false;          // scoring waits on ev_fit before touching GP state
   // round schedule: 1 = the variance GEMM waits for the side stream's hash +
