@@ -1,0 +1,17 @@
+#!/bin/bash
+# round 4: where the K* kernel's cycles go (C3 pruned round: k_gp_kstar<double,
+# true, true>): the counter list, then SQ issue / wait counters in passes of their own
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
+export TMPDIR=/tmp
+O=gpurun_out/r04g; mkdir -p $O
+timeout -s KILL 60 rocprofv3 -L > $O/counters.txt 2>&1 || echo "list rc=$?"
+B="python3 bench.py --config c3 --prune 256 --steps 2 --warmup 1 --no-cpu-baseline --no-parity"
+i=0
+for set in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_MISC SQ_WAVES" \
+           "SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_BRANCH" \
+           "SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CU_CYCLES SQ_WAIT_INST_LDS SQ_INST_CYCLES_VMEM_RD SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_SCA GRBM_GUI_ACTIVE GRBM_COUNT"; do
+  i=$((i+1))
+  timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $set -d $O/p$i -o run --output-format csv -- $B > $O/p$i.log 2>&1
+  echo "pass $i rc=$?"
+done
+exit 0
