@@ -12,6 +12,6 @@ for set in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_AC
            "SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CU_CYCLES SQ_WAIT_INST_LDS SQ_INST_CYCLES_VMEM_RD SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_SCA GRBM_GUI_ACTIVE GRBM_COUNT"; do
   i=$((i+1))
   timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $set -d $O/p$i -o run --output-format csv -- $B > $O/p$i.log 2>&1
-  echo "pass $i rc=$?"
+  rc=$?; echo "pass $i rc=$rc"; [ $rc -eq 0 ] || exit $rc
 done
 exit 0
