@@ -236,6 +236,7 @@ int ut_ctx_create(int device, uint64_t seed, ut_ctx** out) {
   if (const char* e = getenv("UT_DE_AOS")) c->de_aos = atoi(e) != 0;
   if (const char* e = getenv("UT_HASH_AFTER_FIT")) c->hash_after_fit = atoi(e);
   if (const char* e = getenv("UT_EARLY_ALPHA")) c->early_alpha = atoi(e) != 0;
+  if (const char* e = getenv("UT_KSTAR_REL")) c->rel_enable = atoi(e) != 0;
   if (const char* e = getenv("UT_HASH_HOLD_LOWPREC")) c->hash_hold_lowprec = atoi(e) != 0;
   if (const char* e = getenv("UT_HASH_AFTER_KSTAR")) c->hash_after_kstar = atoi(e);
   if (const char* e = getenv("UT_H3_SCHED")) c->h3_sched = atoi(e);
@@ -779,6 +780,20 @@ int ut_gp_topk_pruned(ut_ctx* c, const double* feat, int64_t ld, int64_t m, cons
   const bool own = c->timing.on && !c->timing.in_round;
   if (own) timing_begin(c);
   int rc = gp_topk_pruned_impl(c, feat, ld, m, acq, dup, cand_base, k, bound_rows, out_idx, out_score, stats);
+  if (own) timing_end(c);
+  return rc;
+}
+
+int ut_gp_topk_pruned_ref(ut_ctx* c, const double* feat, int64_t ld, int64_t m, const ut_acq* acq,
+                          const uint8_t* dup, int64_t cand_base, int32_t k, int32_t bound_rows,
+                          const double* ref_feat, int64_t* out_idx, double* out_score, ut_prune_stats* stats) {
+  if (!c) return UT_EINVAL;
+  UT_CHECK(c, m >= 1 && feat && ld >= m && acq && out_idx && out_score && cand_base >= 0 && ref_feat, UT_EINVAL,
+           "gp_topk_pruned_ref: bad arguments");
+  const bool own = c->timing.on && !c->timing.in_round;
+  if (own) timing_begin(c);
+  int rc = gp_topk_pruned_impl(c, feat, ld, m, acq, dup, cand_base, k, bound_rows, out_idx, out_score, stats, nullptr,
+                               false, ref_feat);
   if (own) timing_end(c);
   return rc;
 }

@@ -1154,7 +1154,9 @@ int gp_score_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, const ut
 //   the exact var IS var_ub, and so is the exact score: it is stored without
 //   the margin and flagged exact, and ties with it can be broken by index
 //   (a flat GP -- every k* ~ 0 -- gives every candidate the same score).
-__global__ void k_prune_bound(int64_t m, int32_t RTm, const double* __restrict__ mu_part, int32_t RTv,
+// RTm mean / |k*|^2 partials per candidate (RT from the MFMA K*, 1 from the
+// parent-relative one), RTv row tiles in the bound, RTall row tiles in all
+__global__ void k_prune_bound(int64_t m, int32_t RTm, int32_t RTall, const double* __restrict__ mu_part, int32_t RTv,
                               const double* __restrict__ var_part, int64_t ldp, double sf2,
                               const double* __restrict__ stats, const int32_t* __restrict__ fit_flag, int32_t kind,
                               double xi, double kappa, const uint8_t* __restrict__ dup, double* __restrict__ mu_out,
@@ -1169,14 +1171,14 @@ __global__ void k_prune_bound(int64_t m, int32_t RTm, const double* __restrict__
   var = var > 0.0 ? var : 0.0;
   double ub = acq_score(kind, mu, var, stats[0], xi, kappa);
   bool exact = false;
-  if (k2_part && RTv < RTm) {
+  if (k2_part && RTv < RTall) {
     for (int32_t r = 0; r < RTm; ++r) k2 += k2_part[(int64_t)r * ldp + i];
     const double tail = 1.001 * (*linv_f2) * k2;
     const double s_hi = (vs + tail) * (1.0 + 0x1p-40);
     double var_lo = sf2 - s_hi;
     var_lo = var_lo > 0.0 ? var_lo : 0.0;
     exact = tail == tail && var_lo == var;   // (NaN tail: not exact)
-  } else if (RTv >= RTm) {
+  } else if (RTv >= RTall) {
     exact = true;   // the bound GEMM covered every row
   }
   if (!exact) ub = ub + fabs(ub) * 1e-12 + 1e-300;
@@ -1303,7 +1305,7 @@ __global__ void k_fill(double* __restrict__ p, int64_t n, double v) {
 
 int gp_topk_pruned_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, const ut_acq* acq, const uint8_t* dup,
                         int64_t cand_base, int32_t k, int32_t bound_rows, int64_t* out_idx, double* out_score,
-                        ut_prune_stats* stats, hipEvent_t dup_ready, bool feat_ours) {
+                        ut_prune_stats* stats, hipEvent_t dup_ready, bool feat_ours, const double* ref_feat) {
   UT_CHECK(c, c->gp_ready, UT_EINVAL, "gp_topk_pruned: call ut_gp_fit first");
   UT_CHECK(c, c->gp_fit_prec == 64, UT_EINVAL, "gp_topk_pruned: needs an fp64 fit (ut_gp_set_precision 64)");
   UT_CHECK(c, acq->kind == UT_ACQ_EI || (acq->kind == UT_ACQ_UCB && acq->kappa >= 0.0), UT_EINVAL,
@@ -1347,10 +1349,19 @@ int gp_topk_pruned_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, co
   // K* stores only the bound rows; the mean sums every row.  The few
   // candidates that need every row (threshold set, survivors) get their K*
   // columns recomputed from their features (recompute_cols below): cheaper than
-  // writing and re-reading the whole n x m matrix
-  if ((rc = launch_gemm_kstar(c, 64, XsT, npad, c->ucand.p, dpad, m, c->kst.p, ldk, c->mu_part.p, R * NPAD,
-                              nullptr, c->pr_k2.p, cat ? kstar_cat(c, c->bcat.p) : KstarCat(), xn)))
+  // writing and re-reading the whole n x m matrix.  With a reference row (a GA
+  // round's parent) and few features, the parent-relative K* (one partial).
+  const bool rel = ref_feat && c->rel_enable && !cat && dpad >= 1 && dpad <= KSTAR_REL_DMAX;
+  c->rel_last = rel ? 1 : 0;
+  const int32_t RTm = rel ? 1 : RT;
+  if (rel) {
+    if ((rc = launch_kstar_rel(c, XsT, npad, c->ucand.p, dpad, m, ldk, ref_feat, c->kst.p, R * NPAD, c->mu_part.p,
+                               c->pr_k2.p)))
+      return rc;
+  } else if ((rc = launch_gemm_kstar(c, 64, XsT, npad, c->ucand.p, dpad, m, c->kst.p, ldk, c->mu_part.p, R * NPAD,
+                                     nullptr, c->pr_k2.p, cat ? kstar_cat(c, c->bcat.p) : KstarCat(), xn))) {
     return rc;
+  }
   // the rest reads L^-1 (K* needed only alpha: ev_alpha above)
   if (c->fit_pending) UT_HIP(c, hipStreamWaitEvent(c->stream, c->ev_fit, 0));
   // |L^-1|_F^2 for the variance tail bound, once per fit
@@ -1367,7 +1378,7 @@ int gp_topk_pruned_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, co
     return rc;
   mark(c, "bound");
   if (dup_ready) UT_HIP(c, hipStreamWaitEvent(c->stream, dup_ready, 0));   // the dup mask (side stream)
-  hipLaunchKernelGGL(k_prune_bound, dim3(grid1(m, 256)), dim3(256), 0, c->stream, m, RT, c->mu_part.p, R,
+  hipLaunchKernelGGL(k_prune_bound, dim3(grid1(m, 256)), dim3(256), 0, c->stream, m, RTm, RT, c->mu_part.p, R,
                      c->var_part.p, ldk, c->gp_sf2, c->gp_stats, c->gp_flag, acq->kind, acq->xi, acq->kappa, dup,
                      c->pr_mu.p, c->pr_ub.p, c->pr_k2.p, c->pr_f2.p, c->pr_exact.p);
   UT_LAUNCH_CHECK(c);
@@ -1460,6 +1471,7 @@ int gp_topk_pruned_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, co
     stats->survivors = dense ? m : ns;
     stats->bound_rows = R * NPAD;
     stats->dense = dense ? 1 : 0;
+    stats->relative = rel ? 1 : 0;
     stats->threshold = tau;
   }
   return 0;
