@@ -962,8 +962,12 @@ def test_gp_topk_pruned_parent_relative(space_name, d_used, m, n):
     assert not st2["relative"]
     _, _, score = e.gp_score(feat, acq=a, dup=dup)
     i_d, t_d = e.topk(score, k, dup=dup, cand_base=7)
-    _close(t_rel.cpu().numpy(), t_mf.cpu().numpy(), rtol=1e-9, atol=1e-12)
-    _close(t_rel.cpu().numpy(), t_d.cpu().numpy(), rtol=1e-9, atol=1e-12)
+    # the two K* forms round differently (|p - x|^2 plus corrections vs
+    # |x|^2 + |u|^2 - 2 x.u), and sigma^2 = sf2 - |L^-1 k*|^2 amplifies a k*
+    # rounding difference by |L^-1|^2 (n = 333 points with sigma_n^2 = 1e-6):
+    # 1e-7 relative, still 100x inside the fp64 bar against the oracle
+    _close(t_rel.cpu().numpy(), t_mf.cpu().numpy(), rtol=1e-7, atol=1e-12)
+    _close(t_rel.cpu().numpy(), t_d.cpu().numpy(), rtol=1e-7, atol=1e-12)
     g = ogp.GP(Xtr, y, lengthscale=0.5, sigma_f2=1.0, sigma_n2=1e-6, jitter=1e-8)
     mu, var = g.posterior(features(space, vals.cpu().numpy()).T)
     sc = ogp.acquisition(mu, var, g.f_best)
@@ -978,7 +982,7 @@ def test_gp_topk_pruned_parent_relative(space_name, d_used, m, n):
     i_r, t_r, st3 = e.gp_topk_pruned(fr, 16, acq=a, bound_rows=128, ref=ref)
     i_r2, t_r2, _ = e.gp_topk_pruned(fr, 16, acq=a, bound_rows=128)
     assert st3["relative"]
-    _close(t_r.cpu().numpy(), t_r2.cpu().numpy(), rtol=1e-9, atol=1e-12)
+    _close(t_r.cpu().numpy(), t_r2.cpu().numpy(), rtol=1e-7, atol=1e-12)
     e.close()
     old = os.environ.get("UT_KSTAR_REL")
     os.environ["UT_KSTAR_REL"] = "0"
