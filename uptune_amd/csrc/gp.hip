@@ -830,6 +830,7 @@ int gp_fit_enqueue(ut_ctx* c, const double* X, const double* y, int32_t n, int32
   int rc = gp_alloc(c, npad, d);
   if (rc) return rc;
   c->pr_f2_valid = false;   // |L^-1|_F^2 (pruned scoring) belongs to the previous factor
+  c->pr_a2_valid = false;   // |alpha|^2 too
   const size_t need = (size_t)n * d + n + d;
   bool fresh = false;   // a new staging buffer holds no previous rows
   if (c->fit_host_n < need) {
@@ -1161,7 +1162,8 @@ __global__ void k_prune_bound(int64_t m, int32_t RTm, int32_t RTall, const doubl
                               const double* __restrict__ stats, const int32_t* __restrict__ fit_flag, int32_t kind,
                               double xi, double kappa, const uint8_t* __restrict__ dup, double* __restrict__ mu_out,
                               double* __restrict__ ub_out, const double* __restrict__ k2_part,
-                              const double* __restrict__ linv_f2, uint8_t* __restrict__ exact_out) {
+                              const double* __restrict__ linv_f2, uint8_t* __restrict__ exact_out,
+                              const double* __restrict__ alpha2) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= m) return;
   double mu = 0.0, vs = 0.0, k2 = 0.0;
@@ -1169,10 +1171,18 @@ __global__ void k_prune_bound(int64_t m, int32_t RTm, int32_t RTall, const doubl
   for (int32_t r = 0; r < RTv; ++r) vs += var_part[(int64_t)r * ldp + i];
   double var = sf2 - vs;
   var = var > 0.0 ? var : 0.0;
-  double ub = acq_score(kind, mu, var, stats[0], xi, kappa);
-  bool exact = false;
-  if (k2_part && RTv < RTall) {
+  if (k2_part)
     for (int32_t r = 0; r < RTm; ++r) k2 += k2_part[(int64_t)r * ldp + i];
+  // alpha2 (the parent-relative K*): mu came from other arithmetic than the
+  // exact scores' (the MFMA K* of the recomputed columns), so the bound takes
+  // mu - dmu, dmu = 2e-11 |alpha| |k*| >= 20x the rounding of either form
+  // (sum_r |alpha_r| k*_r <= |alpha| |k*|; both scores decrease with mu)
+  const double dmu = alpha2 ? 2e-11 * sqrt(*alpha2 * k2) : 0.0;
+  double ub = acq_score(kind, mu - dmu, var, stats[0], xi, kappa);
+  bool exact = false;
+  if (alpha2) {
+    exact = false;   // the stored bound is not the exact score
+  } else if (k2_part && RTv < RTall) {
     const double tail = 1.001 * (*linv_f2) * k2;
     const double s_hi = (vs + tail) * (1.0 + 0x1p-40);
     double var_lo = sf2 - s_hi;
@@ -1247,8 +1257,10 @@ __global__ void k_gather_cols(const double* __restrict__ kst, int64_t ldk, const
 }
 
 // exact scores of the gathered candidates: compact[j], and scattered to full[idx[j]]
+// mean: sum of the recomputed columns' partials mcol [RT][ldp] (the MFMA K*'s
+// k* . alpha, the same arithmetic as the unpruned pruned-K*'s)
 __global__ void k_prune_exact(int64_t n, const int64_t* __restrict__ idx, int64_t base, int32_t RT,
-                              const double* __restrict__ var_part, int64_t ldp, const double* __restrict__ mu_full,
+                              const double* __restrict__ var_part, int64_t ldp, const double* __restrict__ mcol,
                               double sf2, const double* __restrict__ stats, const int32_t* __restrict__ fit_flag,
                               int32_t kind, double xi, double kappa, double* __restrict__ compact,
                               double* __restrict__ full) {
@@ -1259,11 +1271,12 @@ __global__ void k_prune_exact(int64_t n, const int64_t* __restrict__ idx, int64_
     if (compact) compact[j] = -1.0 / 0.0;
     return;
   }
-  double vs = 0.0;
+  double vs = 0.0, mu = 0.0;
   for (int32_t r = 0; r < RT; ++r) vs += var_part[(int64_t)r * ldp + j];
+  for (int32_t r = 0; r < RT; ++r) mu += mcol[(int64_t)r * ldp + j];
   double var = sf2 - vs;
   var = var > 0.0 ? var : 0.0;
-  double sc = acq_score(kind, mu_full[q - base], var, stats[0], xi, kappa);
+  double sc = acq_score(kind, mu, var, stats[0], xi, kappa);
   if (*fit_flag != 0) sc = __builtin_nan("");
   if (compact) compact[j] = sc;
   if (full) full[q - base] = sc;
@@ -1355,9 +1368,23 @@ int gp_topk_pruned_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, co
   c->rel_last = rel ? 1 : 0;
   const int32_t RTm = rel ? 1 : RT;
   if (rel) {
-    if ((rc = launch_kstar_rel(c, XsT, npad, c->ucand.p, dpad, m, ldk, ref_feat, c->kst.p, R * NPAD, c->mu_part.p,
+    // the mean and |k*|^2 from the relative form; the bound rows from the MFMA
+    // K* over their R row tiles only (the same k* as the exact recomputation
+    // below, so the bound variance stays >= the exact one bit for bit)
+    if ((rc = launch_kstar_rel(c, XsT, npad, c->ucand.p, dpad, m, ldk, ref_feat, c->kst.p, 0, c->mu_part.p,
                                c->pr_k2.p)))
       return rc;
+    if ((rc = launch_gemm_kstar(c, 64, XsT, npad, c->ucand.p, dpad, m, c->kst.p, ldk, nullptr, -1, nullptr, nullptr,
+                                KstarCat(), xn, R * NPAD)))
+      return rc;
+    if (!c->pr_a2_valid) {
+      if ((rc = ensure(c, c->pr_a2, 1 + SQ_BLOCKS))) return rc;
+      hipLaunchKernelGGL(k_sumsq_part, dim3(SQ_BLOCKS), dim3(256), 0, c->stream, c->gp_alpha, (int64_t)npad,
+                         c->pr_a2.p + 1);
+      hipLaunchKernelGGL(k_sumsq_final, dim3(1), dim3(256), 0, c->stream, c->pr_a2.p + 1, SQ_BLOCKS, c->pr_a2.p);
+      UT_LAUNCH_CHECK(c);
+      c->pr_a2_valid = true;
+    }
   } else if ((rc = launch_gemm_kstar(c, 64, XsT, npad, c->ucand.p, dpad, m, c->kst.p, ldk, c->mu_part.p, R * NPAD,
                                      nullptr, c->pr_k2.p, cat ? kstar_cat(c, c->bcat.p) : KstarCat(), xn))) {
     return rc;
@@ -1380,7 +1407,7 @@ int gp_topk_pruned_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, co
   if (dup_ready) UT_HIP(c, hipStreamWaitEvent(c->stream, dup_ready, 0));   // the dup mask (side stream)
   hipLaunchKernelGGL(k_prune_bound, dim3(grid1(m, 256)), dim3(256), 0, c->stream, m, RTm, RT, c->mu_part.p, R,
                      c->var_part.p, ldk, c->gp_sf2, c->gp_stats, c->gp_flag, acq->kind, acq->xi, acq->kappa, dup,
-                     c->pr_mu.p, c->pr_ub.p, c->pr_k2.p, c->pr_f2.p, c->pr_exact.p);
+                     c->pr_mu.p, c->pr_ub.p, c->pr_k2.p, c->pr_f2.p, c->pr_exact.p, rel ? c->pr_a2.p : nullptr);
   UT_LAUNCH_CHECK(c);
   // 3. threshold: exact scores of the best 1024 bounds, tau = their k-th best
   const int32_t kp = (int32_t)(m < 1024 ? m : 1024);
@@ -1394,6 +1421,7 @@ int gp_topk_pruned_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, co
     int r2;
     if ((r2 = ensure(c, c->pr_kst, (size_t)npad * ldc))) return r2;
     if ((r2 = ensure(c, c->pr_vpart, (size_t)RT * ldc))) return r2;
+    if ((r2 = ensure(c, c->pr_mcol, (size_t)RT * ldc))) return r2;
     if ((r2 = ensure(c, c->pr_ucand, (size_t)(dpad > 0 ? dpad : 1) * ldc))) return r2;
     if ((r2 = ensure(c, c->pr_cnorm, (size_t)ldc))) return r2;
     if (dpad > 0)
@@ -1407,7 +1435,8 @@ int gp_topk_pruned_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, co
                          c->stream, c->bcat.p, ldk, idx, base, nc, ldc, c->pr_bcat.p);
     }
     UT_LAUNCH_CHECK(c);
-    return launch_gemm_kstar(c, 64, XsT, npad, c->pr_ucand.p, dpad, nc, c->pr_kst.p, ldc, nullptr, -1,
+    // (with the mean partials: the exact scores take k* . alpha of these columns)
+    return launch_gemm_kstar(c, 64, XsT, npad, c->pr_ucand.p, dpad, nc, c->pr_kst.p, ldc, c->pr_mcol.p, -1,
                              c->pr_cnorm.p, nullptr, cat ? kstar_cat(c, c->pr_bcat.p) : KstarCat(), xn);
   };
   const int64_t ldt = ((int64_t)kp + VAR_BN - 1) / VAR_BN * VAR_BN;
@@ -1416,7 +1445,7 @@ int gp_topk_pruned_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, co
                             c->pr_mpart.p)))
     return rc;
   hipLaunchKernelGGL(k_prune_exact, dim3(grid1(kp, 256)), dim3(256), 0, c->stream, (int64_t)kp, tset, cand_base, RT,
-                     c->pr_vpart.p, ldt, c->pr_mu.p, c->gp_sf2, c->gp_stats, c->gp_flag, acq->kind, acq->xi,
+                     c->pr_vpart.p, ldt, c->pr_mcol.p, c->gp_sf2, c->gp_stats, c->gp_flag, acq->kind, acq->xi,
                      acq->kappa, tex, nullptr);
   UT_LAUNCH_CHECK(c);
   int64_t* tk_i = out_idx;   // the caller's [k] outputs hold tau's top-k for now
@@ -1459,8 +1488,8 @@ int gp_topk_pruned_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, co
                                 c->pr_mpart.p)))
         return rc;
       hipLaunchKernelGGL(k_prune_exact, dim3(grid1(ns, 256)), dim3(256), 0, c->stream, ns, c->pr_idx.p, (int64_t)0,
-                         RT, c->pr_vpart.p, lds, c->pr_mu.p, c->gp_sf2, c->gp_stats, c->gp_flag, acq->kind, acq->xi,
-                         acq->kappa, nullptr, c->pr_score.p);
+                         RT, c->pr_vpart.p, lds, c->pr_mcol.p, c->gp_sf2, c->gp_stats, c->gp_flag, acq->kind,
+                         acq->xi, acq->kappa, nullptr, c->pr_score.p);
       UT_LAUNCH_CHECK(c);
     }
   }

@@ -386,15 +386,18 @@ int h3_kstar_exp(double sf2) { return H3_KSCALE_EXP - ilogb(sf2); }  // sf2 * 2^
 
 int launch_gemm_kstar(ut_ctx* c, int prec, const double* XsT, int32_t npad, const double* ucand, int32_t dpad,
                       int64_t m, void* kst, int64_t ldk, double* part, int32_t store_rows, const double* cn,
-                      double* part2, const KstarCat& cat, const double* xn) {
+                      double* part2, const KstarCat& cat, const double* xn, int32_t rows) {
   const bool has_cat = cat.nkc > 0;
+  UT_CHECK(c, rows < 0 || (rows > 0 && rows % K_BM == 0 && rows <= npad && !has_cat && part == nullptr), UT_EINVAL,
+           "gemm_kstar: bad row limit");
   UT_CHECK(c, npad % K_BM == 0 && dpad % 4 == 0 && (dpad >= 4 || has_cat) && ldk % K_BN == 0 && ldk >= m, UT_EINVAL,
            "gemm_kstar: bad padding");
   UT_CHECK(c, !has_cat || (cat.acat && cat.bcat), UT_EINVAL, "gemm_kstar: categorical operands missing");
   UT_CHECK(c, prec == 64 || prec == 32 || prec == 16, UT_EINVAL, "gemm_kstar: bad precision");
   UT_CHECK(c, part != nullptr || prec == 64, UT_EINVAL,
            "gemm_kstar: fp32 / h3 mode takes the mean partial here");
-  const int32_t RT = npad / K_BM;
+  // (a row limit computes the first rows / 128 row tiles; A keeps its npad stride)
+  const int32_t RT = (rows > 0 ? rows : npad) / K_BM;
   const int32_t CT = (int32_t)(ldk / K_BN);  // every column of K* (zeros past m) is written
   // fp64: only the first store_rows rows of K* are written (the mean still
   // sums every row); the other precisions always store everything

@@ -338,6 +338,9 @@ struct ut_ctx {
   bool pr_f2_valid = false;                    // pr_f2 belongs to the current fit
   ut::DevBuf<uint8_t> pr_exact;                // [ld] the stored score is the exact score
   ut::DevBuf<double> rel_up;                   // parent-relative K*: the parent's u' [64] and |x_r - u'_p|^2 [npad]
+  ut::DevBuf<double> pr_mcol;                  // recomputed columns' mean partials [RT][lds] (their exact scores)
+  ut::DevBuf<double> pr_a2;                    // [1] |alpha|^2 (+ block partials): the relative mean's slack
+  bool pr_a2_valid = false;
   bool rel_enable = true;                      // UT_KSTAR_REL=0: pruned rounds always take the dense K*
   int32_t rel_last = 0;                        // the last pruned call took the parent-relative K* (tests)
   int64_t r_ld = 0;
@@ -527,7 +530,8 @@ int launch_gemm_kstar(ut_ctx* c, int prec, const double* XsT, int32_t npad, cons
                       const double* cn = nullptr,    // candidate norms (nullptr: c->cnorm)
                       double* part2 = nullptr,       // fp64 with part: also sum_r k*_r^2 partials
                       const KstarCat& cat = KstarCat(),
-                      const double* xn = nullptr);   // training norms (nullptr: c->gp_xnorm)
+                      const double* xn = nullptr,    // training norms (nullptr: c->gp_xnorm)
+                      int32_t rows = -1);            // > 0: only the first `rows` rows of K* (a multiple of 128)
 int launch_prep_cand(ut_ctx* c, const double* feat, int64_t ld, int64_t m, int32_t d, int32_t dpad, double* u,
                      int64_t ldu, double* cn);
 // categorical K*: the K* operands of the candidate side when the fit is in
