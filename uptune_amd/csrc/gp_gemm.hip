@@ -153,17 +153,17 @@ __global__ __launch_bounds__(K_NT, 2) void k_gp_kstar(const double* __restrict__
   // as well, for the tail bound of the variance (gp.hip k_prune_bound)
   // TS = _Float16 (h3): k* * kscale split into fp16 hi + lo, stored candidate-major
   // in the blocked layout of k_gp_var_h3 (K = npad = RT * K_BM; ldk % 256 == 0);
-  // the lo plane starts lo_off elements after the hi plane
+  // the lo plane starts lo_off elements after the hi plane.  h3 permutes the
+  // tile's training rows over the MFMA rows, pi(rho) = 4 (rho & 3) + (rho >> 2),
+  // so that a lane's four accumulator rows (l >> 4) + 4 r hold the training
+  // rows 4 (l >> 4) + r: four consecutive k of one candidate, 8 contiguous bytes
+  // per plane in the blocked layout, stored straight from registers (round 3
+  // transposed the tile through LDS with 128 ds_write_b16 per lane per item)
   constexpr bool H3 = sizeof(TS) == 2;
   // one __shared__ object (see k_gp_var): the 2-stage ring, the exp table,
   // then the ticket slot
-  // h3: the epilogue transposes the tile through LDS, [plane][col][row] with a
-  // 264-B column pitch (2-way at worst on the ds_write_b16s), then stores whole
-  // 256-B candidate rows; the mean reduction sits after that image
-  constexpr int T_PITCH = K_BM + 4;                                  // fp16 elements
-  constexpr int T_DBL = H3 ? 2 * K_BN * T_PITCH * 2 / 8 : 0;          // image size in doubles
-  constexpr int RED_OFF = H3 ? T_DBL : 0;
-  constexpr int MAIN = H3 ? (T_DBL + 2 * K_BN > 2 * K_STAGE ? T_DBL + 2 * K_BN : 2 * K_STAGE) : 2 * K_STAGE;
+  constexpr int RED_OFF = 0;
+  constexpr int MAIN = 2 * K_STAGE;
   // + the item's epilogue operands, staged by glds with its first K stage:
   // |x_r|^2 and alpha_r of its 128 rows, |u_c|^2 of its 128 columns (read from
   // LDS in the epilogue instead of 16 + 16 + 4 doubles held in VGPRs per lane:
@@ -172,7 +172,6 @@ __global__ __launch_bounds__(K_NT, 2) void k_gp_kstar(const double* __restrict__
   double* etab = lds + MAIN;
   int32_t& s_item = *reinterpret_cast<int32_t*>(lds + MAIN + EXP_TAB);
   double* const rowop = lds + MAIN + EXP_TAB + 2;   // [xnorm 128][alpha 128][cnorm 128]
-  _Float16* timg = reinterpret_cast<_Float16*>(lds);
   const int t = threadIdx.x, lane = t & 63;
   // h3: the table carries the split's power-of-two scale, so ks below is
   // k* * kscale exactly (and the mean's alpha is divided by it: the product is
@@ -188,8 +187,10 @@ __global__ __launch_bounds__(K_NT, 2) void k_gp_kstar(const double* __restrict__
   const int32_t ncs = CAT ? nkc : 0;          // int8 stages first, then the fp64 ones
   const int32_t ntot = ncs + nk;
   const int npad_a = RT * K_BM;
-  // the i8 MFMA's row rho of A is tile row sigma(rho) (see above)
-  const int sig = ((lane & 15) >> 2) + 4 * (lane & 3);
+  // the i8 MFMA's row rho of A is tile row sigma(rho) (see above); h3: the
+  // f64 MFMA's row rho is tile row pi(rho), and the i8 one's row rho itself
+  const int sig = H3 ? (lane & 15) : ((lane & 15) >> 2) + 4 * (lane & 3);
+  const int arow = H3 ? 4 * (lane & 3) + ((lane & 15) >> 2) : (lane & 15);
   typedef kd4 d4;
 
   for (;;) {
@@ -280,7 +281,7 @@ __global__ __launch_bounds__(K_NT, 2) void k_gp_kstar(const double* __restrict__
         const int kr = ks * 4 + (lane >> 4);
         double af[4], bf[4];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) af[i] = as[kr * K_BM + wm * 64 + i * 16 + (lane & 15)];
+        for (int i = 0; i < 4; ++i) af[i] = as[kr * K_BM + wm * 64 + i * 16 + arow];
 #pragma unroll
         for (int jj = 0; jj < 4; ++jj) bf[jj] = bs[kr * K_BN + wn * 64 + jj * 16 + (lane & 15)];
 #pragma unroll
@@ -305,35 +306,57 @@ __global__ __launch_bounds__(K_NT, 2) void k_gp_kstar(const double* __restrict__
     }
     const bool want2 = !H3 && MU && part2 != nullptr;
     double s[4] = {0.0, 0.0, 0.0, 0.0}, s2[4] = {0.0, 0.0, 0.0, 0.0};
+    if constexpr (H3) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int rl = wm * 64 + i * 16 + (lane >> 4) + 4 * r;
-        const int32_t row = row0 + rl;
-        const double hx = row < n ? -0.5 * rowop[rl] : -1e300;
-        double al = 0.0;
-        if constexpr (MU) al = H3 ? rowop[K_BM + rl] * ikscale : rowop[K_BM + rl];
+      for (int i = 0; i < 4; ++i) {
+        // the four rows of this lane in row group i: training rows 4 (l >> 4) + r
+        const int rl0 = wm * 64 + i * 16 + 4 * (lane >> 4);
 #pragma unroll
         for (int jj = 0; jj < 4; ++jj) {
-          const int cl = wn * 64 + jj * 16 + (lane & 15);
-          const int64_t col = col0 + cl;
-          // -|x - u|^2 / 2 = C - |x|^2/2 - |u|^2/2, clamped to [-1000, 0]
-          const double x = __builtin_fmax(__builtin_fmin((acc[i][jj][r] + hx) + hc[jj], 0.0), -1000.0);
-          const double ks = sf2_exp_nonpos(x, etab);
-          if constexpr (H3) {
+          const int64_t col = col0 + wn * 64 + jj * 16 + (lane & 15);
+          uint32_t hpk[2] = {0u, 0u}, lpk[2] = {0u, 0u};   // the four rows' fp16 hi / lo, packed
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const double hx = row0 + rl0 + r < n ? -0.5 * rowop[rl0 + r] : -1e300;
+            const double x = __builtin_fmax(__builtin_fmin((acc[i][jj][r] + hx) + hc[jj], 0.0), -1000.0);
+            const double ks = sf2_exp_nonpos(x, etab);
             // ks = k* * kscale (< 2^15): hi = fp16(ks), lo = fp16 of the rest,
             // the rest taken in f32 (exact there: hi is within 2^-11 of xf)
             const float xf = (float)ks;
             const _Float16 hi = (_Float16)xf;
-            const int o = cl * T_PITCH + rl;
-            timg[o] = hi;
-            timg[K_BN * T_PITCH + o] = (_Float16)(xf - (float)hi);
-          } else {
-            if (rt < store_rt) kst[(int64_t)row * ldk + col] = (TS)ks;   // pruned scoring stores the bound rows only
+            const uint32_t hb = __builtin_bit_cast(uint16_t, hi);
+            const uint32_t lb = __builtin_bit_cast(uint16_t, (_Float16)(xf - (float)hi));
+            hpk[r >> 1] |= (r & 1) ? hb << 16 : hb;
+            lpk[r >> 1] |= (r & 1) ? lb << 16 : lb;
+            s[jj] += (rowop[K_BM + rl0 + r] * ikscale) * ks;
           }
-          if constexpr (MU) s[jj] += al * ks;
-          if constexpr (MU && !H3) s2[jj] += ks * ks;
+          // rows 4 (l >> 4) .. + 3 of this column: 8 bytes per plane in the blocked layout
+          const int64_t o = h3_blk_off(col, row0 + rl0, RT * K_BM);
+          *reinterpret_cast<uint2*>(kst + o) = make_uint2(hpk[0], hpk[1]);
+          *reinterpret_cast<uint2*>(kst + lo_off + o) = make_uint2(lpk[0], lpk[1]);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int rl = wm * 64 + i * 16 + (lane >> 4) + 4 * r;
+          const int32_t row = row0 + rl;
+          const double hx = row < n ? -0.5 * rowop[rl] : -1e300;
+          double al = 0.0;
+          if constexpr (MU) al = rowop[K_BM + rl];
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj) {
+            const int cl = wn * 64 + jj * 16 + (lane & 15);
+            const int64_t col = col0 + cl;
+            // -|x - u|^2 / 2 = C - |x|^2/2 - |u|^2/2, clamped to [-1000, 0]
+            const double x = __builtin_fmax(__builtin_fmin((acc[i][jj][r] + hx) + hc[jj], 0.0), -1000.0);
+            const double ks = sf2_exp_nonpos(x, etab);
+            if (rt < store_rt) kst[(int64_t)row * ldk + col] = (TS)ks;   // pruned scoring stores the bound rows only
+            if constexpr (MU) s[jj] += al * ks;
+            if constexpr (MU) s2[jj] += ks * ks;
+          }
         }
       }
     }
@@ -353,7 +376,7 @@ __global__ __launch_bounds__(K_NT, 2) void k_gp_kstar(const double* __restrict__
         }
       }
     }
-    if constexpr (MU || H3) __syncthreads();
+    if constexpr (MU) __syncthreads();
     if constexpr (MU) {
       if (t < K_BN) {
         const int64_t col = col0 + t;
@@ -361,22 +384,6 @@ __global__ __launch_bounds__(K_NT, 2) void k_gp_kstar(const double* __restrict__
           part[(int64_t)rt * ldk + col] = red[t] + red[K_BN + t];
           if (want2) part2[(int64_t)rt * ldk + col] = red[2 * K_BN + t] + red[3 * K_BN + t];
         }
-      }
-    }
-    if constexpr (H3) {
-      // into the blocked layout: a wave instruction stores 16 candidates' 64-B
-      // pieces of one 32-k block, 1 KiB contiguous (2 planes x 4 k-blocks x 8
-      // candidate groups = 64 instructions per tile)
-      const int32_t npad = RT * K_BM;
-      const int ch = lane & 3;
-#pragma unroll 4
-      for (int it = 0; it < 16; ++it) {
-        const int u = it * 4 + w;
-        const int pl = u >> 5, kb = (u >> 3) & 3, cl = (u & 7) * 16 + (lane >> 2);
-        const _Float16* src = timg + (pl * K_BN + cl) * T_PITCH + kb * 32 + ch * 8;
-        const uint2 v0 = *reinterpret_cast<const uint2*>(src), v1 = *reinterpret_cast<const uint2*>(src + 4);
-        *reinterpret_cast<uint4*>(kst + pl * lo_off + h3_blk_off(col0 + cl, row0 + kb * 32 + ch * 8, npad)) =
-            make_uint4(v0.x, v0.y, v1.x, v1.y);
       }
     }
   }
