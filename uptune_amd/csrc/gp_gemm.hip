@@ -193,12 +193,18 @@ __global__ __launch_bounds__(K_NT, 2) void k_gp_kstar(const double* __restrict__
   const int arow = H3 ? 4 * (lane & 3) + ((lane & 15) >> 2) : (lane & 15);
   typedef kd4 d4;
 
+  // the next item's ticket is taken at the start of the current one, so its
+  // atomic round trip overlaps the item's first K stage instead of sitting
+  // between two items (one ticket past the end per workgroup is drawn and unused)
+  int32_t nxt = 0;
+  if (t == 0) nxt = atomicAdd(&ticket[xcd], 1);
   for (;;) {
-    if (t == 0) s_item = atomicAdd(&ticket[xcd], 1);
+    if (t == 0) s_item = nxt;
     __syncthreads();
     const int32_t j = s_item;
     const int32_t ct = (j / RT) * 8 + xcd;
     if (ct >= CT) break;
+    if (t == 0) nxt = atomicAdd(&ticket[xcd], 1);
     const int32_t rt = j % RT;
     const int64_t col0 = (int64_t)ct * K_BN;
     const int32_t row0 = rt * K_BM;
