@@ -968,7 +968,9 @@ def test_gp_topk_pruned_parent_relative(space_name, d_used, m, n):
     # MFMA K* of their recomputed columns, as on the path without a reference
     np.testing.assert_array_equal(i_rel.cpu().numpy(), i_mf.cpu().numpy())
     _close(t_rel.cpu().numpy(), t_mf.cpu().numpy(), rtol=1e-13, atol=0.0)
-    _close(t_rel.cpu().numpy(), t_d.cpu().numpy(), rtol=1e-9, atol=1e-12)
+    # against the dense scoring: mu = k* . alpha here, (L^-1 k*) . (L^-1 y) there,
+    # two roundings of an ill-conditioned sum (n = 333, sigma_n^2 = 1e-6)
+    _close(t_rel.cpu().numpy(), t_d.cpu().numpy(), rtol=1e-7, atol=1e-12)
     g = ogp.GP(Xtr, y, lengthscale=0.5, sigma_f2=1.0, sigma_n2=1e-6, jitter=1e-8)
     mu, var = g.posterior(features(space, vals.cpu().numpy()).T)
     sc = ogp.acquisition(mu, var, g.f_best)
