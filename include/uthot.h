@@ -293,26 +293,10 @@ typedef struct ut_prune_stats {
   int32_t bound_rows;    /* rows of L^-1 k* in the bound (a multiple of 128) */
   int32_t dense;         /* 1: too many survivors, the round ran the dense variance instead */
   double threshold;      /* tau */
-  int32_t relative;      /* 1: K* came from the parent-relative kernel (ut_gp_topk_pruned_ref) */
-  int32_t pad;
 } ut_prune_stats;
 int ut_gp_topk_pruned(ut_ctx* ctx, const double* features, int64_t ld, int64_t m, const ut_acq* acq,
                       const uint8_t* dup, int64_t cand_base, int32_t k, int32_t bound_rows, int64_t* out_idx,
                       double* out_score, ut_prune_stats* stats_host);
-/* the same selection for a pool whose candidates mostly differ from ONE
- * reference configuration in a few features -- a GA / GGA round's children of
- * its parent (evolutionarytechniques.py:29-61: GreedySelectionMixin's best
- * config, mutation rate 0.1).  ref_features: the reference's features [d]
- * (device, the same encoding as `features`).  K* is then formed as
- * |u - x|^2 = |p - x|^2 + sum over the changed features of (u_j - p_j)(u_j + p_j - 2 x_j)
- * on the VALU (fp64) instead of the K = d contraction (d <= 64; a child with
- * more than 16 changed features takes the direct sum); any other shape, or
- * UT_KSTAR_REL=0, takes ut_gp_topk_pruned's path.  The selection is the same
- * (scores equal to fp64 rounding). */
-int ut_gp_topk_pruned_ref(ut_ctx* ctx, const double* features, int64_t ld, int64_t m, const ut_acq* acq,
-                          const uint8_t* dup, int64_t cand_base, int32_t k, int32_t bound_rows,
-                          const double* ref_features, int64_t* out_idx, double* out_score,
-                          ut_prune_stats* stats_host);
 /* arithmetic of the two scoring contractions (K* and L^-1 K*^T) for fits made
  * after this call: 64 = fp64 MFMA (default; 1e-5 parity), 32 = fp32 MFMA
  * (1e-3 parity), 16 = "f16x3": K* in fp64, the variance contraction as three

@@ -926,84 +926,6 @@ def test_gp_topk_pruned_equals_dense(acq, bound_rows):
         assert idx.cpu().numpy().tolist() == i2.cpu().numpy().tolist() == want
 
 
-@pytest.mark.parametrize("space_name,d_used,m,n", [("r64", 64, 20000, 1000), ("mixed", None, 7777, 333),
-                                                   ("r64", 64, 4096, 4096)])
-def test_gp_topk_pruned_parent_relative(space_name, d_used, m, n):
-    """ut_gp_topk_pruned_ref: GA children of one parent (mutation 0.1, so most
-    change a few features; some many, which take the direct sum), with the
-    training set around the parent and the parent's features as the reference.
-    The parent-relative K* gives the selection and the scores of the MFMA K*
-    path (ut_gp_topk_pruned: the same survivors' exact scores), the dense
-    top-k and the oracle's; ragged m and n (padded columns and rows), a
-    reference that is not a child's parent (random candidates: every candidate
-    takes the direct sum) and UT_KSTAR_REL=0"""
-    _require_gpu()
-    space = r64_space() if space_name == "r64" else mixed_space()
-    e = engine(space, seed=21)
-    F = e.spec.n_features
-    if F > 64:
-        pytest.skip("the parent-relative K* takes d <= 64")
-    pop = ode.population_init(space, max(n, 64), seed=5)
-    parent = pop[:, 3].copy()
-    kids, _ = e.propose_ga(n, parent1=parent, mutation_rate=0.1, round_=1)
-    Xtr = features(space, kids.cpu().numpy()).T
-    rng = np.random.default_rng(6)
-    y = np.sum((Xtr - 0.45) ** 2, axis=1) + 0.01 * rng.standard_normal(n)
-    e.gp_fit(Xtr, y, lengthscale=0.5, sigma_f2=1.0, sigma_n2=1e-6, jitter=1e-8)
-    vals, _ = e.propose_ga(m, parent1=parent, mutation_rate=0.1, round_=2)
-    feat = e.encode(vals)
-    ref = e.encode(dev(parent.reshape(-1, 1)))[:, 0]
-    dup = torch.zeros(m, dtype=torch.uint8, device="cuda")
-    dup[::89] = 1
-    a = e.acq("ei", xi=0.0)
-    k = 32
-    i_rel, t_rel, st = e.gp_topk_pruned(feat, k, acq=a, dup=dup, cand_base=7, bound_rows=256, ref=ref)
-    assert st["relative"], st
-    i_mf, t_mf, st2 = e.gp_topk_pruned(feat, k, acq=a, dup=dup, cand_base=7, bound_rows=256)
-    assert not st2["relative"]
-    _, _, score = e.gp_score(feat, acq=a, dup=dup)
-    i_d, t_d = e.topk(score, k, dup=dup, cand_base=7)
-    # the relative K* only decides which candidates survive (its mean and the
-    # bound carry a rounding slack); the survivors' exact scores come from the
-    # MFMA K* of their recomputed columns, as on the path without a reference
-    np.testing.assert_array_equal(i_rel.cpu().numpy(), i_mf.cpu().numpy())
-    _close(t_rel.cpu().numpy(), t_mf.cpu().numpy(), rtol=1e-13, atol=0.0)
-    # against the dense scoring: mu = k* . alpha here, (L^-1 k*) . (L^-1 y) there,
-    # two roundings of an ill-conditioned sum (n = 333, sigma_n^2 = 1e-6)
-    _close(t_rel.cpu().numpy(), t_d.cpu().numpy(), rtol=1e-7, atol=1e-12)
-    g = ogp.GP(Xtr, y, lengthscale=0.5, sigma_f2=1.0, sigma_n2=1e-6, jitter=1e-8)
-    mu, var = g.posterior(features(space, vals.cpu().numpy()).T)
-    sc = ogp.acquisition(mu, var, g.f_best)
-    sc = np.where(dup.cpu().numpy() != 0, -np.inf, sc)
-    want = [7 + i for i in sorted(range(m), key=lambda i: (-sc[i], i))[:k]]
-    gaps = np.abs(np.diff(np.sort(sc[np.isfinite(sc)])[::-1][:k + 1]))
-    if gaps.min() > 1e-9:
-        assert i_rel.cpu().numpy().tolist() == i_mf.cpu().numpy().tolist() == i_d.cpu().numpy().tolist() == want
-    # random candidates against the same reference: every one takes the direct sum
-    rnd = dev(ode.population_init(space, 3000, seed=9))
-    fr = e.encode(rnd)
-    i_r, t_r, st3 = e.gp_topk_pruned(fr, 16, acq=a, bound_rows=128, ref=ref)
-    i_r2, t_r2, _ = e.gp_topk_pruned(fr, 16, acq=a, bound_rows=128)
-    assert st3["relative"]
-    np.testing.assert_array_equal(i_r.cpu().numpy(), i_r2.cpu().numpy())
-    _close(t_r.cpu().numpy(), t_r2.cpu().numpy(), rtol=1e-13, atol=0.0)
-    e.close()
-    old = os.environ.get("UT_KSTAR_REL")
-    os.environ["UT_KSTAR_REL"] = "0"
-    try:
-        e2 = engine(space, seed=21)
-        e2.gp_fit(Xtr, y, lengthscale=0.5, sigma_f2=1.0, sigma_n2=1e-6, jitter=1e-8)
-        _, t_off, st4 = e2.gp_topk_pruned(feat, k, acq=a, dup=dup, cand_base=7, bound_rows=256, ref=ref)
-        assert not st4["relative"]
-        _close(t_off.cpu().numpy(), t_mf.cpu().numpy(), rtol=1e-12, atol=1e-15)
-        e2.close()
-    finally:
-        if old is None:
-            os.environ.pop("UT_KSTAR_REL", None)
-        else:
-            os.environ["UT_KSTAR_REL"] = old
-
-
 def test_gp_topk_pruned_degenerate_exact_ties():
     """far-away candidates (k* ~ 0 everywhere): every score is the same.  The
     tail bound |L^-1|_F^2 |k*|^2 proves each candidate's variance from the first
@@ -1252,58 +1174,6 @@ def test_chol_fused_refit_bitwise_and_not_pd():
             os.environ.pop("UT_CHOL_FUSE", None)
         else:
             os.environ["UT_CHOL_FUSE"] = old
-
-
-@pytest.mark.parametrize("prec", [64, 32, 16])
-def test_early_alpha_equals_inverse_products(prec):
-    """alpha = K^-1 y and beta = L^-1 y by the triangular solves that ride on
-    the refit's panel steps (UT_EARLY_ALPHA=1, the default: scoring that takes
-    the mean in K* starts before the recursive inverse) against the products
-    with L^-1 (UT_EARLY_ALPHA=0): the posterior agrees to fp64 rounding, and
-    both to the oracle; the pruned top-k is the same selection"""
-    _require_gpu()
-    rng = np.random.default_rng(43)
-    n, d = 1500, 8
-    X = rng.uniform(size=(n, d))
-    y = np.sin(3 * X[:, 0]) + np.sum((X - 0.4) ** 2, axis=1)
-    U = np.ascontiguousarray(rng.uniform(size=(d, 5000)))
-    U[:, :4] = X[:4].T
-    space = [Param("f%d" % i, FLOAT, 0.0, 1.0) for i in range(d)]
-    old = os.environ.get("UT_EARLY_ALPHA")
-    outs, sels = [], []
-    try:
-        for early in ("0", "1"):
-            os.environ["UT_EARLY_ALPHA"] = early
-            e = engine(space, seed=2)
-            e.gp_set_precision(prec)
-            e.gp_fit(X, y, lengthscale=0.3, sigma_f2=1.0, sigma_n2=1e-6, jitter=1e-8, wait=False)
-            Ud = torch.from_numpy(U).cuda()
-            outs.append([t.cpu().numpy() for t in e.gp_score(Ud, acq=e.acq("ei"))])
-            if prec == 64:
-                e.gp_fit(X[:1400], y[:1400], lengthscale=0.3, sigma_f2=1.0, sigma_n2=1e-6, jitter=1e-8, wait=False)
-                idx, sc, _ = e.gp_topk_pruned(Ud, 16, acq=e.acq("ei"), bound_rows=256)
-                sels.append(idx.cpu().numpy())
-            e.close()
-    finally:
-        if old is None:
-            os.environ.pop("UT_EARLY_ALPHA", None)
-        else:
-            os.environ["UT_EARLY_ALPHA"] = old
-    (mu0, var0, ei0), (mu1, var1, ei1) = outs
-    assert np.array_equal(var0, var1)          # the variance reads L^-1 only
-    np.testing.assert_allclose(mu1, mu0, rtol=1e-9, atol=1e-12)
-    np.testing.assert_allclose(ei1, ei0, rtol=1e-9, atol=1e-12)
-    g = ogp.GP(X, y, lengthscale=0.3, sigma_f2=1.0, sigma_n2=1e-6, jitter=1e-8)
-    mu_o, var_o = g.posterior(U.T)
-    ei_o = ogp.acquisition(mu_o, var_o, g.f_best)
-    _close(mu1, mu_o)                          # the mean is fp64 in every tier
-    if prec == 64:
-        _close(var1, var_o, atol=1e-8)
-        _close(ei1, ei_o, atol=1e-8)
-        assert (sels[0] == sels[1]).all()
-    else:
-        _close(var1, var_o, rtol=1e-3, atol=1e-5)
-        _close(ei1, ei_o, rtol=1e-3, atol=1e-5)
 
 
 @pytest.mark.parametrize("which", ["hpl", "gcc", "mixed", "perm"])

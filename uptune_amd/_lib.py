@@ -54,8 +54,7 @@ class DeParams(C.Structure):
 
 
 class PruneStats(C.Structure):
-    _fields_ = [("survivors", C.c_int64), ("bound_rows", C.c_int32), ("dense", C.c_int32), ("threshold", C.c_double),
-                ("relative", C.c_int32), ("pad", C.c_int32)]
+    _fields_ = [("survivors", C.c_int64), ("bound_rows", C.c_int32), ("dense", C.c_int32), ("threshold", C.c_double)]
 
 
 class PsoParams(C.Structure):
@@ -107,8 +106,6 @@ SIGNATURES = {
     "ut_score_round_de_pruned": (C.c_int, [P, C.POINTER(DeParams), C.POINTER(Acq), U32, I64, I64, I32, I32,
                                            C.POINTER(RoundOut), C.POINTER(PruneStats)]),
     "ut_gp_topk_pruned": (C.c_int, [P, P, I64, I64, C.POINTER(Acq), P, I64, I32, I32, P, P, C.POINTER(PruneStats)]),
-    "ut_gp_topk_pruned_ref": (C.c_int, [P, P, I64, I64, C.POINTER(Acq), P, I64, I32, I32, P, P, P,
-                                        C.POINTER(PruneStats)]),
     "ut_hash_de": (C.c_int, [P, P, I64, I64, I64, P]),
     "ut_hash_parent": (C.c_int, [P, P, I64, I64, P, P]),
     "ut_propose_de": (C.c_int, [P, C.POINTER(DeParams), U32, I64, I64, P, I64]),

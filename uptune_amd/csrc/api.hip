@@ -221,7 +221,6 @@ int ut_ctx_create(int device, uint64_t seed, ut_ctx** out) {
       hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_fit, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&c->ev_alpha, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_prefit, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_fit_x, hipEventDisableTiming) != hipSuccess) {
     ut_ctx_destroy(c);
@@ -235,8 +234,6 @@ int ut_ctx_create(int device, uint64_t seed, ut_ctx** out) {
   if (const char* e = getenv("UT_FIT_APPEND")) c->fit_append = atoi(e) != 0;
   if (const char* e = getenv("UT_DE_AOS")) c->de_aos = atoi(e) != 0;
   if (const char* e = getenv("UT_HASH_AFTER_FIT")) c->hash_after_fit = atoi(e);
-  if (const char* e = getenv("UT_EARLY_ALPHA")) c->early_alpha = atoi(e) != 0;
-  if (const char* e = getenv("UT_KSTAR_REL")) c->rel_enable = atoi(e) != 0;
   if (const char* e = getenv("UT_HASH_HOLD_LOWPREC")) c->hash_hold_lowprec = atoi(e) != 0;
   if (const char* e = getenv("UT_HASH_AFTER_KSTAR")) c->hash_after_kstar = atoi(e);
   if (const char* e = getenv("UT_H3_SCHED")) c->h3_sched = atoi(e);
@@ -277,7 +274,7 @@ int ut_ctx_destroy(ut_ctx* c) {
   fr(c->forest_nodes); fr(c->forest_roots); fr(c->r_topk_vals.p);
   fr(c->cm_send.p); fr(c->cm_recv.p); fr(c->cm_keep.p); fr(c->cm_pay.p); fr(c->cm_cnt.p);
   for (auto& m : c->timing.marks) hipEventDestroy(m.ev);
-  for (hipEvent_t e : {c->ev_fork, c->ev_join, c->ev_fit, c->ev_prefit, c->ev_fit_x, c->ev_alpha})
+  for (hipEvent_t e : {c->ev_fork, c->ev_join, c->ev_fit, c->ev_prefit, c->ev_fit_x})
     if (e) hipEventDestroy(e);
   if (c->fit_host) hipHostFree(c->fit_host);
   if (c->flag_host) hipHostFree(c->flag_host);
@@ -780,20 +777,6 @@ int ut_gp_topk_pruned(ut_ctx* c, const double* feat, int64_t ld, int64_t m, cons
   const bool own = c->timing.on && !c->timing.in_round;
   if (own) timing_begin(c);
   int rc = gp_topk_pruned_impl(c, feat, ld, m, acq, dup, cand_base, k, bound_rows, out_idx, out_score, stats);
-  if (own) timing_end(c);
-  return rc;
-}
-
-int ut_gp_topk_pruned_ref(ut_ctx* c, const double* feat, int64_t ld, int64_t m, const ut_acq* acq,
-                          const uint8_t* dup, int64_t cand_base, int32_t k, int32_t bound_rows,
-                          const double* ref_feat, int64_t* out_idx, double* out_score, ut_prune_stats* stats) {
-  if (!c) return UT_EINVAL;
-  UT_CHECK(c, m >= 1 && feat && ld >= m && acq && out_idx && out_score && cand_base >= 0 && ref_feat, UT_EINVAL,
-           "gp_topk_pruned_ref: bad arguments");
-  const bool own = c->timing.on && !c->timing.in_round;
-  if (own) timing_begin(c);
-  int rc = gp_topk_pruned_impl(c, feat, ld, m, acq, dup, cand_base, k, bound_rows, out_idx, out_score, stats, nullptr,
-                               false, ref_feat);
   if (own) timing_end(c);
   return rc;
 }

@@ -267,34 +267,12 @@ __global__ __launch_bounds__(256) void k_chol_diag(double* __restrict__ K, doubl
   chol_diag_core(a, K, Li, npad, kb, flag, col, Ls, invd);
 }
 
-// w_kb = inv(L_kk) yw_kb: thread t < 64 of the calling workgroup, row t
-__device__ __forceinline__ double fwd_block(const double* __restrict__ Li, int32_t npad, int64_t base,
-                                           const double* __restrict__ yw, int t) {
-  const double* li = Li + (base + t) * npad + base;
-  double s = 0.0;
-  for (int c = 0; c <= t; ++c) s = __builtin_fma(li[c], yw[base + c], s);
-  return s;
-}
-
-// Panel kb, step 2: row block i > kb:  L_ik = A_ik * inv(L_kk)^T  (NT product).
-// yw != NULL: the forward solve L beta = y rides along (the right-looking
-// update of an extra column): every workgroup forms w_kb = inv(L_kk) yw_kb
-// (yw_kb is final: blocks <= kb are not written in this launch), workgroup 0
-// stores it as beta_kb, and each updates its own block, yw_i -= L_ik w_kb.
+// Panel kb, step 2: row block i > kb:  L_ik = A_ik * inv(L_kk)^T  (NT product)
 __global__ __launch_bounds__(256) void k_chol_rows(double* __restrict__ K, const double* __restrict__ Li,
-                                                   int32_t npad, int32_t kb, double* __restrict__ yw,
-                                                   double* __restrict__ beta) {
+                                                   int32_t npad, int32_t kb) {
   __shared__ double As[16 * 80];
   __shared__ double Bs[16 * 80];
-  __shared__ double Lt[NB * (NB + 1)];
-  __shared__ double wv[NB];
   const int64_t base = (int64_t)kb * NB, rb = (int64_t)(kb + 1 + blockIdx.x) * NB;
-  const int t = threadIdx.x;
-  if (yw && t < NB) {
-    const double w = fwd_block(Li, npad, base, yw, t);
-    wv[t] = w;
-    if (blockIdx.x == 0) beta[base + t] = w;
-  }
   fd4 acc[2][2];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -306,46 +284,7 @@ __global__ __launch_bounds__(256) void k_chol_rows(double* __restrict__ K, const
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        K[(rb + tile_row(i, r)) * npad + base + tile_col(j)] = acc[i][j][r];
-        if (yw) Lt[tile_row(i, r) * (NB + 1) + tile_col(j)] = acc[i][j][r];
-      }
-  if (!yw) return;
-  __syncthreads();
-  if (t < NB) {
-    double s = 0.0;
-    for (int c = 0; c < NB; ++c) s = __builtin_fma(Lt[t * (NB + 1) + c], wv[c], s);
-    yw[rb + t] -= s;
-  }
-}
-
-// the forward solve's last block (no row block below it): beta_kb = inv(L_kk) yw_kb
-__global__ __launch_bounds__(64) void k_fwd_last(const double* __restrict__ Li, int32_t npad, int32_t kb,
-                                                 const double* __restrict__ yw, double* __restrict__ beta) {
-  const int64_t base = (int64_t)kb * NB;
-  beta[base + threadIdx.x] = fwd_block(Li, npad, base, yw, threadIdx.x);
-}
-
-// Backward solve L^T alpha = beta, right-looking from the last block: launch b
-// forms alpha_b = inv(L_bb)^T z_b (z_b final: only blocks < b are written
-// here), workgroup 0 stores it, and workgroup c < b updates its block,
-// z_c -= L_bc^T alpha_b (row r of L_bc read coalesced).  z starts as beta.
-__global__ __launch_bounds__(64) void k_bwd_step(const double* __restrict__ L, const double* __restrict__ Li,
-                                                 int32_t npad, int32_t b, double* __restrict__ z,
-                                                 double* __restrict__ alpha) {
-  __shared__ double av[NB];
-  const int t = threadIdx.x;
-  const int64_t bb = (int64_t)b * NB;
-  double s = 0.0;
-  for (int j = t; j < NB; ++j) s = __builtin_fma(Li[(bb + j) * npad + bb + t], z[bb + j], s);
-  av[t] = s;
-  if (blockIdx.x == 0) alpha[bb + t] = s;
-  if (b == 0) return;
-  __syncthreads();
-  const int64_t cb = (int64_t)blockIdx.x * NB;
-  double u = 0.0;
-  for (int r = 0; r < NB; ++r) u = __builtin_fma(L[(bb + r) * npad + cb + t], av[r], u);
-  z[cb + t] -= u;
+      for (int r = 0; r < 4; ++r) K[(rb + tile_row(i, r)) * npad + base + tile_col(j)] = acc[i][j][r];
 }
 
 // Trailing update A_ij -= L_i,kb L_j,kb^T for kb < j <= i < nb.
@@ -830,7 +769,6 @@ int gp_fit_enqueue(ut_ctx* c, const double* X, const double* y, int32_t n, int32
   int rc = gp_alloc(c, npad, d);
   if (rc) return rc;
   c->pr_f2_valid = false;   // |L^-1|_F^2 (pruned scoring) belongs to the previous factor
-  c->pr_a2_valid = false;   // |alpha|^2 too
   const size_t need = (size_t)n * d + n + d;
   bool fresh = false;   // a new staging buffer holds no previous rows
   if (c->fit_host_n < need) {
@@ -951,21 +889,13 @@ int gp_fit_enqueue(ut_ctx* c, const double* X, const double* y, int32_t n, int32
     const int32_t nb = npad / NB;
     UT_HIP(c, hipMemsetAsync(c->gp_Linv, 0, sizeof(double) * npad * npad, c->stream));
     const bool fuse = c->chol_fuse > 0 || (c->chol_fuse < 0 && npad >= 2048);
-    // early alpha: beta = L^-1 y by a forward solve riding on the panel steps
-    // and alpha = L^-T beta by a backward solve, both before the inverse, so
-    // the scoring that takes the mean in K* (pruned, fp32, f16x3) starts at
-    // ev_alpha while the recursive inverse is still running.  The work vector
-    // is the inverse's scratch (gp_T), free until then.
-    double* yw = c->early_alpha ? c->gp_T : nullptr;
-    if (yw) UT_HIP(c, hipMemcpyAsync(yw, c->gp_y, sizeof(double) * npad, hipMemcpyDeviceToDevice, c->stream));
     for (int32_t kb = 0; kb < nb; ++kb) {
       // (fused: diagonal blocks after the first come from the previous update)
       if (!fuse || kb == 0)
         hipLaunchKernelGGL(k_chol_diag, dim3(1), dim3(256), 0, c->stream, c->gp_K, c->gp_Linv, npad, kb, c->gp_flag);
       const int32_t T = nb - kb - 1;
       if (T > 0) {
-        hipLaunchKernelGGL(k_chol_rows, dim3(T), dim3(256), 0, c->stream, c->gp_K, c->gp_Linv, npad, kb, yw,
-                           c->gp_beta);
+        hipLaunchKernelGGL(k_chol_rows, dim3(T), dim3(256), 0, c->stream, c->gp_K, c->gp_Linv, npad, kb);
         if (fuse)
           hipLaunchKernelGGL(k_chol_update_diag, dim3(T * (T + 1) / 2), dim3(256), 0, c->stream, c->gp_K, c->gp_Linv,
                              npad, kb, c->gp_flag);
@@ -973,15 +903,7 @@ int gp_fit_enqueue(ut_ctx* c, const double* X, const double* y, int32_t n, int32
           hipLaunchKernelGGL(k_chol_update, dim3(T * (T + 1) / 2), dim3(256), 0, c->stream, c->gp_K, npad, kb);
       }
     }
-    if (yw) {
-      hipLaunchKernelGGL(k_fwd_last, dim3(1), dim3(64), 0, c->stream, c->gp_Linv, npad, nb - 1, yw, c->gp_beta);
-      UT_HIP(c, hipMemcpyAsync(yw, c->gp_beta, sizeof(double) * npad, hipMemcpyDeviceToDevice, c->stream));
-      for (int32_t b = nb - 1; b >= 0; --b)
-        hipLaunchKernelGGL(k_bwd_step, dim3(b > 0 ? b : 1), dim3(64), 0, c->stream, c->gp_K, c->gp_Linv, npad, b, yw,
-                           c->gp_alpha);
-    }
     UT_LAUNCH_CHECK(c);
-    UT_HIP(c, hipEventRecord(c->ev_alpha, c->stream));
     // off-diagonal blocks of L^-1 by recursive doubling (diagonal blocks came from k_chol_diag)
     for (int32_t lv = NB; lv < npad; lv *= 2) {
       const int32_t pairs = (int32_t)((npad - lv + 2 * lv - 1) / (2 * lv));
@@ -991,23 +913,17 @@ int gp_fit_enqueue(ut_ctx* c, const double* X, const double* y, int32_t n, int32
     }
     UT_LAUNCH_CHECK(c);
   }
-  const bool solved = !app && c->early_alpha;   // beta and alpha came from the solves above
-  if (!solved) {
-    hipLaunchKernelGGL(k_lower_mv, dim3(grid1(npad, 4)), dim3(256), 0, c->stream, c->gp_Linv, npad, c->gp_y,
-                       c->gp_beta);
-    UT_LAUNCH_CHECK(c);
-  }
+  hipLaunchKernelGGL(k_lower_mv, dim3(grid1(npad, 4)), dim3(256), 0, c->stream, c->gp_Linv, npad, c->gp_y,
+                     c->gp_beta);
+  UT_LAUNCH_CHECK(c);
   if (c->gp_prec == 32 && (rc = launch_to_f32(c, c->gp_Xs, c->gp_Xs_f, (int64_t)npad * d))) return rc;
   // (an append wrote its rows of LinvT itself)
   if ((!app || c->gp_prec == 32) &&
       (rc = launch_transpose(c, c->gp_Linv, npad, c->gp_LinvT, c->gp_prec == 32 ? c->gp_LinvT_f : nullptr)))
     return rc;
-  if (!solved) {
-    hipLaunchKernelGGL(k_upper_mv, dim3(grid1(npad, 4)), dim3(256), 0, c->stream, c->gp_LinvT, npad, c->gp_beta,
-                       c->gp_alpha);
-    UT_LAUNCH_CHECK(c);
-    UT_HIP(c, hipEventRecord(c->ev_alpha, c->stream));
-  }
+  hipLaunchKernelGGL(k_upper_mv, dim3(grid1(npad, 4)), dim3(256), 0, c->stream, c->gp_LinvT, npad, c->gp_beta,
+                     c->gp_alpha);
+  UT_LAUNCH_CHECK(c);
   if (c->gp_prec == 16 && (rc = launch_split_h3(c, c->gp_Linv, npad, reinterpret_cast<_Float16*>(c->gp_LinvT_f))))
     return rc;
   c->gp_fit_prec = c->gp_prec;
@@ -1082,7 +998,7 @@ int gp_score_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, const ut
   // overlaps the rest of an asynchronous fit and only the variance GEMM waits
   // for L^-1.  fp32 keeps the mean in K*'s fp64 epilogue (k* . alpha, before
   // k* is rounded to fp32) and waits for the whole fit.
-  if (c->fit_pending) UT_HIP(c, hipStreamWaitEvent(c->stream, fp32 ? c->ev_alpha : c->ev_fit_x, 0));
+  if (c->fit_pending) UT_HIP(c, hipStreamWaitEvent(c->stream, fp32 ? c->ev_fit : c->ev_fit_x, 0));
   const int32_t n = c->gp_n, d = c->gp_d;
   const int32_t npad = ((n + NPAD - 1) / NPAD) * NPAD;
   // the categorical K* when the candidates came through ut's encoder
@@ -1111,7 +1027,7 @@ int gp_score_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, const ut
     return rc;
   mark(c, "kstar");
   if (mid && (rc = mid())) return rc;
-  if (c->fit_pending) UT_HIP(c, hipStreamWaitEvent(c->stream, c->ev_fit, 0));
+  if (c->fit_pending && !fp32) UT_HIP(c, hipStreamWaitEvent(c->stream, c->ev_fit, 0));
   if (dup_ready && c->join_before_var && var_joins) UT_HIP(c, hipStreamWaitEvent(c->stream, dup_ready, 0));
   mark(c, "");  // the wait for the fit is not variance time
   if ((rc = launch_gemm_var(c, prec, fp32 ? (const void*)c->gp_LinvT_f : (const void*)c->gp_LinvT, npad, c->kst.p,
@@ -1155,15 +1071,12 @@ int gp_score_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, const ut
 //   the exact var IS var_ub, and so is the exact score: it is stored without
 //   the margin and flagged exact, and ties with it can be broken by index
 //   (a flat GP -- every k* ~ 0 -- gives every candidate the same score).
-// RTm mean / |k*|^2 partials per candidate (RT from the MFMA K*, 1 from the
-// parent-relative one), RTv row tiles in the bound, RTall row tiles in all
-__global__ void k_prune_bound(int64_t m, int32_t RTm, int32_t RTall, const double* __restrict__ mu_part, int32_t RTv,
+__global__ void k_prune_bound(int64_t m, int32_t RTm, const double* __restrict__ mu_part, int32_t RTv,
                               const double* __restrict__ var_part, int64_t ldp, double sf2,
                               const double* __restrict__ stats, const int32_t* __restrict__ fit_flag, int32_t kind,
                               double xi, double kappa, const uint8_t* __restrict__ dup, double* __restrict__ mu_out,
                               double* __restrict__ ub_out, const double* __restrict__ k2_part,
-                              const double* __restrict__ linv_f2, uint8_t* __restrict__ exact_out,
-                              const double* __restrict__ alpha2) {
+                              const double* __restrict__ linv_f2, uint8_t* __restrict__ exact_out) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= m) return;
   double mu = 0.0, vs = 0.0, k2 = 0.0;
@@ -1171,24 +1084,16 @@ __global__ void k_prune_bound(int64_t m, int32_t RTm, int32_t RTall, const doubl
   for (int32_t r = 0; r < RTv; ++r) vs += var_part[(int64_t)r * ldp + i];
   double var = sf2 - vs;
   var = var > 0.0 ? var : 0.0;
-  if (k2_part)
-    for (int32_t r = 0; r < RTm; ++r) k2 += k2_part[(int64_t)r * ldp + i];
-  // alpha2 (the parent-relative K*): mu came from other arithmetic than the
-  // exact scores' (the MFMA K* of the recomputed columns), so the bound takes
-  // mu - dmu, dmu = 2e-11 |alpha| |k*| >= 20x the rounding of either form
-  // (sum_r |alpha_r| k*_r <= |alpha| |k*|; both scores decrease with mu)
-  const double dmu = alpha2 ? 2e-11 * sqrt(*alpha2 * k2) : 0.0;
-  double ub = acq_score(kind, mu - dmu, var, stats[0], xi, kappa);
+  double ub = acq_score(kind, mu, var, stats[0], xi, kappa);
   bool exact = false;
-  if (alpha2) {
-    exact = false;   // the stored bound is not the exact score
-  } else if (k2_part && RTv < RTall) {
+  if (k2_part && RTv < RTm) {
+    for (int32_t r = 0; r < RTm; ++r) k2 += k2_part[(int64_t)r * ldp + i];
     const double tail = 1.001 * (*linv_f2) * k2;
     const double s_hi = (vs + tail) * (1.0 + 0x1p-40);
     double var_lo = sf2 - s_hi;
     var_lo = var_lo > 0.0 ? var_lo : 0.0;
     exact = tail == tail && var_lo == var;   // (NaN tail: not exact)
-  } else if (RTv >= RTall) {
+  } else if (RTv >= RTm) {
     exact = true;   // the bound GEMM covered every row
   }
   if (!exact) ub = ub + fabs(ub) * 1e-12 + 1e-300;
@@ -1257,10 +1162,8 @@ __global__ void k_gather_cols(const double* __restrict__ kst, int64_t ldk, const
 }
 
 // exact scores of the gathered candidates: compact[j], and scattered to full[idx[j]]
-// mean: sum of the recomputed columns' partials mcol [RT][ldp] (the MFMA K*'s
-// k* . alpha, the same arithmetic as the unpruned pruned-K*'s)
 __global__ void k_prune_exact(int64_t n, const int64_t* __restrict__ idx, int64_t base, int32_t RT,
-                              const double* __restrict__ var_part, int64_t ldp, const double* __restrict__ mcol,
+                              const double* __restrict__ var_part, int64_t ldp, const double* __restrict__ mu_full,
                               double sf2, const double* __restrict__ stats, const int32_t* __restrict__ fit_flag,
                               int32_t kind, double xi, double kappa, double* __restrict__ compact,
                               double* __restrict__ full) {
@@ -1271,12 +1174,11 @@ __global__ void k_prune_exact(int64_t n, const int64_t* __restrict__ idx, int64_
     if (compact) compact[j] = -1.0 / 0.0;
     return;
   }
-  double vs = 0.0, mu = 0.0;
+  double vs = 0.0;
   for (int32_t r = 0; r < RT; ++r) vs += var_part[(int64_t)r * ldp + j];
-  for (int32_t r = 0; r < RT; ++r) mu += mcol[(int64_t)r * ldp + j];
   double var = sf2 - vs;
   var = var > 0.0 ? var : 0.0;
-  double sc = acq_score(kind, mu, var, stats[0], xi, kappa);
+  double sc = acq_score(kind, mu_full[q - base], var, stats[0], xi, kappa);
   if (*fit_flag != 0) sc = __builtin_nan("");
   if (compact) compact[j] = sc;
   if (full) full[q - base] = sc;
@@ -1318,13 +1220,13 @@ __global__ void k_fill(double* __restrict__ p, int64_t n, double v) {
 
 int gp_topk_pruned_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, const ut_acq* acq, const uint8_t* dup,
                         int64_t cand_base, int32_t k, int32_t bound_rows, int64_t* out_idx, double* out_score,
-                        ut_prune_stats* stats, hipEvent_t dup_ready, bool feat_ours, const double* ref_feat) {
+                        ut_prune_stats* stats, hipEvent_t dup_ready, bool feat_ours) {
   UT_CHECK(c, c->gp_ready, UT_EINVAL, "gp_topk_pruned: call ut_gp_fit first");
   UT_CHECK(c, c->gp_fit_prec == 64, UT_EINVAL, "gp_topk_pruned: needs an fp64 fit (ut_gp_set_precision 64)");
   UT_CHECK(c, acq->kind == UT_ACQ_EI || (acq->kind == UT_ACQ_UCB && acq->kappa >= 0.0), UT_EINVAL,
            "gp_topk_pruned: the score must increase with sigma (EI, or UCB with kappa >= 0)");
   UT_CHECK(c, k >= 1 && k <= 1024, UT_EINVAL, "gp_topk_pruned: k must be in [1, 1024]");
-  if (c->fit_pending) UT_HIP(c, hipStreamWaitEvent(c->stream, c->ev_alpha, 0));   // K* takes mu = k* . alpha
+  if (c->fit_pending) UT_HIP(c, hipStreamWaitEvent(c->stream, c->ev_fit, 0));   // K* takes mu = k* . alpha
   const int32_t n = c->gp_n, d = c->gp_d;
   const int32_t npad = ((n + NPAD - 1) / NPAD) * NPAD;
   const bool cat = feat_ours && c->cat_on;   // the categorical K* (features from ut's encoder)
@@ -1362,35 +1264,10 @@ int gp_topk_pruned_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, co
   // K* stores only the bound rows; the mean sums every row.  The few
   // candidates that need every row (threshold set, survivors) get their K*
   // columns recomputed from their features (recompute_cols below): cheaper than
-  // writing and re-reading the whole n x m matrix.  With a reference row (a GA
-  // round's parent) and few features, the parent-relative K* (one partial).
-  const bool rel = ref_feat && c->rel_enable && !cat && dpad >= 1 && dpad <= KSTAR_REL_DMAX;
-  c->rel_last = rel ? 1 : 0;
-  const int32_t RTm = rel ? 1 : RT;
-  if (rel) {
-    // the mean and |k*|^2 from the relative form; the bound rows from the MFMA
-    // K* over their R row tiles only (the same k* as the exact recomputation
-    // below, so the bound variance stays >= the exact one bit for bit)
-    if ((rc = launch_kstar_rel(c, XsT, npad, c->ucand.p, dpad, m, ldk, ref_feat, c->kst.p, 0, c->mu_part.p,
-                               c->pr_k2.p)))
-      return rc;
-    if ((rc = launch_gemm_kstar(c, 64, XsT, npad, c->ucand.p, dpad, m, c->kst.p, ldk, nullptr, -1, nullptr, nullptr,
-                                KstarCat(), xn, R * NPAD)))
-      return rc;
-    if (!c->pr_a2_valid) {
-      if ((rc = ensure(c, c->pr_a2, 1 + SQ_BLOCKS))) return rc;
-      hipLaunchKernelGGL(k_sumsq_part, dim3(SQ_BLOCKS), dim3(256), 0, c->stream, c->gp_alpha, (int64_t)npad,
-                         c->pr_a2.p + 1);
-      hipLaunchKernelGGL(k_sumsq_final, dim3(1), dim3(256), 0, c->stream, c->pr_a2.p + 1, SQ_BLOCKS, c->pr_a2.p);
-      UT_LAUNCH_CHECK(c);
-      c->pr_a2_valid = true;
-    }
-  } else if ((rc = launch_gemm_kstar(c, 64, XsT, npad, c->ucand.p, dpad, m, c->kst.p, ldk, c->mu_part.p, R * NPAD,
-                                     nullptr, c->pr_k2.p, cat ? kstar_cat(c, c->bcat.p) : KstarCat(), xn))) {
+  // writing and re-reading the whole n x m matrix
+  if ((rc = launch_gemm_kstar(c, 64, XsT, npad, c->ucand.p, dpad, m, c->kst.p, ldk, c->mu_part.p, R * NPAD,
+                              nullptr, c->pr_k2.p, cat ? kstar_cat(c, c->bcat.p) : KstarCat(), xn)))
     return rc;
-  }
-  // the rest reads L^-1 (K* needed only alpha: ev_alpha above)
-  if (c->fit_pending) UT_HIP(c, hipStreamWaitEvent(c->stream, c->ev_fit, 0));
   // |L^-1|_F^2 for the variance tail bound, once per fit
   if (!c->pr_f2_valid) {
     hipLaunchKernelGGL(k_sumsq_part, dim3(SQ_BLOCKS), dim3(256), 0, c->stream, c->gp_Linv, (int64_t)npad * npad,
@@ -1405,9 +1282,9 @@ int gp_topk_pruned_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, co
     return rc;
   mark(c, "bound");
   if (dup_ready) UT_HIP(c, hipStreamWaitEvent(c->stream, dup_ready, 0));   // the dup mask (side stream)
-  hipLaunchKernelGGL(k_prune_bound, dim3(grid1(m, 256)), dim3(256), 0, c->stream, m, RTm, RT, c->mu_part.p, R,
+  hipLaunchKernelGGL(k_prune_bound, dim3(grid1(m, 256)), dim3(256), 0, c->stream, m, RT, c->mu_part.p, R,
                      c->var_part.p, ldk, c->gp_sf2, c->gp_stats, c->gp_flag, acq->kind, acq->xi, acq->kappa, dup,
-                     c->pr_mu.p, c->pr_ub.p, c->pr_k2.p, c->pr_f2.p, c->pr_exact.p, rel ? c->pr_a2.p : nullptr);
+                     c->pr_mu.p, c->pr_ub.p, c->pr_k2.p, c->pr_f2.p, c->pr_exact.p);
   UT_LAUNCH_CHECK(c);
   // 3. threshold: exact scores of the best 1024 bounds, tau = their k-th best
   const int32_t kp = (int32_t)(m < 1024 ? m : 1024);
@@ -1421,7 +1298,6 @@ int gp_topk_pruned_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, co
     int r2;
     if ((r2 = ensure(c, c->pr_kst, (size_t)npad * ldc))) return r2;
     if ((r2 = ensure(c, c->pr_vpart, (size_t)RT * ldc))) return r2;
-    if ((r2 = ensure(c, c->pr_mcol, (size_t)RT * ldc))) return r2;
     if ((r2 = ensure(c, c->pr_ucand, (size_t)(dpad > 0 ? dpad : 1) * ldc))) return r2;
     if ((r2 = ensure(c, c->pr_cnorm, (size_t)ldc))) return r2;
     if (dpad > 0)
@@ -1435,8 +1311,7 @@ int gp_topk_pruned_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, co
                          c->stream, c->bcat.p, ldk, idx, base, nc, ldc, c->pr_bcat.p);
     }
     UT_LAUNCH_CHECK(c);
-    // (with the mean partials: the exact scores take k* . alpha of these columns)
-    return launch_gemm_kstar(c, 64, XsT, npad, c->pr_ucand.p, dpad, nc, c->pr_kst.p, ldc, c->pr_mcol.p, -1,
+    return launch_gemm_kstar(c, 64, XsT, npad, c->pr_ucand.p, dpad, nc, c->pr_kst.p, ldc, nullptr, -1,
                              c->pr_cnorm.p, nullptr, cat ? kstar_cat(c, c->pr_bcat.p) : KstarCat(), xn);
   };
   const int64_t ldt = ((int64_t)kp + VAR_BN - 1) / VAR_BN * VAR_BN;
@@ -1445,7 +1320,7 @@ int gp_topk_pruned_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, co
                             c->pr_mpart.p)))
     return rc;
   hipLaunchKernelGGL(k_prune_exact, dim3(grid1(kp, 256)), dim3(256), 0, c->stream, (int64_t)kp, tset, cand_base, RT,
-                     c->pr_vpart.p, ldt, c->pr_mcol.p, c->gp_sf2, c->gp_stats, c->gp_flag, acq->kind, acq->xi,
+                     c->pr_vpart.p, ldt, c->pr_mu.p, c->gp_sf2, c->gp_stats, c->gp_flag, acq->kind, acq->xi,
                      acq->kappa, tex, nullptr);
   UT_LAUNCH_CHECK(c);
   int64_t* tk_i = out_idx;   // the caller's [k] outputs hold tau's top-k for now
@@ -1488,8 +1363,8 @@ int gp_topk_pruned_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, co
                                 c->pr_mpart.p)))
         return rc;
       hipLaunchKernelGGL(k_prune_exact, dim3(grid1(ns, 256)), dim3(256), 0, c->stream, ns, c->pr_idx.p, (int64_t)0,
-                         RT, c->pr_vpart.p, lds, c->pr_mcol.p, c->gp_sf2, c->gp_stats, c->gp_flag, acq->kind,
-                         acq->xi, acq->kappa, nullptr, c->pr_score.p);
+                         RT, c->pr_vpart.p, lds, c->pr_mu.p, c->gp_sf2, c->gp_stats, c->gp_flag, acq->kind, acq->xi,
+                         acq->kappa, nullptr, c->pr_score.p);
       UT_LAUNCH_CHECK(c);
     }
   }
@@ -1500,7 +1375,6 @@ int gp_topk_pruned_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, co
     stats->survivors = dense ? m : ns;
     stats->bound_rows = R * NPAD;
     stats->dense = dense ? 1 : 0;
-    stats->relative = rel ? 1 : 0;
     stats->threshold = tau;
   }
   return 0;

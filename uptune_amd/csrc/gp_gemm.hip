@@ -399,18 +399,15 @@ int h3_kstar_exp(double sf2) { return H3_KSCALE_EXP - ilogb(sf2); }  // sf2 * 2^
 
 int launch_gemm_kstar(ut_ctx* c, int prec, const double* XsT, int32_t npad, const double* ucand, int32_t dpad,
                       int64_t m, void* kst, int64_t ldk, double* part, int32_t store_rows, const double* cn,
-                      double* part2, const KstarCat& cat, const double* xn, int32_t rows) {
+                      double* part2, const KstarCat& cat, const double* xn) {
   const bool has_cat = cat.nkc > 0;
-  UT_CHECK(c, rows < 0 || (rows > 0 && rows % K_BM == 0 && rows <= npad && !has_cat && part == nullptr), UT_EINVAL,
-           "gemm_kstar: bad row limit");
   UT_CHECK(c, npad % K_BM == 0 && dpad % 4 == 0 && (dpad >= 4 || has_cat) && ldk % K_BN == 0 && ldk >= m, UT_EINVAL,
            "gemm_kstar: bad padding");
   UT_CHECK(c, !has_cat || (cat.acat && cat.bcat), UT_EINVAL, "gemm_kstar: categorical operands missing");
   UT_CHECK(c, prec == 64 || prec == 32 || prec == 16, UT_EINVAL, "gemm_kstar: bad precision");
   UT_CHECK(c, part != nullptr || prec == 64, UT_EINVAL,
            "gemm_kstar: fp32 / h3 mode takes the mean partial here");
-  // (a row limit computes the first rows / 128 row tiles; A keeps its npad stride)
-  const int32_t RT = (rows > 0 ? rows : npad) / K_BM;
+  const int32_t RT = npad / K_BM;
   const int32_t CT = (int32_t)(ldk / K_BN);  // every column of K* (zeros past m) is written
   // fp64: only the first store_rows rows of K* are written (the mean still
   // sums every row); the other precisions always store everything
@@ -448,156 +445,6 @@ int launch_gemm_kstar(ut_ctx* c, int prec, const double* XsT, int32_t npad, cons
     UT_KSTAR_BOTH(double, false, (double*)kst, part, 1.0, (int64_t)0, store_rt, nullptr);
 #undef UT_KSTAR_BOTH
 #undef UT_KSTAR_LAUNCH
-  UT_LAUNCH_CHECK(c);
-  return 0;
-}
-
-// ---------------------------------------------------------------------------
-// Parent-relative K* (pruned scoring of single-parent GA / GGA rounds): a
-// child u of the round's parent p differs from it in a few features S(u)
-// (evolutionarytechniques.py:51-61: mutation rate 0.1 plus the forced
-// mutation), so
-//   |u - x|^2 = |p - x|^2 + sum_{j in S(u)} (u_j - p_j)(u_j + p_j - 2 x_j)
-// with |p - x|^2 computed once per round (k_rel_dp).  About |S| + 1 FMAs per
-// (child, training point) on the VALU instead of a K = dpad contraction on
-// the fp64 MFMA, which shares the SIMD's DP issue with the exp epilogue.
-// The outputs are what the pruned path's MU K* writes: the mean sum_r
-// alpha_r k*_r and sum_r k*_r^2 per candidate (one partial: RTm = 1) and the
-// first store_rows rows of K*^T (the bound rows).
-//   A workgroup takes 64 candidates (16 per wave, wave-uniform) and walks
-//   the training set in tiles of 64 rows (one per lane) staged in LDS as
-//   [feature][row]; each candidate's changed features (index, u_j - p_j,
-//   u_j + p_j) are listed once at the start in LDS and read back as
-//   broadcasts (a register array indexed by the feature would go to scratch).
-//   A child with more than REL_KMAX changed features takes the direct sum
-//   over all features.
-// ---------------------------------------------------------------------------
-constexpr int REL_KMAX = 16, REL_CPW = 16, REL_CB = 64, REL_TR = 64, REL_DMAX = KSTAR_REL_DMAX;
-
-// up[j] = ref[j] / ell_j (the same product k_gp_prep_cand forms), Dp[r] = |xs_r - up|^2
-// (rows >= n: 1e300, so their k* is exactly 0)
-__global__ void k_rel_dp(const double* __restrict__ ref, int32_t d, int32_t dpad, const double* __restrict__ inv_ell,
-                         const double* __restrict__ XsT, int32_t n, int32_t npad, double* __restrict__ up,
-                         double* __restrict__ dp) {
-  const int32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= npad) return;
-  double s = 0.0;
-  for (int32_t j = 0; j < dpad; ++j) {
-    const double u = j < d ? ref[j] * inv_ell[j] : 0.0;
-    if (r == 0) up[j] = u;
-    const double dx = XsT[(int64_t)j * npad + r] - u;
-    s = __builtin_fma(dx, dx, s);
-  }
-  dp[r] = r < n ? s : 1e300;
-}
-
-__global__ __launch_bounds__(256, 2) void k_gp_kstar_rel(const double* __restrict__ XsT, int32_t npad,
-                                                         const double* __restrict__ U, int64_t ldk, int32_t dpad,
-                                                         const double* __restrict__ up, const double* __restrict__ dp,
-                                                         const double* __restrict__ alpha, double sf2, int64_t m,
-                                                         double* __restrict__ kst, int32_t store_rows,
-                                                         double* __restrict__ mu_out, double* __restrict__ k2_out) {
-  __shared__ double xt[REL_DMAX * REL_TR];                 // [feature][row] tile
-  __shared__ double2 lst[4 * REL_CPW * REL_KMAX];          // (u_j - p_j, u_j + p_j) per changed feature
-  __shared__ uint8_t lj[4 * REL_CPW * REL_KMAX];           // its feature index
-  __shared__ int32_t lcnt[4 * REL_CPW];                    // count, -1: direct sum, -2: padded column
-  __shared__ double dpt[REL_TR], alt[REL_TR];
-  __shared__ double etab[EXP_TAB];
-  const int t = threadIdx.x, lane = t & 63;
-  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
-  if (t < EXP_TAB) etab[t] = sf2 * exp2((double)t / EXP_TAB);
-  const int64_t cw = (int64_t)blockIdx.x * REL_CB + w * REL_CPW;   // this wave's first candidate
-  // the changed features of each of the wave's candidates (bitwise compare)
-  for (int cc = 0; cc < REL_CPW; ++cc) {
-    const int64_t c = cw + cc;
-    const int sl = w * REL_CPW + cc;
-    bool ch = false;
-    double u = 0.0, p = 0.0;
-    if (lane < dpad && c < m) {
-      u = U[(int64_t)lane * ldk + c];
-      p = up[lane];
-      ch = __builtin_bit_cast(uint64_t, u) != __builtin_bit_cast(uint64_t, p);
-    }
-    const uint64_t mask = __ballot(ch);
-    const int cnt = __popcll(mask);
-    if (ch && cnt <= REL_KMAX) {
-      const int pos = __popcll(mask & ((1ull << lane) - 1ull));
-      lst[sl * REL_KMAX + pos] = make_double2(u - p, u + p);
-      lj[sl * REL_KMAX + pos] = (uint8_t)lane;
-    }
-    if (lane == 0) lcnt[sl] = c >= m ? -2 : (cnt <= REL_KMAX ? cnt : -1);
-  }
-  double mu[REL_CPW], k2[REL_CPW];
-#pragma unroll
-  for (int cc = 0; cc < REL_CPW; ++cc) mu[cc] = k2[cc] = 0.0;
-  for (int32_t r0 = 0; r0 < npad; r0 += REL_TR) {
-    __syncthreads();   // the previous tile is fully read (first pass: etab and the lists)
-    for (int j = w; j < dpad; j += 4) xt[j * REL_TR + lane] = XsT[(int64_t)j * npad + r0 + lane];
-    if (w == 0) dpt[lane] = dp[r0 + lane];
-    else if (w == 1) alt[lane] = alpha[r0 + lane];
-    __syncthreads();
-    const double db = dpt[lane], al = alt[lane];
-    const int32_t row = r0 + lane;
-#pragma unroll
-    for (int cc = 0; cc < REL_CPW; ++cc) {
-      const int sl = w * REL_CPW + cc;
-      const int64_t c = cw + cc;
-      const int cnt = __builtin_amdgcn_readfirstlane(lcnt[sl]);
-      double D;
-      if (cnt >= 0) {
-        D = db;
-        for (int q = 0; q < cnt; ++q) {
-          const int j = __builtin_amdgcn_readfirstlane((int)lj[sl * REL_KMAX + q]);
-          const double2 e = lst[sl * REL_KMAX + q];
-          D = __builtin_fma(e.x, __builtin_fma(-2.0, xt[j * REL_TR + lane], e.y), D);
-        }
-      } else if (cnt == -1) {   // many changed features: the direct sum
-        D = 0.0;
-        for (int j = 0; j < dpad; ++j) {
-          const double dx = U[(int64_t)j * ldk + c] - xt[j * REL_TR + lane];
-          D = __builtin_fma(dx, dx, D);
-        }
-        D = db < 1e299 ? D : 1e300;   // padded rows stay 0
-      } else {
-        D = 1e300;   // padded columns
-      }
-      const double x = __builtin_fmax(__builtin_fmin(-0.5 * D, 0.0), -1000.0);
-      const double ks = sf2_exp_nonpos(x, etab);
-      mu[cc] = __builtin_fma(al, ks, mu[cc]);
-      k2[cc] = __builtin_fma(ks, ks, k2[cc]);
-      if (row < store_rows) kst[(int64_t)row * ldk + c] = ks;
-    }
-  }
-#pragma unroll
-  for (int cc = 0; cc < REL_CPW; ++cc) {
-    double a = mu[cc], b = k2[cc];
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-      a += __shfl_xor(a, off);
-      b += __shfl_xor(b, off);
-    }
-    const int64_t c = cw + cc;
-    if (lane == 0 && c < ldk) {
-      mu_out[c] = a;
-      k2_out[c] = b;
-    }
-  }
-}
-
-int launch_kstar_rel(ut_ctx* c, const double* XsT, int32_t npad, const double* ucand, int32_t dpad, int64_t m,
-                     int64_t ldk, const double* ref_feat, double* kst, int32_t store_rows, double* mu_out,
-                     double* k2_out) {
-  UT_CHECK(c, dpad >= 1 && dpad <= REL_DMAX && npad % REL_TR == 0 && ldk % REL_CB == 0 && ldk >= m, UT_EINVAL,
-           "kstar_rel: bad shape");
-  const int64_t nwg = ldk / REL_CB;
-  int rc;
-  if ((rc = ensure(c, c->rel_up, (size_t)REL_DMAX + npad))) return rc;
-  double* up = c->rel_up.p;
-  double* dp = c->rel_up.p + REL_DMAX;
-  hipLaunchKernelGGL(k_rel_dp, dim3(grid1(npad, 256)), dim3(256), 0, c->stream, ref_feat, c->gp_d, dpad,
-                     c->gp_inv_ell, XsT, c->gp_n, npad, up, dp);
-  hipLaunchKernelGGL(k_gp_kstar_rel, dim3((unsigned)nwg), dim3(256), 0, c->stream, XsT, npad, ucand, ldk, dpad, up, dp,
-                     c->gp_alpha, c->gp_sf2, m, kst, store_rows, mu_out, k2_out);
   UT_LAUNCH_CHECK(c);
   return 0;
 }

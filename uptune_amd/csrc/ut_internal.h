@@ -136,11 +136,6 @@ struct ut_ctx {
   hipStream_t side = nullptr;
   hipStream_t fit_stream = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_fit = nullptr, ev_prefit = nullptr;
-  // alpha = K^-1 y (and beta = L^-1 y) ready: a refit solves for them right after
-  // the Cholesky, before the recursive inverse (early_alpha; UT_EARLY_ALPHA=0
-  // takes them from L^-1 as before); an append records it with ev_fit
-  hipEvent_t ev_alpha = nullptr;
-  bool early_alpha = true;
   hipEvent_t ev_fit_x = nullptr;     // fit stream: scaled training inputs ready (K* may start)
   bool fit_pending = false;          // scoring waits on ev_fit before touching GP state
   // round schedule: 1 = the variance GEMM waits for the side stream's hash +
@@ -337,12 +332,6 @@ struct ut_ctx {
   ut::DevBuf<double> pr_f2;                    // [1] |L^-1|_F^2 (+ its block partials)
   bool pr_f2_valid = false;                    // pr_f2 belongs to the current fit
   ut::DevBuf<uint8_t> pr_exact;                // [ld] the stored score is the exact score
-  ut::DevBuf<double> rel_up;                   // parent-relative K*: the parent's u' [64] and |x_r - u'_p|^2 [npad]
-  ut::DevBuf<double> pr_mcol;                  // recomputed columns' mean partials [RT][lds] (their exact scores)
-  ut::DevBuf<double> pr_a2;                    // [1] |alpha|^2 (+ block partials): the relative mean's slack
-  bool pr_a2_valid = false;
-  bool rel_enable = true;                      // UT_KSTAR_REL=0: pruned rounds always take the dense K*
-  int32_t rel_last = 0;                        // the last pruned call took the parent-relative K* (tests)
   int64_t r_ld = 0;
   int64_t r_m = 0;
   bool r_feat_valid = false;        // r_feat holds the last round's features (pruned rounds only)
@@ -501,19 +490,9 @@ int topk_pairs_impl(ut_ctx* c, const double* score, const int64_t* idx, int64_t 
                     double* out_score);
 // feat_ours: the features come from ut's own encoder (one-hot ENUM blocks),
 // so the categorical K* may read them as codes
-// ref_feat: features [d] of a configuration most candidates differ from in a
-// few features (a GA round's parent): K* then comes from the parent-relative
-// kernel (launch_kstar_rel) when the shapes allow it
 int gp_topk_pruned_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, const ut_acq* acq, const uint8_t* dup,
                         int64_t cand_base, int32_t k, int32_t bound_rows, int64_t* out_idx, double* out_score,
-                        ut_prune_stats* stats, hipEvent_t dup_ready = nullptr, bool feat_ours = false,
-                        const double* ref_feat = nullptr);
-// parent-relative K* of the pruned path: the mean and sum k*^2 per candidate
-// (one partial each) and the first store_rows rows of K*^T, fp64
-int launch_kstar_rel(ut_ctx* c, const double* XsT, int32_t npad, const double* ucand, int32_t dpad, int64_t m,
-                     int64_t ldk, const double* ref_feat, double* kst, int32_t store_rows, double* mu_out,
-                     double* k2_out);
-constexpr int32_t KSTAR_REL_DMAX = 64;
+                        ut_prune_stats* stats, hipEvent_t dup_ready = nullptr, bool feat_ours = false);
 // prec: 64 (fp64 MFMA), 32 (fp32 MFMA), 16 (f16x3: fp16 hi/lo split operands,
 // three fp16 MFMA products, f32 accumulate -- see gp_gemm.hip)
 constexpr int H3_KSCALE_EXP = 14;  // K* (<= sf2) is scaled by 2^(14 - ceil(log2 sf2)) before the split
@@ -530,8 +509,7 @@ int launch_gemm_kstar(ut_ctx* c, int prec, const double* XsT, int32_t npad, cons
                       const double* cn = nullptr,    // candidate norms (nullptr: c->cnorm)
                       double* part2 = nullptr,       // fp64 with part: also sum_r k*_r^2 partials
                       const KstarCat& cat = KstarCat(),
-                      const double* xn = nullptr,    // training norms (nullptr: c->gp_xnorm)
-                      int32_t rows = -1);            // > 0: only the first `rows` rows of K* (a multiple of 128)
+                      const double* xn = nullptr);   // training norms (nullptr: c->gp_xnorm)
 int launch_prep_cand(ut_ctx* c, const double* feat, int64_t ld, int64_t m, int32_t d, int32_t dpad, double* u,
                      int64_t ldu, double* cn);
 // categorical K*: the K* operands of the candidate side when the fit is in

@@ -356,33 +356,20 @@ class BatchEngine:
         return mu, var, score
 
     def gp_topk_pruned(self, feat: torch.Tensor, k: int, m: Optional[int] = None, acq: Optional[L.Acq] = None,
-                       dup: Optional[torch.Tensor] = None, cand_base: int = 0, bound_rows: int = 256,
-                       ref: Optional[torch.Tensor] = None):
+                       dup: Optional[torch.Tensor] = None, cand_base: int = 0, bound_rows: int = 256):
         """ut_gp_topk_pruned: the top-k of the GP score, selection-exact, with the
         full variance GEMM only for candidates whose score bound (first
-        `bound_rows` rows of L^-1 k*) reaches the threshold.  ref: features [d]
-        of a configuration the candidates mostly differ from in a few features
-        (a GA round's parent; ut_gp_topk_pruned_ref's parent-relative K*).
-        -> (idx, score, stats dict)"""
+        `bound_rows` rows of L^-1 k*) reaches the threshold.  -> (idx, score, stats dict)"""
         m = feat.shape[1] if m is None else m
         acq = acq or self.acq()
         idx = self._empty(k, dtype=torch.int64)
         top = self._empty(k)
         st = L.PruneStats()
-        if ref is None:
-            rc = self.lib.ut_gp_topk_pruned(self.ctx, _ptr(feat), feat.stride(0), m, C.byref(acq), _ptr(dup),
-                                            int(cand_base), int(k), int(bound_rows), _ptr(idx), _ptr(top),
-                                            C.byref(st))
-        else:
-            ref = ref.reshape(-1).to(device=self.device, dtype=torch.float64).contiguous()
-            if ref.numel() != feat.shape[0]:
-                raise ValueError(f"gp_topk_pruned: ref has {ref.numel()} features, the candidates {feat.shape[0]}")
-            rc = self.lib.ut_gp_topk_pruned_ref(self.ctx, _ptr(feat), feat.stride(0), m, C.byref(acq), _ptr(dup),
-                                                int(cand_base), int(k), int(bound_rows), _ptr(ref), _ptr(idx),
-                                                _ptr(top), C.byref(st))
-        L.check(self.ctx, rc, "ut_gp_topk_pruned")
+        L.check(self.ctx, self.lib.ut_gp_topk_pruned(self.ctx, _ptr(feat), feat.stride(0), m, C.byref(acq), _ptr(dup),
+                                                     int(cand_base), int(k), int(bound_rows), _ptr(idx), _ptr(top),
+                                                     C.byref(st)), "ut_gp_topk_pruned")
         return idx, top, {"survivors": st.survivors, "bound_rows": st.bound_rows, "dense": bool(st.dense),
-                          "threshold": st.threshold, "m": m, "relative": bool(st.relative)}
+                          "threshold": st.threshold, "m": m}
 
     # -- tree-ensemble surrogate ---------------------------------------------
     def forest_set(self, model):

@@ -604,7 +604,7 @@ class GpuBatchTechnique(SearchTechnique):
         elif have_model:
             if self.prune_rows > 0 and self.model.precision == 64:
                 idx, top, _ = eng.gp_topk_pruned(eng.encode(vals), self.batch, acq=eng.acq(self.acq_kind), dup=dup,
-                                                 cand_base=base, bound_rows=self.prune_rows, ref=self.prune_ref(eng))
+                                                 cand_base=base, bound_rows=self.prune_rows)
                 loc = torch.where(idx >= 0, idx - base, torch.zeros_like(idx))
                 return vals, idx, top, dig[loc], vals[:, loc]
             # encoding fused into the K* operand pass (no feature matrix)
@@ -672,12 +672,6 @@ class GpuBatchTechnique(SearchTechnique):
 
     def after_round(self, idx, hexes):
         pass
-
-    def prune_ref(self, eng):
-        """features of the configuration this round's candidates mostly differ
-        from in a few features (pruned scoring then takes the parent-relative
-        K*), or None"""
-        return None
 
     def desired_configuration(self):
         try:
@@ -778,17 +772,6 @@ class GpuGA(GpuBatchTechnique):
         # GreedySelectionMixin.select: the global best config (random() before any result)
         self._parent = self.best_row()
         return self.engine.propose_ga(m, self._parent, None, round_=self.round, cand_base=self.round_base(), **self.ga)
-
-    def prune_ref(self, eng):
-        # every child is the parent with a few mutated params
-        # (evolutionarytechniques.py:51-61; GGA's crossover partner is the same
-        # best configuration, globalGA.py:227-235 with select() twice)
-        parent = getattr(self, "_parent", None)
-        if parent is None:
-            return None
-        import torch
-        col = torch.as_tensor(np.ascontiguousarray(parent, dtype=np.float64).reshape(-1, 1), device=eng.device)
-        return eng.encode(col)[:, 0]
 
     def hash_proposals(self, vals, base):
         # children keep most of the parent's values: reuse its inner digests
