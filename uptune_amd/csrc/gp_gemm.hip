@@ -9,6 +9,8 @@
 //
 //   fp64: v_mfma_f64_16x16x4_f64   (C/D: col = lane&15, row = (lane>>4) + 4r)
 //   fp32: v_mfma_f32_32x32x2_f32   (C/D: col = lane&31, row = (r&3) + 8(r>>2) + 4(lane>>5))
+#include <type_traits>
+
 #include "ut_internal.h"
 
 namespace ut {
@@ -304,11 +306,15 @@ __global__ __launch_bounds__(K_NT, 2) void k_gp_kstar(const double* __restrict__
     // epilogue operands from the LDS copies (landed with the first K stage).
     // Padding rows / columns get a huge negative half-norm, so their k* is
     // exactly 0 without a select.
+    // (every LDS read is unconditional and the padding goes in by a select:
+    // a branch around a read splits the epilogue into basic blocks and each
+    // read's wait then stalls the wave instead of overlapping other elements)
     double hc[4];
 #pragma unroll
     for (int jj = 0; jj < 4; ++jj) {
       const int cl = wn * 64 + jj * 16 + (lane & 15);
-      hc[jj] = col0 + cl < m ? -0.5 * rowop[2 * K_BM + cl] : -1e300;
+      const double hv = -0.5 * rowop[2 * K_BM + cl];
+      hc[jj] = col0 + cl < m ? hv : -1e300;
     }
     const bool want2 = !H3 && MU && part2 != nullptr;
     double s[4] = {0.0, 0.0, 0.0, 0.0}, s2[4] = {0.0, 0.0, 0.0, 0.0};
@@ -323,7 +329,8 @@ __global__ __launch_bounds__(K_NT, 2) void k_gp_kstar(const double* __restrict__
           uint32_t hpk[2] = {0u, 0u}, lpk[2] = {0u, 0u};   // the four rows' fp16 hi / lo, packed
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const double hx = row0 + rl0 + r < n ? -0.5 * rowop[rl0 + r] : -1e300;
+            const double hv = -0.5 * rowop[rl0 + r];
+            const double hx = row0 + rl0 + r < n ? hv : -1e300;
             const double x = __builtin_fmax(__builtin_fmin((acc[i][jj][r] + hx) + hc[jj], 0.0), -1000.0);
             const double ks = sf2_exp_nonpos(x, etab);
             // ks = k* * kscale (< 2^15): hi = fp16(ks), lo = fp16 of the rest,
@@ -343,28 +350,35 @@ __global__ __launch_bounds__(K_NT, 2) void k_gp_kstar(const double* __restrict__
         }
       }
     } else {
+      // STORE: this tile's rows are stored (pruned scoring stores the bound
+      // rows only); decided once per item, so the element code has no branch
+      auto epi = [&](auto store_c) {
+        constexpr bool STORE = decltype(store_c)::value;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
+        for (int i = 0; i < 4; ++i) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int rl = wm * 64 + i * 16 + (lane >> 4) + 4 * r;
-          const int32_t row = row0 + rl;
-          const double hx = row < n ? -0.5 * rowop[rl] : -1e300;
-          double al = 0.0;
-          if constexpr (MU) al = rowop[K_BM + rl];
+          for (int r = 0; r < 4; ++r) {
+            const int rl = wm * 64 + i * 16 + (lane >> 4) + 4 * r;
+            const int32_t row = row0 + rl;
+            const double hv = -0.5 * rowop[rl];
+            const double hx = row < n ? hv : -1e300;
+            double al = 0.0;
+            if constexpr (MU) al = rowop[K_BM + rl];
+            TS* kp = kst + (int64_t)row * ldk + col0 + wn * 64 + (lane & 15);
 #pragma unroll
-          for (int jj = 0; jj < 4; ++jj) {
-            const int cl = wn * 64 + jj * 16 + (lane & 15);
-            const int64_t col = col0 + cl;
-            // -|x - u|^2 / 2 = C - |x|^2/2 - |u|^2/2, clamped to [-1000, 0]
-            const double x = __builtin_fmax(__builtin_fmin((acc[i][jj][r] + hx) + hc[jj], 0.0), -1000.0);
-            const double ks = sf2_exp_nonpos(x, etab);
-            if (rt < store_rt) kst[(int64_t)row * ldk + col] = (TS)ks;   // pruned scoring stores the bound rows only
-            if constexpr (MU) s[jj] += al * ks;
-            if constexpr (MU) s2[jj] += ks * ks;
+            for (int jj = 0; jj < 4; ++jj) {
+              // -|x - u|^2 / 2 = C - |x|^2/2 - |u|^2/2, clamped to [-1000, 0]
+              const double x = __builtin_fmax(__builtin_fmin((acc[i][jj][r] + hx) + hc[jj], 0.0), -1000.0);
+              const double ks = sf2_exp_nonpos(x, etab);
+              if constexpr (STORE) kp[jj * 16] = (TS)ks;
+              if constexpr (MU) s[jj] += al * ks;
+              if constexpr (MU) s2[jj] += ks * ks;
+            }
           }
         }
-      }
+      };
+      if (rt < store_rt) epi(std::integral_constant<bool, true>{});
+      else epi(std::integral_constant<bool, false>{});
     }
     if constexpr (MU) {
 #pragma unroll
