@@ -61,7 +61,7 @@ __global__ void k_gp_num_train(const double* __restrict__ Xs, int32_t npad, int3
   double s = 0.0;
   for (int32_t k = 0; k < dpad_num; ++k) {
     const double v = k < n_num ? Xs[(int64_t)r * d + num_feat[k]] : 0.0;
-    XsT_num[(int64_t)k * npad + r] = v;
+    XsT_num[(int64_t)k * npad + r] = v * KSTAR_T_SCALE;   // the K* operand, in 2^(1/256) units (gp_gemm.hip)
     s += v * v;
   }
   xnorm_num[r] = s;

@@ -49,30 +49,35 @@ __device__ __forceinline__ int64_t h3_blk_off(int64_t r, int32_t k, int32_t K) {
 }
   // CUs left to an in-flight GP fit (launch_gemm_kstar)
 
-// sf2 * exp(x) for x in [-1000, 0], table-driven: x = (256 k' + j) ln2/256 + r,
-// |r| <= ln2/512, so exp(x) = 2^k' * 2^(j/256) * e^r with a degree-4 polynomial
-// for e^r (truncation < 4e-17) and etab[j] = sf2 * 2^(j/256) built in LDS by each
-// workgroup (2 KiB).  About 14 VALU ops against ~32 for the library exp with its
-// range checks (the epilogue shares the SIMDs with the f64 MFMAs, so every op
-// counts; the 32-entry table with a degree-6 polynomial took two more FMAs).
+// sf2 * exp(x) for x <= 0, table-driven: etab[j] = sf2 * 2^(j/256) built in LDS by
+// each workgroup (2 KiB); about 12 VALU ops against ~32 for the library exp with
+// its range checks (the epilogue shares the SIMDs with the f64 MFMAs, so every
+// op counts; a 32-entry table with a degree-6 polynomial took two more FMAs).
 // Max error ~2 ulp; 2^k' underflows to exactly 0 at x = -1000.
 constexpr int EXP_TAB = 256;
 
-__device__ __forceinline__ double sf2_exp_nonpos(double x, const double* etab) {
-  constexpr double INV_L = 369.3299304675746;         // 256 / ln 2
-  constexpr double L_HI = 0.00270760617331689;        // ln2/256 to 32 bits: kf * L_HI is exact
-  constexpr double L_LO = 7.453964567463233e-13;      // ln2/256 - L_HI
-  const double kf = __builtin_rint(x * INV_L);
-  double r = __builtin_fma(kf, -L_HI, x);
-  r = __builtin_fma(kf, -L_LO, r);
-  double p = 1.0 / 24.0;
-  p = __builtin_fma(p, r, 1.0 / 6.0);
-  p = __builtin_fma(p, r, 0.5);
-  p = __builtin_fma(p, r, 1.0);
-  p = __builtin_fma(p, r, 1.0);
+// The K* contraction works in units of 2^(1/256): its training operand is
+// Xs^T * (256 / ln 2) (KSTAR_T_SCALE, applied where Xs^T is built, k_gp_xs_t /
+// k_gp_num_train), the epilogue's norms and categorical coefficients carry the
+// same factor, so the accumulator is t = -|x - u|^2 / 2 * 256 / ln 2 directly
+// and the exp needs no multiply and no two-step reduction: t = 256 k' + j + f
+// with kf = rint(t), f = t - kf exact (|f| <= 1/2), and
+// exp = 2^k' * 2^(j/256) * e^(f ln2/256) with the same degree-4 polynomial
+// (|f ln2/256| <= 1.36e-3: truncation < 4e-17).  Two DP ops fewer per k*
+// than sf2_exp_nonpos, whose rounding it shares to ~1 ulp.
+__device__ __forceinline__ double sf2_exp2t_nonpos(double t, const double* etab) {
+  constexpr double L = 0.002707606174582214;          // ln 2 / 256
+  constexpr double C2 = L * L / 2.0, C3 = L * L * L / 6.0, C4 = L * L * L * L / 24.0;
+  const double kf = __builtin_rint(t);
+  const double f = t - kf;
+  double p = __builtin_fma(C4, f, C3);
+  p = __builtin_fma(p, f, C2);
+  p = __builtin_fma(p, f, L);
+  p = __builtin_fma(p, f, 1.0);
   const int k = (int)kf;
   return __builtin_ldexp(p * etab[k & (EXP_TAB - 1)], k >> 8);
 }
+constexpr double KSTAR_T_MIN = -1000.0 * KSTAR_T_SCALE;   // exp(-1000): the table's 2^k' underflows to 0
 
 constexpr int K_SA = K_BK * K_BM, K_SB = K_BK * K_BN, K_STAGE = K_SA + K_SB;
 
@@ -266,7 +271,8 @@ __global__ __launch_bounds__(K_NT, 2) void k_gp_kstar(const double* __restrict__
 #pragma unroll
         for (int jj = 0; jj < 4; ++jj)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) acc[i][jj][r] = __builtin_fma((double)iacc[i][jj][r], cat_c1, cat_c0);
+          for (int r = 0; r < 4; ++r)
+            acc[i][jj][r] = __builtin_fma((double)iacc[i][jj][r], cat_c1, cat_c0);   // (in t units: see the launch)
     } else {
 #pragma unroll
       for (int i = 0; i < 4; ++i)
@@ -313,7 +319,7 @@ __global__ __launch_bounds__(K_NT, 2) void k_gp_kstar(const double* __restrict__
 #pragma unroll
     for (int jj = 0; jj < 4; ++jj) {
       const int cl = wn * 64 + jj * 16 + (lane & 15);
-      const double hv = -0.5 * rowop[2 * K_BM + cl];
+      const double hv = (-0.5 * KSTAR_T_SCALE) * rowop[2 * K_BM + cl];
       hc[jj] = col0 + cl < m ? hv : -1e300;
     }
     const bool want2 = !H3 && MU && part2 != nullptr;
@@ -329,10 +335,10 @@ __global__ __launch_bounds__(K_NT, 2) void k_gp_kstar(const double* __restrict__
           uint32_t hpk[2] = {0u, 0u}, lpk[2] = {0u, 0u};   // the four rows' fp16 hi / lo, packed
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const double hv = -0.5 * rowop[rl0 + r];
+            const double hv = (-0.5 * KSTAR_T_SCALE) * rowop[rl0 + r];
             const double hx = row0 + rl0 + r < n ? hv : -1e300;
-            const double x = __builtin_fmax(__builtin_fmin((acc[i][jj][r] + hx) + hc[jj], 0.0), -1000.0);
-            const double ks = sf2_exp_nonpos(x, etab);
+            const double x = __builtin_fmax(__builtin_fmin((acc[i][jj][r] + hx) + hc[jj], 0.0), KSTAR_T_MIN);
+            const double ks = sf2_exp2t_nonpos(x, etab);
             // ks = k* * kscale (< 2^15): hi = fp16(ks), lo = fp16 of the rest,
             // the rest taken in f32 (exact there: hi is within 2^-11 of xf)
             const float xf = (float)ks;
@@ -360,16 +366,16 @@ __global__ __launch_bounds__(K_NT, 2) void k_gp_kstar(const double* __restrict__
           for (int r = 0; r < 4; ++r) {
             const int rl = wm * 64 + i * 16 + (lane >> 4) + 4 * r;
             const int32_t row = row0 + rl;
-            const double hv = -0.5 * rowop[rl];
+            const double hv = (-0.5 * KSTAR_T_SCALE) * rowop[rl];
             const double hx = row < n ? hv : -1e300;
             double al = 0.0;
             if constexpr (MU) al = rowop[K_BM + rl];
             TS* kp = kst + (int64_t)row * ldk + col0 + wn * 64 + (lane & 15);
 #pragma unroll
             for (int jj = 0; jj < 4; ++jj) {
-              // -|x - u|^2 / 2 = C - |x|^2/2 - |u|^2/2, clamped to [-1000, 0]
-              const double x = __builtin_fmax(__builtin_fmin((acc[i][jj][r] + hx) + hc[jj], 0.0), -1000.0);
-              const double ks = sf2_exp_nonpos(x, etab);
+              // t = (C - |x|^2/2 - |u|^2/2) * 256 / ln 2, clamped to [-1000 * 256 / ln 2, 0]
+              const double x = __builtin_fmax(__builtin_fmin((acc[i][jj][r] + hx) + hc[jj], 0.0), KSTAR_T_MIN);
+              const double ks = sf2_exp2t_nonpos(x, etab);
               if constexpr (STORE) kp[jj * 16] = (TS)ks;
               if constexpr (MU) s[jj] += al * ks;
               if constexpr (MU) s2[jj] += ks * ks;
@@ -442,7 +448,8 @@ int launch_gemm_kstar(ut_ctx* c, int prec, const double* XsT, int32_t npad, cons
 #define UT_KSTAR_LAUNCH(TS, MU, CAT, KST, PART, KSCALE, LOOFF, SRT, PART2)                                         \
   hipLaunchKernelGGL((k_gp_kstar<TS, MU, CAT>), dim3(nb), dim3(K_NT), 0, c->stream, XsT, (int64_t)npad, ucand, ldk, \
                      dpad, RT, CT, xnorm, cnorm, c->gp_alpha, c->gp_sf2, c->gp_n, m, c->gp_ctr + 8, KST, ldk, PART, \
-                     KSCALE, LOOFF, SRT, PART2, cat.acat, cat.bcat, cat.nkc, cat.c0, cat.c1)
+                     KSCALE, LOOFF, SRT, PART2, cat.acat, cat.bcat, cat.nkc, cat.c0 * KSTAR_T_SCALE,        \
+                     cat.c1 * KSTAR_T_SCALE)
 #define UT_KSTAR_BOTH(TS, MU, ...)                   \
   do {                                               \
     if (has_cat) UT_KSTAR_LAUNCH(TS, MU, true, __VA_ARGS__); \
@@ -545,7 +552,7 @@ __global__ void k_gp_xs_t(const double* __restrict__ Xs, int32_t npad, int32_t d
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= (int64_t)dpad * npad) return;
   const int32_t k = (int32_t)(e / npad), r = (int32_t)(e % npad);
-  XsT[e] = (k < d) ? Xs[(int64_t)r * d + k] : 0.0;
+  XsT[e] = (k < d) ? Xs[(int64_t)r * d + k] * KSTAR_T_SCALE : 0.0;   // the K* operand, in 2^(1/256) units
 }
 
 int launch_xs_t(ut_ctx* c, const double* Xs, int32_t npad, int32_t d, int32_t dpad, double* XsT) {

@@ -497,6 +497,10 @@ int gp_topk_pruned_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, co
 // three fp16 MFMA products, f32 accumulate -- see gp_gemm.hip)
 constexpr int H3_KSCALE_EXP = 14;  // K* (<= sf2) is scaled by 2^(14 - ceil(log2 sf2)) before the split
 int h3_kstar_exp(double sf2);
+// K*'s training operand (Xs^T, the numeric part in categorical mode) is stored
+// times 256 / ln 2: the contraction then yields the exponent in 2^(1/256) units
+// (gp_gemm.hip sf2_exp2t_nonpos)
+constexpr double KSTAR_T_SCALE = 369.3299304675746;   // 256 / ln 2
 // the K* contraction's categorical operands (nkc = cat_k / 128 int8 stages; 0 = none)
 struct KstarCat {
   const int8_t* acat = nullptr;
