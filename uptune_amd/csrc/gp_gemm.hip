@@ -66,7 +66,7 @@ constexpr int EXP_TAB = 256;
 // (|f ln2/256| <= 1.36e-3: truncation < 4e-17).  Two DP ops fewer per k*
 // than sf2_exp_nonpos, whose rounding it shares to ~1 ulp.
 __device__ __forceinline__ double sf2_exp2t_nonpos(double t, const double* etab) {
-  constexpr double L = 0.002707606174582214;          // ln 2 / 256
+  constexpr double L = 0.6931471805599453 / 256.0;    // ln 2 / 256 (exact: a power-of-two division)
   constexpr double C2 = L * L / 2.0, C3 = L * L * L / 6.0, C4 = L * L * L * L / 24.0;
   const double kf = __builtin_rint(t);
   const double f = t - kf;
