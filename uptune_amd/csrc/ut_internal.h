@@ -211,10 +211,14 @@ struct ut_ctx {
   // fp32 / f16x3 dense rounds: 1 = enqueue the hash after K* (their K* waits
   // for the whole fit, which the hash would otherwise crowd out of the CUs: at
   // n = 4096 the refit stretches from ~6 to ~14 ms beside it) and let the
-  // variance GEMM run beside it; 0 = fork it before encode; -1 (default) = 1
-  // for fits of n >= 2048.  Measured, f16x3: C3 (n 4096) 149.2 vs 153.0 ms per
-  // round; C2 (n 1024) 12.9-13.1 vs 12.8 ms.  UT_HASH_AFTER_KSTAR
-  int32_t hash_after_kstar = -1;
+  // variance GEMM run beside it; 0 (default) = fork it before encode; -1 = 1
+  // for fits of n >= 2048.  Measured, f16x3: round 3, C3 (n 4096) 149.2 vs
+  // 153.0 ms per round, C2 (n 1024) 12.9-13.1 vs 12.8 ms; round 4, with the
+  // categorical K* (C3's K* 46 -> 22 ms, so the fit's crowding costs less than
+  // the hash's 7-ms tail after the variance GEMM): C3 121.9 ms after K* vs
+  // 120.4 before encode, the tail 6.7 -> 0.2 ms (profiles/r04l_c3h*.log).
+  // UT_HASH_AFTER_KSTAR
+  int32_t hash_after_kstar = 0;
   // k_gp_var_h3 item order: 0 = strip-major, 1 = paired row tiles in XCD
   // groups (L^-1 stages shared in L2 by the group's workgroups); UT_H3_SCHED
   int32_t h3_sched = 1;
