@@ -24,6 +24,8 @@ run 600 bench_c3_f64 python bench.py --config c3 --steps 3 --warmup 1 --no-cpu-b
 run 400 bench_c4 python bench.py --config c4 --steps 5 --warmup 2 --no-cpu-baseline
 run 300 c5_dense python scripts/c5_bandit.py --generations 100
 run 300 c5_prune python scripts/c5_bandit.py --generations 100 --prune 256
+}
+[ -n "$SKIP_MEM" ] || {
 UT_DIST_BACKEND=gloo run 400 mem_strong8_c2 python bench.py --gpus 8 --scaling strong --steps 2 --warmup 1 --no-cpu-baseline --no-parity
 UT_DIST_BACKEND=gloo run 600 mem_strong8_c3 python bench.py --config c3 --precision 16 --gpus 8 --scaling strong --steps 2 --warmup 1 --no-cpu-baseline --no-parity
 }
