@@ -318,6 +318,15 @@ def parity_ga_round(eng, space, idx, top, dig, parent, seed, round_, X, y, ell, 
             "digests_equal": bool(ghex == hexes), "ei_max_rel_err": rel, "round": int(round_)}
 
 
+def kstar_fp64_features(eng, d):
+    """the features K* contracts in fp64: every feature, or in categorical mode
+    (ENUM / BOOL one-hot blocks as int8 codes) the numeric ones only"""
+    if eng.gp_kstar_mode() != "categorical":
+        return d
+    from uptune_amd import _lib as L
+    return sum(p.n_feat for p in eng.spec.params if p.kind not in (L.UT_BOOL, L.UT_ENUM))
+
+
 def main():
     if "WORLD_SIZE" not in os.environ:
         pre = argparse.ArgumentParser(add_help=False)
@@ -530,7 +539,8 @@ def main():
     elapsed = time.perf_counter() - t0
     # per-stage device times of the timed rounds (HIP events recorded on the
     # library's streams during the rounds, read once here)
-    for st in ("propose", "hash", "dedup", "encode", "kstar", "bound", "prune", "var", "finalize", "topk"):
+    for st in ("propose", "hash", "dedup", "encode", "fit_wait", "kstar", "bound", "prune", "var", "finalize",
+               "topk"):
         try:
             stage_ms[st] = [eng.stage_time(st)]
         except Exception:
@@ -619,11 +629,18 @@ def main():
         flops_var = 2.0 * m * n * d
         kernel = "k_gp_kstar<double, false> (K* = exp(-|x - u|^2 / 2), v_mfma_f64_16x16x4_f64)"
     if args.prune and prune_stats:
-        # the variance GEMM of the survivors (+ the 1024-candidate threshold set)
-        timed = prune_stats[-args.steps:]
-        surv = float(np.mean([s["survivors"] for s in timed]))
-        flops_var = (surv + min(m, 1024)) * n * (n + 1)
-        kernel += " [pruned: survivors + threshold set only]"
+        # a pruned round's dominant kernel is K* (with the mean in its epilogue):
+        # its fp64 contraction over the features it contracts in fp64 (the
+        # numeric ones in categorical mode; the one-hot blocks' int8 code
+        # product beside it is not counted), its "kstar" stage without the wait
+        # for the fit ("fit_wait")
+        var_ms = stages.get("kstar")
+        k64 = kstar_fp64_features(eng, d)
+        flops_var = 2.0 * m * n * k64
+        kernel = ("k_gp_kstar<double, true, %s> (K* with the mean k* . alpha in its epilogue, "
+                  "v_mfma_f64_16x16x4_f64 over %d fp64 features%s) [pruned round: the variance GEMM runs for the "
+                  "survivors only]" % ("true" if k64 < d else "false", k64,
+                                       " + the one-hot codes on v_mfma_i32_16x16x64_i8" if k64 < d else ""))
     achieved = flops_var / (var_ms * 1e-3) / 1e12 if var_ms else None
     peak = {64: PEAK_FP64_TFLOPS, 32: PEAK_FP32_TFLOPS, 16: PEAK_FP16_TFLOPS / 3.0}[args.precision]
     # HBM bytes per launch and the rocprof average duration were profiled on the

@@ -999,6 +999,7 @@ int gp_score_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, const ut
   // for L^-1.  fp32 keeps the mean in K*'s fp64 epilogue (k* . alpha, before
   // k* is rounded to fp32) and waits for the whole fit.
   if (c->fit_pending) UT_HIP(c, hipStreamWaitEvent(c->stream, fp32 ? c->ev_fit : c->ev_fit_x, 0));
+  mark(c, "fit_wait");   // (the wait is not K* time)
   const int32_t n = c->gp_n, d = c->gp_d;
   const int32_t npad = ((n + NPAD - 1) / NPAD) * NPAD;
   // the categorical K* when the candidates came through ut's encoder
@@ -1227,6 +1228,7 @@ int gp_topk_pruned_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, co
            "gp_topk_pruned: the score must increase with sigma (EI, or UCB with kappa >= 0)");
   UT_CHECK(c, k >= 1 && k <= 1024, UT_EINVAL, "gp_topk_pruned: k must be in [1, 1024]");
   if (c->fit_pending) UT_HIP(c, hipStreamWaitEvent(c->stream, c->ev_fit, 0));   // K* takes mu = k* . alpha
+  mark(c, "fit_wait");   // (the wait is not K* time)
   const int32_t n = c->gp_n, d = c->gp_d;
   const int32_t npad = ((n + NPAD - 1) / NPAD) * NPAD;
   const bool cat = feat_ours && c->cat_on;   // the categorical K* (features from ut's encoder)
