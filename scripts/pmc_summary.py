@@ -18,8 +18,8 @@ from collections import defaultdict
 
 STAGES = {  # stage key -> kernel-name prefixes (the first match wins)
     "var": ("void ut::k_gp_var_pp<false>(", "ut::k_gp_var_pp(", "void ut::k_gp_var<double>"), "var_1wg": ("void ut::k_gp_var<double>",),
-    "kstar": ("void ut::k_gp_kstar<double, false>",),
-    "var32": ("void ut::k_gp_var<float>",), "kstar32": ("void ut::k_gp_kstar<float, true>",),
+    "kstar": ("void ut::k_gp_kstar<double, false, false>", "void ut::k_gp_kstar<double, false>"),
+    "var32": ("void ut::k_gp_var<float>",), "kstar32": ("void ut::k_gp_kstar<float, true, false>", "void ut::k_gp_kstar<float, true>"),
     "hash": ("void ut::k_hash<true", "void ut::k_hash<", "ut::k_hash("),
     "propose": ("void ut::k_de<", "ut::k_de("), "encode": ("ut::k_encode_scaled", "ut::k_encode("), "prep_cand": ("ut::k_gp_prep_cand",),
     "finalize": ("ut::k_gp_finalize",),
