@@ -203,6 +203,15 @@ int ut_device_bytes(int32_t device, int64_t* bytes) {
   return 0;
 }
 
+// the fit stream: non-blocking, at the highest priority when c->fit_priority
+static hipError_t hip_create_fit_stream(ut_ctx* c) {
+  if (!c->fit_priority) return hipStreamCreateWithFlags(&c->fit_stream, hipStreamNonBlocking);
+  int lo = 0, hi = 0;
+  hipError_t e = hipDeviceGetStreamPriorityRange(&lo, &hi);
+  if (e != hipSuccess) return e;
+  return hipStreamCreateWithPriority(&c->fit_stream, hipStreamNonBlocking, hi);
+}
+
 int ut_ctx_create(int device, uint64_t seed, ut_ctx** out) {
   if (!out) return UT_EINVAL;
   *out = nullptr;
@@ -211,13 +220,14 @@ int ut_ctx_create(int device, uint64_t seed, ut_ctx** out) {
   if (hipSetDevice(device) != hipSuccess) return UT_EHIP;
   ut_ctx* c = new ut_ctx();
   c->device = device;
+  if (const char* e = getenv("UT_FIT_PRIORITY")) c->fit_priority = atoi(e) != 0;
   c->seed = seed;
   int ncu = 0;
   if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && ncu >= 8)
     c->n_cu = ncu;
   if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&c->fit_stream, hipStreamNonBlocking) != hipSuccess ||
+      hip_create_fit_stream(c) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_fit, hipEventDisableTiming) != hipSuccess ||
@@ -235,6 +245,7 @@ int ut_ctx_create(int device, uint64_t seed, ut_ctx** out) {
   if (const char* e = getenv("UT_DE_AOS")) c->de_aos = atoi(e) != 0;
   if (const char* e = getenv("UT_HASH_AFTER_FIT")) c->hash_after_fit = atoi(e);
   if (const char* e = getenv("UT_HASH_HOLD_LOWPREC")) c->hash_hold_lowprec = atoi(e) != 0;
+  if (const char* e = getenv("UT_HASH_HOLD_PRUNED")) c->hash_hold_pruned = atoi(e);
   if (const char* e = getenv("UT_HASH_AFTER_KSTAR")) c->hash_after_kstar = atoi(e);
   if (const char* e = getenv("UT_H3_SCHED")) c->h3_sched = atoi(e);
   if (const char* e = getenv("UT_VAR_SCHED")) c->var_sched = atoi(e);
@@ -876,7 +887,8 @@ static int score_round_de_impl(ut_ctx* c, const ut_de_params* de, const ut_acq* 
     UT_HIP(c, hipStreamWaitEvent(c->side, c->ev_fork, 0));
     StreamScope on_side(c, c->side);
     mark(c, "");
-    c->round_hash_hold = (prune_rows == 0 && (c->gp_fit_prec == 64 || c->hash_hold_lowprec)) ? c->hash_after_fit : 0;
+    c->round_hash_hold = prune_rows > 0 ? c->hash_hold_pruned
+                         : ((c->gp_fit_prec == 64 || c->hash_hold_lowprec) ? c->hash_after_fit : 0);
     int r = launch_hash_de(c, c->r_values.p, ld, m, cand_base, c->r_digest.p, true);
     c->round_hash_hold = 0;
     if (r) return r;

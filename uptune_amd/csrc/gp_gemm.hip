@@ -497,19 +497,20 @@ int launch_prep_cand(ut_ctx* c, const double* feat, int64_t ld, int64_t m, int32
 // encoder (ENUM blocks one-hot, BOOL 0 / 1): numeric U' and norms as
 // k_encode_scaled_cat writes them, codes from the blocks (the first 1.0 of an
 // ENUM block; no 1.0: no code, as for an out-of-range value)
-__global__ void k_gp_prep_cand_cat(const DevParam* __restrict__ params, int32_t P, const double* __restrict__ feat,
-                                   int64_t ld, int64_t m, const int32_t* __restrict__ num_feat, int32_t n_num,
-                                   int32_t dpad, const double* __restrict__ inv_ell,
-                                   const int32_t* __restrict__ cat_ccol, int32_t cat_k, double* __restrict__ u,
-                                   int64_t ldu, double* __restrict__ cn, int8_t* __restrict__ bcat) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= ldu) return;
-  const uint4 z = make_uint4(0u, 0u, 0u, 0u);
-  for (int32_t kb = 0; kb < cat_k / 128; ++kb) {
-    uint4* row = reinterpret_cast<uint4*>(bcat + ((int64_t)kb * ldu + i) * 128);
-#pragma unroll
-    for (int q = 0; q < 8; ++q) row[q] = z;
-  }
+__global__ __launch_bounds__(256) void k_gp_prep_cand_cat(const DevParam* __restrict__ params, int32_t P,
+                                                          const double* __restrict__ feat, int64_t ld, int64_t m,
+                                                          const int32_t* __restrict__ num_feat, int32_t n_num,
+                                                          int32_t dpad, const double* __restrict__ inv_ell,
+                                                          const int32_t* __restrict__ cat_ccol, int32_t cat_k,
+                                                          double* __restrict__ u, int64_t ldu,
+                                                          double* __restrict__ cn, int8_t* __restrict__ bcat) {
+  extern __shared__ uint32_t dyn[];
+  const int32_t stride = cat_k / 32 + 1;
+  uint32_t* bits = dyn;
+  uint32_t* img = dyn + 256 * stride;
+  const int t = threadIdx.x;
+  const int64_t i0 = (int64_t)blockIdx.x * 256, i = i0 + t;
+  for (int32_t w = 0; w < stride; ++w) bits[t * stride + w] = 0u;
   double s = 0.0;
   for (int32_t k = 0; k < dpad; ++k) {
     const int32_t f = k < n_num ? num_feat[k] : 0;
@@ -518,30 +519,35 @@ __global__ void k_gp_prep_cand_cat(const DevParam* __restrict__ params, int32_t 
     s += v * v;
   }
   cn[i] = s;
-  if (i >= m) return;
-  for (int32_t p = 0; p < P; ++p) {
-    const int32_t cc = cat_ccol[p];
-    if (cc < 0) continue;
-    const DevParam pr = params[p];
-    const double* x = feat + (int64_t)pr.feat_col * ld + i;
-    int32_t o = -1;
-    if (pr.kind == UT_BOOL) {
-      o = x[0] != 0.0 ? 1 : 0;
-    } else {
-      for (int32_t k = 0; k < (int32_t)pr.n_opt; ++k)
-        if (x[(int64_t)k * ld] == 1.0) { o = k; break; }
+  if (i < m) {
+    for (int32_t p = 0; p < P; ++p) {
+      const int32_t cc = cat_ccol[p];
+      if (cc < 0) continue;
+      const DevParam pr = params[p];
+      const double* x = feat + (int64_t)pr.feat_col * ld + i;
+      int32_t o = -1;
+      if (pr.kind == UT_BOOL) {
+        o = x[0] != 0.0 ? 1 : 0;
+      } else {
+        for (int32_t k = 0; k < (int32_t)pr.n_opt; ++k)
+          if (x[(int64_t)k * ld] == 1.0) { o = k; break; }
+      }
+      if (o < 0) continue;
+      const int32_t q = cc + o;
+      bits[t * stride + (q >> 5)] |= 1u << (q & 31);
     }
-    if (o < 0) continue;
-    const int32_t q = cc + o;
-    bcat[((int64_t)(q >> 7) * ldu + i) * 128 + (q & 127)] = 1;
   }
+  __syncthreads();
+  store_code_rows(bits, stride, cat_k / 128, img, bcat, ldu, i0);
 }
 
 int launch_prep_cand_cat(ut_ctx* c, const double* feat, int64_t ld, int64_t m, double* u, int32_t dpad, int64_t ldu,
                          double* cn, int8_t* bcat) {
   const Space& s = c->space;
-  hipLaunchKernelGGL(k_gp_prep_cand_cat, dim3(grid1(ldu, 256)), dim3(256), 0, c->stream, s.d_params, s.P, feat, ld, m,
-                     s.d_num_feat, s.n_num, dpad, c->gp_inv_ell, s.d_cat_ccol, s.cat_k, u, ldu, cn, bcat);
+  UT_CHECK(c, ldu % 256 == 0 && s.cat_k % 128 == 0, UT_EINVAL, "prep_cand_cat: bad padding");
+  hipLaunchKernelGGL(k_gp_prep_cand_cat, dim3((unsigned)(ldu / 256)), dim3(256), code_rows_lds(s.cat_k), c->stream,
+                     s.d_params, s.P, feat, ld, m, s.d_num_feat, s.n_num, dpad, c->gp_inv_ell, s.d_cat_ccol, s.cat_k,
+                     u, ldu, cn, bcat);
   UT_LAUNCH_CHECK(c);
   return 0;
 }

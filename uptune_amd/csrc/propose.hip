@@ -424,24 +424,26 @@ __global__ __launch_bounds__(256) void k_encode_scaled(const DevParam* __restric
 // the padding columns), cnorm[i] = |u'_i|^2 over the numeric features in
 // feature order, and the one-hot codes bcat[(q >> 7)][i][q & 127] = 1 at code
 // column q = ccol + option (ENUM), ccol + (value != 0) (BOOL); every code byte
-// of the candidate is written (zeros, then its ones)
+// of the candidate is written.  One thread per candidate, 256 per workgroup
+// (ldu % 256 == 0): each numeric feature of U' is written once (the padding
+// rows >= n_num zero) and |u'|^2 summed in feature order on the way; the codes
+// are set as bits in LDS and stored as whole 128-byte rows (store_code_rows:
+// the byte stores per candidate row made this kernel 18 ms at C4)
 __global__ __launch_bounds__(256) void k_encode_scaled_cat(const DevParam* __restrict__ params, int32_t P,
                                                            const double* __restrict__ vtab,
                                                            const double* __restrict__ values, int64_t ld, int64_t m,
-                                                           const int32_t* __restrict__ feat_num, int32_t dpad,
-                                                           const double* __restrict__ inv_ell,
+                                                           const int32_t* __restrict__ feat_num, int32_t n_num,
+                                                           int32_t dpad, const double* __restrict__ inv_ell,
                                                            const int32_t* __restrict__ cat_ccol, int32_t cat_k,
                                                            double* __restrict__ u, int64_t ldu, double* __restrict__ cn,
                                                            int8_t* __restrict__ bcat) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= ldu) return;
-  const uint4 z = make_uint4(0u, 0u, 0u, 0u);
-  for (int32_t kb = 0; kb < cat_k / 128; ++kb) {
-    uint4* row = reinterpret_cast<uint4*>(bcat + ((int64_t)kb * ldu + i) * 128);
-#pragma unroll
-    for (int q = 0; q < 8; ++q) row[q] = z;
-  }
-  for (int32_t k = 0; k < dpad; ++k) u[(int64_t)k * ldu + i] = 0.0;
+  extern __shared__ uint32_t dyn[];
+  const int32_t stride = cat_k / 32 + 1;
+  uint32_t* bits = dyn;
+  uint32_t* img = dyn + 256 * stride;
+  const int t = threadIdx.x;
+  const int64_t i0 = (int64_t)blockIdx.x * 256, i = i0 + t;
+  for (int32_t w = 0; w < stride; ++w) bits[t * stride + w] = 0u;
   double s = 0.0;
   if (i < m) {
     for (int32_t p = 0; p < P; ++p) {
@@ -449,24 +451,23 @@ __global__ __launch_bounds__(256) void k_encode_scaled_cat(const DevParam* __res
       const DevParam pr = params[p];
       if (cc >= 0) {
         const double v = values[(int64_t)pr.col * ld + i];
-        int64_t o = pr.kind == UT_BOOL ? (v != 0.0 ? 1 : 0) : (int64_t)v;
+        const int64_t o = pr.kind == UT_BOOL ? (v != 0.0 ? 1 : 0) : (int64_t)v;
         if (o < 0 || o >= (pr.kind == UT_BOOL ? 2 : pr.n_opt)) continue;   // no option: no match
         const int32_t q = cc + (int32_t)o;
-        bcat[((int64_t)(q >> 7) * ldu + i) * 128 + (q & 127)] = 1;
+        bits[t * stride + (q >> 5)] |= 1u << (q & 31);
         continue;
       }
       encode_param(pr, values, ld, i, vtab, [&](int32_t c, double f) {
         const double v = f * inv_ell[c];
         u[(int64_t)feat_num[c] * ldu + i] = v;
+        s += v * v;
       });
     }
-    // the norm in numeric-feature order (= feature order), as k_gp_num_train sums the training side
-    for (int32_t k = 0; k < dpad; ++k) {
-      const double v = u[(int64_t)k * ldu + i];
-      s += v * v;
-    }
   }
+  for (int32_t k = i < m ? n_num : 0; k < dpad; ++k) u[(int64_t)k * ldu + i] = 0.0;
   cn[i] = s;
+  __syncthreads();
+  store_code_rows(bits, stride, cat_k / 128, img, bcat, ldu, i0);
 }
 
 __global__ void k_gather_rows(int32_t NC, const double* __restrict__ values, int64_t ld,
@@ -929,8 +930,10 @@ int launch_encode_scaled(ut_ctx* c, const double* values, int64_t ld, int64_t m,
 int launch_encode_scaled_cat(ut_ctx* c, const double* values, int64_t ld, int64_t m, double* u, int32_t dpad,
                              int64_t ldu, double* cn, int8_t* bcat) {
   const Space& s = c->space;
-  hipLaunchKernelGGL(k_encode_scaled_cat, dim3(grid1(ldu, 256)), dim3(256), 0, c->stream, s.d_params, s.P, s.d_vtab,
-                     values, ld, m, s.d_feat_num, dpad, c->gp_inv_ell, s.d_cat_ccol, s.cat_k, u, ldu, cn, bcat);
+  UT_CHECK(c, ldu % 256 == 0 && s.cat_k % 128 == 0, UT_EINVAL, "encode_scaled_cat: bad padding");
+  hipLaunchKernelGGL(k_encode_scaled_cat, dim3((unsigned)(ldu / 256)), dim3(256), code_rows_lds(s.cat_k), c->stream,
+                     s.d_params, s.P, s.d_vtab, values, ld, m, s.d_feat_num, s.n_num, dpad, c->gp_inv_ell,
+                     s.d_cat_ccol, s.cat_k, u, ldu, cn, bcat);
   UT_LAUNCH_CHECK(c);
   return 0;
 }

@@ -203,6 +203,12 @@ struct ut_ctx {
   // 1: fp32 / f16x3 dense rounds hold the hash for an in-flight fit as well
   // (their K* waits for the whole fit anyway); UT_HASH_HOLD_LOWPREC
   int32_t hash_hold_lowprec = 0;
+  // the same for pruned rounds (their K* takes the mean from alpha, so it
+  // waits for the whole fit); UT_HASH_HOLD_PRUNED
+  int32_t hash_hold_pruned = 0;
+  // the fit stream at the device's highest stream priority (UT_FIT_PRIORITY=1):
+  // its chain of small kernels gets the CU slots freed by other streams first
+  bool fit_priority = false;
   // refit: the next diagonal block factored inside the trailing update
   // (k_chol_update_diag). -1 = from 2048 padded rows on: the fit alone 6.5 ->
   // 5.7 ms at n = 4096, C3 pruned 60.1 -> 59.2 ms; at C2 (n = 1024, the fit
@@ -525,6 +531,34 @@ int launch_prep_cand(ut_ctx* c, const double* feat, int64_t ld, int64_t m, int32
 // one-hot codes into c->bcat (from values, or from features made by ut's own
 // encoder)
 inline int32_t cat_dpad(const ut_ctx* c) { return kstar_dpad(c->space.n_num); }
+// the candidates' 128-byte code rows of one 256-candidate workgroup, written
+// coalesced: each thread sets its codes as bits in LDS (bits [256][stride],
+// stride = cat_k / 32 + 1 dwords), then every 128-column block is expanded to
+// bytes through an LDS image and stored as whole rows (propose.hip)
+__device__ inline void store_code_rows(const uint32_t* bits, int32_t stride, int32_t nkb, uint32_t* img, int8_t* bcat,
+                                int64_t ldu, int64_t i0) {
+  const int t = threadIdx.x;
+  for (int32_t kb = 0; kb < nkb; ++kb) {
+    // this thread's 128 codes of block kb: bits 4w .. 4w + 3 -> the 4 bytes of dword w
+#pragma unroll
+    for (int w = 0; w < 32; ++w) {
+      const uint32_t b = (bits[t * stride + kb * 4 + (w >> 3)] >> ((w & 7) * 4)) & 15u;
+      img[t * 33 + w] = (b & 1u) | ((b & 2u) << 7) | ((b & 4u) << 14) | ((b & 8u) << 21);
+    }
+    __syncthreads();
+    // the block's 256 rows of 128 bytes are contiguous in bcat: 16-byte stores in order
+    uint4* dst = reinterpret_cast<uint4*>(bcat + ((int64_t)kb * ldu + i0) * 128);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int e = q * 256 + t, r = e >> 3, c = e & 7;
+      const uint32_t* src = img + r * 33 + 4 * c;
+      dst[e] = make_uint4(src[0], src[1], src[2], src[3]);
+    }
+    __syncthreads();
+  }
+}
+
+inline size_t code_rows_lds(int32_t cat_k) { return sizeof(uint32_t) * 256 * ((cat_k / 32 + 1) + 33); }
 int launch_encode_scaled_cat(ut_ctx* c, const double* values, int64_t ld, int64_t m, double* u, int32_t dpad,
                              int64_t ldu, double* cn, int8_t* bcat);
 int launch_prep_cand_cat(ut_ctx* c, const double* feat, int64_t ld, int64_t m, double* u, int32_t dpad, int64_t ldu,
