@@ -247,6 +247,7 @@ int ut_ctx_create(int device, uint64_t seed, ut_ctx** out) {
   if (const char* e = getenv("UT_HASH_HOLD_LOWPREC")) c->hash_hold_lowprec = atoi(e) != 0;
   if (const char* e = getenv("UT_HASH_HOLD_PRUNED")) c->hash_hold_pruned = atoi(e);
   if (const char* e = getenv("UT_HASH_AFTER_KSTAR")) c->hash_after_kstar = atoi(e);
+  if (const char* e = getenv("UT_H3_REV")) c->h3_rev = atoi(e);
   if (const char* e = getenv("UT_H3_SCHED")) c->h3_sched = atoi(e);
   if (const char* e = getenv("UT_VAR_SCHED")) c->var_sched = atoi(e);
   if (const char* e = getenv("UT_CAT_KSTAR")) c->cat_enable = atoi(e) != 0;

@@ -1168,7 +1168,7 @@ __global__ __launch_bounds__(512, 2) void k_gp_var_h3(const _Float16* __restrict
                                                       int32_t RT2, int32_t CT, int64_t m, int32_t* __restrict__ ticket,
                                                       double* __restrict__ part, int64_t ldp,
                                                       const unsigned long long* __restrict__ amax_bits, int32_t kexp,
-                                                      int32_t sched, int32_t S) {
+                                                      int32_t sched, int32_t S, int32_t rev_short) {
   __shared__ __attribute__((aligned(16))) _Float16 lds[H3_NS * H3_STAGE + 8];
   int32_t& s_item = *reinterpret_cast<int32_t*>(lds + H3_NS * H3_STAGE);
   const int t = threadIdx.x, lane = t & 63;
@@ -1212,29 +1212,41 @@ __global__ __launch_bounds__(512, 2) void k_gp_var_h3(const _Float16* __restrict
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[i][jj][r] = 0.0f;
 
-    h3_issue<3>(Ab, a_lo, Bb, b_lo, lds, w, lane);   // stage 0 (nk >= 4: K and row0 + 256 are multiples of 128)
-    auto pipe = [&](int32_t kt) -> const _Float16* {
+    // rev (sched 1, the pair's second, short tile): its k stages in descending
+    // order.  The strip's P workgroups then read K* stage t (long tiles) or
+    // RT2 - t (short tiles, reversed) at step t of their items -- two stages
+    // per step across the strip instead of up to P -- so the L2 serves the
+    // rest.  (Ascending, each second tile restarted at stage 0 while the
+    // others were far ahead: 344 GB fetched per C3 launch for 32 GB of K*.)
+    const bool rev = rev_short && ri > 0;
+    auto ktof = [&](int32_t u) -> int32_t { return rev ? nk - 1 - u : u; };
+    h3_issue<3>(Ab + (int64_t)ktof(0) * H3_BLK, a_lo, Bb + (int64_t)ktof(0) * H3_BLK, b_lo, lds, w, lane);
+    auto pipe = [&](int32_t u) -> const _Float16* {
       wait_vmcnt<0>();
-      __builtin_amdgcn_s_barrier();   // stage kt landed everywhere; stage kt - 1 fully read
+      __builtin_amdgcn_s_barrier();   // step u landed everywhere; step u - 1 fully read
       asm volatile("" ::: "memory");
-      if (kt + 1 < nk)
-        h3_issue<1>(Ab + (int64_t)(kt + 1) * H3_BLK, a_lo, nullptr, 0, lds + ((kt + 1) & 1) * H3_STAGE, w, lane);
-      return lds + (kt & 1) * H3_STAGE;
+      if (u + 1 < nk)
+        h3_issue<1>(Ab + (int64_t)ktof(u + 1) * H3_BLK, a_lo, nullptr, 0, lds + ((u + 1) & 1) * H3_STAGE, w, lane);
+      return lds + (u & 1) * H3_STAGE;
     };
-    auto refill_b = [&](int32_t kt) {
-      return [&, kt]() {
-        if (kt + 1 < nk)
-          h3_issue<2>(nullptr, 0, Bb + (int64_t)(kt + 1) * H3_BLK, b_lo, lds + ((kt + 1) & 1) * H3_STAGE, w, lane);
+    auto refill_b = [&](int32_t u) {
+      return [&, u]() {
+        if (u + 1 < nk)
+          h3_issue<2>(nullptr, 0, Bb + (int64_t)ktof(u + 1) * H3_BLK, b_lo, lds + ((u + 1) & 1) * H3_STAGE, w, lane);
       };
     };
     const int32_t nfull = min(nk, row0 / H3_BK);
-    for (int32_t kt = 0; kt < nfull; ++kt) var_step_h3(pipe(kt), wm, wn, lane, 0, acc, refill_b(kt));
-    for (int32_t kt = nfull; kt < nk; ++kt) {
-      const _Float16* st = pipe(kt);
-      const int kd = kt - nfull - 2 * wm;   // 32-row blocks of this wave entirely above the diagonal
-      const int imin = kd < 0 ? 0 : kd;
-      if (imin < 2) var_step_h3(st, wm, wn, lane, imin, acc, refill_b(kt));
-      else refill_b(kt)();
+    for (int32_t u = 0; u < nk; ++u) {
+      const int32_t kt = ktof(u);
+      const _Float16* st = pipe(u);
+      if (kt < nfull) {
+        var_step_h3(st, wm, wn, lane, 0, acc, refill_b(u));
+      } else {
+        const int kd = kt - nfull - 2 * wm;   // 32-row blocks of this wave entirely above the diagonal
+        const int imin = kd < 0 ? 0 : kd;
+        if (imin < 2) var_step_h3(st, wm, wn, lane, imin, acc, refill_b(u));
+        else refill_b(u)();
+      }
     }
 
     __syncthreads();
@@ -1332,7 +1344,8 @@ int launch_gemm_var(ut_ctx* c, int prec, const void* LinvT, int64_t lda, const v
     const int32_t S2 = W / P2 > 1 ? W / P2 : 1;
     hipLaunchKernelGGL(k_gp_var_h3, dim3(nb2), dim3(512), 0, c->stream, (const _Float16*)LinvT, (int64_t)n256 * npad,
                        (const _Float16*)kst, ldk * (int64_t)npad, npad, RT2, (int32_t)((m + H3_BN - 1) / H3_BN), m,
-                       c->gp_ctr, part, ldk, amax, h3_kstar_exp(c->gp_sf2), c->h3_sched, S2);
+                       c->gp_ctr, part, ldk, amax, h3_kstar_exp(c->gp_sf2), c->h3_sched, S2,
+                       c->h3_sched == 1 ? c->h3_rev : 0);
   }
   else if (fp32)
     hipLaunchKernelGGL(k_gp_var<float>, dim3(nb), dim3(V_NT), 0, c->stream, (const float*)LinvT, lda,

@@ -228,6 +228,9 @@ struct ut_ctx {
   // k_gp_var_h3 item order: 0 = strip-major, 1 = paired row tiles in XCD
   // groups (L^-1 stages shared in L2 by the group's workgroups); UT_H3_SCHED
   int32_t h3_sched = 1;
+  // k_gp_var_h3 (sched 1): a pair's short tile walks k in descending order so the
+  // strip's workgroups read the same K* stages at the same step (UT_H3_REV)
+  int32_t h3_rev = 1;
   // k_gp_var_pp (fp64) item order: 0 = strip-major, 1 = paired row tiles in XCD groups (C2:
   // FETCH 41.1 -> 24.3 GB per launch, round 26.10-26.15 -> 25.99 ms; scripts/ab/r04c_varsched.sh); UT_VAR_SCHED
   int32_t var_sched = 1;
