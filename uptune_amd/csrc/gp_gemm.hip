@@ -1236,17 +1236,21 @@ __global__ __launch_bounds__(512, 2) void k_gp_var_h3(const _Float16* __restrict
       };
     };
     const int32_t nfull = min(nk, row0 / H3_BK);
-    for (int32_t u = 0; u < nk; ++u) {
-      const int32_t kt = ktof(u);
+    // (two plain loops per order: one loop with the full / diagonal test inside
+    // spilled 236 VGPRs and ran 3x slower)
+    auto diag_step = [&](int32_t u) {
       const _Float16* st = pipe(u);
-      if (kt < nfull) {
-        var_step_h3(st, wm, wn, lane, 0, acc, refill_b(u));
-      } else {
-        const int kd = kt - nfull - 2 * wm;   // 32-row blocks of this wave entirely above the diagonal
-        const int imin = kd < 0 ? 0 : kd;
-        if (imin < 2) var_step_h3(st, wm, wn, lane, imin, acc, refill_b(u));
-        else refill_b(u)();
-      }
+      const int kd = ktof(u) - nfull - 2 * wm;   // 32-row blocks of this wave entirely above the diagonal
+      const int imin = kd < 0 ? 0 : kd;
+      if (imin < 2) var_step_h3(st, wm, wn, lane, imin, acc, refill_b(u));
+      else refill_b(u)();
+    };
+    if (!rev) {
+      for (int32_t u = 0; u < nfull; ++u) var_step_h3(pipe(u), wm, wn, lane, 0, acc, refill_b(u));
+      for (int32_t u = nfull; u < nk; ++u) diag_step(u);
+    } else {
+      for (int32_t u = 0; u < nk - nfull; ++u) diag_step(u);
+      for (int32_t u = nk - nfull; u < nk; ++u) var_step_h3(pipe(u), wm, wn, lane, 0, acc, refill_b(u));
     }
 
     __syncthreads();
