@@ -29,6 +29,12 @@ ranks on fewer GPUs (records over gloo, merge on the device).
 `hbm_bytes_per_rank` is the device memory libuthot holds per rank (max over
 ranks; each rank caches inner digests for its own shard's DE targets only).
 
+`roofline` is the round's dominant kernel: the variance GEMM (fp64 / fp32 /
+f16x3 dense lines), K* where it carries more work (C4), and in a pruned line
+(--prune) the K* with the mean in its epilogue -- flops of its fp64
+contraction only (in categorical mode the one-hot blocks' int8 code product
+beside it is not counted), timed without the wait for the fit (`fit_wait`).
+
 After the timed rounds (outside the timed region) rank 0 checks the last
 round's selections against the oracle (`parity`: DE trials, hash_config
 digests, EI) and runs one extra round at a lengthscale whose EI top-k is
