@@ -246,6 +246,7 @@ int ut_ctx_create(int device, uint64_t seed, ut_ctx** out) {
   if (const char* e = getenv("UT_HASH_AFTER_FIT")) c->hash_after_fit = atoi(e);
   if (const char* e = getenv("UT_HASH_HOLD_LOWPREC")) c->hash_hold_lowprec = atoi(e) != 0;
   if (const char* e = getenv("UT_HASH_HOLD_PRUNED")) c->hash_hold_pruned = atoi(e);
+  if (const char* e = getenv("UT_HASH_WG_PER_CU")) c->hash_wg_per_cu = atoi(e);
   if (const char* e = getenv("UT_HASH_AFTER_KSTAR")) c->hash_after_kstar = atoi(e);
   if (const char* e = getenv("UT_H3_REV")) c->h3_rev = atoi(e);
   if (const char* e = getenv("UT_H3_SCHED")) c->h3_sched = atoi(e);

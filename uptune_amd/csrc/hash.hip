@@ -429,7 +429,9 @@ static int launch_hash_impl(ut_ctx* c, const double* values, int64_t ld, int64_t
     UT_LAUNCH_CHECK(c);
     pd = c->perm_dig.p;
   }
-  const int64_t nb = (int64_t)grid1(m, HASH_NT);
+  // (grid-stride: a cap on the grid leaves CU slots to the fit stream's kernels)
+  int64_t nb = (int64_t)grid1(m, HASH_NT);
+  if (c->hash_wg_per_cu > 0) nb = std::min<int64_t>(nb, (int64_t)c->n_cu * c->hash_wg_per_cu);
 #ifndef UT_HASH_REF_WAVES
 #define UT_HASH_REF_WAVES 4
 #endif
@@ -536,7 +538,8 @@ int launch_hash_de(ut_ctx* c, const double* values, int64_t ld, int64_t m, int64
     UT_LAUNCH_CHECK(c);
   }
   const int64_t want = ((int64_t)s.n_comp * m + HASH_NT - 1) / HASH_NT;
-  const unsigned grid = (unsigned)std::min<int64_t>(std::max<int64_t>(want, 1), (int64_t)c->n_cu * 8);
+  const unsigned grid = (unsigned)std::min<int64_t>(std::max<int64_t>(want, 1),
+                                                    (int64_t)c->n_cu * (c->hash_wg_per_cu > 0 ? c->hash_wg_per_cu : 8));
   const bool hold = c->round_hash_hold > 0 && c->fit_pending && hipEventQuery(c->ev_fit) == hipErrorNotReady;
   if (hold && c->round_hash_hold == 2) UT_HIP(c, hipStreamWaitEvent(c->stream, c->ev_fit, 0));
   hipLaunchKernelGGL(k_inner_pairs, dim3(grid), dim3(HASH_NT), 0, c->stream, s.d_params, s.d_comp, values, ld,

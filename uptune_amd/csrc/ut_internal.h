@@ -206,6 +206,9 @@ struct ut_ctx {
   // the same for pruned rounds (their K* takes the mean from alpha, so it
   // waits for the whole fit); UT_HASH_HOLD_PRUNED
   int32_t hash_hold_pruned = 0;
+  // > 0: the side stream's hash kernels (grid-stride) launch at most this many
+  // workgroups per CU, leaving slots for the fit's chain (UT_HASH_WG_PER_CU)
+  int32_t hash_wg_per_cu = 0;
   // the fit stream at the device's highest stream priority (UT_FIT_PRIORITY=1):
   // its chain of small kernels gets the CU slots freed by other streams first
   bool fit_priority = false;
