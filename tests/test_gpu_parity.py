@@ -1176,6 +1176,41 @@ def test_chol_fused_refit_bitwise_and_not_pd():
             os.environ["UT_CHOL_FUSE"] = old
 
 
+def test_trinv_big_bitwise():
+    """k_trinv_big (L^-1 levels of 256 rows and up on 128 x 128 tiles) gives
+    bitwise the inverse of k_trinv_level's 64 x 64 tiles (UT_TRINV_BIG=0 vs 1:
+    the posterior and EI of a batch are bitwise equal), with a ragged last
+    pair (npad 2304: level 2048 pairs 2048 rows with 256), and the posterior
+    matches the oracle"""
+    _require_gpu()
+    rng = np.random.default_rng(43)
+    n, d = 2200, 6
+    X = rng.uniform(size=(n, d))
+    y = np.sum((X - 0.4) ** 2, axis=1)
+    U = torch.from_numpy(np.ascontiguousarray(rng.uniform(size=(d, 3000)))).cuda()
+    U[:, :5] = torch.from_numpy(np.ascontiguousarray(X[:5].T)).cuda()
+    space = [Param("f%d" % i, FLOAT, 0.0, 1.0) for i in range(d)]
+    old = os.environ.get("UT_TRINV_BIG")
+    outs = []
+    try:
+        for big in ("0", "1"):
+            os.environ["UT_TRINV_BIG"] = big
+            e = engine(space, seed=2)
+            e.gp_fit(X, y, lengthscale=0.3, sigma_f2=1.0, sigma_n2=1e-6, jitter=1e-8)
+            outs.append([t.cpu() for t in e.gp_score(U, acq=e.acq("ei"))])
+            e.close()
+    finally:
+        if old is None:
+            os.environ.pop("UT_TRINV_BIG", None)
+        else:
+            os.environ["UT_TRINV_BIG"] = old
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+    mu, var = ogp.GP(X, y, lengthscale=0.3, sigma_f2=1.0, sigma_n2=1e-6, jitter=1e-8).posterior(U.cpu().numpy().T)
+    np.testing.assert_allclose(outs[1][0].numpy(), mu, rtol=RTOL, atol=ATOL)
+    np.testing.assert_allclose(outs[1][1].numpy(), var, rtol=RTOL, atol=ATOL)
+
+
 @pytest.mark.parametrize("which", ["hpl", "gcc", "mixed", "perm"])
 @pytest.mark.parametrize("prec", [64, 32, 16])
 def test_categorical_kstar_equals_dense(which, prec):

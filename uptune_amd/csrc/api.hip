@@ -238,6 +238,12 @@ int ut_ctx_create(int device, uint64_t seed, ut_ctx** out) {
   }
   c->stream = c->own_stream;
   if (const char* e = getenv("UT_CHOL_FUSE")) c->chol_fuse = atoi(e);
+  if (const char* e = getenv("UT_TRINV_BIG")) c->trinv_big = atoi(e);
+  if (const char* e = getenv("UT_FIT_SETPRIO")) c->fit_setprio = atoi(e);
+  if (ut::set_fit_prio(c->fit_setprio)) {
+    ut_ctx_destroy(c);
+    return UT_EHIP;
+  }
   if (const char* e = getenv("UT_JOIN_BEFORE_VAR")) c->join_before_var = atoi(e) != 0;
   if (const char* e = getenv("UT_VAR_KERNEL")) c->var_kernel = atoi(e);
   if (const char* e = getenv("UT_VAR_SPLIT")) c->var_split = atoi(e) != 0;

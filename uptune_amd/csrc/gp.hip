@@ -36,9 +36,25 @@ constexpr int NPAD = 128;  // training set padded to the GEMM row tile
 // ---------------------------------------------------------------------------
 // fit
 // ---------------------------------------------------------------------------
+// The fit's kernels are a chain of small, latency-bound launches on the fit
+// stream, beside the round's hash / proposal / encode on the other streams.
+// With g_fit_prio set (UT_FIT_SETPRIO) every fit wave raises its issue
+// priority (s_setprio 3): where it shares a SIMD with the hash's waves, its
+// instructions go first.
+__device__ int32_t g_fit_prio = 0;
+__device__ __forceinline__ void fit_prio() {
+  if (g_fit_prio) __builtin_amdgcn_s_setprio(3);
+}
+
+int set_fit_prio(int32_t on) {
+  if (hipMemcpyToSymbol(HIP_SYMBOL(g_fit_prio), &on, sizeof(on)) != hipSuccess) return UT_EHIP;
+  return set_fit_prio_gemm(on);
+}
+
 __global__ void k_gp_prep_train(const double* __restrict__ X, int32_t n, int32_t npad, int32_t d,
                                 const double* __restrict__ inv_ell, double* __restrict__ Xs,
                                 double* __restrict__ xnorm) {
+  fit_prio();
   const int32_t j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= npad) return;
   double s = 0.0;
@@ -56,6 +72,7 @@ __global__ void k_gp_prep_train(const double* __restrict__ X, int32_t n, int32_t
 __global__ void k_gp_num_train(const double* __restrict__ Xs, int32_t npad, int32_t d,
                                const int32_t* __restrict__ num_feat, int32_t n_num, int32_t dpad_num,
                                double* __restrict__ XsT_num, double* __restrict__ xnorm_num) {
+  fit_prio();
   const int32_t r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= npad) return;
   double s = 0.0;
@@ -73,6 +90,7 @@ __global__ void k_gp_num_train(const double* __restrict__ Xs, int32_t npad, int3
 __global__ void k_gp_cat_train(const DevParam* __restrict__ params, int32_t P, const int32_t* __restrict__ cat_ccol,
                                const double* __restrict__ X, int32_t n, int32_t d, int32_t npad,
                                int8_t* __restrict__ acat) {
+  fit_prio();
   const int32_t r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= n) return;
   for (int32_t p = 0; p < P; ++p) {
@@ -95,6 +113,7 @@ __global__ void k_gp_cat_train(const DevParam* __restrict__ params, int32_t P, c
 // mean / std (ddof=0) / standardise / f_best = min(ys); one workgroup
 __global__ __launch_bounds__(256) void k_gp_ystats(const double* __restrict__ y, int32_t n, int32_t npad,
                                                    double* __restrict__ ys, double* __restrict__ stats) {
+  fit_prio();
   __shared__ double red[256];
   const int t = threadIdx.x;
   double s = 0.0;
@@ -254,6 +273,7 @@ __device__ __forceinline__ void chol_diag_core(double (&a)[16], double* __restri
 
 __global__ __launch_bounds__(256) void k_chol_diag(double* __restrict__ K, double* __restrict__ Li, int32_t npad,
                                                    int32_t kb, int32_t* flag) {
+  fit_prio();
   __shared__ double col[2][NB];
   __shared__ double Ls[NB * (NB + 1)];
   __shared__ double invd[NB];
@@ -270,6 +290,7 @@ __global__ __launch_bounds__(256) void k_chol_diag(double* __restrict__ K, doubl
 // Panel kb, step 2: row block i > kb:  L_ik = A_ik * inv(L_kk)^T  (NT product)
 __global__ __launch_bounds__(256) void k_chol_rows(double* __restrict__ K, const double* __restrict__ Li,
                                                    int32_t npad, int32_t kb) {
+  fit_prio();
   __shared__ double As[16 * 80];
   __shared__ double Bs[16 * 80];
   const int64_t base = (int64_t)kb * NB, rb = (int64_t)(kb + 1 + blockIdx.x) * NB;
@@ -289,6 +310,7 @@ __global__ __launch_bounds__(256) void k_chol_rows(double* __restrict__ K, const
 
 // Trailing update A_ij -= L_i,kb L_j,kb^T for kb < j <= i < nb.
 __global__ __launch_bounds__(256) void k_chol_update(double* __restrict__ K, int32_t npad, int32_t kb) {
+  fit_prio();
   __shared__ double As[16 * 80];
   __shared__ double Bs[16 * 80];
   int32_t tid = blockIdx.x;
@@ -316,6 +338,7 @@ __global__ __launch_bounds__(256) void k_chol_update(double* __restrict__ K, int
 // fit's serial chain loses one launch per level (ut_ctx::chol_fuse)
 __global__ __launch_bounds__(256) void k_chol_update_diag(double* __restrict__ K, double* __restrict__ Li,
                                                           int32_t npad, int32_t kb, int32_t* flag) {
+  fit_prio();
   // As / Bs of the tile product, then (workgroup 0) Ls, col, invd of the diagonal block
   __shared__ double sm[NB * (NB + 1) + 2 * NB + NB];
   double* As = sm;
@@ -368,6 +391,7 @@ __global__ __launch_bounds__(256) void k_chol_update_diag(double* __restrict__ K
 __global__ __launch_bounds__(256) void k_gp_kmat(const double* __restrict__ Xs, const double* __restrict__ xnorm,
                                                  int32_t n, int32_t npad, int32_t d, double sf2, double diag,
                                                  double* __restrict__ K, int32_t rb0) {
+  fit_prio();
   __shared__ double As[16 * 80];
   __shared__ double Bs[16 * 80];
   const int64_t ib = (int64_t)(blockIdx.y + rb0) * 64, jb = (int64_t)blockIdx.x * 64;
@@ -406,6 +430,7 @@ __global__ __launch_bounds__(256) void k_gp_kmat(const double* __restrict__ Xs, 
 // the K range of each tile.
 __global__ __launch_bounds__(256) void k_trinv_level(const double* __restrict__ L, double* __restrict__ Li,
                                                      double* __restrict__ T, int32_t npad, int32_t s, int32_t phase) {
+  fit_prio();
   __shared__ double As[16 * 80];
   __shared__ double Bs[16 * 80];
   const int32_t z = blockIdx.z;
@@ -475,9 +500,116 @@ __global__ __launch_bounds__(256) void k_trinv_level(const double* __restrict__ 
       }
 }
 
+// The same two products for levels s >= TRB_MIN, where k_trinv_level's 64 x 64
+// tiles and plain loads dominate the fit (at n = 4096 the top level is 75 % of
+// the inverse's 23 GFLOP).  128 x 128 output tile per 256-thread workgroup
+// (2 x 2 waves of 64 x 64, 4 x 4 v_mfma_f64_16x16x4 sub-tiles each), 16-k
+// stages through a 2-deep global_load_lds ring (k_gp_var_pp's pipeline), two
+// workgroups per CU.
+//   right operand, [k][col] row-major (Ai, T): one 1-KiB wave-instruction per k row;
+//   left operand, [row][k] row-major (the L block, Ci): one wave-instruction
+//   moves 8 rows x 16 k; lane l fetches 16-B chunk (l & 7) ^ ((row >> 1) & 7)
+//   of its row, so an MFMA fragment read (16 rows at one k) hits 16 distinct
+//   bank pairs.
+// k runs upward in MFMA groups of 4 from a multiple of 64, as in k_trinv_level;
+// the extra products a 128-wide tile takes on are exact zeros of the
+// triangular operand, so the two kernels give the same bits.
+constexpr int TRB_MIN = 256, TRB_BM = 128, TRB_BK = 16, TRB_SL = TRB_BM * TRB_BK;
+
+__global__ __launch_bounds__(256, 2) void k_trinv_big(const double* __restrict__ L, double* __restrict__ Li,
+                                                      double* __restrict__ T, int32_t npad, int32_t s, int32_t phase) {
+  fit_prio();
+  // one __shared__ object (see k_gp_var): [stage][left | right]
+  __shared__ __attribute__((aligned(16))) double lds[2 * 2 * TRB_SL];
+  const int32_t z = blockIdx.z;
+  const int64_t o = (int64_t)z * 2 * s;
+  const int32_t s2 = (int32_t)min((int64_t)s, (int64_t)npad - o - s);  // multiple of 128 (npad % NPAD == 0)
+  const int32_t tr = blockIdx.y * TRB_BM, tc = blockIdx.x * TRB_BM;
+  if (s2 <= 0 || tr >= s2) return;
+  const double* A;
+  const double* B;
+  int64_t lda, ldb, ldc;
+  int32_t k_lo, k_hi;
+  double* C;
+  double sign;
+  if (phase == 0) {
+    A = L + (o + s) * npad + o; lda = npad;
+    B = Li + o * npad + o; ldb = npad;
+    k_lo = tc; k_hi = s;
+    C = T + (int64_t)z * s * s; ldc = s; sign = 1.0;
+  } else {
+    A = Li + (o + s) * npad + (o + s); lda = npad;
+    B = T + (int64_t)z * s * s; ldb = s;
+    k_lo = 0; k_hi = min(tr + TRB_BM, s2);
+    C = Li + (o + s) * npad + o; ldc = npad; sign = -1.0;
+  }
+  const int t = threadIdx.x, lane = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wm = w >> 1, wn = w & 1;
+  auto issue = [&](int32_t k0, double* st) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int q = 4 * w + u;
+      const int row = 8 * q + (lane >> 3);
+      const int ch = (lane & 7) ^ ((row >> 1) & 7);
+      __builtin_amdgcn_global_load_lds(A + (int64_t)(tr + row) * lda + k0 + 2 * ch,
+                                       (__attribute__((address_space(3))) void*)(st + q * 128), 16, 0, 0);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int q = 4 * w + u;
+      __builtin_amdgcn_global_load_lds(B + (int64_t)(k0 + q) * ldb + tc + lane * 2,
+                                       (__attribute__((address_space(3))) void*)(st + TRB_SL + q * 128), 16, 0, 0);
+    }
+  };
+  typedef double d4 __attribute__((ext_vector_type(4)));
+  d4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (d4){0.0, 0.0, 0.0, 0.0};
+  const int32_t nk = (k_hi - k_lo) / TRB_BK;
+  issue(k_lo, lds);
+  for (int32_t kt = 0; kt < nk; ++kt) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // stage kt landed everywhere; stage kt-1 fully read
+    asm volatile("" ::: "memory");
+    if (kt + 1 < nk) issue(k_lo + (kt + 1) * TRB_BK, lds + ((kt + 1) & 1) * 2 * TRB_SL);
+    const double* as = lds + (kt & 1) * 2 * TRB_SL;
+    const double* bs = as + TRB_SL;
+#pragma unroll
+    for (int ks = 0; ks < TRB_BK / 4; ++ks) {
+      const int kr = ks * 4 + (lane >> 4);
+      double af[4], bf[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bf[j] = bs[kr * TRB_BM + wn * 64 + j * 16 + (lane & 15)];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = wm * 64 + i * 16 + (lane & 15);
+        af[i] = as[row * TRB_BK + 2 * ((kr >> 1) ^ ((row >> 1) & 7)) + (kr & 1)];
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[i], bf[j], acc[i][j], 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = tr + wm * 64 + i * 16 + (lane >> 4) + 4 * r;
+        const int col = tc + wn * 64 + j * 16 + (lane & 15);
+        C[(int64_t)row * ldc + col] = sign * acc[i][j][r];
+      }
+}
+
 // out = Linv * v  (one wave per row)
 __global__ __launch_bounds__(256) void k_lower_mv(const double* __restrict__ Li, int32_t npad,
                                                   const double* __restrict__ v, double* __restrict__ out) {
+  fit_prio();
   const int32_t r = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (r >= npad) return;
@@ -492,6 +624,7 @@ __global__ __launch_bounds__(256) void k_lower_mv(const double* __restrict__ Li,
 // L^-1 ran on npad / 64 workgroups at ~250 GB/s)
 __global__ __launch_bounds__(256) void k_upper_mv(const double* __restrict__ LiT, int32_t npad,
                                                   const double* __restrict__ v, double* __restrict__ out) {
+  fit_prio();
   const int32_t r = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (r >= npad) return;
@@ -541,6 +674,7 @@ template <int MODE>
 __global__ __launch_bounds__(256) void k_app_part(const double* __restrict__ Li, const double* __restrict__ LinvT,
                                                   const double* __restrict__ K, const double* __restrict__ T,
                                                   int32_t npad, int32_t b, int32_t maxq, double* __restrict__ W) {
+  fit_prio();
   __shared__ double As[16 * 80];
   __shared__ double Bs[16 * 80];
   const int64_t q = blockIdx.x, t = blockIdx.y;
@@ -569,6 +703,7 @@ __global__ __launch_bounds__(256) void k_app_red(const double* __restrict__ Li, 
                                                  double* __restrict__ K, double* __restrict__ T, int32_t npad,
                                                  int32_t b, int32_t maxq, const double* __restrict__ W,
                                                  double* __restrict__ Et) {
+  fit_prio();
   const int64_t t = blockIdx.x, base = (int64_t)b * 64;
   const AppGemm g = app_gemm<MODE>(Li, LinvT, K, T, npad, b, t);
   const int32_t nq = (g.khi - g.klo + APP_KC - 1) / APP_KC;
@@ -587,6 +722,7 @@ __global__ __launch_bounds__(256) void k_app_red(const double* __restrict__ Li, 
 // LinvT); workgroup cb == b copies D^-1 (k_chol_diag's output) into LinvT
 __global__ __launch_bounds__(256) void k_app_c(double* __restrict__ Li, double* __restrict__ LinvT,
                                                const double* __restrict__ Et, int32_t npad, int32_t b) {
+  fit_prio();
   __shared__ double As[16 * 80];
   __shared__ double Bs[16 * 80];
   const int64_t cb = blockIdx.x, base = (int64_t)b * 64;
@@ -907,6 +1043,12 @@ int gp_fit_enqueue(ut_ctx* c, const double* X, const double* y, int32_t n, int32
     // off-diagonal blocks of L^-1 by recursive doubling (diagonal blocks came from k_chol_diag)
     for (int32_t lv = NB; lv < npad; lv *= 2) {
       const int32_t pairs = (int32_t)((npad - lv + 2 * lv - 1) / (2 * lv));
+      if (c->trinv_big && lv >= TRB_MIN) {
+        const dim3 gb(lv / TRB_BM, lv / TRB_BM, pairs);
+        hipLaunchKernelGGL(k_trinv_big, gb, dim3(256), 0, c->stream, c->gp_K, c->gp_Linv, c->gp_T, npad, lv, 0);
+        hipLaunchKernelGGL(k_trinv_big, gb, dim3(256), 0, c->stream, c->gp_K, c->gp_Linv, c->gp_T, npad, lv, 1);
+        continue;
+      }
       const dim3 grid(lv / 64, lv / 64, pairs);
       hipLaunchKernelGGL(k_trinv_level, grid, dim3(256), 0, c->stream, c->gp_K, c->gp_Linv, c->gp_T, npad, lv, 0);
       hipLaunchKernelGGL(k_trinv_level, grid, dim3(256), 0, c->stream, c->gp_K, c->gp_Linv, c->gp_T, npad, lv, 1);

@@ -15,7 +15,18 @@
 
 namespace ut {
 
+// the fit kernels here (see gp.hip g_fit_prio): s_setprio 3 when set
+__device__ int32_t g_fit_prio_g = 0;
+__device__ __forceinline__ void fit_prio_g() {
+  if (g_fit_prio_g) __builtin_amdgcn_s_setprio(3);
+}
+
+int set_fit_prio_gemm(int32_t on) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_fit_prio_g), &on, sizeof(on)) == hipSuccess ? 0 : UT_EHIP;
+}
+
 __global__ void k_to_f32(const double* __restrict__ src, float* __restrict__ dst, int64_t n) {
+  fit_prio_g();
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) dst[i] = (float)src[i];
 }
@@ -555,6 +566,7 @@ int launch_prep_cand_cat(ut_ctx* c, const double* feat, int64_t ld, int64_t m, d
 // Xs^T [dpad][npad] from Xs [npad][d] (rows >= d zero)
 __global__ void k_gp_xs_t(const double* __restrict__ Xs, int32_t npad, int32_t d, int32_t dpad,
                           double* __restrict__ XsT) {
+  fit_prio_g();
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= (int64_t)dpad * npad) return;
   const int32_t k = (int32_t)(e / npad), r = (int32_t)(e % npad);
@@ -1279,6 +1291,7 @@ __global__ __launch_bounds__(512, 2) void k_gp_var_h3(const _Float16* __restrict
 // max |x| over cnt doubles into *out (as bits: non-negative doubles order like their bits)
 __global__ __launch_bounds__(256) void k_absmax(const double* __restrict__ x, int64_t cnt,
                                                 unsigned long long* __restrict__ out) {
+  fit_prio_g();
   double v = 0.0;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < cnt; i += (int64_t)gridDim.x * blockDim.x)
     v = fmax(v, fabs(x[i]));
@@ -1297,6 +1310,7 @@ __global__ __launch_bounds__(256) void k_absmax(const double* __restrict__ x, in
 // the lo plane n256 * n elements after the hi plane)
 __global__ void k_split_h3(const double* __restrict__ x, int32_t n, int32_t n256,
                            const unsigned long long* __restrict__ amax_bits, _Float16* __restrict__ dst) {
+  fit_prio_g();
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= (int64_t)n256 * n) return;
   const int64_t r = i / n;
@@ -1396,6 +1410,7 @@ int launch_gemm_var(ut_ctx* c, int prec, const void* LinvT, int64_t lda, const v
 // dst[c][r] = src[r][c] (n x n, n % 64 == 0), optionally also as fp32
 __global__ __launch_bounds__(256) void k_transpose(const double* __restrict__ src, int32_t n, double* __restrict__ dst,
                                                    float* __restrict__ dst_f) {
+  fit_prio_g();
   __shared__ double tile[64][65];
   const int32_t r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;

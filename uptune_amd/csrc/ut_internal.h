@@ -212,11 +212,16 @@ struct ut_ctx {
   // the fit stream at the device's highest stream priority (UT_FIT_PRIORITY=1):
   // its chain of small kernels gets the CU slots freed by other streams first
   bool fit_priority = false;
+  // the fit kernels' waves at s_setprio 3 (gp.hip g_fit_prio); UT_FIT_SETPRIO
+  int32_t fit_setprio = 0;
   // refit: the next diagonal block factored inside the trailing update
   // (k_chol_update_diag). -1 = from 2048 padded rows on: the fit alone 6.5 ->
   // 5.7 ms at n = 4096, C3 pruned 60.1 -> 59.2 ms; at C2 (n = 1024, the fit
   // beside K*) the heavier update workgroups cost the round 0.25 ms. UT_CHOL_FUSE
   int32_t chol_fuse = -1;
+  // L^-1 levels of 256 rows and more on k_trinv_big (128 x 128 tiles, glds
+  // ring) instead of k_trinv_level (64 x 64 tiles, plain loads); UT_TRINV_BIG
+  int32_t trinv_big = 1;
   // fp32 / f16x3 dense rounds: 1 = enqueue the hash after K* (their K* waits
   // for the whole fit, which the hash would otherwise crowd out of the CUs: at
   // n = 4096 the refit stretches from ~6 to ~14 ms beside it) and let the
@@ -578,6 +583,9 @@ int launch_transpose(ut_ctx* c, const double* src, int32_t n, double* dst, float
 int launch_split_h3(ut_ctx* c, const double* Linv, int32_t n, _Float16* dst);
 constexpr int VAR_BM = 128, VAR_BN = 256;  // variance-contraction tile (rows of L^-1 x candidates)
 int launch_to_f32(ut_ctx* c, const double* src, float* dst, int64_t n);
+// gp.hip: the fit kernels' issue priority (UT_FIT_SETPRIO; process-wide)
+int set_fit_prio(int32_t on);
+int set_fit_prio_gemm(int32_t on);   // gp_gemm.hip's fit kernels
 int launch_gather_rows(ut_ctx* c, const double* values, int64_t ld, const int64_t* idx, int64_t cand_base,
                        int32_t k, double* out, int64_t ldo, const uint32_t* dig, uint32_t* out_dig);
 // comm.hip: release the context's communicator (ut_ctx_destroy)
