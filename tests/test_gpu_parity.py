@@ -222,6 +222,32 @@ def test_hash_de_shard_window(which):
             assert hexes(e.hash_de(trial, base)) == hexes(e.hash(trial))
 
 
+@pytest.mark.parametrize("which", ["r64", "hpl"])
+def test_hash_capped_grid(which):
+    """the grid-stride hash kernels with their grids capped at one workgroup
+    per CU (UT_HASH_WG_PER_CU=1: what a round does while a large refit runs,
+    at 4) give the digests of the full grids, for ut_hash_de and ut_hash"""
+    space = {"r64": r64_space, "hpl": hpl_space}[which]()
+    m, base = 200000, 0
+    outs = []
+    old = os.environ.get("UT_HASH_WG_PER_CU")
+    try:
+        for cap in ("0", "1"):
+            os.environ["UT_HASH_WG_PER_CU"] = cap
+            e = engine(space, seed=39)
+            e.population_init(m, round_=1)
+            trial = e.propose_de(m, round_=2, cand_base=base, cr=0.2)
+            outs.append((e.hash_de(trial, base).cpu(), e.hash(trial).cpu()))
+            e.close()
+    finally:
+        if old is None:
+            os.environ.pop("UT_HASH_WG_PER_CU", None)
+        else:
+            os.environ["UT_HASH_WG_PER_CU"] = old
+    (a_de, a), (b_de, b) = outs
+    assert torch.equal(a_de, a) and torch.equal(b_de, b) and torch.equal(a, b)
+
+
 def test_hash_small_m_of_a_wide_array():
     """a few columns of a wide SoA array (ld much larger than m): the small-m
     path sizes its scratch by m, not by ld, and the digests equal

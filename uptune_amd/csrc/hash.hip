@@ -416,6 +416,28 @@ __global__ __launch_bounds__(HASH_NT, MINW) void k_hash(const DevParam* __restri
   }
 }
 
+// Workgroups per CU for the grid-stride hash grids (0 = uncapped).  A large
+// refit (>= HASH_CAP_MIN_NPAD padded rows) still running when the hash is
+// enqueued is a chain of small latency-bound kernels the round's scoring
+// waits for; a full hash grid takes every CU slot it frees, so the chain runs
+// ~2.5x longer than alone.  Capped (with the fit's waves at s_setprio 3), the
+// chain keeps slots and the hash, off the critical path, takes ~2x longer.
+// Only for hashes of at most HASH_CAP_MAX_BLOCKS outer SHA-256 blocks, which
+// stay off the critical path at half speed.  Measured, C3 (n 4096, 2^21
+// candidates): pruned 39.6 -> 36.7-37.5 ms, f16x3 119.7 -> 115.6 ms; C2
+// (n 1024) 26.2 -> 29.2 ms and C4 (2^22 x 472 blocks) 191 -> 247 ms had they
+// been capped (scripts/ab/r04s_fitprio.sh, r04t_capsweep.sh).
+// UT_HASH_WG_PER_CU: N > 0 always N, 0 never, -1 (default) as above.
+constexpr int32_t HASH_CAP_MIN_NPAD = 2048, HASH_CAP_WG = 4;
+constexpr double HASH_CAP_MAX_BLOCKS = 5e8;
+
+static int32_t hash_cap(ut_ctx* c, int64_t m) {
+  if (c->hash_wg_per_cu >= 0) return c->hash_wg_per_cu;
+  if (!c->fit_pending || c->gp_npad_fit < HASH_CAP_MIN_NPAD) return 0;
+  if ((double)m * (double)c->space.outer_blocks > HASH_CAP_MAX_BLOCKS) return 0;
+  return hipEventQuery(c->ev_fit) == hipErrorNotReady ? HASH_CAP_WG : 0;
+}
+
 static int launch_hash_impl(ut_ctx* c, const double* values, int64_t ld, int64_t m, uint32_t* out, InnerRef ref) {
   if (m <= 0) return 0;
   const Space& s = c->space;
@@ -431,7 +453,7 @@ static int launch_hash_impl(ut_ctx* c, const double* values, int64_t ld, int64_t
   }
   // (grid-stride: a cap on the grid leaves CU slots to the fit stream's kernels)
   int64_t nb = (int64_t)grid1(m, HASH_NT);
-  if (c->hash_wg_per_cu > 0) nb = std::min<int64_t>(nb, (int64_t)c->n_cu * c->hash_wg_per_cu);
+  if (const int32_t cap = hash_cap(c, m)) nb = std::min<int64_t>(nb, (int64_t)c->n_cu * cap);
 #ifndef UT_HASH_REF_WAVES
 #define UT_HASH_REF_WAVES 4
 #endif
@@ -538,8 +560,8 @@ int launch_hash_de(ut_ctx* c, const double* values, int64_t ld, int64_t m, int64
     UT_LAUNCH_CHECK(c);
   }
   const int64_t want = ((int64_t)s.n_comp * m + HASH_NT - 1) / HASH_NT;
-  const unsigned grid = (unsigned)std::min<int64_t>(std::max<int64_t>(want, 1),
-                                                    (int64_t)c->n_cu * (c->hash_wg_per_cu > 0 ? c->hash_wg_per_cu : 8));
+  const int32_t cap = hash_cap(c, m);
+  const unsigned grid = (unsigned)std::min<int64_t>(std::max<int64_t>(want, 1), (int64_t)c->n_cu * (cap > 0 ? cap : 8));
   const bool hold = c->round_hash_hold > 0 && c->fit_pending && hipEventQuery(c->ev_fit) == hipErrorNotReady;
   if (hold && c->round_hash_hold == 2) UT_HIP(c, hipStreamWaitEvent(c->stream, c->ev_fit, 0));
   hipLaunchKernelGGL(k_inner_pairs, dim3(grid), dim3(HASH_NT), 0, c->stream, s.d_params, s.d_comp, values, ld,

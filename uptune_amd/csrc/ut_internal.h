@@ -206,14 +206,15 @@ struct ut_ctx {
   // the same for pruned rounds (their K* takes the mean from alpha, so it
   // waits for the whole fit); UT_HASH_HOLD_PRUNED
   int32_t hash_hold_pruned = 0;
-  // > 0: the side stream's hash kernels (grid-stride) launch at most this many
-  // workgroups per CU, leaving slots for the fit's chain (UT_HASH_WG_PER_CU)
-  int32_t hash_wg_per_cu = 0;
+  // the grid-stride hash kernels' workgroups per CU: > 0 at most this many, 0
+  // uncapped, -1 capped while a large refit is in flight (hash.hip hash_cap);
+  // UT_HASH_WG_PER_CU
+  int32_t hash_wg_per_cu = -1;
   // the fit stream at the device's highest stream priority (UT_FIT_PRIORITY=1):
   // its chain of small kernels gets the CU slots freed by other streams first
   bool fit_priority = false;
   // the fit kernels' waves at s_setprio 3 (gp.hip g_fit_prio); UT_FIT_SETPRIO
-  int32_t fit_setprio = 0;
+  int32_t fit_setprio = 1;
   // refit: the next diagonal block factored inside the trailing update
   // (k_chol_update_diag). -1 = from 2048 padded rows on: the fit alone 6.5 ->
   // 5.7 ms at n = 4096, C3 pruned 60.1 -> 59.2 ms; at C2 (n = 1024, the fit
