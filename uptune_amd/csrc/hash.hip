@@ -418,27 +418,35 @@ __global__ __launch_bounds__(HASH_NT, MINW) void k_hash(const DevParam* __restri
 
 // Workgroups per CU for the grid-stride hash grids (0 = uncapped).  A large
 // refit (>= HASH_CAP_MIN_NPAD padded rows) still running when the hash is
-// enqueued is a chain of small latency-bound kernels the round's scoring
-// waits for; a full hash grid takes every CU slot it frees, so the chain runs
-// ~2.5x longer than alone.  Capped (with the fit's waves at s_setprio 3), the
-// chain keeps slots and the hash, off the critical path, takes ~2x longer.
-// Only for hashes of at most HASH_CAP_MAX_BLOCKS outer SHA-256 blocks, which
-// stay off the critical path at half speed.  Measured, C3 (n 4096, 2^21
-// candidates): pruned 39.6 -> 36.7-37.5 ms, f16x3 119.7 -> 115.6 ms; C2
-// (n 1024) 26.2 -> 29.2 ms and C4 (2^22 x 472 blocks) 191 -> 247 ms had they
-// been capped (scripts/ab/r04s_fitprio.sh, r04t_capsweep.sh).
+// enqueued (and not waited for by the hash's stream first) is a chain of small
+// latency-bound kernels the round's scoring waits for; a full hash grid takes
+// every CU slot the chain frees, so the chain runs ~2.5x longer than alone.
+// Capped (with the fit's waves at s_setprio 3), the chain keeps slots and the
+// hash, off the critical path, takes ~2x longer.  Only for hashes small enough
+// to stay off the critical path at half speed (m x components <=
+// HASH_CAP_MAX_PAIRS for the inner digests, m x outer blocks <=
+// HASH_CAP_MAX_BLOCKS for the outer hash).  Measured: C3 (n 4096, 2^21
+// candidates) pruned 39.6 -> 36.7-37.5 ms, f16x3 119.7 -> 115.6 ms; capped,
+// C2 (n 1024) went 26.2 -> 29.2 ms, C4 (2^22 x 472 blocks) 191 -> 247 ms, and
+// C2 f16x3 with only its inner digests capped 11.44 -> 11.79 ms (its fit_wait
+// 4.0 -> 1.5 ms, but the hash then overlapped K*: 3.4 -> 5.0 ms)
+// (scripts/ab/r04s_fitprio.sh, r04t_capsweep.sh, r04x_innercap.sh).
 // UT_HASH_WG_PER_CU: N > 0 always N, 0 never, -1 (default) as above.
 constexpr int32_t HASH_CAP_MIN_NPAD = 2048, HASH_CAP_WG = 4;
-constexpr double HASH_CAP_MAX_BLOCKS = 5e8;
+constexpr double HASH_CAP_MAX_BLOCKS = 5e8, HASH_CAP_MAX_PAIRS = 268435456.0;
 
-static int32_t hash_cap(ut_ctx* c, int64_t m) {
+static int32_t hash_cap(ut_ctx* c, int64_t m, bool outer, bool after_fit) {
   if (c->hash_wg_per_cu >= 0) return c->hash_wg_per_cu;
-  if (!c->fit_pending || c->gp_npad_fit < HASH_CAP_MIN_NPAD) return 0;
-  if ((double)m * (double)c->space.outer_blocks > HASH_CAP_MAX_BLOCKS) return 0;
+  if (after_fit || !c->fit_pending) return 0;
+  if (c->gp_npad_fit < HASH_CAP_MIN_NPAD) return 0;
+  if (outer ? (double)m * (double)c->space.outer_blocks > HASH_CAP_MAX_BLOCKS
+            : (double)m * (double)c->space.n_comp > HASH_CAP_MAX_PAIRS)
+    return 0;
   return hipEventQuery(c->ev_fit) == hipErrorNotReady ? HASH_CAP_WG : 0;
 }
 
-static int launch_hash_impl(ut_ctx* c, const double* values, int64_t ld, int64_t m, uint32_t* out, InnerRef ref) {
+static int launch_hash_impl(ut_ctx* c, const double* values, int64_t ld, int64_t m, uint32_t* out, InnerRef ref,
+                            bool after_fit = false) {
   if (m <= 0) return 0;
   const Space& s = c->space;
   const uint32_t* pd = nullptr;
@@ -453,7 +461,7 @@ static int launch_hash_impl(ut_ctx* c, const double* values, int64_t ld, int64_t
   }
   // (grid-stride: a cap on the grid leaves CU slots to the fit stream's kernels)
   int64_t nb = (int64_t)grid1(m, HASH_NT);
-  if (const int32_t cap = hash_cap(c, m)) nb = std::min<int64_t>(nb, (int64_t)c->n_cu * cap);
+  if (const int32_t cap = hash_cap(c, m, true, after_fit)) nb = std::min<int64_t>(nb, (int64_t)c->n_cu * cap);
 #ifndef UT_HASH_REF_WAVES
 #define UT_HASH_REF_WAVES 4
 #endif
@@ -560,9 +568,9 @@ int launch_hash_de(ut_ctx* c, const double* values, int64_t ld, int64_t m, int64
     UT_LAUNCH_CHECK(c);
   }
   const int64_t want = ((int64_t)s.n_comp * m + HASH_NT - 1) / HASH_NT;
-  const int32_t cap = hash_cap(c, m);
-  const unsigned grid = (unsigned)std::min<int64_t>(std::max<int64_t>(want, 1), (int64_t)c->n_cu * (cap > 0 ? cap : 8));
   const bool hold = c->round_hash_hold > 0 && c->fit_pending && hipEventQuery(c->ev_fit) == hipErrorNotReady;
+  const int32_t cap = hash_cap(c, m, false, hold && c->round_hash_hold == 2);
+  const unsigned grid = (unsigned)std::min<int64_t>(std::max<int64_t>(want, 1), (int64_t)c->n_cu * (cap > 0 ? cap : 8));
   if (hold && c->round_hash_hold == 2) UT_HIP(c, hipStreamWaitEvent(c->stream, c->ev_fit, 0));
   hipLaunchKernelGGL(k_inner_pairs, dim3(grid), dim3(HASH_NT), 0, c->stream, s.d_params, s.d_comp, values, ld,
                      c->r_pairs.p, np, reinterpret_cast<uint4*>(c->r_fresh.p));
@@ -571,7 +579,8 @@ int launch_hash_de(ut_ctx* c, const double* values, int64_t ld, int64_t m, int64
   return launch_hash_impl(c, values, ld, m, out,
                           InnerRef{c->r_mask.p, reinterpret_cast<const uint4*>(c->r_fresh.p),
                                    reinterpret_cast<const uint4*>(c->pop_dig), c->npop, cand_base, c->pop_dig_lo,
-                                   c->pop_dig_n, ld});
+                                   c->pop_dig_n, ld},
+                          hold);
 }
 
 int launch_hash_parent(ut_ctx* c, const double* values, int64_t ld, int64_t m, const double* parent, uint32_t* out) {
