@@ -1237,6 +1237,44 @@ def test_trinv_big_bitwise():
     np.testing.assert_allclose(outs[1][1].numpy(), var, rtol=RTOL, atol=ATOL)
 
 
+@pytest.mark.parametrize("n", [300, 2200])
+def test_chol_merged_bitwise(n):
+    """the diagonal blocks' inverse solved inside the Cholesky column loop
+    (UT_CHOL_MERGED=1, the default) gives bitwise the factor and inverse of the
+    separate substitution sweep (=0): unfused k_chol_diag at n = 300, the
+    fused k_chol_update_diag at n = 2200 (posterior and EI bitwise equal),
+    and an appended fit on top of each matches its refit within RTOL"""
+    _require_gpu()
+    rng = np.random.default_rng(47)
+    d = 6
+    X = rng.uniform(size=(n + 40, d))
+    y = np.sum((X - 0.4) ** 2, axis=1)
+    U = torch.from_numpy(np.ascontiguousarray(rng.uniform(size=(d, 2000)))).cuda()
+    space = [Param("f%d" % i, FLOAT, 0.0, 1.0) for i in range(d)]
+    old = os.environ.get("UT_CHOL_MERGED")
+    outs = []
+    try:
+        for merged in ("0", "1"):
+            os.environ["UT_CHOL_MERGED"] = merged
+            e = engine(space, seed=2)
+            e.gp_fit(X[:n], y[:n], lengthscale=0.3, sigma_f2=1.0, sigma_n2=1e-6, jitter=1e-8)
+            full = [t.cpu() for t in e.gp_score(U, acq=e.acq("ei"))]
+            e.gp_fit(X, y, lengthscale=0.3, sigma_f2=1.0, sigma_n2=1e-6, jitter=1e-8)   # appended rows
+            outs.append((full, [t.cpu() for t in e.gp_score(U, acq=e.acq("ei"))]))
+            e.close()
+    finally:
+        if old is None:
+            os.environ.pop("UT_CHOL_MERGED", None)
+        else:
+            os.environ["UT_CHOL_MERGED"] = old
+    for a, b in zip(outs[0][0], outs[1][0]):
+        assert torch.equal(a, b)
+    mu, var = ogp.GP(X, y, lengthscale=0.3, sigma_f2=1.0, sigma_n2=1e-6, jitter=1e-8).posterior(U.cpu().numpy().T)
+    for app in (outs[0][1], outs[1][1]):
+        np.testing.assert_allclose(app[0].numpy(), mu, rtol=RTOL, atol=ATOL)
+        np.testing.assert_allclose(app[1].numpy(), var, rtol=RTOL, atol=ATOL)
+
+
 @pytest.mark.parametrize("which", ["hpl", "gcc", "mixed", "perm"])
 @pytest.mark.parametrize("prec", [64, 32, 16])
 def test_categorical_kstar_equals_dense(which, prec):

@@ -239,6 +239,7 @@ int ut_ctx_create(int device, uint64_t seed, ut_ctx** out) {
   c->stream = c->own_stream;
   if (const char* e = getenv("UT_CHOL_FUSE")) c->chol_fuse = atoi(e);
   if (const char* e = getenv("UT_TRINV_BIG")) c->trinv_big = atoi(e);
+  if (const char* e = getenv("UT_CHOL_MERGED")) c->chol_merged = atoi(e);
   if (const char* e = getenv("UT_FIT_SETPRIO")) c->fit_setprio = atoi(e);
   if (ut::set_fit_prio(c->fit_setprio)) {
     ut_ctx_destroy(c);

@@ -217,7 +217,16 @@ __device__ __forceinline__ double readlane_f64(double v, int lane) {
 }
 
 // the diagonal block kb from a[] (thread t: row t & 63, columns 16 (t >> 6) ..
-// + 15 of the updated block); col [2][NB], Ls [NB][NB + 1], invd [NB] in LDS
+// + 15 of the updated block); col [2][NB], Ls [NB][NB + 1], invd [NB] in LDS.
+// MERGED (ut_ctx::chol_merged): the substitution for inv(L_kk) runs inside the
+// column loop instead of after it: at step c, row c of the solution is final
+// (its accumulator took every earlier column's update), so each wave reads it
+// from lane c and applies column c of L to the rows below, behind the same
+// barrier as the factor's rank-1 update.  The same operations in the same
+// order as the separate sweep (x_c = acc_c * (1 / piv_c), acc_r -= l_r x_c by
+// fma, the rows' final scaling by 1 / piv_r), so the same bits, with 64 steps
+// of latency fewer.
+template <bool MERGED>
 __device__ __forceinline__ void chol_diag_core(double (&a)[16], double* __restrict__ K, double* __restrict__ Li,
                                                int32_t npad, int32_t kb, int32_t* flag, double (*col)[NB],
                                                double* Ls, double* invd) {
@@ -225,6 +234,45 @@ __device__ __forceinline__ void chol_diag_core(double (&a)[16], double* __restri
   const int g = __builtin_amdgcn_readfirstlane(t >> 6);
   const int64_t base = (int64_t)kb * NB;
   double* rowp = K + (base + r) * npad + base + 16 * g;
+  if constexpr (MERGED) {
+    double b[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) b[j] = (16 * g + j == r) ? 1.0 : 0.0;
+    for (int cb = 0; cb < NB / 16; ++cb) {
+#pragma unroll
+      for (int cc = 0; cc < 16; ++cc) {
+        const int c = 16 * cb + cc;
+        double* cl = col[c & 1];
+        if (g == cb) {  // wave-uniform: the owner of column c
+          const double dv = readlane_f64(a[cc], c);
+          if (r == 0 && !(dv > 0.0)) atomicOr(flag, 1);
+          const double piv = sqrt(dv > 0.0 ? dv : 1e-300);
+          const double ip = 1.0 / piv;
+          const double l = a[cc] * ip;
+          cl[r] = r > c ? l : 0.0;
+          if (r == 0) invd[c] = ip;
+          a[cc] = r > c ? l : (r == c ? piv : a[cc]);
+        }
+        __syncthreads();  // column c published; the buffer written at step c+1 was last read at step c-1
+        const double lr = cl[r];
+        const double is = invd[c];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) a[j] = __builtin_fma(-lr, cl[16 * g + j], a[j]);
+#pragma unroll
+        for (int j = 0; j < 16; ++j) b[j] = __builtin_fma(-lr, readlane_f64(b[j], c) * is, b[j]);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int sc = 16 * g + j;
+      rowp[j] = sc <= r ? a[j] : 0.0;
+    }
+    const double ir = invd[r];   // written at step r, behind that step's barrier
+    double* lip = Li + (base + r) * npad + base + 16 * g;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) lip[j] = b[j] * ir;
+    return;
+  }
   for (int cb = 0; cb < NB / 16; ++cb) {
 #pragma unroll
     for (int cc = 0; cc < 16; ++cc) {
@@ -271,6 +319,7 @@ __device__ __forceinline__ void chol_diag_core(double (&a)[16], double* __restri
   for (int j = 0; j < 16; ++j) lip[j] = b[j] * ir;
 }
 
+template <bool MERGED>
 __global__ __launch_bounds__(256) void k_chol_diag(double* __restrict__ K, double* __restrict__ Li, int32_t npad,
                                                    int32_t kb, int32_t* flag) {
   fit_prio();
@@ -284,7 +333,7 @@ __global__ __launch_bounds__(256) void k_chol_diag(double* __restrict__ K, doubl
   double a[16];
 #pragma unroll
   for (int j = 0; j < 16; ++j) a[j] = rowp[j];
-  chol_diag_core(a, K, Li, npad, kb, flag, col, Ls, invd);
+  chol_diag_core<MERGED>(a, K, Li, npad, kb, flag, col, Ls, invd);
 }
 
 // Panel kb, step 2: row block i > kb:  L_ik = A_ik * inv(L_kk)^T  (NT product)
@@ -336,6 +385,7 @@ __global__ __launch_bounds__(256) void k_chol_update(double* __restrict__ K, int
 // launch: the workgroup that updates block (kb + 1, kb + 1) keeps it in LDS
 // and runs k_chol_diag's steps on it while the others update the rest, so the
 // fit's serial chain loses one launch per level (ut_ctx::chol_fuse)
+template <bool MERGED>
 __global__ __launch_bounds__(256) void k_chol_update_diag(double* __restrict__ K, double* __restrict__ Li,
                                                           int32_t npad, int32_t kb, int32_t* flag) {
   fit_prio();
@@ -383,7 +433,7 @@ __global__ __launch_bounds__(256) void k_chol_update_diag(double* __restrict__ K
 #pragma unroll
   for (int q = 0; q < 16; ++q) av[q] = Ls[rr * (NB + 1) + 16 * g + q];
   __syncthreads();   // Ls is rewritten by the substitution's setup
-  chol_diag_core(av, K, Li, npad, kb + 1, flag, col, Ls, invd);
+  chol_diag_core<MERGED>(av, K, Li, npad, kb + 1, flag, col, Ls, invd);
 }
 
 // K = sf2 exp(-0.5 |xs_i - xs_j|^2) + diag I, 64 x 64 tiles on fp64 MFMA;
@@ -805,6 +855,11 @@ __global__ void k_gp_finalize(int64_t m, int32_t RT1, int32_t RT2, const double*
 // ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
+static void launch_chol_diag(ut_ctx* c, int32_t npad, int32_t kb) {
+  hipLaunchKernelGGL(c->chol_merged ? k_chol_diag<true> : k_chol_diag<false>, dim3(1), dim3(256), 0, c->stream,
+                     c->gp_K, c->gp_Linv, npad, kb, c->gp_flag);
+}
+
 static int gp_alloc(ut_ctx* c, int32_t npad_need, int32_t d) {
   if (c->gp_cap_n >= npad_need && c->gp_d == d && c->gp_Xs) return 0;
   // room for a growing training set (the tuning loop adds a few rows per fit):
@@ -1006,7 +1061,7 @@ int gp_fit_enqueue(ut_ctx* c, const double* X, const double* y, int32_t n, int32
         hipLaunchKernelGGL(k_app_red<1>, dim3(1), dim3(256), 0, c->stream, c->gp_Linv, c->gp_LinvT, c->gp_K,
                            c->gp_T, npad, b, maxq, W, Et);
       }
-      hipLaunchKernelGGL(k_chol_diag, dim3(1), dim3(256), 0, c->stream, c->gp_K, c->gp_Linv, npad, b, c->gp_flag);
+      launch_chol_diag(c, npad, b);
       if (b > 0) {
         double* W = c->app_ws.p;
         hipLaunchKernelGGL(k_app_part<2>, dim3(maxq, b), dim3(256), 0, c->stream, c->gp_Linv, c->gp_LinvT,
@@ -1028,13 +1083,13 @@ int gp_fit_enqueue(ut_ctx* c, const double* X, const double* y, int32_t n, int32
     for (int32_t kb = 0; kb < nb; ++kb) {
       // (fused: diagonal blocks after the first come from the previous update)
       if (!fuse || kb == 0)
-        hipLaunchKernelGGL(k_chol_diag, dim3(1), dim3(256), 0, c->stream, c->gp_K, c->gp_Linv, npad, kb, c->gp_flag);
+        launch_chol_diag(c, npad, kb);
       const int32_t T = nb - kb - 1;
       if (T > 0) {
         hipLaunchKernelGGL(k_chol_rows, dim3(T), dim3(256), 0, c->stream, c->gp_K, c->gp_Linv, npad, kb);
         if (fuse)
-          hipLaunchKernelGGL(k_chol_update_diag, dim3(T * (T + 1) / 2), dim3(256), 0, c->stream, c->gp_K, c->gp_Linv,
-                             npad, kb, c->gp_flag);
+          hipLaunchKernelGGL(c->chol_merged ? k_chol_update_diag<true> : k_chol_update_diag<false>,
+                             dim3(T * (T + 1) / 2), dim3(256), 0, c->stream, c->gp_K, c->gp_Linv, npad, kb, c->gp_flag);
         else
           hipLaunchKernelGGL(k_chol_update, dim3(T * (T + 1) / 2), dim3(256), 0, c->stream, c->gp_K, npad, kb);
       }

@@ -223,6 +223,9 @@ struct ut_ctx {
   // L^-1 levels of 256 rows and more on k_trinv_big (128 x 128 tiles, glds
   // ring) instead of k_trinv_level (64 x 64 tiles, plain loads); UT_TRINV_BIG
   int32_t trinv_big = 1;
+  // the diagonal blocks' inverse solved inside the Cholesky column loop
+  // (gp.hip chol_diag_core<true>); UT_CHOL_MERGED
+  int32_t chol_merged = 1;
   // fp32 / f16x3 dense rounds: 1 = enqueue the hash after K* (their K* waits
   // for the whole fit, which the hash would otherwise crowd out of the CUs: at
   // n = 4096 the refit stretches from ~6 to ~14 ms beside it) and let the
