@@ -783,6 +783,7 @@ int ut_gp_score_values(ut_ctx* c, const double* values, int64_t ld, int64_t m, c
   if (own) timing_begin(c);
   // encode + 1/ell scaling + |u'|^2 in one pass (k_encode_scaled): no feature matrix
   int rc = gp_encode_scaled(c, values, ld, m);
+  mark(c, "encode");   // (else the encode's time would land in the next stage, fit_wait)
   if (!rc) rc = gp_score_impl(c, nullptr, ld, m, acq, dup, mu, var, score);
   if (own) timing_end(c);
   return rc;
