@@ -361,10 +361,10 @@ __global__ __launch_bounds__(AOS ? 64 : 256) void k_de(const DevParam* __restric
 
 // GP features of a configuration: emit(feature column, value) for each feature
 // of param pr at candidate i (every column of the param is emitted)
+// (encode_param_v: the same with the param's first value column already loaded)
 template <class Emit>
-__device__ __forceinline__ void encode_param(const DevParam& pr, const double* __restrict__ values, int64_t ld,
-                                             int64_t i, const double* __restrict__ vtab, Emit&& emit) {
-  const double v = values[(int64_t)pr.col * ld + i];
+__device__ __forceinline__ void encode_param_v(const DevParam& pr, double v, const double* __restrict__ values,
+                                               int64_t ld, int64_t i, const double* __restrict__ vtab, Emit&& emit) {
   if (is_primitive(pr.kind)) {
     emit(pr.feat_col, unit_of(pr, v, vtab));
   } else if (pr.kind == UT_BOOL) {
@@ -383,13 +383,29 @@ __device__ __forceinline__ void encode_param(const DevParam& pr, const double* _
   }
 }
 
+template <class Emit>
+__device__ __forceinline__ void encode_param(const DevParam& pr, const double* __restrict__ values, int64_t ld,
+                                             int64_t i, const double* __restrict__ vtab, Emit&& emit) {
+  encode_param_v(pr, values[(int64_t)pr.col * ld + i], values, ld, i, vtab, emit);
+}
+
 __global__ __launch_bounds__(256) void k_encode(const DevParam* __restrict__ params, int32_t P,
                                                 const double* __restrict__ vtab, const double* __restrict__ values, int64_t ld, int64_t m,
                                                 double* __restrict__ feat, int64_t ldf) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= m) return;
-  for (int32_t p = 0; p < P; ++p)
-    encode_param(params[p], values, ld, i, vtab, [&](int32_t c, double f) { feat[(int64_t)c * ldf + i] = f; });
+  constexpr int ENC_PF = 8;   // value columns loaded ahead (see k_encode_scaled_cat)
+  for (int32_t p0 = 0; p0 < P; p0 += ENC_PF) {
+    double vv[ENC_PF];
+#pragma unroll
+    for (int q = 0; q < ENC_PF; ++q) vv[q] = p0 + q < P ? values[(int64_t)params[p0 + q].col * ld + i] : 0.0;
+#pragma unroll
+    for (int q = 0; q < ENC_PF; ++q) {
+      if (p0 + q >= P) break;
+      encode_param_v(params[p0 + q], vv[q], values, ld, i, vtab,
+                     [&](int32_t c, double f) { feat[(int64_t)c * ldf + i] = f; });
+    }
+  }
 }
 
 // k_encode and k_gp_prep_cand in one pass (dense scoring rounds): the K* B
@@ -406,12 +422,21 @@ __global__ __launch_bounds__(256) void k_encode_scaled(const DevParam* __restric
   if (i >= ldu) return;
   double s = 0.0;
   if (i < m) {
-    for (int32_t p = 0; p < P; ++p)
-      encode_param(params[p], values, ld, i, vtab, [&](int32_t c, double f) {
-        const double v = f * inv_ell[c];
-        u[(int64_t)c * ldu + i] = v;
-        s += v * v;
-      });
+    constexpr int ENC_PF = 8;   // value columns loaded ahead (see k_encode_scaled_cat)
+    for (int32_t p0 = 0; p0 < P; p0 += ENC_PF) {
+      double vv[ENC_PF];
+#pragma unroll
+      for (int q = 0; q < ENC_PF; ++q) vv[q] = p0 + q < P ? values[(int64_t)params[p0 + q].col * ld + i] : 0.0;
+#pragma unroll
+      for (int q = 0; q < ENC_PF; ++q) {
+        if (p0 + q >= P) break;
+        encode_param_v(params[p0 + q], vv[q], values, ld, i, vtab, [&](int32_t c, double f) {
+          const double v = f * inv_ell[c];
+          u[(int64_t)c * ldu + i] = v;
+          s += v * v;
+        });
+      }
+    }
   } else {
     for (int32_t k = 0; k < F; ++k) u[(int64_t)k * ldu + i] = 0.0;
   }
@@ -446,22 +471,35 @@ __global__ __launch_bounds__(256) void k_encode_scaled_cat(const DevParam* __res
   for (int32_t w = 0; w < stride; ++w) bits[t * stride + w] = 0u;
   double s = 0.0;
   if (i < m) {
-    for (int32_t p = 0; p < P; ++p) {
-      const int32_t cc = cat_ccol[p];
-      const DevParam pr = params[p];
-      if (cc >= 0) {
-        const double v = values[(int64_t)pr.col * ld + i];
-        const int64_t o = pr.kind == UT_BOOL ? (v != 0.0 ? 1 : 0) : (int64_t)v;
-        if (o < 0 || o >= (pr.kind == UT_BOOL ? 2 : pr.n_opt)) continue;   // no option: no match
-        const int32_t q = cc + (int32_t)o;
-        bits[t * stride + (q >> 5)] |= 1u << (q & 31);
-        continue;
+    // the params' value columns loaded ENC_PF at a time ahead of their use: one
+    // load in flight per param left the kernel latency-bound (two workgroups per
+    // CU for the LDS; C4: 339 params, ~10 ms at 2^22 candidates)
+    constexpr int ENC_PF = 8;
+    for (int32_t p0 = 0; p0 < P; p0 += ENC_PF) {
+      double vv[ENC_PF];
+#pragma unroll
+      for (int q = 0; q < ENC_PF; ++q)
+        vv[q] = p0 + q < P ? values[(int64_t)params[p0 + q].col * ld + i] : 0.0;
+#pragma unroll
+      for (int q = 0; q < ENC_PF; ++q) {
+        const int32_t p = p0 + q;
+        if (p >= P) break;
+        const int32_t cc = cat_ccol[p];
+        const DevParam pr = params[p];
+        const double v = vv[q];
+        if (cc >= 0) {
+          const int64_t o = pr.kind == UT_BOOL ? (v != 0.0 ? 1 : 0) : (int64_t)v;
+          if (o < 0 || o >= (pr.kind == UT_BOOL ? 2 : pr.n_opt)) continue;   // no option: no match
+          const int32_t qb = cc + (int32_t)o;
+          bits[t * stride + (qb >> 5)] |= 1u << (qb & 31);
+          continue;
+        }
+        encode_param_v(pr, v, values, ld, i, vtab, [&](int32_t c, double f) {
+          const double x = f * inv_ell[c];
+          u[(int64_t)feat_num[c] * ldu + i] = x;
+          s += x * x;
+        });
       }
-      encode_param(pr, values, ld, i, vtab, [&](int32_t c, double f) {
-        const double v = f * inv_ell[c];
-        u[(int64_t)feat_num[c] * ldu + i] = v;
-        s += v * v;
-      });
     }
   }
   for (int32_t k = i < m ? n_num : 0; k < dpad; ++k) u[(int64_t)k * ldu + i] = 0.0;
