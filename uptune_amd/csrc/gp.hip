@@ -1099,6 +1099,8 @@ int gp_fit_enqueue(ut_ctx* c, const double* X, const double* y, int32_t n, int32
     for (int32_t lv = NB; lv < npad; lv *= 2) {
       const int32_t pairs = (int32_t)((npad - lv + 2 * lv - 1) / (2 * lv));
       if (c->trinv_big && lv >= TRB_MIN) {
+        // k_trinv_big's tiles: every pair's sizes are multiples of 128
+        UT_CHECK(c, npad % TRB_BM == 0 && lv % TRB_BM == 0, UT_EINVAL, "gp_fit: npad not a multiple of 128");
         const dim3 gb(lv / TRB_BM, lv / TRB_BM, pairs);
         hipLaunchKernelGGL(k_trinv_big, gb, dim3(256), 0, c->stream, c->gp_K, c->gp_Linv, c->gp_T, npad, lv, 0);
         hipLaunchKernelGGL(k_trinv_big, gb, dim3(256), 0, c->stream, c->gp_K, c->gp_Linv, c->gp_T, npad, lv, 1);
