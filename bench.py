@@ -545,7 +545,7 @@ def main():
     elapsed = time.perf_counter() - t0
     # per-stage device times of the timed rounds (HIP events recorded on the
     # library's streams during the rounds, read once here)
-    for st in ("propose", "hash", "dedup", "encode", "fit_wait", "kstar", "bound", "prune", "var", "finalize",
+    for st in ("propose", "hash", "dedup", "encode", "prep", "fit_wait", "kstar", "bound", "prune", "var", "finalize",
                "topk"):
         try:
             stage_ms[st] = [eng.stage_time(st)]

@@ -1426,8 +1426,11 @@ int gp_topk_pruned_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, co
   UT_CHECK(c, acq->kind == UT_ACQ_EI || (acq->kind == UT_ACQ_UCB && acq->kappa >= 0.0), UT_EINVAL,
            "gp_topk_pruned: the score must increase with sigma (EI, or UCB with kappa >= 0)");
   UT_CHECK(c, k >= 1 && k <= 1024, UT_EINVAL, "gp_topk_pruned: k must be in [1, 1024]");
-  if (c->fit_pending) UT_HIP(c, hipStreamWaitEvent(c->stream, c->ev_fit, 0));   // K* takes mu = k* . alpha
-  mark(c, "fit_wait");   // (the wait is not K* time)
+  // the candidates' K* operands need only the fit's scaled inputs (1/ell):
+  // they are prepared while the factorisation still runs, and K* then waits
+  // for the whole fit (C3 pruned: the 2.8-ms categorical prep came off the
+  // critical path, scripts/ab/r04ad_prep_early.sh)
+  if (c->fit_pending) UT_HIP(c, hipStreamWaitEvent(c->stream, c->ev_fit_x, 0));
   const int32_t n = c->gp_n, d = c->gp_d;
   const int32_t npad = ((n + NPAD - 1) / NPAD) * NPAD;
   const bool cat = feat_ours && c->cat_on;   // the categorical K* (features from ut's encoder)
@@ -1460,6 +1463,9 @@ int gp_topk_pruned_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, co
     return rc;
   }
   c->ucand_cat = cat;
+  mark(c, "prep");
+  if (c->fit_pending) UT_HIP(c, hipStreamWaitEvent(c->stream, c->ev_fit, 0));   // K* takes mu = k* . alpha
+  mark(c, "fit_wait");   // (the wait is not K* time)
   const double* XsT = cat ? c->gp_XsT_num.p : c->gp_XsT;
   const double* xn = cat ? c->gp_xnorm_num.p : nullptr;
   // K* stores only the bound rows; the mean sums every row.  The few
