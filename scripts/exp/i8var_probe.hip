@@ -1,0 +1,704 @@
+// Probe for the int8-sliced ("Ozaki") variance contraction on gfx950.
+//  1. lane map of v_mfma_i32_32x32x32_i8 with exact integer data;
+//  2. a prototype of k_gp_var_i8<S>: V = L^-1 K*^T from S int8 digit planes of
+//     each operand, pairs p + q <= S + 1 accumulated exactly in int32 per group
+//     g = p + q, recombined in fp64 in the epilogue; column sums of V^2 per
+//     64-row tile.  Checked against an exact CPU recombination at a small shape,
+//     timed at the C2 shape (n = 1024, m = 2^20).
+//   hipcc -O3 -std=c++17 --offload-arch=gfx950 scripts/exp/i8var_probe.hip -o scripts/exp/i8var_probe
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#define CK(x)                                                                   \
+  do {                                                                          \
+    hipError_t e_ = (x);                                                        \
+    if (e_ != hipSuccess) {                                                     \
+      printf("HIP error %s at %s:%d\n", hipGetErrorString(e_), __FILE__, __LINE__); \
+      exit(1);                                                                  \
+    }                                                                           \
+  } while (0)
+
+typedef int32_t v4i __attribute__((ext_vector_type(4)));
+typedef int32_t v16i __attribute__((ext_vector_type(16)));
+
+// ---------------------------------------------------------------- 1. lane map
+// assumed: lane l holds A[row l&31][k = 16 (l>>5) + j], B[k = 16 (l>>5) + j][col l&31]
+// (j = 0..15), D[row (r&3) + 8 (r>>2) + 4 (l>>5)][col l&31] (r = 0..15)
+__global__ void k_map(const int8_t* A, const int8_t* B, int32_t* D) {
+  const int l = threadIdx.x;
+  v4i a, b;
+  int8_t* pa = reinterpret_cast<int8_t*>(&a);
+  int8_t* pb = reinterpret_cast<int8_t*>(&b);
+  for (int j = 0; j < 16; ++j) {
+    pa[j] = A[(l & 31) * 32 + 16 * (l >> 5) + j];
+    pb[j] = B[(16 * (l >> 5) + j) * 32 + (l & 31)];
+  }
+  v16i acc;
+  for (int r = 0; r < 16; ++r) acc[r] = 0;
+  acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b, acc, 0, 0, 0);
+  for (int r = 0; r < 16; ++r) D[((r & 3) + 8 * (r >> 2) + 4 * (l >> 5)) * 32 + (l & 31)] = acc[r];
+}
+
+// ---------------------------------------------------------------- 2. prototype
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+  static_assert(N >= 0 && N < 64, "vmcnt");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+}
+constexpr int IM = 64, IN = 64, IK = 32;   // tile rows, candidates, k per stage
+constexpr int PL = IM * IK;                // bytes per plane per stage (2 KiB)
+
+// element (r, k) of a plane in the [KB][rows][32] layout, chunk swizzled by row bit 3
+__host__ __device__ inline int64_t i8_off(int64_t r, int32_t k, int64_t ld) {
+  return ((int64_t)(k >> 5) * ld + r) * 32 + ((((k >> 4) & 1) ^ ((int)(r >> 3) & 1)) << 4) + (k & 15);
+}
+
+template <int S, int MODE, int NST = 2>
+__global__ __launch_bounds__(256, 2) void k_var_i8(const int8_t* __restrict__ Ad, const int8_t* __restrict__ Bd,
+                                                   int32_t npad, int64_t ldk, int32_t RT, int32_t CT, int64_t m,
+                                                   int32_t* __restrict__ ticket, const double* __restrict__ rscale,
+                                                   double* __restrict__ part, int32_t Sg) {
+  constexpr int STAGE = 2 * S * PL;
+  __shared__ __attribute__((aligned(16))) int8_t lds[NST * STAGE + 2 * IN * 8 + IM * 8 + 16];
+  double* red = reinterpret_cast<double*>(lds + NST * STAGE);   // [2][64]
+  double* srs = red + 2 * IN;                                  // row scales of the tile
+  int32_t& s_item = *reinterpret_cast<int32_t*>(srs + IM);
+  const int t = threadIdx.x, lane = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wm = w >> 1, wn = w & 1;
+  const int32_t xcd = blockIdx.x & 7;
+  const int64_t KB = npad / IK;
+  const int64_t aplane = KB * npad * 32, bplane = KB * ldk * 32;   // bytes per plane
+
+  auto issue = [&](int32_t row0, int64_t col0, int32_t kt, int8_t* st) {
+#pragma unroll
+    for (int j = 0; j < S; ++j) {
+      const int u = w + 4 * j;          // 0 .. 4S-1
+      const int pl = u >> 1, h = u & 1;
+      const int8_t* src = pl < S ? Ad + pl * aplane + ((int64_t)kt * npad + row0) * 32
+                                 : Bd + (pl - S) * bplane + ((int64_t)kt * ldk + col0) * 32;
+      __builtin_amdgcn_global_load_lds(src + h * 1024 + lane * 16,
+                                       (__attribute__((address_space(3))) void*)(st + pl * PL + h * 1024), 16, 0, 0);
+    }
+  };
+
+  const int32_t P = (RT + 1) / 2;
+  for (;;) {
+    if (t == 0) s_item = atomicAdd(&ticket[xcd], 1);
+    __syncthreads();
+    const int32_t j = s_item;
+    const int32_t G = j / (P * Sg), q = j % (P * Sg), p = q % P;
+    const int32_t ct = (G * Sg + q / P) * 8 + xcd;
+    if (ct >= CT) break;
+    int32_t rts[2] = {RT - 1 - p, p};
+    const int nrt = rts[1] == rts[0] ? 1 : 2;
+    for (int ri = 0; ri < nrt; ++ri) {
+      if (ri > 0) __syncthreads();
+      const int32_t rt = rts[ri];
+      const int32_t row0 = rt * IM;
+      const int64_t col0 = (int64_t)ct * IN;
+      const int32_t nk = (row0 + IM) / IK;
+      v16i acc[S];
+#pragma unroll
+      for (int g = 0; g < S; ++g)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[g][r] = 0;
+      if (w == 0 && lane < 32)
+        __builtin_amdgcn_global_load_lds(rscale + row0 + lane * 2, (__attribute__((address_space(3))) void*)srs, 16, 0,
+                                         0);
+      const int32_t arow = MODE == 2 ? 0 : row0;
+      const int64_t bcol = MODE == 2 ? (int64_t)xcd * IN : col0;
+      if (MODE != 1) issue(arow, bcol, 0, lds);
+      if (MODE != 1 && NST == 3 && nk > 1) issue(arow, bcol, 1, lds + STAGE);
+      for (int32_t kt = 0; kt < nk; ++kt) {
+        if (NST == 3 && MODE != 1 && kt + 1 < nk) vm_wait<S>();   // S glds per wave per stage
+        else vm_wait<0>();
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (MODE != 1 && kt + NST - 1 < nk) issue(arow, bcol, kt + NST - 1, lds + ((kt + NST - 1) % NST) * STAGE);
+        // L^-1 is zero for k > row: wave rows [row0 + 32 wm, +32) see nothing at kt >= (row0 + 32 wm + 32) / 32
+        if (kt * IK >= row0 + 32 * wm + 32) continue;
+        const int8_t* st = lds + (kt % NST) * STAGE;
+        v4i af[S], bf[S];
+        const int c = lane >> 5;
+        const int ra = wm * 32 + (lane & 31), cb = wn * 32 + (lane & 31);
+#pragma unroll
+        for (int pp = 0; pp < S; ++pp) {
+          af[pp] = *reinterpret_cast<const v4i*>(st + pp * PL + ra * 32 + ((c ^ ((ra >> 3) & 1)) << 4));
+          bf[pp] = *reinterpret_cast<const v4i*>(st + (S + pp) * PL + cb * 32 + ((c ^ ((cb >> 3) & 1)) << 4));
+        }
+#pragma unroll
+        for (int g = 2; g <= S + 1; ++g)
+#pragma unroll
+          for (int pa = 1; pa < g; ++pa)
+            acc[g - 2] = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[pa - 1], bf[g - pa - 1], acc[g - 2], 0, 0, 0);
+      }
+      // epilogue: V = 2^-14 sum_g T_g 2^{-7 (g - 2)} * rowscale (Horner from the smallest)
+      double s = 0.0;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        double v = (double)acc[S - 1][r];
+#pragma unroll
+        for (int g = S - 2; g >= 0; --g) v = __builtin_fma(v, 0x1p-7, (double)acc[g][r]);
+        const int rl = wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        v *= srs[rl];
+        s = __builtin_fma(v, v, s);
+      }
+      s += __shfl_xor(s, 32);
+      if (lane < 32) red[wm * IN + wn * 32 + lane] = s;
+      __syncthreads();
+      if (t < IN) {
+        const int64_t col = col0 + t;
+        if (col < m) part[(int64_t)rt * ldk + col] = red[t] + red[IN + t];
+      }
+    }
+  }
+}
+
+// v2: one 512-thread workgroup per CU, 128-row x 64-candidate tiles (waves 4 x 2
+// of 32 x 32; waves on one SIMD get row groups wm and 3 - wm), a 3-stage ring
+// (S = 7: 42 KiB per stage).  MODE 1: no global loads; MODE 2: A always from
+// row tile 0 and B from strip 0 of its XCD (L2 hits).
+constexpr int JM = 128;
+template <int S, int MODE>
+__global__ __launch_bounds__(512, 1) void k_var_i8b(const int8_t* __restrict__ Ad, const int8_t* __restrict__ Bd,
+                                                    int32_t npad, int64_t ldk, int32_t RT, int32_t CT, int64_t m,
+                                                    int32_t* __restrict__ ticket, const double* __restrict__ rscale,
+                                                    double* __restrict__ part, int32_t Sg) {
+  constexpr int APL = JM * IK, BPL = IN * IK;                 // 4 KiB, 2 KiB per plane per stage
+  constexpr int STAGE = S * (APL + BPL);
+  constexpr int NI = 6 * S;                                   // 1-KiB glds per stage
+  __shared__ __attribute__((aligned(16))) int8_t lds[3 * STAGE + 4 * IN * 8 + JM * 8 + 16];
+  double* red = reinterpret_cast<double*>(lds + 3 * STAGE);   // [4][64]
+  double* srs = red + 4 * IN;                                  // row scales of the tile
+  int32_t& s_item = *reinterpret_cast<int32_t*>(srs + JM);
+  const int t = threadIdx.x, lane = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wm = w < 4 ? (w >> 1) : 3 - ((w - 4) >> 1), wn = w & 1;
+  const int32_t xcd = blockIdx.x & 7;
+  const int64_t KB = npad / IK;
+  const int64_t aplane = KB * npad * 32, bplane = KB * ldk * 32;
+  const int nw = (NI - w + 7) / 8;   // this wave's glds per stage
+
+  auto issue = [&](int32_t row0, int64_t col0, int32_t kt, int8_t* st) {
+#pragma unroll
+    for (int j = 0; j < (NI + 7) / 8; ++j) {
+      const int u = w + 8 * j;
+      if (u >= NI) break;
+      // u < 4S: A plane u / 4, quarter u % 4; else B plane (u - 4S) / 2, half
+      const int8_t* src;
+      int8_t* dst;
+      if (u < 4 * S) {
+        const int pl = u >> 2, h = u & 3;
+        src = Ad + pl * aplane + ((int64_t)kt * npad + row0) * 32 + h * 1024;
+        dst = st + pl * APL + h * 1024;
+      } else {
+        const int pl = (u - 4 * S) >> 1, h = (u - 4 * S) & 1;
+        src = Bd + pl * bplane + ((int64_t)kt * ldk + col0) * 32 + h * 1024;
+        dst = st + S * APL + pl * BPL + h * 1024;
+      }
+      __builtin_amdgcn_global_load_lds(src + lane * 16, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+    }
+  };
+  auto wait_one_behind = [&]() {   // all but the newest stage landed (per wave counts)
+    if (nw == (NI + 7) / 8) vm_wait<(NI + 7) / 8>();
+    else vm_wait<NI / 8>();
+  };
+
+  const int32_t P = (RT + 1) / 2;
+  for (;;) {
+    if (t == 0) s_item = atomicAdd(&ticket[xcd], 1);
+    __syncthreads();
+    const int32_t j = s_item;
+    const int32_t G = j / (P * Sg), q = j % (P * Sg), p = q % P;
+    const int32_t ct = (G * Sg + q / P) * 8 + xcd;
+    if (ct >= CT) break;
+    int32_t rts[2] = {RT - 1 - p, p};
+    const int nrt = rts[1] == rts[0] ? 1 : 2;
+    for (int ri = 0; ri < nrt; ++ri) {
+      if (ri > 0) __syncthreads();
+      const int32_t rt = rts[ri];
+      const int32_t row0 = rt * JM;
+      const int64_t col0 = (int64_t)ct * IN;
+      const int32_t arow = MODE == 2 ? 0 : row0;
+      const int64_t bcol = MODE == 2 ? (int64_t)xcd * IN : col0;
+      const int32_t nk = (row0 + JM) / IK;
+      v16i acc[S];
+#pragma unroll
+      for (int g = 0; g < S; ++g)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[g][r] = 0;
+      if (w == 0)
+        __builtin_amdgcn_global_load_lds(rscale + row0 + lane * 2, (__attribute__((address_space(3))) void*)srs, 16, 0,
+                                         0);
+      if (MODE != 1) {
+        issue(arow, bcol, 0, lds);
+        if (nk > 1) issue(arow, bcol, 1, lds + STAGE);
+      }
+      for (int32_t kt = 0; kt < nk; ++kt) {
+        if (MODE != 1) {
+          if (kt + 1 < nk) wait_one_behind();
+          else vm_wait<0>();
+        } else {
+          vm_wait<0>();
+        }
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (MODE != 1 && kt + 2 < nk) issue(arow, bcol, kt + 2, lds + ((kt + 2) % 3) * STAGE);
+        if (kt * IK >= row0 + 32 * wm + 32) continue;
+        const int8_t* st = lds + (kt % 3) * STAGE;
+        v4i af[S], bf[S];
+        const int c = lane >> 5;
+        const int ra = wm * 32 + (lane & 31), cb = wn * 32 + (lane & 31);
+#pragma unroll
+        for (int pp = 0; pp < S; ++pp) {
+          af[pp] = *reinterpret_cast<const v4i*>(st + pp * APL + ra * 32 + ((c ^ ((ra >> 3) & 1)) << 4));
+          bf[pp] = *reinterpret_cast<const v4i*>(st + S * APL + pp * BPL + cb * 32 + ((c ^ ((cb >> 3) & 1)) << 4));
+        }
+#pragma unroll
+        for (int g = 2; g <= S + 1; ++g)
+#pragma unroll
+          for (int pa = 1; pa < g; ++pa)
+            acc[g - 2] = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[pa - 1], bf[g - pa - 1], acc[g - 2], 0, 0, 0);
+      }
+      double s = 0.0;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        double v = (double)acc[S - 1][r];
+#pragma unroll
+        for (int g = S - 2; g >= 0; --g) v = __builtin_fma(v, 0x1p-7, (double)acc[g][r]);
+        const int rl = wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        v *= srs[rl];
+        s = __builtin_fma(v, v, s);
+      }
+      s += __shfl_xor(s, 32);
+      if (lane < 32) red[wm * IN + wn * 32 + lane] = s;
+      __syncthreads();
+      if (t < IN) {
+        const int64_t col = col0 + t;
+        if (col < m) part[(int64_t)rt * ldk + col] = (red[t] + red[IN + t]) + (red[2 * IN + t] + red[3 * IN + t]);
+      }
+    }
+  }
+}
+
+// v3: v1's shape (2 x 256-thread workgroups per CU, 64 x 64 tiles, waves 2 x 2
+// of 32 x 32) with the A fragments (L^-1 planes, L2-resident) loaded straight
+// into VGPRs one stage ahead and only B (K* planes) staged through LDS, in a
+// 3-stage glds ring: half of v1's LDS traffic.  B glds per stage padded to a
+// multiple of 4 (dummies into a scratch KiB) so every wave counts the same.
+template <int S, int MODE>
+__global__ __launch_bounds__(256, 2) void k_var_i8c(const int8_t* __restrict__ Ad, const int8_t* __restrict__ Bd,
+                                                    int32_t npad, int64_t ldk, int32_t RT, int32_t CT, int64_t m,
+                                                    int32_t* __restrict__ ticket, const double* __restrict__ rscale,
+                                                    double* __restrict__ part, int32_t Sg) {
+  constexpr int NI = (2 * S + 3) / 4 * 4, NBW = NI / 4;   // B glds per stage, per wave
+  constexpr int BST = S * PL + (NI - 2 * S) * 1024;       // one ring slot (+ scratch)
+  __shared__ __attribute__((aligned(16))) int8_t lds[3 * BST + 2 * IN * 8 + IM * 8 + 16];
+  double* red = reinterpret_cast<double*>(lds + 3 * BST);   // [2][64]
+  double* srs = red + 2 * IN;
+  int32_t& s_item = *reinterpret_cast<int32_t*>(srs + IM);
+  const int t = threadIdx.x, lane = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wm = w >> 1, wn = w & 1;
+  const int32_t xcd = blockIdx.x & 7;
+  const int64_t KB = npad / IK;
+  const int64_t aplane = KB * npad * 32, bplane = KB * ldk * 32;
+
+  auto issue_b = [&](int64_t col0, int32_t kt, int8_t* st) {
+#pragma unroll
+    for (int j = 0; j < NBW; ++j) {
+      const int u = w + 4 * j;
+      const int uu = u < 2 * S ? u : u - 2 * S;            // dummies re-load a real piece
+      const int pl = uu >> 1, h = uu & 1;
+      const int8_t* src = Bd + pl * bplane + ((int64_t)kt * ldk + col0) * 32 + h * 1024;
+      int8_t* dst = u < 2 * S ? st + pl * PL + h * 1024 : st + S * PL + (u - 2 * S) * 1024;
+      __builtin_amdgcn_global_load_lds(src + lane * 16, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+    }
+  };
+  const int c = lane >> 5;
+  auto load_a = [&](int32_t row0, int32_t kt, v4i(&af)[S]) {
+    const int64_t ra = row0 + wm * 32 + (lane & 31);
+#pragma unroll
+    for (int pp = 0; pp < S; ++pp)
+      af[pp] = __builtin_nontemporal_load(reinterpret_cast<const v4i*>(Ad + pp * aplane + i8_off(ra, kt * IK + 16 * c, npad)));
+  };
+
+  const int32_t P = (RT + 1) / 2;
+  for (;;) {
+    if (t == 0) s_item = atomicAdd(&ticket[xcd], 1);
+    __syncthreads();
+    const int32_t j = s_item;
+    const int32_t G = j / (P * Sg), q = j % (P * Sg), p = q % P;
+    const int32_t ct = (G * Sg + q / P) * 8 + xcd;
+    if (ct >= CT) break;
+    int32_t rts[2] = {RT - 1 - p, p};
+    const int nrt = rts[1] == rts[0] ? 1 : 2;
+    for (int ri = 0; ri < nrt; ++ri) {
+      if (ri > 0) __syncthreads();
+      const int32_t rt = rts[ri];
+      const int32_t row0 = rt * IM;
+      const int64_t col0 = (int64_t)ct * IN;
+      const int32_t arow = MODE == 2 ? 0 : row0;
+      const int64_t bcol = MODE == 2 ? (int64_t)xcd * IN : col0;
+      const int32_t nk = (row0 + IM) / IK;   // even
+      v16i acc[S];
+#pragma unroll
+      for (int g = 0; g < S; ++g)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[g][r] = 0;
+      if (w == 0 && lane < 32)
+        __builtin_amdgcn_global_load_lds(rscale + row0 + lane * 2, (__attribute__((address_space(3))) void*)srs, 16, 0,
+                                         0);
+      v4i af0[S], af1[S];
+      load_a(arow, 0, af0);
+      issue_b(bcol, 0, lds);
+      issue_b(bcol, 1, lds + BST);
+      auto step = [&](int32_t kt, v4i(&cur)[S], v4i(&nxt)[S]) {
+        if (kt + 1 < nk) vm_wait<NBW>();
+        else vm_wait<0>();
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (kt + 1 < nk) load_a(arow, kt + 1, nxt);
+        if (kt + 2 < nk) issue_b(bcol, kt + 2, lds + ((kt + 2) % 3) * BST);
+        if (kt * IK >= row0 + 32 * wm + 32) return;
+        const int8_t* st = lds + (kt % 3) * BST;
+        v4i bf[S];
+        const int cb = wn * 32 + (lane & 31);
+#pragma unroll
+        for (int pp = 0; pp < S; ++pp)
+          bf[pp] = *reinterpret_cast<const v4i*>(st + pp * PL + cb * 32 + ((c ^ ((cb >> 3) & 1)) << 4));
+#pragma unroll
+        for (int g = 2; g <= S + 1; ++g)
+#pragma unroll
+          for (int pa = 1; pa < g; ++pa)
+            acc[g - 2] = __builtin_amdgcn_mfma_i32_32x32x32_i8(cur[pa - 1], bf[g - pa - 1], acc[g - 2], 0, 0, 0);
+      };
+      for (int32_t kt = 0; kt < nk; kt += 2) {
+        step(kt, af0, af1);
+        step(kt + 1, af1, af0);
+      }
+      double s = 0.0;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        double v = (double)acc[S - 1][r];
+#pragma unroll
+        for (int g = S - 2; g >= 0; --g) v = __builtin_fma(v, 0x1p-7, (double)acc[g][r]);
+        const int rl = wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        v *= srs[rl];
+        s = __builtin_fma(v, v, s);
+      }
+      s += __shfl_xor(s, 32);
+      if (lane < 32) red[wm * IN + wn * 32 + lane] = s;
+      __syncthreads();
+      if (t < IN) {
+        const int64_t col = col0 + t;
+        if (col < m) part[(int64_t)rt * ldk + col] = red[t] + red[IN + t];
+      }
+    }
+  }
+}
+
+// v4: v3 with the A fragments fetched by buffer loads (descriptor in SGPRs,
+// one 32-bit voffset per lane, plane + stage offsets in soffset) into ONE set
+// of S registers: plane p of stage kt + 1 is requested right after the last
+// MFMA of stage kt that reads plane p (MFMAs in plane-major order), so it has
+// the rest of the stage and the next stage's earlier planes to land.
+template <int S, int MODE>
+__global__ __launch_bounds__(256, 2) void k_var_i8d(const int8_t* __restrict__ Ad, const int8_t* __restrict__ Bd,
+                                                    int32_t npad, int64_t ldk, int32_t RT, int32_t CT, int64_t m,
+                                                    int32_t* __restrict__ ticket, const double* __restrict__ rscale,
+                                                    double* __restrict__ part, int32_t Sg) {
+  constexpr int NI = (2 * S + 3) / 4 * 4, NBW = NI / 4;
+  constexpr int BST = S * PL + (NI - 2 * S) * 1024;
+  __shared__ __attribute__((aligned(16))) int8_t lds[3 * BST + 2 * IN * 8 + IM * 8 + 16];
+  double* red = reinterpret_cast<double*>(lds + 3 * BST);
+  double* srs = red + 2 * IN;
+  int32_t& s_item = *reinterpret_cast<int32_t*>(srs + IM);
+  const int t = threadIdx.x, lane = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wm = w >> 1, wn = w & 1;
+  const int32_t xcd = blockIdx.x & 7;
+  const int64_t KB = npad / IK;
+  const int64_t bplane = KB * ldk * 32;
+  const int32_t aplane = (int32_t)(KB * npad * 32);          // < 2^31 (npad <= 16384, bytes per plane)
+  const int32_t astage = npad * 32;
+  const __amdgpu_buffer_rsrc_t arsrc =
+      __builtin_amdgcn_make_buffer_rsrc((void*)Ad, (short)0, 0x7fffffff, 0x00020000);
+
+  auto issue_b = [&](int64_t col0, int32_t kt, int8_t* st) {
+#pragma unroll
+    for (int j = 0; j < NBW; ++j) {
+      const int u = w + 4 * j;
+      const int uu = u < 2 * S ? u : u - 2 * S;
+      const int pl = uu >> 1, h = uu & 1;
+      const int8_t* src = Bd + pl * bplane + ((int64_t)kt * ldk + col0) * 32 + h * 1024;
+      int8_t* dst = u < 2 * S ? st + pl * PL + h * 1024 : st + S * PL + (u - 2 * S) * 1024;
+      __builtin_amdgcn_global_load_lds(src + lane * 16, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+    }
+  };
+  const int c = lane >> 5;
+  auto load_a1 = [&](int32_t voff, int32_t kt, int pp) -> v4i {
+    return __builtin_bit_cast(v4i, __builtin_amdgcn_raw_buffer_load_b128(
+                                       arsrc, voff, __builtin_amdgcn_readfirstlane(pp * aplane + kt * astage), 0));
+  };
+
+  const int32_t P = (RT + 1) / 2;
+  for (;;) {
+    if (t == 0) s_item = atomicAdd(&ticket[xcd], 1);
+    __syncthreads();
+    const int32_t j = __builtin_amdgcn_readfirstlane(s_item);
+    const int32_t G = j / (P * Sg), q = j % (P * Sg), p = q % P;
+    const int32_t ct = (G * Sg + q / P) * 8 + xcd;
+    if (ct >= CT) break;
+    int32_t rts[2] = {RT - 1 - p, p};
+    const int nrt = rts[1] == rts[0] ? 1 : 2;
+    for (int ri = 0; ri < nrt; ++ri) {
+      if (ri > 0) __syncthreads();
+      const int32_t rt = rts[ri];
+      const int32_t row0 = rt * IM;
+      const int64_t col0 = (int64_t)ct * IN;
+      const int32_t arow = MODE == 2 ? 0 : row0;
+      const int64_t bcol = MODE == 2 ? (int64_t)xcd * IN : col0;
+      const int32_t nk = (row0 + IM) / IK;
+      // lane's byte offset inside a plane's stage: row ra's 16-B chunk c (swizzled)
+      const int32_t ra = arow + wm * 32 + (lane & 31);
+      const int32_t voff = ra * 32 + ((c ^ ((ra >> 3) & 1)) << 4);
+      v16i acc[S];
+#pragma unroll
+      for (int g = 0; g < S; ++g)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[g][r] = 0;
+      if (w == 0 && lane < 32)
+        __builtin_amdgcn_global_load_lds(rscale + row0 + lane * 2, (__attribute__((address_space(3))) void*)srs, 16, 0,
+                                         0);
+      v4i af[S];
+#pragma unroll
+      for (int pp = 0; pp < S; ++pp) af[pp] = load_a1(voff, 0, pp);
+      issue_b(bcol, 0, lds);
+      issue_b(bcol, 1, lds + BST);
+      for (int32_t kt = 0; kt < nk; ++kt) {
+        // B(kt) landed: allow the VMEM ops issued after it (A(kt - 1), B(kt + 1), A(kt))
+        const int after = kt == 0 ? (nk > 1 ? NBW : 0)
+                        : kt == 1 ? (nk > 2 ? NBW : 0) + S
+                                  : 2 * S + (kt + 1 < nk ? NBW : 0);
+        if (after == 2 * S + NBW) vm_wait<2 * S + NBW>();
+        else if (after == 2 * S) vm_wait<2 * S>();
+        else if (after == NBW + S) vm_wait<NBW + S>();
+        else if (after == S) vm_wait<S>();
+        else if (after == NBW) vm_wait<NBW>();
+        else vm_wait<0>();
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (kt + 2 < nk) issue_b(bcol, kt + 2, lds + ((kt + 2) % 3) * BST);
+        const bool more = kt + 1 < nk;
+        if (kt * IK >= row0 + 32 * wm + 32) {   // nothing to multiply: still fetch the next stage's A
+          if (more) {
+#pragma unroll
+            for (int pp = 0; pp < S; ++pp) af[pp] = load_a1(voff, kt + 1, pp);
+          }
+          continue;
+        }
+        const int8_t* st = lds + (kt % 3) * BST;
+        v4i bf[S];
+        const int cb = wn * 32 + (lane & 31);
+#pragma unroll
+        for (int pp = 0; pp < S; ++pp)
+          bf[pp] = *reinterpret_cast<const v4i*>(st + pp * PL + cb * 32 + ((c ^ ((cb >> 3) & 1)) << 4));
+#pragma unroll
+        for (int pa = 1; pa <= S; ++pa) {
+#pragma unroll
+          for (int qb = 1; pa + qb <= S + 1; ++qb)
+            acc[pa + qb - 2] = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[pa - 1], bf[qb - 1], acc[pa + qb - 2], 0, 0, 0);
+          if (more) af[pa - 1] = load_a1(voff, kt + 1, pa - 1);
+        }
+      }
+      double s = 0.0;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        double v = (double)acc[S - 1][r];
+#pragma unroll
+        for (int g = S - 2; g >= 0; --g) v = __builtin_fma(v, 0x1p-7, (double)acc[g][r]);
+        const int rl = wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        v *= srs[rl];
+        s = __builtin_fma(v, v, s);
+      }
+      s += __shfl_xor(s, 32);
+      if (lane < 32) red[wm * IN + wn * 32 + lane] = s;
+      __syncthreads();
+      if (t < IN) {
+        const int64_t col = col0 + t;
+        if (col < m) part[(int64_t)rt * ldk + col] = red[t] + red[IN + t];
+      }
+    }
+  }
+}
+
+// random digits: A lower triangular (zero for k > row), signed in [-127, 127];
+// B in [0, 127]
+__device__ inline uint32_t mix(uint64_t x) {
+  x ^= x >> 33;
+  x *= 0xff51afd7ed558ccdull;
+  x ^= x >> 33;
+  x *= 0xc4ceb9fe1a85ec53ull;
+  x ^= x >> 33;
+  return (uint32_t)x;
+}
+__global__ void k_fill_a(int8_t* A, int S, int32_t n, int32_t npad) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (int64_t)S * npad * npad) return;
+  const int pl = (int)(e / ((int64_t)npad * npad));
+  const int64_t rk = e % ((int64_t)npad * npad);
+  const int32_t r = (int32_t)(rk / npad), k = (int32_t)(rk % npad);
+  int8_t v = 0;
+  if (r < n && k <= r) v = (int8_t)((int)(mix(e * 7 + 1) % 255) - 127);
+  A[(int64_t)pl * npad * npad + i8_off(r, k, npad)] = v;
+}
+__global__ void k_fill_b(int8_t* B, int S, int32_t n, int32_t npad, int64_t m, int64_t ldk) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (int64_t)S * npad * ldk) return;
+  const int pl = (int)(e / ((int64_t)npad * ldk));
+  const int64_t ck = e % ((int64_t)npad * ldk);
+  const int64_t c = ck / npad;
+  const int32_t k = (int32_t)(ck % npad);
+  int8_t v = 0;
+  if (c < m && k < n) v = (int8_t)(mix(e * 13 + 5) % 128);
+  B[(int64_t)pl * npad * ldk + i8_off(c, k, ldk)] = v;
+}
+
+template <int S, int MODE, int KIND = 0>
+double run(int32_t n, int64_t m, bool check, int reps) {
+  const int TM = KIND == 1 ? JM : IM;
+  const int32_t npad = (n + 127) / 128 * 128;
+  const int64_t ldk = (m + 255) / 256 * 256;
+  const int32_t RT = npad / TM, CT = (int32_t)(ldk / IN);
+  int8_t *A, *B;
+  double *part, *rs;
+  int32_t* ticket;
+  CK(hipMalloc(&A, (size_t)S * npad * npad));
+  CK(hipMalloc(&B, (size_t)S * npad * ldk));
+  CK(hipMalloc(&part, sizeof(double) * RT * ldk));
+  CK(hipMalloc(&rs, sizeof(double) * npad));
+  CK(hipMalloc(&ticket, sizeof(int32_t) * 8));
+  std::vector<double> hrs(npad);
+  for (int i = 0; i < npad; ++i) hrs[i] = std::ldexp(1.0, -14 - (i % 5));
+  CK(hipMemcpy(rs, hrs.data(), sizeof(double) * npad, hipMemcpyHostToDevice));
+  hipLaunchKernelGGL(k_fill_a, dim3((unsigned)(((int64_t)S * npad * npad + 255) / 256)), dim3(256), 0, 0, A, S, n, npad);
+  hipLaunchKernelGGL(k_fill_b, dim3((unsigned)(((int64_t)S * npad * ldk + 255) / 256)), dim3(256), 0, 0, B, S, n, npad, m,
+                     ldk);
+  CK(hipDeviceSynchronize());
+  int ncu = 0;
+  CK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0));
+  const int32_t P = (RT + 1) / 2;
+  const int32_t nb = KIND == 1 ? ncu : 2 * ncu;
+  const int32_t W = nb / 8, Sg = W / P > 1 ? W / P : 1;
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  double best = 1e30;
+  for (int it = 0; it < reps + 1; ++it) {
+    CK(hipMemset(ticket, 0, sizeof(int32_t) * 8));
+    CK(hipEventRecord(e0));
+    if (KIND == 3)
+      hipLaunchKernelGGL((k_var_i8d<S, MODE>), dim3(nb), dim3(256), 0, 0, A, B, npad, ldk, RT, CT, m, ticket, rs, part, Sg);
+    else if (KIND == 2)
+      hipLaunchKernelGGL((k_var_i8c<S, MODE>), dim3(nb), dim3(256), 0, 0, A, B, npad, ldk, RT, CT, m, ticket, rs, part, Sg);
+    else if (KIND == 1)
+      hipLaunchKernelGGL((k_var_i8b<S, MODE>), dim3(nb), dim3(512), 0, 0, A, B, npad, ldk, RT, CT, m, ticket, rs, part, Sg);
+    else if (KIND == 4)
+      hipLaunchKernelGGL((k_var_i8<S, MODE, 3>), dim3(nb), dim3(256), 0, 0, A, B, npad, ldk, RT, CT, m, ticket, rs, part, Sg);
+    else
+      hipLaunchKernelGGL((k_var_i8<S, MODE>), dim3(nb), dim3(256), 0, 0, A, B, npad, ldk, RT, CT, m, ticket, rs, part, Sg);
+    CK(hipEventRecord(e1));
+    CK(hipEventSynchronize(e1));
+    float ms = 0;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    if (it > 0) best = std::min(best, (double)ms);
+  }
+  if (check) {
+    std::vector<int8_t> hA((size_t)S * npad * npad), hB((size_t)S * npad * ldk);
+    std::vector<double> hp((size_t)RT * ldk);
+    CK(hipMemcpy(hA.data(), A, hA.size(), hipMemcpyDeviceToHost));
+    CK(hipMemcpy(hB.data(), B, hB.size(), hipMemcpyDeviceToHost));
+    CK(hipMemcpy(hp.data(), part, sizeof(double) * hp.size(), hipMemcpyDeviceToHost));
+    double maxrel = 0.0;
+    for (int64_t c = 0; c < m; ++c)
+      for (int32_t rt = 0; rt < RT; ++rt) {
+        long double sum = 0.0L;
+        for (int32_t r = rt * TM; r < rt * TM + TM; ++r) {
+          long double v = 0.0L;
+          for (int g = 2; g <= S + 1; ++g) {
+            int64_t T = 0;
+            for (int pa = 1; pa < g; ++pa) {
+              const int qb = g - pa;
+              for (int32_t k = 0; k < npad; ++k)
+                T += (int64_t)hA[(size_t)(pa - 1) * npad * npad + i8_off(r, k, npad)] *
+                     (int64_t)hB[(size_t)(qb - 1) * npad * ldk + i8_off(c, k, ldk)];
+            }
+            v += (long double)T * std::ldexp(1.0L, -7 * (g - 2));
+          }
+          v *= (long double)hrs[r];
+          sum += v * v;
+        }
+        const double got = hp[(size_t)rt * ldk + c];
+        const double rel = std::fabs((double)((long double)got - sum)) / std::max(1e-300, (double)sum);
+        maxrel = std::max(maxrel, rel);
+      }
+    printf("  kind %d S=%d check n=%d m=%lld: max rel err %.3e %s\n", KIND, S, n, (long long)m, maxrel, maxrel < 1e-12 ? "OK" : "BAD");
+  }
+  CK(hipFree(A));
+  CK(hipFree(B));
+  CK(hipFree(part));
+  CK(hipFree(rs));
+  CK(hipFree(ticket));
+  return best;
+}
+
+int main(int argc, char** argv) {
+  {
+    int8_t hA[32 * 32], hB[32 * 32];
+    srand(11);
+    for (int i = 0; i < 32 * 32; ++i) hA[i] = (int8_t)(rand() % 255 - 127);
+    for (int i = 0; i < 32 * 32; ++i) hB[i] = (int8_t)(rand() % 255 - 127);
+    int8_t *dA, *dB;
+    int32_t* dD;
+    CK(hipMalloc(&dA, sizeof(hA)));
+    CK(hipMalloc(&dB, sizeof(hB)));
+    CK(hipMalloc(&dD, 1024 * 4));
+    CK(hipMemcpy(dA, hA, sizeof(hA), hipMemcpyHostToDevice));
+    CK(hipMemcpy(dB, hB, sizeof(hB), hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(k_map, dim3(1), dim3(64), 0, 0, dA, dB, dD);
+    int32_t hD[1024];
+    CK(hipMemcpy(hD, dD, sizeof(hD), hipMemcpyDeviceToHost));
+    int bad = 0;
+    for (int r = 0; r < 32; ++r)
+      for (int c = 0; c < 32; ++c) {
+        int32_t s = 0;
+        for (int k = 0; k < 32; ++k) s += (int32_t)hA[r * 32 + k] * (int32_t)hB[k * 32 + c];
+        bad += hD[r * 32 + c] != s;
+      }
+    printf("i8 32x32x32 map: %d / 1024 wrong\n", bad);
+    if (bad) return 1;
+  }
+  run<6, 0, 4>(300, 333, true, 1);
+  const int32_t n = argc > 1 ? atoi(argv[1]) : 1024;
+  const int64_t m = argc > 2 ? atoll(argv[2]) : (1 << 20);
+  const double alg = (double)m * n * (n + 1);   // fp64-equivalent flops of the triangular contraction
+  auto rep = [&](const char* name, int S, double ms) {
+    printf("%-28s S=%d  %8.3f ms  %6.1f TF(fp64-equiv)  %7.1f TOPS(i8)\n", name, S, ms, alg / ms * 1e-9,
+           alg * S * (S + 1) / 2 / ms * 1e-9);
+  };
+  rep("v1 2st full", 6, run<6, 0>(n, m, false, 5));
+  rep("v1 3st full", 6, run<6, 0, 4>(n, m, false, 5));
+  rep("v1 3st L2-hit", 6, run<6, 2, 4>(n, m, false, 5));
+  rep("v1 3st no loads", 6, run<6, 1, 4>(n, m, false, 5));
+  rep("v1 2st L2-hit", 6, run<6, 2>(n, m, false, 5));
+  rep("v1 2st no loads", 6, run<6, 1>(n, m, false, 5));
+  return 0;
+}

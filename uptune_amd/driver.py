@@ -130,6 +130,9 @@ class SearchDriver:
         self.results: Dict[str, Result] = {}               # hash -> first result (convenience view)
         self._unprocessed: List[Result] = []
         self._todo: List[DesiredResult] = []               # REQUESTED, not yet measured
+        # (test_count, requestor, first requestor, OLD | PENDING) per duplicate
+        # request: the reference's log line (driver.py:186-191) as data
+        self.duplicate_log: List[tuple] = []
         if hasattr(self.objective, "set_driver"):
             self.objective.set_driver(self)
         self.root_technique.set_driver(self)
@@ -246,7 +249,12 @@ class SearchDriver:
             first = self._first_request.get(dr.key)
             self._add_request(dr)
             if first is not None:
-                log.debug("duplicate configuration request %s/%s", dr.requestor, first.requestor)
+                # driver.py:186-191: the earliest request of the configuration,
+                # OLD once it has a result, PENDING before
+                cls = "OLD" if first.result is not None else "PENDING"
+                self.duplicate_log.append((self.test_count, dr.requestor, first.requestor, cls))
+                log.warning("duplicate configuration request #%d %s/%s %s", self.test_count, dr.requestor,
+                            first.requestor, cls)
 
                 def cb(result, dr=dr):
                     dr.result = result
