@@ -59,6 +59,8 @@ sys.path.insert(0, ROOT)
 PEAK_FP64_TFLOPS = 78.6
 PEAK_FP32_TFLOPS = 157.3
 PEAK_FP16_TFLOPS = 2516.6   # dense fp16 MFMA (256 CU x 4 SIMD x 1024 flop/clk x 2.4 GHz)
+PEAK_I8_TOPS = 5033.2       # dense int8 MFMA (2x the fp16 rate: 32x32x32 i8 in the cycles of 32x32x16 f16)
+I8_PRODUCTS = 21            # digit-plane products per algorithmic multiply-add at precision 8 (gp_i8.hip)
 PEAK_HBM_GBS = 8000.0
 
 
@@ -363,9 +365,11 @@ def main():
     ap.add_argument("--no-parity", action="store_true", help="skip the oracle check of the selections")
     ap.add_argument("--parity-sample", type=int, default=1 << 16,
                     help="random other candidates whose oracle EI must not beat the score-determined top-k")
-    ap.add_argument("--precision", type=int, default=64, choices=(64, 32, 16),
+    ap.add_argument("--precision", type=int, default=64, choices=(64, 32, 16, 8),
                     help="GP contractions on fp64 MFMA (1e-5 parity) or fp32 MFMA (1e-3 parity); 16 = f16x3: "
-                         "the variance contraction as 3 fp16 MFMA products of hi/lo splits (fp32 tier, 1e-3)")
+                         "the variance contraction as 3 fp16 MFMA products of hi/lo splits (fp32 tier, 1e-3); "
+                         "8 = the fp64 tier (1e-5) on the int8 MFMA: six-digit slices, per-candidate error "
+                         "bound, fp64 recompute of the candidates it does not clear")
     ap.add_argument("--config", default="c2", choices=("c2", "c3", "c4"),
                     help="c2 = BASELINE configs[1] (R64, m=1M, n=1024: the headline); c3 = configs[2] per GPU "
                          "(HPL-64 mixed space, 16M/8 = 2M candidates per GPU, n=4096); c4 = configs[3] "
@@ -546,12 +550,13 @@ def main():
     # per-stage device times of the timed rounds (HIP events recorded on the
     # library's streams during the rounds, read once here)
     for st in ("propose", "hash", "dedup", "encode", "prep", "fit_wait", "kstar", "bound", "prune", "var", "finalize",
-               "topk"):
+               "recompute", "topk"):
         try:
             stage_ms[st] = [eng.stage_time(st)]
         except Exception:
             pass
     eng.set_timing(False)
+    i8_timed = eng.gp_i8_stats() if args.precision == 8 else None
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -630,6 +635,10 @@ def main():
     if args.precision == 16:
         kernel = ("k_gp_var_h3 (persistent var contraction L^-1 K*^T, 3 x v_mfma_f32_32x32x16_f16 per product "
                   "on hi/lo fp16 splits; peak = fp16 dense peak / 3)")
+    if args.precision == 8:
+        kernel = ("k_gp_var_i8 (persistent var contraction L^-1 K*^T over six balanced int8 digit planes per "
+                  "operand, %d v_mfma_i32_32x32x32_i8 digit products per multiply-add, exact int32 group sums; "
+                  "peak = int8 dense peak / %d)" % (I8_PRODUCTS, I8_PRODUCTS))
     if args.config == "c4" and stages.get("kstar", 0.0) > (var_ms or 0.0):
         var_ms = stages["kstar"]
         flops_var = 2.0 * m * n * d
@@ -648,13 +657,22 @@ def main():
                   "survivors only]" % ("true" if k64 < d else "false", k64,
                                        " + the one-hot codes on v_mfma_i32_16x16x64_i8" if k64 < d else ""))
     achieved = flops_var / (var_ms * 1e-3) / 1e12 if var_ms else None
-    peak = {64: PEAK_FP64_TFLOPS, 32: PEAK_FP32_TFLOPS, 16: PEAK_FP16_TFLOPS / 3.0}[args.precision]
+    peak = {64: PEAK_FP64_TFLOPS, 32: PEAK_FP32_TFLOPS, 16: PEAK_FP16_TFLOPS / 3.0,
+            8: PEAK_I8_TOPS / I8_PRODUCTS}[args.precision]
     # HBM bytes per launch and the rocprof average duration were profiled on the
     # default C2 round (profiles/pmc_summary.json)
     profiled = args.config == "c2" and (m, n, d) == (1 << 20, 1024, 64) and not args.prune
-    pmc, pmc_note = load_pmc({64: "var", 32: "var32", 16: "var16"}[args.precision]) if profiled else ({}, "")
+    pmc, pmc_note = load_pmc({64: "var", 32: "var32", 16: "var16", 8: "var8"}[args.precision]) if profiled else ({}, "")
     traffic = pmc.get("hbm_bytes_per_launch")
     frac_rocprof = (flops_var / (pmc["avg_ns"] * 1e-9) / 1e12 / peak) if pmc.get("avg_ns") else None
+    i8_info = None
+    if args.precision == 8:
+        rec, bound_e = eng.gp_i8_stats()   # the last round run: the score-determined parity round when it ran
+        i8_info = {"recomputed_fp64_last_timed_round": i8_timed[0], "bound_E": i8_timed[1],
+                   "recomputed_fp64_last_round_run": rec, "bound_E_last_round_run": bound_e, "digit_planes": 6,
+                   "products": I8_PRODUCTS, "tolerance": 2.0 ** -20,
+                   "note": "variance error per candidate <= E (2 |v| + E) (+ f64 rounding); accepted iff that is "
+                           "<= tolerance * var, else recomputed on the f64 path (gp_i8.hip)"}
     prune_info = None
     if args.prune and prune_stats:
         timed = prune_stats[-args.steps:]
@@ -694,7 +712,10 @@ def main():
         "dtype": {64: "f64", 32: "f32 (variance L^-1 K*^T on fp32 MFMA; K* contracted in fp64, stored f32; "
                       "fit/mean/EI f64)",
                   16: "f32-tier f16x3 (L^-1 K*^T as hi*hi + hi*lo + lo*hi fp16 MFMA, f32 accumulate; "
-                      "K*/fit/EI f64)"}[args.precision],
+                      "K*/fit/EI f64)",
+                  8: "f64-tier (int8 Ozaki slices: L^-1 K*^T over 6 balanced 8-bit digit planes, exact int32 "
+                     "sums, per-candidate error bound <= 2^-20 relative on the variance, the rest recomputed in "
+                     "f64; K*/mean/fit/EI f64)"}[args.precision],
         "data": data,
         "config": {"workload": workload, "candidates_per_gpu": m, "global_pool": npop, "gp_n": n, "dims": d,
                    "k": k, "parallelism": f"dp{world}", "scaling": args.scaling,
@@ -707,6 +728,7 @@ def main():
         "stage_ms": stages,
         "kernels": (kernel_table(m, n, d, eng.space_info()[1]) if profiled else None),
         "prune": prune_info,
+        "i8": i8_info,
         "roofline": {"bound": "mfma", "kernel": kernel,
                      "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
                      "frac": (achieved / peak) if achieved else None, "traffic": traffic,

@@ -301,9 +301,22 @@ int ut_gp_topk_pruned(ut_ctx* ctx, const double* features, int64_t ld, int64_t m
  * after this call: 64 = fp64 MFMA (default; 1e-5 parity), 32 = fp32 MFMA
  * (1e-3 parity), 16 = "f16x3": K* in fp64, the variance contraction as three
  * fp16 MFMA products (hi*hi + hi*lo + lo*hi) of scaled hi/lo splits of L^-1 and
- * K*, f32 accumulate (fp32-class, the same 1e-3 parity tier).  The fit itself
- * is always fp64. */
+ * K*, f32 accumulate (fp32-class, the same 1e-3 parity tier), 8 = the fp64
+ * tier on the int8 MFMA: K* in fp64 (mean k* . alpha in fp64), the variance
+ * contraction over six 8-bit digit planes of L^-1 and K* with exact int32
+ * sums, each candidate's variance error bounded from the digits' truncation;
+ * candidates whose bound exceeds ut_gp_set_i8_tol (relative) are recomputed
+ * on the fp64 path (1e-5 parity, the fp64 tier's).  The fit itself is always
+ * fp64.  Replaces the variance half of the per-candidate GP posterior the
+ * reference has none of; precision 8 scores need n <= 16384. */
 int ut_gp_set_precision(ut_ctx* ctx, int32_t bits);
+/* precision 8: the largest accepted relative error of a candidate's variance
+ * (default 2^-20); 0 recomputes every candidate in fp64 */
+int ut_gp_set_i8_tol(ut_ctx* ctx, double tol);
+/* precision 8: candidates of the last ut_gp_score / round recomputed in fp64
+ * (-1: most were, and the whole round ran the fp64 contraction), and the
+ * current fit's bound E on |L^-1 k* - v^| */
+int ut_gp_i8_stats(ut_ctx* ctx, int64_t* recomputed_host, double* bound_host);
 /* order everything enqueued on ctx's stream after this call behind the
  * in-flight fit (a stream wait on its event; no host wait).  Scoring that
  * needs the whole fit (pruned, fp32, f16x3) then starts with the fit done, and

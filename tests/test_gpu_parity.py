@@ -335,10 +335,11 @@ def test_gp_small_golden(golden_dir):
     _close(ucb.cpu().numpy(), z["ucb"])
 
 
-@pytest.mark.parametrize("prec", [64, 32, 16])
+@pytest.mark.parametrize("prec", [64, 32, 16, 8])
 @pytest.mark.parametrize("n,d,ell", [(1024, 64, 0.2), (200, 8, 0.5), (77, 3, 0.25), (300, 16, 1.5), (4096, 112, 1.0)])
 def test_gp_vs_oracle(n, d, ell, prec):
-    """fp64: 1e-5 relative; fp32 MFMA / f16x3 variance contraction: 1e-3 relative
+    """fp64 and the int8-sliced fp64 tier (precision 8): 1e-5 relative; fp32
+    MFMA / f16x3 variance contraction: 1e-3 relative
     (north star), absolute floor 1e-5 (variance near training points is a
     cancellation).  K* and mu stay fp64 in both lower tiers: the first ten
     candidates sit 1e-3 from training points, where |x/ell|^2 ~ 500 and a K*
@@ -357,7 +358,7 @@ def test_gp_vs_oracle(n, d, ell, prec):
     mu_o, var_o = g.posterior(U)
     ei_o = ogp.acquisition(mu_o, var_o, g.f_best)
     mu, var, ei = e.gp_score(dev(U.T))
-    if prec == 64:
+    if prec in (64, 8):
         _close(mu.cpu().numpy(), mu_o)
         _close(var.cpu().numpy(), var_o, atol=1e-8)
         _close(ei.cpu().numpy(), ei_o, atol=1e-8)
@@ -402,7 +403,7 @@ def test_gp_f16x3_scaling(sf2, ell, sn2, tier):
     assert err[16] <= max(4 * err[32], 1e-7), err
 
 
-@pytest.mark.parametrize("prec", [64, 32, 16])
+@pytest.mark.parametrize("prec", [64, 32, 16, 8])
 @pytest.mark.parametrize("n0,steps,d", [(130, [120], 8), (1000, [4], 64), (513, [1] * 7 + [3], 16),
                                         (40, [4] * 6, 7), (700, [60, 60, 60], 32)])
 def test_gp_fit_append_equals_refit(n0, steps, d, prec):
@@ -436,7 +437,7 @@ def test_gp_fit_append_equals_refit(n0, steps, d, prec):
     g = ogp.GP(X, y, lengthscale=0.5, sigma_f2=1.0, sigma_n2=1e-6, jitter=1e-8)
     mu_o, var_o = g.posterior(U)
     ei_o = ogp.acquisition(mu_o, var_o, g.f_best)
-    if prec == 64:
+    if prec in (64, 8):
         _close(mu, mu_f, rtol=1e-10, atol=1e-12)
         _close(var, var_f, rtol=1e-10, atol=1e-12)
         _close(mu, mu_o)
@@ -1276,7 +1277,7 @@ def test_chol_merged_bitwise(n):
 
 
 @pytest.mark.parametrize("which", ["hpl", "gcc", "mixed", "perm"])
-@pytest.mark.parametrize("prec", [64, 32, 16])
+@pytest.mark.parametrize("prec", [64, 32, 16, 8])
 def test_categorical_kstar_equals_dense(which, prec):
     """The categorical K* (ENUM / BOOL one-hot blocks as an int8 code product on
     v_mfma_i32_16x16x64_i8, the other features on the fp64 contraction) gives
@@ -1307,7 +1308,7 @@ def test_categorical_kstar_equals_dense(which, prec):
     g = ogp.GP(X, y, lengthscale=ell, sigma_f2=1.0, sigma_n2=1e-6, jitter=1e-8)
     wmu, wvar = g.posterior(features(space, cand).T)
     ei = ogp.acquisition(wmu, wvar, g.f_best)
-    if prec == 64:
+    if prec in (64, 8):
         np.testing.assert_allclose(mu_c, mu_d, rtol=1e-9, atol=1e-10)
         np.testing.assert_allclose(var_c, var_d, rtol=1e-9, atol=1e-10)
         np.testing.assert_allclose(sc_c, sc_d, rtol=1e-9, atol=1e-10)

@@ -804,8 +804,30 @@ int ut_gp_topk_pruned(ut_ctx* c, const double* feat, int64_t ld, int64_t m, cons
 
 int ut_gp_set_precision(ut_ctx* c, int32_t bits) {
   if (!c) return UT_EINVAL;
-  UT_CHECK(c, bits == 64 || bits == 32 || bits == 16, UT_EINVAL, "gp precision must be 64, 32 or 16 (f16x3)");
+  UT_CHECK(c, bits == 64 || bits == 32 || bits == 16 || bits == 8, UT_EINVAL,
+           "gp precision must be 64, 32, 16 (f16x3) or 8 (int8 slices, fp64 tier)");
   c->gp_prec = bits;
+  return 0;
+}
+
+int ut_gp_set_i8_tol(ut_ctx* c, double tol) {
+  if (!c) return UT_EINVAL;
+  UT_CHECK(c, tol >= 0.0 && tol < 1.0, UT_EINVAL, "i8 tolerance must be in [0, 1)");
+  c->i8_tol = tol;
+  return 0;
+}
+
+int ut_gp_i8_stats(ut_ctx* c, int64_t* recomputed, double* bound) {
+  if (!c) return UT_EINVAL;
+  if (recomputed) *recomputed = c->i8_recomputed;
+  if (bound) {
+    *bound = 0.0;
+    if (c->gp_fit_prec == 8 && c->gp_i8rs.p) {
+      UT_HIP(c, hipStreamSynchronize(c->fit_stream));
+      const int32_t npad = ((c->gp_n + 127) / 128) * 128;
+      UT_HIP(c, hipMemcpy(bound, c->gp_i8rs.p + 2 * npad, sizeof(double), hipMemcpyDeviceToHost));
+    }
+  }
   return 0;
 }
 

@@ -852,6 +852,71 @@ __global__ void k_gp_finalize(int64_t m, int32_t RT1, int32_t RT2, const double*
   if (score_out) score_out[i] = sc;
 }
 
+// precision 8 (gp_i8.hip): mu from K*'s fp64 epilogue, |v|^2 from the int8
+// contraction's partials; a candidate is finished here only if the bound
+//   | |v|^2 - s | <= E (2 sqrt(s) + E) + s (2n + 64) 2^-53     (s = the computed sum)
+// is at most tol * (sf2 - s): its variance is then within tol relative of the
+// exact one.  Every other candidate (near a training point sf2 - |v|^2 cancels;
+// or a failed fit) is appended to idx_out for the fp64 recompute (k_gp_fix_i8),
+// one atomic per wave; its outputs are written anyway and overwritten there.
+__global__ void k_gp_finalize_i8(int64_t m, int32_t RT1, int32_t RT2, const double* __restrict__ mu_part,
+                                 const double* __restrict__ var_part, int64_t ldp, double sf2,
+                                 const double* __restrict__ stats, const int32_t* __restrict__ fit_flag, int32_t kind,
+                                 double xi, double kappa, const uint8_t* __restrict__ dup, double* __restrict__ mu_out,
+                                 double* __restrict__ var_out, double* __restrict__ score_out,
+                                 const double* __restrict__ Ebound, double tol, int32_t n, int64_t* __restrict__ idx_out,
+                                 unsigned long long* __restrict__ count) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  bool flag = false;
+  if (i < m) {
+    double mu = 0.0, vs = 0.0;
+    for (int32_t r = 0; r < RT1; ++r) mu += mu_part[(int64_t)r * ldp + i];
+    for (int32_t r = 0; r < RT2; ++r) vs += var_part[(int64_t)r * ldp + i];
+    double var = sf2 - vs;
+    var = var > 0.0 ? var : 0.0;
+    const double E = *Ebound;
+    const double bound = E * (2.0 * sqrt(vs) + E) + vs * (double)(2 * n + 64) * 0x1p-53;
+    flag = !(bound <= tol * var);   // (NaN: flagged)
+    double sc = acq_score(kind, mu, var, stats[0], xi, kappa);
+    if (*fit_flag != 0) {
+      mu = var = sc = __builtin_nan("");
+      flag = false;   // nothing to recompute: the fit failed
+    }
+    if (dup && dup[i]) sc = -1.0 / 0.0;
+    if (mu_out) mu_out[i] = mu;
+    if (var_out) var_out[i] = var;
+    if (score_out) score_out[i] = sc;
+  }
+  const unsigned long long ball = __ballot(flag);
+  const uint32_t nf = __builtin_popcountll(ball);
+  unsigned long long base = 0;
+  if (lane == 0 && nf) base = atomicAdd(count, (unsigned long long)nf);
+  base = __shfl(base, 0, 64);
+  if (flag) idx_out[base + __builtin_popcountll(ball & ((1ull << lane) - 1ull))] = i;
+}
+
+// the flagged candidates' fp64 variance (recomputed K* columns through the fp64
+// contraction, RT partials each) -> var and score (mu stays K*'s)
+__global__ void k_gp_fix_i8(int64_t nf, const int64_t* __restrict__ idx, int32_t RT1, const double* __restrict__ mu_part,
+                            int64_t ldp, int32_t RT, const double* __restrict__ vpart, int64_t ldv, double sf2,
+                            const double* __restrict__ stats, int32_t kind, double xi, double kappa,
+                            const uint8_t* __restrict__ dup, double* __restrict__ var_out,
+                            double* __restrict__ score_out) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= nf) return;
+  const int64_t i = idx[j];
+  double mu = 0.0, vs = 0.0;
+  for (int32_t r = 0; r < RT1; ++r) mu += mu_part[(int64_t)r * ldp + i];
+  for (int32_t r = 0; r < RT; ++r) vs += vpart[(int64_t)r * ldv + j];
+  double var = sf2 - vs;
+  var = var > 0.0 ? var : 0.0;
+  double sc = acq_score(kind, mu, var, stats[0], xi, kappa);
+  if (dup && dup[i]) sc = -1.0 / 0.0;
+  if (var_out) var_out[i] = var;
+  if (score_out) score_out[i] = sc;
+}
+
 // ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
@@ -933,6 +998,8 @@ static bool cat_rows_ok(const Space& s, const double* X, int32_t d, int32_t r0, 
 int gp_fit_enqueue(ut_ctx* c, const double* X, const double* y, int32_t n, int32_t d, const ut_gp_hyper* h) {
   UT_CHECK(c, n >= 1 && d >= 1 && X && y && h && h->lengthscale_host, UT_EINVAL, "gp_fit: bad arguments");
   const int32_t npad = ((n + NPAD - 1) / NPAD) * NPAD;
+  UT_CHECK(c, c->gp_prec != 8 || npad <= I8_MAX_K, UT_EINVAL,
+           "gp_fit: precision 8 takes at most 16384 training points (exact int32 digit sums)");
   // the previous fit's copies out of the pinned staging (and its factor) are
   // complete once ev_fit is
   if (c->fit_pending) UT_HIP(c, hipEventSynchronize(c->ev_fit));
@@ -1125,6 +1192,7 @@ int gp_fit_enqueue(ut_ctx* c, const double* X, const double* y, int32_t n, int32
   UT_LAUNCH_CHECK(c);
   if (c->gp_prec == 16 && (rc = launch_split_h3(c, c->gp_Linv, npad, reinterpret_cast<_Float16*>(c->gp_LinvT_f))))
     return rc;
+  if (c->gp_prec == 8 && (rc = launch_split_i8(c, n, npad))) return rc;
   c->gp_fit_prec = c->gp_prec;
   c->gp_npad_fit = npad;
   c->gp_diag_fit = diag;
@@ -1184,6 +1252,9 @@ static KstarCat kstar_cat(ut_ctx* c, const int8_t* bcat) {
   return k;
 }
 
+static int gather_kstar_cols(ut_ctx* c, bool cat, int32_t dpad, int64_t ldk, const int64_t* idx, int64_t base,
+                             int64_t nc, int64_t ldc);
+
 int gp_score_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, const ut_acq* acq, const uint8_t* dup,
                   double* mu, double* var, double* score, hipEvent_t dup_ready, const std::function<int()>& mid,
                   bool var_joins) {
@@ -1191,7 +1262,8 @@ int gp_score_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, const ut
   UT_CHECK(c, acq != nullptr, UT_EINVAL, "gp_score: acq is NULL");
   if (m <= 0) return 0;
   const int prec = c->gp_fit_prec;
-  const bool fp32 = prec != 64;  // fp32 and h3 (f16x3) take the mean in K* and wait for the whole fit
+  const bool fp32 = prec != 64;  // fp32, h3 (f16x3) and i8 take the mean in K* and wait for the whole fit
+  const bool i8 = prec == 8;
   // fp64: K* needs only the scaled training inputs (ev_fit_x) and the mean
   // comes from the variance epilogue, mu = (L^-1 k*) . (L^-1 y), so K*
   // overlaps the rest of an asynchronous fit and only the variance GEMM waits
@@ -1213,9 +1285,15 @@ int gp_score_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, const ut
   int rc;
   if ((rc = ensure(c, c->kst, (size_t)npad * ldk))) return rc;
   if ((rc = ensure(c, c->mu_part, (size_t)RT * ldk))) return rc;
-  if ((rc = ensure(c, c->var_part, (size_t)RT * ldk))) return rc;
+  // (i8: the variance partials come per 64-row tile)
+  if ((rc = ensure(c, c->var_part, (size_t)(i8 ? 2 * RT : RT) * ldk))) return rc;
   if ((rc = ensure(c, c->cnorm, (size_t)ldk))) return rc;
   if ((rc = ensure(c, c->ucand, (size_t)(dpad > 0 ? dpad : 1) * ldk))) return rc;
+  if (i8) {
+    UT_CHECK(c, npad <= I8_MAX_K, UT_EINVAL, "gp_score: precision 8 takes at most 16384 training points");
+    if ((rc = ensure(c, c->pr_idx, (size_t)ldk))) return rc;
+    if ((rc = ensure(c, c->pr_count, 1))) return rc;
+  }
   if (feat) {
     if ((rc = launch_prep_cand(c, feat, ld, m, d, dpad, c->ucand.p, ldk, c->cnorm.p))) return rc;
     c->ucand_cat = false;
@@ -1230,12 +1308,60 @@ int gp_score_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, const ut
   if (c->fit_pending && !fp32) UT_HIP(c, hipStreamWaitEvent(c->stream, c->ev_fit, 0));
   if (dup_ready && c->join_before_var && var_joins) UT_HIP(c, hipStreamWaitEvent(c->stream, dup_ready, 0));
   mark(c, "");  // the wait for the fit is not variance time
-  if ((rc = launch_gemm_var(c, prec, fp32 ? (const void*)c->gp_LinvT_f : (const void*)c->gp_LinvT, npad, c->kst.p,
-                            ldk, npad, m, c->var_part.p, fp32 ? nullptr : c->gp_beta,
-                            fp32 ? nullptr : c->mu_part.p)))
+  if (i8) {
+    if ((rc = launch_gemm_var_i8(c, npad, reinterpret_cast<const int8_t*>(c->kst.p), ldk, m, c->var_part.p)))
+      return rc;
+  } else if ((rc = launch_gemm_var(c, prec, fp32 ? (const void*)c->gp_LinvT_f : (const void*)c->gp_LinvT, npad,
+                                   c->kst.p, ldk, npad, m, c->var_part.p, fp32 ? nullptr : c->gp_beta,
+                                   fp32 ? nullptr : c->mu_part.p))) {
     return rc;
+  }
   mark(c, "var");
   if (dup_ready) UT_HIP(c, hipStreamWaitEvent(c->stream, dup_ready, 0));
+  if (i8) {
+    // the bound test, then the fp64 recompute of the candidates it did not clear
+    UT_HIP(c, hipMemsetAsync(c->pr_count.p, 0, sizeof(int64_t), c->stream));
+    hipLaunchKernelGGL(k_gp_finalize_i8, dim3(grid1(m, 256)), dim3(256), 0, c->stream, m, RT, 2 * RT, c->mu_part.p,
+                       c->var_part.p, ldk, c->gp_sf2, c->gp_stats, c->gp_flag, acq->kind, acq->xi, acq->kappa, dup,
+                       mu, var, score, c->gp_i8rs.p + 2 * npad, c->i8_tol, n, c->pr_idx.p,
+                       reinterpret_cast<unsigned long long*>(c->pr_count.p));
+    UT_LAUNCH_CHECK(c);
+    mark(c, "finalize");
+    int64_t nf = 0;
+    UT_HIP(c, hipMemcpyAsync(&nf, c->pr_count.p, sizeof(int64_t), hipMemcpyDeviceToHost, c->stream));
+    UT_HIP(c, hipStreamSynchronize(c->stream));
+    c->i8_recomputed = nf;
+    if (nf * 2 > m) {
+      // most candidates need fp64: the whole K* (fp64, over the planes) and the
+      // fp64 contraction; the mean partials stay K*'s
+      c->i8_recomputed = -1;
+      if ((rc = ensure(c, c->pr_mpart, (size_t)RT * ldk))) return rc;
+      if ((rc = launch_gemm_kstar(c, 64, cat ? c->gp_XsT_num.p : c->gp_XsT, npad, c->ucand.p, dpad, m, c->kst.p, ldk,
+                                  nullptr, -1, nullptr, nullptr, cat ? kstar_cat(c, c->bcat.p) : KstarCat(),
+                                  cat ? c->gp_xnorm_num.p : nullptr)))
+        return rc;
+      if ((rc = launch_gemm_var(c, 64, c->gp_LinvT, npad, c->kst.p, ldk, npad, m, c->var_part.p, c->gp_beta,
+                                c->pr_mpart.p)))
+        return rc;
+      hipLaunchKernelGGL(k_gp_finalize, dim3(grid1(m, 256)), dim3(256), 0, c->stream, m, RT, RT, c->mu_part.p,
+                         c->var_part.p, ldk, c->gp_sf2, c->gp_stats, c->gp_flag, acq->kind, acq->xi, acq->kappa, dup,
+                         mu, var, score);
+      UT_LAUNCH_CHECK(c);
+    } else if (nf > 0) {
+      const int64_t ldf = (nf + VAR_BN - 1) / VAR_BN * VAR_BN;
+      if ((rc = ensure(c, c->pr_mpart, (size_t)RT * ldf))) return rc;
+      if ((rc = gather_kstar_cols(c, cat, dpad, ldk, c->pr_idx.p, 0, nf, ldf))) return rc;
+      if ((rc = launch_gemm_var(c, 64, c->gp_LinvT, npad, c->pr_kst.p, ldf, npad, nf, c->pr_vpart.p, c->gp_beta,
+                                c->pr_mpart.p)))
+        return rc;
+      hipLaunchKernelGGL(k_gp_fix_i8, dim3(grid1(nf, 256)), dim3(256), 0, c->stream, nf, c->pr_idx.p, RT,
+                         c->mu_part.p, ldk, RT, c->pr_vpart.p, ldf, c->gp_sf2, c->gp_stats, acq->kind, acq->xi,
+                         acq->kappa, dup, var, score);
+      UT_LAUNCH_CHECK(c);
+    }
+    mark(c, "recompute");
+    return 0;
+  }
   // h3's variance partials come per 256-row tile
   const int32_t RTv = prec == 16 ? (npad + 255) / 256 : RT;
   hipLaunchKernelGGL(k_gp_finalize, dim3(grid1(m, 256)), dim3(256), 0, c->stream, m, RT, RTv, c->mu_part.p,
@@ -1418,6 +1544,38 @@ __global__ void k_fill(double* __restrict__ p, int64_t n, double v) {
   if (i < n) p[i] = v;
 }
 
+// full fp64 K* columns of the candidates idx[0..nc) (global indices - base;
+// idx < 0: an empty slot) into c->pr_kst [npad][ldc]: their scaled features
+// and norms (and categorical codes) gathered from the K* operands of the
+// round (c->ucand / c->cnorm / c->bcat, leading dimension ldk), then the K*
+// GEMM on those columns only (pruned scoring's threshold set and survivors,
+// precision 8's flagged candidates)
+static int gather_kstar_cols(ut_ctx* c, bool cat, int32_t dpad, int64_t ldk, const int64_t* idx, int64_t base,
+                             int64_t nc, int64_t ldc) {
+  const int32_t npad = ((c->gp_n + NPAD - 1) / NPAD) * NPAD;
+  const int32_t RT = npad / NPAD;
+  const double* XsT = cat ? c->gp_XsT_num.p : c->gp_XsT;
+  const double* xn = cat ? c->gp_xnorm_num.p : nullptr;
+  int r2;
+  if ((r2 = ensure(c, c->pr_kst, (size_t)npad * ldc))) return r2;
+  if ((r2 = ensure(c, c->pr_vpart, (size_t)RT * ldc))) return r2;
+  if ((r2 = ensure(c, c->pr_ucand, (size_t)(dpad > 0 ? dpad : 1) * ldc))) return r2;
+  if ((r2 = ensure(c, c->pr_cnorm, (size_t)ldc))) return r2;
+  if (dpad > 0)
+    hipLaunchKernelGGL(k_gather_cols, dim3(grid1(ldc, 256), (unsigned)dpad), dim3(256), 0, c->stream, c->ucand.p,
+                       ldk, idx, base, nc, ldc, c->pr_ucand.p);
+  hipLaunchKernelGGL(k_gather_cols, dim3(grid1(ldc, 256), 1u), dim3(256), 0, c->stream, c->cnorm.p, ldk, idx, base,
+                     nc, ldc, c->pr_cnorm.p);
+  if (cat) {   // the gathered candidates' 128-byte code rows, per code block
+    if ((r2 = ensure(c, c->pr_bcat, (size_t)c->space.cat_k * ldc))) return r2;
+    hipLaunchKernelGGL(k_gather_code_rows, dim3(grid1(ldc * 8, 256), (unsigned)(c->space.cat_k / 128)), dim3(256), 0,
+                       c->stream, c->bcat.p, ldk, idx, base, nc, ldc, c->pr_bcat.p);
+  }
+  UT_LAUNCH_CHECK(c);
+  return launch_gemm_kstar(c, 64, XsT, npad, c->pr_ucand.p, dpad, nc, c->pr_kst.p, ldc, nullptr, -1,
+                           c->pr_cnorm.p, nullptr, cat ? kstar_cat(c, c->pr_bcat.p) : KstarCat(), xn);
+}
+
 int gp_topk_pruned_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, const ut_acq* acq, const uint8_t* dup,
                         int64_t cand_base, int32_t k, int32_t bound_rows, int64_t* out_idx, double* out_score,
                         ut_prune_stats* stats, hipEvent_t dup_ready, bool feat_ours) {
@@ -1499,27 +1657,8 @@ int gp_topk_pruned_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, co
   double* tsc = c->pr_score.p + ldk;                   // [1024] their bounds
   double* tex = c->pr_score.p + ldk + 1024;            // [1024] their exact scores
   if ((rc = topk_impl(c, c->pr_ub.p, dup, m, cand_base, kp < k ? k : kp, tset, tsc))) return rc;
-  // full K* columns of the candidates idx[0..nc) (global indices - base): their
-  // scaled features and norms gathered, then the K* GEMM on those columns only
   auto recompute_cols = [&](const int64_t* idx, int64_t base, int64_t nc, int64_t ldc) -> int {
-    int r2;
-    if ((r2 = ensure(c, c->pr_kst, (size_t)npad * ldc))) return r2;
-    if ((r2 = ensure(c, c->pr_vpart, (size_t)RT * ldc))) return r2;
-    if ((r2 = ensure(c, c->pr_ucand, (size_t)(dpad > 0 ? dpad : 1) * ldc))) return r2;
-    if ((r2 = ensure(c, c->pr_cnorm, (size_t)ldc))) return r2;
-    if (dpad > 0)
-      hipLaunchKernelGGL(k_gather_cols, dim3(grid1(ldc, 256), (unsigned)dpad), dim3(256), 0, c->stream, c->ucand.p,
-                         ldk, idx, base, nc, ldc, c->pr_ucand.p);
-    hipLaunchKernelGGL(k_gather_cols, dim3(grid1(ldc, 256), 1u), dim3(256), 0, c->stream, c->cnorm.p, ldk, idx, base,
-                       nc, ldc, c->pr_cnorm.p);
-    if (cat) {   // the gathered candidates' 128-byte code rows, per code block
-      if ((r2 = ensure(c, c->pr_bcat, (size_t)c->space.cat_k * ldc))) return r2;
-      hipLaunchKernelGGL(k_gather_code_rows, dim3(grid1(ldc * 8, 256), (unsigned)(c->space.cat_k / 128)), dim3(256), 0,
-                         c->stream, c->bcat.p, ldk, idx, base, nc, ldc, c->pr_bcat.p);
-    }
-    UT_LAUNCH_CHECK(c);
-    return launch_gemm_kstar(c, 64, XsT, npad, c->pr_ucand.p, dpad, nc, c->pr_kst.p, ldc, nullptr, -1,
-                             c->pr_cnorm.p, nullptr, cat ? kstar_cat(c, c->pr_bcat.p) : KstarCat(), xn);
+    return gather_kstar_cols(c, cat, dpad, ldk, idx, base, nc, ldc);
   };
   const int64_t ldt = ((int64_t)kp + VAR_BN - 1) / VAR_BN * VAR_BN;
   if ((rc = recompute_cols(tset, cand_base, kp, ldt))) return rc;

@@ -178,6 +178,11 @@ __global__ __launch_bounds__(K_NT, 2) void k_gp_kstar(const double* __restrict__
   // per plane in the blocked layout, stored straight from registers (round 3
   // transposed the tile through LDS with 128 ds_write_b16 per lane per item)
   constexpr bool H3 = sizeof(TS) == 2;
+  // TS = int8_t (precision 8): y = k* * kscale (<= 0.49) as six balanced digit
+  // planes of the int8 variance contraction (gp_i8.hip), four consecutive
+  // training rows of a candidate per dword: the row permutation of h3
+  constexpr bool I8 = sizeof(TS) == 1;
+  constexpr bool PERM = H3 || I8;
   // one __shared__ object (see k_gp_var): the 2-stage ring, the exp table,
   // then the ticket slot
   constexpr int RED_OFF = 0;
@@ -194,7 +199,7 @@ __global__ __launch_bounds__(K_NT, 2) void k_gp_kstar(const double* __restrict__
   // h3: the table carries the split's power-of-two scale, so ks below is
   // k* * kscale exactly (and the mean's alpha is divided by it: the product is
   // unchanged bit for bit)
-  if (t < EXP_TAB) etab[t] = (sf2 * exp2((double)t / EXP_TAB)) * (H3 ? kscale : 1.0);  // published by the first ticket barrier
+  if (t < EXP_TAB) etab[t] = (sf2 * exp2((double)t / EXP_TAB)) * (PERM ? kscale : 1.0);  // published by the first ticket barrier
   const double ikscale = 1.0 / kscale;   // a power of two
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
   const int wm = w >> 1, wn = w & 1;
@@ -207,8 +212,8 @@ __global__ __launch_bounds__(K_NT, 2) void k_gp_kstar(const double* __restrict__
   const int npad_a = RT * K_BM;
   // the i8 MFMA's row rho of A is tile row sigma(rho) (see above); h3: the
   // f64 MFMA's row rho is tile row pi(rho), and the i8 one's row rho itself
-  const int sig = H3 ? (lane & 15) : ((lane & 15) >> 2) + 4 * (lane & 3);
-  const int arow = H3 ? 4 * (lane & 3) + ((lane & 15) >> 2) : (lane & 15);
+  const int sig = PERM ? (lane & 15) : ((lane & 15) >> 2) + 4 * (lane & 3);
+  const int arow = PERM ? 4 * (lane & 3) + ((lane & 15) >> 2) : (lane & 15);
   typedef kd4 d4;
 
   // the next item's ticket is taken at the start of the current one, so its
@@ -333,7 +338,7 @@ __global__ __launch_bounds__(K_NT, 2) void k_gp_kstar(const double* __restrict__
       const double hv = (-0.5 * KSTAR_T_SCALE) * rowop[2 * K_BM + cl];
       hc[jj] = col0 + cl < m ? hv : -1e300;
     }
-    const bool want2 = !H3 && MU && part2 != nullptr;
+    const bool want2 = !PERM && MU && part2 != nullptr;
     double s[4] = {0.0, 0.0, 0.0, 0.0}, s2[4] = {0.0, 0.0, 0.0, 0.0};
     if constexpr (H3) {
 #pragma unroll
@@ -364,6 +369,33 @@ __global__ __launch_bounds__(K_NT, 2) void k_gp_kstar(const double* __restrict__
           const int64_t o = h3_blk_off(col, row0 + rl0, RT * K_BM);
           *reinterpret_cast<uint2*>(kst + o) = make_uint2(hpk[0], hpk[1]);
           *reinterpret_cast<uint2*>(kst + lo_off + o) = make_uint2(lpk[0], lpk[1]);
+        }
+      }
+    } else if constexpr (I8) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int rl0 = wm * 64 + i * 16 + 4 * (lane >> 4);   // this lane's training rows rl0 .. rl0 + 3
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          const int64_t col = col0 + wn * 64 + jj * 16 + (lane & 15);
+          uint32_t lo[4], hi[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const double hv = (-0.5 * KSTAR_T_SCALE) * rowop[rl0 + r];
+            const double hx = row0 + rl0 + r < n ? hv : -1e300;
+            const double x = __builtin_fmax(__builtin_fmin((acc[i][jj][r] + hx) + hc[jj], 0.0), KSTAR_T_MIN);
+            const double ks = sf2_exp2t_nonpos(x, etab);   // y = k* 2^-eb
+            s[jj] += (rowop[K_BM + rl0 + r] * ikscale) * ks;
+            const uint64_t b = i8_biased(ks);
+            lo[r] = (uint32_t)b;
+            hi[r] = (uint32_t)(b >> 32);
+          }
+          uint32_t pl[I8_S];
+          i8_planes(lo, hi, pl);
+          // lo_off: bytes per plane
+          int8_t* dst = reinterpret_cast<int8_t*>(kst) + i8_off(col, row0 + rl0, ldk);
+#pragma unroll
+          for (int p = 0; p < I8_S; ++p) *reinterpret_cast<uint32_t*>(dst + p * lo_off) = pl[p];
         }
       }
     } else {
@@ -435,7 +467,7 @@ int launch_gemm_kstar(ut_ctx* c, int prec, const double* XsT, int32_t npad, cons
   UT_CHECK(c, npad % K_BM == 0 && dpad % 4 == 0 && (dpad >= 4 || has_cat) && ldk % K_BN == 0 && ldk >= m, UT_EINVAL,
            "gemm_kstar: bad padding");
   UT_CHECK(c, !has_cat || (cat.acat && cat.bcat), UT_EINVAL, "gemm_kstar: categorical operands missing");
-  UT_CHECK(c, prec == 64 || prec == 32 || prec == 16, UT_EINVAL, "gemm_kstar: bad precision");
+  UT_CHECK(c, prec == 64 || prec == 32 || prec == 16 || prec == 8, UT_EINVAL, "gemm_kstar: bad precision");
   UT_CHECK(c, part != nullptr || prec == 64, UT_EINVAL,
            "gemm_kstar: fp32 / h3 mode takes the mean partial here");
   const int32_t RT = npad / K_BM;
@@ -468,6 +500,9 @@ int launch_gemm_kstar(ut_ctx* c, int prec, const double* XsT, int32_t npad, cons
   } while (0)
   if (prec == 16)
     UT_KSTAR_BOTH(_Float16, true, (_Float16*)kst, part, ldexp(1.0, h3_kstar_exp(c->gp_sf2)), ldk * (int64_t)npad, RT,
+                  nullptr);
+  else if (prec == 8)   // six digit planes of npad * ldk bytes (kst: [6][npad / 32][ldk][32])
+    UT_KSTAR_BOTH(int8_t, true, (int8_t*)kst, part, ldexp(1.0, -i8_kstar_exp(c->gp_sf2)), ldk * (int64_t)npad, RT,
                   nullptr);
   else if (prec == 32)
     UT_KSTAR_BOTH(float, true, (float*)kst, part, 1.0, (int64_t)0, RT, nullptr);

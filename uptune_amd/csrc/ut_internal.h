@@ -316,6 +316,13 @@ struct ut_ctx {
   bool ucand_cat = false;          // ucand / cnorm / bcat hold the categorical K*'s operands (encode path)
   ut::DevBuf<int8_t> pr_bcat;      // pruned scoring: the gathered candidates' codes
   float* gp_LinvT_f = nullptr;  // fp32 (L^-1)^T; in h3 mode the fp16 hi/lo planes of L^-1 [row][k]
+  // int8-sliced fp64 tier (precision 8, gp_i8.hip): L^-1 as I8_S digit planes,
+  // per-row scales 2^(ea_i + eb) [npad] | e_i^2 [npad] | the bound E [1]
+  ut::DevBuf<int8_t> gp_i8a;
+  ut::DevBuf<double> gp_i8rs;
+  int32_t gp_i8_eb = 0;          // K* digit scale: y = k* 2^-eb <= 0.49
+  double i8_tol = 0x1p-20;       // accepted relative variance error (ut_gp_set_i8_tol)
+  int64_t i8_recomputed = 0;     // candidates of the last score recomputed in fp64 (-1: all, dense)
   int32_t* gp_ctr = nullptr;   // [32] per-XCD work tickets: [0,8) variance, [8,16) K*; [16,18) max|L^-1| bits (h3)
   int32_t n_cu = 256;
   int64_t gp_cap_n = 0;
@@ -519,7 +526,9 @@ int gp_topk_pruned_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, co
                         int64_t cand_base, int32_t k, int32_t bound_rows, int64_t* out_idx, double* out_score,
                         ut_prune_stats* stats, hipEvent_t dup_ready = nullptr, bool feat_ours = false);
 // prec: 64 (fp64 MFMA), 32 (fp32 MFMA), 16 (f16x3: fp16 hi/lo split operands,
-// three fp16 MFMA products, f32 accumulate -- see gp_gemm.hip)
+// three fp16 MFMA products, f32 accumulate -- see gp_gemm.hip), 8 (the fp64
+// tier on the int8 MFMA: six-digit planes, a per-candidate error bound and an
+// fp64 recompute of the candidates it does not clear -- gp_i8.hip)
 constexpr int H3_KSCALE_EXP = 14;  // K* (<= sf2) is scaled by 2^(14 - ceil(log2 sf2)) before the split
 int h3_kstar_exp(double sf2);
 // K*'s training operand (Xs^T, the numeric part in categorical mode) is stored
@@ -582,6 +591,43 @@ int launch_xs_t(ut_ctx* c, const double* Xs, int32_t npad, int32_t d, int32_t dp
 int launch_gemm_var(ut_ctx* c, int prec, const void* LinvT, int64_t lda, const void* kst, int64_t ldk, int32_t npad,
                     int64_t m, double* part, const double* beta, double* mpart);
 int launch_transpose(ut_ctx* c, const double* src, int32_t n, double* dst, float* dst_f);
+// ---- int8-sliced fp64 tier (gp_i8.hip) ----
+// six balanced 8-bit digits per operand value; tiles of the variance contraction
+constexpr int I8_S = 6, I8_BM = 64, I8_BN = 64, I8_BK = 32;
+constexpr int32_t I8_MAX_K = 16384;   // exact int32 group sums: K * 6 * 2^14 < 2^31
+// the digit scale of K*: the smallest eb with sf2 2^-eb <= 0.49 (k* <= sf2)
+inline int i8_kstar_exp(double sf2) { return ilogb(sf2 / 0.49) + 1; }
+// byte offset of element (r, k) in a digit plane [K / 32][ld][32]: a 32-k piece
+// of row r is 32 contiguous bytes, its 16-byte chunks swizzled by bit 3 of r
+__host__ __device__ inline int64_t i8_off(int64_t r, int32_t k, int64_t ld) {
+  return ((int64_t)(k >> 5) * ld + r) * 32 + ((((k >> 4) & 1) ^ (int)((r >> 3) & 1)) << 4) + (k & 15);
+}
+// x in [-0.49, 0.49] -> rint(x 2^48) + 0x808080808080: the fp64 sum x + 24 has
+// ulp 2^-48 and a fixed exponent, so its bits minus a constant are that
+// integer; its six bytes, each XOR 0x80, are the balanced digits (int8) of
+// rint(x 2^48) in base 256, most significant = byte 5
+__device__ __forceinline__ uint64_t i8_biased(double x) {
+  return (uint64_t)__double_as_longlong(x + 24.0) - 0x40377F7F7F7F7F80ull;
+}
+// four values' biased words (lo / hi dwords) -> the six digit planes' dwords
+// (byte u of plane p's dword = digit p of value u; plane 0 = most significant)
+__device__ __forceinline__ uint32_t i8_gather(const uint32_t (&w)[4], int b) {
+  return ((w[0] >> (8 * b)) & 0xFFu) | (((w[1] >> (8 * b)) & 0xFFu) << 8) | (((w[2] >> (8 * b)) & 0xFFu) << 16) |
+         (((w[3] >> (8 * b)) & 0xFFu) << 24);
+}
+__device__ __forceinline__ void i8_planes(const uint32_t (&lo)[4], const uint32_t (&hi)[4], uint32_t (&pl)[I8_S]) {
+  pl[0] = i8_gather(hi, 1) ^ 0x80808080u;
+  pl[1] = i8_gather(hi, 0) ^ 0x80808080u;
+  pl[2] = i8_gather(lo, 3) ^ 0x80808080u;
+  pl[3] = i8_gather(lo, 2) ^ 0x80808080u;
+  pl[4] = i8_gather(lo, 1) ^ 0x80808080u;
+  pl[5] = i8_gather(lo, 0) ^ 0x80808080u;
+}
+// fit: L^-1's planes, row scales and the error bound (c->gp_i8a, c->gp_i8rs)
+int launch_split_i8(ut_ctx* c, int32_t n, int32_t npad);
+// the variance contraction from K*'s digit planes (kst8, [6][npad/32][ldk][32]):
+// part [npad / 64][ldk] column partials of |v|^2
+int launch_gemm_var_i8(ut_ctx* c, int32_t npad, const int8_t* kst8, int64_t ldk, int64_t m, double* part);
 // L^-1 [row][k] (n x n, fp64) -> scaled fp16 hi/lo planes, blocked (h3 A operand, rows padded to 256);
 // the scale exponent is derived on the device from max|L^-1| (kept in gp_ctr[16..17])
 int launch_split_h3(ut_ctx* c, const double* Linv, int32_t n, _Float16* dst);

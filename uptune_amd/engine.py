@@ -278,11 +278,24 @@ class BatchEngine:
 
     # -- GP ----------------------------------------------------------------
     def gp_set_precision(self, bits):
-        """64 (fp64 MFMA, 1e-5 tier), 32 (fp32 MFMA, 1e-3 tier) or 16 / "f16x3"
+        """64 (fp64 MFMA, 1e-5 tier), 32 (fp32 MFMA, 1e-3 tier), 16 / "f16x3"
         (variance contraction as three fp16 MFMA products of hi/lo splits, f32
-        accumulate: the 1e-3 tier at the fp16 MFMA rate); applies to later fits"""
-        bits = 16 if bits == "f16x3" else bits
+        accumulate: the 1e-3 tier at the fp16 MFMA rate) or 8 / "i8" (the fp64
+        tier on the int8 MFMA: six-digit slices, a per-candidate error bound,
+        fp64 recompute of the candidates it does not clear); applies to later fits"""
+        bits = {"f16x3": 16, "i8": 8}.get(bits, bits)
         L.check(self.ctx, self.lib.ut_gp_set_precision(self.ctx, int(bits)), "ut_gp_set_precision")
+
+    def gp_set_i8_tol(self, tol: float):
+        """precision 8: largest accepted relative variance error (0: recompute all in fp64)"""
+        L.check(self.ctx, self.lib.ut_gp_set_i8_tol(self.ctx, float(tol)), "ut_gp_set_i8_tol")
+
+    def gp_i8_stats(self) -> Tuple[int, float]:
+        """precision 8: (candidates of the last score recomputed in fp64, -1 = all;
+        the fit's error bound E on |L^-1 k* - v^|)"""
+        n, e = C.c_int64(), C.c_double()
+        L.check(self.ctx, self.lib.ut_gp_i8_stats(self.ctx, C.byref(n), C.byref(e)), "ut_gp_i8_stats")
+        return int(n.value), float(e.value)
 
     def gp_fit(self, X: np.ndarray, y: np.ndarray, lengthscale, sigma_f2: float = 1.0, sigma_n2: float = 1e-6,
                jitter: float = 0.0, wait: bool = True):
