@@ -629,9 +629,7 @@ def main():
     flops_var = float(m) * n * (n + 1)       # algorithmic: lower-triangular n x n times k* per candidate
     kernel = ("k_gp_var_pp (persistent var contraction L^-1 K*^T, two 4-wave workgroups per CU, "
               "v_mfma_f64_16x16x4_f64)" if args.precision == 64 else
-              "k_gp_var<float> (persistent var contraction L^-1 K*^T, v_mfma_f32_32x32x2_f32)")
-    if args.precision == 64 and os.environ.get("UT_VAR_KERNEL") == "1":
-        kernel = "k_gp_var<double> (persistent var contraction L^-1 K*^T, one 8-wave workgroup per CU)"
+              "k_gp_var_f32 (persistent var contraction L^-1 K*^T, v_mfma_f32_32x32x2_f32)")
     if args.precision == 16:
         kernel = ("k_gp_var_h3 (persistent var contraction L^-1 K*^T, 3 x v_mfma_f32_32x32x16_f16 per product "
                   "on hi/lo fp16 splits; peak = fp16 dense peak / 3)")

@@ -273,7 +273,14 @@ int ut_gp_score(ut_ctx* ctx, const double* features, int64_t ld, int64_t m, cons
 /* ut_gp_score on raw values [ncols][ld] instead of features: the encoding
  * (ut_encode_features), the 1/lengthscale scaling and |u|^2 run as one pass
  * that writes only what the K* GEMM reads, so no [d][m] feature matrix is
- * written and read back.  Same results as ut_gp_score(ut_encode_features(values)). */
+ * written and read back.  Same results as ut_gp_score(ut_encode_features(values))
+ * for values in their parameters' domains: ENUM values are option indices in
+ * [0, n_options) and BOOL values 0 or 1, as every proposal kernel writes them
+ * (the reference has no other values: an out-of-range index raises in
+ * EnumParameter, manipulator.py).  In categorical mode (ut_gp_kstar_mode) an
+ * out-of-range ENUM value matches no option (2 / ell^2 against every training
+ * row, where the dense encoding's all-zero block gives 1 / ell^2) and a BOOL
+ * value other than 0 counts as 1. */
 int ut_gp_score_values(ut_ctx* ctx, const double* values, int64_t ld, int64_t m, const ut_acq* acq,
                        const uint8_t* dup, double* mu, double* var, double* score);
 /* Selection-exact pruned scoring + top-k (fp64 fits only; EI, or UCB with

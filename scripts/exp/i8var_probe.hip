@@ -540,6 +540,140 @@ __global__ __launch_bounds__(256, 2) void k_var_i8d(const int8_t* __restrict__ A
   }
 }
 
+// v6: v1 with 64-row x 128-candidate tiles: each wave owns 32 rows x 64
+// candidates (two 32x32 MFMA column tiles share its A fragments), B planes
+// streamed one at a time (8 registers), S = 6: 2 x 6 x 16 accumulators.
+template <int S, int MODE, int NST, bool REV = false>
+__global__ __launch_bounds__(256, 2) void k_var_i8w(const int8_t* __restrict__ Ad, const int8_t* __restrict__ Bd,
+                                                    int32_t npad, int64_t ldk, int32_t RT, int32_t CT, int64_t m,
+                                                    int32_t* __restrict__ ticket, const double* __restrict__ rscale,
+                                                    double* __restrict__ part, int32_t Sg) {
+  constexpr int WN = 128;                       // candidates per tile
+  constexpr int APL = IM * IK, BPL = WN * IK;   // 2 KiB, 4 KiB per plane per stage
+  constexpr int STAGE = S * (APL + BPL);
+  constexpr int NI = 6 * S, NW = NI / 4;        // 1-KiB glds per stage, per wave
+  static_assert(NI % 4 == 0, "uniform glds per wave");
+  __shared__ __attribute__((aligned(16))) int8_t lds[NST * STAGE + 2 * WN * 8 + IM * 8 + 16];
+  double* red = reinterpret_cast<double*>(lds + NST * STAGE);   // [2][128]
+  double* srs = red + 2 * WN;
+  int32_t& s_item = *reinterpret_cast<int32_t*>(srs + IM);
+  const int t = threadIdx.x, lane = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wm = w >> 1, wn = w & 1;
+  const int32_t xcd = blockIdx.x & 7;
+  const int64_t KB = npad / IK;
+  const int64_t aplane = KB * npad * 32, bplane = KB * ldk * 32;
+
+  auto issue = [&](int32_t row0, int64_t col0, int32_t kt, int8_t* st) {
+#pragma unroll
+    for (int j = 0; j < NW; ++j) {
+      const int u = w + 4 * j;
+      const int8_t* src;
+      int8_t* dst;
+      if (u < 2 * S) {
+        const int pl = u >> 1, h = u & 1;
+        src = Ad + pl * aplane + ((int64_t)kt * npad + row0) * 32 + h * 1024;
+        dst = st + pl * APL + h * 1024;
+      } else {
+        const int v = u - 2 * S, pl = v >> 2, h = v & 3;
+        src = Bd + pl * bplane + ((int64_t)kt * ldk + col0) * 32 + h * 1024;
+        dst = st + S * APL + pl * BPL + h * 1024;
+      }
+      __builtin_amdgcn_global_load_lds(src + lane * 16, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+    }
+  };
+
+  const int32_t P = (RT + 1) / 2;
+  for (;;) {
+    if (t == 0) s_item = atomicAdd(&ticket[xcd], 1);
+    __syncthreads();
+    const int32_t j = s_item;
+    const int32_t G = j / (P * Sg), q = j % (P * Sg), p = q % P;
+    const int32_t ct = (G * Sg + q / P) * 8 + xcd;
+    if (ct >= CT) break;
+    int32_t rts[2] = {RT - 1 - p, p};
+    const int nrt = rts[1] == rts[0] ? 1 : 2;
+    for (int ri = 0; ri < nrt; ++ri) {
+      if (ri > 0) __syncthreads();
+      const int32_t rt = rts[ri];
+      const int32_t row0 = rt * IM;
+      const int64_t col0 = (int64_t)ct * WN;
+      const int32_t arow = MODE == 2 ? 0 : row0;
+      const int64_t bcol = MODE == 2 ? (int64_t)xcd * WN : col0;
+      const int32_t nk = (row0 + IM) / IK;
+      v16i acc[2][S];
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+        for (int g = 0; g < S; ++g)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc[jj][g][r] = 0;
+      if (w == 0 && lane < 32)
+        __builtin_amdgcn_global_load_lds(rscale + row0 + lane * 2, (__attribute__((address_space(3))) void*)srs, 16, 0,
+                                         0);
+      // REV: the pair's second (short) tile walks its k stages in descending order,
+      // so at every step the strip's pairs read at most two distinct K* stages
+      const bool rev = REV && ri > 0;
+      auto ktof = [&](int32_t u) -> int32_t { return rev ? nk - 1 - u : u; };
+      if (MODE != 1) issue(arow, bcol, ktof(0), lds);
+      if (MODE != 1 && NST == 3 && nk > 1) issue(arow, bcol, ktof(1), lds + STAGE);
+      const int c = lane >> 5;
+      const int ra = wm * 32 + (lane & 31);
+      const int aoff = ra * 32 + ((c ^ ((ra >> 3) & 1)) << 4);
+      int boff[2];
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) {
+        const int cb = wn * 64 + jj * 32 + (lane & 31);
+        boff[jj] = S * APL + cb * 32 + ((c ^ ((cb >> 3) & 1)) << 4);
+      }
+      for (int32_t u = 0; u < nk; ++u) {
+        if (NST == 3 && MODE != 1 && u + 1 < nk) vm_wait<NW>();
+        else vm_wait<0>();
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (MODE != 1 && u + NST - 1 < nk) issue(arow, bcol, ktof(u + NST - 1), lds + ((u + NST - 1) % NST) * STAGE);
+        const int32_t kt = ktof(u);
+        if (kt * IK >= row0 + 32 * wm + 32) continue;
+        const int8_t* st = lds + (u % NST) * STAGE;
+        v4i af[S];
+#pragma unroll
+        for (int pp = 0; pp < S; ++pp) af[pp] = *reinterpret_cast<const v4i*>(st + pp * APL + aoff);
+#pragma unroll
+        for (int qb = 0; qb < S; ++qb) {
+          v4i bf[2];
+#pragma unroll
+          for (int jj = 0; jj < 2; ++jj) bf[jj] = *reinterpret_cast<const v4i*>(st + qb * BPL + boff[jj]);
+#pragma unroll
+          for (int pa = 0; pa + qb < S; ++pa)
+#pragma unroll
+            for (int jj = 0; jj < 2; ++jj)
+              acc[jj][pa + qb] = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[pa], bf[jj], acc[jj][pa + qb], 0, 0, 0);
+        }
+      }
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) {
+        double s = 0.0;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          double v = (double)acc[jj][S - 1][r];
+#pragma unroll
+          for (int g = S - 2; g >= 0; --g) v = __builtin_fma(v, 0x1p-7, (double)acc[jj][g][r]);
+          const int rl = wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+          v *= srs[rl];
+          s = __builtin_fma(v, v, s);
+        }
+        s += __shfl_xor(s, 32);
+        if (lane < 32) red[wm * WN + wn * 64 + jj * 32 + lane] = s;
+      }
+      __syncthreads();
+      if (t < WN) {
+        const int64_t col = col0 + t;
+        if (col < m) part[(int64_t)rt * ldk + col] = red[t] + red[WN + t];
+      }
+    }
+  }
+}
+
 // random digits: A lower triangular (zero for k > row), signed in [-127, 127];
 // B in [0, 127]
 __device__ inline uint32_t mix(uint64_t x) {
@@ -577,7 +711,7 @@ double run(int32_t n, int64_t m, bool check, int reps) {
   const int TM = KIND == 1 ? JM : IM;
   const int32_t npad = (n + 127) / 128 * 128;
   const int64_t ldk = (m + 255) / 256 * 256;
-  const int32_t RT = npad / TM, CT = (int32_t)(ldk / IN);
+  const int32_t RT = npad / TM, CT = (int32_t)(ldk / (KIND >= 5 ? 128 : IN));
   int8_t *A, *B;
   double *part, *rs;
   int32_t* ticket;
@@ -611,6 +745,12 @@ double run(int32_t n, int64_t m, bool check, int reps) {
       hipLaunchKernelGGL((k_var_i8c<S, MODE>), dim3(nb), dim3(256), 0, 0, A, B, npad, ldk, RT, CT, m, ticket, rs, part, Sg);
     else if (KIND == 1)
       hipLaunchKernelGGL((k_var_i8b<S, MODE>), dim3(nb), dim3(512), 0, 0, A, B, npad, ldk, RT, CT, m, ticket, rs, part, Sg);
+    else if (KIND == 5)
+      hipLaunchKernelGGL((k_var_i8w<S, MODE, 2>), dim3(nb), dim3(256), 0, 0, A, B, npad, ldk, RT, CT, m, ticket, rs, part, Sg);
+    else if (KIND == 7)
+      hipLaunchKernelGGL((k_var_i8w<S, MODE, 2, true>), dim3(nb), dim3(256), 0, 0, A, B, npad, ldk, RT, CT, m, ticket, rs, part, Sg);
+    else if (KIND == 6)
+      hipLaunchKernelGGL((k_var_i8w<S, MODE, 3>), dim3(nb), dim3(256), 0, 0, A, B, npad, ldk, RT, CT, m, ticket, rs, part, Sg);
     else if (KIND == 4)
       hipLaunchKernelGGL((k_var_i8<S, MODE, 3>), dim3(nb), dim3(256), 0, 0, A, B, npad, ldk, RT, CT, m, ticket, rs, part, Sg);
     else
@@ -686,7 +826,9 @@ int main(int argc, char** argv) {
     printf("i8 32x32x32 map: %d / 1024 wrong\n", bad);
     if (bad) return 1;
   }
-  run<6, 0, 4>(300, 333, true, 1);
+  run<6, 0, 5>(300, 333, true, 1);
+  run<6, 0, 7>(300, 333, true, 1);
+
   const int32_t n = argc > 1 ? atoi(argv[1]) : 1024;
   const int64_t m = argc > 2 ? atoll(argv[2]) : (1 << 20);
   const double alg = (double)m * n * (n + 1);   // fp64-equivalent flops of the triangular contraction
@@ -694,11 +836,11 @@ int main(int argc, char** argv) {
     printf("%-28s S=%d  %8.3f ms  %6.1f TF(fp64-equiv)  %7.1f TOPS(i8)\n", name, S, ms, alg / ms * 1e-9,
            alg * S * (S + 1) / 2 / ms * 1e-9);
   };
-  rep("v1 2st full", 6, run<6, 0>(n, m, false, 5));
   rep("v1 3st full", 6, run<6, 0, 4>(n, m, false, 5));
-  rep("v1 3st L2-hit", 6, run<6, 2, 4>(n, m, false, 5));
-  rep("v1 3st no loads", 6, run<6, 1, 4>(n, m, false, 5));
-  rep("v1 2st L2-hit", 6, run<6, 2>(n, m, false, 5));
-  rep("v1 2st no loads", 6, run<6, 1>(n, m, false, 5));
+  rep("v6 64x128 2st full", 6, run<6, 0, 5>(n, m, false, 5));
+  rep("v6 64x128 2st L2-hit", 6, run<6, 2, 5>(n, m, false, 5));
+  rep("v6 64x128 2st no loads", 6, run<6, 1, 5>(n, m, false, 5));
+  rep("v7 = v6 + rev short tile", 6, run<6, 0, 7>(n, m, false, 5));
+  rep("v7 L2-hit", 6, run<6, 2, 7>(n, m, false, 5));
   return 0;
 }

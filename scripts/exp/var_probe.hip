@@ -1,4 +1,6 @@
-// Experiment: where k_gp_var<double> loses MFMA time on MI355X.  A copy of the
+// Experiment: where k_gp_var<double> loses MFMA time on MI355X.  (Round 2/3
+// measurement aid: it includes gp_gemm.hip as of round 4 -- `git show
+// b6f4ed2:uptune_amd/csrc/gp_gemm.hip` -- whose fp64 k_gp_var<T> round 5 removed.)  A copy of the
 // library kernel's structure (persistent, per-XCD tickets, 128 x 256 tiles,
 // 3-stage global_load_lds ring, triangular skip) with knobs:
 //   MODE 0  as the library

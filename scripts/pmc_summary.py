@@ -19,7 +19,7 @@ from collections import defaultdict
 STAGES = {  # stage key -> kernel-name prefixes (the first match wins)
     "var": ("void ut::k_gp_var_pp<false>(", "ut::k_gp_var_pp(", "void ut::k_gp_var<double>"), "var_1wg": ("void ut::k_gp_var<double>",),
     "kstar": ("void ut::k_gp_kstar<double, false, false>", "void ut::k_gp_kstar<double, false>"),
-    "var32": ("void ut::k_gp_var<float>",), "kstar32": ("void ut::k_gp_kstar<float, true, false>", "void ut::k_gp_kstar<float, true>"),
+    "var32": ("ut::k_gp_var_f32(", "void ut::k_gp_var<float>",), "kstar32": ("void ut::k_gp_kstar<float, true, false>", "void ut::k_gp_kstar<float, true>"),
     "hash": ("void ut::k_hash<true", "void ut::k_hash<", "ut::k_hash("),
     "propose": ("void ut::k_de<", "ut::k_de("), "encode": ("ut::k_encode_scaled", "ut::k_encode("), "prep_cand": ("ut::k_gp_prep_cand",),
     "finalize": ("ut::k_gp_finalize",),
@@ -28,6 +28,9 @@ STAGES = {  # stage key -> kernel-name prefixes (the first match wins)
     "ga": ("ut::k_ga(",),
     # rocprofv3 leaves the _Float16 instantiations mangled
     "var16": ("_ZN2ut11k_gp_var_h3",), "kstar16": ("_ZN2ut10k_gp_kstarIDF16_",),
+    # precision 8 (int8 slices)
+    "var8": ("ut::k_gp_var_i8(",), "kstar8": ("void ut::k_gp_kstar<signed char, true, false>",),
+    "split8": ("ut::k_split_i8(",), "finalize8": ("ut::k_gp_finalize_i8(",),
     "inner_pairs": ("ut::k_inner_pairs",), "de_diff": ("ut::k_de_diff",), "pop_digests": ("ut::k_pop_digests",),
 }
 # stages of the default C2 round that a refreshed C2 profile replaces (a key

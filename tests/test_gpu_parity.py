@@ -1328,6 +1328,29 @@ def test_categorical_kstar_equals_dense(which, prec):
             assert err(got, want) <= max(1.0, 1.25 * err(dense, want)), (err(got, want), err(dense, want))
 
 
+def test_categorical_kstar_too_many_options_is_dense():
+    """the candidates' code rows of an ENUM with thousands of options
+    need more LDS than one workgroup holds (code_rows_lds(cat_k) > the device's
+    hipDeviceAttributeMaxSharedMemoryPerBlock); the fit then scores with the
+    dense contraction instead of failing at launch, and the posterior is the
+    oracle's"""
+    _require_gpu()
+    space = [Param("big", ENUM, options=list(range(5000))), Param("x", FLOAT, 0.0, 1.0), Param("b", BOOL)]
+    e = engine(space, seed=5)
+    tr = ode.population_init(space, 300, seed=5)
+    X = features(space, tr).T
+    y = np.sum((X - 0.3) ** 2, axis=1)
+    e.gp_fit(X, y, lengthscale=1.0, sigma_f2=1.0, sigma_n2=1e-6, jitter=1e-8)
+    assert e.gp_kstar_mode() == "dense"
+    cand = ode.population_init(space, 1500, seed=6)
+    cand[:, :5] = tr[:, :5]
+    mu, var, _ = [t.cpu().numpy() for t in e.gp_score_values(dev(cand), acq=e.acq("ei"))]
+    g = ogp.GP(X, y, lengthscale=1.0, sigma_f2=1.0, sigma_n2=1e-6, jitter=1e-8)
+    wmu, wvar = g.posterior(features(space, cand).T)
+    np.testing.assert_allclose(mu, wmu, rtol=RTOL, atol=ATOL)
+    np.testing.assert_allclose(var, wvar, rtol=RTOL, atol=1e-8)
+
+
 def test_categorical_kstar_fallbacks():
     """the dense contraction when the categorical form does not apply: a
     training row whose ENUM block is not one-hot, per-feature lengthscales

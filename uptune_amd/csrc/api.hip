@@ -203,14 +203,6 @@ int ut_device_bytes(int32_t device, int64_t* bytes) {
   return 0;
 }
 
-// the fit stream: non-blocking, at the highest priority when c->fit_priority
-static hipError_t hip_create_fit_stream(ut_ctx* c) {
-  if (!c->fit_priority) return hipStreamCreateWithFlags(&c->fit_stream, hipStreamNonBlocking);
-  int lo = 0, hi = 0;
-  hipError_t e = hipDeviceGetStreamPriorityRange(&lo, &hi);
-  if (e != hipSuccess) return e;
-  return hipStreamCreateWithPriority(&c->fit_stream, hipStreamNonBlocking, hi);
-}
 
 int ut_ctx_create(int device, uint64_t seed, ut_ctx** out) {
   if (!out) return UT_EINVAL;
@@ -220,14 +212,16 @@ int ut_ctx_create(int device, uint64_t seed, ut_ctx** out) {
   if (hipSetDevice(device) != hipSuccess) return UT_EHIP;
   ut_ctx* c = new ut_ctx();
   c->device = device;
-  if (const char* e = getenv("UT_FIT_PRIORITY")) c->fit_priority = atoi(e) != 0;
   c->seed = seed;
   int ncu = 0;
   if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && ncu >= 8)
     c->n_cu = ncu;
+  int lds = 0;
+  if (hipDeviceGetAttribute(&lds, hipDeviceAttributeMaxSharedMemoryPerBlock, device) == hipSuccess && lds > 0)
+    c->max_lds = (size_t)lds;
   if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess ||
-      hip_create_fit_stream(c) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->fit_stream, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_fit, hipEventDisableTiming) != hipSuccess ||
@@ -237,27 +231,25 @@ int ut_ctx_create(int device, uint64_t seed, ut_ctx** out) {
     return UT_EHIP;
   }
   c->stream = c->own_stream;
+  // ut_comm_bcast_results' count / agreement words: allocated with the
+  // context, so no allocation can fail between a rank's entry into
+  // ut_comm_init and its first collective
+  if (ut::ensure(c, c->cm_cnt, 2)) {
+    ut_ctx_destroy(c);
+    return UT_ENOMEM;
+  }
   if (const char* e = getenv("UT_CHOL_FUSE")) c->chol_fuse = atoi(e);
   if (const char* e = getenv("UT_TRINV_BIG")) c->trinv_big = atoi(e);
   if (const char* e = getenv("UT_CHOL_MERGED")) c->chol_merged = atoi(e);
-  if (const char* e = getenv("UT_FIT_SETPRIO")) c->fit_setprio = atoi(e);
-  if (ut::set_fit_prio(c->fit_setprio)) {
+  // the fit kernels' waves at s_setprio 3 (gp.hip g_fit_prio): beside the
+  // round's hash grid their instructions go first
+  if (ut::set_fit_prio(1)) {
     ut_ctx_destroy(c);
     return UT_EHIP;
   }
-  if (const char* e = getenv("UT_JOIN_BEFORE_VAR")) c->join_before_var = atoi(e) != 0;
-  if (const char* e = getenv("UT_VAR_KERNEL")) c->var_kernel = atoi(e);
   if (const char* e = getenv("UT_VAR_SPLIT")) c->var_split = atoi(e) != 0;
-  if (const char* e = getenv("UT_FIT_APPEND")) c->fit_append = atoi(e) != 0;
   if (const char* e = getenv("UT_DE_AOS")) c->de_aos = atoi(e) != 0;
-  if (const char* e = getenv("UT_HASH_AFTER_FIT")) c->hash_after_fit = atoi(e);
-  if (const char* e = getenv("UT_HASH_HOLD_LOWPREC")) c->hash_hold_lowprec = atoi(e) != 0;
-  if (const char* e = getenv("UT_HASH_HOLD_PRUNED")) c->hash_hold_pruned = atoi(e);
   if (const char* e = getenv("UT_HASH_WG_PER_CU")) c->hash_wg_per_cu = atoi(e);
-  if (const char* e = getenv("UT_HASH_AFTER_KSTAR")) c->hash_after_kstar = atoi(e);
-  if (const char* e = getenv("UT_H3_REV")) c->h3_rev = atoi(e);
-  if (const char* e = getenv("UT_H3_SCHED")) c->h3_sched = atoi(e);
-  if (const char* e = getenv("UT_VAR_SCHED")) c->var_sched = atoi(e);
   if (const char* e = getenv("UT_CAT_KSTAR")) c->cat_enable = atoi(e) != 0;
   *out = c;
   return 0;
@@ -287,6 +279,7 @@ int ut_ctx_destroy(ut_ctx* c) {
   fr(c->gp_alpha); fr(c->gp_beta); fr(c->gp_inv_ell); fr(c->gp_stats); fr(c->gp_flag); fr(c->gp_Xs_f); fr(c->gp_T);
   fr(c->gp_LinvT); fr(c->gp_LinvT_f); fr(c->gp_ctr); fr(c->gp_XsT); fr(c->ucand.p);
   fr(c->gp_XsT_num.p); fr(c->gp_xnorm_num.p); fr(c->gp_acat.p); fr(c->bcat.p); fr(c->pr_bcat.p);
+  fr(c->gp_i8a.p); fr(c->gp_i8rs.p);
   fr(c->kst.p); fr(c->mu_part.p); fr(c->var_part.p); fr(c->cnorm.p);
   fr(c->r_values.p); fr(c->r_feat.p); fr(c->r_mu.p); fr(c->r_var.p); fr(c->r_score.p); fr(c->r_digest.p);
   fr(c->r_dup.p); fr(c->tk_score[0].p); fr(c->tk_score[1].p); fr(c->tk_idx[0].p); fr(c->tk_idx[1].p);
@@ -912,17 +905,21 @@ static int score_round_de_impl(ut_ctx* c, const ut_de_params* de, const ut_acq* 
   if ((rc = check_de_params(c, de, m, cand_base))) return rc;
   if ((rc = launch_de(c, de, round_, cand_base, m, c->r_values.p, ld, true))) return rc;
   mark(c, "propose");
-  // fork: hash_config + dedup on the side stream, beside encode + GP scoring
-  // (low-precision dense rounds with hash_after_kstar: forked after K*)
+  // fork: hash_config + dedup on the side stream, beside encode + GP scoring.
+  // Dense fp64 rounds (the only ones whose K* does not wait for the whole
+  // fit) hold the hash for an in-flight fit: beside the full hash grid the
+  // fit's chain of small kernels stretches from ~1.5 to ~9 ms and the
+  // variance GEMM waits for it; held, the fit runs beside K* alone (C2:
+  // 26.10 ms per round, against 26.32 holding only the outer hash and 26.54
+  // holding nothing; round 3).
   auto fork_hash = [&]() -> int {
     UT_HIP(c, hipEventRecord(c->ev_fork, c->stream));
     UT_HIP(c, hipStreamWaitEvent(c->side, c->ev_fork, 0));
     StreamScope on_side(c, c->side);
     mark(c, "");
-    c->round_hash_hold = prune_rows > 0 ? c->hash_hold_pruned
-                         : ((c->gp_fit_prec == 64 || c->hash_hold_lowprec) ? c->hash_after_fit : 0);
+    c->round_hash_hold = prune_rows == 0 && c->gp_fit_prec == 64;
     int r = launch_hash_de(c, c->r_values.p, ld, m, cand_base, c->r_digest.p, true);
-    c->round_hash_hold = 0;
+    c->round_hash_hold = false;
     if (r) return r;
     mark(c, "hash");
     if ((r = launch_dedup(c, c->r_digest.p, m, c->r_dup.p))) return r;
@@ -930,9 +927,7 @@ static int score_round_de_impl(ut_ctx* c, const ut_de_params* de, const ut_acq* 
     UT_HIP(c, hipEventRecord(c->ev_join, c->side));
     return 0;
   };
-  const bool late_hash = prune_rows == 0 && c->gp_fit_prec != 64 &&
-                         (c->hash_after_kstar > 0 || (c->hash_after_kstar < 0 && c->gp_n >= 2048));
-  if (!late_hash && (rc = fork_hash())) return rc;
+  if ((rc = fork_hash())) return rc;
   // dense rounds encode straight into the K* operand (features * 1/ell and
   // their norms); the pruned round keeps the features, which it gathers for
   // its threshold set and survivors
@@ -951,13 +946,10 @@ static int score_round_de_impl(ut_ctx* c, const ut_de_params* de, const ut_acq* 
                                   c->r_topk_score.p, stats, c->ev_join, true)))
       return rc;
   } else {
-    // join before the finalize kernel, which masks duplicates
-    if (late_hash)
-      rc = gp_score_impl(c, nullptr, ld, m, acq, c->r_dup.p, c->r_mu.p, c->r_var.p, c->r_score.p, c->ev_join,
-                         fork_hash, false);
-    else
-      rc = gp_score_impl(c, nullptr, ld, m, acq, c->r_dup.p, c->r_mu.p, c->r_var.p, c->r_score.p, c->ev_join);
-    if (rc) return rc;
+    // the variance GEMM joins the side stream's hash + dedup (they share the
+    // CUs with K* only), the finalize kernel masks duplicates
+    if ((rc = gp_score_impl(c, nullptr, ld, m, acq, c->r_dup.p, c->r_mu.p, c->r_var.p, c->r_score.p, c->ev_join)))
+      return rc;
     if ((rc = topk_impl(c, c->r_score.p, c->r_dup.p, m, cand_base, k, c->r_topk_idx.p, c->r_topk_score.p)))
       return rc;
     mark(c, "topk");

@@ -243,10 +243,8 @@ int ut_comm_init(ut_ctx* c, int32_t rank, int32_t nranks, const uint8_t* id_host
   ncclUniqueId id;
   memcpy(&id, id_host, sizeof(id));
   ncclComm_t comm = nullptr;
-  // the count / agreement words of ut_comm_bcast_results, allocated here so
-  // that no allocation can fail between a rank's entry and its first collective
-  int rc;
-  if ((rc = ensure(c, c->cm_cnt, 2))) return rc;
+  // (the count / agreement words of ut_comm_bcast_results come with the
+  // context: nothing is allocated between a rank's entry and the collective init)
   UT_RCCL(c, ncclCommInitRank(&comm, nranks, id, rank));
   c->comm = comm;
   c->comm_rank = rank;

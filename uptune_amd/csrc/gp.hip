@@ -1052,7 +1052,9 @@ int gp_fit_enqueue(ut_ctx* c, const double* X, const double* y, int32_t n, int32
   // categorical K*: every ENUM / BOOL feature under one lengthscale and every
   // training row one-hot there (an append checks only its new rows)
   const Space& sp = c->space;
-  bool cat = c->cat_enable && c->has_space && sp.n_cat > 0 && d == sp.n_feat;
+  // (and the candidates' code rows fit one workgroup's LDS: a space with
+  // thousands of ENUM options scores with the dense contraction)
+  bool cat = c->cat_enable && c->has_space && sp.n_cat > 0 && d == sp.n_feat && code_rows_lds(sp.cat_k) <= c->max_lds;
   double cinv = 0.0;
   if (cat) {
     cinv = hinv[sp.host_params[sp.host_cat[0]].feat_col];
@@ -1256,8 +1258,7 @@ static int gather_kstar_cols(ut_ctx* c, bool cat, int32_t dpad, int64_t ldk, con
                              int64_t nc, int64_t ldc);
 
 int gp_score_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, const ut_acq* acq, const uint8_t* dup,
-                  double* mu, double* var, double* score, hipEvent_t dup_ready, const std::function<int()>& mid,
-                  bool var_joins) {
+                  double* mu, double* var, double* score, hipEvent_t dup_ready) {
   UT_CHECK(c, c->gp_ready, UT_EINVAL, "gp_score: call ut_gp_fit first");
   UT_CHECK(c, acq != nullptr, UT_EINVAL, "gp_score: acq is NULL");
   if (m <= 0) return 0;
@@ -1304,9 +1305,11 @@ int gp_score_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, const ut
                               cat ? kstar_cat(c, c->bcat.p) : KstarCat(), cat ? c->gp_xnorm_num.p : nullptr)))
     return rc;
   mark(c, "kstar");
-  if (mid && (rc = mid())) return rc;
   if (c->fit_pending && !fp32) UT_HIP(c, hipStreamWaitEvent(c->stream, c->ev_fit, 0));
-  if (dup_ready && c->join_before_var && var_joins) UT_HIP(c, hipStreamWaitEvent(c->stream, dup_ready, 0));
+  // the variance GEMM runs alone: the side stream's hash + dedup share the CUs
+  // with K* only (C2: 27.95 -> 28.2 ms per round when they spilled into it, the
+  // GEMM at 0.74 instead of 0.80 of peak; round 1)
+  if (dup_ready) UT_HIP(c, hipStreamWaitEvent(c->stream, dup_ready, 0));
   mark(c, "");  // the wait for the fit is not variance time
   if (i8) {
     if ((rc = launch_gemm_var_i8(c, npad, reinterpret_cast<const int8_t*>(c->kst.p), ldk, m, c->var_part.p)))

@@ -618,7 +618,7 @@ int launch_xs_t(ut_ctx* c, const double* Xs, int32_t npad, int32_t d, int32_t dp
 // ---------------------------------------------------------------------------
 // Variance contraction, persistent:  part[rt][col] = sum_{r in tile rt} (L^-1 K*^T)[r][col]^2
 //
-// One 512-thread workgroup per CU (8 waves as 2 x 4 of 64 x 64 outputs) walks
+// fp32 (precision 32): one 512-thread workgroup per CU (8 waves as 2 x 4 of 64 x 64 outputs) walks
 // (column strip, row tile) work items: 128 rows of L^-1 x 256 candidates, K
 // loop over [0, (rt+1)*128) (L^-1 is lower triangular).  Work items of XCD
 // group x (blocks b = x mod 8) are the column strips ct = x mod 8, handed out
@@ -630,7 +630,7 @@ int launch_xs_t(ut_ctx* c, const double* Xs, int32_t npad, int32_t d, int32_t dp
 // A non-persistent grid of these tiles left CUs idle ~30% of the time: the
 // in-order workgroup dispatcher stalls behind long (late row) tiles.
 //   A = (L^-1)^T [k][row] (ld npad), B = K*^T [k][col] (ld ldk, ldk % 256 == 0)
-//   fp64: v_mfma_f64_16x16x4_f64, BK 16;  fp32: v_mfma_f32_32x32x2_f32, BK 32
+//   v_mfma_f32_32x32x2_f32, BK 32 (the fp64 tier's kernel is k_gp_var_pp below)
 // ---------------------------------------------------------------------------
 constexpr int V_NT = 512, V_ST = 3;
 
@@ -667,26 +667,8 @@ __device__ __forceinline__ void var_issue(const T* __restrict__ AT, int64_t lda,
 typedef double vd4 __attribute__((ext_vector_type(4)));
 typedef float vf16 __attribute__((ext_vector_type(16)));
 
-// one BK step of the variance contraction for row sub-tiles i >= imin
+// one BK step of the fp32 variance contraction for row sub-tiles i >= imin
 // (imin wave-uniform: scalar branches around each sub-tile's MFMAs)
-__device__ __forceinline__ void var_step_f64(const double* as, const double* bs, int wm, int wn, int lane, int imin,
-                                             vd4 (&acc)[4][4]) {
-#pragma unroll
-  for (int ks = 0; ks < 4; ++ks) {
-    const int kr = ks * 4 + (lane >> 4);
-    double af[4], bf[4];
-#pragma unroll
-    for (int jj = 0; jj < 4; ++jj) bf[jj] = bs[kr * VAR_BN + wn * 64 + jj * 16 + (lane & 15)];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      if (i < imin) continue;
-      af[i] = as[kr * VAR_BM + wm * 64 + i * 16 + (lane & 15)];
-#pragma unroll
-      for (int jj = 0; jj < 4; ++jj) acc[i][jj] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[i], bf[jj], acc[i][jj], 0, 0, 0);
-    }
-  }
-}
-
 __device__ __forceinline__ void var_step_f32(const float* as, const float* bs, int wm, int wn, int lane, int imin,
                                              vf16 (&acc)[2][2]) {
 #pragma unroll
@@ -705,17 +687,16 @@ __device__ __forceinline__ void var_step_f32(const float* as, const float* bs, i
   }
 }
 
-template <typename T>
-__global__ __launch_bounds__(V_NT, 1) void k_gp_var(const T* __restrict__ AT, int64_t lda, const T* __restrict__ B,
-                                                     int64_t ldb, int32_t K, int32_t RT, int32_t CT, int64_t m,
-                                                     int32_t* __restrict__ ticket, double* __restrict__ part,
-                                                     int64_t ldp, const double* __restrict__ beta,
-                                                     double* __restrict__ mpart) {
-  using C = VCfg<T>;
+__global__ __launch_bounds__(V_NT, 1) void k_gp_var_f32(const float* __restrict__ AT, int64_t lda,
+                                                         const float* __restrict__ B, int64_t ldb, int32_t K,
+                                                         int32_t RT, int32_t CT, int64_t m,
+                                                         int32_t* __restrict__ ticket, double* __restrict__ part,
+                                                         int64_t ldp) {
+  using C = VCfg<float>;
   constexpr int BK = C::BK;
   // ALL LDS in one object: a second __shared__ beside the glds ring makes
   // hipcc wait vmcnt(0) before every step's first ds_read (drains the ring)
-  __shared__ __attribute__((aligned(16))) T lds[V_ST * C::STAGE + 16 / sizeof(T)];
+  __shared__ __attribute__((aligned(16))) float lds[V_ST * C::STAGE + 4];
   int32_t& s_item = *reinterpret_cast<int32_t*>(lds + V_ST * C::STAGE);
   const int t = threadIdx.x, lane = t & 63;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
@@ -733,27 +714,19 @@ __global__ __launch_bounds__(V_NT, 1) void k_gp_var(const T* __restrict__ AT, in
     const int32_t row0 = rt * VAR_BM;
     const int32_t nk = min(K, row0 + VAR_BM) / BK;
 
-    vd4 accd[4][4];
-    vf16 accf[2][2];
-    if constexpr (sizeof(T) == 8) {
+    vf16 acc[2][2];
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int jj = 0; jj < 4; ++jj) accd[i][jj] = (vd4){0.0, 0.0, 0.0, 0.0};
-    } else {
+      for (int jj = 0; jj < 2; ++jj)
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int jj = 0; jj < 2; ++jj)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) accf[i][jj][r] = 0.0f;
-    }
+        for (int r = 0; r < 16; ++r) acc[i][jj][r] = 0.0f;
 
-    var_issue<T>(AT, lda, B, ldb, row0, col0, 0, lds, w, lane);
-    if (nk > 1) var_issue<T>(AT, lda, B, ldb, row0, col0, BK, lds + C::STAGE, w, lane);
+    var_issue<float>(AT, lda, B, ldb, row0, col0, 0, lds, w, lane);
+    if (nk > 1) var_issue<float>(AT, lda, B, ldb, row0, col0, BK, lds + C::STAGE, w, lane);
     // one pipeline step: retire stage kt (6 glds per wave per stage; stage kt+1
     // stays in flight), then refill the slot of stage kt-1 with stage kt+2
-    auto pipe = [&](int32_t kt) -> const T* {
+    auto pipe = [&](int32_t kt) -> const float* {
       if (kt + 1 < nk)
         asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
       else
@@ -761,83 +734,43 @@ __global__ __launch_bounds__(V_NT, 1) void k_gp_var(const T* __restrict__ AT, in
       __builtin_amdgcn_s_barrier();  // all waves' stage kt landed; all reads of stage kt-1 done
       asm volatile("" ::: "memory");
       if (kt + 2 < nk)
-        var_issue<T>(AT, lda, B, ldb, row0, col0, (kt + 2) * BK, lds + ((kt + 2) % V_ST) * C::STAGE, w, lane);
+        var_issue<float>(AT, lda, B, ldb, row0, col0, (kt + 2) * BK, lds + ((kt + 2) % V_ST) * C::STAGE, w, lane);
       return lds + (kt % V_ST) * C::STAGE;
     };
     // k blocks left of the diagonal block: every MFMA sub-tile
     const int32_t nfull = min(nk, row0 / BK);
     for (int32_t kt = 0; kt < nfull; ++kt) {
-      const T* as = pipe(kt);
-      if constexpr (sizeof(T) == 8) var_step_f64(as, as + C::SA, wm, wn, lane, 0, accd);
-      else var_step_f32(as, as + C::SA, wm, wn, lane, 0, accf);
+      const float* as = pipe(kt);
+      var_step_f32(as, as + C::SA, wm, wn, lane, 0, acc);
     }
     // the diagonal block: (L^-1)^T is zero for k > row, so the MFMA sub-tiles
-    // of rows below k are skipped (wave-uniform).  The two waves sharing a
-    // SIMD (wm = 0, 1) issue 36 instead of 64 sub-tile steps here (f64), ~10%
-    // of the kernel's MFMAs at n = 1024.  Skipped terms are exact zeros, so
-    // the result is bit-identical.
+    // of rows below k are skipped (wave-uniform); skipped terms are exact
+    // zeros, so the result is bit-identical
     for (int32_t kt = nfull; kt < nk; ++kt) {
-      const T* as = pipe(kt);
-      const int kd = kt - nfull - (sizeof(T) == 8 ? 4 : 2) * wm;
+      const float* as = pipe(kt);
+      const int kd = kt - nfull - 2 * wm;
       const int imin = kd < 0 ? 0 : kd;
-      if constexpr (sizeof(T) == 8) {
-        if (imin < 4) var_step_f64(as, as + C::SA, wm, wn, lane, imin, accd);
-      } else {
-        if (imin < 2) var_step_f32(as, as + C::SA, wm, wn, lane, imin, accf);
-      }
+      if (imin < 2) var_step_f32(as, as + C::SA, wm, wn, lane, imin, acc);
     }
 
-    // epilogue: column sums of squares over this tile's 128 rows and (fp64)
-    // the mean partial sum_r V[r][c] beta_r, beta = L^-1 y
+    // epilogue: column sums of squares over this tile's 128 rows
     __syncthreads();
-    double* red = reinterpret_cast<double*>(lds);  // [2][256] squares, then [2][256] mean
-    if constexpr (sizeof(T) == 8) {
-      double bt[4][4];
+    double* red = reinterpret_cast<double*>(lds);  // [2][256]
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+    for (int jj = 0; jj < 2; ++jj) {
+      const int cl = wn * 64 + jj * 32 + (lane & 31);
+      double s = 0.0;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) bt[i][r] = beta[row0 + wm * 64 + i * 16 + (lane >> 4) + 4 * r];
+      for (int i = 0; i < 2; ++i)
 #pragma unroll
-      for (int jj = 0; jj < 4; ++jj) {
-        const int cl = wn * 64 + jj * 16 + (lane & 15);
-        double s = 0.0, u = 0.0;
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const double v = accd[i][jj][r];
-            s += v * v;
-            u += v * bt[i][r];
-          }
-        s += __shfl_xor(s, 16);
-        s += __shfl_xor(s, 32);
-        u += __shfl_xor(u, 16);
-        u += __shfl_xor(u, 32);
-        if ((lane >> 4) == 0) {
-          red[wm * VAR_BN + cl] = s;
-          red[2 * VAR_BN + wm * VAR_BN + cl] = u;
-        }
-      }
-    } else {
-#pragma unroll
-      for (int jj = 0; jj < 2; ++jj) {
-        const int cl = wn * 64 + jj * 32 + (lane & 31);
-        double s = 0.0;
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) s += (double)accf[i][jj][r] * (double)accf[i][jj][r];
-        s += __shfl_xor(s, 32);
-        if ((lane >> 5) == 0) red[wm * VAR_BN + cl] = s;
-      }
+        for (int r = 0; r < 16; ++r) s += (double)acc[i][jj][r] * (double)acc[i][jj][r];
+      s += __shfl_xor(s, 32);
+      if ((lane >> 5) == 0) red[wm * VAR_BN + cl] = s;
     }
     __syncthreads();
     if (t < VAR_BN) {
       const int64_t col = col0 + t;
-      if (col < m) {
-        part[(int64_t)rt * ldp + col] = red[t] + red[VAR_BN + t];
-        if (sizeof(T) == 8) mpart[(int64_t)rt * ldp + col] = red[2 * VAR_BN + t] + red[3 * VAR_BN + t];
-      }
+      if (col < m) part[(int64_t)rt * ldp + col] = red[t] + red[VAR_BN + t];
     }
   }
 }
@@ -846,8 +779,9 @@ __global__ __launch_bounds__(V_NT, 1) void k_gp_var(const T* __restrict__ AT, in
 // Variance contraction, fp64, "ping-pong": TWO 256-thread workgroups per CU
 // (__launch_bounds__(256, 2), 68 KiB of LDS each), so every SIMD holds one wave
 // of each and one workgroup's barrier wait, pipeline fill and epilogue overlap
-// the other's MFMAs.  k_gp_var<double> (one 512-thread workgroup per CU) puts
-// both waves of a SIMD behind the same barrier every 16 k.
+// the other's MFMAs.  The one-512-thread-workgroup-per-CU form (k_gp_var_f32's
+// shape in fp64, removed in round 5) put both waves of a SIMD behind the same
+// barrier every 16 k.
 //   tile: 128 rows of L^-1 x 128 candidates, 2 x 2 waves of 64 x 64 outputs;
 //   rows interleaved by 16-row sub-tiles (wave wm owns sub-tiles 2i + wm), so
 //   in the diagonal block -- where (L^-1)^T is zero for k > row and the
@@ -857,9 +791,9 @@ __global__ __launch_bounds__(V_NT, 1) void k_gp_var(const T* __restrict__ AT, in
 //   ring: 2 stages of 16 k (32 KiB), global_load_lds_dwordx4, 8 per wave per
 //   stage; stage kt+1 is issued right after the barrier of step kt.
 // Measured on MI355X, C2 shape (scripts/exp/var_probe.hip): 16.9 ms (0.83 of
-// the fp64 peak) against 18.1 ms for k_gp_var<double>; 0.88 without any global
+// the fp64 peak) against 18.1 ms for the one-workgroup form; 0.88 without any global
 // loads, 0.93 without the triangle (full K, no loads).
-// Work items, tickets and the part / mpart layouts are k_gp_var's.
+// Tickets and the part / mpart layouts: [RT][ldk] column partials per 128-row tile.
 // ---------------------------------------------------------------------------
 constexpr int VP_NT = 256, VP_BN = 128, VP_BK = 16, VP_ST = 2;
 constexpr int VP_SA = VP_BK * VAR_BM, VP_STAGE = VP_SA + VP_BK * VP_BN;
@@ -880,7 +814,7 @@ __global__ __launch_bounds__(VP_NT, 2) void k_gp_var_pp(const double* __restrict
                                                         int32_t* __restrict__ ticket, double* __restrict__ part,
                                                         int64_t ldp, const double* __restrict__ beta,
                                                         double* __restrict__ mpart, int32_t kcs, int32_t per_strip,
-                                                        double* __restrict__ vbuf, int32_t sched, int32_t S) {
+                                                        double* __restrict__ vbuf, int32_t S) {
   // one __shared__ object (see k_gp_var): ring, reduction buffer, ticket slot
   __shared__ __attribute__((aligned(16))) double lds[VP_ST * VP_STAGE + 4 * VP_BN + VAR_BM + 2];
   double* red = lds + VP_ST * VP_STAGE;  // [2][128] squares, [2][128] mean
@@ -912,7 +846,7 @@ __global__ __launch_bounds__(VP_NT, 2) void k_gp_var_pp(const double* __restrict
     __syncthreads();  // also: the previous item's epilogue is done with `red`
     const int32_t j = s_item;
     int32_t ct, rt, kt0, kt1, g = 0;
-    int32_t rt2 = -1;   // sched 1: the pair's second (short) row tile
+    int32_t rt2 = -1;   // the pair's second (short) row tile
     if constexpr (SPLIT) {
       g = j * 8 + xcd;
       if (g >= CT * per_strip) break;
@@ -927,25 +861,21 @@ __global__ __launch_bounds__(VP_NT, 2) void k_gp_var_pp(const double* __restrict
       }
       kt0 = rem * kcs;
       kt1 = min(var_nk(K, rt), kt0 + kcs);
-    } else if (sched == 1) {
+    } else {
       // paired groups (as k_gp_var_h3): item = row tiles (RT - 1 - p, p) of one
       // strip, every item the same length; an XCD's workgroups take P pairs x S
-      // strips at once, so a group shares each L^-1 stage through L2
+      // strips at once, so a group shares each L^-1 stage through L2 (C2: FETCH
+      // 41.1 -> 24.3 GB per launch against strip-major items, round 26.10-26.15
+      // -> 25.99 ms; round 4)
       const int32_t G = j / (P * S), q = j % (P * S), p = q % P;
       ct = (G * S + q / P) * 8 + xcd;
-      if (ct >= CT) break;
+      if (ct >= CT) break;  // uniform: every wave of the block leaves together
       rt = RT - 1 - p;
       rt2 = p != rt ? p : -1;
       kt0 = 0;
       kt1 = var_nk(K, rt);
-    } else {
-      ct = (j / RT) * 8 + xcd;
-      if (ct >= CT) break;  // uniform: every wave of the block leaves together
-      rt = RT - 1 - (j % RT);
-      kt0 = 0;
-      kt1 = var_nk(K, rt);
     }
-    for (;;) {   // the item's row tiles (one, or sched 1's pair)
+    for (;;) {   // the item's row tiles (its pair)
     const int64_t col0 = (int64_t)ct * VP_BN;
     const int32_t row0 = rt * VAR_BM;
     vd4 acc[4][4];
@@ -1201,21 +1131,20 @@ __device__ __forceinline__ int h3_linv_exp(const unsigned long long* amax_bits) 
 // stage kt's 48 MFMAs per wave run.  part[rt][col] gets the column partial
 // sum_{r in tile} V[r][col]^2 (RT2 = rows / 256 of them).
 //
-// Item order (sched): 0 = per XCD, strip-major (a strip's row tiles, longest
-// first, then the next strip); 1 = "paired groups": an item is the row-tile
-// pair (RT2 - 1 - p, p) of one strip (every pair the same length, RT2 + 1
-// tiles of k), and an XCD's W workgroups take W items at once as P pairs x
-// S strips (P = ceil(RT2 / 2), S = W / P).  Equal lengths keep a group in
-// step, so the S workgroups of a pair read each L^-1 stage at about the same
-// time (one fetch from the Infinity Cache, S - 1 L2 hits) and the P
-// workgroups of a strip share its long-tile K* stages -- where sched 0 reads
-// the whole L^-1 triangle per strip from the Infinity Cache.
+// Item order ("paired groups"): an item is the row-tile pair (RT2 - 1 - p, p)
+// of one strip (every pair the same length, RT2 + 1 tiles of k), and an XCD's
+// W workgroups take W items at once as P pairs x S strips (P = ceil(RT2 / 2),
+// S = W / P).  Equal lengths keep a group in step, so the S workgroups of a
+// pair read each L^-1 stage at about the same time (one fetch from the
+// Infinity Cache, S - 1 L2 hits) and the P workgroups of a strip share its
+// long-tile K* stages -- where strip-major items (round 3) read the whole
+// L^-1 triangle per strip from the Infinity Cache.
 __global__ __launch_bounds__(512, 2) void k_gp_var_h3(const _Float16* __restrict__ A, int64_t a_lo,
                                                       const _Float16* __restrict__ B, int64_t b_lo, int32_t K,
                                                       int32_t RT2, int32_t CT, int64_t m, int32_t* __restrict__ ticket,
                                                       double* __restrict__ part, int64_t ldp,
                                                       const unsigned long long* __restrict__ amax_bits, int32_t kexp,
-                                                      int32_t sched, int32_t S, int32_t rev_short) {
+                                                      int32_t S) {
   __shared__ __attribute__((aligned(16))) _Float16 lds[H3_NS * H3_STAGE + 8];
   int32_t& s_item = *reinterpret_cast<int32_t*>(lds + H3_NS * H3_STAGE);
   const int t = threadIdx.x, lane = t & 63;
@@ -1230,18 +1159,10 @@ __global__ __launch_bounds__(512, 2) void k_gp_var_h3(const _Float16* __restrict
     if (t == 0) s_item = atomicAdd(&ticket[xcd], 1);
     __syncthreads();
     const int32_t j = s_item;
-    int32_t ct, rts[2], nrt;
-    if (sched == 1) {
-      const int32_t G = j / (P * S), q = j % (P * S), p = q % P;
-      ct = (G * S + q / P) * 8 + xcd;
-      rts[0] = RT2 - 1 - p;
-      rts[1] = p;
-      nrt = rts[1] == rts[0] ? 1 : 2;
-    } else {
-      ct = (j / RT2) * 8 + xcd;
-      rts[0] = RT2 - 1 - (j % RT2);
-      nrt = 1;
-    }
+    const int32_t G = j / (P * S), q = j % (P * S), p = q % P;
+    const int32_t ct = (G * S + q / P) * 8 + xcd;
+    const int32_t rts[2] = {RT2 - 1 - p, p};
+    const int32_t nrt = rts[1] == rts[0] ? 1 : 2;
     if (ct >= CT) break;
     for (int32_t ri = 0; ri < nrt; ++ri) {
     if (ri > 0) __syncthreads();   // the previous tile's reduction buffer (LDS ring) fully read
@@ -1259,13 +1180,13 @@ __global__ __launch_bounds__(512, 2) void k_gp_var_h3(const _Float16* __restrict
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[i][jj][r] = 0.0f;
 
-    // rev (sched 1, the pair's second, short tile): its k stages in descending
+    // rev (the pair's second, short tile): its k stages in descending
     // order.  The strip's P workgroups then read K* stage t (long tiles) or
     // RT2 - t (short tiles, reversed) at step t of their items -- two stages
     // per step across the strip instead of up to P -- so the L2 serves the
     // rest.  (Ascending, each second tile restarted at stage 0 while the
     // others were far ahead: 344 GB fetched per C3 launch for 32 GB of K*.)
-    const bool rev = rev_short && ri > 0;
+    const bool rev = ri > 0;
     auto ktof = [&](int32_t u) -> int32_t { return rev ? nk - 1 - u : u; };
     h3_issue<3>(Ab + (int64_t)ktof(0) * H3_BLK, a_lo, Bb + (int64_t)ktof(0) * H3_BLK, b_lo, lds, w, lane);
     auto pipe = [&](int32_t u) -> const _Float16* {
@@ -1397,15 +1318,11 @@ int launch_gemm_var(ut_ctx* c, int prec, const void* LinvT, int64_t lda, const v
     const int32_t S2 = W / P2 > 1 ? W / P2 : 1;
     hipLaunchKernelGGL(k_gp_var_h3, dim3(nb2), dim3(512), 0, c->stream, (const _Float16*)LinvT, (int64_t)n256 * npad,
                        (const _Float16*)kst, ldk * (int64_t)npad, npad, RT2, (int32_t)((m + H3_BN - 1) / H3_BN), m,
-                       c->gp_ctr, part, ldk, amax, h3_kstar_exp(c->gp_sf2), c->h3_sched, S2,
-                       c->h3_sched == 1 ? c->h3_rev : 0);
+                       c->gp_ctr, part, ldk, amax, h3_kstar_exp(c->gp_sf2), S2);
   }
   else if (fp32)
-    hipLaunchKernelGGL(k_gp_var<float>, dim3(nb), dim3(V_NT), 0, c->stream, (const float*)LinvT, lda,
-                       (const float*)kst, ldk, npad, RT, CT, m, c->gp_ctr, part, ldk, nullptr, nullptr);
-  else if (c->var_kernel == 1)   // UT_VAR_KERNEL=1: the one-workgroup-per-CU kernel (measurements)
-    hipLaunchKernelGGL(k_gp_var<double>, dim3(nb), dim3(V_NT), 0, c->stream, (const double*)LinvT, lda,
-                       (const double*)kst, ldk, npad, RT, CT, m, c->gp_ctr, part, ldk, beta, mpart);
+    hipLaunchKernelGGL(k_gp_var_f32, dim3(nb), dim3(V_NT), 0, c->stream, (const float*)LinvT, lda,
+                       (const float*)kst, ldk, npad, RT, CT, m, c->gp_ctr, part, ldk);
   else {
     // two workgroups per CU on 128-candidate column tiles
     const int32_t CTp = (int32_t)((m + VP_BN - 1) / VP_BN);
@@ -1426,7 +1343,7 @@ int launch_gemm_var(ut_ctx* c, int prec, const void* LinvT, int64_t lda, const v
       if (items_s < nbp) nbp = (int32_t)(((items_s + 7) / 8) * 8);
       hipLaunchKernelGGL(k_gp_var_pp<true>, dim3(nbp), dim3(VP_NT), 0, c->stream, (const double*)LinvT, lda,
                          (const double*)kst, ldk, npad, RT, CTp, m, c->gp_ctr, part, ldk, beta, mpart, kcs, per_strip,
-                         c->var_vbuf.p, 0, 1);
+                         c->var_vbuf.p, 1);
       hipLaunchKernelGGL(k_var_split_red, dim3(RT, CTp), dim3(1024), 0, c->stream, c->var_vbuf.p, npad, kcs, per_strip,
                          m, beta, part, mpart, ldk);
     } else {
@@ -1435,7 +1352,7 @@ int launch_gemm_var(ut_ctx* c, int prec, const void* LinvT, int64_t lda, const v
       const int32_t Sp = Wp / Pp > 1 ? Wp / Pp : 1;
       hipLaunchKernelGGL(k_gp_var_pp<false>, dim3(nbp), dim3(VP_NT), 0, c->stream, (const double*)LinvT, lda,
                          (const double*)kst, ldk, npad, RT, CTp, m, c->gp_ctr, part, ldk, beta, mpart, 0, 0, nullptr,
-                         c->var_sched, Sp);
+                         Sp);
     }
   }
   UT_LAUNCH_CHECK(c);

@@ -42,23 +42,12 @@ typedef int32_t i8v4 __attribute__((ext_vector_type(4)));
 typedef int32_t i8v16 __attribute__((ext_vector_type(16)));
 
 constexpr int I8_PL = I8_BM * I8_BK;   // one plane's piece of a stage: 64 rows x 32 k = 2 KiB
-constexpr int I8_NST = 3;              // ring stages
 constexpr double I8_C = 3.5 * 0x1p-49;
 
 template <int N>
 __device__ __forceinline__ void i8_vm_wait() {
   static_assert(N >= 0 && N < 64, "vmcnt");
   __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
-}
-
-// v_ic's digit-product groups of one 32 x 32 wave tile: T_g for g = 2 .. 7
-// (pairs (p, q) with p + q = g, p, q in 1 .. 6), over one 32-k stage
-__device__ __forceinline__ void i8_stage_mfma(const i8v4 (&af)[I8_S], const i8v4 (&bf)[I8_S], i8v16 (&acc)[I8_S]) {
-#pragma unroll
-  for (int g = 2; g <= I8_S + 1; ++g)
-#pragma unroll
-    for (int p = 1; p < g; ++p)
-      acc[g - 2] = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[p - 1], bf[g - p - 1], acc[g - 2], 0, 0, 0);
 }
 
 // ---------------------------------------------------------------------------
@@ -137,23 +126,32 @@ int launch_split_i8(ut_ctx* c, int32_t n, int32_t npad) {
 //
 // Persistent, TWO 256-thread workgroups per CU (one's barrier waits and
 // epilogue overlap the other's MFMAs, as k_gp_var_pp); a work item is the
-// row-tile pair (RT - 1 - p, p) of one 64-candidate strip (every item the same
-// length), handed out per XCD in groups of P pairs x Sg strips so the group
-// shares each L^-1 stage through L2.  Tile 64 rows x 64 candidates, waves 2 x 2
-// of 32 x 32; a 3-stage ring of 32-k stages (6 A + 6 B planes, 24 KiB), filled
-// by global_load_lds (6 per wave per stage).  The wave's rows [32 wm, +32) see
-// zeros once k passes them (L^-1 is lower triangular): those stages skip
-// their MFMAs.  Probe (scripts/exp/i8var_probe.hip, C2 shape n = 1024,
-// m = 2^20, random digits): see DESIGN.md §4.
+// row-tile pair (RT - 1 - p, p) of one 128-candidate strip (every item the
+// same length), handed out per XCD in groups of P pairs x Sg strips so the
+// group shares each L^-1 stage through L2.  The pair's second (short) tile
+// walks its k stages in descending order: at every step the strip's P
+// workgroups then read at most two distinct K* stages, the rest L2 hits.
+// Tile 64 rows x 128 candidates; waves 2 x 2 of 32 rows x 64 candidates (two
+// 32 x 32 MFMA column tiles share the wave's A fragments; B planes streamed
+// one at a time); a 2-stage ring of 32-k stages (6 A planes x 2 KiB + 6 B
+// planes x 4 KiB = 36 KiB), filled by global_load_lds (9 per wave per stage).
+// The wave's rows [32 wm, +32) see zeros once k passes them (L^-1 is lower
+// triangular): those stages skip their MFMAs.  Probe on random digits
+// (scripts/exp/i8var_probe.hip, n = 1024, m = 2^20): 9.26 ms against 10.0 for
+// 64-candidate tiles with a 3-stage ring.
 // ---------------------------------------------------------------------------
+constexpr int I8_WN = 128;                 // candidates per tile
+constexpr int I8_BPL = I8_WN * I8_BK;      // one B plane's piece of a stage (4 KiB)
+
 __global__ __launch_bounds__(256, 2) void k_gp_var_i8(const int8_t* __restrict__ Ad, const int8_t* __restrict__ Bd,
                                                       int32_t npad, int64_t ldk, int32_t RT, int32_t CT, int64_t m,
                                                       int32_t* __restrict__ ticket, const double* __restrict__ rs,
                                                       double* __restrict__ part, int32_t Sg) {
-  constexpr int STAGE = 2 * I8_S * I8_PL;
-  __shared__ __attribute__((aligned(16))) int8_t lds[I8_NST * STAGE + 2 * I8_BN * 8 + I8_BM * 8 + 16];
-  double* red = reinterpret_cast<double*>(lds + I8_NST * STAGE);   // [2][64]
-  double* srs = red + 2 * I8_BN;                                    // row scales of the tile
+  constexpr int STAGE = I8_S * (I8_PL + I8_BPL);
+  constexpr int NW = 6 * I8_S / 4;   // glds per wave per stage
+  __shared__ __attribute__((aligned(16))) int8_t lds[2 * STAGE + 2 * I8_WN * 8 + I8_BM * 8 + 16];
+  double* red = reinterpret_cast<double*>(lds + 2 * STAGE);   // [2][128]
+  double* srs = red + 2 * I8_WN;                               // row scales of the tile
   int32_t& s_item = *reinterpret_cast<int32_t*>(srs + I8_BM);
   const int t = threadIdx.x, lane = t & 63;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
@@ -161,20 +159,37 @@ __global__ __launch_bounds__(256, 2) void k_gp_var_i8(const int8_t* __restrict__
   const int32_t xcd = blockIdx.x & 7;
   const int64_t aplane = (int64_t)npad * npad, bplane = (int64_t)npad * ldk;
 
-  // stage kt of tile (row0, col0): 12 planes x 2 KiB, wave w moves pieces w + 4j
+  // stage kt of tile (row0, col0): A planes 2 KiB (2 pieces), B planes 4 KiB (4 pieces);
+  // wave w moves pieces w + 4j
   auto issue = [&](int32_t row0, int64_t col0, int32_t kt, int8_t* st) {
 #pragma unroll
-    for (int j = 0; j < I8_S; ++j) {
+    for (int j = 0; j < NW; ++j) {
       const int u = w + 4 * j;
-      const int pl = u >> 1, h = u & 1;
-      const int8_t* src = pl < I8_S ? Ad + pl * aplane + ((int64_t)kt * npad + row0) * 32
-                                    : Bd + (pl - I8_S) * bplane + ((int64_t)kt * ldk + col0) * 32;
-      __builtin_amdgcn_global_load_lds(src + h * 1024 + lane * 16,
-                                       (__attribute__((address_space(3))) void*)(st + pl * I8_PL + h * 1024), 16, 0, 0);
+      const int8_t* src;
+      int8_t* dst;
+      if (u < 2 * I8_S) {
+        const int pl = u >> 1, h = u & 1;
+        src = Ad + pl * aplane + ((int64_t)kt * npad + row0) * 32 + h * 1024;
+        dst = st + pl * I8_PL + h * 1024;
+      } else {
+        const int v = u - 2 * I8_S, pl = v >> 2, h = v & 3;
+        src = Bd + pl * bplane + ((int64_t)kt * ldk + col0) * 32 + h * 1024;
+        dst = st + I8_S * I8_PL + pl * I8_BPL + h * 1024;
+      }
+      __builtin_amdgcn_global_load_lds(src + lane * 16, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
     }
   };
 
   const int32_t P = (RT + 1) / 2;
+  const int c = lane >> 5;
+  const int ra = wm * 32 + (lane & 31);
+  const int aoff = ra * 32 + ((c ^ ((ra >> 3) & 1)) << 4);
+  int boff[2];
+#pragma unroll
+  for (int jj = 0; jj < 2; ++jj) {
+    const int cb = wn * 64 + jj * 32 + (lane & 31);
+    boff[jj] = I8_S * I8_PL + cb * 32 + ((c ^ ((cb >> 3) & 1)) << 4);
+  }
   for (;;) {
     if (t == 0) s_item = atomicAdd(&ticket[xcd], 1);
     __syncthreads();
@@ -188,64 +203,74 @@ __global__ __launch_bounds__(256, 2) void k_gp_var_i8(const int8_t* __restrict__
       if (ri > 0) __syncthreads();   // the previous tile's ring, red and srs are read
       const int32_t rt = rts[ri];
       const int32_t row0 = rt * I8_BM;
-      const int64_t col0 = (int64_t)ct * I8_BN;
+      const int64_t col0 = (int64_t)ct * I8_WN;
       const int32_t nk = (row0 + I8_BM) / I8_BK;   // >= 2
-      i8v16 acc[I8_S];
+      const bool rev = ri > 0;
+      auto ktof = [&](int32_t u) -> int32_t { return rev ? nk - 1 - u : u; };
+      i8v16 acc[2][I8_S];
 #pragma unroll
-      for (int g = 0; g < I8_S; ++g)
+      for (int jj = 0; jj < 2; ++jj)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) acc[g][r] = 0;
+        for (int g = 0; g < I8_S; ++g)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc[jj][g][r] = 0;
       if (w == 0 && lane < 32)   // 64 row scales: one 512-B glds, retired with stage 0
         __builtin_amdgcn_global_load_lds(rs + row0 + lane * 2, (__attribute__((address_space(3))) void*)srs, 16, 0, 0);
-      issue(row0, col0, 0, lds);
-      issue(row0, col0, 1, lds + STAGE);
-      const int c = lane >> 5;
-      const int ra = wm * 32 + (lane & 31), cb = wn * 32 + (lane & 31);
-      const int aoff = ra * 32 + ((c ^ ((ra >> 3) & 1)) << 4);
-      const int boff = I8_S * I8_PL + cb * 32 + ((c ^ ((cb >> 3) & 1)) << 4);
-      for (int32_t kt = 0; kt < nk; ++kt) {
-        if (kt + 1 < nk) i8_vm_wait<I8_S>();   // stage kt landed; kt + 1 (this wave's 6 glds) may fly
-        else i8_vm_wait<0>();
-        __builtin_amdgcn_s_barrier();           // every wave's stage kt landed; stage kt - 1 fully read
+      issue(row0, col0, ktof(0), lds);
+      for (int32_t u = 0; u < nk; ++u) {
+        i8_vm_wait<0>();                        // stage u landed (this wave's pieces)
+        __builtin_amdgcn_s_barrier();           // every wave's stage u landed; stage u - 1 fully read
         asm volatile("" ::: "memory");
-        if (kt + 2 < nk) issue(row0, col0, kt + 2, lds + ((kt + 2) % I8_NST) * STAGE);
-        if (kt * I8_BK >= row0 + 32 * wm + 32) continue;   // rows of this wave: all zero from here on
-        const int8_t* st = lds + (kt % I8_NST) * STAGE;
-        i8v4 af[I8_S], bf[I8_S];
+        if (u + 1 < nk) issue(row0, col0, ktof(u + 1), lds + ((u + 1) & 1) * STAGE);
+        const int32_t kt = ktof(u);
+        if (kt * I8_BK >= row0 + 32 * wm + 32) continue;   // rows of this wave: all zero here
+        const int8_t* st = lds + (u & 1) * STAGE;
+        i8v4 af[I8_S];
 #pragma unroll
-        for (int pp = 0; pp < I8_S; ++pp) {
-          af[pp] = *reinterpret_cast<const i8v4*>(st + pp * I8_PL + aoff);
-          bf[pp] = *reinterpret_cast<const i8v4*>(st + pp * I8_PL + boff);
+        for (int pp = 0; pp < I8_S; ++pp) af[pp] = *reinterpret_cast<const i8v4*>(st + pp * I8_PL + aoff);
+#pragma unroll
+        for (int qb = 0; qb < I8_S; ++qb) {
+          i8v4 bf[2];
+#pragma unroll
+          for (int jj = 0; jj < 2; ++jj) bf[jj] = *reinterpret_cast<const i8v4*>(st + qb * I8_BPL + boff[jj]);
+          // digit products of group g = pa + qb (0-based): pairs with (pa + 1) + (qb + 1) <= 7
+#pragma unroll
+          for (int pa = 0; pa + qb < I8_S; ++pa)
+#pragma unroll
+            for (int jj = 0; jj < 2; ++jj)
+              acc[jj][pa + qb] = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[pa], bf[jj], acc[jj][pa + qb], 0, 0, 0);
         }
-        i8_stage_mfma(af, bf, acc);
       }
       // epilogue: v = 2^-16 (T_2 + 2^-8 (T_3 + ...)) * 2^(ea_row + eb), column sums of v^2
       // (C/D map of the 32x32 MFMA: row (r & 3) + 8 (r >> 2) + 4 (lane >> 5), column lane & 31)
-      double s = 0.0;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        double v = (double)acc[I8_S - 1][r];
+      for (int jj = 0; jj < 2; ++jj) {
+        double s = 0.0;
 #pragma unroll
-        for (int g = I8_S - 2; g >= 0; --g) v = __builtin_fma(v, 0x1p-8, (double)acc[g][r]);
-        v *= 0x1p-16 * srs[wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)];
-        s = __builtin_fma(v, v, s);
+        for (int r = 0; r < 16; ++r) {
+          double v = (double)acc[jj][I8_S - 1][r];
+#pragma unroll
+          for (int g = I8_S - 2; g >= 0; --g) v = __builtin_fma(v, 0x1p-8, (double)acc[jj][g][r]);
+          v *= 0x1p-16 * srs[wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)];
+          s = __builtin_fma(v, v, s);
+        }
+        s += __shfl_xor(s, 32);
+        if (lane < 32) red[wm * I8_WN + wn * 64 + jj * 32 + lane] = s;
       }
-      s += __shfl_xor(s, 32);
-      if (lane < 32) red[wm * I8_BN + wn * 32 + lane] = s;
       __syncthreads();
-      if (t < I8_BN) {
+      if (t < I8_WN) {
         const int64_t col = col0 + t;
-        if (col < m) part[(int64_t)rt * ldk + col] = red[t] + red[I8_BN + t];
+        if (col < m) part[(int64_t)rt * ldk + col] = red[t] + red[I8_WN + t];
       }
     }
   }
 }
 
 int launch_gemm_var_i8(ut_ctx* c, int32_t npad, const int8_t* kst8, int64_t ldk, int64_t m, double* part) {
-  UT_CHECK(c, npad % 128 == 0 && npad <= I8_MAX_K && ldk % I8_BN == 0 && ldk >= m, UT_EINVAL,
+  UT_CHECK(c, npad % 128 == 0 && npad <= I8_MAX_K && ldk % I8_WN == 0 && ldk >= m, UT_EINVAL,
            "gemm_var_i8: bad padding");
   UT_CHECK(c, c->gp_i8a.p && c->gp_i8rs.p, UT_EINVAL, "gemm_var_i8: the fit has no int8 planes");
-  const int32_t RT = npad / I8_BM, CT = (int32_t)((m + I8_BN - 1) / I8_BN);
+  const int32_t RT = npad / I8_BM, CT = (int32_t)((m + I8_WN - 1) / I8_WN);
   const int32_t P = (RT + 1) / 2;
   const int64_t items = (int64_t)P * CT;
   int32_t nb = 2 * (c->n_cu / 8) * 8;   // two workgroups per CU, a multiple of 8 (every XCD group works)

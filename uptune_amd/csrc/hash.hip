@@ -568,14 +568,14 @@ int launch_hash_de(ut_ctx* c, const double* values, int64_t ld, int64_t m, int64
     UT_LAUNCH_CHECK(c);
   }
   const int64_t want = ((int64_t)s.n_comp * m + HASH_NT - 1) / HASH_NT;
-  const bool hold = c->round_hash_hold > 0 && c->fit_pending && hipEventQuery(c->ev_fit) == hipErrorNotReady;
-  const int32_t cap = hash_cap(c, m, false, hold && c->round_hash_hold == 2);
+  // (ctx.round_hash_hold: the round's inner digests and outer hash wait for an in-flight fit)
+  const bool hold = c->round_hash_hold && c->fit_pending && hipEventQuery(c->ev_fit) == hipErrorNotReady;
+  const int32_t cap = hash_cap(c, m, false, hold);
   const unsigned grid = (unsigned)std::min<int64_t>(std::max<int64_t>(want, 1), (int64_t)c->n_cu * (cap > 0 ? cap : 8));
-  if (hold && c->round_hash_hold == 2) UT_HIP(c, hipStreamWaitEvent(c->stream, c->ev_fit, 0));
+  if (hold) UT_HIP(c, hipStreamWaitEvent(c->stream, c->ev_fit, 0));
   hipLaunchKernelGGL(k_inner_pairs, dim3(grid), dim3(HASH_NT), 0, c->stream, s.d_params, s.d_comp, values, ld,
                      c->r_pairs.p, np, reinterpret_cast<uint4*>(c->r_fresh.p));
   UT_LAUNCH_CHECK(c);
-  if (hold && c->round_hash_hold == 1) UT_HIP(c, hipStreamWaitEvent(c->stream, c->ev_fit, 0));
   return launch_hash_impl(c, values, ld, m, out,
                           InnerRef{c->r_mask.p, reinterpret_cast<const uint4*>(c->r_fresh.p),
                                    reinterpret_cast<const uint4*>(c->pop_dig), c->npop, cand_base, c->pop_dig_lo,

@@ -138,16 +138,6 @@ struct ut_ctx {
   hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_fit = nullptr, ev_prefit = nullptr;
   hipEvent_t ev_fit_x = nullptr;     // fit stream: scaled training inputs ready (K* may start)
   bool fit_pending = false;          // scoring waits on ev_fit before touching GP state
-  // round schedule: 1 = the variance GEMM waits for the side stream's hash +
-  // dedup (they share CUs with K* only, and the variance GEMM runs alone),
-  // 0 = only the finalize waits (the hash may spill into the variance GEMM).
-  // Measured at C2: 28.2 vs 27.95 ms per round, variance GEMM 0.80 vs 0.74 of
-  // the fp64 peak (it shares CUs with the tail of the hash).  1 is the
-  // default; UT_JOIN_BEFORE_VAR=0 selects the other schedule.
-  int32_t join_before_var = 1;
-  // fp64 variance kernel: 0 = k_gp_var_pp (two 4-wave workgroups per CU, the
-  // default), 1 = k_gp_var<double> (one 8-wave workgroup per CU); UT_VAR_KERNEL
-  int32_t var_kernel = 0;
   // fp64 variance with few candidate strips: 1 = split the k loops
   // (k_gp_var_pp<true> + k_var_split_red), 0 = one item per row tile; UT_VAR_SPLIT
   int32_t var_split = 1;
@@ -191,30 +181,13 @@ struct ut_ctx {
   int64_t pop_aos_cap = 0;
   bool pop_aos_valid = false;
   int32_t de_aos = 1;   // 0: k_de gathers donor values from the column-major population (UT_DE_AOS=0)
-  // round schedule of dense fp64 DE rounds (the only ones whose K* does not
-  // wait for the whole GP fit): 2 = the side stream's inner digests and outer
-  // hash wait for an in-flight fit, 1 = only the outer hash, 0 = neither
-  // (UT_HASH_AFTER_FIT).  Beside the hash, the fit's chain of ~70 small kernels
-  // finds no free CU slots and stretches from ~1.5 to ~9 ms, and the variance
-  // GEMM waits for it; held, the fit runs beside K* alone.  Measured at C2:
-  // 26.10-26.12 ms per round (2), 26.32-26.34 (1), 26.54-26.80 (0).
-  int32_t hash_after_fit = 2;
-  int32_t round_hash_hold = 0;   // the value in force for the round being enqueued
-  // 1: fp32 / f16x3 dense rounds hold the hash for an in-flight fit as well
-  // (their K* waits for the whole fit anyway); UT_HASH_HOLD_LOWPREC
-  int32_t hash_hold_lowprec = 0;
-  // the same for pruned rounds (their K* takes the mean from alpha, so it
-  // waits for the whole fit); UT_HASH_HOLD_PRUNED
-  int32_t hash_hold_pruned = 0;
+  // the round being enqueued holds its hash for an in-flight fit (dense fp64
+  // rounds: api.hip score_round_de_impl)
+  bool round_hash_hold = false;
   // the grid-stride hash kernels' workgroups per CU: > 0 at most this many, 0
   // uncapped, -1 capped while a large refit is in flight (hash.hip hash_cap);
   // UT_HASH_WG_PER_CU
   int32_t hash_wg_per_cu = -1;
-  // the fit stream at the device's highest stream priority (UT_FIT_PRIORITY=1):
-  // its chain of small kernels gets the CU slots freed by other streams first
-  bool fit_priority = false;
-  // the fit kernels' waves at s_setprio 3 (gp.hip g_fit_prio); UT_FIT_SETPRIO
-  int32_t fit_setprio = 1;
   // refit: the next diagonal block factored inside the trailing update
   // (k_chol_update_diag). -1 = from 2048 padded rows on: the fit alone 6.5 ->
   // 5.7 ms at n = 4096, C3 pruned 60.1 -> 59.2 ms; at C2 (n = 1024, the fit
@@ -226,26 +199,6 @@ struct ut_ctx {
   // the diagonal blocks' inverse solved inside the Cholesky column loop
   // (gp.hip chol_diag_core<true>); UT_CHOL_MERGED
   int32_t chol_merged = 1;
-  // fp32 / f16x3 dense rounds: 1 = enqueue the hash after K* (their K* waits
-  // for the whole fit, which the hash would otherwise crowd out of the CUs: at
-  // n = 4096 the refit stretches from ~6 to ~14 ms beside it) and let the
-  // variance GEMM run beside it; 0 (default) = fork it before encode; -1 = 1
-  // for fits of n >= 2048.  Measured, f16x3: round 3, C3 (n 4096) 149.2 vs
-  // 153.0 ms per round, C2 (n 1024) 12.9-13.1 vs 12.8 ms; round 4, with the
-  // categorical K* (C3's K* 46 -> 22 ms, so the fit's crowding costs less than
-  // the hash's 7-ms tail after the variance GEMM): C3 121.9 ms after K* vs
-  // 120.4 before encode, the tail 6.7 -> 0.2 ms (profiles/r04l_c3h*.log).
-  // UT_HASH_AFTER_KSTAR
-  int32_t hash_after_kstar = 0;
-  // k_gp_var_h3 item order: 0 = strip-major, 1 = paired row tiles in XCD
-  // groups (L^-1 stages shared in L2 by the group's workgroups); UT_H3_SCHED
-  int32_t h3_sched = 1;
-  // k_gp_var_h3 (sched 1): a pair's short tile walks k in descending order so the
-  // strip's workgroups read the same K* stages at the same step (UT_H3_REV)
-  int32_t h3_rev = 1;
-  // k_gp_var_pp (fp64) item order: 0 = strip-major, 1 = paired row tiles in XCD groups (C2:
-  // FETCH 41.1 -> 24.3 GB per launch, round 26.10-26.15 -> 25.99 ms; scripts/ab/r04c_varsched.sh); UT_VAR_SCHED
-  int32_t var_sched = 1;
 
   struct PopSlot {
     double* pop = nullptr;
@@ -293,7 +246,7 @@ struct ut_ctx {
   int32_t gp_prec = 64;        // precision requested for the next fit
   int32_t gp_fit_prec = 64;    // precision of the fitted factors used by scoring
   // incremental fit (gp.hip gp_fit_enqueue): 1 = a fit whose training set
-  // extends the previous one's extends its factor (ut_gp_set_fit_append, UT_FIT_APPEND)
+  // extends the previous one's extends its factor (ut_gp_set_fit_append)
   int32_t fit_append = 1;
   int32_t gp_npad_fit = 0;     // padded size of the current factor
   double gp_diag_fit = 0.0;    // its sigma_n2 + jitter
@@ -325,6 +278,9 @@ struct ut_ctx {
   int64_t i8_recomputed = 0;     // candidates of the last score recomputed in fp64 (-1: all, dense)
   int32_t* gp_ctr = nullptr;   // [32] per-XCD work tickets: [0,8) variance, [8,16) K*; [16,18) max|L^-1| bits (h3)
   int32_t n_cu = 256;
+  // LDS one workgroup may hold (hipDeviceAttributeMaxSharedMemoryPerBlock): the
+  // categorical K*'s code-row kernels need code_rows_lds(cat_k) of it
+  size_t max_lds = 65536;
   int64_t gp_cap_n = 0;
 
   // scratch for GP scoring / round pipeline
@@ -505,13 +461,10 @@ int launch_hist_insert(ut_ctx* c, const uint32_t* dig, int64_t n);
 int launch_hist_rehash(ut_ctx* c, const uint32_t* okeys, const uint32_t* ostate, int64_t ocap);
 int launch_dedup(ut_ctx* c, const uint32_t* dig, int64_t m, uint8_t* dup);
 // feat == nullptr: the candidates' scaled features and norms are already in
-// c->ucand / c->cnorm (gp_encode_scaled)
-// mid (optional): enqueued work between K* and the variance GEMM (the round's
-// hash when it runs after K*); var_joins = false: the variance GEMM does not
-// wait for dup_ready (only the finalize does)
+// c->ucand / c->cnorm (gp_encode_scaled); dup_ready: the event of the dup
+// mask (the round's side stream), joined before the variance GEMM
 int gp_score_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, const ut_acq* acq, const uint8_t* dup,
-                  double* mu, double* var, double* score, hipEvent_t dup_ready = nullptr,
-                  const std::function<int()>& mid = nullptr, bool var_joins = true);
+                  double* mu, double* var, double* score, hipEvent_t dup_ready = nullptr);
 // encode + scale in one pass into c->ucand / c->cnorm (sized for m), for gp_score_impl(feat = nullptr)
 int gp_encode_scaled(ut_ctx* c, const double* values, int64_t ld, int64_t m);
 int launch_encode_scaled(ut_ctx* c, const double* values, int64_t ld, int64_t m, double* u, int32_t dpad, int64_t ldu,
