@@ -75,6 +75,13 @@ def training_set(n, d, seed):
     return X, rosenbrock_decoded(X)
 
 
+def selection_sha(idx, dig):
+    """sha256 of a round's merged selections (global indices, then digests)"""
+    import hashlib
+    return hashlib.sha256(idx.detach().cpu().numpy().astype("<i8").tobytes() +
+                          dig.detach().cpu().numpy().view(np.uint32).astype(">u4").tobytes()).hexdigest()
+
+
 def host_info():
     """CPU model, logical CPUs of the machine, and the threads this job may use
     (OMP_NUM_THREADS, else the affinity mask: 16 per GPU on the MI355X boxes)"""
@@ -155,13 +162,15 @@ def load_pmc(kernel_key):
 SHA256_CEIL_GCPS = 28.5   # measured chip ceiling of SHA-256 compressions (scripts/exp/sha_rate.hip)
 
 
-def kernel_table(m, n, d, outer_blocks):
+def kernel_table(m, n, d, outer_blocks, prec=64):
     """Per-kernel rooflines of the default C2 round from the committed rocprofv3
     record (profiles/pmc_summary.json: average launch duration from the
     --kernel-trace --stats pass, HBM bytes from the FETCH_SIZE / WRITE_SIZE
     passes of the same command).  Algorithmic work per launch:
       k_de: 40 d B per candidate (target, 3 donors, trial); k_hash (outer):
-      outer_blocks compressions per candidate; K*: 2 n dpad flops; encode: 16 F B."""
+      outer_blocks compressions per candidate; K*: 2 n dpad flops; encode: 16 F B.
+    prec 8: K* is k_gp_kstar<int8_t> (the mean k* . alpha and six digit planes
+    in its epilogue; record key kstar8)."""
     out = {}
     try:
         with open(os.path.join(ROOT, "profiles", "pmc_summary.json")) as f:
@@ -197,7 +206,7 @@ def kernel_table(m, n, d, outer_blocks):
 
     hbm("propose", 40.0 * d * m)
     hbm("encode", 16.0 * d * m)
-    mfma("kstar", 2.0 * n * (d + (-d) % 16) * m)   # the variance GEMM is `roofline` (HIP events of this run)
+    mfma("kstar8" if prec == 8 else "kstar", 2.0 * n * (d + (-d) % 16) * m)   # the variance GEMM is `roofline`
     t, traffic = rec("hash")
     if t > 0:
         c = float(outer_blocks) * m
@@ -365,11 +374,11 @@ def main():
     ap.add_argument("--no-parity", action="store_true", help="skip the oracle check of the selections")
     ap.add_argument("--parity-sample", type=int, default=1 << 16,
                     help="random other candidates whose oracle EI must not beat the score-determined top-k")
-    ap.add_argument("--precision", type=int, default=64, choices=(64, 32, 16, 8),
+    ap.add_argument("--precision", type=int, default=None, choices=(64, 32, 16, 8),
                     help="GP contractions on fp64 MFMA (1e-5 parity) or fp32 MFMA (1e-3 parity); 16 = f16x3: "
                          "the variance contraction as 3 fp16 MFMA products of hi/lo splits (fp32 tier, 1e-3); "
                          "8 = the fp64 tier (1e-5) on the int8 MFMA: six-digit slices, per-candidate error "
-                         "bound, fp64 recompute of the candidates it does not clear")
+                         "bound, fp64 recompute of the candidates it does not clear (the default; --prune: 64)")
     ap.add_argument("--config", default="c2", choices=("c2", "c3", "c4"),
                     help="c2 = BASELINE configs[1] (R64, m=1M, n=1024: the headline); c3 = configs[2] per GPU "
                          "(HPL-64 mixed space, 16M/8 = 2M candidates per GPU, n=4096); c4 = configs[3] "
@@ -378,6 +387,8 @@ def main():
                     help="selection-exact EI-bound pruning (ut_score_round_de_pruned) with the first ROWS rows of "
                          "L^-1 k* as the bound; a secondary line, fp64 only (the dense round stays the headline)")
     args = ap.parse_args()
+    if args.precision is None:
+        args.precision = 64 if args.prune else 8
     if args.prune and args.precision != 64:
         ap.error("--prune needs --precision 64")
     if args.config == "c3":
@@ -600,7 +611,10 @@ def main():
                 rep2.update({"lengthscale": 2.0, "sample": int(len(samp)),
                              "kth_selected_ei": kth, "best_unselected_sample_ei": float(np.max(ei_s)),
                              "topk_beats_sample": bool(np.max(ei_s) <= kth * (1.0 + 1e-5)),
-                             "distinct_selected_scores": int(len(np.unique(tx.cpu().numpy())))})
+                             "distinct_selected_scores": int(len(np.unique(tx.cpu().numpy()))),
+                             # this round's merged selections: decided by the scores (all
+                             # distinct), so equal shas across N check the cross-rank merge
+                             "selection_sha": selection_sha(ix, dx)})
                 parity["score_determined"] = rep2
         if rank == 0:
             legs = [v for v in parity.values() if v]
@@ -610,9 +624,7 @@ def main():
     # the last timed round's merged selections, as one digest comparable across
     # N (strong scaling: the same at every N; weak: equal to a one-rank run
     # with --m N*m) -- computed outside the timed region
-    import hashlib
-    sel_sha = hashlib.sha256(idx.detach().cpu().numpy().astype("<i8").tobytes() +
-                             sdig.detach().cpu().numpy().view(np.uint32).astype(">u4").tobytes()).hexdigest()
+    sel_sha = selection_sha(idx, sdig)
     # device memory per rank: what libuthot holds on the rank's GPU (max over ranks)
     mem = torch.tensor([float(eng.device_bytes())], dtype=torch.float64)
     if world > 1:
@@ -724,7 +736,7 @@ def main():
         "hbm_bytes_per_rank": hbm_rank,
         "hbm_device_used_bytes": int(total_b - free_b),
         "stage_ms": stages,
-        "kernels": (kernel_table(m, n, d, eng.space_info()[1]) if profiled else None),
+        "kernels": (kernel_table(m, n, d, eng.space_info()[1], args.precision) if profiled else None),
         "prune": prune_info,
         "i8": i8_info,
         "roofline": {"bound": "mfma", "kernel": kernel,
@@ -744,6 +756,12 @@ def main():
                 result["cpu_baseline"] = cpu_baseline_b1(args.b1_sample, n, d, k, host["threads"])
         except Exception as ex:  # keep the GPU number even if the baseline fails
             result["cpu_baseline"] = {"error": repr(ex)}
+        try:       # the same B1 on every CPU of the job's affinity mask (the box's OMP_NUM_THREADS is 16)
+            if args.b1_sample > 0 and host["affinity_cpus"] > host["threads"]:
+                result["cpu_baseline_full_affinity"] = cpu_baseline_b1(args.b1_sample, n, d, k,
+                                                                       host["affinity_cpus"])
+        except Exception as ex:
+            result["cpu_baseline_full_affinity"] = {"error": repr(ex)}
         try:       # the reference's per-candidate, single-threaded search loop (api.py:428-446)
             if args.cpu_sample > 0:
                 result["cpu_baseline_1thread"] = cpu_baseline(args.cpu_sample, n, d, k)

@@ -150,7 +150,6 @@ def b1_baseline(m_sample, n, d, k, seed=1, threads=None):
     from . import gp as ogp
     from .space import FLOAT, Param
     threads = threads or int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count()
-    os.environ["OMP_NUM_THREADS"] = str(threads)
     space = [Param(i, FLOAT, -1000.0, 1000.0) for i in range(d)]
     rng = np.random.default_rng(seed + 100)
     X = rng.uniform(size=(n, d))

@@ -6,7 +6,7 @@ as the HIP kernel):
   * --scaling strong: the global pool is fixed, rank r scores
     [r*M/N, (r+1)*M/N).  The 8-rank line selects exactly what the 1-rank
     line selects (equal `selection_sha` of the last timed round's merged
-    (index, digest) list) and both pass the oracle parity block -- SURVEY.md
+    (index, digest) list, and of the score-determined parity round's) and both pass the oracle parity block -- SURVEY.md
     §8(e)'s "the same top-k at 1/2/4/8 GPUs", checked on the bench's own
     output (the analog of the reference's parallel_factor instances that
     exchange results every round, python/uptune/api.py:400-401,547-553);
@@ -52,6 +52,11 @@ def test_strong_scaling_selections_equal_at_1_and_8_ranks():
     assert eight["config"]["candidates_per_gpu"] == M // 8
     assert one["parity"]["all_ok"] and eight["parity"]["all_ok"], (one["parity"], eight["parity"])
     assert one["selection_sha"] == eight["selection_sha"]
+    # the score-determined round (ell = 2: every selected score distinct), so the
+    # equal shas check the cross-rank score merge, not only the index tie-break
+    sd1, sd8 = one["parity"]["score_determined"], eight["parity"]["score_determined"]
+    assert sd1["distinct_selected_scores"] == sd8["distinct_selected_scores"] == 256
+    assert sd1["selection_sha"] == sd8["selection_sha"]
     # the shard-local inner-digest cache: an eighth of the pool's targets per rank
     assert 0 < eight["hbm_bytes_per_rank"] < one["hbm_bytes_per_rank"]
 
@@ -67,3 +72,4 @@ def test_weak_scaling_line_equals_one_rank_with_the_whole_pool():
     assert two["config"]["global_pool"] == one["config"]["global_pool"] == 2 * m
     assert two["parity"]["all_ok"] and one["parity"]["all_ok"]
     assert two["selection_sha"] == one["selection_sha"]
+    assert two["parity"]["score_determined"]["selection_sha"] == one["parity"]["score_determined"]["selection_sha"]
