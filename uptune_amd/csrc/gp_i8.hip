@@ -108,11 +108,15 @@ __global__ __launch_bounds__(256) void k_i8_errsum(const double* __restrict__ e2
   if (t == 0) *E = sqrt((red[0] + red[1]) + (red[2] + red[3])) * (1.0 + 0x1p-40);
 }
 
-int launch_split_i8(ut_ctx* c, int32_t n, int32_t npad) {
+int alloc_split_i8(ut_ctx* c, int32_t npad) {
   int rc;
   if ((rc = ensure(c, c->gp_i8a, (size_t)I8_S * npad * npad))) return rc;
-  if ((rc = ensure(c, c->gp_i8rs, (size_t)2 * npad + 1))) return rc;   // [rs | e2 | E]
-  c->gp_i8_eb = i8_kstar_exp(c->gp_sf2);
+  return ensure(c, c->gp_i8rs, (size_t)2 * npad + 1);   // [rs | e2 | E]
+}
+
+int launch_split_i8(ut_ctx* c, int32_t n, int32_t npad) {
+  UT_CHECK(c, c->gp_i8a.n >= (size_t)I8_S * npad * npad && c->gp_i8rs.n >= (size_t)2 * npad + 1, UT_EINVAL,
+           "split_i8: planes not allocated (alloc_split_i8)");
   double* rs = c->gp_i8rs.p;
   hipLaunchKernelGGL(k_split_i8, dim3(npad), dim3(256), 0, c->stream, c->gp_Linv, n, npad, c->gp_i8_eb,
                      c->gp_i8a.p, rs, rs + npad);

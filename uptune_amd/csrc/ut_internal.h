@@ -138,6 +138,12 @@ struct ut_ctx {
   hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_fit = nullptr, ev_prefit = nullptr;
   hipEvent_t ev_fit_x = nullptr;     // fit stream: scaled training inputs ready (K* may start)
   bool fit_pending = false;          // scoring waits on ev_fit before touching GP state
+  // the fit's device work as two captured graphs (gp_fit_enqueue): captured
+  // when a fit's signature repeats the previous one's, replayed while it does
+  bool fit_graph = true;                       // UT_FIT_GRAPH=0: always launch directly
+  hipGraphExec_t fit_exec[2] = {nullptr, nullptr};
+  std::vector<uint64_t> fit_key, fit_last;     // signature of the graphs / of the previous fit
+  int64_t fit_graph_stats[3] = {0, 0, 0};      // fits launched directly / captured / replayed
   // fp64 variance with few candidate strips: 1 = split the k loops
   // (k_gp_var_pp<true> + k_var_split_red), 0 = one item per row tile; UT_VAR_SPLIT
   int32_t var_split = 1;
@@ -576,7 +582,9 @@ __device__ __forceinline__ void i8_planes(const uint32_t (&lo)[4], const uint32_
   pl[4] = i8_gather(lo, 1) ^ 0x80808080u;
   pl[5] = i8_gather(lo, 0) ^ 0x80808080u;
 }
-// fit: L^-1's planes, row scales and the error bound (c->gp_i8a, c->gp_i8rs)
+// fit: L^-1's planes, row scales and the error bound (c->gp_i8a, c->gp_i8rs,
+// allocated beforehand by alloc_split_i8; the digit scale of K* in c->gp_i8_eb)
+int alloc_split_i8(ut_ctx* c, int32_t npad);
 int launch_split_i8(ut_ctx* c, int32_t n, int32_t npad);
 // the variance contraction from K*'s digit planes (kst8, [6][npad/32][ldk][32]):
 // part [npad / 64][ldk] column partials of |v|^2
