@@ -375,17 +375,22 @@ __global__ __launch_bounds__(K_NT, 2) void k_gp_kstar(const double* __restrict__
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int rl0 = wm * 64 + i * 16 + 4 * (lane >> 4);   // this lane's training rows rl0 .. rl0 + 3
+        double hx[4], al[4];   // (per row, shared by the four column groups)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const double hv = (-0.5 * KSTAR_T_SCALE) * rowop[rl0 + r];
+          hx[r] = row0 + rl0 + r < n ? hv : -1e300;
+          al[r] = rowop[K_BM + rl0 + r] * ikscale;
+        }
 #pragma unroll
         for (int jj = 0; jj < 4; ++jj) {
           const int64_t col = col0 + wn * 64 + jj * 16 + (lane & 15);
           uint32_t lo[4], hi[4];
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const double hv = (-0.5 * KSTAR_T_SCALE) * rowop[rl0 + r];
-            const double hx = row0 + rl0 + r < n ? hv : -1e300;
-            const double x = __builtin_fmax(__builtin_fmin((acc[i][jj][r] + hx) + hc[jj], 0.0), KSTAR_T_MIN);
+            const double x = __builtin_fmax(__builtin_fmin((acc[i][jj][r] + hx[r]) + hc[jj], 0.0), KSTAR_T_MIN);
             const double ks = sf2_exp2t_nonpos(x, etab);   // y = k* 2^-eb
-            s[jj] += (rowop[K_BM + rl0 + r] * ikscale) * ks;
+            s[jj] = __builtin_fma(al[r], ks, s[jj]);
             const uint64_t b = i8_biased(ks);
             lo[r] = (uint32_t)b;
             hi[r] = (uint32_t)(b >> 32);

@@ -10,7 +10,7 @@
 //   column c of K*: y_kc = k*_kc 2^-eb      (eb from sf2 >= k*: |y| <= 0.49)
 //   X = rint(x 2^48) = sum_{p=1..6} a_p 256^(6-p), a_p in [-128, 127] ("balanced"
 //   digits: the bytes of X + 0x808080808080, each XOR 0x80, taken from the bits
-//   of the fp64 sum x + 24, whose ulp is 2^-48 -- i8_biased below), Y likewise.
+//   of the fp64 sum x + 24.50196..., whose ulp is 2^-48 -- i8_biased), Y likewise.
 //   x y ~ sum_{p+q <= 7} a_p b_q 2^-8(p+q):  21 of the 36 digit products, in
 //   six groups g = p + q whose int32 sums T_g = sum_k sum_{p+q=g} a_p b_q are
 //   exact (|a b| <= 2^14, at most 6 pairs per group: K < 2^14 rows keep every

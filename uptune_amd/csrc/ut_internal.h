@@ -561,26 +561,32 @@ inline int i8_kstar_exp(double sf2) { return ilogb(sf2 / 0.49) + 1; }
 __host__ __device__ inline int64_t i8_off(int64_t r, int32_t k, int64_t ld) {
   return ((int64_t)(k >> 5) * ld + r) * 32 + ((((k >> 4) & 1) ^ (int)((r >> 3) & 1)) << 4) + (k & 15);
 }
-// x in [-0.49, 0.49] -> rint(x 2^48) + 0x808080808080: the fp64 sum x + 24 has
-// ulp 2^-48 and a fixed exponent, so its bits minus a constant are that
-// integer; its six bytes, each XOR 0x80, are the balanced digits (int8) of
-// rint(x 2^48) in base 256, most significant = byte 5
+// x in [-0.49, 0.49] -> bits 0..47 = rint(x 2^48) + 0x808080808080: the fp64
+// sum x + 24.5019... (24 + 0x808080808080 2^-48, exact) lies in [16, 32), so
+// its ulp is 2^-48, its exponent field fixed, and its mantissa's low 48 bits
+// that integer (rounded to nearest even: the offset is even); its six bytes,
+// each XOR 0x80, are the balanced digits (int8) of rint(x 2^48) in base 256,
+// most significant = byte 5 (bits 48.. are the exponent: ignored)
 __device__ __forceinline__ uint64_t i8_biased(double x) {
-  return (uint64_t)__double_as_longlong(x + 24.0) - 0x40377F7F7F7F7F80ull;
+  return (uint64_t)__double_as_longlong(x + 0x1.8808080808080p4);
 }
 // four values' biased words (lo / hi dwords) -> the six digit planes' dwords
-// (byte u of plane p's dword = digit p of value u; plane 0 = most significant)
-__device__ __forceinline__ uint32_t i8_gather(const uint32_t (&w)[4], int b) {
-  return ((w[0] >> (8 * b)) & 0xFFu) | (((w[1] >> (8 * b)) & 0xFFu) << 8) | (((w[2] >> (8 * b)) & 0xFFu) << 16) |
-         (((w[3] >> (8 * b)) & 0xFFu) << 24);
-}
+// (byte u of plane p's dword = digit p of value u; plane 0 = most significant):
+// a 4 x 4 byte transpose by v_perm_b32 (byte j of perm(a, b, s) is byte
+// s_j of the pair, 0..3 = b, 4..7 = a)
 __device__ __forceinline__ void i8_planes(const uint32_t (&lo)[4], const uint32_t (&hi)[4], uint32_t (&pl)[I8_S]) {
-  pl[0] = i8_gather(hi, 1) ^ 0x80808080u;
-  pl[1] = i8_gather(hi, 0) ^ 0x80808080u;
-  pl[2] = i8_gather(lo, 3) ^ 0x80808080u;
-  pl[3] = i8_gather(lo, 2) ^ 0x80808080u;
-  pl[4] = i8_gather(lo, 1) ^ 0x80808080u;
-  pl[5] = i8_gather(lo, 0) ^ 0x80808080u;
+  const uint32_t t0 = __builtin_amdgcn_perm(lo[1], lo[0], 0x05010400u);   // w0.b0 w1.b0 w0.b1 w1.b1
+  const uint32_t t1 = __builtin_amdgcn_perm(lo[1], lo[0], 0x07030602u);   // w0.b2 w1.b2 w0.b3 w1.b3
+  const uint32_t t2 = __builtin_amdgcn_perm(lo[3], lo[2], 0x05010400u);
+  const uint32_t t3 = __builtin_amdgcn_perm(lo[3], lo[2], 0x07030602u);
+  const uint32_t u0 = __builtin_amdgcn_perm(hi[1], hi[0], 0x05010400u);
+  const uint32_t u2 = __builtin_amdgcn_perm(hi[3], hi[2], 0x05010400u);
+  pl[0] = __builtin_amdgcn_perm(u2, u0, 0x07060302u) ^ 0x80808080u;      // byte 5
+  pl[1] = __builtin_amdgcn_perm(u2, u0, 0x05040100u) ^ 0x80808080u;      // byte 4
+  pl[2] = __builtin_amdgcn_perm(t3, t1, 0x07060302u) ^ 0x80808080u;      // byte 3
+  pl[3] = __builtin_amdgcn_perm(t3, t1, 0x05040100u) ^ 0x80808080u;      // byte 2
+  pl[4] = __builtin_amdgcn_perm(t2, t0, 0x07060302u) ^ 0x80808080u;      // byte 1
+  pl[5] = __builtin_amdgcn_perm(t2, t0, 0x05040100u) ^ 0x80808080u;      // byte 0
 }
 // fit: L^-1's planes, row scales and the error bound (c->gp_i8a, c->gp_i8rs,
 // allocated beforehand by alloc_split_i8; the digit scale of K* in c->gp_i8_eb)
