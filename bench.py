@@ -758,7 +758,8 @@ def main():
             result["cpu_baseline"] = {"error": repr(ex)}
         try:       # the same B1 on every CPU of the job's affinity mask (the box's OMP_NUM_THREADS is 16)
             if args.b1_sample > 0 and host["affinity_cpus"] > host["threads"]:
-                result["cpu_baseline_full_affinity"] = cpu_baseline_b1(args.b1_sample, n, d, k,
+                # (a 4x larger sample: every thread gets rows to work on)
+                result["cpu_baseline_full_affinity"] = cpu_baseline_b1(4 * args.b1_sample, n, d, k,
                                                                        host["affinity_cpus"])
         except Exception as ex:
             result["cpu_baseline_full_affinity"] = {"error": repr(ex)}

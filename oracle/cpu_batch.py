@@ -120,7 +120,10 @@ class BatchPosterior:
         from concurrent.futures import ThreadPoolExecutor
 
         from threadpoolctl import threadpool_limits
-        parts = [U[i:i + self.chunk] for i in range(0, U.shape[0], self.chunk)]
+        # at least one chunk per thread (a 256-thread pool on 2^18 candidates
+        # in 8192-row chunks kept 32 threads busy)
+        ch = max(256, min(self.chunk, -(-U.shape[0] // self.threads)))
+        parts = [U[i:i + ch] for i in range(0, U.shape[0], ch)]
         with threadpool_limits(limits=1), ThreadPoolExecutor(self.threads) as ex:
             out = list(ex.map(self._part, parts))
         return np.concatenate([o[0] for o in out]), np.concatenate([o[1] for o in out])
@@ -144,7 +147,7 @@ def c2_round(space, pop, gp, seed, round_, m, k, hist=None, cr=0.2, threads=None
 
 def b1_baseline(m_sample, n, d, k, seed=1, threads=None):
     """candidates/s of the C2 round on `threads` host cores (OpenMP + BLAS)"""
-    from threadpoolctl import threadpool_limits
+    from threadpoolctl import threadpool_info, threadpool_limits
 
     from . import de as ode
     from . import gp as ogp
@@ -157,7 +160,13 @@ def b1_baseline(m_sample, n, d, k, seed=1, threads=None):
     y = np.sum(100.0 * (xs[:, 1:] - xs[:, :-1] ** 2) ** 2 + (xs[:, :-1] - 1.0) ** 2, axis=1)
     pop = ode.population_init(space, m_sample, seed)
     lib()
-    with threadpool_limits(limits=threads):
+    # OpenMP (DE + hash) and the posterior's chunk pool on every thread; the
+    # fit's BLAS calls on no more threads than OpenBLAS started with (its
+    # buffers are sized then: asked for more -- 32 or 256 where the box's
+    # OMP_NUM_THREADS is 16 -- it crashes in solve_triangular)
+    blas_threads = min([threads] + [i["num_threads"] for i in threadpool_info() if i.get("user_api") == "blas"])
+    with threadpool_limits(limits=threads, user_api="openmp"), \
+            threadpool_limits(limits=blas_threads, user_api="blas"):
         c2_round(space, pop[:, :4096], ogp.GP(X, y, lengthscale=0.2), seed, 0, 4096, k, threads=threads)  # warm-up
         t0 = time.perf_counter()
         gp = BatchPosterior(ogp.GP(X, y, lengthscale=0.2, sigma_f2=1.0, sigma_n2=1e-6), threads)
@@ -166,4 +175,5 @@ def b1_baseline(m_sample, n, d, k, seed=1, threads=None):
     return {"value": m_sample / dt, "unit": "candidates/s", "cores": threads, "kind": "port",
             "sample": f"B1 batch port: oracle/cpu_batch.cpp (C++/OpenMP DE-Alt + repr + OpenSSL SHA-256 "
                       f"hash_config + dedup set) + NumPy/SciPy BLAS GP fit n={n} (L^-1 once) + chunked K*/L^-1 K* "
-                      f"GEMM posterior + EI + top-{k}, {m_sample} R64 candidates, {threads} threads, {dt:.2f} s"}
+                      f"GEMM posterior + EI + top-{k}, {m_sample} R64 candidates, {threads} threads "
+                      f"(the fit's BLAS on {blas_threads}), {dt:.2f} s"}

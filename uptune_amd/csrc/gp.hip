@@ -1125,7 +1125,7 @@ static std::vector<uint64_t> fit_signature(const ut_ctx* c, int32_t n, int32_t n
   std::memcpy(&diagb, &diag, 8);
   const Space& sp = c->space;
   std::vector<uint64_t> k = {
-      (uint64_t)n, (uint64_t)n0, (uint64_t)d, (uint64_t)npad, (uint64_t)dpn, (uint64_t)app, (uint64_t)xr0, sf2b, diagb,
+      (uint64_t)n, (uint64_t)(app ? n0 : -1), (uint64_t)d, (uint64_t)npad, (uint64_t)dpn, (uint64_t)app, (uint64_t)xr0, sf2b, diagb,
       (uint64_t)c->gp_prec, (uint64_t)c->gp_i8_eb, (uint64_t)c->cat_on, (uint64_t)sp.cat_k, (uint64_t)sp.P,
       (uint64_t)sp.n_num, (uint64_t)(int64_t)c->chol_fuse, (uint64_t)c->trinv_big, (uint64_t)c->chol_merged};
   for (const void* p : {(const void*)c->fit_host, (const void*)c->gp_tmp, (const void*)c->gp_inv_ell,
