@@ -1,3 +1,11 @@
+// MEASURED, NOT KEPT (round 5): K* of a precision-8 fit with the distance
+// contraction on the int8 MFMA.  This is the last version measured (it was
+// wired into libuthot through launch_gemm_kstar for precision-8 fits; the first
+// version is in git history, commit 01cd36a); it is kept here as the record of
+// the experiment ("Round 5: an int8 distance contraction for
+// K*") and is not built.  C2: K* 2.6-2.7 ms + 0.33 ms candidate split against
+// 3.1-3.3 ms for k_gp_kstar<int8_t>; the round did not move (17.1-17.2 ms
+// against 17.0); C3 pruned K* 25.6 ms against 20.1 (fp64 MFMA).
 // gp_kq.hip -- K* for precision-8 fits: the distance contraction on the int8
 // MFMA ("Ozaki" digits, exact int32 sums), the exp epilogue on the VALU beside it.
 //
@@ -126,6 +134,54 @@ __global__ __launch_bounds__(256) void k_q_split_u(const double* __restrict__ U,
   }
 }
 
+// s_waitcnt vmcnt(n) lgkmcnt(0) for a run-time n (uniform), clamped to 63
+__device__ __forceinline__ void vm_wait_n(int32_t n) {
+  n = n < 0 ? 0 : (n > 63 ? 63 : n);
+  switch (n) {
+#define UT_VMW(N) \
+  case N: asm volatile("s_waitcnt vmcnt(" #N ") lgkmcnt(0)" ::: "memory"); break;
+    UT_VMW(0) UT_VMW(1) UT_VMW(2) UT_VMW(3) UT_VMW(4) UT_VMW(5) UT_VMW(6) UT_VMW(7) UT_VMW(8) UT_VMW(9) UT_VMW(10)
+    UT_VMW(11) UT_VMW(12) UT_VMW(13) UT_VMW(14) UT_VMW(15) UT_VMW(16) UT_VMW(17) UT_VMW(18) UT_VMW(19) UT_VMW(20)
+    UT_VMW(21) UT_VMW(22) UT_VMW(23) UT_VMW(24) UT_VMW(25) UT_VMW(26) UT_VMW(27) UT_VMW(28) UT_VMW(29) UT_VMW(30)
+    UT_VMW(31) UT_VMW(32) UT_VMW(33) UT_VMW(34) UT_VMW(35) UT_VMW(36) UT_VMW(37) UT_VMW(38) UT_VMW(39) UT_VMW(40)
+    UT_VMW(41) UT_VMW(42) UT_VMW(43) UT_VMW(44) UT_VMW(45) UT_VMW(46) UT_VMW(47) UT_VMW(48) UT_VMW(49) UT_VMW(50)
+    UT_VMW(51) UT_VMW(52) UT_VMW(53) UT_VMW(54) UT_VMW(55) UT_VMW(56) UT_VMW(57) UT_VMW(58) UT_VMW(59) UT_VMW(60)
+    UT_VMW(61) UT_VMW(62) UT_VMW(63)
+#undef UT_VMW
+  }
+}
+
+// a categorical stage's loads into an LDS ring slot: 64 code rows of 128 B for
+// A and B, 8 pieces of 1 KiB each; wave w moves pieces w + 4u (u < 4)
+__device__ __forceinline__ void q_issue_cat(const int8_t* __restrict__ acat, const int8_t* __restrict__ bcat,
+                                            int32_t npad, int64_t ldk, int w, int lane, int32_t row0, int64_t col0,
+                                            int32_t s2, int8_t* st) {
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int q = w + 4 * u;        // 0..15: A pieces 0..7, B pieces 8..15
+    const bool isb = q >= 8;
+    const int qq = q & 7;
+    const int r = 8 * qq + (lane >> 3);
+    const int cch = (lane & 7) ^ (r & 7);   // the source chunk that lands at position lane & 7
+    const int8_t* src = isb ? bcat + ((int64_t)s2 * ldk + col0 + r) * 128 + cch * 16
+                            : acat + ((int64_t)s2 * npad + row0 + r) * 128 + cch * 16;
+    __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(st + (isb ? 8192 : 0) + qq * 1024),
+                                     16, 0, 0);
+  }
+}
+
+// an item's epilogue operands (512 B each: waves 0..3 load xnorm, alpha, cnorm, scol)
+template <bool MU>
+__device__ __forceinline__ void q_issue_ops(const double* __restrict__ xnorm, const double* __restrict__ alpha,
+                                            const double* __restrict__ cnorm, const double* __restrict__ scol, int w,
+                                            int lane, int32_t row0, int64_t col0, double* ops) {
+  if (lane < 32 && (MU || w != 1)) {
+    const double* src = w == 0 ? xnorm + row0 : (w == 1 ? alpha + row0 : (w == 2 ? cnorm + col0 : scol + col0));
+    __builtin_amdgcn_global_load_lds(src + lane * 2, (__attribute__((address_space(3))) void*)(ops + w * Q_BM), 16, 0,
+                                     0);
+  }
+}
+
 // ---------------------------------------------------------------------------
 // the contraction + epilogue
 // ---------------------------------------------------------------------------
@@ -134,20 +190,18 @@ __global__ __launch_bounds__(Q_NT, 2) void k_gp_kstar_q(
     const int8_t* __restrict__ Xd, int32_t npad, const int8_t* __restrict__ Ud, int64_t ldk, int32_t K32,
     const double* __restrict__ scol, int32_t RT, int32_t CT, const double* __restrict__ xnorm,
     const double* __restrict__ cnorm, const double* __restrict__ alpha, double sf2, int32_t n, int64_t m,
-    int32_t* __restrict__ ticket, TS* __restrict__ kst, double* __restrict__ part, double kscale, int64_t lo_off,
+    TS* __restrict__ kst, double* __restrict__ part, double kscale, int64_t lo_off,
     int32_t store_rt, double* __restrict__ part2, const int8_t* __restrict__ acat, const int8_t* __restrict__ bcat,
     int32_t nkc, double cat_c0, double cat_c1) {
   constexpr bool I8 = sizeof(TS) == 1;
   constexpr int OPS = 2 * Q_BM + 2 * Q_BN;              // one item's epilogue operands (doubles)
-  constexpr int DB = EXP_TAB + 2 * OPS + 4 * Q_BN;      // doubles after the ring
-  __shared__ __attribute__((aligned(16))) int8_t lds[2 * Q_STAGE + 8 * DB + 16];
-  double* etab = reinterpret_cast<double*>(lds + 2 * Q_STAGE);
-  // two buffers of [rx 64 | ra 64 | cn 64 | cs 64] (alternate items):
+  // a 3-slot ring (80 KiB in all: two workgroups per CU)
+  __shared__ __attribute__((aligned(16))) int8_t lds[3 * Q_STAGE + 8 * (EXP_TAB + 3 * OPS)];
+  double* etab = reinterpret_cast<double*>(lds + 3 * Q_STAGE);
+  // three buffers (items k mod 3) of [rx 64 | ra 64 | cn 64 | cs 64]:
   //   rx training half-norms (t units; -1e300 past n), ra alpha (I8: / kscale),
   //   cn candidate half-norms (-1e300 past m), cs column scales
   double* ops0 = etab + EXP_TAB;
-  double* red = ops0 + 2 * OPS;  // [2][64] mean partials, [2][64] sum k*^2
-  int32_t* s_tk = reinterpret_cast<int32_t*>(red + 4 * Q_BN);   // [2] tickets (alternate items)
   const int t = threadIdx.x, lane = t & 63;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
   const int wm = w >> 1, wn = w & 1;
@@ -164,85 +218,90 @@ __global__ __launch_bounds__(Q_NT, 2) void k_gp_kstar_q(
   const int aoff = ra_ * 32 + ((c ^ ((ra_ >> 3) & 1)) << 4);
   const int boff = I8_S * Q_PL + cb * 32 + ((c ^ ((cb >> 3) & 1)) << 4);
 
-  auto issue_stage = [&](int32_t row0, int64_t col0, int32_t s2, int8_t* st) {
-    if (CAT && s2 < ncs) {
-      // 64 code rows of 128 B each for A and B (8 pieces each; wave w moves pieces w, w + 4)
+  // Items: XCD x's strips (ct = x mod 8), each strip's row tiles in turn, dealt
+  // round-robin to the XCD's W workgroups (equal items: no ticket atomic, whose
+  // return would drain this wave's stores every item).  The items' stages form
+  // one stream, g = k ntot + s for item k, issued two stages ahead into a
+  // 3-slot ring (the next items' first stages and epilogue operands load under
+  // the current item's MFMAs and epilogue).  s_waitcnt vmcnt counts loads,
+  // stores and LDS-DMA together in issue order (MI355X_MICROARCH.md), so stage
+  // g waits for all but the vector-memory instructions this wave issued after
+  // g's loads (counted below; the uncounted MU partial stores only add to the
+  // younger ones: the wait is then longer, never short).
+  const int32_t W = gridDim.x >> 3, b0 = blockIdx.x >> 3;
+  const int32_t Wq = W / RT, Wr = W % RT;    // an item's successor: W items on
+  const int ops_n = (MU || w != 1) ? 1 : 0;   // this wave's epilogue-operand load per item
+  int32_t cnt = 0;                           // vector-memory instructions issued (counted ones)
+  int32_t at0 = 0, at1 = 0, at2 = 0;         // cnt just after stage g's loads, slot g mod 3
+  // this wave's digit-stage pieces u = 0..5: piece q = w + 4u is half q & 1 of
+  // plane (q >> 1) of A (u < 3) or of B (plane (q >> 1) - 6): the plane and
+  // half offsets of the source and of the LDS image, fixed per wave
+  int64_t so[6];
+  int32_t ldo[6];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int q = w + 4 * u;        // 0..15: A pieces 0..7, B pieces 8..15
-        const bool isb = q >= 8;
-        const int qq = q & 7;
-        const int r = 8 * qq + (lane >> 3);
-        const int cch = (lane & 7) ^ (r & 7);   // the source chunk that lands at position lane & 7
-        const int8_t* src = isb ? bcat + ((int64_t)s2 * ldk + col0 + r) * 128 + cch * 16
-                                : acat + ((int64_t)s2 * npad + row0 + r) * 128 + cch * 16;
-        __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(st + (isb ? 8192 : 0) +
-                                                                                          qq * 1024),
-                                         16, 0, 0);
-      }
-    } else {
-      const int32_t kb = s2 - ncs;
-#pragma unroll
-      for (int u = 0; u < 6; ++u) {
-        const int q = w + 4 * u;        // 0..23: plane (q >> 1) of A (q < 12) or B, half q & 1
-        const int pl = (q >> 1) % I8_S, h = q & 1;
-        const int8_t* src = q < 12 ? Xd + pl * xplane + ((int64_t)kb * npad + row0) * 32 + h * 1024
-                                   : Ud + pl * uplane + ((int64_t)kb * ldk + col0) * 32 + h * 1024;
-        __builtin_amdgcn_global_load_lds(src + lane * 16,
-                                         (__attribute__((address_space(3))) void*)(st + (q >> 1) * Q_PL + h * 1024),
-                                         16, 0, 0);
-      }
-    }
-  };
-
-  auto issue_ops = [&](int32_t row0, int64_t col0, double* ops) {
-    if (lane < 32 && (MU || w != 1)) {   // the item's epilogue operands (512 B each)
-      const double* src = w == 0 ? xnorm + row0 : (w == 1 ? alpha + row0 : (w == 2 ? cnorm + col0 : scol + col0));
-      __builtin_amdgcn_global_load_lds(src + lane * 2, (__attribute__((address_space(3))) void*)(ops + w * Q_BM), 16,
-                                       0, 0);
-    }
-  };
-  // Items come from the per-XCD ticket; the next item's ticket is drawn when an
-  // item starts, and at the item's last stage its first stage and epilogue
-  // operands are issued (the ring slot and the operand buffer alternate), so
-  // their loads run under the current item's last MFMAs and epilogue.
-  if (t == 0) s_tk[0] = atomicAdd(&ticket[xcd], 1);
-  __syncthreads();
-  int32_t j = s_tk[0];
-  if ((j / RT) * 8 + xcd >= CT) return;   // (uniform)
-  int32_t row0 = (j % RT) * Q_BM;
-  int64_t col0 = (int64_t)((j / RT) * 8 + xcd) * Q_BN;
-  int slot = 0;
-  issue_stage(row0, col0, 0, lds);
-  issue_ops(row0, col0, ops0);
-  for (int it = 0;; ++it) {
-    if (t == 0) s_tk[(it + 1) & 1] = atomicAdd(&ticket[xcd], 1);
-    double* ops = ops0 + (it & 1) * OPS;
+  for (int u = 0; u < 6; ++u) {
+    const int q = w + 4 * u, h = q & 1;
+    so[u] = (int64_t)((q >> 1) % I8_S) * (u < 3 ? xplane : uplane) + h * 1024 + lane * 16;
+    ldo[u] = (q >> 1) * Q_PL + h * 1024;
+  }
+  // the issue cursor: stage is_ of item (row tile irt, column tile ict), ring
+  // slot isl, operand buffer iob; iok false past the last item
+  int32_t irt = b0 % RT, ictq = b0 / RT, is_ = 0, isl = 0, iob = 0;
+  bool iok = ictq * 8 + xcd < CT;
+#define UT_KQ_ISSUE()                                                                                            \
+  do {                                                                                                          \
+    if (iok) {                                                                                                  \
+      const int32_t r0_ = irt * Q_BM;                                                                            \
+      const int64_t c0_ = (int64_t)(ictq * 8 + xcd) * Q_BN;                                                      \
+      int8_t* st_ = lds + isl * Q_STAGE;                                                                         \
+      if (CAT && is_ < ncs) {                                                                                    \
+        q_issue_cat(acat, bcat, npad, ldk, w, lane, r0_, c0_, is_, st_);                                         \
+        cnt += 4;                                                                                               \
+      } else {                                                                                                  \
+        const int32_t kb_ = is_ - ncs;                                                                           \
+        const int8_t* ab_ = Xd + ((int64_t)kb_ * npad + r0_) * 32;                                              \
+        const int8_t* bb_ = Ud + ((int64_t)kb_ * ldk + c0_) * 32;                                               \
+        _Pragma("unroll") for (int u = 0; u < 6; ++u)                                                           \
+          __builtin_amdgcn_global_load_lds((u < 3 ? ab_ : bb_) + so[u],                                         \
+                                           (__attribute__((address_space(3))) void*)(st_ + ldo[u]), 16, 0, 0);  \
+        cnt += 6;                                                                                               \
+      }                                                                                                         \
+      if (is_ == 0) {                                                                                           \
+        q_issue_ops<MU>(xnorm, alpha, cnorm, scol, w, lane, r0_, c0_, ops0 + iob * OPS);                        \
+        cnt += ops_n;                                                                                           \
+      }                                                                                                         \
+      if (isl == 0) at0 = cnt;                                                                                  \
+      else if (isl == 1) at1 = cnt;                                                                             \
+      else at2 = cnt;                                                                                           \
+      isl = isl == 2 ? 0 : isl + 1;                                                                             \
+      if (++is_ == ntot) {                                                                                      \
+        is_ = 0;                                                                                                \
+        iob = iob == 2 ? 0 : iob + 1;                                                                           \
+        irt += Wr;                                                                                              \
+        ictq += Wq;                                                                                             \
+        if (irt >= RT) {                                                                                        \
+          irt -= RT;                                                                                            \
+          ++ictq;                                                                                               \
+        }                                                                                                       \
+        iok = ictq * 8 + xcd < CT;                                                                              \
+      }                                                                                                         \
+    }                                                                                                           \
+  } while (0)
+  __syncthreads();   // (the exp table)
+  if (!iok) return;   // (uniform: no item)
+  UT_KQ_ISSUE();
+  UT_KQ_ISSUE();
+  // the consumer: item (row tile crt, column tile cctq), stage slot csl, operand buffer cob
+  int32_t crt = b0 % RT, cctq = b0 / RT, csl = 0, cob = 0;
+  for (;;) {
+    const int32_t row0 = crt * Q_BM;
+    const int64_t col0 = (int64_t)(cctq * 8 + xcd) * Q_BN;
+    double* ops = ops0 + cob * OPS;
     double* rx = ops;
     double* ra = ops + Q_BM;
     double* cn = ops + 2 * Q_BM;
     double* cs = cn + Q_BN;
-    const int32_t rt = row0 / Q_BM;
-    bool nvalid = false;
-    int32_t nrow0 = 0;
-    int64_t ncol0 = 0;
-    // after stage s2's barrier: the next stage of this item, or the next item's first
-    auto issue_next = [&](int32_t s2) {
-      int8_t* st = lds + (slot ^ 1) * Q_STAGE;
-      if (s2 + 1 < ntot) {
-        issue_stage(row0, col0, s2 + 1, st);
-        return;
-      }
-      const int32_t jn = s_tk[(it + 1) & 1];
-      const int32_t nct = (jn / RT) * 8 + xcd;
-      nvalid = nct < CT;
-      if (nvalid) {
-        nrow0 = (jn % RT) * Q_BM;
-        ncol0 = (int64_t)nct * Q_BN;
-        issue_stage(nrow0, ncol0, 0, st);
-        issue_ops(nrow0, ncol0, ops0 + ((it + 1) & 1) * OPS);
-      }
-    };
+    const int32_t rt = crt;
     i8v16 acc[I8_S], iacc;
     if (K32 == 0) {
 #pragma unroll
@@ -250,14 +309,30 @@ __global__ __launch_bounds__(Q_NT, 2) void k_gp_kstar_q(
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[g][r] = 0;
     }
+    // the epilogue operands in place, once they landed (after the item's first
+    // stage barrier; the next barrier publishes them): row / column half-norms
+    // with the padding's -1e300 (its k* is then exactly 0), alpha / kscale
+#define UT_KQ_OPS_IN()                                                 \
+  if (t < Q_BM) {                                                      \
+    const double hv = (-0.5 * KSTAR_T_SCALE) * rx[t];                  \
+    rx[t] = row0 + t < n ? hv : -1e300;                                \
+    if (MU) ra[t] = ra[t] * ikscale;                                   \
+  } else if (t < Q_BM + Q_BN) {                                        \
+    const int u = t - Q_BM;                                            \
+    const double hv = (-0.5 * KSTAR_T_SCALE) * cn[u];                  \
+    cn[u] = col0 + u < m ? hv : -1e300;                                \
+  }
     // the categorical stages first (the match count), then the digit stages
+#define UT_KQ_STAGE_IN()                                                                               \
+  vm_wait_n(cnt - (csl == 0 ? at0 : (csl == 1 ? at1 : at2)));   /* this stage (+ the item's operands) */ \
+  __builtin_amdgcn_s_barrier();   /* ... landed in every wave; the slot two ahead fully read */       \
+  asm volatile("" ::: "memory");                                                                      \
+  UT_KQ_ISSUE();                                                                                      \
+  const int8_t* st = lds + csl * Q_STAGE;                                                             \
+  csl = csl == 2 ? 0 : csl + 1
     for (int32_t s2 = 0; s2 < ncs; ++s2) {
-      i8_vm_wait<0>();
-      __builtin_amdgcn_s_barrier();   // stage s2 landed everywhere; the other slot fully read
-      asm volatile("" ::: "memory");
-      issue_next(s2);
-      const int8_t* st = lds + slot * Q_STAGE;
-      slot ^= 1;
+      UT_KQ_STAGE_IN();
+      if (s2 == 0) UT_KQ_OPS_IN();
       // four 32-code steps (the first stage's first from zero)
       auto cbody = [&](auto first_c) {
         constexpr bool FIRST = decltype(first_c)::value;
@@ -273,12 +348,8 @@ __global__ __launch_bounds__(Q_NT, 2) void k_gp_kstar_q(
       else cbody(std::integral_constant<bool, false>{});
     }
     for (int32_t s2 = ncs; s2 < ntot; ++s2) {
-      i8_vm_wait<0>();
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-      issue_next(s2);
-      const int8_t* st = lds + slot * Q_STAGE;
-      slot ^= 1;
+      UT_KQ_STAGE_IN();
+      if (s2 == 0) UT_KQ_OPS_IN();
       i8v4 af[I8_S];
 #pragma unroll
       for (int p = 0; p < I8_S; ++p) af[p] = *reinterpret_cast<const i8v4*>(st + p * Q_PL + aoff);
@@ -299,18 +370,14 @@ __global__ __launch_bounds__(Q_NT, 2) void k_gp_kstar_q(
       if (s2 == ncs) body(std::integral_constant<bool, true>{});
       else body(std::integral_constant<bool, false>{});
     }
-    // the epilogue operands in place: row / column half-norms with the padding's
-    // -1e300 (its k* is then exactly 0), alpha / kscale
-    if (t < Q_BM) {
-      const double hv = (-0.5 * KSTAR_T_SCALE) * rx[t];
-      rx[t] = row0 + t < n ? hv : -1e300;
-      if (MU) ra[t] = ra[t] * ikscale;
-    } else if (t < Q_BM + Q_BN) {
-      const int u = t - Q_BM;
-      const double hv = (-0.5 * KSTAR_T_SCALE) * cn[u];
-      cn[u] = col0 + u < m ? hv : -1e300;
+#undef UT_KQ_STAGE_IN
+#undef UT_KQ_OPS_IN
+#undef UT_KQ_ISSUE
+    if (ntot == 1) {   // (no stage barrier after the first: publish the operands)
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
     }
-    __syncthreads();
     // lane: column cb of the tile, rows wm*32 + (q & 3) + 8 (q >> 2) + 4 (l >> 5)
     const double hc = cn[cb], sc = cs[cb];
     const int64_t col = col0 + cb;
@@ -369,21 +436,26 @@ __global__ __launch_bounds__(Q_NT, 2) void k_gp_kstar_q(
       }
     }
     if constexpr (MU) {
+      // each wave's 32 rows: one partial per 32-row half tile (no cross-wave
+      // reduction, so no barrier; the scoring sums npad / 32 partials)
       s += __shfl_xor(s, 32);
       if (want2) s2v += __shfl_xor(s2v, 32);
-      if (lane < 32) {
-        red[wm * Q_BN + cb] = s;
-        if (want2) red[2 * Q_BN + wm * Q_BN + cb] = s2v;
-      }
-      __syncthreads();
-      if (t < Q_BN && col0 + t < m) {
-        part[(int64_t)rt * ldk + col0 + t] = red[t] + red[Q_BN + t];
-        if (want2) part2[(int64_t)rt * ldk + col0 + t] = red[2 * Q_BN + t] + red[3 * Q_BN + t];
+      if (lane < 32 && col < m) {
+        const int64_t o = (int64_t)(2 * rt + wm) * ldk + col;
+        part[o] = s;
+        if (want2) part2[o] = s2v;
       }
     }
-    if (!nvalid) break;   // (uniform: every thread read the same ticket)
-    row0 = nrow0;
-    col0 = ncol0;
+    if constexpr (I8) cnt += I8_S;   // the plane stores
+    else if (store) cnt += 16;        // the rows' stores
+    cob = cob == 2 ? 0 : cob + 1;
+    crt += Wr;
+    cctq += Wq;
+    if (crt >= RT) {
+      crt -= RT;
+      ++cctq;
+    }
+    if (cctq * 8 + xcd >= CT) break;   // (uniform: no next item)
   }
 }
 
@@ -441,14 +513,13 @@ int launch_gemm_kstar_q(ut_ctx* c, bool planes, const double* XsT, int32_t npad,
   const int32_t spare = fit_in_flight ? 2 : 0;   // as launch_gemm_kstar
   int32_t nb = 2 * (c->n_cu / 8 - spare) * 8;
   if (items < nb) nb = (int32_t)(((items + 7) / 8) * 8);
-  UT_HIP(c, hipMemsetAsync(c->gp_ctr + 8, 0, sizeof(int32_t) * 8, c->stream));
   const double* xnorm = xn ? xn : c->gp_xnorm;
   const double* cnorm = cn ? cn : c->cnorm.p;
   const double kscale = planes ? ldexp(1.0, -i8_kstar_exp(c->gp_sf2)) : 1.0;
 #define UT_KQ_LAUNCH(TS, MU, CAT, PAIR, PART)                                                                     \
   hipLaunchKernelGGL((k_gp_kstar_q<TS, MU, CAT, PAIR>), dim3(nb), dim3(Q_NT), 0, c->stream, xd.p, npad, u8.p, ldk, \
-                     K32, scol.p, RT, CT, xnorm, cnorm, c->gp_alpha, c->gp_sf2, c->gp_n, m, c->gp_ctr + 8,         \
-                     (TS*)kst, PART, kscale, (int64_t)npad * ldk, store_rt, part2, cat.acat, cat.bcat, cat.nkc,    \
+                     K32, scol.p, RT, CT, xnorm, cnorm, c->gp_alpha, c->gp_sf2, c->gp_n, m, (TS*)kst, PART,         \
+                     kscale, (int64_t)npad * ldk, store_rt, part2, cat.acat, cat.bcat, cat.nkc,    \
                      cat.c0 * KSTAR_T_SCALE, cat.c1 * KSTAR_T_SCALE)
 #define UT_KQ_CAT(TS, MU, PAIR, PART)                    \
   do {                                                   \

@@ -1025,11 +1025,6 @@ static int fit_device(ut_ctx* c, int part, int32_t n, int32_t n0, int32_t d, int
                          dX, n, d, npad, c->gp_acat.p);
       UT_LAUNCH_CHECK(c);
     }
-    // precision 8: K*'s training operand as int8 digit planes (gp_kq.hip)
-    if (c->gp_prec == 8) {
-      if ((rc = launch_split_x8(c, c->gp_XsT, kstar_dpad(d), npad, false))) return rc;
-      if (c->cat_on && (rc = launch_split_x8(c, c->gp_XsT_num.p, dpn, npad, true))) return rc;
-    }
     return 0;
   }
   if (app) {
@@ -1140,8 +1135,7 @@ static std::vector<uint64_t> fit_signature(const ut_ctx* c, int32_t n, int32_t n
                         (const void*)c->gp_alpha, (const void*)c->gp_LinvT, (const void*)c->gp_LinvT_f,
                         (const void*)c->gp_Xs_f, (const void*)c->gp_ctr, (const void*)c->app_ws.p,
                         (const void*)c->gp_XsT_num.p, (const void*)c->gp_xnorm_num.p, (const void*)c->gp_acat.p,
-                        (const void*)c->gp_i8a.p, (const void*)c->gp_i8rs.p, (const void*)c->gp_x8.p,
-                        (const void*)c->gp_x8n.p, (const void*)c->gp_q8.p, (const void*)sp.d_params,
+                        (const void*)c->gp_i8a.p, (const void*)c->gp_i8rs.p, (const void*)sp.d_params,
                         (const void*)sp.d_cat_ccol, (const void*)sp.d_num_feat})
     k.push_back((uint64_t)(uintptr_t)p);
   return k;
@@ -1251,8 +1245,6 @@ int gp_fit_enqueue(ut_ctx* c, const double* X, const double* y, int32_t n, int32
   if (c->gp_prec == 8) {
     if ((rc = alloc_split_i8(c, npad))) return rc;
     c->gp_i8_eb = i8_kstar_exp(h->sigma_f2);
-    if ((rc = alloc_split_x8(c, npad, kstar_dpad(d), false))) return rc;
-    if (c->cat_on && (rc = alloc_split_x8(c, npad, dpn, true))) return rc;
   }
   UT_HIP(c, hipEventRecord(c->ev_prefit, c->stream));
   UT_HIP(c, hipStreamWaitEvent(c->fit_stream, c->ev_prefit, 0));
@@ -1392,11 +1384,9 @@ int gp_score_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, const ut
   // full 256-candidate strips (the K* kernel writes zeros past m)
   const int64_t ldk = ((m + VAR_BN - 1) / VAR_BN) * VAR_BN;
   const int32_t RT = npad / NPAD;
-  // (i8: the mean partials come per 64-row tile, gp_kq.hip)
-  const int32_t RTm = i8 ? 2 * RT : RT;
   int rc;
   if ((rc = ensure(c, c->kst, (size_t)npad * ldk))) return rc;
-  if ((rc = ensure(c, c->mu_part, (size_t)RTm * ldk))) return rc;
+  if ((rc = ensure(c, c->mu_part, (size_t)RT * ldk))) return rc;
   // (i8: the variance partials come per 64-row tile)
   if ((rc = ensure(c, c->var_part, (size_t)(i8 ? 2 * RT : RT) * ldk))) return rc;
   if ((rc = ensure(c, c->cnorm, (size_t)ldk))) return rc;
@@ -1435,7 +1425,7 @@ int gp_score_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, const ut
   if (i8) {
     // the bound test, then the fp64 recompute of the candidates it did not clear
     UT_HIP(c, hipMemsetAsync(c->pr_count.p, 0, sizeof(int64_t), c->stream));
-    hipLaunchKernelGGL(k_gp_finalize_i8, dim3(grid1(m, 256)), dim3(256), 0, c->stream, m, RTm, 2 * RT, c->mu_part.p,
+    hipLaunchKernelGGL(k_gp_finalize_i8, dim3(grid1(m, 256)), dim3(256), 0, c->stream, m, RT, 2 * RT, c->mu_part.p,
                        c->var_part.p, ldk, c->gp_sf2, c->gp_stats, c->gp_flag, acq->kind, acq->xi, acq->kappa, dup,
                        mu, var, score, c->gp_i8rs.p + 2 * npad, c->i8_tol, n, c->pr_idx.p,
                        reinterpret_cast<unsigned long long*>(c->pr_count.p));
@@ -1457,7 +1447,7 @@ int gp_score_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, const ut
       if ((rc = launch_gemm_var(c, 64, c->gp_LinvT, npad, c->kst.p, ldk, npad, m, c->var_part.p, c->gp_beta,
                                 c->pr_mpart.p)))
         return rc;
-      hipLaunchKernelGGL(k_gp_finalize, dim3(grid1(m, 256)), dim3(256), 0, c->stream, m, RTm, RT, c->mu_part.p,
+      hipLaunchKernelGGL(k_gp_finalize, dim3(grid1(m, 256)), dim3(256), 0, c->stream, m, RT, RT, c->mu_part.p,
                          c->var_part.p, ldk, c->gp_sf2, c->gp_stats, c->gp_flag, acq->kind, acq->xi, acq->kappa, dup,
                          mu, var, score);
       UT_LAUNCH_CHECK(c);
@@ -1468,7 +1458,7 @@ int gp_score_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, const ut
       if ((rc = launch_gemm_var(c, 64, c->gp_LinvT, npad, c->pr_kst.p, ldf, npad, nf, c->pr_vpart.p, c->gp_beta,
                                 c->pr_mpart.p)))
         return rc;
-      hipLaunchKernelGGL(k_gp_fix_i8, dim3(grid1(nf, 256)), dim3(256), 0, c->stream, nf, c->pr_idx.p, RTm,
+      hipLaunchKernelGGL(k_gp_fix_i8, dim3(grid1(nf, 256)), dim3(256), 0, c->stream, nf, c->pr_idx.p, RT,
                          c->mu_part.p, ldk, RT, c->pr_vpart.p, ldf, c->gp_sf2, c->gp_stats, acq->kind, acq->xi,
                          acq->kappa, dup, var, score);
       UT_LAUNCH_CHECK(c);
@@ -1516,7 +1506,7 @@ __global__ void k_prune_bound(int64_t m, int32_t RTm, const double* __restrict__
                               const double* __restrict__ stats, const int32_t* __restrict__ fit_flag, int32_t kind,
                               double xi, double kappa, const uint8_t* __restrict__ dup, double* __restrict__ mu_out,
                               double* __restrict__ ub_out, const double* __restrict__ k2_part,
-                              const double* __restrict__ linv_f2, uint8_t* __restrict__ exact_out, int32_t covered) {
+                              const double* __restrict__ linv_f2, uint8_t* __restrict__ exact_out) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= m) return;
   double mu = 0.0, vs = 0.0, k2 = 0.0;
@@ -1526,14 +1516,14 @@ __global__ void k_prune_bound(int64_t m, int32_t RTm, const double* __restrict__
   var = var > 0.0 ? var : 0.0;
   double ub = acq_score(kind, mu, var, stats[0], xi, kappa);
   bool exact = false;
-  if (k2_part && !covered) {
+  if (k2_part && RTv < RTm) {
     for (int32_t r = 0; r < RTm; ++r) k2 += k2_part[(int64_t)r * ldp + i];
     const double tail = 1.001 * (*linv_f2) * k2;
     const double s_hi = (vs + tail) * (1.0 + 0x1p-40);
     double var_lo = sf2 - s_hi;
     var_lo = var_lo > 0.0 ? var_lo : 0.0;
     exact = tail == tail && var_lo == var;   // (NaN tail: not exact)
-  } else if (covered) {
+  } else if (RTv >= RTm) {
     exact = true;   // the bound GEMM covered every row
   }
   if (!exact) ub = ub + fabs(ub) * 1e-12 + 1e-300;
@@ -1694,8 +1684,7 @@ int gp_topk_pruned_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, co
                         int64_t cand_base, int32_t k, int32_t bound_rows, int64_t* out_idx, double* out_score,
                         ut_prune_stats* stats, hipEvent_t dup_ready, bool feat_ours) {
   UT_CHECK(c, c->gp_ready, UT_EINVAL, "gp_topk_pruned: call ut_gp_fit first");
-  UT_CHECK(c, c->gp_fit_prec == 64 || c->gp_fit_prec == 8, UT_EINVAL,
-           "gp_topk_pruned: needs an fp64-tier fit (ut_gp_set_precision 64 or 8)");
+  UT_CHECK(c, c->gp_fit_prec == 64, UT_EINVAL, "gp_topk_pruned: needs an fp64 fit (ut_gp_set_precision 64)");
   UT_CHECK(c, acq->kind == UT_ACQ_EI || (acq->kind == UT_ACQ_UCB && acq->kappa >= 0.0), UT_EINVAL,
            "gp_topk_pruned: the score must increase with sigma (EI, or UCB with kappa >= 0)");
   UT_CHECK(c, k >= 1 && k <= 1024, UT_EINVAL, "gp_topk_pruned: k must be in [1, 1024]");
@@ -1709,14 +1698,12 @@ int gp_topk_pruned_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, co
   const bool cat = feat_ours && c->cat_on;   // the categorical K* (features from ut's encoder)
   const int32_t dpad = cat ? cat_dpad(c) : kstar_dpad(d);
   const int32_t RT = npad / NPAD;
-  // (precision 8: K*'s mean and sum k*^2 partials come per 64-row tile, gp_kq.hip)
-  const int32_t RTm = c->gp_fit_prec == 8 ? 2 * RT : RT;
   int32_t R = (bound_rows + NPAD - 1) / NPAD;
   R = R < 1 ? 1 : (R > RT ? RT : R);
   const int64_t ldk = ((m + VAR_BN - 1) / VAR_BN) * VAR_BN;
   int rc;
   if ((rc = ensure(c, c->kst, (size_t)npad * ldk))) return rc;
-  if ((rc = ensure(c, c->mu_part, (size_t)RTm * ldk))) return rc;
+  if ((rc = ensure(c, c->mu_part, (size_t)RT * ldk))) return rc;
   if ((rc = ensure(c, c->var_part, (size_t)RT * ldk))) return rc;
   if ((rc = ensure(c, c->pr_mpart, (size_t)RT * ldk))) return rc;
   if ((rc = ensure(c, c->cnorm, (size_t)ldk))) return rc;
@@ -1727,7 +1714,7 @@ int gp_topk_pruned_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, co
   if ((rc = ensure(c, c->pr_score, (size_t)ldk + 2048))) return rc;   // + the threshold set's two [1024] arrays
   if ((rc = ensure(c, c->pr_idx, (size_t)ldk + 2048))) return rc;
   if ((rc = ensure(c, c->pr_count, 1))) return rc;
-  if ((rc = ensure(c, c->pr_k2, (size_t)RTm * ldk))) return rc;
+  if ((rc = ensure(c, c->pr_k2, (size_t)RT * ldk))) return rc;
   if ((rc = ensure(c, c->pr_f2, 1 + SQ_BLOCKS))) return rc;   // [0] the norm, [1..] block partials
   if ((rc = ensure(c, c->pr_exact, (size_t)ldk))) return rc;
   const double* LinvT = c->gp_LinvT;
@@ -1764,9 +1751,9 @@ int gp_topk_pruned_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, co
     return rc;
   mark(c, "bound");
   if (dup_ready) UT_HIP(c, hipStreamWaitEvent(c->stream, dup_ready, 0));   // the dup mask (side stream)
-  hipLaunchKernelGGL(k_prune_bound, dim3(grid1(m, 256)), dim3(256), 0, c->stream, m, RTm, c->mu_part.p, R,
+  hipLaunchKernelGGL(k_prune_bound, dim3(grid1(m, 256)), dim3(256), 0, c->stream, m, RT, c->mu_part.p, R,
                      c->var_part.p, ldk, c->gp_sf2, c->gp_stats, c->gp_flag, acq->kind, acq->xi, acq->kappa, dup,
-                     c->pr_mu.p, c->pr_ub.p, c->pr_k2.p, c->pr_f2.p, c->pr_exact.p, (int32_t)(R == RT));
+                     c->pr_mu.p, c->pr_ub.p, c->pr_k2.p, c->pr_f2.p, c->pr_exact.p);
   UT_LAUNCH_CHECK(c);
   // 3. threshold: exact scores of the best 1024 bounds, tau = their k-th best
   const int32_t kp = (int32_t)(m < 1024 ? m : 1024);
@@ -1811,7 +1798,7 @@ int gp_topk_pruned_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, co
     if ((rc = launch_gemm_var(c, 64, LinvT, npad, c->kst.p, ldk, npad, m, c->var_part.p, c->gp_beta,
                               c->pr_mpart.p)))
       return rc;
-    hipLaunchKernelGGL(k_gp_finalize, dim3(grid1(m, 256)), dim3(256), 0, c->stream, m, RTm, RT, c->mu_part.p,
+    hipLaunchKernelGGL(k_gp_finalize, dim3(grid1(m, 256)), dim3(256), 0, c->stream, m, RT, RT, c->mu_part.p,
                        c->var_part.p, ldk, c->gp_sf2, c->gp_stats, c->gp_flag, acq->kind, acq->xi, acq->kappa, dup,
                        nullptr, nullptr, c->pr_score.p);
     UT_LAUNCH_CHECK(c);

@@ -38,8 +38,17 @@
 
 namespace ut {
 
+typedef int32_t i8v4 __attribute__((ext_vector_type(4)));
+typedef int32_t i8v16 __attribute__((ext_vector_type(16)));
+
 constexpr int I8_PL = I8_BM * I8_BK;   // one plane's piece of a stage: 64 rows x 32 k = 2 KiB
 constexpr double I8_C = 3.5 * 0x1p-49;
+
+template <int N>
+__device__ __forceinline__ void i8_vm_wait() {
+  static_assert(N >= 0 && N < 64, "vmcnt");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+}
 
 // ---------------------------------------------------------------------------
 // fit side: L^-1 -> digit planes, row scales 2^(ea_i + eb), e_i^2
