@@ -450,8 +450,9 @@ __global__ __launch_bounds__(K_NT, 2) void k_gp_kstar(const double* __restrict__
               const double x = __builtin_fmax(__builtin_fmin((acc[i][jj][r] + hx) + hc[jj], 0.0), KSTAR_T_MIN);
               const double ks = sf2_exp2t_nonpos(x, etab);
               if constexpr (STORE) kp[jj * 16] = (TS)ks;
-              if constexpr (MU) s[jj] += al * ks;
-              if constexpr (MU) s2[jj] += ks * ks;
+              // (fused: the build contracts nothing by itself)
+              if constexpr (MU) s[jj] = __builtin_fma(al, ks, s[jj]);
+              if constexpr (MU) s2[jj] = __builtin_fma(ks, ks, s2[jj]);
             }
           }
         }
