@@ -324,12 +324,6 @@ int ut_gp_set_i8_tol(ut_ctx* ctx, double tol);
  * (-1: most were, and the whole round ran the fp64 contraction), and the
  * current fit's bound E on |L^-1 k* - v^| */
 int ut_gp_i8_stats(ut_ctx* ctx, int64_t* recomputed_host, double* bound_host);
-/* fits so far whose device work was launched kernel by kernel / captured into
- * a graph / replayed from it.  A fit whose shapes, path, hyperparameters and
- * buffers repeat the previous fit's is captured, and replayed while that holds
- * (the staged X and y are read at replay); UT_FIT_GRAPH=0 disables graphs.
- * Any argument may be NULL. */
-int ut_gp_fit_graph_stats(ut_ctx* ctx, int64_t* direct_host, int64_t* captured_host, int64_t* replayed_host);
 /* order everything enqueued on ctx's stream after this call behind the
  * in-flight fit (a stream wait on its event; no host wait).  Scoring that
  * needs the whole fit (pruned, fp32, f16x3) then starts with the fit done, and

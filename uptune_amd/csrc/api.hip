@@ -241,7 +241,6 @@ int ut_ctx_create(int device, uint64_t seed, ut_ctx** out) {
   if (const char* e = getenv("UT_CHOL_FUSE")) c->chol_fuse = atoi(e);
   if (const char* e = getenv("UT_TRINV_BIG")) c->trinv_big = atoi(e);
   if (const char* e = getenv("UT_CHOL_MERGED")) c->chol_merged = atoi(e);
-  if (const char* e = getenv("UT_FIT_GRAPH")) c->fit_graph = atoi(e) != 0;
   // the fit kernels' waves at s_setprio 3 (gp.hip g_fit_prio): beside the
   // round's hash grid their instructions go first
   if (ut::set_fit_prio(1)) {
@@ -288,8 +287,6 @@ int ut_ctx_destroy(ut_ctx* c) {
   fr(c->forest_nodes); fr(c->forest_roots); fr(c->r_topk_vals.p);
   fr(c->cm_send.p); fr(c->cm_recv.p); fr(c->cm_keep.p); fr(c->cm_pay.p); fr(c->cm_cnt.p);
   for (auto& m : c->timing.marks) hipEventDestroy(m.ev);
-  for (hipGraphExec_t g : c->fit_exec)
-    if (g) hipGraphExecDestroy(g);
   for (hipEvent_t e : {c->ev_fork, c->ev_join, c->ev_fit, c->ev_prefit, c->ev_fit_x})
     if (e) hipEventDestroy(e);
   if (c->fit_host) hipHostFree(c->fit_host);
@@ -823,14 +820,6 @@ int ut_gp_i8_stats(ut_ctx* c, int64_t* recomputed, double* bound) {
       UT_HIP(c, hipMemcpy(bound, c->gp_i8rs.p + 2 * (int64_t)c->gp_npad_fit, sizeof(double), hipMemcpyDeviceToHost));
     }
   }
-  return 0;
-}
-
-int ut_gp_fit_graph_stats(ut_ctx* c, int64_t* direct, int64_t* captured, int64_t* replayed) {
-  if (!c) return UT_EINVAL;
-  if (direct) *direct = c->fit_graph_stats[0];
-  if (captured) *captured = c->fit_graph_stats[1];
-  if (replayed) *replayed = c->fit_graph_stats[2];
   return 0;
 }
 

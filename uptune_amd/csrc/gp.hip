@@ -995,8 +995,7 @@ static bool cat_rows_ok(const Space& s, const double* X, int32_t d, int32_t r0, 
 // ev_fit_x: part 0 the staging copies from the pinned host buffer and the
 // scaled inputs; part 1 the factor and L^-1 (a refit, or block rows appended
 // to the previous factor), beta / alpha, and the scoring precision's
-// operands.  Enqueues only: every buffer is allocated by the caller, so each
-// part can be captured into a graph.
+// operands.  Enqueues only: every buffer is allocated by the caller.
 static int fit_device(ut_ctx* c, int part, int32_t n, int32_t n0, int32_t d, int32_t npad, int32_t dpn, bool app,
                       int32_t xr0, double diag, double sf2) {
   int rc;
@@ -1116,31 +1115,6 @@ static int fit_device(ut_ctx* c, int part, int32_t n, int32_t n0, int32_t d, int
   return 0;
 }
 
-// what a captured fit depends on besides the staged data: shapes, path,
-// scalar kernel arguments, configuration, and every buffer address
-static std::vector<uint64_t> fit_signature(const ut_ctx* c, int32_t n, int32_t n0, int32_t d, int32_t npad,
-                                           int32_t dpn, bool app, int32_t xr0, double diag) {
-  uint64_t sf2b, diagb;
-  std::memcpy(&sf2b, &c->gp_sf2, 8);
-  std::memcpy(&diagb, &diag, 8);
-  const Space& sp = c->space;
-  std::vector<uint64_t> k = {
-      (uint64_t)n, (uint64_t)(app ? n0 : -1), (uint64_t)d, (uint64_t)npad, (uint64_t)dpn, (uint64_t)app, (uint64_t)xr0, sf2b, diagb,
-      (uint64_t)c->gp_prec, (uint64_t)c->gp_i8_eb, (uint64_t)c->cat_on, (uint64_t)sp.cat_k, (uint64_t)sp.P,
-      (uint64_t)sp.n_num, (uint64_t)(int64_t)c->chol_fuse, (uint64_t)c->trinv_big, (uint64_t)c->chol_merged};
-  for (const void* p : {(const void*)c->fit_host, (const void*)c->gp_tmp, (const void*)c->gp_inv_ell,
-                        (const void*)c->gp_Xs, (const void*)c->gp_xnorm, (const void*)c->gp_XsT, (const void*)c->gp_K,
-                        (const void*)c->gp_Linv, (const void*)c->gp_T, (const void*)c->gp_y,
-                        (const void*)c->gp_stats, (const void*)c->gp_flag, (const void*)c->gp_beta,
-                        (const void*)c->gp_alpha, (const void*)c->gp_LinvT, (const void*)c->gp_LinvT_f,
-                        (const void*)c->gp_Xs_f, (const void*)c->gp_ctr, (const void*)c->app_ws.p,
-                        (const void*)c->gp_XsT_num.p, (const void*)c->gp_xnorm_num.p, (const void*)c->gp_acat.p,
-                        (const void*)c->gp_i8a.p, (const void*)c->gp_i8rs.p, (const void*)sp.d_params,
-                        (const void*)sp.d_cat_ccol, (const void*)sp.d_num_feat})
-    k.push_back((uint64_t)(uintptr_t)p);
-  return k;
-}
-
 // Enqueue a fit on the fit stream, ordered after everything already enqueued
 // on the caller's stream (earlier rounds read the GP state being replaced).
 // Scoring waits on ev_fit; failure (not positive definite) is reported by
@@ -1228,8 +1202,7 @@ int gp_fit_enqueue(ut_ctx* c, const double* X, const double* y, int32_t n, int32
     c->cat_c0 = -0.5 * base * (double)pw;
   }
   const double diag = h->sigma_n2 + h->jitter;
-  // every buffer the device work touches exists before it is enqueued (a
-  // captured graph may hold no allocation, and its pointers must stay valid)
+  // every buffer the device work touches exists before it is enqueued
   const int32_t dpn = cat_dpad(c);
   if (c->cat_on) {
     if ((rc = ensure(c, c->gp_XsT_num, (size_t)(dpn > 0 ? dpn : 1) * npad))) return rc;
@@ -1251,51 +1224,9 @@ int gp_fit_enqueue(ut_ctx* c, const double* X, const double* y, int32_t n, int32
   StreamScope on_fit(c, c->fit_stream);
   c->gp_n = n;
   c->gp_sf2 = h->sigma_f2;
-  // The fit is a chain of ~70 (n = 1024) to ~200 (n = 4096) small launches
-  // whose host enqueue delays everything the caller enqueues after it.  A fit
-  // whose signature -- shapes, path, scalar arguments and every buffer address
-  // -- repeats the previous one's (the bench refits the same set every round;
-  // a tuning loop refits at a fixed size) is captured once into a hipGraph and
-  // replayed with one launch; the graph's copies read the pinned staging at
-  // replay time, so the new X / y land as before.
-  // (two graphs, split at ev_fit_x: fp64 K* starts on the scaled inputs while
-  // the factor runs, and an event recorded outside a graph is the portable way
-  // for another stream to wait on a point inside the fit)
-  std::vector<uint64_t> key;
-  if (c->fit_graph) key = fit_signature(c, n, n0, d, npad, dpn, app, xr0, diag);
-  const bool replay = c->fit_graph && c->fit_exec[0] && c->fit_exec[1] && key == c->fit_key;
-  const bool capture = c->fit_graph && !replay && key == c->fit_last;
-  if (capture) c->fit_key.clear();
-  for (int part = 0; part < 2; ++part) {
-    if (part == 1) UT_HIP(c, hipEventRecord(c->ev_fit_x, c->stream));
-    if (replay) {
-      UT_HIP(c, hipGraphLaunch(c->fit_exec[part], c->stream));
-      continue;
-    }
-    if (!capture) {
-      if ((rc = fit_device(c, part, n, n0, d, npad, dpn, app, xr0, diag, h->sigma_f2))) return rc;
-      continue;
-    }
-    hipGraph_t g = nullptr;
-    UT_HIP(c, hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
-    rc = fit_device(c, part, n, n0, d, npad, dpn, app, xr0, diag, h->sigma_f2);
-    const hipError_t ec = hipStreamEndCapture(c->stream, &g);
-    if (rc) {
-      if (g) hipGraphDestroy(g);
-      return rc;
-    }
-    if (ec != hipSuccess) return set_err(c, UT_EHIP, std::string("gp_fit: capture: ") + hipGetErrorString(ec));
-    hipGraphExec_t ge = nullptr;
-    const hipError_t ei = hipGraphInstantiate(&ge, g, nullptr, nullptr, 0);
-    hipGraphDestroy(g);
-    if (ei != hipSuccess) return set_err(c, UT_EHIP, std::string("gp_fit: graph: ") + hipGetErrorString(ei));
-    if (c->fit_exec[part]) hipGraphExecDestroy(c->fit_exec[part]);
-    c->fit_exec[part] = ge;
-    UT_HIP(c, hipGraphLaunch(ge, c->stream));
-  }
-  if (capture) c->fit_key = key;
-  if (c->fit_graph) c->fit_last = key;
-  c->fit_graph_stats[replay ? 2 : capture ? 1 : 0] += 1;
+  if ((rc = fit_device(c, 0, n, n0, d, npad, dpn, app, xr0, diag, h->sigma_f2))) return rc;
+  UT_HIP(c, hipEventRecord(c->ev_fit_x, c->stream));   // the scaled inputs: fp64 K* may start
+  if ((rc = fit_device(c, 1, n, n0, d, npad, dpn, app, xr0, diag, h->sigma_f2))) return rc;
   c->gp_fit_prec = c->gp_prec;
   c->gp_npad_fit = npad;
   c->gp_diag_fit = diag;

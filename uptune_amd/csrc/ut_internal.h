@@ -138,12 +138,6 @@ struct ut_ctx {
   hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_fit = nullptr, ev_prefit = nullptr;
   hipEvent_t ev_fit_x = nullptr;     // fit stream: scaled training inputs ready (K* may start)
   bool fit_pending = false;          // scoring waits on ev_fit before touching GP state
-  // the fit's device work as two captured graphs (gp_fit_enqueue): captured
-  // when a fit's signature repeats the previous one's, replayed while it does
-  bool fit_graph = true;                       // UT_FIT_GRAPH=0: always launch directly
-  hipGraphExec_t fit_exec[2] = {nullptr, nullptr};
-  std::vector<uint64_t> fit_key, fit_last;     // signature of the graphs / of the previous fit
-  int64_t fit_graph_stats[3] = {0, 0, 0};      // fits launched directly / captured / replayed
   // fp64 variance with few candidate strips: 1 = split the k loops
   // (k_gp_var_pp<true> + k_var_split_red), 0 = one item per row tile; UT_VAR_SPLIT
   int32_t var_split = 1;

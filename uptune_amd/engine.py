@@ -297,13 +297,6 @@ class BatchEngine:
         L.check(self.ctx, self.lib.ut_gp_i8_stats(self.ctx, C.byref(n), C.byref(e)), "ut_gp_i8_stats")
         return int(n.value), float(e.value)
 
-    def gp_fit_graph_stats(self) -> Tuple[int, int, int]:
-        """fits launched (directly, captured into a graph, replayed from it)"""
-        a, b, r = C.c_int64(), C.c_int64(), C.c_int64()
-        L.check(self.ctx, self.lib.ut_gp_fit_graph_stats(self.ctx, C.byref(a), C.byref(b), C.byref(r)),
-                "ut_gp_fit_graph_stats")
-        return int(a.value), int(b.value), int(r.value)
-
     def gp_fit(self, X: np.ndarray, y: np.ndarray, lengthscale, sigma_f2: float = 1.0, sigma_n2: float = 1e-6,
                jitter: float = 0.0, wait: bool = True):
         """ut_gp_fit (wait=True) or ut_gp_fit_async (wait=False: the fit runs on the
