@@ -36,7 +36,8 @@ def registry():
     R.the_registry.clear()
 
 
-@pytest.mark.parametrize("name", ["GpuDifferentialEvolution", "GpuPSO-PMX", "GpuGA-CX", "GPU_PSO_GA_DE"])
+@pytest.mark.parametrize("name", ["GpuDifferentialEvolution", "GpuPSO-PMX", "GpuGA-CX", "GPU_PSO_GA_DE",
+                                  "GpuAUCBanditMetaTechniqueA"])
 def test_reference_driver_on_device(registry, name, caplog):
     tech = {t.name: t for t in registry}[name]
     m = R.Manipulator(_mirror())
@@ -52,7 +53,7 @@ def test_reference_driver_on_device(registry, name, caplog):
     for dr in d._drs:
         assert dr.configuration.hash == m.hash_config(dr.configuration.data)
     assert d.best_result.time < max(r.time for r in d._results)
-    if name == "GPU_PSO_GA_DE":
+    if name in ("GPU_PSO_GA_DE", "GpuAUCBanditMetaTechniqueA"):
         model = d.root_technique.techniques[0].gpu.model
         assert 0 < model.fits <= d.generation
 

@@ -52,20 +52,24 @@ def _run(tech, generations=6, parallelism=4):
 
 
 def test_register_all_wraps_every_technique(registry):
-    assert R.the_registry == registry and len(registry) == 22
-    for t in registry[:-1]:
+    assert R.the_registry == registry and len(registry) == 24
+    names = ("GPU_PSO_GA_DE", "GpuAUCBanditMetaTechniqueA", "GpuAUCBanditMetaTechniqueB")
+    bandits = [t for t in registry if t.name in names]
+    assert [b.name for b in bandits] == list(names)
+    for t in registry:
+        if t in bandits:
+            continue
         assert isinstance(t, R.SearchTechnique)                       # the reference's class
         assert t.desired_result.__func__ is R.SearchTechnique.desired_result
         assert isinstance(t.gpu, T.GpuBatchTechnique)
-    bandit = registry[-1]
-    assert bandit.name == "GPU_PSO_GA_DE"
-    assert all(isinstance(c, R.SearchTechnique) for c in bandit.techniques)
-    models = {id(c.gpu.model) for c in bandit.techniques}
-    assert len(models) == 1                                            # one shared surrogate
+    for bandit in bandits:
+        assert all(isinstance(c, R.SearchTechnique) for c in bandit.techniques)
+        models = {id(c.gpu.model) for c in bandit.techniques}
+        assert len(models) == 1                                        # one shared surrogate per bandit
 
 
 @pytest.mark.parametrize("name", ["GpuDifferentialEvolutionAlt", "GpuPSO-OX1", "GpuGA-OX3", "GpuGGA",
-                                  "GpuNormalGreedyMutation10", "GPU_PSO_GA_DE"])
+                                  "GpuNormalGreedyMutation10", "GPU_PSO_GA_DE", "GpuAUCBanditMetaTechniqueA"])
 def test_reference_driver_runs_gpu_technique(registry, name, caplog):
     tech = {t.name: t for t in registry}[name]
     with caplog.at_level("WARNING"):

@@ -159,3 +159,31 @@ def test_queued_selections_are_in_the_dedup_set():
     hb = {h for _, h in b.queue}
     assert len(ha) == 4 and len(hb) == 4 and not (ha & hb)
     assert ha | hb <= a.model._hist
+
+
+def test_rank_transform_fits_normal_scores():
+    """y_transform="rank": the GP is fitted on Phi^-1((rank + 1/2) / n) of the
+    objective in the fit's row order (order preserved, so the incumbent is the
+    minimum); the rows and the append prefix are the untransformed run's"""
+    from scipy.special import ndtri
+    rng = np.random.default_rng(1)
+    raw, rk = SharedModel(), SharedModel(y_transform="rank")
+    raw.engine, rk.engine = _Engine(), _Engine()
+    d = _Driver()
+    d.add(10.0 ** rng.uniform(0, 14, size=100), rng)          # an objective spanning 14 decades
+    for step in range(3):
+        assert raw.fit(d) and rk.fit(d)
+        (Xr, yr), (Xk, yk) = raw.engine.fits[-1], rk.engine.fits[-1]
+        assert np.array_equal(Xr, Xk)
+        n = len(yr)
+        want = np.empty(n)
+        want[np.argsort(yr, kind="stable")] = ndtri((np.arange(n) + 0.5) / n)
+        assert np.array_equal(yk, want)
+        assert np.argmin(yk) == np.argmin(yr)
+        d.add(10.0 ** rng.uniform(0, 14, size=8), rng)
+    try:
+        SharedModel(y_transform="log")
+    except ValueError:
+        pass
+    else:
+        raise AssertionError("unknown y_transform accepted")

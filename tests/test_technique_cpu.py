@@ -207,7 +207,7 @@ def test_reference_registry_mirrors_reference_techniques():
     from uptune_amd._lib import CROSSOVERS
     reg = T.reference_registry(pool=256, batch=4)
     names = [t.name for t in reg]
-    assert len(names) == len(set(names)) == 22
+    assert len(names) == len(set(names)) == 24
     by = {t.name: t for t in reg}
     assert by["GpuDifferentialEvolution"].cr == 0.9 and by["GpuDifferentialEvolutionAlt"].cr == 0.2
     for xo in ("OX1", "OX3", "PMX", "PX", "CX"):
@@ -218,10 +218,45 @@ def test_reference_registry_mirrors_reference_techniques():
     assert by["GpuGGA"].ga["crossover_strength"] == 0.2
     assert all(getattr(t, "engine", None) is None for t in reg if isinstance(t, T.GpuBatchTechnique))
     assert by["GPU_PSO_GA_DE"].bandit is not None
+    # the default root technique, AUCBanditMetaTechniqueA (bandittechniques.py:273-278),
+    # without RandomNelderMead; its children share one model
+    a = by["GpuAUCBanditMetaTechniqueA"]
+    kids = {t.name: t for t in a.techniques}
+    assert kids["gpu-de-alt"].cr == 0.2
+    assert kids["gpu-uniform-greedy-mutation"].ga["mutation_rate"] == 0.1
+    assert not kids["gpu-uniform-greedy-mutation"].ga["normal"]
+    assert kids["gpu-normal-greedy-mutation"].ga["mutation_rate"] == 0.3
+    assert kids["gpu-normal-greedy-mutation"].ga["normal"]
+    assert len({id(t.model) for t in a.techniques}) == 1
+    assert [t.name for t in by["GpuAUCBanditMetaTechniqueB"].techniques] == ["gpu-de-alt",
+                                                                           "gpu-uniform-greedy-mutation"]
+    assert T.bandit_a(pool=256).bandit.C == 0.05 and T.bandit_a(pool=256).bandit.window == 500
     # the reference-side binding rebases every class through `wrap`
     class _Tag:
         pass
 
     reg2 = T.reference_registry(wrap=lambda c: type("W" + c.__name__, (c, _Tag), {}), pool=256)
-    assert all(isinstance(t, _Tag) for t in reg2[:-1])
-    assert all(isinstance(c, _Tag) for c in reg2[-1].techniques)
+    bandits = [t for t in reg2 if isinstance(t, T.AUCBanditMetaTechnique)]
+    assert len(bandits) == 3
+    assert all(isinstance(t, _Tag) for t in reg2 if t not in bandits)
+    assert all(isinstance(c, _Tag) for b in bandits for c in b.techniques)
+
+
+def test_c1_bandit_a_over_the_oracle_engine():
+    """C1's root technique (AUCBanditMetaTechniqueA's device counterpart,
+    technique.bandit_a) through the driver with the CPU stand-in engine
+    (tests/_oracle_engine.py: the oracle's propose / hash / GP): every child runs,
+    nothing is evaluated twice, and the bandit's credits are the new bests"""
+    from _oracle_engine import OracleEngine
+    m = _space2()
+    meta = T.bandit_a(bandit_seed=5, pool=256, batch=4, population=30, seed=11, lengthscale=0.3,
+                      y_transform="rank", engine_factory=OracleEngine)
+    d = SearchDriver(m, meta, parallelism=4, hash_fn=_hash_fn(m))
+    best = d.main(_rosen, test_limit=160)
+    assert d.test_count >= 160
+    assert len(d.results) == d.test_count
+    b = d.root_technique.bandit
+    assert set(b.use_counts) == {"gpu-de-alt", "gpu-uniform-greedy-mutation", "gpu-normal-greedy-mutation"}
+    assert all(v > 0 for v in b.use_counts.values())
+    assert best.time == min(r.time for r in d.results.values())
+    assert sum(1 for _, v in b.history if v) == sum(1 for r in d.results.values() if r.was_new_best)

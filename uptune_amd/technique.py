@@ -273,9 +273,17 @@ class SharedModel:
 
     def __init__(self, device: int = 0, seed: int = 0, lengthscale: float = 0.3, min_train: int = 4,
                  precision: int = 64, sigma_f2: float = 1.0, sigma_n2: float = 1e-6, jitter: float = 1e-8,
-                 engine_factory=None):
+                 engine_factory=None, y_transform: Optional[str] = None):
         self.device, self.seed, self.lengthscale, self.min_train = device, seed, lengthscale, min_train
         self.precision = precision
+        # y_transform: what the GP is fitted on.  None = the objective as
+        # measured; "rank" = its normal scores, Phi^-1((rank + 1/2) / n) (order
+        # preserving, so the incumbent stays the minimum): an objective spanning
+        # many decades (Rosenbrock over [-1000, 1000]^2: 0 .. 1e14) otherwise
+        # standardises to a flat landscape where EI only explores
+        if y_transform not in (None, "rank"):
+            raise ValueError("y_transform: None or 'rank'")
+        self.y_transform = y_transform
         # engine_factory(manipulator, device, seed) -> a BatchEngine-compatible
         # object; None = uptune_amd.engine.BatchEngine (the device path).  Tests
         # substitute a CPU stand-in to exercise the plugin plumbing without a GPU.
@@ -427,7 +435,13 @@ class SharedModel:
             self._Xf[self._nf:n] = self._Xa[self._nf:n]
             self._yf[self._nf:n] = self._ya[self._nf:n]
         self._nf = n
-        self.engine.gp_fit(self._Xf[:n], self._yf[:n], lengthscale=self.lengthscale, wait=False, **self.hyper)
+        y = self._yf[:n]
+        if self.y_transform == "rank":
+            from scipy.special import ndtri
+            r = np.empty(n)
+            r[np.argsort(y, kind="stable")] = np.arange(n)
+            y = ndtri((r + 0.5) / n)
+        self.engine.gp_fit(self._Xf[:n], y, lengthscale=self.lengthscale, wait=False, **self.hyper)
         self._fit_key = key
         self._fit_unverified = True
         self.fits += 1
@@ -494,7 +508,7 @@ class GpuBatchTechnique(SearchTechnique):
     def __init__(self, pool: int = 1 << 14, batch: int = 8, population: int = 1024, device: int = 0,
                  seed: int = 0, lengthscale: float = 0.3, min_train: int = 4, acq: str = "ei",
                  group=None, surrogate=None, shared: Optional[SharedModel] = None, engine_factory=None,
-                 prune_rows: int = 0, precision: int = 64, *pargs, **kwargs):
+                 prune_rows: int = 0, precision: int = 64, y_transform: Optional[str] = None, *pargs, **kwargs):
         super().__init__(*pargs, **kwargs)
         # prune_rows > 0: score rounds with ut_gp_topk_pruned (selection-exact EI
         # bound from the first prune_rows rows of L^-1 k*; fp64 fits, EI / UCB):
@@ -511,7 +525,8 @@ class GpuBatchTechnique(SearchTechnique):
         self.model = shared if shared is not None else SharedModel(device=device, seed=seed,
                                                                    lengthscale=lengthscale, min_train=min_train,
                                                                    precision=precision,
-                                                                   engine_factory=engine_factory)
+                                                                   engine_factory=engine_factory,
+                                                                   y_transform=y_transform)
         # multi-GPU: with torch.distributed initialised and
         # world > 1, rank r scores candidates [base + r*pool, base + (r+1)*pool)
         # of every round and the local top-k lists are all-gathered and merged
@@ -793,7 +808,7 @@ class GpuGGA(GpuGA):
 def _shared_model(kw) -> SharedModel:
     return SharedModel(device=kw.get("device", 0), seed=kw.get("seed", 0), lengthscale=kw.get("lengthscale", 0.3),
                        min_train=kw.get("min_train", 4), precision=kw.get("precision", 64),
-                       engine_factory=kw.pop("engine_factory", None))
+                       engine_factory=kw.pop("engine_factory", None), y_transform=kw.get("y_transform"))
 
 
 def pso_ga_de_bandit(bandit_seed: Optional[int] = None, **kw) -> AUCBanditMetaTechnique:
@@ -810,6 +825,34 @@ def pso_ga_de_bandit(bandit_seed: Optional[int] = None, **kw) -> AUCBanditMetaTe
         GpuDifferentialEvolution(name="gpu-de", shared=shared, **kw),
         GpuGGA(name="gpu-gga", shared=shared, **kw),
     ], name="GPU_PSO_GA_DE", seed=bandit_seed)
+
+
+def bandit_a(bandit_seed: Optional[int] = None, **kw) -> AUCBanditMetaTechnique:
+    """GPU counterpart of the reference's default root technique,
+    "AUCBanditMetaTechniqueA" (bandittechniques.py:273-278; technique.py:349):
+    DifferentialEvolutionAlt (cr 0.2), UniformGreedyMutation (mutation rate
+    0.1, evolutionarytechniques.py:13-24) and NormalGreedyMutation(mutation_rate
+    =0.3) on one shared model.  The fourth child, RandomNelderMead, is a
+    sequential simplex technique outside the scoring path (DESIGN.md "Out of
+    scope") and is not built."""
+    kw = dict(kw)
+    shared = kw.pop("shared", None) or _shared_model(kw)
+    return AUCBanditMetaTechnique([
+        GpuDifferentialEvolution(name="gpu-de-alt", cr=0.2, shared=shared, **kw),
+        GpuGA(name="gpu-uniform-greedy-mutation", mutation_rate=0.1, shared=shared, **kw),
+        GpuGA(name="gpu-normal-greedy-mutation", mutation_rate=0.3, normal=True, shared=shared, **kw),
+    ], name="GpuAUCBanditMetaTechniqueA", seed=bandit_seed)
+
+
+def bandit_b(bandit_seed: Optional[int] = None, **kw) -> AUCBanditMetaTechnique:
+    """"AUCBanditMetaTechniqueB" (bandittechniques.py:279-282): DifferentialEvolutionAlt
+    and UniformGreedyMutation on one shared model"""
+    kw = dict(kw)
+    shared = kw.pop("shared", None) or _shared_model(kw)
+    return AUCBanditMetaTechnique([
+        GpuDifferentialEvolution(name="gpu-de-alt", cr=0.2, shared=shared, **kw),
+        GpuGA(name="gpu-uniform-greedy-mutation", mutation_rate=0.1, shared=shared, **kw),
+    ], name="GpuAUCBanditMetaTechniqueB", seed=bandit_seed)
 
 
 _XO = ("op3_cross_OX3", "op3_cross_OX1", "op3_cross_PMX", "op3_cross_PX", "op3_cross_CX")
@@ -829,6 +872,8 @@ def reference_registry(wrap=None, bandit_cls=None, **kw) -> List[SearchTechnique
                                         evolutionarytechniques.py:151-158
       GGA                               globalGA.py:129
       PSO_GA_DE bandit                  bandittechniques.py:311-320
+      AUCBanditMetaTechniqueA / B       bandittechniques.py:273-282 (A without
+                                        RandomNelderMead: see bandit_a)
 
     `wrap(cls)` maps each GPU technique class before construction (the
     reference-side binding rebases them onto its SearchTechnique)
@@ -863,4 +908,14 @@ def reference_registry(wrap=None, bandit_cls=None, **kw) -> List[SearchTechnique
     children = [PSO(name="gpu-pso", shared=sm, **kw), GA(name="gpu-ga", crossover_rate=0.5, shared=sm, **kw),
                 DE(name="gpu-de", shared=sm, **kw), GGA(name="gpu-gga", shared=sm, **kw)]
     out.append((bandit_cls or AUCBanditMetaTechnique)(children, name="GPU_PSO_GA_DE"))
+    # AUCBanditMetaTechniqueA / B, each with a model of its own
+    sa, sb = _shared_model(dict(kw)), _shared_model(dict(kw))
+    for nm, kids in (("GpuAUCBanditMetaTechniqueA",
+                      [DE(name="gpu-de-alt", cr=0.2, shared=sa, **kw),
+                       GA(name="gpu-uniform-greedy-mutation", mutation_rate=0.1, shared=sa, **kw),
+                       GA(name="gpu-normal-greedy-mutation", mutation_rate=0.3, normal=True, shared=sa, **kw)]),
+                     ("GpuAUCBanditMetaTechniqueB",
+                      [DE(name="gpu-de-alt", cr=0.2, shared=sb, **kw),
+                       GA(name="gpu-uniform-greedy-mutation", mutation_rate=0.1, shared=sb, **kw)])):
+        out.append((bandit_cls or AUCBanditMetaTechnique)(kids, name=nm))
     return out
