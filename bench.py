@@ -386,6 +386,9 @@ def main():
     ap.add_argument("--prune", type=int, default=0, metavar="ROWS",
                     help="selection-exact EI-bound pruning (ut_score_round_de_pruned) with the first ROWS rows of "
                          "L^-1 k* as the bound; a secondary line, fp64 only (the dense round stays the headline)")
+    ap.add_argument("--prune-pass", type=int, default=32, choices=(32, 64),
+                    help="--prune's bound pass over every candidate: 32 = k* in f32 past the bound rows with every "
+                         "rounding bounded (ut_gp_set_prune_pass; the default), 64 = fp64")
     args = ap.parse_args()
     if args.precision is None:
         args.precision = 64 if args.prune else 8
@@ -446,6 +449,8 @@ def main():
         manip = ConfigurationManipulator([FloatParameter(i, -1000.0, 1000.0) for i in range(d)])
     eng = BatchEngine(manip, device=local, seed=1)
     eng.gp_set_precision(args.precision)
+    if args.prune:
+        eng.gp_set_prune_pass(args.prune_pass)
     eng.population_init(npop)
     # the results history holds the evaluated configurations: the n training
     # points (C2/C3) or the 3,680 recorded gcc configs (C4), plus every round's
@@ -662,10 +667,12 @@ def main():
         var_ms = stages.get("kstar")
         k64 = kstar_fp64_features(eng, d)
         flops_var = 2.0 * m * n * k64
-        kernel = ("k_gp_kstar<double, true, %s> (K* with the mean k* . alpha in its epilogue, "
-                  "v_mfma_f64_16x16x4_f64 over %d fp64 features%s) [pruned round: the variance GEMM runs for the "
-                  "survivors only]" % ("true" if k64 < d else "false", k64,
-                                       " + the one-hot codes on v_mfma_i32_16x16x64_i8" if k64 < d else ""))
+        kernel = ("k_gp_kstar<double, true, %s, %s> (K* with the mean k* . alpha in its epilogue, "
+                  "v_mfma_f64_16x16x4_f64 over %d fp64 features%s%s) [pruned round: the variance GEMM runs for the "
+                  "survivors only]" % ("true" if k64 < d else "false", "true" if args.prune_pass == 32 else "false",
+                                       k64, " + the one-hot codes on v_mfma_i32_16x16x64_i8" if k64 < d else "",
+                                       "; bound pass: k* = sf2 2^t by v_exp_f32 past the bound rows, rounding "
+                                       "bounded" if args.prune_pass == 32 else ""))
     achieved = flops_var / (var_ms * 1e-3) / 1e12 if var_ms else None
     peak = {64: PEAK_FP64_TFLOPS, 32: PEAK_FP32_TFLOPS, 16: PEAK_FP16_TFLOPS / 3.0,
             8: PEAK_I8_TOPS / I8_PRODUCTS}[args.precision]
@@ -686,7 +693,7 @@ def main():
     prune_info = None
     if args.prune and prune_stats:
         timed = prune_stats[-args.steps:]
-        prune_info = {"bound_rows": timed[-1]["bound_rows"],
+        prune_info = {"bound_rows": timed[-1]["bound_rows"], "bound_pass": args.prune_pass,
                       "survivor_frac": float(np.mean([s["survivors"] / m for s in timed])),
                       "dense_rounds": int(sum(s["dense"] for s in timed)),
                       "dense_equivalent_tflops": float(m) * n * (n + 1) / (elapsed / args.steps) / 1e12,

@@ -917,14 +917,17 @@ def test_perm_score_round():
 
 
 # --------------------------------------------------------------------------- EI-bound pruning
+@pytest.mark.parametrize("prune_pass", [32, 64])
 @pytest.mark.parametrize("acq,bound_rows", [("ei", 128), ("ei", 384), ("ucb", 256)])
-def test_gp_topk_pruned_equals_dense(acq, bound_rows):
+def test_gp_topk_pruned_equals_dense(acq, bound_rows, prune_pass):
     """ut_gp_topk_pruned: the top-k of a non-degenerate GP --
     training points drawn from the population the candidates come from, so
     many candidates sit near training data and their bound is loose -- equals
-    the dense device top-k and the oracle's; the survivors are a strict subset"""
+    the dense device top-k and the oracle's; the survivors are a strict subset.
+    Both bound passes: f32 k* with its rounding bounded (32, the default) and fp64"""
     space = mixed_space()
     e = engine(space, seed=8)
+    e.gp_set_prune_pass(prune_pass)
     pop = ode.population_init(space, 4096, seed=8)
     e.population_set(dev(pop))
     n = 640
@@ -967,12 +970,14 @@ def test_gp_topk_pruned_degenerate_exact_ties():
     e.gp_fit(X, y, lengthscale=0.2)
     vals = e.propose_de(8192, round_=1)
     feat = e.encode(vals)
-    for base in (0, 1000):
-        idx, top, st = e.gp_topk_pruned(feat, 32, bound_rows=128, cand_base=base)
-        _, _, score = e.gp_score(feat)
-        i2, t2 = e.topk(score, 32, cand_base=base)
-        assert idx.cpu().numpy().tolist() == i2.cpu().numpy().tolist() == list(range(base, base + 32))
-        assert not st["dense"] and st["survivors"] == 32, st
+    for prune_pass in (32, 64):   # the f32 pass pins these scores too (k*^ flushes to 0 within its bound)
+        e.gp_set_prune_pass(prune_pass)
+        for base in (0, 1000):
+            idx, top, st = e.gp_topk_pruned(feat, 32, bound_rows=128, cand_base=base)
+            _, _, score = e.gp_score(feat)
+            i2, t2 = e.topk(score, 32, cand_base=base)
+            assert idx.cpu().numpy().tolist() == i2.cpu().numpy().tolist() == list(range(base, base + 32))
+            assert not st["dense"] and st["survivors"] == 32, (prune_pass, st)
 
 
 def test_gp_topk_pruned_dense_fallback():

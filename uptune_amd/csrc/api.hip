@@ -803,6 +803,13 @@ int ut_gp_set_precision(ut_ctx* c, int32_t bits) {
   return 0;
 }
 
+int ut_gp_set_prune_pass(ut_ctx* c, int32_t bits) {
+  if (!c) return UT_EINVAL;
+  UT_CHECK(c, bits == 32 || bits == 64, UT_EINVAL, "prune pass must be 32 or 64");
+  c->prune_pass = bits;
+  return 0;
+}
+
 int ut_gp_set_i8_tol(ut_ctx* c, double tol) {
   if (!c) return UT_EINVAL;
   UT_CHECK(c, tol >= 0.0 && tol < 1.0, UT_EINVAL, "i8 tolerance must be in [0, 1)");

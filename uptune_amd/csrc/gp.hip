@@ -1151,6 +1151,7 @@ int gp_fit_enqueue(ut_ctx* c, const double* X, const double* y, int32_t n, int32
   int rc = gp_alloc(c, npad, d);
   if (rc) return rc;
   c->pr_f2_valid = false;   // |L^-1|_F^2 (pruned scoring) belongs to the previous factor
+  c->pr_ab_valid = false;
   const size_t need = (size_t)n * d + n + d;
   bool fresh = false;   // a new staging buffer holds no previous rows
   if (c->fit_host_n < need) {
@@ -1287,7 +1288,7 @@ static KstarCat kstar_cat(ut_ctx* c, const int8_t* bcat) {
 }
 
 static int gather_kstar_cols(ut_ctx* c, bool cat, int32_t dpad, int64_t ldk, const int64_t* idx, int64_t base,
-                             int64_t nc, int64_t ldc);
+                             int64_t nc, int64_t ldc, double* mu_part = nullptr);
 
 int gp_score_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, const ut_acq* acq, const uint8_t* dup,
                   double* mu, double* var, double* score, hipEvent_t dup_ready) {
@@ -1468,14 +1469,80 @@ __global__ void k_prune_bound(int64_t m, int32_t RTm, const double* __restrict__
   if (exact_out) exact_out[i] = exact ? 1 : 0;
 }
 
+// The bound of the f32 pass (ut_gp_set_prune_pass 32; K* by k_gp_kstar<double,
+// true, *, true>: the stored bound rows in fp64 as before, every other k*^ =
+// sf2 2^t^ with |k*^ - k*| <= 2^-17 k*^ + 2^-125 sf2, its f32 tile sums within
+// 2^-16 of sum |alpha| k*^ together with that).  Per candidate:
+//   mean  |mu - mu^| <= dmu = 2^-16 S + 2^-125 sf2 sum|alpha| + RT 2^-51
+//         sum_rt |mu^_rt|: S = sum_r |alpha_r| k*^_r over the f32 rows (part3),
+//         mu the fp64 k* . alpha the survivors are scored with (k_gp_kstar's
+//         fp64 epilogue on their columns: its bound-row tile partials are these
+//         bitwise, its other tiles within the first term; the last term the
+//         different rounding of the two sums over tiles);
+//   bound rows  exact k*: var <= var_ub = sf2 - |v^_R|^2 (as k_prune_bound);
+//   lower end (rows past R: |L^-1|_F^2 |k*|^2 as k_prune_bound's tail)
+//         var >= var_lo = sf2 - (|v^_R|^2 + 1.001 |L^-1|_F^2 ((1 + 2^-16) |k*^|^2 +
+//         n (2^-125 sf2)^2));
+// the score bound is the acquisition at (mu^ - dmu, var_ub), raised by
+// k_prune_bound's 1e-12 margin -- unless both ends pin the exact score: var_lo
+// == var_ub and the mean's two ends give the same I = f_best - mu - xi (EI) or
+// the same score (UCB); then the exact score is that double, stored as is and
+// flagged exact (a flat GP keeps its index tie-break).  fp64 rounding of the
+// sums: a 2^-36 margin.  cst: [0] |L^-1|_F^2, [1 + SQ_BLOCKS] sum |alpha|.
+constexpr int SQ_BLOCKS = 1024;
+__global__ void k_prune_bound32(int64_t m, int32_t RTm, const double* __restrict__ mu_part,
+                                const double* __restrict__ sa_part, const double* __restrict__ k2_part, int32_t RTv,
+                                const double* __restrict__ var_part, int64_t ldp, double sf2, int32_t n,
+                                const double* __restrict__ stats, const int32_t* __restrict__ fit_flag, int32_t kind,
+                                double xi, double kappa, const uint8_t* __restrict__ dup,
+                                const double* __restrict__ cst, double* __restrict__ ub_out,
+                                uint8_t* __restrict__ exact_out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= m) return;
+  double mu = 0.0, mabs = 0.0, sa = 0.0, k2 = 0.0, vs = 0.0;
+  for (int32_t r = 0; r < RTm; ++r) {
+    const int64_t o = (int64_t)r * ldp + i;
+    mu += mu_part[o];
+    mabs += fabs(mu_part[o]);
+    sa += sa_part[o];
+    k2 += k2_part[o];
+  }
+  for (int32_t r = 0; r < RTv; ++r) vs += var_part[(int64_t)r * ldp + i];
+  const double F2 = cst[0], A1 = cst[1 + SQ_BLOCKS];
+  const double tiny = 0x1p-125 * sf2;
+  const double dmu = (0x1p-16 * sa + tiny * A1 + (double)RTm * 0x1p-51 * mabs) * (1.0 + 0x1p-20);
+  double var_ub = sf2 - vs;   // the bound rows' partials: bitwise the exact GEMM's first RTv (k_prune_bound)
+  var_ub = var_ub > 0.0 ? var_ub : 0.0;
+  const double tail = 1.001 * F2 * ((1.0 + 0x1p-16) * k2 + (double)n * tiny * tiny);
+  double var_lo = sf2 - (vs + tail) * (1.0 + 0x1p-36);
+  var_lo = var_lo > 0.0 ? var_lo : 0.0;
+  double ub = acq_score(kind, mu - dmu, var_ub, stats[0], xi, kappa);
+  bool exact = var_lo == var_ub && dmu == dmu;
+  if (exact) {
+    if (kind == UT_ACQ_UCB)
+      exact = ub == acq_score(kind, mu + dmu, var_lo, stats[0], xi, kappa);
+    else
+      exact = (stats[0] - (mu - dmu) - xi) == (stats[0] - (mu + dmu) - xi);
+  }
+  if (!exact) ub = ub + fabs(ub) * 1e-12 + 1e-300;
+  if (*fit_flag != 0 || ub != ub) {
+    ub = __builtin_nan("");
+    exact = false;
+  }
+  if (dup && dup[i]) ub = -1.0 / 0.0;
+  ub_out[i] = ub;
+  exact_out[i] = exact ? 1 : 0;
+}
+
 // sum of squares of cnt doubles (|L^-1|_F^2), deterministic: pass 1 writes one
 // partial per block (grid-stride), pass 2 (one block) adds them in order
-constexpr int SQ_BLOCKS = 1024;
+template <bool ABS>   // ABS: sum |x| instead
 __global__ __launch_bounds__(256) void k_sumsq_part(const double* __restrict__ x, int64_t cnt,
                                                     double* __restrict__ part) {
   __shared__ double red[4];
   double s = 0.0;
-  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < cnt; e += (int64_t)gridDim.x * 256) s += x[e] * x[e];
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < cnt; e += (int64_t)gridDim.x * 256)
+    s += ABS ? fabs(x[e]) : x[e] * x[e];
   for (int d = 32; d > 0; d >>= 1) s += __shfl_xor(s, d, 64);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
   __syncthreads();
@@ -1523,11 +1590,14 @@ __global__ void k_gather_cols(const double* __restrict__ kst, int64_t ldk, const
 }
 
 // exact scores of the gathered candidates: compact[j], and scattered to full[idx[j]]
+// mu_full: the bound pass's exact mean by global index; or (nullptr) the fp64
+// mean partials k* . alpha of these columns' K* (gather_kstar_cols: the f32
+// bound pass has no exact mean)
 __global__ void k_prune_exact(int64_t n, const int64_t* __restrict__ idx, int64_t base, int32_t RT,
                               const double* __restrict__ var_part, int64_t ldp, const double* __restrict__ mu_full,
                               double sf2, const double* __restrict__ stats, const int32_t* __restrict__ fit_flag,
                               int32_t kind, double xi, double kappa, double* __restrict__ compact,
-                              double* __restrict__ full) {
+                              double* __restrict__ full, const double* __restrict__ mu_part) {
   const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= n) return;
   const int64_t q = idx[j];
@@ -1535,11 +1605,16 @@ __global__ void k_prune_exact(int64_t n, const int64_t* __restrict__ idx, int64_
     if (compact) compact[j] = -1.0 / 0.0;
     return;
   }
-  double vs = 0.0;
+  double vs = 0.0, mu = 0.0;
   for (int32_t r = 0; r < RT; ++r) vs += var_part[(int64_t)r * ldp + j];
+  if (mu_full) {
+    mu = mu_full[q - base];
+  } else {
+    for (int32_t r = 0; r < RT; ++r) mu += mu_part[(int64_t)r * ldp + j];
+  }
   double var = sf2 - vs;
   var = var > 0.0 ? var : 0.0;
-  double sc = acq_score(kind, mu_full[q - base], var, stats[0], xi, kappa);
+  double sc = acq_score(kind, mu, var, stats[0], xi, kappa);
   if (*fit_flag != 0) sc = __builtin_nan("");
   if (compact) compact[j] = sc;
   if (full) full[q - base] = sc;
@@ -1584,9 +1659,10 @@ __global__ void k_fill(double* __restrict__ p, int64_t n, double v) {
 // and norms (and categorical codes) gathered from the K* operands of the
 // round (c->ucand / c->cnorm / c->bcat, leading dimension ldk), then the K*
 // GEMM on those columns only (pruned scoring's threshold set and survivors,
-// precision 8's flagged candidates)
+// precision 8's flagged candidates); mu_part: also their fp64 mean partials
+// k* . alpha per row tile [RT][ldc] (pruned scoring's f32 bound pass)
 static int gather_kstar_cols(ut_ctx* c, bool cat, int32_t dpad, int64_t ldk, const int64_t* idx, int64_t base,
-                             int64_t nc, int64_t ldc) {
+                             int64_t nc, int64_t ldc, double* mu_part) {
   const int32_t npad = ((c->gp_n + NPAD - 1) / NPAD) * NPAD;
   const int32_t RT = npad / NPAD;
   const double* XsT = cat ? c->gp_XsT_num.p : c->gp_XsT;
@@ -1607,7 +1683,7 @@ static int gather_kstar_cols(ut_ctx* c, bool cat, int32_t dpad, int64_t ldk, con
                        c->stream, c->bcat.p, ldk, idx, base, nc, ldc, c->pr_bcat.p);
   }
   UT_LAUNCH_CHECK(c);
-  return launch_gemm_kstar(c, 64, XsT, npad, c->pr_ucand.p, dpad, nc, c->pr_kst.p, ldc, nullptr, -1,
+  return launch_gemm_kstar(c, 64, XsT, npad, c->pr_ucand.p, dpad, nc, c->pr_kst.p, ldc, mu_part, -1,
                            c->pr_cnorm.p, nullptr, cat ? kstar_cat(c, c->pr_bcat.p) : KstarCat(), xn);
 }
 
@@ -1646,7 +1722,11 @@ int gp_topk_pruned_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, co
   if ((rc = ensure(c, c->pr_idx, (size_t)ldk + 2048))) return rc;
   if ((rc = ensure(c, c->pr_count, 1))) return rc;
   if ((rc = ensure(c, c->pr_k2, (size_t)RT * ldk))) return rc;
-  if ((rc = ensure(c, c->pr_f2, 1 + SQ_BLOCKS))) return rc;   // [0] the norm, [1..] block partials
+  // [0] |L^-1|_F^2, [1..] block partials, then the f32 pass's sum |alpha|
+  if ((rc = ensure(c, c->pr_f2, 2 + SQ_BLOCKS))) return rc;
+  const bool f32 = c->prune_pass == 32;
+  if (f32 && (rc = ensure(c, c->pr_sa, (size_t)RT * ldk))) return rc;
+  if (f32 && (rc = ensure(c, c->pr_gmu, (size_t)RT * (ldk + 1024)))) return rc;   // survivors / threshold set
   if ((rc = ensure(c, c->pr_exact, (size_t)ldk))) return rc;
   const double* LinvT = c->gp_LinvT;
   // 1. K* with the mean in its epilogue, 2. the first R row tiles of L^-1 K*^T
@@ -1666,15 +1746,28 @@ int gp_topk_pruned_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, co
   // columns recomputed from their features (recompute_cols below): cheaper than
   // writing and re-reading the whole n x m matrix
   if ((rc = launch_gemm_kstar(c, 64, XsT, npad, c->ucand.p, dpad, m, c->kst.p, ldk, c->mu_part.p, R * NPAD,
-                              nullptr, c->pr_k2.p, cat ? kstar_cat(c, c->bcat.p) : KstarCat(), xn)))
+                              nullptr, c->pr_k2.p, cat ? kstar_cat(c, c->bcat.p) : KstarCat(), xn,
+                              f32 ? c->pr_sa.p : nullptr)))
     return rc;
-  // |L^-1|_F^2 for the variance tail bound, once per fit
-  if (!c->pr_f2_valid) {
-    hipLaunchKernelGGL(k_sumsq_part, dim3(SQ_BLOCKS), dim3(256), 0, c->stream, c->gp_Linv, (int64_t)npad * npad,
-                       c->pr_f2.p + 1);
-    hipLaunchKernelGGL(k_sumsq_final, dim3(1), dim3(256), 0, c->stream, c->pr_f2.p + 1, SQ_BLOCKS, c->pr_f2.p);
+  // |L^-1|_F^2 for the variance tail bound, once per fit (the block partials
+  // in pr_f2[1..] are scratch, reused pass after pass in stream order)
+  auto sumsq = [&](bool abs_, const double* x, int64_t cnt, double* out) -> int {
+    if (abs_)
+      hipLaunchKernelGGL(k_sumsq_part<true>, dim3(SQ_BLOCKS), dim3(256), 0, c->stream, x, cnt, c->pr_f2.p + 1);
+    else
+      hipLaunchKernelGGL(k_sumsq_part<false>, dim3(SQ_BLOCKS), dim3(256), 0, c->stream, x, cnt, c->pr_f2.p + 1);
+    hipLaunchKernelGGL(k_sumsq_final, dim3(1), dim3(256), 0, c->stream, c->pr_f2.p + 1, SQ_BLOCKS, out);
     UT_LAUNCH_CHECK(c);
+    return 0;
+  };
+  if (!c->pr_f2_valid) {
+    if ((rc = sumsq(false, c->gp_Linv, (int64_t)npad * npad, c->pr_f2.p))) return rc;
     c->pr_f2_valid = true;
+  }
+  if (f32 && !c->pr_ab_valid) {   // the f32 bound's per-fit constants
+    double* cst = c->pr_f2.p + 1 + SQ_BLOCKS;
+    if ((rc = sumsq(true, c->gp_alpha, n, cst))) return rc;
+    c->pr_ab_valid = true;
   }
   mark(c, "kstar");
   if ((rc = launch_gemm_var(c, 64, LinvT, npad, c->kst.p, ldk, R * NPAD, m, c->var_part.p, c->gp_beta,
@@ -1682,9 +1775,14 @@ int gp_topk_pruned_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, co
     return rc;
   mark(c, "bound");
   if (dup_ready) UT_HIP(c, hipStreamWaitEvent(c->stream, dup_ready, 0));   // the dup mask (side stream)
-  hipLaunchKernelGGL(k_prune_bound, dim3(grid1(m, 256)), dim3(256), 0, c->stream, m, RT, c->mu_part.p, R,
-                     c->var_part.p, ldk, c->gp_sf2, c->gp_stats, c->gp_flag, acq->kind, acq->xi, acq->kappa, dup,
-                     c->pr_mu.p, c->pr_ub.p, c->pr_k2.p, c->pr_f2.p, c->pr_exact.p);
+  if (f32)
+    hipLaunchKernelGGL(k_prune_bound32, dim3(grid1(m, 256)), dim3(256), 0, c->stream, m, RT, c->mu_part.p,
+                       c->pr_sa.p, c->pr_k2.p, R, c->var_part.p, ldk, c->gp_sf2, n, c->gp_stats, c->gp_flag,
+                       acq->kind, acq->xi, acq->kappa, dup, c->pr_f2.p, c->pr_ub.p, c->pr_exact.p);
+  else
+    hipLaunchKernelGGL(k_prune_bound, dim3(grid1(m, 256)), dim3(256), 0, c->stream, m, RT, c->mu_part.p, R,
+                       c->var_part.p, ldk, c->gp_sf2, c->gp_stats, c->gp_flag, acq->kind, acq->xi, acq->kappa, dup,
+                       c->pr_mu.p, c->pr_ub.p, c->pr_k2.p, c->pr_f2.p, c->pr_exact.p);
   UT_LAUNCH_CHECK(c);
   // 3. threshold: exact scores of the best 1024 bounds, tau = their k-th best
   const int32_t kp = (int32_t)(m < 1024 ? m : 1024);
@@ -1692,17 +1790,20 @@ int gp_topk_pruned_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, co
   double* tsc = c->pr_score.p + ldk;                   // [1024] their bounds
   double* tex = c->pr_score.p + ldk + 1024;            // [1024] their exact scores
   if ((rc = topk_impl(c, c->pr_ub.p, dup, m, cand_base, kp < k ? k : kp, tset, tsc))) return rc;
+  // (the f32 pass has no exact mean: the recomputed columns' fp64 k* . alpha)
+  double* gmu = f32 ? c->pr_gmu.p : nullptr;
   auto recompute_cols = [&](const int64_t* idx, int64_t base, int64_t nc, int64_t ldc) -> int {
-    return gather_kstar_cols(c, cat, dpad, ldk, idx, base, nc, ldc);
+    return gather_kstar_cols(c, cat, dpad, ldk, idx, base, nc, ldc, gmu);
   };
   const int64_t ldt = ((int64_t)kp + VAR_BN - 1) / VAR_BN * VAR_BN;
   if ((rc = recompute_cols(tset, cand_base, kp, ldt))) return rc;
   if ((rc = launch_gemm_var(c, 64, LinvT, npad, c->pr_kst.p, ldt, npad, kp, c->pr_vpart.p, c->gp_beta,
                             c->pr_mpart.p)))
     return rc;
+  const double* mu_full = f32 ? nullptr : c->pr_mu.p;
   hipLaunchKernelGGL(k_prune_exact, dim3(grid1(kp, 256)), dim3(256), 0, c->stream, (int64_t)kp, tset, cand_base, RT,
-                     c->pr_vpart.p, ldt, c->pr_mu.p, c->gp_sf2, c->gp_stats, c->gp_flag, acq->kind, acq->xi,
-                     acq->kappa, tex, nullptr);
+                     c->pr_vpart.p, ldt, mu_full, c->gp_sf2, c->gp_stats, c->gp_flag, acq->kind, acq->xi,
+                     acq->kappa, tex, nullptr, gmu);
   UT_LAUNCH_CHECK(c);
   int64_t* tk_i = out_idx;   // the caller's [k] outputs hold tau's top-k for now
   double* tk_s = out_score;
@@ -1744,8 +1845,8 @@ int gp_topk_pruned_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, co
                                 c->pr_mpart.p)))
         return rc;
       hipLaunchKernelGGL(k_prune_exact, dim3(grid1(ns, 256)), dim3(256), 0, c->stream, ns, c->pr_idx.p, (int64_t)0,
-                         RT, c->pr_vpart.p, lds, c->pr_mu.p, c->gp_sf2, c->gp_stats, c->gp_flag, acq->kind, acq->xi,
-                         acq->kappa, nullptr, c->pr_score.p);
+                         RT, c->pr_vpart.p, lds, mu_full, c->gp_sf2, c->gp_stats, c->gp_flag, acq->kind, acq->xi,
+                         acq->kappa, nullptr, c->pr_score.p, gmu);
       UT_LAUNCH_CHECK(c);
     }
   }

@@ -156,7 +156,16 @@ __device__ __forceinline__ void kcat_issue(const int8_t* __restrict__ Ab, const 
 
 // MU: also the column partial of the mean, sum_r alpha_r k*_r (fp32 scoring;
 // fp64 takes the mean from the variance epilogue instead)
-template <typename TS, bool MU, bool CAT>
+// F32E (TS = double, MU; pruned scoring's bound pass, ut_gp_set_prune_pass 32):
+// past the stored bound rows, the exponent t from the fp64 accumulator as
+// before, then k* = sf2 2^(t/256) by v_exp_f32 and the tile partials of k*
+// alpha, k* |alpha| (part3) and k*^2 (part2) as f32 sums: ~7 VALU ops per k*
+// where the fp64 epilogue takes ~15 DP ops (the f64 MFMA does not issue beside
+// the VALU, so the epilogue is ~half of K*).  Every error is bounded in
+// k_prune_bound32: |k*^ - k*| <= 2^-17 k*^ + 2^-125 sf2 (t in f32: |t / 256| <=
+// 126 for a k* that is not flushed, 7.5e-6 in log2 units; v_exp_f32), the f32
+// sums within 2^-16 of sum |alpha| k*^ together with that.
+template <typename TS, bool MU, bool CAT, bool F32E>
 __global__ __launch_bounds__(K_NT, 2) void k_gp_kstar(const double* __restrict__ AT, int64_t lda,
                                                       const double* __restrict__ B, int64_t ldb, int32_t dpad,
                                                       int32_t RT, int32_t CT, const double* __restrict__ xnorm,
@@ -166,7 +175,8 @@ __global__ __launch_bounds__(K_NT, 2) void k_gp_kstar(const double* __restrict__
                                                       int64_t ldk, double* __restrict__ part, double kscale,
                                                       int64_t lo_off, int32_t store_rt, double* __restrict__ part2,
                                                       const int8_t* __restrict__ acat, const int8_t* __restrict__ bcat,
-                                                      int32_t nkc, double cat_c0, double cat_c1) {
+                                                      int32_t nkc, double cat_c0, double cat_c1,
+                                                      double* __restrict__ part3) {
   // part2 (MU, fp64/fp32 only; pruned scoring): the column partial sum_r k*_r^2
   // as well, for the tail bound of the variance (gp.hip k_prune_bound)
   // TS = _Float16 (h3): k* * kscale split into fp16 hi + lo, stored candidate-major
@@ -349,7 +359,7 @@ __global__ __launch_bounds__(K_NT, 2) void k_gp_kstar(const double* __restrict__
       hc[jj] = col0 + cl < m ? hv : -1e300;
     }
     const bool want2 = !PERM && MU && part2 != nullptr;
-    double s[4] = {0.0, 0.0, 0.0, 0.0}, s2[4] = {0.0, 0.0, 0.0, 0.0};
+    double s[4] = {0.0, 0.0, 0.0, 0.0}, s2[4] = {0.0, 0.0, 0.0, 0.0}, s3[4] = {0.0, 0.0, 0.0, 0.0};
     if constexpr (H3) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -457,8 +467,45 @@ __global__ __launch_bounds__(K_NT, 2) void k_gp_kstar(const double* __restrict__
           }
         }
       };
-      if (rt < store_rt) epi(std::integral_constant<bool, true>{});
-      else epi(std::integral_constant<bool, false>{});
+      if constexpr (F32E) {
+        // the stored bound rows keep the fp64 epilogue (exact k*: their |L^-1 k*|
+        // needs no error term, and their |alpha| k* partial stays 0); every other
+        // tile: k* = sf2 2^(t / 256) in f32 (alpha scaled by sf2 in f32, k*^2 by
+        // sf2^2 at the end)
+        if (rt < store_rt) {
+          epi(std::integral_constant<bool, true>{});
+        } else {
+          float fs[4] = {0.f, 0.f, 0.f, 0.f}, fa[4] = {0.f, 0.f, 0.f, 0.f}, f2[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int rl = wm * 64 + i * 16 + (lane >> 4) + 4 * r;
+              const double hv = (-0.5 * KSTAR_T_SCALE) * rowop[rl];
+              const double hx = row0 + rl < n ? hv : -1e300;
+              const float al = (float)(rowop[K_BM + rl] * sf2);
+              const float aa = __builtin_fabsf(al);
+#pragma unroll
+              for (int jj = 0; jj < 4; ++jj) {
+                const float tf = (float)((acc[i][jj][r] + hx) + hc[jj]) * 0x1p-8f;   // log2 units (-inf: padding)
+                const float kf = __builtin_amdgcn_exp2f(tf);
+                fs[jj] = __builtin_fmaf(al, kf, fs[jj]);
+                fa[jj] = __builtin_fmaf(aa, kf, fa[jj]);
+                f2[jj] = __builtin_fmaf(kf, kf, f2[jj]);
+              }
+            }
+          }
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj) {
+            s[jj] = fs[jj];
+            s3[jj] = fa[jj];
+            s2[jj] = (double)f2[jj] * (sf2 * sf2);
+          }
+        }
+      } else {
+        if (rt < store_rt) epi(std::integral_constant<bool, true>{});
+        else epi(std::integral_constant<bool, false>{});
+      }
     }
     if constexpr (MU) {
 #pragma unroll
@@ -474,6 +521,12 @@ __global__ __launch_bounds__(K_NT, 2) void k_gp_kstar(const double* __restrict__
           b += __shfl_xor(b, 32);
           if ((lane >> 4) == 0) red[2 * K_BN + wm * K_BN + cl] = b;
         }
+        if constexpr (F32E) {
+          double b = s3[jj];
+          b += __shfl_xor(b, 16);
+          b += __shfl_xor(b, 32);
+          if ((lane >> 4) == 0) red[4 * K_BN + wm * K_BN + cl] = b;
+        }
       }
     }
     if constexpr (MU) __syncthreads();
@@ -483,6 +536,7 @@ __global__ __launch_bounds__(K_NT, 2) void k_gp_kstar(const double* __restrict__
         if (col < m) {
           part[(int64_t)rt * ldk + col] = red[t] + red[K_BN + t];
           if (want2) part2[(int64_t)rt * ldk + col] = red[2 * K_BN + t] + red[3 * K_BN + t];
+          if constexpr (F32E) part3[(int64_t)rt * ldk + col] = red[4 * K_BN + t] + red[5 * K_BN + t];
         }
       }
     }
@@ -493,7 +547,7 @@ int h3_kstar_exp(double sf2) { return H3_KSCALE_EXP - ilogb(sf2); }  // sf2 * 2^
 
 int launch_gemm_kstar(ut_ctx* c, int prec, const double* XsT, int32_t npad, const double* ucand, int32_t dpad,
                       int64_t m, void* kst, int64_t ldk, double* part, int32_t store_rows, const double* cn,
-                      double* part2, const KstarCat& cat, const double* xn) {
+                      double* part2, const KstarCat& cat, const double* xn, double* part3) {
   const bool has_cat = cat.nkc > 0;
   UT_CHECK(c, npad % K_BM == 0 && dpad % 4 == 0 && (dpad >= 4 || has_cat) && ldk % K_BN == 0 && ldk >= m, UT_EINVAL,
            "gemm_kstar: bad padding");
@@ -501,6 +555,8 @@ int launch_gemm_kstar(ut_ctx* c, int prec, const double* XsT, int32_t npad, cons
   UT_CHECK(c, prec == 64 || prec == 32 || prec == 16 || prec == 8, UT_EINVAL, "gemm_kstar: bad precision");
   UT_CHECK(c, part != nullptr || prec == 64, UT_EINVAL,
            "gemm_kstar: fp32 / h3 mode takes the mean partial here");
+  UT_CHECK(c, !part3 || (prec == 64 && part && part2), UT_EINVAL,
+           "gemm_kstar: the f32 bound epilogue takes the fp64 mean, k*^2 and |alpha| k* partials");
   const int32_t RT = npad / K_BM;
   const int32_t CT = (int32_t)(ldk / K_BN);  // every column of K* (zeros past m) is written
   // fp64: only the first store_rows rows of K* are written (the mean still
@@ -519,15 +575,15 @@ int launch_gemm_kstar(ut_ctx* c, int prec, const double* XsT, int32_t npad, cons
   UT_HIP(c, hipMemsetAsync(c->gp_ctr + 8, 0, sizeof(int32_t) * 8, c->stream));
   const double* xnorm = xn ? xn : c->gp_xnorm;
   const double* cnorm = cn ? cn : c->cnorm.p;
-#define UT_KSTAR_LAUNCH(TS, MU, CAT, KST, PART, KSCALE, LOOFF, SRT, PART2)                                         \
-  hipLaunchKernelGGL((k_gp_kstar<TS, MU, CAT>), dim3(nb), dim3(K_NT), 0, c->stream, XsT, (int64_t)npad, ucand, ldk, \
-                     dpad, RT, CT, xnorm, cnorm, c->gp_alpha, c->gp_sf2, c->gp_n, m, c->gp_ctr + 8, KST, ldk, PART, \
-                     KSCALE, LOOFF, SRT, PART2, cat.acat, cat.bcat, cat.nkc, cat.c0 * KSTAR_T_SCALE,        \
-                     cat.c1 * KSTAR_T_SCALE)
-#define UT_KSTAR_BOTH(TS, MU, ...)                   \
-  do {                                               \
-    if (has_cat) UT_KSTAR_LAUNCH(TS, MU, true, __VA_ARGS__); \
-    else UT_KSTAR_LAUNCH(TS, MU, false, __VA_ARGS__);        \
+#define UT_KSTAR_LAUNCH(TS, MU, CAT, F32E, KST, PART, KSCALE, LOOFF, SRT, PART2)                                   \
+  hipLaunchKernelGGL((k_gp_kstar<TS, MU, CAT, F32E>), dim3(nb), dim3(K_NT), 0, c->stream, XsT, (int64_t)npad, ucand, \
+                     ldk, dpad, RT, CT, xnorm, cnorm, c->gp_alpha, c->gp_sf2, c->gp_n, m, c->gp_ctr + 8, KST, ldk, \
+                     PART, KSCALE, LOOFF, SRT, PART2, cat.acat, cat.bcat, cat.nkc, cat.c0 * KSTAR_T_SCALE,        \
+                     cat.c1 * KSTAR_T_SCALE, part3)
+#define UT_KSTAR_BOTH(TS, MU, ...)                                 \
+  do {                                                             \
+    if (has_cat) UT_KSTAR_LAUNCH(TS, MU, true, false, __VA_ARGS__); \
+    else UT_KSTAR_LAUNCH(TS, MU, false, false, __VA_ARGS__);        \
   } while (0)
   if (prec == 16)
     UT_KSTAR_BOTH(_Float16, true, (_Float16*)kst, part, ldexp(1.0, h3_kstar_exp(c->gp_sf2)), ldk * (int64_t)npad, RT,
@@ -537,7 +593,10 @@ int launch_gemm_kstar(ut_ctx* c, int prec, const double* XsT, int32_t npad, cons
                   nullptr);
   else if (prec == 32)
     UT_KSTAR_BOTH(float, true, (float*)kst, part, 1.0, (int64_t)0, RT, nullptr);
-  else if (part)   // fp64 with the mean k* . alpha in the epilogue (pruned scoring: needs the whole fit)
+  else if (part3) {   // pruned scoring's f32 bound pass
+    if (has_cat) UT_KSTAR_LAUNCH(double, true, true, true, (double*)kst, part, 1.0, (int64_t)0, store_rt, part2);
+    else UT_KSTAR_LAUNCH(double, true, false, true, (double*)kst, part, 1.0, (int64_t)0, store_rt, part2);
+  } else if (part)   // fp64 with the mean k* . alpha in the epilogue (pruned scoring: needs the whole fit)
     UT_KSTAR_BOTH(double, true, (double*)kst, part, 1.0, (int64_t)0, store_rt, part2);
   else
     UT_KSTAR_BOTH(double, false, (double*)kst, part, 1.0, (int64_t)0, store_rt, nullptr);

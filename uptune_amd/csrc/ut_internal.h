@@ -317,8 +317,13 @@ struct ut_ctx {
   ut::DevBuf<double> var_vbuf;                 // split variance: raw partial tiles [items][128][128]
   ut::DevBuf<double> app_ws;                   // split-K partials of the incremental fit [b][maxq][64][64]
   ut::DevBuf<double> pr_k2;                    // [RT][ldk] partials of |k*|^2 (the variance tail bound)
-  ut::DevBuf<double> pr_f2;                    // [1] |L^-1|_F^2 (+ its block partials)
+  ut::DevBuf<double> pr_f2;                    // [1] |L^-1|_F^2 (+ its block partials), then the f32
+                                               // pass's sum |alpha|
   bool pr_f2_valid = false;                    // pr_f2 belongs to the current fit
+  bool pr_ab_valid = false;                    // ... and its sum |alpha|
+  ut::DevBuf<double> pr_sa;                    // [RT][ldk] partials of sum |alpha_r| k*_r (f32 bound pass)
+  ut::DevBuf<double> pr_gmu;                   // [RT][ldc] fp64 mean partials of recomputed columns (f32 pass)
+  int32_t prune_pass = 32;                     // ut_gp_set_prune_pass: the bound pass's k* in f32 or fp64
   ut::DevBuf<uint8_t> pr_exact;                // [ld] the stored score is the exact score
   int64_t r_ld = 0;
   int64_t r_m = 0;
@@ -500,7 +505,8 @@ int launch_gemm_kstar(ut_ctx* c, int prec, const double* XsT, int32_t npad, cons
                       const double* cn = nullptr,    // candidate norms (nullptr: c->cnorm)
                       double* part2 = nullptr,       // fp64 with part: also sum_r k*_r^2 partials
                       const KstarCat& cat = KstarCat(),
-                      const double* xn = nullptr);   // training norms (nullptr: c->gp_xnorm)
+                      const double* xn = nullptr,    // training norms (nullptr: c->gp_xnorm)
+                      double* part3 = nullptr);      // f32 bound pass: sum_r |alpha_r| k*_r partials
 int launch_prep_cand(ut_ctx* c, const double* feat, int64_t ld, int64_t m, int32_t d, int32_t dpad, double* u,
                      int64_t ldu, double* cn);
 // categorical K*: the K* operands of the candidate side when the fit is in

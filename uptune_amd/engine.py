@@ -286,6 +286,10 @@ class BatchEngine:
         bits = {"f16x3": 16, "i8": 8}.get(bits, bits)
         L.check(self.ctx, self.lib.ut_gp_set_precision(self.ctx, int(bits)), "ut_gp_set_precision")
 
+    def gp_set_prune_pass(self, bits: int):
+        """gp_topk_pruned's bound pass: 32 (default, f32 k* with bounded rounding) or 64 (fp64)"""
+        L.check(self.ctx, self.lib.ut_gp_set_prune_pass(self.ctx, int(bits)), "ut_gp_set_prune_pass")
+
     def gp_set_i8_tol(self, tol: float):
         """precision 8: largest accepted relative variance error (0: recompute all in fp64)"""
         L.check(self.ctx, self.lib.ut_gp_set_i8_tol(self.ctx, float(tol)), "ut_gp_set_i8_tol")
