@@ -387,8 +387,8 @@ def main():
                     help="selection-exact EI-bound pruning (ut_score_round_de_pruned) with the first ROWS rows of "
                          "L^-1 k* as the bound; a secondary line, fp64 only (the dense round stays the headline)")
     ap.add_argument("--prune-pass", type=int, default=32, choices=(32, 64),
-                    help="--prune's bound pass over every candidate: 32 = k* in f32 past the bound rows with every "
-                         "rounding bounded (ut_gp_set_prune_pass; the default), 64 = fp64")
+                    help="--prune's bound pass over every candidate: 32 = K* past the bound rows on the f32 MFMA "
+                         "with v_exp_f32, every rounding bounded (ut_gp_set_prune_pass; the default), 64 = fp64")
     args = ap.parse_args()
     if args.precision is None:
         args.precision = 64 if args.prune else 8
@@ -667,15 +667,22 @@ def main():
         var_ms = stages.get("kstar")
         k64 = kstar_fp64_features(eng, d)
         flops_var = 2.0 * m * n * k64
-        kernel = ("k_gp_kstar<double, true, %s, %s> (K* with the mean k* . alpha in its epilogue, "
-                  "v_mfma_f64_16x16x4_f64 over %d fp64 features%s%s) [pruned round: the variance GEMM runs for the "
-                  "survivors only]" % ("true" if k64 < d else "false", "true" if args.prune_pass == 32 else "false",
-                                       k64, " + the one-hot codes on v_mfma_i32_16x16x64_i8" if k64 < d else "",
-                                       "; bound pass: k* = sf2 2^t by v_exp_f32 past the bound rows, rounding "
-                                       "bounded" if args.prune_pass == 32 else ""))
+        if args.prune_pass == 32:
+            kernel = ("k_gp_kstar_f32c<%s> (the bound pass: K* with the mean k* . alpha in its epilogue, "
+                      "v_mfma_f32_16x16x4f32 over %d features%s, k* by v_exp_f32, every rounding bounded; the "
+                      "bound rows in fp64) [pruned round: the variance GEMM runs for the survivors only; peak = "
+                      "the f32 MFMA's]" % ("true" if k64 < d else "false", k64,
+                                            " + the one-hot codes on v_mfma_i32_16x16x64_i8" if k64 < d else ""))
+        else:
+            kernel = ("k_gp_kstar<double, true, %s> (K* with the mean k* . alpha in its epilogue, "
+                      "v_mfma_f64_16x16x4_f64 over %d fp64 features%s) [pruned round: the variance GEMM runs for "
+                      "the survivors only]" % ("true" if k64 < d else "false", k64,
+                                               " + the one-hot codes on v_mfma_i32_16x16x64_i8" if k64 < d else ""))
     achieved = flops_var / (var_ms * 1e-3) / 1e12 if var_ms else None
     peak = {64: PEAK_FP64_TFLOPS, 32: PEAK_FP32_TFLOPS, 16: PEAK_FP16_TFLOPS / 3.0,
             8: PEAK_I8_TOPS / I8_PRODUCTS}[args.precision]
+    if args.prune and args.prune_pass == 32:
+        peak = PEAK_FP32_TFLOPS   # the bound pass's contraction runs on the f32 MFMA
     # HBM bytes per launch and the rocprof average duration were profiled on the
     # default C2 round (profiles/pmc_summary.json)
     profiled = args.config == "c2" and (m, n, d) == (1 << 20, 1024, 64) and not args.prune

@@ -317,14 +317,14 @@ int ut_gp_topk_pruned(ut_ctx* ctx, const double* features, int64_t ld, int64_t m
  * fp64.  Replaces the variance half of the per-candidate GP posterior the
  * reference has none of; precision 8 scores need n <= 16384. */
 int ut_gp_set_precision(ut_ctx* ctx, int32_t bits);
-/* ut_gp_topk_pruned's bound pass over every candidate: 32 (default) computes
- * k* = sf2 2^t in f32 from the fp64 distance contraction (v_exp_f32, f32 tile
- * sums) and bounds every rounding in the score bound (|k*^ - k*| <= 2^-17 k*^
- * + 2^-125 sf2, the mean within 2^-16 sum |alpha| k*^, the bound rows' |L^-1
- * k*| within |L_R^-1|_F times that); the threshold set and the survivors are
- * then scored in fp64 with the dense path's mean (L^-1 k*) . (L^-1 y), so the
- * selection is the dense one.  64: the bound pass in fp64 (its mean k* . alpha
- * exact and reused for the survivors). */
+/* ut_gp_topk_pruned's bound pass over every candidate: 32 (default) runs the
+ * distance contraction past the bound rows on the f32 MFMA and k* = sf2 2^t
+ * by v_exp_f32, and widens each candidate's score bound by every rounding of
+ * it (|k*^ - k*| <= rho k*^ + 2^-125 sf2 with rho from the contraction length
+ * and the norms; the mean within (rho + 2^-19) sum |alpha| k*^; the bound rows
+ * stay fp64); the threshold set and the survivors are then scored in fp64
+ * (mean k* . alpha), so the selection is the dense one.  64: the bound pass in
+ * fp64 (its mean exact and reused for the survivors). */
 int ut_gp_set_prune_pass(ut_ctx* ctx, int32_t bits);
 /* precision 8: the largest accepted relative error of a candidate's variance
  * (default 2^-20); 0 recomputes every candidate in fp64 */

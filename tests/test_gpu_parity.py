@@ -924,7 +924,8 @@ def test_gp_topk_pruned_equals_dense(acq, bound_rows, prune_pass):
     training points drawn from the population the candidates come from, so
     many candidates sit near training data and their bound is loose -- equals
     the dense device top-k and the oracle's; the survivors are a strict subset.
-    Both bound passes: f32 k* with its rounding bounded (32, the default) and fp64"""
+    Both bound passes: f32 contraction and k* with every rounding bounded (32,
+    the default) and fp64"""
     space = mixed_space()
     e = engine(space, seed=8)
     e.gp_set_prune_pass(prune_pass)

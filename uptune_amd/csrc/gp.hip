@@ -1152,6 +1152,7 @@ int gp_fit_enqueue(ut_ctx* c, const double* X, const double* y, int32_t n, int32
   if (rc) return rc;
   c->pr_f2_valid = false;   // |L^-1|_F^2 (pruned scoring) belongs to the previous factor
   c->pr_ab_valid = false;
+  c->pr_xf_valid = false;
   const size_t need = (size_t)n * d + n + d;
   bool fresh = false;   // a new staging buffer holds no previous rows
   if (c->fit_host_n < need) {
@@ -1469,26 +1470,30 @@ __global__ void k_prune_bound(int64_t m, int32_t RTm, const double* __restrict__
   if (exact_out) exact_out[i] = exact ? 1 : 0;
 }
 
-// The bound of the f32 pass (ut_gp_set_prune_pass 32; K* by k_gp_kstar<double,
-// true, *, true>: the stored bound rows in fp64 as before, every other k*^ =
-// sf2 2^t^ with |k*^ - k*| <= 2^-17 k*^ + 2^-125 sf2, its f32 tile sums within
-// 2^-16 of sum |alpha| k*^ together with that).  Per candidate:
-//   mean  |mu - mu^| <= dmu = 2^-16 S + 2^-125 sf2 sum|alpha| + RT 2^-51
-//         sum_rt |mu^_rt|: S = sum_r |alpha_r| k*^_r over the f32 rows (part3),
+// The bound of the f32 pass (ut_gp_set_prune_pass 32, k_gp_kstar_f32c): the
+// stored bound rows in fp64 as before, every other k*^ = sf2 2^t^ with |k*^ -
+// k*| <= rho k*^ / (1 - rho) + 2^-125 sf2 (v_exp_f32 flushes below 2^-126), its
+// f32 tile sums within 2^-19 of sum |alpha| k*^.  rho = 2^dt (1 + 2^-21) - 1 per
+// candidate, dt = (Kc + 9) 2^-24 (2 |c0| + max_r |x_r|^2 + |u|^2) / ln 2 (log2
+// units; Kc the contraction length, c0 the categorical offset; the f32
+// contraction's bound, see k_gp_kstar_f32c).  Per candidate:
+//   mean  |mu - mu^| <= dmu = (rho / (1 - rho) + 2^-19) S + 2^-125 sf2 sum|alpha|
+//         + RT 2^-51 sum_rt |mu^_rt|: S = sum_r |alpha_r| k*^_r over the f32 rows (part3),
 //         mu the fp64 k* . alpha the survivors are scored with (k_gp_kstar's
 //         fp64 epilogue on their columns: its bound-row tile partials are these
 //         bitwise, its other tiles within the first term; the last term the
 //         different rounding of the two sums over tiles);
 //   bound rows  exact k*: var <= var_ub = sf2 - |v^_R|^2 (as k_prune_bound);
 //   lower end (rows past R: |L^-1|_F^2 |k*|^2 as k_prune_bound's tail)
-//         var >= var_lo = sf2 - (|v^_R|^2 + 1.001 |L^-1|_F^2 ((1 + 2^-16) |k*^|^2 +
-//         n (2^-125 sf2)^2));
+//         var >= var_lo = sf2 - (|v^_R|^2 + 1.001 |L^-1|_F^2 ((1 + rho') |k*^| +
+//         sqrt(n) 2^-125 sf2)^2);
 // the score bound is the acquisition at (mu^ - dmu, var_ub), raised by
 // k_prune_bound's 1e-12 margin -- unless both ends pin the exact score: var_lo
 // == var_ub and the mean's two ends give the same I = f_best - mu - xi (EI) or
 // the same score (UCB); then the exact score is that double, stored as is and
 // flagged exact (a flat GP keeps its index tie-break).  fp64 rounding of the
-// sums: a 2^-36 margin.  cst: [0] |L^-1|_F^2, [1 + SQ_BLOCKS] sum |alpha|.
+// sums: a 2^-36 margin.  cst: [0] |L^-1|_F^2, [1 + SQ_BLOCKS] sum |alpha|,
+// [2 + SQ_BLOCKS] max_r |x_r|^2.
 constexpr int SQ_BLOCKS = 1024;
 __global__ void k_prune_bound32(int64_t m, int32_t RTm, const double* __restrict__ mu_part,
                                 const double* __restrict__ sa_part, const double* __restrict__ k2_part, int32_t RTv,
@@ -1496,7 +1501,8 @@ __global__ void k_prune_bound32(int64_t m, int32_t RTm, const double* __restrict
                                 const double* __restrict__ stats, const int32_t* __restrict__ fit_flag, int32_t kind,
                                 double xi, double kappa, const uint8_t* __restrict__ dup,
                                 const double* __restrict__ cst, double* __restrict__ ub_out,
-                                uint8_t* __restrict__ exact_out) {
+                                uint8_t* __restrict__ exact_out, int32_t Kc, double c0abs,
+                                const double* __restrict__ cnorm) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= m) return;
   double mu = 0.0, mabs = 0.0, sa = 0.0, k2 = 0.0, vs = 0.0;
@@ -1510,10 +1516,16 @@ __global__ void k_prune_bound32(int64_t m, int32_t RTm, const double* __restrict
   for (int32_t r = 0; r < RTv; ++r) vs += var_part[(int64_t)r * ldp + i];
   const double F2 = cst[0], A1 = cst[1 + SQ_BLOCKS];
   const double tiny = 0x1p-125 * sf2;
-  const double dmu = (0x1p-16 * sa + tiny * A1 + (double)RTm * 0x1p-51 * mabs) * (1.0 + 0x1p-20);
+  const double dt = (Kc + 9.0) * 0x1p-24 * (2.0 * c0abs + cst[2 + SQ_BLOCKS] + cnorm[i]) * 1.4426950408889634 *
+                        (1.0 + 0x1p-20) + Kc * 0x1p-120;
+  const double rho = (exp2(dt) * (1.0 + 0x1p-21) - 1.0) * (1.0 + 0x1p-20) + 0x1p-50;
+  const double rp = rho / (1.0 - rho);   // |k*^ - k*| / k*^ (rho < 1/2, or the bound is useless: NaN below)
+  const double dmu = ((rp + 0x1p-19) * sa * (1.0 + 0x1p-18) + tiny * A1 + (double)RTm * 0x1p-51 * mabs) *
+                     (1.0 + 0x1p-20);
   double var_ub = sf2 - vs;   // the bound rows' partials: bitwise the exact GEMM's first RTv (k_prune_bound)
   var_ub = var_ub > 0.0 ? var_ub : 0.0;
-  const double tail = 1.001 * F2 * ((1.0 + 0x1p-16) * k2 + (double)n * tiny * tiny);
+  const double kn = (1.0 + rp) * sqrt(k2 * (1.0 + 0x1p-18)) + sqrt((double)n) * tiny;
+  const double tail = 1.001 * F2 * kn * kn;
   double var_lo = sf2 - (vs + tail) * (1.0 + 0x1p-36);
   var_lo = var_lo > 0.0 ? var_lo : 0.0;
   double ub = acq_score(kind, mu - dmu, var_ub, stats[0], xi, kappa);
@@ -1525,13 +1537,28 @@ __global__ void k_prune_bound32(int64_t m, int32_t RTm, const double* __restrict
       exact = (stats[0] - (mu - dmu) - xi) == (stats[0] - (mu + dmu) - xi);
   }
   if (!exact) ub = ub + fabs(ub) * 1e-12 + 1e-300;
-  if (*fit_flag != 0 || ub != ub) {
+  if (!(rho < 0.5)) {   // no usable bound: the candidate survives
+    ub = 1.0 / 0.0;
+    exact = false;
+  }
+  if (*fit_flag != 0) {
     ub = __builtin_nan("");
     exact = false;
   }
   if (dup && dup[i]) ub = -1.0 / 0.0;
   ub_out[i] = ub;
   exact_out[i] = exact ? 1 : 0;
+}
+
+// max of x[0 .. n) (one workgroup): the f32-contraction bound's max_r |x_r|^2
+__global__ __launch_bounds__(256) void k_max_n(const double* __restrict__ x, int32_t n, double* __restrict__ out) {
+  __shared__ double red[4];
+  double v = 0.0;
+  for (int32_t e = threadIdx.x; e < n; e += 256) v = fmax(v, x[e]);
+  for (int d = 32; d > 0; d >>= 1) v = fmax(v, __shfl_xor(v, d, 64));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) *out = fmax(fmax(red[0], red[1]), fmax(red[2], red[3]));
 }
 
 // sum of squares of cnt doubles (|L^-1|_F^2), deterministic: pass 1 writes one
@@ -1722,9 +1749,9 @@ int gp_topk_pruned_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, co
   if ((rc = ensure(c, c->pr_idx, (size_t)ldk + 2048))) return rc;
   if ((rc = ensure(c, c->pr_count, 1))) return rc;
   if ((rc = ensure(c, c->pr_k2, (size_t)RT * ldk))) return rc;
-  // [0] |L^-1|_F^2, [1..] block partials, then the f32 pass's sum |alpha|
-  if ((rc = ensure(c, c->pr_f2, 2 + SQ_BLOCKS))) return rc;
-  const bool f32 = c->prune_pass == 32;
+  // [0] |L^-1|_F^2, [1..] block partials, then the f32 passes' sum |alpha|, max |x|^2
+  if ((rc = ensure(c, c->pr_f2, 3 + SQ_BLOCKS))) return rc;
+  const bool f32 = c->prune_pass == 32;   // the bound pass in f32 (k_gp_kstar_f32c)
   if (f32 && (rc = ensure(c, c->pr_sa, (size_t)RT * ldk))) return rc;
   if (f32 && (rc = ensure(c, c->pr_gmu, (size_t)RT * (ldk + 1024)))) return rc;   // survivors / threshold set
   if ((rc = ensure(c, c->pr_exact, (size_t)ldk))) return rc;
@@ -1745,10 +1772,32 @@ int gp_topk_pruned_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, co
   // candidates that need every row (threshold set, survivors) get their K*
   // columns recomputed from their features (recompute_cols below): cheaper than
   // writing and re-reading the whole n x m matrix
-  if ((rc = launch_gemm_kstar(c, 64, XsT, npad, c->ucand.p, dpad, m, c->kst.p, ldk, c->mu_part.p, R * NPAD,
-                              nullptr, c->pr_k2.p, cat ? kstar_cat(c, c->bcat.p) : KstarCat(), xn,
-                              f32 ? c->pr_sa.p : nullptr)))
+  if (f32) {
+    // the bound rows through the fp64 kernel (tiles < R), every other tile
+    // through k_gp_kstar_f32c on f32 copies of the operands (Xs^T once per fit)
+    const double* xnn = xn ? xn : c->gp_xnorm;
+    if (!c->pr_xf_valid) {
+      if ((rc = ensure(c, c->pr_xsT_f, (size_t)dpad * npad))) return rc;
+      if ((rc = launch_to_f32(c, XsT, c->pr_xsT_f.p, (int64_t)dpad * npad))) return rc;
+      hipLaunchKernelGGL(k_max_n, dim3(1), dim3(256), 0, c->stream, xnn, n, c->pr_f2.p + 2 + SQ_BLOCKS);
+      UT_LAUNCH_CHECK(c);
+      c->pr_xf_valid = true;
+    }
+    if ((rc = ensure(c, c->pr_ucand_f, (size_t)(dpad > 0 ? dpad : 1) * ldk))) return rc;
+    if ((rc = launch_to_f32(c, c->ucand.p, c->pr_ucand_f.p, (int64_t)dpad * ldk))) return rc;
+    if ((rc = launch_gemm_kstar(c, 64, XsT, npad, c->ucand.p, dpad, m, c->kst.p, ldk, c->mu_part.p, R * NPAD,
+                                nullptr, c->pr_k2.p, cat ? kstar_cat(c, c->bcat.p) : KstarCat(), xn, R)))
+      return rc;
+    UT_HIP(c, hipMemsetAsync(c->pr_sa.p, 0, sizeof(double) * R * ldk, c->stream));
+    if (R < RT &&
+        (rc = launch_gemm_kstar_f32c(c, c->pr_xsT_f.p, npad, c->pr_ucand_f.p, dpad, m, ldk, R, c->mu_part.p,
+                                     c->pr_k2.p, c->pr_sa.p, cat ? kstar_cat(c, c->bcat.p) : KstarCat(), xnn,
+                                     c->cnorm.p)))
+      return rc;
+  } else if ((rc = launch_gemm_kstar(c, 64, XsT, npad, c->ucand.p, dpad, m, c->kst.p, ldk, c->mu_part.p, R * NPAD,
+                                     nullptr, c->pr_k2.p, cat ? kstar_cat(c, c->bcat.p) : KstarCat(), xn))) {
     return rc;
+  }
   // |L^-1|_F^2 for the variance tail bound, once per fit (the block partials
   // in pr_f2[1..] are scratch, reused pass after pass in stream order)
   auto sumsq = [&](bool abs_, const double* x, int64_t cnt, double* out) -> int {
@@ -1778,7 +1827,8 @@ int gp_topk_pruned_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, co
   if (f32)
     hipLaunchKernelGGL(k_prune_bound32, dim3(grid1(m, 256)), dim3(256), 0, c->stream, m, RT, c->mu_part.p,
                        c->pr_sa.p, c->pr_k2.p, R, c->var_part.p, ldk, c->gp_sf2, n, c->gp_stats, c->gp_flag,
-                       acq->kind, acq->xi, acq->kappa, dup, c->pr_f2.p, c->pr_ub.p, c->pr_exact.p);
+                       acq->kind, acq->xi, acq->kappa, dup, c->pr_f2.p, c->pr_ub.p, c->pr_exact.p,
+                       dpad + (cat ? 1 : 0), cat ? fabs(c->cat_c0) : 0.0, c->cnorm.p);
   else
     hipLaunchKernelGGL(k_prune_bound, dim3(grid1(m, 256)), dim3(256), 0, c->stream, m, RT, c->mu_part.p, R,
                        c->var_part.p, ldk, c->gp_sf2, c->gp_stats, c->gp_flag, acq->kind, acq->xi, acq->kappa, dup,

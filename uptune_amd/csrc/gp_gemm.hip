@@ -156,16 +156,7 @@ __device__ __forceinline__ void kcat_issue(const int8_t* __restrict__ Ab, const 
 
 // MU: also the column partial of the mean, sum_r alpha_r k*_r (fp32 scoring;
 // fp64 takes the mean from the variance epilogue instead)
-// F32E (TS = double, MU; pruned scoring's bound pass, ut_gp_set_prune_pass 32):
-// past the stored bound rows, the exponent t from the fp64 accumulator as
-// before, then k* = sf2 2^(t/256) by v_exp_f32 and the tile partials of k*
-// alpha, k* |alpha| (part3) and k*^2 (part2) as f32 sums: ~7 VALU ops per k*
-// where the fp64 epilogue takes ~15 DP ops (the f64 MFMA does not issue beside
-// the VALU, so the epilogue is ~half of K*).  Every error is bounded in
-// k_prune_bound32: |k*^ - k*| <= 2^-17 k*^ + 2^-125 sf2 (t in f32: |t / 256| <=
-// 126 for a k* that is not flushed, 7.5e-6 in log2 units; v_exp_f32), the f32
-// sums within 2^-16 of sum |alpha| k*^ together with that.
-template <typename TS, bool MU, bool CAT, bool F32E>
+template <typename TS, bool MU, bool CAT>
 __global__ __launch_bounds__(K_NT, 2) void k_gp_kstar(const double* __restrict__ AT, int64_t lda,
                                                       const double* __restrict__ B, int64_t ldb, int32_t dpad,
                                                       int32_t RT, int32_t CT, const double* __restrict__ xnorm,
@@ -175,8 +166,7 @@ __global__ __launch_bounds__(K_NT, 2) void k_gp_kstar(const double* __restrict__
                                                       int64_t ldk, double* __restrict__ part, double kscale,
                                                       int64_t lo_off, int32_t store_rt, double* __restrict__ part2,
                                                       const int8_t* __restrict__ acat, const int8_t* __restrict__ bcat,
-                                                      int32_t nkc, double cat_c0, double cat_c1,
-                                                      double* __restrict__ part3) {
+                                                      int32_t nkc, double cat_c0, double cat_c1, int32_t RTe) {
   // part2 (MU, fp64/fp32 only; pruned scoring): the column partial sum_r k*_r^2
   // as well, for the tail bound of the variance (gp.hip k_prune_bound)
   // TS = _Float16 (h3): k* * kscale split into fp16 hi + lo, stored candidate-major
@@ -235,10 +225,11 @@ __global__ __launch_bounds__(K_NT, 2) void k_gp_kstar(const double* __restrict__
     if (t == 0) s_item = nxt;
     __syncthreads();
     const int32_t j = s_item;
-    const int32_t ct = (j / RT) * 8 + xcd;
+    // (RTe <= RT: the item's row tiles; RT sizes the operands' layout)
+    const int32_t ct = (j / RTe) * 8 + xcd;
     if (ct >= CT) break;
     if (t == 0) nxt = atomicAdd(&ticket[xcd], 1);
-    const int32_t rt = j % RT;
+    const int32_t rt = j % RTe;
     const int64_t col0 = (int64_t)ct * K_BN;
     const int32_t row0 = rt * K_BM;
 
@@ -359,7 +350,7 @@ __global__ __launch_bounds__(K_NT, 2) void k_gp_kstar(const double* __restrict__
       hc[jj] = col0 + cl < m ? hv : -1e300;
     }
     const bool want2 = !PERM && MU && part2 != nullptr;
-    double s[4] = {0.0, 0.0, 0.0, 0.0}, s2[4] = {0.0, 0.0, 0.0, 0.0}, s3[4] = {0.0, 0.0, 0.0, 0.0};
+    double s[4] = {0.0, 0.0, 0.0, 0.0}, s2[4] = {0.0, 0.0, 0.0, 0.0};
     if constexpr (H3) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -467,45 +458,8 @@ __global__ __launch_bounds__(K_NT, 2) void k_gp_kstar(const double* __restrict__
           }
         }
       };
-      if constexpr (F32E) {
-        // the stored bound rows keep the fp64 epilogue (exact k*: their |L^-1 k*|
-        // needs no error term, and their |alpha| k* partial stays 0); every other
-        // tile: k* = sf2 2^(t / 256) in f32 (alpha scaled by sf2 in f32, k*^2 by
-        // sf2^2 at the end)
-        if (rt < store_rt) {
-          epi(std::integral_constant<bool, true>{});
-        } else {
-          float fs[4] = {0.f, 0.f, 0.f, 0.f}, fa[4] = {0.f, 0.f, 0.f, 0.f}, f2[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const int rl = wm * 64 + i * 16 + (lane >> 4) + 4 * r;
-              const double hv = (-0.5 * KSTAR_T_SCALE) * rowop[rl];
-              const double hx = row0 + rl < n ? hv : -1e300;
-              const float al = (float)(rowop[K_BM + rl] * sf2);
-              const float aa = __builtin_fabsf(al);
-#pragma unroll
-              for (int jj = 0; jj < 4; ++jj) {
-                const float tf = (float)((acc[i][jj][r] + hx) + hc[jj]) * 0x1p-8f;   // log2 units (-inf: padding)
-                const float kf = __builtin_amdgcn_exp2f(tf);
-                fs[jj] = __builtin_fmaf(al, kf, fs[jj]);
-                fa[jj] = __builtin_fmaf(aa, kf, fa[jj]);
-                f2[jj] = __builtin_fmaf(kf, kf, f2[jj]);
-              }
-            }
-          }
-#pragma unroll
-          for (int jj = 0; jj < 4; ++jj) {
-            s[jj] = fs[jj];
-            s3[jj] = fa[jj];
-            s2[jj] = (double)f2[jj] * (sf2 * sf2);
-          }
-        }
-      } else {
-        if (rt < store_rt) epi(std::integral_constant<bool, true>{});
-        else epi(std::integral_constant<bool, false>{});
-      }
+      if (rt < store_rt) epi(std::integral_constant<bool, true>{});
+      else epi(std::integral_constant<bool, false>{});
     }
     if constexpr (MU) {
 #pragma unroll
@@ -521,12 +475,6 @@ __global__ __launch_bounds__(K_NT, 2) void k_gp_kstar(const double* __restrict__
           b += __shfl_xor(b, 32);
           if ((lane >> 4) == 0) red[2 * K_BN + wm * K_BN + cl] = b;
         }
-        if constexpr (F32E) {
-          double b = s3[jj];
-          b += __shfl_xor(b, 16);
-          b += __shfl_xor(b, 32);
-          if ((lane >> 4) == 0) red[4 * K_BN + wm * K_BN + cl] = b;
-        }
       }
     }
     if constexpr (MU) __syncthreads();
@@ -536,18 +484,259 @@ __global__ __launch_bounds__(K_NT, 2) void k_gp_kstar(const double* __restrict__
         if (col < m) {
           part[(int64_t)rt * ldk + col] = red[t] + red[K_BN + t];
           if (want2) part2[(int64_t)rt * ldk + col] = red[2 * K_BN + t] + red[3 * K_BN + t];
-          if constexpr (F32E) part3[(int64_t)rt * ldk + col] = red[4 * K_BN + t] + red[5 * K_BN + t];
         }
       }
     }
   }
 }
 
+// ---------------------------------------------------------------------------
+// Pruned scoring's bound pass in f32 (ut_gp_set_prune_pass 32, the default):
+// row tiles rt0 .. RT-1 of K* (the bound rows before rt0 run through
+// k_gp_kstar's fp64 epilogue), A = f32(Xs^T) and B = f32(U') on
+// v_mfma_f32_16x16x4f32 (1.9x the f64 MFMA's rate; C/D: col = lane & 15, row =
+// 4 (lane >> 4) + r, the i8 MFMA's map; scripts/exp/f32_mfma_probe.hip), then
+// from the f32 accumulator t = C + hx + hc in f32 (t in units of 2^(1/256), the
+// operands' KSTAR_T_SCALE), k* = sf2 2^(t/256) by v_exp_f32, and the tile
+// partials of k* alpha, k* |alpha| and k*^2 as f32 sums: ~7 VALU ops per k*
+// against the fp64 epilogue's ~15 DP ops, and the f32 MFMA, like the f64 one,
+// does not issue beside them.  Error (k_prune_bound32):
+// every partial sum of the contraction is at most |c0| + |x|^2/2 + |u|^2/2 in
+// magnitude (|x . u| <= (|x|^2 + |u|^2) / 2), so |t^ - t| <= (K + 9) 2^-24
+// (2 |c0| + |x|^2 + |u|^2) (units of t; K the contraction length: products
+// and sums rounded to f32, hx / hc rounded once, two adds).
+// ---------------------------------------------------------------------------
+typedef float kf4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void kstar_issue_f32(const float* __restrict__ AT, int64_t lda, const float* __restrict__ B,
+                                                int64_t ldb, int32_t row0, int64_t col0, int32_t k0, float* st, int w,
+                                                int lane, int32_t dpad) {
+  // 8 KiB of A and 8 KiB of B per 16-k stage: wave w loads k rows 4w .. 4w+3,
+  // two 512-B rows per 1-KiB glds (lanes 0-31 row q, 32-63 row q + 1)
+  if (k0 + 4 * w >= dpad) return;
+  const int rr = lane >> 5, cc = (lane & 31) * 4;
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int q = 4 * w + 2 * u;
+    __builtin_amdgcn_global_load_lds(AT + (int64_t)(k0 + q + rr) * lda + row0 + cc,
+                                     (__attribute__((address_space(3))) void*)(st + q * 128), 16, 0, 0);
+    __builtin_amdgcn_global_load_lds(B + (int64_t)(k0 + q + rr) * ldb + col0 + cc,
+                                     (__attribute__((address_space(3))) void*)(st + K_SA + q * 128), 16, 0, 0);
+  }
+}
+
+template <bool CAT>
+__global__ __launch_bounds__(K_NT, 2) void k_gp_kstar_f32c(const float* __restrict__ AT, int64_t lda,
+                                                           const float* __restrict__ B, int64_t ldb, int32_t dpad,
+                                                           int32_t rt0, int32_t RT, int32_t CT,
+                                                           const double* __restrict__ xnorm,
+                                                           const double* __restrict__ cnorm,
+                                                           const double* __restrict__ alpha, double sf2, int32_t n,
+                                                           int64_t m, int32_t* __restrict__ ticket, int64_t ldk,
+                                                           double* __restrict__ part, double* __restrict__ part2,
+                                                           double* __restrict__ part3, const int8_t* __restrict__ acat,
+                                                           const int8_t* __restrict__ bcat, int32_t nkc, float cat_c0,
+                                                           float cat_c1) {
+  // the ring (sized as k_gp_kstar's: the int8 stages fill it, the f32 ones half),
+  // the ticket slot, the item's row / column operands
+  __shared__ __attribute__((aligned(16))) double lds[2 * K_STAGE + 2 + 3 * K_BM];
+  int32_t& s_item = *reinterpret_cast<int32_t*>(lds + 2 * K_STAGE);
+  double* const rowop = lds + 2 * K_STAGE + 2;   // [xnorm 128][alpha 128][cnorm 128]
+  const int t = threadIdx.x, lane = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wm = w >> 1, wn = w & 1;
+  const int32_t xcd = blockIdx.x & 7;
+  const int32_t nk_full = dpad / K_BK, k_rem = (dpad % K_BK) / 4;
+  const int32_t nk = nk_full + (k_rem ? 1 : 0);
+  const int32_t ncs = CAT ? nkc : 0;
+  const int32_t ntot = ncs + nk;
+  const int npad_a = RT * K_BM;
+  const int32_t RTe = RT - rt0;
+  int32_t nxt = 0;
+  if (t == 0) nxt = atomicAdd(&ticket[xcd], 1);
+  for (;;) {
+    if (t == 0) s_item = nxt;
+    __syncthreads();
+    const int32_t j = s_item;
+    const int32_t ct = (j / RTe) * 8 + xcd;
+    if (ct >= CT) break;
+    if (t == 0) nxt = atomicAdd(&ticket[xcd], 1);
+    const int32_t rt = rt0 + j % RTe;
+    const int64_t col0 = (int64_t)ct * K_BN;
+    const int32_t row0 = rt * K_BM;
+    auto issue_stage = [&](int32_t s2, double* st) {
+      if (CAT && s2 < ncs)
+        kcat_issue(acat + ((int64_t)s2 * npad_a + row0) * 128, bcat + ((int64_t)s2 * ldb + col0) * 128, st, w, lane);
+      else
+        kstar_issue_f32(AT, lda, B, ldb, row0, col0, (s2 - ncs) * K_BK, reinterpret_cast<float*>(st), w, lane, dpad);
+    };
+    if (ntot > 0) issue_stage(0, lds);
+    {
+      const double* src = w == 0 ? xnorm + row0 : (w == 1 ? alpha + row0 : cnorm + col0);
+      if (w < 3)
+        __builtin_amdgcn_global_load_lds(src + lane * 2, (__attribute__((address_space(3))) void*)(rowop + w * K_BM),
+                                         16, 0, 0);
+    }
+    kf4 acc[4][4];
+    if constexpr (CAT) {
+      ki4 iacc[4][4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) iacc[i][jj] = (ki4){0, 0, 0, 0};
+      for (int32_t s2 = 0; s2 < ncs; ++s2) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (s2 + 1 < ntot) issue_stage(s2 + 1, lds + ((s2 + 1) & 1) * K_STAGE);
+        const int8_t* as8 = reinterpret_cast<const int8_t*>(lds + (s2 & 1) * K_STAGE);
+        const int8_t* bs8 = as8 + K_SA * 8;
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+          const int c16 = (lane >> 4) + 4 * kk;
+          ki4 af[4], bf[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int row = wm * 64 + i * 16 + (lane & 15);   // the f32 MFMA's rows are the i8 one's
+            af[i] = *reinterpret_cast<const ki4*>(as8 + row * 128 + ((c16 ^ (row & 7)) << 4));
+          }
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj) {
+            const int col = wn * 64 + jj * 16 + (lane & 15);
+            bf[jj] = *reinterpret_cast<const ki4*>(bs8 + col * 128 + ((c16 ^ (col & 7)) << 4));
+          }
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj)
+              iacc[i][jj] = __builtin_amdgcn_mfma_i32_16x16x64_i8(af[i], bf[jj], iacc[i][jj], 0, 0, 0);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[i][jj][r] = __builtin_fmaf((float)iacc[i][jj][r], cat_c1, cat_c0);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) acc[i][jj] = (kf4){0.f, 0.f, 0.f, 0.f};
+    }
+    for (int32_t s2 = ncs; s2 < ntot; ++s2) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      if (s2 + 1 < ntot) issue_stage(s2 + 1, lds + ((s2 + 1) & 1) * K_STAGE);
+      const float* as = reinterpret_cast<const float*>(lds + (s2 & 1) * K_STAGE);
+      const float* bs = as + K_SA;
+      const int32_t kt = s2 - ncs;
+      const int nks = kt < nk_full ? K_BK / 4 : k_rem;
+#pragma unroll
+      for (int ks = 0; ks < K_BK / 4; ++ks) {
+        if (ks >= nks) break;
+        const int kr = ks * 4 + (lane >> 4);
+        float af[4], bf[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) af[i] = as[kr * K_BM + wm * 64 + i * 16 + (lane & 15)];
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) bf[jj] = bs[kr * K_BN + wn * 64 + jj * 16 + (lane & 15)];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj)
+            acc[i][jj] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bf[jj], acc[i][jj], 0, 0, 0);
+      }
+    }
+    if (ntot == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();   // ring free: the column reduction buffer
+    double* red = lds;   // [6][128]
+    float hc[4];
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+      const int cl = wn * 64 + jj * 16 + (lane & 15);
+      hc[jj] = col0 + cl < m ? (float)((-0.5 * KSTAR_T_SCALE) * rowop[2 * K_BM + cl]) : -1.0f / 0.0f;
+    }
+    float fs[4] = {0.f, 0.f, 0.f, 0.f}, fa[4] = {0.f, 0.f, 0.f, 0.f}, f2[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int rl = wm * 64 + i * 16 + 4 * (lane >> 4) + r;
+        const float hx = row0 + rl < n ? (float)((-0.5 * KSTAR_T_SCALE) * rowop[rl]) : -1.0f / 0.0f;
+        const float al = (float)(rowop[K_BM + rl] * sf2);
+        const float aa = __builtin_fabsf(al);
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          const float kf = __builtin_amdgcn_exp2f(((acc[i][jj][r] + hx) + hc[jj]) * 0x1p-8f);
+          fs[jj] = __builtin_fmaf(al, kf, fs[jj]);
+          fa[jj] = __builtin_fmaf(aa, kf, fa[jj]);
+          f2[jj] = __builtin_fmaf(kf, kf, f2[jj]);
+        }
+      }
+    }
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+      const int cl = wn * 64 + jj * 16 + (lane & 15);
+      double a = fs[jj], b = f2[jj], q = fa[jj];
+      a += __shfl_xor(a, 16);
+      a += __shfl_xor(a, 32);
+      b += __shfl_xor(b, 16);
+      b += __shfl_xor(b, 32);
+      q += __shfl_xor(q, 16);
+      q += __shfl_xor(q, 32);
+      if ((lane >> 4) == 0) {
+        red[wm * K_BN + cl] = a;
+        red[2 * K_BN + wm * K_BN + cl] = b;
+        red[4 * K_BN + wm * K_BN + cl] = q;
+      }
+    }
+    __syncthreads();
+    if (t < K_BN) {
+      const int64_t col = col0 + t;
+      if (col < m) {
+        part[(int64_t)rt * ldk + col] = red[t] + red[K_BN + t];
+        part2[(int64_t)rt * ldk + col] = (red[2 * K_BN + t] + red[3 * K_BN + t]) * (sf2 * sf2);
+        part3[(int64_t)rt * ldk + col] = red[4 * K_BN + t] + red[5 * K_BN + t];
+      }
+    }
+  }
+}
+
+int launch_gemm_kstar_f32c(ut_ctx* c, const float* XsT_f, int32_t npad, const float* ucand_f, int32_t dpad,
+                           int64_t m, int64_t ldk, int32_t rt0, double* part, double* part2, double* part3,
+                           const KstarCat& cat, const double* xn, const double* cn) {
+  const bool has_cat = cat.nkc > 0;
+  UT_CHECK(c, npad % K_BM == 0 && dpad % 4 == 0 && (dpad >= 4 || has_cat) && ldk % K_BN == 0 && ldk >= m, UT_EINVAL,
+           "gemm_kstar_f32c: bad padding");
+  UT_CHECK(c, !has_cat || (cat.acat && cat.bcat), UT_EINVAL, "gemm_kstar_f32c: categorical operands missing");
+  UT_CHECK(c, part && part2 && part3, UT_EINVAL, "gemm_kstar_f32c: partial outputs missing");
+  const int32_t RT = npad / K_BM;
+  UT_CHECK(c, rt0 >= 0 && rt0 < RT, UT_EINVAL, "gemm_kstar_f32c: bad first row tile");
+  const int32_t CT = (int32_t)(ldk / K_BN);
+  const int64_t items = (int64_t)(RT - rt0) * CT;
+  int32_t nb = 2 * (c->n_cu / 8) * 8;
+  if (items < nb) nb = (int32_t)(((items + 7) / 8) * 8);
+  UT_HIP(c, hipMemsetAsync(c->gp_ctr + 8, 0, sizeof(int32_t) * 8, c->stream));
+  const float c0 = (float)(cat.c0 * KSTAR_T_SCALE), c1 = (float)(cat.c1 * KSTAR_T_SCALE);
+  if (has_cat)
+    hipLaunchKernelGGL(k_gp_kstar_f32c<true>, dim3(nb), dim3(K_NT), 0, c->stream, XsT_f, (int64_t)npad, ucand_f, ldk,
+                       dpad, rt0, RT, CT, xn, cn, c->gp_alpha, c->gp_sf2, c->gp_n, m, c->gp_ctr + 8, ldk, part, part2,
+                       part3, cat.acat, cat.bcat, cat.nkc, c0, c1);
+  else
+    hipLaunchKernelGGL(k_gp_kstar_f32c<false>, dim3(nb), dim3(K_NT), 0, c->stream, XsT_f, (int64_t)npad, ucand_f, ldk,
+                       dpad, rt0, RT, CT, xn, cn, c->gp_alpha, c->gp_sf2, c->gp_n, m, c->gp_ctr + 8, ldk, part, part2,
+                       part3, cat.acat, cat.bcat, cat.nkc, c0, c1);
+  UT_LAUNCH_CHECK(c);
+  return 0;
+}
+
 int h3_kstar_exp(double sf2) { return H3_KSCALE_EXP - ilogb(sf2); }  // sf2 * 2^e < 2^15
 
 int launch_gemm_kstar(ut_ctx* c, int prec, const double* XsT, int32_t npad, const double* ucand, int32_t dpad,
                       int64_t m, void* kst, int64_t ldk, double* part, int32_t store_rows, const double* cn,
-                      double* part2, const KstarCat& cat, const double* xn, double* part3) {
+                      double* part2, const KstarCat& cat, const double* xn, int32_t row_tiles) {
   const bool has_cat = cat.nkc > 0;
   UT_CHECK(c, npad % K_BM == 0 && dpad % 4 == 0 && (dpad >= 4 || has_cat) && ldk % K_BN == 0 && ldk >= m, UT_EINVAL,
            "gemm_kstar: bad padding");
@@ -555,14 +744,14 @@ int launch_gemm_kstar(ut_ctx* c, int prec, const double* XsT, int32_t npad, cons
   UT_CHECK(c, prec == 64 || prec == 32 || prec == 16 || prec == 8, UT_EINVAL, "gemm_kstar: bad precision");
   UT_CHECK(c, part != nullptr || prec == 64, UT_EINVAL,
            "gemm_kstar: fp32 / h3 mode takes the mean partial here");
-  UT_CHECK(c, !part3 || (prec == 64 && part && part2), UT_EINVAL,
-           "gemm_kstar: the f32 bound epilogue takes the fp64 mean, k*^2 and |alpha| k* partials");
   const int32_t RT = npad / K_BM;
+  // row_tiles: only the first row_tiles tiles (the f32-contraction bound pass's fp64 bound rows)
+  const int32_t RTe = row_tiles > 0 && row_tiles < RT ? row_tiles : RT;
   const int32_t CT = (int32_t)(ldk / K_BN);  // every column of K* (zeros past m) is written
   // fp64: only the first store_rows rows of K* are written (the mean still
   // sums every row); the other precisions always store everything
   const int32_t store_rt = store_rows < 0 ? RT : (store_rows + K_BM - 1) / K_BM;
-  const int64_t items = (int64_t)RT * CT;
+  const int64_t items = (int64_t)RTe * CT;
   // Two K* workgroups fill a CU's VGPRs, so a full persistent grid leaves no
   // slot for the GP fit running beside it on the fit stream, and the fit's
   // serial chain of small kernels then stalls the variance GEMM that waits for
@@ -575,15 +764,15 @@ int launch_gemm_kstar(ut_ctx* c, int prec, const double* XsT, int32_t npad, cons
   UT_HIP(c, hipMemsetAsync(c->gp_ctr + 8, 0, sizeof(int32_t) * 8, c->stream));
   const double* xnorm = xn ? xn : c->gp_xnorm;
   const double* cnorm = cn ? cn : c->cnorm.p;
-#define UT_KSTAR_LAUNCH(TS, MU, CAT, F32E, KST, PART, KSCALE, LOOFF, SRT, PART2)                                   \
-  hipLaunchKernelGGL((k_gp_kstar<TS, MU, CAT, F32E>), dim3(nb), dim3(K_NT), 0, c->stream, XsT, (int64_t)npad, ucand, \
-                     ldk, dpad, RT, CT, xnorm, cnorm, c->gp_alpha, c->gp_sf2, c->gp_n, m, c->gp_ctr + 8, KST, ldk, \
-                     PART, KSCALE, LOOFF, SRT, PART2, cat.acat, cat.bcat, cat.nkc, cat.c0 * KSTAR_T_SCALE,        \
-                     cat.c1 * KSTAR_T_SCALE, part3)
-#define UT_KSTAR_BOTH(TS, MU, ...)                                 \
-  do {                                                             \
-    if (has_cat) UT_KSTAR_LAUNCH(TS, MU, true, false, __VA_ARGS__); \
-    else UT_KSTAR_LAUNCH(TS, MU, false, false, __VA_ARGS__);        \
+#define UT_KSTAR_LAUNCH(TS, MU, CAT, KST, PART, KSCALE, LOOFF, SRT, PART2)                                         \
+  hipLaunchKernelGGL((k_gp_kstar<TS, MU, CAT>), dim3(nb), dim3(K_NT), 0, c->stream, XsT, (int64_t)npad, ucand, ldk, \
+                     dpad, RT, CT, xnorm, cnorm, c->gp_alpha, c->gp_sf2, c->gp_n, m, c->gp_ctr + 8, KST, ldk, PART, \
+                     KSCALE, LOOFF, SRT, PART2, cat.acat, cat.bcat, cat.nkc, cat.c0 * KSTAR_T_SCALE,        \
+                     cat.c1 * KSTAR_T_SCALE, RTe)
+#define UT_KSTAR_BOTH(TS, MU, ...)                   \
+  do {                                               \
+    if (has_cat) UT_KSTAR_LAUNCH(TS, MU, true, __VA_ARGS__); \
+    else UT_KSTAR_LAUNCH(TS, MU, false, __VA_ARGS__);        \
   } while (0)
   if (prec == 16)
     UT_KSTAR_BOTH(_Float16, true, (_Float16*)kst, part, ldexp(1.0, h3_kstar_exp(c->gp_sf2)), ldk * (int64_t)npad, RT,
@@ -593,10 +782,7 @@ int launch_gemm_kstar(ut_ctx* c, int prec, const double* XsT, int32_t npad, cons
                   nullptr);
   else if (prec == 32)
     UT_KSTAR_BOTH(float, true, (float*)kst, part, 1.0, (int64_t)0, RT, nullptr);
-  else if (part3) {   // pruned scoring's f32 bound pass
-    if (has_cat) UT_KSTAR_LAUNCH(double, true, true, true, (double*)kst, part, 1.0, (int64_t)0, store_rt, part2);
-    else UT_KSTAR_LAUNCH(double, true, false, true, (double*)kst, part, 1.0, (int64_t)0, store_rt, part2);
-  } else if (part)   // fp64 with the mean k* . alpha in the epilogue (pruned scoring: needs the whole fit)
+  else if (part)   // fp64 with the mean k* . alpha in the epilogue (pruned scoring: needs the whole fit)
     UT_KSTAR_BOTH(double, true, (double*)kst, part, 1.0, (int64_t)0, store_rt, part2);
   else
     UT_KSTAR_BOTH(double, false, (double*)kst, part, 1.0, (int64_t)0, store_rt, nullptr);

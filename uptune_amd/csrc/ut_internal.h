@@ -321,9 +321,11 @@ struct ut_ctx {
                                                // pass's sum |alpha|
   bool pr_f2_valid = false;                    // pr_f2 belongs to the current fit
   bool pr_ab_valid = false;                    // ... and its sum |alpha|
+  bool pr_xf_valid = false;                    // pr_xsT_f and max |x|^2 belong to the current fit
+  ut::DevBuf<float> pr_xsT_f, pr_ucand_f;      // f32 K* operands of the f32-contraction bound pass
   ut::DevBuf<double> pr_sa;                    // [RT][ldk] partials of sum |alpha_r| k*_r (f32 bound pass)
   ut::DevBuf<double> pr_gmu;                   // [RT][ldc] fp64 mean partials of recomputed columns (f32 pass)
-  int32_t prune_pass = 32;                     // ut_gp_set_prune_pass: the bound pass's k* in f32 or fp64
+  int32_t prune_pass = 32;                     // ut_gp_set_prune_pass: the bound pass in f32 or fp64
   ut::DevBuf<uint8_t> pr_exact;                // [ld] the stored score is the exact score
   int64_t r_ld = 0;
   int64_t r_m = 0;
@@ -506,7 +508,10 @@ int launch_gemm_kstar(ut_ctx* c, int prec, const double* XsT, int32_t npad, cons
                       double* part2 = nullptr,       // fp64 with part: also sum_r k*_r^2 partials
                       const KstarCat& cat = KstarCat(),
                       const double* xn = nullptr,    // training norms (nullptr: c->gp_xnorm)
-                      double* part3 = nullptr);      // f32 bound pass: sum_r |alpha_r| k*_r partials
+                      int32_t row_tiles = -1);       // > 0: only the first row_tiles 128-row tiles
+int launch_gemm_kstar_f32c(ut_ctx* c, const float* XsT_f, int32_t npad, const float* ucand_f, int32_t dpad,
+                           int64_t m, int64_t ldk, int32_t rt0, double* part, double* part2, double* part3,
+                           const KstarCat& cat, const double* xn, const double* cn);
 int launch_prep_cand(ut_ctx* c, const double* feat, int64_t ld, int64_t m, int32_t d, int32_t dpad, double* u,
                      int64_t ldu, double* cn);
 // categorical K*: the K* operands of the candidate side when the fit is in
