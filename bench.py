@@ -516,16 +516,13 @@ def main():
         return i, s_, d_
 
     def step_c4(r):
-        """GA round: UniformGreedyMutation proposals from the best recorded config
-        -> hash_config -> dedup vs history + batch -> encode (fused) -> GP-EI -> top-k"""
+        """GA round (ut_score_round_ga): UniformGreedyMutation proposals from the
+        best recorded config -> hash_config (the parent's inner digests reused) +
+        dedup vs history + batch on a second stream, beside encode (fused) ->
+        GP-EI -> top-k"""
         eng.gp_fit(X, y, lengthscale=ell, sigma_f2=1.0, sigma_n2=1e-6, jitter=1e-8, wait=False)
-        vals, invalid = eng.propose_ga(m, parent1=parent, round_=r, cand_base=cand_base, mutation_rate=0.1)
-        dig = eng.hash_parent(vals, parent)   # children keep most of the parent's values: its inner digests are reused
-        dup = torch.maximum(eng.dedup(dig), invalid)
-        _, _, score = eng.gp_score_values(vals, acq=acq, dup=dup)   # encode fused into the K* operand pass
-        idx, top = eng.topk(score, k, dup=dup, cand_base=cand_base)
-        sel = torch.where(idx >= 0, idx - cand_base, torch.zeros_like(idx))
-        sdig = torch.where((idx >= 0).unsqueeze(1), dig[sel], torch.zeros_like(dig[sel]))
+        idx, top, sdig, _ = eng.score_round_ga(m, k, parent1=parent, round_=r, cand_base=cand_base,
+                                               mutation_rate=0.1, acq=acq, want_values=False)
         idx, top, sdig = exchange(idx, top, sdig)
         eng.history_add(sdig)                             # the merged selections join every rank's history
         return idx, top, sdig

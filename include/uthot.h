@@ -371,6 +371,16 @@ typedef struct ut_round_out {
 } ut_round_out;
 int ut_score_round_de(ut_ctx* ctx, const ut_de_params* de, const ut_acq* acq, uint32_t round_, int64_t cand_base,
                       int64_t m, int32_t k, const ut_round_out* out);
+/* A GA / GGA scoring round (UniformGreedyMutation / NormalGreedyMutation / GA /
+ * GGA proposals, evolutionarytechniques.py:29-61, globalGA.py:187-235): the
+ * children of parent1 (ut_propose_ga's parameters), hash_config of the children
+ * (ut_hash_parent with parent1; ut_hash without) and dedup against the history
+ * + the batch on a second stream beside the encode and the GP posterior,
+ * invalid children (every retry reproduced a parent) counted as duplicates,
+ * then the top-k.  The fit must be current (ut_gp_fit / _async). */
+int ut_score_round_ga(ut_ctx* ctx, const ut_ga_params* ga, const double* parent1, const double* parent2,
+                      const ut_acq* acq, uint32_t round_, int64_t cand_base, int64_t m, int32_t k,
+                      const ut_round_out* out);
 /* the same round with ut_gp_topk_pruned's selection-exact pruning in place of
  * the dense variance (fp64 fits; the round's mu/var/score buffers are not
  * filled) */

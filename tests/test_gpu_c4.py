@@ -143,6 +143,37 @@ def test_c4_ga_round(c4, mutation_rate, crossover_rate, two):
     _score_and_check(c4, allv, full)
 
 
+@pytest.mark.parametrize("two", [False, True])
+def test_score_round_ga_equals_separate_calls(c4, two):
+    """ut_score_round_ga (the bench's C4 step: hash + dedup on a second stream
+    beside encode + GP) selects what the separate calls select -- propose_ga,
+    hash_parent, dedup with the invalid children, gp_score_values, topk -- with
+    the same scores and digests, and its selections' digests are the oracle's"""
+    e, space = c4["e"], c4["space"]
+    n, k, m = 1024, 64, 50000
+    ok_rows = np.flatnonzero(np.isfinite(c4["qor"]))[:n]
+    X = features(space, c4["hist"][:, ok_rows]).T
+    y = c4["qor"][ok_rows].astype(np.float64)
+    p2 = c4["second"] if two else None
+    kw = dict(mutation_rate=0.05, crossover_rate=0.5 if two else 0.0)
+    e.gp_fit(X, y, lengthscale=2.0, sigma_f2=1.0, sigma_n2=1e-6, jitter=1e-8)
+    acq = e.acq("ei")
+    idx, top, dig, vals = e.score_round_ga(m, k, parent1=c4["best"], parent2=p2, round_=5, cand_base=100, acq=acq,
+                                           **kw)
+    v2, inv = e.propose_ga(m, parent1=c4["best"], parent2=p2, round_=5, cand_base=100, **kw)
+    d2 = e.hash_parent(v2, c4["best"])
+    dup = torch.maximum(e.dedup(d2), inv)
+    _, _, score = e.gp_score_values(v2, acq=acq, dup=dup)
+    i2, t2 = e.topk(score, k, dup=dup, cand_base=100)
+    assert idx.cpu().tolist() == i2.cpu().tolist()
+    np.testing.assert_array_equal(top.cpu().numpy(), t2.cpu().numpy())
+    sel = (i2 - 100).cpu().numpy()
+    np.testing.assert_array_equal(dig.cpu().numpy(), d2[sel].cpu().numpy())
+    np.testing.assert_array_equal(vals.cpu().numpy(), v2[:, sel].cpu().numpy())
+    from uptune_amd.engine import digests_to_hex
+    assert digests_to_hex(dig) == c4["H"](vals.cpu().numpy())
+
+
 def test_c4_pso_round(c4):
     """PSO (pso.py:23-77) over a swarm of recorded configs toward the best one;
     Enum flags keep the reference quirk (enum_mode 0: never move)"""

@@ -137,6 +137,8 @@ SIGNATURES = {
     "ut_gp_stats": (C.c_int, [P, C.POINTER(D), C.POINTER(D), C.POINTER(D)]),
     "ut_gp_kstar_mode": (C.c_int, [P, C.POINTER(I32)]),
     "ut_topk": (C.c_int, [P, P, P, I64, I64, I32, P, P]),
+    "ut_score_round_ga": (C.c_int, [P, C.POINTER(GaParams), C.c_void_p, C.c_void_p, C.POINTER(Acq), U32, I64, I64,
+                                    I32, C.POINTER(RoundOut)]),
     "ut_score_round_de": (C.c_int, [P, C.POINTER(DeParams), C.POINTER(Acq), U32, I64, I64, I32,
                                     C.POINTER(RoundOut)]),
     "ut_round_buffers": (C.c_int, [P, C.POINTER(P), C.POINTER(P), C.POINTER(P), C.POINTER(P), C.POINTER(P),

@@ -866,6 +866,7 @@ int ut_topk(ut_ctx* c, const double* score, const uint8_t* dup, int64_t m, int64
   return topk_impl(c, score, dup, m, cand_base, k, out_idx, out_score);
 }
 
+static int round_outputs(ut_ctx* c, const ut_round_out* out, int64_t ld, int64_t cand_base, int32_t k);
 static int score_round_de_impl(ut_ctx* c, const ut_de_params* de, const ut_acq* acq, uint32_t round_,
                                int64_t cand_base, int64_t m, int32_t k, const ut_round_out* out, int32_t prune_rows,
                                ut_prune_stats* stats);
@@ -960,24 +961,92 @@ static int score_round_de_impl(ut_ctx* c, const ut_de_params* de, const ut_acq* 
       return rc;
     mark(c, "topk");
   }
-  if (out) {
-    if (out->topk_idx)
-      UT_HIP(c, hipMemcpyAsync(out->topk_idx, c->r_topk_idx.p, sizeof(int64_t) * k, hipMemcpyDeviceToDevice,
-                               c->stream));
-    if (out->topk_score)
-      UT_HIP(c, hipMemcpyAsync(out->topk_score, c->r_topk_score.p, sizeof(double) * k, hipMemcpyDeviceToDevice,
-                               c->stream));
-    if (out->topk_values || out->topk_digest) {
-      double* vals = out->topk_values;
-      if (!vals) {  // digests only: the rows go to a context buffer (no per-round alloc / sync)
-        if ((rc = ensure(c, c->r_topk_vals, (size_t)NC * k))) return rc;
-        vals = c->r_topk_vals.p;
-      }
-      if ((rc = launch_gather_rows(c, c->r_values.p, ld, c->r_topk_idx.p, cand_base, k, vals, k, c->r_digest.p,
-                                   out->topk_digest)))
-        return rc;
+  if ((rc = round_outputs(c, out, ld, cand_base, k))) return rc;
+  return timing_end(c);
+}
+
+// a round's selections to the caller: indices, scores, rows and digests
+static int round_outputs(ut_ctx* c, const ut_round_out* out, int64_t ld, int64_t cand_base, int32_t k) {
+  if (!out) return 0;
+  int rc;
+  if (out->topk_idx)
+    UT_HIP(c, hipMemcpyAsync(out->topk_idx, c->r_topk_idx.p, sizeof(int64_t) * k, hipMemcpyDeviceToDevice,
+                             c->stream));
+  if (out->topk_score)
+    UT_HIP(c, hipMemcpyAsync(out->topk_score, c->r_topk_score.p, sizeof(double) * k, hipMemcpyDeviceToDevice,
+                             c->stream));
+  if (out->topk_values || out->topk_digest) {
+    double* vals = out->topk_values;
+    if (!vals) {  // digests only: the rows go to a context buffer (no per-round alloc / sync)
+      if ((rc = ensure(c, c->r_topk_vals, (size_t)c->space.ncols * k))) return rc;
+      vals = c->r_topk_vals.p;
     }
+    if ((rc = launch_gather_rows(c, c->r_values.p, ld, c->r_topk_idx.p, cand_base, k, vals, k, c->r_digest.p,
+                                 out->topk_digest)))
+      return rc;
   }
+  return 0;
+}
+
+// A GA / GGA scoring round (ut_score_round_ga): the children of parent1
+// (evolutionarytechniques.py:29-61, globalGA.py:187-235), then hash_config of
+// the children (the parent's inner digests reused) + dedup on the side stream
+// beside the fused encode and the GP scoring, their invalid children joined to
+// the duplicates, top-k.  What the C4 round ran as separate calls on one stream.
+int ut_score_round_ga(ut_ctx* c, const ut_ga_params* ga, const double* parent1, const double* parent2,
+                      const ut_acq* acq, uint32_t round_, int64_t cand_base, int64_t m, int32_t k,
+                      const ut_round_out* out) {
+  if (!c) return UT_EINVAL;
+  UT_CHECK(c, c->has_space, UT_ENOSPACE, "space not defined");
+  UT_CHECK(c, c->gp_ready, UT_EINVAL, "score_round: call ut_gp_fit first");
+  UT_CHECK(c, c->gp_d == c->space.n_feat, UT_EINVAL, "score_round: GP feature width != space feature width");
+  UT_CHECK(c, m >= 1 && ga && acq && cand_base >= 0 && k >= 1, UT_EINVAL, "score_round_ga: bad arguments");
+  UT_CHECK(c, ga->max_retries >= 1 && ga->max_retries <= 15, UT_EINVAL, "propose_ga: max_retries must be in [1, 15]");
+  UT_CHECK(c, ga->must_mutate_count >= 0 && ga->must_mutate_count <= c->space.P, UT_EINVAL,
+           "propose_ga: must_mutate_count out of range");
+  UT_CHECK(c, ga->op >= 0 && ga->op < 256, UT_EINVAL, "propose_ga: op must fit 8 bits");
+  UT_CHECK(c, ga->crossover >= UT_X_NONE && ga->crossover <= UT_X_PMX, UT_EINVAL, "propose_ga: bad crossover");
+  const int64_t ld = ((m + 127) / 128) * 128;
+  int rc;
+  if ((rc = ensure(c, c->r_values, (size_t)c->space.ncols * ld))) return rc;
+  if ((rc = ensure(c, c->r_digest, (size_t)8 * ld))) return rc;
+  if ((rc = ensure(c, c->r_dup, (size_t)ld))) return rc;
+  if ((rc = ensure(c, c->r_inval, (size_t)ld))) return rc;
+  if ((rc = ensure(c, c->r_mu, (size_t)ld))) return rc;
+  if ((rc = ensure(c, c->r_var, (size_t)ld))) return rc;
+  if ((rc = ensure(c, c->r_score, (size_t)ld))) return rc;
+  if ((rc = ensure(c, c->r_topk_idx, (size_t)k))) return rc;
+  if ((rc = ensure(c, c->r_topk_score, (size_t)k))) return rc;
+  c->r_ld = ld;
+  c->r_m = m;
+  c->r_feat_valid = false;
+  timing_begin(c);
+  if ((rc = launch_ga(c, ga, parent1, parent2, round_, cand_base, m, c->r_values.p, ld, c->r_inval.p))) return rc;
+  mark(c, "propose");
+  // fork right after the proposal: forked after K* instead (beside the int8
+  // variance GEMM) the hash ran 106 ms where it runs 79 beside encode + K*, C4
+  // 147.5 -> 156.5 ms (scripts/ab/r05_ga_fork.sh)
+  UT_HIP(c, hipEventRecord(c->ev_fork, c->stream));
+  UT_HIP(c, hipStreamWaitEvent(c->side, c->ev_fork, 0));
+  {
+    StreamScope on_side(c, c->side);
+    mark(c, "");
+    rc = parent1 ? launch_hash_parent(c, c->r_values.p, ld, m, parent1, c->r_digest.p)
+                 : launch_hash(c, c->r_values.p, ld, m, c->r_digest.p);
+    if (rc) return rc;
+    mark(c, "hash");
+    if ((rc = launch_dedup(c, c->r_digest.p, m, c->r_dup.p))) return rc;
+    if ((rc = launch_mask_or(c, c->r_dup.p, c->r_inval.p, m))) return rc;
+    mark(c, "dedup");
+    UT_HIP(c, hipEventRecord(c->ev_join, c->side));
+  }
+  if ((rc = gp_encode_scaled(c, c->r_values.p, ld, m))) return rc;
+  mark(c, "encode");
+  if ((rc = gp_score_impl(c, nullptr, ld, m, acq, c->r_dup.p, c->r_mu.p, c->r_var.p, c->r_score.p, c->ev_join)))
+    return rc;
+  if ((rc = topk_impl(c, c->r_score.p, c->r_dup.p, m, cand_base, k, c->r_topk_idx.p, c->r_topk_score.p))) return rc;
+  mark(c, "topk");
+  if ((rc = round_outputs(c, out, ld, cand_base, k))) return rc;
   return timing_end(c);
 }
 

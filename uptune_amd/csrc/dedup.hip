@@ -122,6 +122,19 @@ int launch_hist_insert(ut_ctx* c, const uint32_t* dig, int64_t n) {
   return 0;
 }
 
+// dst[i] |= src[i] (a GA round's invalid children join its duplicates)
+__global__ void k_mask_or(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src, int64_t m) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < m && src[i]) dst[i] = 1;
+}
+
+int launch_mask_or(ut_ctx* c, uint8_t* dst, const uint8_t* src, int64_t m) {
+  if (m <= 0) return 0;
+  hipLaunchKernelGGL(k_mask_or, dim3(grid1(m, 256)), dim3(256), 0, c->stream, dst, src, m);
+  UT_LAUNCH_CHECK(c);
+  return 0;
+}
+
 int launch_dedup(ut_ctx* c, const uint32_t* dig, int64_t m, uint8_t* dup) {
   if (m <= 0) return 0;
   int64_t cap = 1024;

@@ -292,6 +292,7 @@ struct ut_ctx {
   ut::DevBuf<double> r_values, r_feat, r_mu, r_var, r_score;
   ut::DevBuf<uint32_t> r_digest;
   ut::DevBuf<uint8_t> r_dup;
+  ut::DevBuf<uint8_t> r_inval;      // GA rounds: children whose retries all reproduced a parent
   ut::DevBuf<double> tk_score[2];
   ut::DevBuf<int64_t> tk_idx[2];
   ut::DevBuf<int64_t> r_topk_idx;
@@ -467,6 +468,7 @@ inline int64_t pop_aos_ld(const ut_ctx* c) { return ((int64_t)c->space.ncols + 1
 int launch_hist_insert(ut_ctx* c, const uint32_t* dig, int64_t n);
 int launch_hist_rehash(ut_ctx* c, const uint32_t* okeys, const uint32_t* ostate, int64_t ocap);
 int launch_dedup(ut_ctx* c, const uint32_t* dig, int64_t m, uint8_t* dup);
+int launch_mask_or(ut_ctx* c, uint8_t* dst, const uint8_t* src, int64_t m);
 // feat == nullptr: the candidates' scaled features and norms are already in
 // c->ucand / c->cnorm (gp_encode_scaled); dup_ready: the event of the dup
 // mask (the round's side stream), joined before the variance GEMM

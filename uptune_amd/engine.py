@@ -435,6 +435,29 @@ class BatchEngine:
                 "ut_score_round_de")
         return idx, top, dig, vals
 
+    def score_round_ga(self, m: int, k: int, parent1=None, parent2=None, round_: int = 0, cand_base: int = 0,
+                       mutation_rate: float = 0.1, sigma: float = 0.1, crossover_rate: float = 0.0,
+                       crossover_strength: float = 0.0, must_mutate_count: int = 1, normal: bool = False,
+                       max_retries: int = 10, op: int = 4, crossover: Optional[str] = None,
+                       acq: Optional[L.Acq] = None, want_values: bool = True):
+        """ut_score_round_ga: propose_ga -> hash_parent + dedup (side stream) beside
+        encode + GP posterior -> top-k; -> (idx, top, digests, values)"""
+        p1, p2 = self._row(parent1), self._row(parent2)
+        a = L.GaParams(mutation_rate=mutation_rate, sigma=sigma, crossover_rate=crossover_rate,
+                       crossover_strength=crossover_strength, must_mutate_count=must_mutate_count,
+                       normal=1 if normal else 0, max_retries=max_retries, op=op, crossover=_xop(crossover))
+        acq = acq or self.acq()
+        idx = self._empty(k, dtype=torch.int64)
+        top = self._empty(k)
+        dig = self._empty(k, 8, dtype=torch.int32)
+        vals = self._empty(self.spec.ncols, k) if want_values else None
+        out = L.RoundOut(topk_idx=idx.data_ptr(), topk_score=top.data_ptr(), topk_digest=dig.data_ptr(),
+                         topk_values=vals.data_ptr() if vals is not None else None)
+        L.check(self.ctx, self.lib.ut_score_round_ga(self.ctx, C.byref(a), _ptr(p1), _ptr(p2), C.byref(acq),
+                                                     int(round_), int(cand_base), int(m), int(k), C.byref(out)),
+                "ut_score_round_ga")
+        return idx, top, dig, vals
+
     def score_round_de_pruned(self, m: int, k: int, round_: int = 0, cand_base: int = 0, cr: float = 0.2,
                               n_cross: int = 1, acq: Optional[L.Acq] = None, want_values: bool = True, best=None,
                               information_sharing: int = 1, bound_rows: int = 256):
