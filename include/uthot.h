@@ -388,8 +388,8 @@ int ut_score_round_de_pruned(ut_ctx* ctx, const ut_de_params* de, const ut_acq* 
                              int64_t cand_base, int64_t m, int32_t k, int32_t bound_rows, const ut_round_out* out,
                              ut_prune_stats* stats_host);
 /* device pointers to the last round's internal buffers (for tests/bench);
- * features is NULL after a dense round, which encodes straight into the K*
- * operand (features / ell) and keeps no feature matrix */
+ * features is NULL: the rounds (dense and pruned) encode straight into the K*
+ * operands (features / ell, norms, one-hot codes) and keep no feature matrix */
 int ut_round_buffers(ut_ctx* ctx, double** values, double** features, uint32_t** digests, uint8_t** dup,
                      double** mu, double** var, double** score, int64_t* ld);
 

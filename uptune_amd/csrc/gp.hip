@@ -1729,7 +1729,9 @@ int gp_topk_pruned_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, co
   if (c->fit_pending) UT_HIP(c, hipStreamWaitEvent(c->stream, c->ev_fit_x, 0));
   const int32_t n = c->gp_n, d = c->gp_d;
   const int32_t npad = ((n + NPAD - 1) / NPAD) * NPAD;
-  const bool cat = feat_ours && c->cat_on;   // the categorical K* (features from ut's encoder)
+  // feat == nullptr: the K* operands are already in c->ucand / c->cnorm (/ c->bcat),
+  // from gp_encode_scaled (a scoring round's fused encode)
+  const bool cat = feat ? feat_ours && c->cat_on : c->ucand_cat;   // the categorical K* (ut's encoder)
   const int32_t dpad = cat ? cat_dpad(c) : kstar_dpad(d);
   const int32_t RT = npad / NPAD;
   int32_t R = (bound_rows + NPAD - 1) / NPAD;
@@ -1757,13 +1759,15 @@ int gp_topk_pruned_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, co
   if ((rc = ensure(c, c->pr_exact, (size_t)ldk))) return rc;
   const double* LinvT = c->gp_LinvT;
   // 1. K* with the mean in its epilogue, 2. the first R row tiles of L^-1 K*^T
-  if (cat) {
-    if ((rc = launch_prep_cand_cat(c, feat, ld, m, c->ucand.p, dpad, ldk, c->cnorm.p, c->bcat.p))) return rc;
-  } else if ((rc = launch_prep_cand(c, feat, ld, m, d, dpad, c->ucand.p, ldk, c->cnorm.p))) {
-    return rc;
+  if (feat) {
+    if (cat) {
+      if ((rc = launch_prep_cand_cat(c, feat, ld, m, c->ucand.p, dpad, ldk, c->cnorm.p, c->bcat.p))) return rc;
+    } else if ((rc = launch_prep_cand(c, feat, ld, m, d, dpad, c->ucand.p, ldk, c->cnorm.p))) {
+      return rc;
+    }
+    c->ucand_cat = cat;
+    mark(c, "prep");
   }
-  c->ucand_cat = cat;
-  mark(c, "prep");
   if (c->fit_pending) UT_HIP(c, hipStreamWaitEvent(c->stream, c->ev_fit, 0));   // K* takes mu = k* . alpha
   mark(c, "fit_wait");   // (the wait is not K* time)
   const double* XsT = cat ? c->gp_XsT_num.p : c->gp_XsT;
