@@ -14,7 +14,8 @@ KERNELS = {"var": ("void ut::k_gp_var_pp<false>(", "ut::k_gp_var_pp(", "void ut:
            "kstar": ("void ut::k_gp_kstar<double, false, false>", "void ut::k_gp_kstar<double, false>"), "inner_pairs": ("ut::k_inner_pairs",),
            "encode": ("ut::k_encode_scaled",),
            "hash": ("void ut::k_hash<true", "void ut::k_hash<", "ut::k_hash("), "propose": ("void ut::k_de<", "ut::k_de("),
-           "var16": ("_ZN2ut11k_gp_var_h3",), "kstar16": ("_ZN2ut10k_gp_kstarIDF16_",)}
+           "var16": ("_ZN2ut11k_gp_var_h3",), "kstar16": ("_ZN2ut10k_gp_kstarIDF16_",),
+           "kstar_f32c": ("void ut::k_gp_kstar_f32c<",), "kstar_bound64": ("void ut::k_gp_kstar<double, true, true>",)}
 
 
 def main(d, n_cu=256, peak_ghz=2.4):
