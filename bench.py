@@ -162,31 +162,55 @@ def load_pmc(kernel_key):
 SHA256_CEIL_GCPS = 28.5   # measured chip ceiling of SHA-256 compressions (scripts/exp/sha_rate.hip)
 
 
-def kernel_table(m, n, d, outer_blocks, prec=64):
+def profile_suffix(ell):
+    """record-key suffix of a profiled C2 pass: "" at the headline's ell = 0.2,
+    "_l2" for the secondary line's ell = 2 (scripts/r06_prof.sh)"""
+    return "" if ell == 0.2 else "_l2"
+
+
+def load_clock():
+    """profiles/clock_summary.json: per kernel the duration, clock and MFMA busy
+    of the rocprofv3 counter pass (dispatches serialized: each kernel alone)"""
+    try:
+        with open(os.path.join(ROOT, "profiles", "clock_summary.json")) as f:
+            return json.load(f)
+    except Exception:
+        return {}
+
+
+def kernel_table(m, n, d, outer_blocks, prec=64, suffix=""):
     """Per-kernel rooflines of the default C2 round from the committed rocprofv3
-    record (profiles/pmc_summary.json: average launch duration from the
-    --kernel-trace --stats pass, HBM bytes from the FETCH_SIZE / WRITE_SIZE
-    passes of the same command).  Algorithmic work per launch:
+    record (profiles/pmc_summary.json: HBM bytes from the FETCH_SIZE /
+    WRITE_SIZE passes; profiles/clock_summary.json: durations from the counter
+    pass, where rocprofv3 serializes the dispatches -- else the --kernel-trace
+    --stats average of the concurrent round).  Algorithmic work per launch
+    (SURVEY.md §8(d)):
       k_de: 40 d B per candidate (target, 3 donors, trial); k_hash (outer):
       outer_blocks compressions per candidate; K*: 2 n dpad flops; encode: 16 F B.
     prec 8: K* is k_gp_kstar<int8_t> (the mean k* . alpha and six digit planes
-    in its epilogue; record key kstar8)."""
+    in its epilogue; record key kstar8).  suffix "_l2": the ell = 2 records."""
     out = {}
     try:
         with open(os.path.join(ROOT, "profiles", "pmc_summary.json")) as f:
             pmc = json.load(f)
     except Exception:
         return out
-    try:   # the counter pass of the same round (dispatches serialized: each kernel alone on the chip)
-        with open(os.path.join(ROOT, "profiles", "clock_summary.json")) as f:
-            clk = json.load(f)
-    except Exception:
-        clk = {}
+    clk = load_clock()
+    srcs = set()
 
     def rec(key):
+        key = key + suffix
         r = pmc.get(key) or {}
         c = clk.get(key) or {}
-        t = c.get("duration_ms", 0.0) * 1e-3 or (r.get("avg_ns") or 0.0) * 1e-9
+        if c:
+            t = c.get("duration_ms", 0.0) * 1e-3
+            srcs.add("%s: clock_summary.json (counter pass %s, serialized) + pmc_summary.json (%s)" %
+                     (key, c.get("source", "?"), r.get("source", "?")))
+        else:
+            t = (r.get("avg_ns") or 0.0) * 1e-9
+            if r:
+                srcs.add("%s: pmc_summary.json (%s; duration = --kernel-trace --stats average, concurrent)" %
+                         (key, r.get("source", "?")))
         return t, r.get("hbm_bytes_per_launch")
 
     def hbm(key, alg_bytes):
@@ -214,12 +238,10 @@ def kernel_table(m, n, d, outer_blocks, prec=64):
                        "frac": c / t / 1e9 / SHA256_CEIL_GCPS, "compressions": c, "traffic_bytes": traffic,
                        "ceiling": f"{SHA256_CEIL_GCPS} G compressions/s (measured, scripts/exp/sha_rate.hip)"}
     for key, r in out.items():
-        if key in clk:
-            r["clock_ghz"] = clk[key].get("clock_ghz")
-            r["mfma_busy"] = clk[key].get("mfma_busy")
-    out["_source"] = ("durations: profiles/clock_summary.json (rocprofv3 counter pass of the C2 round, dispatches "
-                      "serialized, so each kernel ran alone), else the --kernel-trace --stats average; HBM bytes: "
-                      "profiles/pmc_summary.json (" + pmc.get("_note", "").split("source:")[-1].strip() + ")")
+        if key + suffix in clk:
+            r["clock_ghz"] = clk[key + suffix].get("clock_ghz")
+            r["mfma_busy"] = clk[key + suffix].get("mfma_busy")
+    out["_source"] = sorted(srcs)
     return out
 
 
@@ -370,6 +392,10 @@ def main():
                     help="candidates in the 1-thread oracle baseline sample (about 4 s of single-thread work)")
     ap.add_argument("--b1-sample", type=int, default=1 << 18,
                     help="candidates in the B1 batch baseline sample (C++/OpenMP + BLAS on the host cores)")
+    ap.add_argument("--ell", type=float, default=None,
+                    help="the GP lengthscale of the timed rounds (default: the config's -- C2 0.2, C3 1, C4 2)")
+    ap.add_argument("--no-secondary", dest="secondary", action="store_false",
+                    help="C2: skip the secondary line (the same rounds timed at ell = 2, score-determined)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true", help="skip the oracle check of the selections")
     ap.add_argument("--parity-sample", type=int, default=1 << 16,
@@ -488,7 +514,7 @@ def main():
         hv = torch.from_numpy(np.ascontiguousarray((X * 2000.0 - 1000.0).T)).to(eng.device)   # decoded configs
         eng.history_add(eng.hash(hv))
     acq = eng.acq("ei", xi=0.0)
-    ell = {"c2": 0.2, "c3": 1.0, "c4": 2.0}[args.config]
+    ell = args.ell if args.ell is not None else {"c2": 0.2, "c3": 1.0, "c4": 2.0}[args.config]
 
     comm = None
     exchange_note = None
@@ -544,36 +570,56 @@ def main():
         eng.history_add(dig)                              # the merged selections join every rank's history
         return idx, top, dig
 
+    def timed_rounds(first, steps, ell_):
+        """`steps` rounds from round `first` at lengthscale ell_, bracketed by a
+        barrier + device sync on both sides; -> (seconds, max over ranks;
+        per-stage device ms; i8 stats of the last round; its selections)"""
+        eng.set_timing(True)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for s in range(steps):
+            out = step(first + s, ell=ell_)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        el = time.perf_counter() - t0
+        # per-stage device times of the timed rounds (HIP events recorded on the
+        # library's streams during the rounds, read once here)
+        st_ms = {}
+        for st in ("propose", "hash", "dedup", "encode", "prep", "fit_wait", "kstar", "bound", "prune", "var",
+                   "finalize", "recompute", "topk"):
+            try:
+                st_ms[st] = eng.stage_time(st)
+            except Exception:
+                pass
+        eng.set_timing(False)
+        i8s = eng.gp_i8_stats() if args.precision == 8 else None
+        if world > 1:
+            t = torch.tensor([el], dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t.item())
+        return el, st_ms, i8s, out
+
     for w in range(args.warmup):
         step(w)
     torch.cuda.synchronize()
+    elapsed, stages, i8_timed, (idx, top, sdig) = timed_rounds(args.warmup, args.steps, ell)
 
-    eng.set_timing(True)
-    stage_ms = {}
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for s in range(args.steps):
-        idx, top, sdig = step(args.warmup + s)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    # per-stage device times of the timed rounds (HIP events recorded on the
-    # library's streams during the rounds, read once here)
-    for st in ("propose", "hash", "dedup", "encode", "prep", "fit_wait", "kstar", "bound", "prune", "var", "finalize",
-               "recompute", "topk"):
-        try:
-            stage_ms[st] = [eng.stage_time(st)]
-        except Exception:
-            pass
-    eng.set_timing(False)
-    i8_timed = eng.gp_i8_stats() if args.precision == 8 else None
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    # the secondary C2 line (VERDICT r5 #1): the same round timed at ell = 2,
+    # where k* spans (1e-3, 1), every K* digit plane carries data, EI values
+    # spread and the top-k is decided by the scores (at the headline's ell =
+    # 0.2 every k* underflows to ~1e-58: zero digit planes, index-order top-k)
+    sec = None
+    r_next = args.warmup + args.steps
+    if args.secondary and args.config == "c2" and not args.prune and ell != 2.0:
+        for w in range(max(1, args.warmup // 2)):
+            step(r_next + w, ell=2.0)
+        r_next += max(1, args.warmup // 2)
+        sel2, st2, i8_2, out2 = timed_rounds(r_next, args.steps, 2.0)
+        sec = {"lengthscale": 2.0, "first_round": r_next, "elapsed": sel2, "stages": st2, "i8": i8_2, "out": out2}
+        r_next += args.steps
 
     # ---- the checker, outside the timed region ------------------------------
     parity = None
@@ -593,9 +639,14 @@ def main():
         if args.config == "c2":
             # a round whose top-k the scores decide (ell = 2.0: EI values spread,
             # where the headline's ell = 0.2 makes every k* underflow to ~1e-58
-            # and the selection is decided by index order)
-            r_x = r_last + 1
-            ix, tx, dx = step(r_x, ell=2.0)
+            # and the selection is decided by index order): the secondary
+            # line's last timed round, else one extra round
+            if sec is not None:
+                r_x = r_next - 1
+                ix, tx, dx = sec["out"]
+            else:
+                r_x = r_next
+                ix, tx, dx = step(r_x, ell=2.0)
             torch.cuda.synchronize()
             if rank == 0:
                 rep2, _, ei_sel = parity_de_round(eng, space, ix, tx, dx, npop, 1, r_x, X, y, 2.0, jit, k)
@@ -636,7 +687,6 @@ def main():
 
     ms_per_step = elapsed * 1000.0 / args.steps
     value = npop / (elapsed / args.steps)   # every candidate of the global pool, all ranks together
-    stages = {st: float(np.mean(v)) for st, v in stage_ms.items()}
     # dominant kernel: the variance GEMM  V = L^-1 K*^T  (fp64 MFMA); at C4 (707
     # features) the K* contraction (2 n d flops per candidate) carries more flops
     var_ms = stages.get("var")
@@ -691,9 +741,25 @@ def main():
     # HBM bytes per launch and the rocprof average duration were profiled on the
     # default C2 round (profiles/pmc_summary.json)
     profiled = args.config == "c2" and (m, n, d) == (1 << 20, 1024, 64) and not args.prune
-    pmc, pmc_note = load_pmc({64: "var", 32: "var32", 16: "var16", 8: "var8"}[args.precision]) if profiled else ({}, "")
-    traffic = pmc.get("hbm_bytes_per_launch")
-    frac_rocprof = (flops_var / (pmc["avg_ns"] * 1e-9) / 1e12 / peak) if pmc.get("avg_ns") else None
+    var_key = {64: "var", 32: "var32", 16: "var16", 8: "var8"}[args.precision]
+
+    def rocprof_of(key, ell_):
+        """(HBM bytes per launch, roofline frac at the rocprof duration, source
+        label) of a profiled C2 kernel at lengthscale ell_ (records of the ell =
+        2 rounds carry the suffix _l2)"""
+        if not profiled or ell_ not in (0.2, 2.0):
+            return None, None, None
+        rec, note = load_pmc(key + profile_suffix(ell_))
+        if not rec:
+            return None, None, None
+        clk = load_clock().get(key + profile_suffix(ell_)) or {}
+        dur = clk.get("duration_ms", 0.0) * 1e-3 or (rec.get("avg_ns") or 0.0) * 1e-9
+        src = ("profiles/pmc_summary.json[%s] (HBM bytes: %s; duration: %s)" %
+               (key + profile_suffix(ell_), rec.get("source") or note.split("source:")[-1].strip(),
+                "profiles/clock_summary.json, %s" % clk.get("source", "?") if clk else "--kernel-trace --stats avg"))
+        return rec.get("hbm_bytes_per_launch"), (flops_var / dur / 1e12 / peak) if dur > 0 else None, src
+
+    traffic, frac_rocprof, rocprof_src = rocprof_of(var_key, ell)
     i8_info = None
     if args.precision == 8:
         rec, bound_e = eng.gp_i8_stats()   # the last round run: the score-determined parity round when it ran
@@ -755,18 +821,40 @@ def main():
         "hbm_bytes_per_rank": hbm_rank,
         "hbm_device_used_bytes": int(total_b - free_b),
         "stage_ms": stages,
-        "kernels": (kernel_table(m, n, d, eng.space_info()[1], args.precision) if profiled else None),
+        "kernels": (kernel_table(m, n, d, eng.space_info()[1], args.precision, profile_suffix(ell))
+                    if profiled else None),
         "prune": prune_info,
         "i8": i8_info,
         "roofline": {"bound": "mfma", "kernel": kernel,
                      "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
                      "frac": (achieved / peak) if achieved else None, "traffic": traffic,
-                     "frac_rocprof": frac_rocprof,
-                     "rocprof_source": ("profiles/pmc_summary.json (" + pmc_note.split("source:")[-1].strip() + ")")
-                     if pmc else None,
+                     "frac_rocprof": frac_rocprof, "rocprof_source": rocprof_src,
                      "flops_per_launch": flops_var},
         "cpu_baseline": None,
     }
+    if sec is not None:
+        # the secondary line: the same C2 rounds at ell = 2 (every K* digit plane
+        # non-zero, score-determined top-k), timed like the headline
+        v2_ms = sec["stages"].get("var")
+        a2 = flops_var / (v2_ms * 1e-3) / 1e12 if v2_ms else None
+        t2, f2r, s2 = rocprof_of(var_key, 2.0)
+        sd = (parity or {}).get("score_determined") or {}
+        result["secondary_ell2"] = {
+            "lengthscale": 2.0, "rounds": [sec["first_round"], sec["first_round"] + args.steps - 1],
+            "value": npop / (sec["elapsed"] / args.steps), "unit": "candidates/s",
+            "ms_per_step": sec["elapsed"] * 1000.0 / args.steps, "steps": args.steps,
+            "stage_ms": sec["stages"],
+            "roofline": {"kernel": kernel, "achieved": a2, "peak": peak, "unit": "TFLOP/s",
+                         "frac": (a2 / peak) if a2 else None, "traffic": t2, "frac_rocprof": f2r,
+                         "rocprof_source": s2},
+            "i8": ({"recomputed_fp64_last_timed_round": sec["i8"][0], "bound_E": sec["i8"][1]}
+                   if sec["i8"] else None),
+            "kernels": kernel_table(m, n, d, eng.space_info()[1], args.precision, "_l2") if profiled else None,
+            "parity": ({"round": sd.get("round"), "all_ok": bool(sd.get("trials_equal") and sd.get("digests_equal")
+                                                                 and sd.get("ei_max_rel_err", 1.0) <= 1e-5
+                                                                 and sd.get("topk_beats_sample")),
+                        "note": "the last timed round of this line is parity.score_determined"} if sd else None),
+        }
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "c2":
         host = host_info()
         result["host"] = host

@@ -173,14 +173,14 @@ int ut_propose_de(ut_ctx* ctx, const ut_de_params* p, uint32_t round_, int64_t c
 /* PSO (pso.py:11-77, HybridParticle + op3_swarm per kind).  Candidate g
  * moves particle g % npop towards gbest (device row [P]) and its own best. */
 typedef struct ut_pso_params {
-  double omega, phi_l, phi_g;   /* 0.5, 0.5, 0.5 (pso.py:202) */
+  double omega, phi_l, phi_g;   /* 0.5, 0.5, 0.5 (pso.py:49) */
   double sigma;                 /* Int/Pow2 gaussian noise, unit scale 0.2 (manipulator.py:661) */
-  int32_t alias_pbest;          /* 1 = reference: particle.best IS the position (pso.py:212-213) */
+  int32_t alias_pbest;          /* 1 = reference: particle.best IS the position (pso.py:46, :60) */
   int32_t enum_mode;            /* 0 = reference: enum never moves (manipulator.py:442); 1 = corrected */
   int32_t crossover;            /* PERM: UT_X_* of PSO(crossover=...) (pso.py:80-84; op3_swarm :1115-1140) */
   int32_t pad;
 } ut_pso_params;
-/* velocities := 0 and particle bests := positions (pso.py:218-221) */
+/* velocities := 0 and particle bests := positions (pso.py:59-68) */
 int ut_pso_reset(ut_ctx* ctx);
 int ut_propose_pso(ut_ctx* ctx, const ut_pso_params* p, const double* gbest, uint32_t round_, int64_t cand_base,
                    int64_t m, double* out_values, double* out_velocity, int64_t ld);
@@ -372,7 +372,7 @@ typedef struct ut_round_out {
 int ut_score_round_de(ut_ctx* ctx, const ut_de_params* de, const ut_acq* acq, uint32_t round_, int64_t cand_base,
                       int64_t m, int32_t k, const ut_round_out* out);
 /* A GA / GGA scoring round (UniformGreedyMutation / NormalGreedyMutation / GA /
- * GGA proposals, evolutionarytechniques.py:29-61, globalGA.py:187-235): the
+ * GGA proposals, evolutionarytechniques.py:29-61, globalGA.py:28-48 and :68-76): the
  * children of parent1 (ut_propose_ga's parameters), hash_config of the children
  * (ut_hash_parent with parent1; ut_hash without) and dedup against the history
  * + the batch on a second stream beside the encode and the GP posterior,

@@ -1,6 +1,6 @@
 """Batched GA-family proposal restated from
 python/uptune/opentuner/search/evolutionarytechniques.py:29-134 and
-globalGA.py:187-243.
+globalGA.py:28-76.
 
 Per candidate (one `desired_configuration` call):
   parents   = [select(), select()] if random() < crossover_rate else [select()]   (:72-78)
@@ -8,7 +8,7 @@ Per candidate (one `desired_configuration` call):
               or manipulator.random() when there is none (parent1 is None)
   crossover = GGA (crossover_strength > 0): copy the first
               int(crossover_strength * P) params of a shuffle from parent 2
-              (globalGA.py:227-235); GA(crossover=op) (CrossoverMixin, :123-134):
+              (globalGA.py:68-76); GA(crossover=op) (CrossoverMixin, :123-134):
               op3_cross_<op>(new, parent1, parent2, d=size // 3) on every
               permutation of size > 6 when two parents were selected (perm draw
               site p|5<<28)

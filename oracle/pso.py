@@ -15,7 +15,7 @@ so with cfg = x, cfg1 = g, cfg2 = l:
           value never changes (enum_mode=0, reference); enum_mode=1 copies from
           the drawn parent instead (corrected).
 Reference quirk kept by default: `self.best = self.position` aliases the same
-dict (pso.py:212-213, :199), so l == x and the local term is 0 -- pass
+dict (pso.py:60, :46), so l == x and the local term is 0 -- pass
 pbest = pos to reproduce it.
 
   Permutation (:1115-1140): if uniform(0,1) > c: op3_cross(cfg, cfg, g if

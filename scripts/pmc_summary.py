@@ -1,6 +1,10 @@
 """Summarise rocprofv3 output into profiles/:
 
-  python scripts/pmc_summary.py gpurun_out/prof rNN
+  python scripts/pmc_summary.py gpurun_out/prof rNN [SUFFIX]
+
+SUFFIX ("_l2" for the C2 rounds at ell = 2, bench.py --ell 2) is appended to
+every record key, so the headline's and the secondary line's records sit side
+by side; every record carries the tag of the pass it came from ("source").
 
 * kernel_stats (from --kernel-trace --stats) -> profiles/<tag>_kernel_stats.csv
 * FETCH_SIZE / WRITE_SIZE passes (separate --pmc runs) -> per-kernel mean per
@@ -36,7 +40,7 @@ STAGES = {  # stage key -> kernel-name prefixes (the first match wins)
 # stages of the default C2 round that a refreshed C2 profile replaces (a key
 # absent from the new profile -- e.g. de_diff, now folded into k_de -- is dropped)
 C2_ROUND = ("var", "var_1wg", "kstar", "hash", "propose", "encode", "prep_cand", "finalize", "dedup_insert",
-            "dedup_mark", "topk0", "topk1", "inner_pairs", "de_diff", "pop_digests")
+            "dedup_mark", "topk0", "topk1", "inner_pairs", "de_diff", "pop_digests", "var8", "kstar8", "split8", "finalize8")
 
 
 
@@ -49,7 +53,7 @@ def per_kernel(path, counter):
     return {k: sum(v) / len(v) for k, v in acc.items()}
 
 
-def main(prof, tag):
+def main(prof, tag, suffix=""):
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     out_dir = os.path.join(root, "profiles")
     os.makedirs(out_dir, exist_ok=True)
@@ -73,8 +77,8 @@ def main(prof, tag):
         if not (kf and kw):
             continue
         fr, wr = fetch[kf[0]], write[kw[0]]
-        summary[key] = {
-            "kernel": kf[0][:120],
+        summary[key + suffix] = {
+            "kernel": kf[0][:120], "source": tag,
             "fetch_size_kb_raw": fr, "write_size_kb_raw": wr,
             "read_bytes_per_launch": 2.0 * fr * 1024.0, "write_bytes_per_launch": wr * 1024.0,
             "hbm_bytes_per_launch": 2.0 * fr * 1024.0 + wr * 1024.0,
@@ -87,11 +91,13 @@ def main(prof, tag):
             merged = json.load(f)
     except Exception:
         pass
-    if "var" in summary:
+    if "var" + suffix in summary or "var8" + suffix in summary:
         for k in C2_ROUND:
-            merged.pop(k, None)
+            merged.pop(k + suffix, None)
     merged.update({k: v for k, v in summary.items() if k != "_note"})
-    merged["_note"] = summary["_note"] if "var" in summary else merged.get("_note", summary["_note"])
+    merged["_note"] = ("bytes per launch; read = 2 x FETCH_SIZE x 1024 (gfx950 correction, MI355X_MICROARCH.md "
+                       "§HBM), write = WRITE_SIZE x 1024; raw counters kept. Each record's 'source' names its pass; "
+                       "keys ending _l2 are the C2 rounds at ell = 2")
     with open(os.path.join(out_dir, "pmc_summary.json"), "w") as f:
         json.dump(merged, f, indent=1)
     with open(os.path.join(out_dir, f"{tag}_pmc_summary.json"), "w") as f:
@@ -100,4 +106,4 @@ def main(prof, tag):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2])
+    main(sys.argv[1], sys.argv[2], sys.argv[3] if len(sys.argv) > 3 else "")

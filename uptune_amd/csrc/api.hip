@@ -984,7 +984,7 @@ static int round_outputs(ut_ctx* c, const ut_round_out* out, int64_t ld, int64_t
 }
 
 // A GA / GGA scoring round (ut_score_round_ga): the children of parent1
-// (evolutionarytechniques.py:29-61, globalGA.py:187-235), then hash_config of
+// (evolutionarytechniques.py:29-61, globalGA.py:28-48 and :68-76), then hash_config of
 // the children (the parent's inner digests reused) + dedup on the side stream
 // beside the fused encode and the GP scoring, their invalid children joined to
 // the duplicates, top-k.  What the C4 round ran as separate calls on one stream.

@@ -615,7 +615,7 @@ __global__ __launch_bounds__(256) void k_pso(const DevParam* __restrict__ params
 // GA family: EvolutionaryTechnique.desired_configuration
 // (evolutionarytechniques.py:29-61), NormalMutationMixin (:98-114),
 // CrossoverMixin (:117-134, PERM params of size > 6), GGA crossover
-// (globalGA.py:227-235).  Random d-subsets ("first d of a shuffle") by
+// (globalGA.py:68-76).  Random d-subsets ("first d of a shuffle") by
 // selection sampling, one uniform per parameter (oracle/ga.py).
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ double parent_value(const DevParam& pr, const double* parent, int32_t p, uint32_t sub,

@@ -200,7 +200,7 @@ class BatchEngine:
                    crossover_strength: float = 0.0, must_mutate_count: int = 1, normal: bool = False,
                    max_retries: int = 10, op: int = 4, crossover: Optional[str] = None):
         """EvolutionaryTechnique / GGA proposals (evolutionarytechniques.py:29-61,
-        globalGA.py:187-235); `crossover` = GA(crossover=...) for permutation
+        globalGA.py:28-48 and :68-76); `crossover` = GA(crossover=...) for permutation
         params (CrossoverMixin, :117-134).  Returns (values [ncols][m], invalid [m])."""
         p1, p2 = self._row(parent1), self._row(parent2)
         out = self._empty(self.spec.ncols, m)

@@ -798,7 +798,7 @@ class GpuGA(GpuBatchTechnique):
 
 
 class GpuGGA(GpuGA):
-    """globalGA.NormalGreedyMutation(crossover_rate=0.5, crossover_strength=0.2) (globalGA.py:288)"""
+    """globalGA.NormalGreedyMutation(crossover_rate=0.5, crossover_strength=0.2) (globalGA.py:129)"""
 
     def __init__(self, *pargs, **kwargs):
         kwargs.setdefault("mutation_rate", 0.1)
