@@ -436,7 +436,10 @@ int ut_comm_info(ut_ctx* ctx, int32_t* rank, int32_t* nranks);
  * in: idx [k] (global, -1 = empty), score [k], digest [k][8], and optionally
  * the selected rows [ncols][ld_rows] (ncols = 0: none).  out: the merged
  * idx / score / digest [k] and rows [ncols][ld_out], identical on every rank
- * (any output may be NULL). */
+ * (any output may be NULL).  When a call needs larger record buffers than the
+ * ranks last agreed on, every rank allocates and the ranks agree on success
+ * (an all-reduce MIN) before the all-gather: an allocation failure on any
+ * rank returns UT_ENOMEM on every rank, none is left inside the collective. */
 int ut_comm_allgather_topk(ut_ctx* ctx, int32_t k, const int64_t* idx, const double* score, const uint32_t* digest,
                            const double* rows, int64_t ld_rows, int32_t ncols, int64_t* out_idx, double* out_score,
                            uint32_t* out_digest, double* out_rows, int64_t ld_out);
@@ -465,6 +468,9 @@ enum { UT_RED_SUM = 0, UT_RED_MAX = 1, UT_RED_MIN = 2 };
 int ut_comm_allreduce_f64(ut_ctx* ctx, double* buf, int64_t n, int32_t op);
 /* every rank's stream reaches this point (an all-reduce, then a stream sync) */
 int ut_comm_barrier(ut_ctx* ctx);
+/* Fault injection for tests: the next `count` device allocations of the
+ * context that would grow a buffer fail with UT_ENOMEM (0 clears it). */
+int ut_debug_fail_alloc(ut_ctx* ctx, int32_t count);
 
 /* per-kernel device time (ms) of the ut_score_round_* calls since timing was
  * enabled with ut_set_timing(ctx, 1), averaged over those rounds.  Events are

@@ -1,0 +1,401 @@
+// Round 6 probe: shapes of the int8-digit variance contraction (gp_i8.hip
+// k_gp_var_i8) on RANDOM digit planes -- the power-limited regime of the C2
+// round at ell = 2, where the library kernel runs 10.4 ms at 1.75 GHz (MFMA
+// busy 0.59) against 7.8 ms at 2.26 GHz on the ell = 0.2 round's zero planes.
+//
+// One template, k_var<WR, NW, NST, WPC>:
+//   WR  rows per wave (32: two 32x32 column tiles of one row block; 64: 2 x 2)
+//   NW  waves per workgroup (4 or 8); tile = (NW / 2) * WR rows x 128 candidates
+//   NST ring stages of 32 k (global_load_lds, issued NST - 1 ahead)
+//   WPC workgroups per CU (launch bounds)
+// v0 = <32, 4, 2, 2> is the library kernel's shape.  Every variant's per-column
+// sum over rows of v^2 is compared with v0's (the same exact int32 group sums
+// per element, fp64 sums in another order: <= 1e-13 relative).
+//   hipcc -O3 -std=c++17 --offload-arch=gfx950 scripts/exp/var8_probe.hip -o scripts/exp/var8_probe
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <algorithm>
+#include <type_traits>
+#include <vector>
+
+#define CK(x)                                                                            \
+  do {                                                                                   \
+    hipError_t e_ = (x);                                                                 \
+    if (e_ != hipSuccess) {                                                              \
+      printf("HIP error %s at %s:%d\n", hipGetErrorString(e_), __FILE__, __LINE__);      \
+      exit(1);                                                                           \
+    }                                                                                    \
+  } while (0)
+
+typedef int32_t v4i __attribute__((ext_vector_type(4)));
+typedef int32_t v16i __attribute__((ext_vector_type(16)));
+constexpr int S = 6;     // digit planes
+constexpr int BK = 32;   // k per stage
+constexpr int WN = 128;  // candidates per tile
+
+__host__ __device__ inline int64_t i8_off(int64_t r, int32_t k, int64_t ld) {
+  return ((int64_t)(k >> 5) * ld + r) * 32 + ((((k >> 4) & 1) ^ (int)((r >> 3) & 1)) << 4) + (k & 15);
+}
+
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+  static_assert(N >= 0 && N < 64, "vmcnt");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+}
+
+template <int WR, int NW, int NST, int WPC, bool STATIC, bool SPREAD = false>
+__global__ __launch_bounds__(NW * 64, WPC) void k_var(const int8_t* __restrict__ Ad, const int8_t* __restrict__ Bd,
+                                                      int32_t npad, int64_t ldk, int32_t RT, int32_t CT, int64_t m,
+                                                      int32_t* __restrict__ ticket, const double* __restrict__ rs,
+                                                      double* __restrict__ part, int32_t Sg) {
+  constexpr int RB = WR / 32;               // 32-row blocks per wave
+  constexpr int BM = (NW / 2) * WR;         // tile rows
+  constexpr int APL = BM * BK;              // one A plane's piece of a stage
+  constexpr int BPL = WN * BK;              // one B plane's piece (4 KiB)
+  constexpr int STAGE = S * (APL + BPL);
+  constexpr int PIECES = STAGE / 1024;      // 1-KiB glds pieces per stage
+  static_assert(PIECES % NW == 0, "pieces per wave");
+  constexpr int PW = PIECES / NW;           // per wave per stage
+  constexpr int APIECES = S * APL / 1024;
+  __shared__ __attribute__((aligned(16))) int8_t lds[NST * STAGE + (NW / 2) * WN * 8 + BM * 8 + 16];
+  double* red = reinterpret_cast<double*>(lds + NST * STAGE);   // [NW/2][128]
+  double* srs = red + (NW / 2) * WN;                            // row scales of the tile
+  int32_t& s_item = *reinterpret_cast<int32_t*>(srs + BM);
+  const int t = threadIdx.x, lane = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wm = w >> 1, wn = w & 1;
+  const int32_t xcd = blockIdx.x & 7;
+  const int64_t aplane = (int64_t)npad * npad, bplane = (int64_t)npad * ldk;
+
+  // stage kt of tile (row0, col0): piece u = w + NW j; A pieces first (APL / 1024 per plane)
+  auto issue = [&](int32_t row0, int64_t col0, int32_t kt, int8_t* st) {
+#pragma unroll
+    for (int j = 0; j < PW; ++j) {
+      const int u = w + NW * j;
+      const int8_t* src;
+      int8_t* dst;
+      if (u < APIECES) {
+        const int pl = u / (APL / 1024), h = u % (APL / 1024);
+        src = Ad + pl * aplane + ((int64_t)kt * npad + row0) * 32 + h * 1024;
+        dst = st + pl * APL + h * 1024;
+      } else {
+        const int v = u - APIECES, pl = v / (BPL / 1024), h = v % (BPL / 1024);
+        src = Bd + pl * bplane + ((int64_t)kt * ldk + col0) * 32 + h * 1024;
+        dst = st + S * APL + pl * BPL + h * 1024;
+      }
+      __builtin_amdgcn_global_load_lds(src + lane * 16, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+    }
+  };
+
+  // piece j (of PW) of stage kt: SPREAD issues them one by one between the MFMAs
+  auto issue_piece = [&](int32_t row0, int64_t col0, int32_t kt, int8_t* st, int j) {
+    const int u = w + NW * j;
+    const int8_t* src;
+    int8_t* dst;
+    if (u < APIECES) {
+      const int pl = u / (APL / 1024), h = u % (APL / 1024);
+      src = Ad + pl * aplane + ((int64_t)kt * npad + row0) * 32 + h * 1024;
+      dst = st + pl * APL + h * 1024;
+    } else {
+      const int v = u - APIECES, pl = v / (BPL / 1024), h = v % (BPL / 1024);
+      src = Bd + pl * bplane + ((int64_t)kt * ldk + col0) * 32 + h * 1024;
+      dst = st + S * APL + pl * BPL + h * 1024;
+    }
+    __builtin_amdgcn_global_load_lds(src + lane * 16, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+  };
+  const int32_t P = (RT + 1) / 2;
+  const int c = lane >> 5;
+  int aoff[RB];
+#pragma unroll
+  for (int rb = 0; rb < RB; ++rb) {
+    const int ra = wm * WR + rb * 32 + (lane & 31);
+    aoff[rb] = ra * 32 + ((c ^ ((ra >> 3) & 1)) << 4);
+  }
+  int boff[2];
+#pragma unroll
+  for (int jj = 0; jj < 2; ++jj) {
+    const int cb = wn * 64 + jj * 32 + (lane & 31);
+    boff[jj] = S * APL + cb * 32 + ((c ^ ((cb >> 3) & 1)) << 4);
+  }
+  const int32_t Wx = gridDim.x >> 3, bx = blockIdx.x >> 3;
+  for (int32_t it = 0;; ++it) {
+    int32_t j;
+    if constexpr (STATIC) {
+      // every workgroup of the XCD group walks its own fixed item sequence:
+      // the P pairs of a strip start together and, all items being the same
+      // length, stay in step -- each B stage is read by them within a few stages
+      j = it * Wx + bx;
+    } else {
+      if (t == 0) s_item = atomicAdd(&ticket[xcd], 1);
+      __syncthreads();
+      j = __builtin_amdgcn_readfirstlane(s_item);   // uniform: scalar item arithmetic
+    }
+    const int32_t G = j / (P * Sg), q = j % (P * Sg), p = q % P;
+    const int32_t ct = (G * Sg + q / P) * 8 + xcd;
+    if (ct >= CT) break;
+    int32_t rts[2] = {RT - 1 - p, p};
+    const int nrt = rts[1] == rts[0] ? 1 : 2;
+    for (int ri = 0; ri < nrt; ++ri) {
+      if (ri > 0) __syncthreads();
+      const int32_t rt = rts[ri];
+      const int32_t row0 = rt * BM;
+      const int64_t col0 = (int64_t)ct * WN;
+      const int32_t nk = (row0 + BM) / BK;
+      const bool rev = ri > 0;
+      auto ktof = [&](int32_t u) -> int32_t { return rev ? nk - 1 - u : u; };
+      v16i acc[RB][2][S];
+#pragma unroll
+      for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+          for (int g = 0; g < S; ++g)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[rb][jj][g][r] = 0;
+      if (w == 0 && lane < BM / 2)
+        __builtin_amdgcn_global_load_lds(rs + row0 + lane * 2, (__attribute__((address_space(3))) void*)srs, 16, 0, 0);
+#pragma unroll
+      for (int s0 = 0; s0 < NST - 1; ++s0)
+        if (s0 < nk) issue(row0, col0, ktof(s0), lds + s0 * STAGE);
+      for (int32_t u = 0; u < nk; ++u) {
+        // stage u landed: at most NST - 2 younger stages of this wave in flight
+        if constexpr (NST == 3) {
+          if (u + 1 < nk) vm_wait<PW>();
+          else vm_wait<0>();
+        } else {
+          vm_wait<0>();
+        }
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        const bool nxt = u + NST - 1 < nk;
+        const int32_t ktn = nxt ? ktof(u + NST - 1) : 0;
+        int8_t* stn = lds + ((u + NST - 1) % NST) * STAGE;
+        const int32_t kt = ktof(u);
+        const int8_t* st = lds + (u % NST) * STAGE;
+        if constexpr (SPREAD && RB == 1) {
+          if (kt * BK >= row0 + WR * wm + 32) {   // this wave's rows are all zero here: loads only
+            if (nxt) issue(row0, col0, ktn, stn);
+            continue;
+          }
+          v4i af[S];
+#pragma unroll
+          for (int pp = 0; pp < S; ++pp) af[pp] = *reinterpret_cast<const v4i*>(st + pp * APL + aoff[0]);
+#pragma unroll
+          for (int qb = 0; qb < S; ++qb) {
+            v4i bf[2];
+#pragma unroll
+            for (int jj = 0; jj < 2; ++jj) bf[jj] = *reinterpret_cast<const v4i*>(st + qb * BPL + boff[jj]);
+#pragma unroll
+            for (int pa = 0; pa + qb < S; ++pa)
+#pragma unroll
+              for (int jj = 0; jj < 2; ++jj)
+                acc[0][jj][pa + qb] = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[pa], bf[jj], acc[0][jj][pa + qb], 0, 0, 0);
+            // this qb's share of the next stage's pieces, between the MFMAs
+            if (nxt) {
+#pragma unroll
+              for (int jp = 0; jp < PW; ++jp)
+                if (jp % S == qb) issue_piece(row0, col0, ktn, stn, jp);
+            }
+          }
+          continue;
+        }
+        if (nxt) issue(row0, col0, ktn, stn);
+        if constexpr (RB == 2) {
+          // both row blocks: A fragments of both once, each B fragment once per stage
+          const bool l1 = kt * BK < row0 + WR * wm + 64, l0 = kt * BK < row0 + WR * wm + 32;
+          if (!l1) continue;
+          auto body = [&](auto both_c) {
+            constexpr bool BOTH = decltype(both_c)::value;
+            v4i af[2][S];
+#pragma unroll
+            for (int pp = 0; pp < S; ++pp) {
+              if (BOTH) af[0][pp] = *reinterpret_cast<const v4i*>(st + pp * APL + aoff[0]);
+              af[1][pp] = *reinterpret_cast<const v4i*>(st + pp * APL + aoff[1]);
+            }
+#pragma unroll
+            for (int qb = 0; qb < S; ++qb) {
+              v4i bf[2];
+#pragma unroll
+              for (int jj = 0; jj < 2; ++jj) bf[jj] = *reinterpret_cast<const v4i*>(st + qb * BPL + boff[jj]);
+#pragma unroll
+              for (int pa = 0; pa + qb < S; ++pa)
+#pragma unroll
+                for (int rb = BOTH ? 0 : 1; rb < 2; ++rb)
+#pragma unroll
+                  for (int jj = 0; jj < 2; ++jj)
+                    acc[rb][jj][pa + qb] =
+                        __builtin_amdgcn_mfma_i32_32x32x32_i8(af[rb][pa], bf[jj], acc[rb][jj][pa + qb], 0, 0, 0);
+            }
+          };
+          if (l0) body(std::integral_constant<bool, true>{});
+          else body(std::integral_constant<bool, false>{});
+          continue;
+        }
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb) {
+          if (kt * BK >= row0 + WR * wm + 32 * rb + 32) continue;   // rows of this block: all zero here
+          v4i af[S];
+#pragma unroll
+          for (int pp = 0; pp < S; ++pp) af[pp] = *reinterpret_cast<const v4i*>(st + pp * APL + aoff[rb]);
+#pragma unroll
+          for (int qb = 0; qb < S; ++qb) {
+            v4i bf[2];
+#pragma unroll
+            for (int jj = 0; jj < 2; ++jj) bf[jj] = *reinterpret_cast<const v4i*>(st + qb * BPL + boff[jj]);
+#pragma unroll
+            for (int pa = 0; pa + qb < S; ++pa)
+#pragma unroll
+              for (int jj = 0; jj < 2; ++jj)
+                acc[rb][jj][pa + qb] = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[pa], bf[jj], acc[rb][jj][pa + qb], 0, 0, 0);
+          }
+        }
+      }
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) {
+        double s = 0.0;
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            double v = (double)acc[rb][jj][S - 1][r];
+#pragma unroll
+            for (int g = S - 2; g >= 0; --g) v = __builtin_fma(v, 0x1p-8, (double)acc[rb][jj][g][r]);
+            v *= 0x1p-16 * srs[wm * WR + rb * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)];
+            s = __builtin_fma(v, v, s);
+          }
+        s += __shfl_xor(s, 32);
+        if (lane < 32) red[wm * WN + wn * 64 + jj * 32 + lane] = s;
+      }
+      __syncthreads();
+      if (t < WN) {
+        const int64_t col = col0 + t;
+        double a = 0.0;
+#pragma unroll
+        for (int q2 = 0; q2 < NW / 2; ++q2) a += red[q2 * WN + t];
+        if (col < m) part[(int64_t)rt * ldk + col] = a;
+      }
+    }
+  }
+}
+
+struct Res {
+  double ms;
+  std::vector<double> colsum;
+};
+
+template <int WR, int NW, int NST, int WPC, bool STATIC, bool SPREAD = false>
+static void launch(const int8_t* A, const int8_t* B, int npad, int64_t ldk, int64_t m, int32_t* tk, const double* rs,
+                   double* part, int n_cu, hipStream_t st) {
+  constexpr int BM = (NW / 2) * WR;
+  const int32_t RT = npad / BM, CT = (int32_t)((m + WN - 1) / WN);
+  const int32_t P = (RT + 1) / 2;
+  const int64_t items = (int64_t)P * CT;
+  int32_t nb = WPC * (n_cu / 8) * 8;
+  if (items < nb) nb = (int32_t)(((items + 7) / 8) * 8);
+  const int32_t W = nb / 8, Sg = W / P > 1 ? W / P : 1;
+  CK(hipMemsetAsync(tk, 0, 8 * sizeof(int32_t), st));
+  hipLaunchKernelGGL((k_var<WR, NW, NST, WPC, STATIC, SPREAD>), dim3(nb), dim3(NW * 64), 0, st, A, B, npad, ldk, RT, CT, m, tk, rs,
+                     part, Sg);
+}
+
+int main(int argc, char** argv) {
+  const int npad = argc > 1 ? atoi(argv[1]) : 1024;
+  const int64_t m = argc > 2 ? atoll(argv[2]) : (1 << 20);
+  const int reps = argc > 3 ? atoi(argv[3]) : 5;
+  const int zeroB = argc > 4 ? atoi(argv[4]) : 0;   // 1: B planes 2..6 zero (the ell = 0.2 round's operands)
+  const int64_t ldk = (m + 255) / 256 * 256;
+  hipDeviceProp_t prop;
+  CK(hipGetDeviceProperties(&prop, 0));
+  const int n_cu = prop.multiProcessorCount;
+  const size_t abytes = (size_t)S * npad * npad, bbytes = (size_t)S * npad * ldk;
+  std::vector<int8_t> hA(abytes, 0);
+  srand(7);
+  for (int p = 0; p < S; ++p)
+    for (int r = 0; r < npad; ++r)
+      for (int k = 0; k <= r; ++k) hA[(size_t)p * npad * npad + i8_off(r, k, npad)] = (int8_t)(rand() & 255);
+  std::vector<double> hrs(npad);
+  for (int r = 0; r < npad; ++r) hrs[r] = std::ldexp(1.0, -(rand() % 4));
+  int8_t *A, *B;
+  double *rs, *part;
+  int32_t* tk;
+  CK(hipMalloc(&A, abytes));
+  CK(hipMalloc(&B, bbytes));
+  CK(hipMalloc(&rs, npad * sizeof(double)));
+  CK(hipMalloc(&part, (size_t)(npad / 64) * ldk * sizeof(double)));
+  CK(hipMalloc(&tk, 32 * sizeof(int32_t)));
+  CK(hipMemcpy(A, hA.data(), abytes, hipMemcpyHostToDevice));
+  CK(hipMemcpy(rs, hrs.data(), npad * sizeof(double), hipMemcpyHostToDevice));
+  {  // B: random digits (device-side fill: 6.4 GB)
+    std::vector<int8_t> chunk(1 << 26);
+    for (auto& x : chunk) x = (int8_t)(rand() & 255);
+    for (size_t o = 0; o < bbytes; o += chunk.size()) {
+      const size_t nb = std::min(chunk.size(), bbytes - o);
+      const int p = (int)(o / ((size_t)npad * ldk));
+      if (zeroB && p >= 1) CK(hipMemset(B + o, 0, nb));
+      else CK(hipMemcpy(B + o, chunk.data(), nb, hipMemcpyHostToDevice));
+    }
+  }
+  hipStream_t st;
+  CK(hipStreamCreate(&st));
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  const char* names[] = {"v0 <32,4,2,2> (library)", "v2 <32,8,3,1>", "v6 <32,4,2,2> spread",
+                         "v7 <32,8,3,1> spread"};
+  const int NV = 4;
+  auto run = [&](int v) {
+    switch (v) {
+      case 0: launch<32, 4, 2, 2, false>(A, B, npad, ldk, m, tk, rs, part, n_cu, st); break;
+      case 1: launch<32, 8, 3, 1, false>(A, B, npad, ldk, m, tk, rs, part, n_cu, st); break;
+      case 2: launch<32, 4, 2, 2, false, true>(A, B, npad, ldk, m, tk, rs, part, n_cu, st); break;
+      case 3: launch<32, 8, 3, 1, false, true>(A, B, npad, ldk, m, tk, rs, part, n_cu, st); break;
+    }
+  };
+  const int bm[] = {64, 128, 64, 128};
+  std::vector<double> ref;
+  bool ok = true;
+  for (int v = 0; v < NV; ++v) {   // correctness: column sums against v0
+    CK(hipMemsetAsync(part, 0, (size_t)(npad / 64) * ldk * sizeof(double), st));
+    run(v);
+    CK(hipStreamSynchronize(st));
+    std::vector<double> hp((size_t)(npad / bm[v]) * ldk);
+    CK(hipMemcpy(hp.data(), part, hp.size() * sizeof(double), hipMemcpyDeviceToHost));
+    std::vector<double> cs(m, 0.0);
+    for (int rt = 0; rt < npad / bm[v]; ++rt)
+      for (int64_t c = 0; c < m; ++c) cs[c] += hp[(size_t)rt * ldk + c];
+    if (v == 0) {
+      ref = cs;
+    } else {
+      double mx = 0.0;
+      for (int64_t c = 0; c < m; ++c) mx = std::max(mx, std::fabs(cs[c] - ref[c]) / std::max(std::fabs(ref[c]), 1e-300));
+      printf("%s: max rel diff vs v0 %.3e\n", names[v], mx);
+      if (!(mx <= 1e-12)) ok = false;
+    }
+  }
+  const double flops = (double)m * npad * (npad + 1);
+  std::vector<std::vector<float>> ms(NV);
+  for (int w = 0; w < 3; ++w)
+    for (int v = 0; v < NV; ++v) run(v);   // warm the clock
+  for (int r = 0; r < reps; ++r)
+    for (int v = 0; v < NV; ++v) {
+      CK(hipEventRecord(e0, st));
+      run(v);
+      CK(hipEventRecord(e1, st));
+      CK(hipEventSynchronize(e1));
+      float t;
+      CK(hipEventElapsedTime(&t, e0, e1));
+      ms[v].push_back(t);
+    }
+  for (int v = 0; v < NV; ++v) {
+    std::vector<float> s = ms[v];
+    std::sort(s.begin(), s.end());
+    printf("%-28s median %.3f ms  min %.3f  (%.1f fp64-eq TF/s, frac of int8/21 %.3f)\n", names[v], s[s.size() / 2],
+           s[0], flops / (s[s.size() / 2] * 1e-3) / 1e12, flops / (s[s.size() / 2] * 1e-3) / 1e12 / 239.676);
+  }
+  printf("%s\n", ok ? "CHECK OK" : "CHECK FAILED");
+  return ok ? 0 : 1;
+}

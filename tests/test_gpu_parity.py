@@ -1025,6 +1025,49 @@ def test_score_round_de_pruned_equals_dense_round():
         np.testing.assert_array_equal(a[3].cpu().numpy(), b[3].cpu().numpy())
 
 
+@pytest.mark.parametrize("order", ["feat_first", "round_first"])
+def test_pruned_entry_points_share_one_categorical_fit(order):
+    """the f32 bound pass caches an f32 copy of the training operand
+    per fit.  In categorical mode the feature entry (ut_gp_topk_pruned: every
+    feature, dense K*) and the fused DE round (ut_score_round_de_pruned: the
+    numeric block + one-hot codes) take different operands; run both on ONE
+    fit, in either order, and each must equal its dense counterpart."""
+    _require_gpu()
+    space = hpl_space()
+    e = engine(space, seed=21)
+    e.gp_set_prune_pass(32)
+    pop = ode.population_init(space, 8192, seed=21)
+    e.population_set(dev(pop))
+    n = 512
+    X = features(space, pop[:, :n]).T
+    y = np.sum((X - 0.4) ** 2, axis=1)
+    e.gp_fit(X, y, lengthscale=1.0, sigma_f2=1.0, sigma_n2=1e-6, jitter=1e-8)
+    assert e.gp_kstar_mode() == "categorical"
+    e.history_reset(0)
+    trial = e.propose_de(8192, round_=5, cr=0.3)
+    feat = e.encode(trial)
+
+    def feat_entry():
+        idx, top, st = e.gp_topk_pruned(feat, 32, bound_rows=128)
+        _, _, score = e.gp_score(feat)
+        i2, t2 = e.topk(score, 32)
+        _close(top.cpu().numpy(), t2.cpu().numpy(), rtol=1e-9, atol=1e-12)
+        if np.abs(np.diff(t2.cpu().numpy())).min() > 1e-9:
+            assert idx.cpu().numpy().tolist() == i2.cpu().numpy().tolist()
+
+    def round_entry():
+        a = e.score_round_de(8192, 32, round_=3, cand_base=0, cr=0.3)
+        b = e.score_round_de_pruned(8192, 32, round_=3, cand_base=0, cr=0.3, bound_rows=128)
+        sa, sb = a[1].cpu().numpy(), b[1].cpu().numpy()
+        _close(sb, sa, rtol=1e-9, atol=1e-12)
+        if np.abs(np.diff(sa)).min() > 1e-9:
+            assert a[0].cpu().numpy().tolist() == b[0].cpu().numpy().tolist()
+
+    for f in ((feat_entry, round_entry, feat_entry) if order == "feat_first" else
+              (round_entry, feat_entry, round_entry)):
+        f()
+
+
 @pytest.mark.parametrize("which", ["mixed", "r64", "hpl", "perm"])
 def test_hash_parent_reuses_parent_digests(which):
     """ut_hash_parent (inner digests of values equal to the parent's taken from

@@ -47,6 +47,17 @@ def _worker(port, q):
         from uptune_amd import dist as D
         out["via"] = sorted(type(c).__name__ for c in D._COMMS.values())
         out["topk"] = (mi.device.type, mi.cpu().tolist(), ms.cpu().tolist())
+        # an allocation failure while the record buffers grow (rows: wider
+        # records) returns UT_ENOMEM after the ranks' vote, not a hang inside
+        # the all-gather; the next call allocates and succeeds
+        comm = list(D._COMMS.values())[0]
+        comm.lib.ut_debug_fail_alloc(comm.ctx, 1)
+        try:
+            allgather_topk(idx, sc, dig, 4, rows=torch.ones((3, 4), dtype=torch.float64, device=dev))
+            out["enomem"] = "no error"
+        except Exception as ex:
+            out["enomem"] = str(ex)
+        comm.lib.ut_debug_fail_alloc(comm.ctx, 0)
         rows = torch.arange(12, dtype=torch.float64, device=dev).reshape(3, 4)
         si, ss, sr, sd = allgather_selection(idx, sc, dig, rows, 4, with_digests=True)
         out["sel"] = (si.cpu().tolist(), sr.device.type, sr.cpu().tolist(), sd.shape[0])
@@ -93,5 +104,6 @@ def test_rccl_collectives_and_loop_world1():
     bdev, y, same = out["bcast"]
     assert bdev == "cuda" and y == [1.5, 2.5] and same
     assert out["agree"] == (True, False)
+    assert "UT_ENOMEM" in out["enomem"] and "no memory for the records" in out["enomem"], out["enomem"]
     tc, nres, best = out["loop"]
     assert tc > 40 and 0.8 * tc <= nres <= tc and best < 6 * 2.5 ** 2

@@ -110,7 +110,7 @@ def _check(drv, fx):
         first.setdefault(r["configuration_id"], r["id"])
     assert dup_ids == [3, 7, 8, 9, 12]
     want = [(d["test_count"], d["requestor"], d["first_requestor"], d["class"]) for d in fx["log_duplicates"]]
-    assert drv.duplicate_log == want
+    assert list(drv.duplicate_log) == want and drv.duplicate_count == len(want)
     assert drv.best_result.time == min(r["time"] for r in res)
 
 

@@ -153,6 +153,7 @@ SIGNATURES = {
     "ut_comm_bcast": (C.c_int, [P, P, I64, I32]),
     "ut_comm_allreduce_f64": (C.c_int, [P, P, I64, I32]),
     "ut_comm_barrier": (C.c_int, [P]),
+    "ut_debug_fail_alloc": (C.c_int, [P, I32]),
     "ut_set_timing": (C.c_int, [P, I32]),
     "ut_stage_time": (C.c_int, [P, C.c_char_p, C.POINTER(D)]),
 }

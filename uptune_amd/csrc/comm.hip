@@ -218,6 +218,7 @@ void comm_release(ut_ctx* c) {
   }
   c->comm_rank = 0;
   c->comm_size = 1;
+  c->cm_agreed_send = c->cm_agreed_recv = 0;
 }
 
 }  // namespace ut
@@ -291,14 +292,32 @@ int ut_comm_allgather_topk(ut_ctx* c, int32_t k, const int64_t* idx, const doubl
                            uint32_t* out_digest, double* out_rows, int64_t ld_out) {
   if (!c) return UT_EINVAL;
   int rc;
-  UT_CHECK(c, c->comm != nullptr, UT_EINVAL, "comm_allgather_topk: call ut_comm_init first");
+  UT_CHECK(c, c->comm != nullptr && c->cm_cnt.p != nullptr, UT_EINVAL, "comm_allgather_topk: call ut_comm_init first");
   UT_CHECK(c, idx && score, UT_EINVAL, "comm_allgather_topk: NULL idx / score");
   if ((rc = check_merge_args(c, k, ncols, rows, ld_rows, k, out_rows, ld_out))) return rc;
   UT_HIP(c, hipSetDevice(c->device));
   const int32_t W = REC_HDR + ncols;
   const int64_t n = (int64_t)k * c->comm_size;
-  if ((rc = ensure(c, c->cm_send, (size_t)k * W))) return rc;
-  if ((rc = ensure(c, c->cm_recv, (size_t)n * W))) return rc;
+  const size_t need_send = (size_t)k * W, need_recv = (size_t)n * W;
+  if (need_send > c->cm_agreed_send || need_recv > c->cm_agreed_recv) {
+    // the record buffers grow: every rank allocates, then the ranks agree on
+    // success (all-reduce MIN of an ok flag) before the all-gather, so a rank
+    // that could not allocate makes every rank return UT_ENOMEM instead of
+    // leaving its peers inside ncclAllGather (ut_comm_bcast_results' step 2).
+    // The agreed capacity is the same on every rank (the same calls in the same
+    // order), so every rank takes this branch in the same calls.
+    const bool have = ensure(c, c->cm_send, need_send) == 0 && ensure(c, c->cm_recv, need_recv) == 0;
+    int64_t ok = have ? 1 : 0;
+    UT_HIP(c, hipMemcpyAsync(c->cm_cnt.p + 1, &ok, sizeof(ok), hipMemcpyHostToDevice, c->stream));
+    UT_RCCL(c, ncclAllReduce(c->cm_cnt.p + 1, c->cm_cnt.p + 1, 1, ncclInt64, ncclMin, (ncclComm_t)c->comm, c->stream));
+    UT_HIP(c, hipMemcpyAsync(&ok, c->cm_cnt.p + 1, sizeof(ok), hipMemcpyDeviceToHost, c->stream));
+    UT_HIP(c, hipStreamSynchronize(c->stream));
+    if (!ok)
+      return set_err(c, UT_ENOMEM, have ? "comm_allgather_topk: another rank could not allocate the records"
+                                        : "comm_allgather_topk: no memory for the records");
+    c->cm_agreed_send = need_send;
+    c->cm_agreed_recv = need_recv;
+  }
   hipLaunchKernelGGL(k_pack_records, dim3(grid1(k, MG_NT)), dim3(MG_NT), 0, c->stream, (int64_t)k, idx, score,
                      digest, rows, ld_rows, ncols, W, c->cm_send.p);
   UT_LAUNCH_CHECK(c);
@@ -381,6 +400,13 @@ int ut_comm_allreduce_f64(ut_ctx* c, double* buf, int64_t n, int32_t op) {
   UT_HIP(c, hipSetDevice(c->device));
   const ncclRedOp_t rop = op == UT_RED_SUM ? ncclSum : op == UT_RED_MAX ? ncclMax : ncclMin;
   UT_RCCL(c, ncclAllReduce(buf, buf, (size_t)n, ncclFloat64, rop, (ncclComm_t)c->comm, c->stream));
+  return 0;
+}
+
+int ut_debug_fail_alloc(ut_ctx* c, int32_t count) {
+  if (!c) return UT_EINVAL;
+  UT_CHECK(c, count >= 0, UT_EINVAL, "debug_fail_alloc: count < 0");
+  c->dbg_fail_alloc = count;
   return 0;
 }
 

@@ -859,6 +859,7 @@ __global__ void k_gp_finalize(int64_t m, int32_t RT1, int32_t RT2, const double*
 // exact one.  Every other candidate (near a training point sf2 - |v|^2 cancels;
 // or a failed fit) is appended to idx_out for the fp64 recompute (k_gp_fix_i8),
 // one atomic per wave; its outputs are written anyway and overwritten there.
+// Duplicates (dup[i], score -inf) are never flagged.
 __global__ void k_gp_finalize_i8(int64_t m, int32_t RT1, int32_t RT2, const double* __restrict__ mu_part,
                                  const double* __restrict__ var_part, int64_t ldp, double sf2,
                                  const double* __restrict__ stats, const int32_t* __restrict__ fit_flag, int32_t kind,
@@ -883,7 +884,13 @@ __global__ void k_gp_finalize_i8(int64_t m, int32_t RT1, int32_t RT2, const doub
       mu = var = sc = __builtin_nan("");
       flag = false;   // nothing to recompute: the fit failed
     }
-    if (dup && dup[i]) sc = -1.0 / 0.0;
+    if (dup && dup[i]) {
+      // a duplicate of the history is a training point, where sf2 - |v|^2
+      // cancels and the bound always fails: its score is -inf whatever the
+      // variance, so it is not recomputed (its var output stays this tier's)
+      sc = -1.0 / 0.0;
+      flag = false;
+    }
     if (mu_out) mu_out[i] = mu;
     if (var_out) var_out[i] = var;
     if (score_out) score_out[i] = sc;
@@ -1780,12 +1787,19 @@ int gp_topk_pruned_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, co
     // the bound rows through the fp64 kernel (tiles < R), every other tile
     // through k_gp_kstar_f32c on f32 copies of the operands (Xs^T once per fit)
     const double* xnn = xn ? xn : c->gp_xnorm;
-    if (!c->pr_xf_valid) {
+    // the f32 copy depends on the operand as well as the fit: the numeric
+    // block (categorical mode, cat_dpad rows, gp_xnorm_num) or every feature
+    // (kstar_dpad rows, gp_xnorm) -- within one categorical fit the feature
+    // entry (ut_gp_topk_pruned: cat = false) and the fused DE round (cat =
+    // true) take different ones, so the cache is keyed on (fit, cat, dpad)
+    if (!c->pr_xf_valid || c->pr_xf_cat != cat || c->pr_xf_dpad != dpad) {
       if ((rc = ensure(c, c->pr_xsT_f, (size_t)dpad * npad))) return rc;
       if ((rc = launch_to_f32(c, XsT, c->pr_xsT_f.p, (int64_t)dpad * npad))) return rc;
       hipLaunchKernelGGL(k_max_n, dim3(1), dim3(256), 0, c->stream, xnn, n, c->pr_f2.p + 2 + SQ_BLOCKS);
       UT_LAUNCH_CHECK(c);
       c->pr_xf_valid = true;
+      c->pr_xf_cat = cat;
+      c->pr_xf_dpad = dpad;
     }
     if ((rc = ensure(c, c->pr_ucand_f, (size_t)(dpad > 0 ? dpad : 1) * ldk))) return rc;
     if ((rc = launch_to_f32(c, c->ucand.p, c->pr_ucand_f.p, (int64_t)dpad * ldk))) return rc;

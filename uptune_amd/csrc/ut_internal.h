@@ -322,7 +322,9 @@ struct ut_ctx {
                                                // pass's sum |alpha|
   bool pr_f2_valid = false;                    // pr_f2 belongs to the current fit
   bool pr_ab_valid = false;                    // ... and its sum |alpha|
-  bool pr_xf_valid = false;                    // pr_xsT_f and max |x|^2 belong to the current fit
+  bool pr_xf_valid = false;                    // pr_xsT_f and max |x|^2 belong to the current fit,
+  bool pr_xf_cat = false;                      // ... built from this operand (numeric block or all features)
+  int32_t pr_xf_dpad = -1;                     // ... with this many rows
   ut::DevBuf<float> pr_xsT_f, pr_ucand_f;      // f32 K* operands of the f32-contraction bound pass
   ut::DevBuf<double> pr_sa;                    // [RT][ldk] partials of sum |alpha_r| k*_r (f32 bound pass)
   ut::DevBuf<double> pr_gmu;                   // [RT][ldc] fp64 mean partials of recomputed columns (f32 pass)
@@ -346,6 +348,10 @@ struct ut_ctx {
   ut::DevBuf<uint8_t> cm_keep;             // [R k] record survives the digest dedup
   ut::DevBuf<double> cm_pay;               // [n][5] broadcast payload (value + digest)
   ut::DevBuf<int64_t> cm_cnt;              // [2] broadcast count + agreement flag (allocated by ut_comm_init)
+  // record capacity (uint64 words of cm_send / cm_recv) every rank agreed it
+  // holds: the all-gather votes only when a call needs more (comm.hip)
+  size_t cm_agreed_send = 0, cm_agreed_recv = 0;
+  int32_t dbg_fail_alloc = 0;              // ut_debug_fail_alloc: the next N growing ensure() calls fail
 
   ut::Timing timing;
 };
@@ -404,6 +410,10 @@ inline int32_t kstar_dpad(int32_t d) { return ((d + 3) / 4) * 4; }
 template <class T>
 int ensure(ut_ctx* c, DevBuf<T>& b, size_t n) {
   if (b.n >= n && b.p) return 0;
+  if (c->dbg_fail_alloc > 0) {   // fault injection (tests): this growth fails as hipMalloc would
+    --c->dbg_fail_alloc;
+    return set_err(c, UT_ENOMEM, "hipMalloc: injected failure (ut_debug_fail_alloc)");
+  }
   // a buffer that has to grow again (sizes that follow a growing training
   // set) gets headroom, up to 2 GiB: every regrowth costs a device-wide sync
   size_t want = n;

@@ -29,6 +29,7 @@ run the same loop SPMD over torch.distributed (one process per GPU).
 """
 from __future__ import annotations
 
+import collections
 import logging
 from typing import Any, Callable, Dict, List, Optional
 
@@ -107,7 +108,7 @@ class MinimizeTime:
 class SearchDriver:
     def __init__(self, manipulator, root_technique, objective=None, parallelism: int = 4,
                  hash_fn: Optional[Callable[[Dict[Any, Any]], str]] = None, bail_threshold: int = 500,
-                 pipelining: int = 0, tuning_run=None):
+                 pipelining: int = 0, tuning_run=None, no_dups: bool = False, duplicate_log_max: int = 4096):
         import copy
         self.manipulator = manipulator
         self.objective = objective or MinimizeTime()
@@ -131,8 +132,12 @@ class SearchDriver:
         self._unprocessed: List[Result] = []
         self._todo: List[DesiredResult] = []               # REQUESTED, not yet measured
         # (test_count, requestor, first requestor, OLD | PENDING) per duplicate
-        # request: the reference's log line (driver.py:186-191) as data
-        self.duplicate_log: List[tuple] = []
+        # request: the reference's log line (driver.py:186-191) as data, the
+        # latest duplicate_log_max of them (duplicate_count counts them all);
+        # no_dups silences the warning as the reference's --no-dups does (:185)
+        self.no_dups = no_dups
+        self.duplicate_log = collections.deque(maxlen=duplicate_log_max)
+        self.duplicate_count = 0
         if hasattr(self.objective, "set_driver"):
             self.objective.set_driver(self)
         self.root_technique.set_driver(self)
@@ -253,8 +258,10 @@ class SearchDriver:
                 # OLD once it has a result, PENDING before
                 cls = "OLD" if first.result is not None else "PENDING"
                 self.duplicate_log.append((self.test_count, dr.requestor, first.requestor, cls))
-                log.warning("duplicate configuration request #%d %s/%s %s", self.test_count, dr.requestor,
-                            first.requestor, cls)
+                self.duplicate_count += 1
+                if not self.no_dups:
+                    log.warning("duplicate configuration request #%d %s/%s %s", self.test_count, dr.requestor,
+                                first.requestor, cls)
 
                 def cb(result, dr=dr):
                     dr.result = result

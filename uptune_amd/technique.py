@@ -438,8 +438,10 @@ class SharedModel:
         y = self._yf[:n]
         if self.y_transform == "rank":
             from scipy.special import ndtri
-            r = np.empty(n)
-            r[np.argsort(y, kind="stable")] = np.arange(n)
+            from scipy.stats import rankdata
+            # average ranks: tied (repeated) measurements get one normal score,
+            # whatever their row order
+            r = rankdata(y, method="average") - 1.0
             y = ndtri((r + 0.5) / n)
         self.engine.gp_fit(self._Xf[:n], y, lengthscale=self.lengthscale, wait=False, **self.hyper)
         self._fit_key = key
