@@ -763,11 +763,14 @@ def main():
     i8_info = None
     if args.precision == 8:
         rec, bound_e = eng.gp_i8_stats()   # the last round run: the score-determined parity round when it ran
+        _, bound_emu = eng.gp_i8_bounds()
         i8_info = {"recomputed_fp64_last_timed_round": i8_timed[0], "bound_E": i8_timed[1],
+                   "bound_Emu_last_round_run": bound_emu,
                    "recomputed_fp64_last_round_run": rec, "bound_E_last_round_run": bound_e, "digit_planes": 6,
                    "products": I8_PRODUCTS, "tolerance": 2.0 ** -20,
-                   "note": "variance error per candidate <= E (2 |v| + E) (+ f64 rounding); accepted iff that is "
-                           "<= tolerance * var, else recomputed on the f64 path (gp_i8.hip)"}
+                   "note": "variance error per candidate <= E (2 |v| + E) (+ f64 rounding), mean (v . L^-1 y from "
+                           "the int8 variance epilogue) error <= Emu; accepted iff those are <= tolerance * var and "
+                           "<= tolerance * sigma, else recomputed on the f64 path (gp_i8.hip)"}
     prune_info = None
     if args.prune and prune_stats:
         timed = prune_stats[-args.steps:]

@@ -333,6 +333,12 @@ int ut_gp_set_i8_tol(ut_ctx* ctx, double tol);
  * (-1: most were, and the whole round ran the fp64 contraction), and the
  * current fit's bound E on |L^-1 k* - v^| */
 int ut_gp_i8_stats(ut_ctx* ctx, int64_t* recomputed_host, double* bound_host);
+/* precision 8: the fit's error bounds -- E on |L^-1 k* - v^| (the variance)
+ * and Emu = sum_r e_r |(L^-1 y)_r| on the mean mu^ = v^ . L^-1 y, which the
+ * int8 variance epilogue computes (gp_i8.hip); 0 for other fits.  A candidate
+ * is recomputed in fp64 unless its variance bound is <= tol * var and
+ * Emu <= tol * sqrt(var). */
+int ut_gp_i8_bounds(ut_ctx* ctx, double* E, double* Emu);
 /* order everything enqueued on ctx's stream after this call behind the
  * in-flight fit (a stream wait on its event; no host wait).  Scoring that
  * needs the whole fit (pruned, fp32, f16x3) then starts with the fit done, and

@@ -282,6 +282,144 @@ __global__ __launch_bounds__(NW * 64, WPC) void k_var(const int8_t* __restrict__
   }
 }
 
+// v8: the library shape (32 x 64 per wave, 4 waves, 2-stage ring, two
+// workgroups per CU) with every item quantity scalar (readfirstlane'd: glds
+// bases in SGPRs), and the B fragment of qb + 1 read before the MFMAs of qb
+__global__ __launch_bounds__(256, 2) void k_var8(const int8_t* __restrict__ Ad, const int8_t* __restrict__ Bd,
+                                                 int32_t npad, int64_t ldk, int32_t RT, int32_t CT, int64_t m,
+                                                 int32_t* __restrict__ ticket, const double* __restrict__ rs,
+                                                 double* __restrict__ part, int32_t Sg) {
+  constexpr int BM = 64, APL = BM * BK, BPL = WN * BK, STAGE = S * (APL + BPL);
+  __shared__ __attribute__((aligned(16))) int8_t lds[2 * STAGE + 2 * WN * 8 + BM * 8 + 16];
+  double* red = reinterpret_cast<double*>(lds + 2 * STAGE);
+  double* srs = red + 2 * WN;
+  int32_t& s_item = *reinterpret_cast<int32_t*>(srs + BM);
+  const int t = threadIdx.x, lane = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wm = w >> 1, wn = w & 1;
+  const int32_t xcd = __builtin_amdgcn_readfirstlane(blockIdx.x & 7);
+  const int64_t aplane = (int64_t)npad * npad, bplane = (int64_t)npad * ldk;
+  const int32_t P = (RT + 1) / 2;
+  const int c = lane >> 5;
+  const int ra = wm * 32 + (lane & 31);
+  const int aoff = ra * 32 + ((c ^ ((ra >> 3) & 1)) << 4);
+  int boff[2];
+#pragma unroll
+  for (int jj = 0; jj < 2; ++jj) {
+    const int cb = wn * 64 + jj * 32 + (lane & 31);
+    boff[jj] = S * APL + cb * 32 + ((c ^ ((cb >> 3) & 1)) << 4);
+  }
+  const int lo16 = lane * 16;
+  for (;;) {
+    if (t == 0) s_item = atomicAdd(&ticket[xcd], 1);
+    __syncthreads();
+    const int32_t j = __builtin_amdgcn_readfirstlane(s_item);
+    const int32_t G = j / (P * Sg), q = j % (P * Sg), p = q % P;
+    const int32_t ct = (G * Sg + q / P) * 8 + xcd;
+    if (ct >= CT) break;
+    const int nrt = (RT - 1 - p) == p ? 1 : 2;
+    for (int ri = 0; ri < nrt; ++ri) {
+      if (ri > 0) __syncthreads();
+      const int32_t rt = __builtin_amdgcn_readfirstlane(ri == 0 ? RT - 1 - p : p);
+      const int32_t row0 = rt * BM;
+      const int64_t col0 = (int64_t)ct * WN;
+      const int32_t nk = (row0 + BM) / BK;
+      const bool rev = ri > 0;
+      // this wave's 9 pieces of a stage: A planes (pieces 0..11: plane u >> 1, half u & 1), then B
+      auto issue = [&](int32_t kt, int8_t* st) {
+        const int8_t* abase = Ad + ((int64_t)kt * npad + row0) * 32;
+        const int8_t* bbase = Bd + ((int64_t)kt * ldk + col0) * 32;
+#pragma unroll
+        for (int jp = 0; jp < 9; ++jp) {
+          const int u = w + 4 * jp;
+          const int8_t* src;
+          int8_t* dst;
+          if (u < 12) {
+            src = abase + (u >> 1) * aplane + (u & 1) * 1024;
+            dst = st + (u >> 1) * APL + (u & 1) * 1024;
+          } else {
+            const int v = u - 12;
+            src = bbase + (v >> 2) * bplane + (v & 3) * 1024;
+            dst = st + S * APL + (v >> 2) * BPL + (v & 3) * 1024;
+          }
+          __builtin_amdgcn_global_load_lds(src + lo16, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+        }
+      };
+      v16i acc[2][S];
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+        for (int g = 0; g < S; ++g)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc[jj][g][r] = 0;
+      if (w == 0 && lane < 32)
+        __builtin_amdgcn_global_load_lds(rs + row0 + lane * 2, (__attribute__((address_space(3))) void*)srs, 16, 0, 0);
+      issue(rev ? nk - 1 : 0, lds);
+      const int32_t wrow_end = row0 + 32 * wm + 32;
+      for (int32_t u = 0; u < nk; ++u) {
+        vm_wait<0>();
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        const int32_t kt = rev ? nk - 1 - u : u;
+        if (u + 1 < nk) issue(rev ? nk - 2 - u : u + 1, lds + ((u + 1) & 1) * STAGE);
+        if (kt * BK >= wrow_end) continue;
+        const int8_t* st = lds + (u & 1) * STAGE;
+        v4i af[S];
+#pragma unroll
+        for (int pp = 0; pp < S; ++pp) af[pp] = *reinterpret_cast<const v4i*>(st + pp * APL + aoff);
+        v4i bf[2][2];
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj) bf[0][jj] = *reinterpret_cast<const v4i*>(st + boff[jj]);
+#pragma unroll
+        for (int qb = 0; qb < S; ++qb) {
+          if (qb + 1 < S) {
+#pragma unroll
+            for (int jj = 0; jj < 2; ++jj)
+              bf[(qb + 1) & 1][jj] = *reinterpret_cast<const v4i*>(st + (qb + 1) * BPL + boff[jj]);
+          }
+          __builtin_amdgcn_sched_barrier(0);   // the next reads stay ahead of this qb's MFMAs
+#pragma unroll
+          for (int pa = 0; pa + qb < S; ++pa)
+#pragma unroll
+            for (int jj = 0; jj < 2; ++jj)
+              acc[jj][pa + qb] = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[pa], bf[qb & 1][jj], acc[jj][pa + qb], 0, 0, 0);
+        }
+      }
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) {
+        double s = 0.0;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          double v = (double)acc[jj][S - 1][r];
+#pragma unroll
+          for (int g = S - 2; g >= 0; --g) v = __builtin_fma(v, 0x1p-8, (double)acc[jj][g][r]);
+          v *= 0x1p-16 * srs[wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)];
+          s = __builtin_fma(v, v, s);
+        }
+        s += __shfl_xor(s, 32);
+        if (lane < 32) red[wm * WN + wn * 64 + jj * 32 + lane] = s;
+      }
+      __syncthreads();
+      if (t < WN) {
+        const int64_t col = col0 + t;
+        if (col < m) part[(int64_t)rt * ldk + col] = red[t] + red[WN + t];
+      }
+    }
+  }
+}
+
+static void launch8(const int8_t* A, const int8_t* B, int npad, int64_t ldk, int64_t m, int32_t* tk, const double* rs,
+                    double* part, int n_cu, hipStream_t st) {
+  const int32_t RT = npad / 64, CT = (int32_t)((m + WN - 1) / WN);
+  const int32_t P = (RT + 1) / 2;
+  const int64_t items = (int64_t)P * CT;
+  int32_t nb = 2 * (n_cu / 8) * 8;
+  if (items < nb) nb = (int32_t)(((items + 7) / 8) * 8);
+  const int32_t W = nb / 8, Sg = W / P > 1 ? W / P : 1;
+  CK(hipMemsetAsync(tk, 0, 8 * sizeof(int32_t), st));
+  hipLaunchKernelGGL(k_var8, dim3(nb), dim3(256), 0, st, A, B, npad, ldk, RT, CT, m, tk, rs, part, Sg);
+}
+
 struct Res {
   double ms;
   std::vector<double> colsum;
@@ -344,18 +482,16 @@ int main(int argc, char** argv) {
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
-  const char* names[] = {"v0 <32,4,2,2> (library)", "v2 <32,8,3,1>", "v6 <32,4,2,2> spread",
-                         "v7 <32,8,3,1> spread"};
-  const int NV = 4;
+  const char* names[] = {"v0 <32,4,2,2> (library)", "v2 <32,8,3,1>", "v8 scalar + bf double-buffer"};
+  const int NV = 3;
   auto run = [&](int v) {
     switch (v) {
       case 0: launch<32, 4, 2, 2, false>(A, B, npad, ldk, m, tk, rs, part, n_cu, st); break;
       case 1: launch<32, 8, 3, 1, false>(A, B, npad, ldk, m, tk, rs, part, n_cu, st); break;
-      case 2: launch<32, 4, 2, 2, false, true>(A, B, npad, ldk, m, tk, rs, part, n_cu, st); break;
-      case 3: launch<32, 8, 3, 1, false, true>(A, B, npad, ldk, m, tk, rs, part, n_cu, st); break;
+      case 2: launch8(A, B, npad, ldk, m, tk, rs, part, n_cu, st); break;
     }
   };
-  const int bm[] = {64, 128, 64, 128};
+  const int bm[] = {64, 128, 64};
   std::vector<double> ref;
   bool ok = true;
   for (int v = 0; v < NV; ++v) {   // correctness: column sums against v0

@@ -132,6 +132,7 @@ SIGNATURES = {
     "ut_gp_set_i8_tol": (C.c_int, [P, C.c_double]),
     "ut_gp_set_prune_pass": (C.c_int, [P, C.c_int32]),
     "ut_gp_i8_stats": (C.c_int, [P, C.POINTER(C.c_int64), C.POINTER(C.c_double)]),
+    "ut_gp_i8_bounds": (C.c_int, [P, P, P]),
     "ut_gp_fit_status": (C.c_int, [P, C.POINTER(I32)]),
     "ut_gp_join_fit": (C.c_int, [P]),
     "ut_gp_stats": (C.c_int, [P, C.POINTER(D), C.POINTER(D), C.POINTER(D)]),

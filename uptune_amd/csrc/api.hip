@@ -817,6 +817,18 @@ int ut_gp_set_i8_tol(ut_ctx* c, double tol) {
   return 0;
 }
 
+int ut_gp_i8_bounds(ut_ctx* c, double* E, double* Emu) {
+  if (!c) return UT_EINVAL;
+  double b[2] = {0.0, 0.0};
+  if (c->gp_fit_prec == 8 && c->gp_i8rs.p) {
+    UT_HIP(c, hipStreamSynchronize(c->fit_stream));
+    UT_HIP(c, hipMemcpy(b, c->gp_i8rs.p + 2 * (int64_t)c->gp_npad_fit, sizeof(b), hipMemcpyDeviceToHost));
+  }
+  if (E) *E = b[0];
+  if (Emu) *Emu = b[1];
+  return 0;
+}
+
 int ut_gp_i8_stats(ut_ctx* c, int64_t* recomputed, double* bound) {
   if (!c) return UT_EINVAL;
   if (recomputed) *recomputed = c->i8_recomputed;

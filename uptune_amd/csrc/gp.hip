@@ -852,11 +852,14 @@ __global__ void k_gp_finalize(int64_t m, int32_t RT1, int32_t RT2, const double*
   if (score_out) score_out[i] = sc;
 }
 
-// precision 8 (gp_i8.hip): mu from K*'s fp64 epilogue, |v|^2 from the int8
-// contraction's partials; a candidate is finished here only if the bound
+// precision 8 (gp_i8.hip): |v|^2 and the mean mu = v . beta (beta = L^-1 y)
+// from the int8 contraction's partials; a candidate is finished here only if
 //   | |v|^2 - s | <= E (2 sqrt(s) + E) + s (2n + 64) 2^-53     (s = the computed sum)
-// is at most tol * (sf2 - s): its variance is then within tol relative of the
-// exact one.  Every other candidate (near a training point sf2 - |v|^2 cancels;
+// is at most tol * (sf2 - s) -- its variance is then within tol relative of the
+// exact one -- and the mean's bound Emu = sum_r e_r |beta_r| (+ the fp64
+// rounding of the sums, (2n + 64) 2^-53 |mu| |beta|-weighted, below Emu's own
+// 2^-40 slack at these sizes) is at most tol * sigma: the mean within tol of
+// the posterior's own scale.  Every other candidate (near a training point sf2 - |v|^2 cancels;
 // or a failed fit) is appended to idx_out for the fp64 recompute (k_gp_fix_i8),
 // one atomic per wave; its outputs are written anyway and overwritten there.
 // Duplicates (dup[i], score -inf) are never flagged.
@@ -876,9 +879,9 @@ __global__ void k_gp_finalize_i8(int64_t m, int32_t RT1, int32_t RT2, const doub
     for (int32_t r = 0; r < RT2; ++r) vs += var_part[(int64_t)r * ldp + i];
     double var = sf2 - vs;
     var = var > 0.0 ? var : 0.0;
-    const double E = *Ebound;
+    const double E = Ebound[0], Emu = Ebound[1];
     const double bound = E * (2.0 * sqrt(vs) + E) + vs * (double)(2 * n + 64) * 0x1p-53;
-    flag = !(bound <= tol * var);   // (NaN: flagged)
+    flag = !(bound <= tol * var) || !(Emu <= tol * sqrt(var));   // (NaN: flagged)
     double sc = acq_score(kind, mu, var, stats[0], xi, kappa);
     if (*fit_flag != 0) {
       mu = var = sc = __builtin_nan("");
@@ -903,23 +906,24 @@ __global__ void k_gp_finalize_i8(int64_t m, int32_t RT1, int32_t RT2, const doub
   if (flag) idx_out[base + __builtin_popcountll(ball & ((1ull << lane) - 1ull))] = i;
 }
 
-// the flagged candidates' fp64 variance (recomputed K* columns through the fp64
-// contraction, RT partials each) -> var and score (mu stays K*'s)
-__global__ void k_gp_fix_i8(int64_t nf, const int64_t* __restrict__ idx, int32_t RT1, const double* __restrict__ mu_part,
-                            int64_t ldp, int32_t RT, const double* __restrict__ vpart, int64_t ldv, double sf2,
+// the flagged candidates' fp64 mean and variance (recomputed K* columns through
+// the fp64 contraction, RT partials each of v^2 and of v . beta) -> mu, var, score
+__global__ void k_gp_fix_i8(int64_t nf, const int64_t* __restrict__ idx, int32_t RT, const double* __restrict__ mpart,
+                            const double* __restrict__ vpart, int64_t ldv, double sf2,
                             const double* __restrict__ stats, int32_t kind, double xi, double kappa,
-                            const uint8_t* __restrict__ dup, double* __restrict__ var_out,
+                            const uint8_t* __restrict__ dup, double* __restrict__ mu_out, double* __restrict__ var_out,
                             double* __restrict__ score_out) {
   const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= nf) return;
   const int64_t i = idx[j];
   double mu = 0.0, vs = 0.0;
-  for (int32_t r = 0; r < RT1; ++r) mu += mu_part[(int64_t)r * ldp + i];
+  for (int32_t r = 0; r < RT; ++r) mu += mpart[(int64_t)r * ldv + j];
   for (int32_t r = 0; r < RT; ++r) vs += vpart[(int64_t)r * ldv + j];
   double var = sf2 - vs;
   var = var > 0.0 ? var : 0.0;
   double sc = acq_score(kind, mu, var, stats[0], xi, kappa);
   if (dup && dup[i]) sc = -1.0 / 0.0;
+  if (mu_out) mu_out[i] = mu;
   if (var_out) var_out[i] = var;
   if (score_out) score_out[i] = sc;
 }
@@ -1304,14 +1308,16 @@ int gp_score_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, const ut
   UT_CHECK(c, acq != nullptr, UT_EINVAL, "gp_score: acq is NULL");
   if (m <= 0) return 0;
   const int prec = c->gp_fit_prec;
-  const bool fp32 = prec != 64;  // fp32, h3 (f16x3) and i8 take the mean in K* and wait for the whole fit
+  const bool fp32 = prec != 64;  // fp32, h3 (f16x3) and i8: K* stores a reduced-precision K*
   const bool i8 = prec == 8;
-  // fp64: K* needs only the scaled training inputs (ev_fit_x) and the mean
-  // comes from the variance epilogue, mu = (L^-1 k*) . (L^-1 y), so K*
+  // the mean in K*'s fp64 epilogue (k* . alpha, before k* is rounded): fp32 and h3
+  const bool kmu = fp32 && !i8;
+  // fp64 and i8: K* needs only the scaled training inputs (ev_fit_x) and the
+  // mean comes from the variance epilogue, mu = (L^-1 k*) . (L^-1 y), so K*
   // overlaps the rest of an asynchronous fit and only the variance GEMM waits
-  // for L^-1.  fp32 keeps the mean in K*'s fp64 epilogue (k* . alpha, before
-  // k* is rounded to fp32) and waits for the whole fit.
-  if (c->fit_pending) UT_HIP(c, hipStreamWaitEvent(c->stream, fp32 ? c->ev_fit : c->ev_fit_x, 0));
+  // for L^-1 (i8: |mu - mu^| <= Emu, gp_i8.hip).  fp32 / h3 keep the mean in
+  // K*'s fp64 epilogue and wait for the whole fit.
+  if (c->fit_pending) UT_HIP(c, hipStreamWaitEvent(c->stream, kmu ? c->ev_fit : c->ev_fit_x, 0));
   mark(c, "fit_wait");   // (the wait is not K* time)
   const int32_t n = c->gp_n, d = c->gp_d;
   const int32_t npad = ((n + NPAD - 1) / NPAD) * NPAD;
@@ -1326,8 +1332,8 @@ int gp_score_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, const ut
   const int32_t RT = npad / NPAD;
   int rc;
   if ((rc = ensure(c, c->kst, (size_t)npad * ldk))) return rc;
-  if ((rc = ensure(c, c->mu_part, (size_t)RT * ldk))) return rc;
-  // (i8: the variance partials come per 64-row tile)
+  // (i8: the variance and mean partials come per 64-row tile)
+  if ((rc = ensure(c, c->mu_part, (size_t)(i8 ? 2 * RT : RT) * ldk))) return rc;
   if ((rc = ensure(c, c->var_part, (size_t)(i8 ? 2 * RT : RT) * ldk))) return rc;
   if ((rc = ensure(c, c->cnorm, (size_t)ldk))) return rc;
   if ((rc = ensure(c, c->ucand, (size_t)(dpad > 0 ? dpad : 1) * ldk))) return rc;
@@ -1342,18 +1348,19 @@ int gp_score_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, const ut
     mark(c, "cnorm");
   }
   if ((rc = launch_gemm_kstar(c, prec, cat ? c->gp_XsT_num.p : c->gp_XsT, npad, c->ucand.p, dpad, m, c->kst.p, ldk,
-                              fp32 ? c->mu_part.p : nullptr, -1, nullptr, nullptr,
+                              kmu ? c->mu_part.p : nullptr, -1, nullptr, nullptr,
                               cat ? kstar_cat(c, c->bcat.p) : KstarCat(), cat ? c->gp_xnorm_num.p : nullptr)))
     return rc;
   mark(c, "kstar");
-  if (c->fit_pending && !fp32) UT_HIP(c, hipStreamWaitEvent(c->stream, c->ev_fit, 0));
+  if (c->fit_pending && !kmu) UT_HIP(c, hipStreamWaitEvent(c->stream, c->ev_fit, 0));
   // the variance GEMM runs alone: the side stream's hash + dedup share the CUs
   // with K* only (C2: 27.95 -> 28.2 ms per round when they spilled into it, the
   // GEMM at 0.74 instead of 0.80 of peak; round 1)
   if (dup_ready) UT_HIP(c, hipStreamWaitEvent(c->stream, dup_ready, 0));
   mark(c, "");  // the wait for the fit is not variance time
   if (i8) {
-    if ((rc = launch_gemm_var_i8(c, npad, reinterpret_cast<const int8_t*>(c->kst.p), ldk, m, c->var_part.p)))
+    if ((rc = launch_gemm_var_i8(c, npad, reinterpret_cast<const int8_t*>(c->kst.p), ldk, m, c->var_part.p,
+                                 c->mu_part.p)))
       return rc;
   } else if ((rc = launch_gemm_var(c, prec, fp32 ? (const void*)c->gp_LinvT_f : (const void*)c->gp_LinvT, npad,
                                    c->kst.p, ldk, npad, m, c->var_part.p, fp32 ? nullptr : c->gp_beta,
@@ -1365,7 +1372,7 @@ int gp_score_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, const ut
   if (i8) {
     // the bound test, then the fp64 recompute of the candidates it did not clear
     UT_HIP(c, hipMemsetAsync(c->pr_count.p, 0, sizeof(int64_t), c->stream));
-    hipLaunchKernelGGL(k_gp_finalize_i8, dim3(grid1(m, 256)), dim3(256), 0, c->stream, m, RT, 2 * RT, c->mu_part.p,
+    hipLaunchKernelGGL(k_gp_finalize_i8, dim3(grid1(m, 256)), dim3(256), 0, c->stream, m, 2 * RT, 2 * RT, c->mu_part.p,
                        c->var_part.p, ldk, c->gp_sf2, c->gp_stats, c->gp_flag, acq->kind, acq->xi, acq->kappa, dup,
                        mu, var, score, c->gp_i8rs.p + 2 * npad, c->i8_tol, n, c->pr_idx.p,
                        reinterpret_cast<unsigned long long*>(c->pr_count.p));
@@ -1377,7 +1384,7 @@ int gp_score_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, const ut
     c->i8_recomputed = nf;
     if (nf * 2 > m) {
       // most candidates need fp64: the whole K* (fp64, over the planes) and the
-      // fp64 contraction; the mean partials stay K*'s
+      // fp64 contraction, with the mean from its epilogue
       c->i8_recomputed = -1;
       if ((rc = ensure(c, c->pr_mpart, (size_t)RT * ldk))) return rc;
       if ((rc = launch_gemm_kstar(c, 64, cat ? c->gp_XsT_num.p : c->gp_XsT, npad, c->ucand.p, dpad, m, c->kst.p, ldk,
@@ -1387,7 +1394,7 @@ int gp_score_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, const ut
       if ((rc = launch_gemm_var(c, 64, c->gp_LinvT, npad, c->kst.p, ldk, npad, m, c->var_part.p, c->gp_beta,
                                 c->pr_mpart.p)))
         return rc;
-      hipLaunchKernelGGL(k_gp_finalize, dim3(grid1(m, 256)), dim3(256), 0, c->stream, m, RT, RT, c->mu_part.p,
+      hipLaunchKernelGGL(k_gp_finalize, dim3(grid1(m, 256)), dim3(256), 0, c->stream, m, RT, RT, c->pr_mpart.p,
                          c->var_part.p, ldk, c->gp_sf2, c->gp_stats, c->gp_flag, acq->kind, acq->xi, acq->kappa, dup,
                          mu, var, score);
       UT_LAUNCH_CHECK(c);
@@ -1399,8 +1406,8 @@ int gp_score_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, const ut
                                 c->pr_mpart.p)))
         return rc;
       hipLaunchKernelGGL(k_gp_fix_i8, dim3(grid1(nf, 256)), dim3(256), 0, c->stream, nf, c->pr_idx.p, RT,
-                         c->mu_part.p, ldk, RT, c->pr_vpart.p, ldf, c->gp_sf2, c->gp_stats, acq->kind, acq->xi,
-                         acq->kappa, dup, var, score);
+                         c->pr_mpart.p, c->pr_vpart.p, ldf, c->gp_sf2, c->gp_stats, acq->kind, acq->xi, acq->kappa,
+                         dup, mu, var, score);
       UT_LAUNCH_CHECK(c);
     }
     mark(c, "recompute");

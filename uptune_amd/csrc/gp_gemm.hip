@@ -742,7 +742,7 @@ int launch_gemm_kstar(ut_ctx* c, int prec, const double* XsT, int32_t npad, cons
            "gemm_kstar: bad padding");
   UT_CHECK(c, !has_cat || (cat.acat && cat.bcat), UT_EINVAL, "gemm_kstar: categorical operands missing");
   UT_CHECK(c, prec == 64 || prec == 32 || prec == 16 || prec == 8, UT_EINVAL, "gemm_kstar: bad precision");
-  UT_CHECK(c, part != nullptr || prec == 64, UT_EINVAL,
+  UT_CHECK(c, part != nullptr || prec == 64 || prec == 8, UT_EINVAL,
            "gemm_kstar: fp32 / h3 mode takes the mean partial here");
   const int32_t RT = npad / K_BM;
   // row_tiles: only the first row_tiles tiles (the f32-contraction bound pass's fp64 bound rows)
@@ -777,8 +777,9 @@ int launch_gemm_kstar(ut_ctx* c, int prec, const double* XsT, int32_t npad, cons
   if (prec == 16)
     UT_KSTAR_BOTH(_Float16, true, (_Float16*)kst, part, ldexp(1.0, h3_kstar_exp(c->gp_sf2)), ldk * (int64_t)npad, RT,
                   nullptr);
-  else if (prec == 8)   // six digit planes of npad * ldk bytes (kst: [6][npad / 32][ldk][32])
-    UT_KSTAR_BOTH(int8_t, true, (int8_t*)kst, part, ldexp(1.0, -i8_kstar_exp(c->gp_sf2)), ldk * (int64_t)npad, RT,
+  else if (prec == 8)   // six digit planes of npad * ldk bytes (kst: [6][npad / 32][ldk][32]); the
+                        // mean comes from the int8 variance epilogue (part == nullptr: K* needs no alpha)
+    UT_KSTAR_BOTH(int8_t, false, (int8_t*)kst, part, ldexp(1.0, -i8_kstar_exp(c->gp_sf2)), ldk * (int64_t)npad, RT,
                   nullptr);
   else if (prec == 32)
     UT_KSTAR_BOTH(float, true, (float*)kst, part, 1.0, (int64_t)0, RT, nullptr);

@@ -96,31 +96,46 @@ __global__ __launch_bounds__(256) void k_split_i8(const double* __restrict__ Lin
   }
 }
 
-// E = sqrt(sum_r e2[r]) (one workgroup, fixed order), rounded up
-__global__ __launch_bounds__(256) void k_i8_errsum(const double* __restrict__ e2, int32_t npad, double* __restrict__ E) {
-  __shared__ double red[4];
+// E = sqrt(sum_r e2[r]) and Emu = sum_r e_r |beta_r| (beta = L^-1 y; one
+// workgroup, fixed order), both rounded up.  The mean comes from the variance
+// epilogue, mu^ = v^ . beta, so |mu - mu^| <= sum_r |v_r - v^_r| |beta_r| <= Emu.
+__global__ __launch_bounds__(256) void k_i8_errsum(const double* __restrict__ e2, const double* __restrict__ beta,
+                                                   int32_t npad, double* __restrict__ E) {
+  __shared__ double red[2][4];
   const int t = threadIdx.x;
-  double s = 0.0;
-  for (int32_t r = t; r < npad; r += 256) s += e2[r];
-  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
-  if ((t & 63) == 0) red[t >> 6] = s;
+  double s = 0.0, sm = 0.0;
+  for (int32_t r = t; r < npad; r += 256) {
+    s += e2[r];
+    sm = __builtin_fma(sqrt(e2[r]), fabs(beta[r]), sm);
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    s += __shfl_xor(s, o);
+    sm += __shfl_xor(sm, o);
+  }
+  if ((t & 63) == 0) {
+    red[0][t >> 6] = s;
+    red[1][t >> 6] = sm;
+  }
   __syncthreads();
-  if (t == 0) *E = sqrt((red[0] + red[1]) + (red[2] + red[3])) * (1.0 + 0x1p-40);
+  if (t == 0) {
+    E[0] = sqrt((red[0][0] + red[0][1]) + (red[0][2] + red[0][3])) * (1.0 + 0x1p-40);
+    E[1] = ((red[1][0] + red[1][1]) + (red[1][2] + red[1][3])) * (1.0 + 0x1p-40);
+  }
 }
 
 int alloc_split_i8(ut_ctx* c, int32_t npad) {
   int rc;
   if ((rc = ensure(c, c->gp_i8a, (size_t)I8_S * npad * npad))) return rc;
-  return ensure(c, c->gp_i8rs, (size_t)2 * npad + 1);   // [rs | e2 | E]
+  return ensure(c, c->gp_i8rs, (size_t)2 * npad + 2);   // [rs | e2 | E | Emu]
 }
 
 int launch_split_i8(ut_ctx* c, int32_t n, int32_t npad) {
-  UT_CHECK(c, c->gp_i8a.n >= (size_t)I8_S * npad * npad && c->gp_i8rs.n >= (size_t)2 * npad + 1, UT_EINVAL,
+  UT_CHECK(c, c->gp_i8a.n >= (size_t)I8_S * npad * npad && c->gp_i8rs.n >= (size_t)2 * npad + 2, UT_EINVAL,
            "split_i8: planes not allocated (alloc_split_i8)");
   double* rs = c->gp_i8rs.p;
   hipLaunchKernelGGL(k_split_i8, dim3(npad), dim3(256), 0, c->stream, c->gp_Linv, n, npad, c->gp_i8_eb,
                      c->gp_i8a.p, rs, rs + npad);
-  hipLaunchKernelGGL(k_i8_errsum, dim3(1), dim3(256), 0, c->stream, rs + npad, npad, rs + 2 * npad);
+  hipLaunchKernelGGL(k_i8_errsum, dim3(1), dim3(256), 0, c->stream, rs + npad, c->gp_beta, npad, rs + 2 * npad);
   UT_LAUNCH_CHECK(c);
   return 0;
 }
@@ -150,17 +165,19 @@ constexpr int I8_BPL = I8_WN * I8_BK;      // one B plane's piece of a stage (4 
 __global__ __launch_bounds__(256, 2) void k_gp_var_i8(const int8_t* __restrict__ Ad, const int8_t* __restrict__ Bd,
                                                       int32_t npad, int64_t ldk, int32_t RT, int32_t CT, int64_t m,
                                                       int32_t* __restrict__ ticket, const double* __restrict__ rs,
-                                                      double* __restrict__ part, int32_t Sg) {
+                                                      const double* __restrict__ beta, double* __restrict__ part,
+                                                      double* __restrict__ mpart, int32_t Sg) {
   constexpr int STAGE = I8_S * (I8_PL + I8_BPL);
   constexpr int NW = 6 * I8_S / 4;   // glds per wave per stage
-  __shared__ __attribute__((aligned(16))) int8_t lds[2 * STAGE + 2 * I8_WN * 8 + I8_BM * 8 + 16];
-  double* red = reinterpret_cast<double*>(lds + 2 * STAGE);   // [2][128]
-  double* srs = red + 2 * I8_WN;                               // row scales of the tile
-  int32_t& s_item = *reinterpret_cast<int32_t*>(srs + I8_BM);
+  __shared__ __attribute__((aligned(16))) int8_t lds[2 * STAGE + 4 * I8_WN * 8 + 2 * I8_BM * 8 + 16];
+  double* red = reinterpret_cast<double*>(lds + 2 * STAGE);   // [2][128] sums of v^2, [2][128] of v beta
+  double* srs = red + 4 * I8_WN;                               // row scales of the tile
+  double* sbt = srs + I8_BM;                                   // beta of the tile's rows
+  int32_t& s_item = *reinterpret_cast<int32_t*>(sbt + I8_BM);
   const int t = threadIdx.x, lane = t & 63;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
   const int wm = w >> 1, wn = w & 1;
-  const int32_t xcd = blockIdx.x & 7;
+  const int32_t xcd = __builtin_amdgcn_readfirstlane(blockIdx.x & 7);
   const int64_t aplane = (int64_t)npad * npad, bplane = (int64_t)npad * ldk;
 
   // stage kt of tile (row0, col0): A planes 2 KiB (2 pieces), B planes 4 KiB (4 pieces);
@@ -197,15 +214,15 @@ __global__ __launch_bounds__(256, 2) void k_gp_var_i8(const int8_t* __restrict__
   for (;;) {
     if (t == 0) s_item = atomicAdd(&ticket[xcd], 1);
     __syncthreads();
-    const int32_t j = s_item;
+    // (every item quantity scalar: the glds bases and loop bounds in SGPRs)
+    const int32_t j = __builtin_amdgcn_readfirstlane(s_item);
     const int32_t G = j / (P * Sg), q = j % (P * Sg), p = q % P;
     const int32_t ct = (G * Sg + q / P) * 8 + xcd;
     if (ct >= CT) break;   // uniform: the whole workgroup leaves
-    int32_t rts[2] = {RT - 1 - p, p};
-    const int nrt = rts[1] == rts[0] ? 1 : 2;
+    const int nrt = RT - 1 - p == p ? 1 : 2;
     for (int ri = 0; ri < nrt; ++ri) {
       if (ri > 0) __syncthreads();   // the previous tile's ring, red and srs are read
-      const int32_t rt = rts[ri];
+      const int32_t rt = __builtin_amdgcn_readfirstlane(ri == 0 ? RT - 1 - p : p);
       const int32_t row0 = rt * I8_BM;
       const int64_t col0 = (int64_t)ct * I8_WN;
       const int32_t nk = (row0 + I8_BM) / I8_BK;   // >= 2
@@ -218,8 +235,9 @@ __global__ __launch_bounds__(256, 2) void k_gp_var_i8(const int8_t* __restrict__
         for (int g = 0; g < I8_S; ++g)
 #pragma unroll
           for (int r = 0; r < 16; ++r) acc[jj][g][r] = 0;
-      if (w == 0 && lane < 32)   // 64 row scales: one 512-B glds, retired with stage 0
-        __builtin_amdgcn_global_load_lds(rs + row0 + lane * 2, (__attribute__((address_space(3))) void*)srs, 16, 0, 0);
+      if (w < 2 && lane < 32)   // 64 row scales / betas: one 512-B glds each, retired with stage 0
+        __builtin_amdgcn_global_load_lds((w == 0 ? rs : beta) + row0 + lane * 2,
+                                         (__attribute__((address_space(3))) void*)(w == 0 ? srs : sbt), 16, 0, 0);
       issue(row0, col0, ktof(0), lds);
       for (int32_t u = 0; u < nk; ++u) {
         i8_vm_wait<0>();                        // stage u landed (this wave's pieces)
@@ -245,32 +263,43 @@ __global__ __launch_bounds__(256, 2) void k_gp_var_i8(const int8_t* __restrict__
               acc[jj][pa + qb] = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[pa], bf[jj], acc[jj][pa + qb], 0, 0, 0);
         }
       }
-      // epilogue: v = 2^-16 (T_2 + 2^-8 (T_3 + ...)) * 2^(ea_row + eb), column sums of v^2
+      // epilogue: v = 2^-16 (T_2 + 2^-8 (T_3 + ...)) * 2^(ea_row + eb), column sums
+      // of v^2 and of v beta (the mean, mu = (L^-1 k*) . (L^-1 y))
       // (C/D map of the 32x32 MFMA: row (r & 3) + 8 (r >> 2) + 4 (lane >> 5), column lane & 31)
 #pragma unroll
       for (int jj = 0; jj < 2; ++jj) {
-        double s = 0.0;
+        double s = 0.0, sm = 0.0;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           double v = (double)acc[jj][I8_S - 1][r];
 #pragma unroll
           for (int g = I8_S - 2; g >= 0; --g) v = __builtin_fma(v, 0x1p-8, (double)acc[jj][g][r]);
-          v *= 0x1p-16 * srs[wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)];
+          const int rr = wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+          v *= 0x1p-16 * srs[rr];
           s = __builtin_fma(v, v, s);
+          sm = __builtin_fma(v, sbt[rr], sm);
         }
         s += __shfl_xor(s, 32);
-        if (lane < 32) red[wm * I8_WN + wn * 64 + jj * 32 + lane] = s;
+        sm += __shfl_xor(sm, 32);
+        if (lane < 32) {
+          red[wm * I8_WN + wn * 64 + jj * 32 + lane] = s;
+          red[2 * I8_WN + wm * I8_WN + wn * 64 + jj * 32 + lane] = sm;
+        }
       }
       __syncthreads();
       if (t < I8_WN) {
         const int64_t col = col0 + t;
-        if (col < m) part[(int64_t)rt * ldk + col] = red[t] + red[I8_WN + t];
+        if (col < m) {
+          part[(int64_t)rt * ldk + col] = red[t] + red[I8_WN + t];
+          mpart[(int64_t)rt * ldk + col] = red[2 * I8_WN + t] + red[3 * I8_WN + t];
+        }
       }
     }
   }
 }
 
-int launch_gemm_var_i8(ut_ctx* c, int32_t npad, const int8_t* kst8, int64_t ldk, int64_t m, double* part) {
+int launch_gemm_var_i8(ut_ctx* c, int32_t npad, const int8_t* kst8, int64_t ldk, int64_t m, double* part,
+                       double* mpart) {
   UT_CHECK(c, npad % 128 == 0 && npad <= I8_MAX_K && ldk % I8_WN == 0 && ldk >= m, UT_EINVAL,
            "gemm_var_i8: bad padding");
   UT_CHECK(c, c->gp_i8a.p && c->gp_i8rs.p, UT_EINVAL, "gemm_var_i8: the fit has no int8 planes");
@@ -282,7 +311,7 @@ int launch_gemm_var_i8(ut_ctx* c, int32_t npad, const int8_t* kst8, int64_t ldk,
   const int32_t W = nb / 8, Sg = W / P > 1 ? W / P : 1;
   UT_HIP(c, hipMemsetAsync(c->gp_ctr, 0, sizeof(int32_t) * 8, c->stream));
   hipLaunchKernelGGL(k_gp_var_i8, dim3(nb), dim3(256), 0, c->stream, c->gp_i8a.p, kst8, npad, ldk, RT, CT, m,
-                     c->gp_ctr, c->gp_i8rs.p, part, Sg);
+                     c->gp_ctr, c->gp_i8rs.p, c->gp_beta, part, mpart, Sg);
   UT_LAUNCH_CHECK(c);
   return 0;
 }

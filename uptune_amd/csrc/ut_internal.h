@@ -611,7 +611,9 @@ int alloc_split_i8(ut_ctx* c, int32_t npad);
 int launch_split_i8(ut_ctx* c, int32_t n, int32_t npad);
 // the variance contraction from K*'s digit planes (kst8, [6][npad/32][ldk][32]):
 // part [npad / 64][ldk] column partials of |v|^2
-int launch_gemm_var_i8(ut_ctx* c, int32_t npad, const int8_t* kst8, int64_t ldk, int64_t m, double* part);
+// part / mpart: per 64-row tile the column sums of v^2 and of v beta (the mean)
+int launch_gemm_var_i8(ut_ctx* c, int32_t npad, const int8_t* kst8, int64_t ldk, int64_t m, double* part,
+                       double* mpart);
 // L^-1 [row][k] (n x n, fp64) -> scaled fp16 hi/lo planes, blocked (h3 A operand, rows padded to 256);
 // the scale exponent is derived on the device from max|L^-1| (kept in gp_ctr[16..17])
 int launch_split_h3(ut_ctx* c, const double* Linv, int32_t n, _Float16* dst);

@@ -301,6 +301,13 @@ class BatchEngine:
         L.check(self.ctx, self.lib.ut_gp_i8_stats(self.ctx, C.byref(n), C.byref(e)), "ut_gp_i8_stats")
         return int(n.value), float(e.value)
 
+    def gp_i8_bounds(self) -> Tuple[float, float]:
+        """precision 8: the fit's bounds (E on the variance's |L^-1 k* - v^|,
+        Emu on the mean from the int8 variance epilogue); 0, 0 otherwise"""
+        e, em = C.c_double(), C.c_double()
+        L.check(self.ctx, self.lib.ut_gp_i8_bounds(self.ctx, C.byref(e), C.byref(em)), "ut_gp_i8_bounds")
+        return float(e.value), float(em.value)
+
     def gp_fit(self, X: np.ndarray, y: np.ndarray, lengthscale, sigma_f2: float = 1.0, sigma_n2: float = 1e-6,
                jitter: float = 0.0, wait: bool = True):
         """ut_gp_fit (wait=True) or ut_gp_fit_async (wait=False: the fit runs on the
