@@ -1025,6 +1025,33 @@ def test_score_round_de_pruned_equals_dense_round():
         np.testing.assert_array_equal(a[3].cpu().numpy(), b[3].cpu().numpy())
 
 
+@pytest.mark.parametrize("prec", [64, 8])
+def test_repeated_same_shape_categorical_fits(prec):
+    """a replayed fit graph once failed its PD check on the third
+    same-shape categorical fit of one engine.  The fit is launched kernel by
+    kernel now; three same-shape categorical fits with DIFFERENT data in one
+    engine (every signature the same, every buffer reused) must each give the
+    oracle's posterior -- no fit state survives from the previous fit."""
+    _require_gpu()
+    space = hpl_space()
+    e = engine(space, seed=5)
+    e.gp_set_precision(prec)
+    n, m = 512, 3000
+    cand = ode.population_init(space, m, seed=6)
+    for rep in range(3):
+        tr = ode.population_init(space, n, seed=100 + rep)
+        X = features(space, tr).T
+        y = np.sum((X - 0.3 - 0.1 * rep) ** 2, axis=1)
+        e.gp_fit(X, y, lengthscale=1.0, sigma_f2=1.0, sigma_n2=1e-6, jitter=1e-8)
+        assert e.gp_kstar_mode() == "categorical"
+        mu, var, score = [t.cpu().numpy() for t in e.gp_score_values(dev(cand), acq=e.acq("ei"))]
+        g = ogp.GP(X, y, lengthscale=1.0, sigma_f2=1.0, sigma_n2=1e-6, jitter=1e-8)
+        wmu, wvar = g.posterior(features(space, cand).T)
+        np.testing.assert_allclose(mu, wmu, rtol=RTOL, atol=ATOL)
+        np.testing.assert_allclose(var, wvar, rtol=RTOL, atol=ATOL)
+        np.testing.assert_allclose(score, ogp.acquisition(wmu, wvar, g.f_best), rtol=RTOL, atol=ATOL)
+
+
 @pytest.mark.parametrize("order", ["feat_first", "round_first"])
 def test_pruned_entry_points_share_one_categorical_fit(order):
     """the f32 bound pass caches an f32 copy of the training operand
