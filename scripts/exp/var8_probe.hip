@@ -47,7 +47,7 @@ __device__ __forceinline__ void vm_wait() {
   __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
 }
 
-template <int WR, int NW, int NST, int WPC, bool STATIC, bool SPREAD = false>
+template <int WR, int NW, int NST, int WPC, bool STATIC, bool SPREAD = false, int ORD = 0>
 __global__ __launch_bounds__(NW * 64, WPC) void k_var(const int8_t* __restrict__ Ad, const int8_t* __restrict__ Bd,
                                                       int32_t npad, int64_t ldk, int32_t RT, int32_t CT, int64_t m,
                                                       int32_t* __restrict__ ticket, const double* __restrict__ rs,
@@ -137,7 +137,10 @@ __global__ __launch_bounds__(NW * 64, WPC) void k_var(const int8_t* __restrict__
     const int32_t G = j / (P * Sg), q = j % (P * Sg), p = q % P;
     const int32_t ct = (G * Sg + q / P) * 8 + xcd;
     if (ct >= CT) break;
-    int32_t rts[2] = {RT - 1 - p, p};
+    // ORD 0: the long tile ascending, then the short one descending (the
+    // library); ORD 1: the short tile first, both ascending (a B stage's two
+    // reads at most 2p + 2 stages apart instead of up to 33)
+    int32_t rts[2] = {ORD == 1 ? p : RT - 1 - p, ORD == 1 ? RT - 1 - p : p};
     const int nrt = rts[1] == rts[0] ? 1 : 2;
     for (int ri = 0; ri < nrt; ++ri) {
       if (ri > 0) __syncthreads();
@@ -145,7 +148,7 @@ __global__ __launch_bounds__(NW * 64, WPC) void k_var(const int8_t* __restrict__
       const int32_t row0 = rt * BM;
       const int64_t col0 = (int64_t)ct * WN;
       const int32_t nk = (row0 + BM) / BK;
-      const bool rev = ri > 0;
+      const bool rev = ORD == 0 && ri > 0;
       auto ktof = [&](int32_t u) -> int32_t { return rev ? nk - 1 - u : u; };
       v16i acc[RB][2][S];
 #pragma unroll
@@ -425,7 +428,7 @@ struct Res {
   std::vector<double> colsum;
 };
 
-template <int WR, int NW, int NST, int WPC, bool STATIC, bool SPREAD = false>
+template <int WR, int NW, int NST, int WPC, bool STATIC, bool SPREAD = false, int ORD = 0>
 static void launch(const int8_t* A, const int8_t* B, int npad, int64_t ldk, int64_t m, int32_t* tk, const double* rs,
                    double* part, int n_cu, hipStream_t st) {
   constexpr int BM = (NW / 2) * WR;
@@ -436,7 +439,7 @@ static void launch(const int8_t* A, const int8_t* B, int npad, int64_t ldk, int6
   if (items < nb) nb = (int32_t)(((items + 7) / 8) * 8);
   const int32_t W = nb / 8, Sg = W / P > 1 ? W / P : 1;
   CK(hipMemsetAsync(tk, 0, 8 * sizeof(int32_t), st));
-  hipLaunchKernelGGL((k_var<WR, NW, NST, WPC, STATIC, SPREAD>), dim3(nb), dim3(NW * 64), 0, st, A, B, npad, ldk, RT, CT, m, tk, rs,
+  hipLaunchKernelGGL((k_var<WR, NW, NST, WPC, STATIC, SPREAD, ORD>), dim3(nb), dim3(NW * 64), 0, st, A, B, npad, ldk, RT, CT, m, tk, rs,
                      part, Sg);
 }
 
@@ -482,16 +485,18 @@ int main(int argc, char** argv) {
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
-  const char* names[] = {"v0 <32,4,2,2> (library)", "v2 <32,8,3,1>", "v8 scalar + bf double-buffer"};
-  const int NV = 3;
+  const char* names[] = {"v0 <32,4,2,2> (library order)", "v9 <32,4,2,2> short-first asc", "v2 <32,8,3,1>",
+                         "v10 <32,8,3,1> short-first asc"};
+  const int NV = 4;
   auto run = [&](int v) {
     switch (v) {
       case 0: launch<32, 4, 2, 2, false>(A, B, npad, ldk, m, tk, rs, part, n_cu, st); break;
-      case 1: launch<32, 8, 3, 1, false>(A, B, npad, ldk, m, tk, rs, part, n_cu, st); break;
-      case 2: launch8(A, B, npad, ldk, m, tk, rs, part, n_cu, st); break;
+      case 1: launch<32, 4, 2, 2, false, false, 1>(A, B, npad, ldk, m, tk, rs, part, n_cu, st); break;
+      case 2: launch<32, 8, 3, 1, false>(A, B, npad, ldk, m, tk, rs, part, n_cu, st); break;
+      case 3: launch<32, 8, 3, 1, false, false, 1>(A, B, npad, ldk, m, tk, rs, part, n_cu, st); break;
     }
   };
-  const int bm[] = {64, 128, 64};
+  const int bm[] = {64, 64, 128, 128};
   std::vector<double> ref;
   bool ok = true;
   for (int v = 0; v < NV; ++v) {   // correctness: column sums against v0
