@@ -39,13 +39,17 @@ def main():
     ap.add_argument("--batch", type=int, default=8)
     ap.add_argument("--population", type=int, default=4096)
     ap.add_argument("--backend", default="nccl")
-    ap.add_argument("--precision", type=int, default=64, choices=(64, 32, 16))
+    ap.add_argument("--precision", type=int, default=None, choices=(64, 32, 16, 8),
+                    help="the shared GP's contractions: 8 = the fp64 tier on the int8 MFMA (the default for dense "
+                         "rounds, as the bench's), 64 = the fp64 MFMA (the default with --prune, which needs it)")
     ap.add_argument("--prune", type=int, default=0, metavar="ROWS",
                     help="score technique rounds with the selection-exact EI-bound pruning (fp64)")
     ap.add_argument("--warmup-generations", type=int, default=3,
                     help="an untimed short run first (same process): library load, first launches of every "
                          "kernel, allocator growth -- the timed run is the steady-state loop")
     args = ap.parse_args()
+    if args.precision is None:
+        args.precision = 64 if args.prune else 8
 
     import torch
     import torch.distributed as dist
@@ -120,6 +124,7 @@ def main():
     n_train = len(drv.results_query())
     out = {"config": "C5 AUC bandit over GPU DE+PSO+GA+GGA, shared GP, Rosenbrock-64"
                      + (f", EI-bound pruned ({args.prune} rows)" if args.prune else ""), "n_gpus": world,
+           "precision": args.precision,
            "generations": drv.generation, "evaluations": len(drv.results) - args.n_init,
            "initial_design": args.n_init, "best": drv.best_result.time if drv.best_result else None,
            "wall_s": wall, "warmup_generations": args.warmup_generations, "technique_rounds": rounds, "rounds_per_s": sum(rounds.values()) / wall,
