@@ -165,3 +165,45 @@ def test_merge_topk_random_vs_python():
         gi, gs = merge_topk(torch.from_numpy(sc), torch.from_numpy(idx), torch.from_numpy(dg), k)
         assert gi.tolist() == want_i, trial
         assert gs.tolist() == want_s, trial
+
+
+def _enomem_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from uptune_amd import dist as D
+    out = {}
+    idx = torch.arange(4, dtype=torch.int64) + 10 * rank
+    sc = torch.tensor([4.0, 3.0, 2.0, 1.0], dtype=torch.float64) + rank
+    dig = (torch.arange(32, dtype=torch.int32) + 100 * rank).reshape(4, 8)
+    if rank == 1:
+        D._FAIL_NEXT_ALLOC = 1          # this rank's receive buffers fail once
+    try:
+        D.allgather_topk(idx, sc, dig, 4)
+        out["first"] = "no error"
+    except Exception as ex:
+        out["first"] = str(ex)
+    # the next exchange succeeds on both ranks (no rank was left in a collective)
+    mi, ms = D.allgather_topk(idx, sc, dig, 4)[:2]
+    out["second"] = mi.tolist()
+    dist.destroy_process_group()
+    q.put((rank, out))
+
+
+def test_allgather_allocation_failure_on_one_rank_returns_enomem_on_both():
+    """VERDICT r5 #7 on the gloo exchange: an allocation failure injected on
+    rank 1 makes BOTH ranks raise UT_ENOMEM (the agreement before the
+    all_gather), no rank hangs, and the next exchange works"""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_enomem_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(world))
+    for p in ps:
+        p.join(timeout=60)
+    assert "UT_ENOMEM" in res[1]["first"] and "no memory for the records" in res[1]["first"], res
+    assert "UT_ENOMEM" in res[0]["first"] and "another rank" in res[0]["first"], res
+    assert res[0]["second"] == res[1]["second"] == [10, 0, 11, 1], res   # (-score, index) order

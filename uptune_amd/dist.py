@@ -287,10 +287,31 @@ def _comm_device(group, device):
     return torch.device("cpu") if dist.get_backend(group) == "gloo" else device
 
 
+_FAIL_NEXT_ALLOC = 0   # tests: the next N receive allocations of _gather_gloo fail (as ut_debug_fail_alloc)
+
+
 def _gather_gloo(t: torch.Tensor, group, dim: int = 0) -> torch.Tensor:
+    """all_gather of t over gloo.  The receive buffers are allocated first and
+    the ranks agree on success (an all-reduce MIN) before the collective, as
+    ut_comm_allgather_topk does when its record buffers grow: a rank that could
+    not allocate makes every rank raise UT_ENOMEM instead of leaving its peers
+    inside all_gather (VERDICT r5 #7)."""
+    global _FAIL_NEXT_ALLOC
     world = dist.get_world_size(group)
     t = t.cpu().contiguous()
-    parts = [torch.empty_like(t) for _ in range(world)]
+    parts = None
+    try:
+        if _FAIL_NEXT_ALLOC > 0:
+            _FAIL_NEXT_ALLOC -= 1
+            raise MemoryError("injected allocation failure (dist._FAIL_NEXT_ALLOC)")
+        parts = [torch.empty_like(t) for _ in range(world)]
+    except (MemoryError, RuntimeError):
+        parts = None
+    ok = torch.tensor([0 if parts is None else 1], dtype=torch.int32)
+    dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=group)
+    if not int(ok.item()):
+        raise L.UthotError("allgather_topk failed: UT_ENOMEM: " + ("no memory for the records" if parts is None
+                                                                  else "another rank could not allocate the records"))
     dist.all_gather(parts, t, group=group)
     return torch.cat(parts, dim=dim)
 
