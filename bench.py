@@ -589,7 +589,7 @@ def main():
         # library's streams during the rounds, read once here)
         st_ms = {}
         for st in ("propose", "hash", "dedup", "encode", "prep", "fit_wait", "kstar", "bound", "prune", "var",
-                   "finalize", "recompute", "topk"):
+                   "finalize", "recompute", "topk", "outputs", "between"):
             try:
                 st_ms[st] = eng.stage_time(st)
             except Exception:

@@ -75,7 +75,25 @@ static int timing_collect(ut_ctx* c, bool keep) {
   UT_HIP(c, ut::sync_all(c));
   for (size_t i = 0; keep && i < T.marks.size(); ++i) {
     const auto& m = T.marks[i];
-    if (m.name.empty()) continue;
+    if (m.name.empty()) {
+      // a round's first mark: the time since the previous round's last mark on
+      // its stream is "between" (the device idle or finishing unmarked work
+      // while the host is between the two rounds)
+      if (i == 0 || T.marks[i - 1].round == m.round) continue;
+      for (size_t j = i; j-- > 0;) {
+        if (T.marks[j].round != m.round - 1) break;
+        if (T.marks[j].stream != m.stream) continue;
+        float ms = 0.f;
+        hipEventElapsedTime(&ms, T.marks[j].ev, m.ev);
+        auto it = T.totals.begin();
+        while (it != T.totals.end() && it->first != "between") ++it;
+        if (it == T.totals.end()) T.totals.push_back({"between", {0.0, 0}}), it = T.totals.end() - 1;
+        it->second.first += ms;
+        it->second.second += 1;
+        break;
+      }
+      continue;
+    }
     for (size_t j = i; j-- > 0;) {  // the previous mark of the same round on the same stream
       if (T.marks[j].round != m.round) break;
       if (T.marks[j].stream != m.stream) continue;
@@ -251,6 +269,7 @@ int ut_ctx_create(int device, uint64_t seed, ut_ctx** out) {
   if (const char* e = getenv("UT_DE_AOS")) c->de_aos = atoi(e) != 0;
   if (const char* e = getenv("UT_HASH_WG_PER_CU")) c->hash_wg_per_cu = atoi(e);
   if (const char* e = getenv("UT_CAT_KSTAR")) c->cat_enable = atoi(e) != 0;
+  if (const char* e = getenv("UT_FIT_DEFER")) c->fit_defer = atoi(e) != 0;
   *out = c;
   return 0;
 }
@@ -301,12 +320,14 @@ const char* ut_last_error(ut_ctx* c) { return c ? c->err.c_str() : "null context
 
 int ut_set_stream(ut_ctx* c, void* s) {
   if (!c) return UT_EINVAL;
+  if (int rc = gp_fit_flush(c)) return rc;   // (ordered on the stream it was staged against)
   c->stream = (hipStream_t)s;  // NULL = the device's default (null) stream
   return 0;
 }
 
 int ut_sync(ut_ctx* c) {
   if (!c) return UT_EINVAL;
+  if (int rc = gp_fit_flush(c)) return rc;
   UT_HIP(c, ut::sync_all(c));
   return 0;
 }
@@ -315,6 +336,7 @@ int ut_space_define(ut_ctx* c, int32_t P, const ut_param_desc* params, int32_t p
   if (!c) return UT_EINVAL;
   UT_CHECK(c, P >= 1 && params, UT_EINVAL, "space: need at least one parameter");
   UT_HIP(c, hipSetDevice(c->device));
+  if (int rc = gp_fit_flush(c)) return rc;   // a staged fit reads the space's categorical layout
   UT_HIP(c, ut::sync_all(c));
   free_space(c->space);
   c->has_space = false;
@@ -629,7 +651,10 @@ int ut_propose_de(ut_ctx* c, const ut_de_params* p, uint32_t round_, int64_t can
   if (rc) return rc;
   UT_CHECK(c, (out_values || m == 0) && ld >= m, UT_EINVAL, "propose_de: bad arguments");
   if (m == 0) return 0;
-  return launch_de(c, p, round_, cand_base, m, out_values, ld);
+  // a staged fit is issued after the proposal (as in score_round_de_impl)
+  if ((rc = gp_fit_prefit(c))) return rc;
+  if ((rc = launch_de(c, p, round_, cand_base, m, out_values, ld))) return rc;
+  return gp_fit_flush(c);
 }
 
 int ut_encode_features(ut_ctx* c, const double* values, int64_t ld, int64_t m, double* feat, int64_t ldf) {
@@ -739,6 +764,7 @@ int ut_gp_fit_async(ut_ctx* c, const double* X, const double* y, int32_t n, int3
 
 int ut_gp_join_fit(ut_ctx* c) {
   if (!c) return UT_EINVAL;
+  if (int rc = gp_fit_flush(c)) return rc;
   if (c->fit_pending) UT_HIP(c, hipStreamWaitEvent(c->stream, c->ev_fit, 0));
   return 0;
 }
@@ -799,6 +825,7 @@ int ut_gp_set_precision(ut_ctx* c, int32_t bits) {
   if (!c) return UT_EINVAL;
   UT_CHECK(c, bits == 64 || bits == 32 || bits == 16 || bits == 8, UT_EINVAL,
            "gp precision must be 64, 32, 16 (f16x3) or 8 (int8 slices, fp64 tier)");
+  if (int rc = gp_fit_flush(c)) return rc;   // a staged fit was sized for the precision it was staged at
   c->gp_prec = bits;
   return 0;
 }
@@ -819,6 +846,7 @@ int ut_gp_set_i8_tol(ut_ctx* c, double tol) {
 
 int ut_gp_i8_bounds(ut_ctx* c, double* E, double* Emu) {
   if (!c) return UT_EINVAL;
+  if (int rc = gp_fit_flush(c)) return rc;
   double b[2] = {0.0, 0.0};
   if (c->gp_fit_prec == 8 && c->gp_i8rs.p) {
     UT_HIP(c, hipStreamSynchronize(c->fit_stream));
@@ -831,6 +859,7 @@ int ut_gp_i8_bounds(ut_ctx* c, double* E, double* Emu) {
 
 int ut_gp_i8_stats(ut_ctx* c, int64_t* recomputed, double* bound) {
   if (!c) return UT_EINVAL;
+  if (int rc = gp_fit_flush(c)) return rc;
   if (recomputed) *recomputed = c->i8_recomputed;
   if (bound) {
     *bound = 0.0;
@@ -921,7 +950,11 @@ static int score_round_de_impl(ut_ctx* c, const ut_de_params* de, const ut_acq* 
   timing_begin(c);
   // the proposal also writes the DE-diff mask / pairs the hash reuses
   if ((rc = check_de_params(c, de, m, cand_base))) return rc;
+  // a staged fit (ut_gp_fit_async) keeps its place before the proposal but is
+  // issued after it: the proposal runs while the host issues the fit
+  if ((rc = gp_fit_prefit(c))) return rc;
   if ((rc = launch_de(c, de, round_, cand_base, m, c->r_values.p, ld, true))) return rc;
+  if ((rc = gp_fit_flush(c))) return rc;
   mark(c, "propose");
   // fork: hash_config + dedup on the side stream, beside encode + GP scoring.
   // Dense fp64 rounds (the only ones whose K* does not wait for the whole
@@ -969,6 +1002,7 @@ static int score_round_de_impl(ut_ctx* c, const ut_de_params* de, const ut_acq* 
     mark(c, "topk");
   }
   if ((rc = round_outputs(c, out, ld, cand_base, k))) return rc;
+  mark(c, "outputs");
   return timing_end(c);
 }
 
@@ -1028,7 +1062,9 @@ int ut_score_round_ga(ut_ctx* c, const ut_ga_params* ga, const double* parent1, 
   c->r_m = m;
   c->r_feat_valid = false;
   timing_begin(c);
+  if ((rc = gp_fit_prefit(c))) return rc;   // (as score_round_de_impl)
   if ((rc = launch_ga(c, ga, parent1, parent2, round_, cand_base, m, c->r_values.p, ld, c->r_inval.p))) return rc;
+  if ((rc = gp_fit_flush(c))) return rc;
   mark(c, "propose");
   // fork right after the proposal: forked after K* instead (beside the int8
   // variance GEMM) the hash ran 106 ms where it runs 79 beside encode + K*, C4
@@ -1054,6 +1090,7 @@ int ut_score_round_ga(ut_ctx* c, const ut_ga_params* ga, const double* parent1, 
   if ((rc = topk_impl(c, c->r_score.p, c->r_dup.p, m, cand_base, k, c->r_topk_idx.p, c->r_topk_score.p))) return rc;
   mark(c, "topk");
   if ((rc = round_outputs(c, out, ld, cand_base, k))) return rc;
+  mark(c, "outputs");
   return timing_end(c);
 }
 

@@ -1126,17 +1126,22 @@ static int fit_device(ut_ctx* c, int part, int32_t n, int32_t n0, int32_t d, int
   return 0;
 }
 
-// Enqueue a fit on the fit stream, ordered after everything already enqueued
-// on the caller's stream (earlier rounds read the GP state being replaced).
-// Scoring waits on ev_fit; failure (not positive definite) is reported by
-// gp_wait_fit and, on the device, by NaN scores from k_gp_finalize.
+// Stage a fit (X, y, 1/ell in pinned memory, every buffer allocated, the
+// append / categorical decisions taken) whose device work gp_fit_flush
+// enqueues on the fit stream, ordered after everything already enqueued on the
+// caller's stream (earlier rounds read the GP state being replaced).  Scoring
+// waits on ev_fit; failure (not positive definite) is reported by gp_wait_fit
+// and, on the device, by NaN scores from k_gp_finalize.
 int gp_fit_enqueue(ut_ctx* c, const double* X, const double* y, int32_t n, int32_t d, const ut_gp_hyper* h) {
   UT_CHECK(c, n >= 1 && d >= 1 && X && y && h && h->lengthscale_host, UT_EINVAL, "gp_fit: bad arguments");
   const int32_t npad = ((n + NPAD - 1) / NPAD) * NPAD;
   UT_CHECK(c, c->gp_prec != 8 || npad <= I8_MAX_K, UT_EINVAL,
            "gp_fit: precision 8 takes at most 16384 training points (exact int32 digit sums)");
-  // the previous fit's copies out of the pinned staging (and its factor) are
-  // complete once ev_fit is
+  // a fit staged and never used is enqueued first (its staging is about to be
+  // reused; an append compares against it), then the previous fit's copies out
+  // of the pinned staging (and its factor) are complete once ev_fit is
+  int rc = gp_fit_flush(c);
+  if (rc) return rc;
   if (c->fit_pending) UT_HIP(c, hipEventSynchronize(c->ev_fit));
   // Incremental fit: new rows appended to the previous fit's training set
   // (its rows a bitwise prefix of X, same hyperparameters, same padded size,
@@ -1159,8 +1164,7 @@ int gp_fit_enqueue(ut_ctx* c, const double* X, const double* y, int32_t n, int32
       app = *c->flag_host == 0;
     }
   }
-  int rc = gp_alloc(c, npad, d);
-  if (rc) return rc;
+  if ((rc = gp_alloc(c, npad, d))) return rc;
   c->pr_f2_valid = false;   // |L^-1|_F^2 (pruned scoring) belongs to the previous factor
   c->pr_ab_valid = false;
   c->pr_xf_valid = false;
@@ -1232,19 +1236,50 @@ int gp_fit_enqueue(ut_ctx* c, const double* X, const double* y, int32_t n, int32
     if ((rc = alloc_split_i8(c, npad))) return rc;
     c->gp_i8_eb = i8_kstar_exp(h->sigma_f2);
   }
-  UT_HIP(c, hipEventRecord(c->ev_prefit, c->stream));
-  UT_HIP(c, hipStreamWaitEvent(c->fit_stream, c->ev_prefit, 0));
-  StreamScope on_fit(c, c->fit_stream);
   c->gp_n = n;
   c->gp_sf2 = h->sigma_f2;
-  if ((rc = fit_device(c, 0, n, n0, d, npad, dpn, app, xr0, diag, h->sigma_f2))) return rc;
-  UT_HIP(c, hipEventRecord(c->ev_fit_x, c->stream));   // the scaled inputs: fp64 K* may start
-  if ((rc = fit_device(c, 1, n, n0, d, npad, dpn, app, xr0, diag, h->sigma_f2))) return rc;
   c->gp_fit_prec = c->gp_prec;
   c->gp_npad_fit = npad;
   c->gp_diag_fit = diag;
   c->gp_fit_kind = app ? 1 : 0;
-  UT_HIP(c, hipEventRecord(c->ev_fit, c->stream));
+  c->gp_ready = true;
+  ut_ctx::FitJob& j = c->fit_job;
+  j.n = n, j.n0 = n0, j.d = d, j.npad = npad, j.dpn = dpn, j.xr0 = xr0;
+  j.app = app, j.diag = diag, j.sf2 = h->sigma_f2;
+  j.on = true;
+  c->fit_prefit_set = false;
+  return c->fit_defer ? 0 : gp_fit_flush(c);
+}
+
+// The staged fit's place on the caller's stream: recorded before a proposal
+// is enqueued, so the fit flushed after it still runs beside it.
+int gp_fit_prefit(ut_ctx* c) {
+  if (!c->fit_job.on || c->fit_prefit_set) return 0;
+  UT_HIP(c, hipEventRecord(c->ev_prefit, c->stream));
+  c->fit_prefit_set = true;
+  return 0;
+}
+
+// Enqueue the staged fit's device work on the fit stream, ordered after what
+// the caller's stream held at gp_fit_prefit (or now).  Scoring waits on
+// ev_fit_x (scaled inputs) / ev_fit (the factor).
+int gp_fit_flush(ut_ctx* c) {
+  if (!c->fit_job.on) return 0;
+  const ut_ctx::FitJob j = c->fit_job;
+  c->fit_job.on = false;
+  // (a launch that fails below leaves no usable factor)
+  c->gp_ready = false;
+  if (!c->fit_prefit_set) UT_HIP(c, hipEventRecord(c->ev_prefit, c->stream));
+  c->fit_prefit_set = false;
+  UT_HIP(c, hipStreamWaitEvent(c->fit_stream, c->ev_prefit, 0));
+  int rc;
+  {
+    StreamScope on_fit(c, c->fit_stream);
+    if ((rc = fit_device(c, 0, j.n, j.n0, j.d, j.npad, j.dpn, j.app, j.xr0, j.diag, j.sf2))) return rc;
+    UT_HIP(c, hipEventRecord(c->ev_fit_x, c->stream));   // the scaled inputs: fp64 K* may start
+    if ((rc = fit_device(c, 1, j.n, j.n0, j.d, j.npad, j.dpn, j.app, j.xr0, j.diag, j.sf2))) return rc;
+    UT_HIP(c, hipEventRecord(c->ev_fit, c->stream));
+  }
   c->fit_pending = true;
   c->gp_ready = true;
   return 0;
@@ -1252,6 +1287,8 @@ int gp_fit_enqueue(ut_ctx* c, const double* X, const double* y, int32_t n, int32
 
 // Wait for the enqueued fit and check it (positive definite).
 int gp_wait_fit(ut_ctx* c) {
+  int rc;
+  if ((rc = gp_fit_flush(c))) return rc;
   if (!c->fit_pending) return 0;
   // the flag is read on the fit stream itself, after the fit (a pinned
   // asynchronous copy and that stream's sync: ~10 us once the fit is done,
@@ -1270,10 +1307,11 @@ int gp_wait_fit(ut_ctx* c) {
 int gp_encode_scaled(ut_ctx* c, const double* values, int64_t ld, int64_t m) {
   UT_CHECK(c, c->gp_ready, UT_EINVAL, "gp_score: call ut_gp_fit first");
   if (m <= 0) return 0;
+  int rc;
+  if ((rc = gp_fit_flush(c))) return rc;
   // 1/ell comes with the fit's scaled training inputs
   if (c->fit_pending) UT_HIP(c, hipStreamWaitEvent(c->stream, c->ev_fit_x, 0));
   const int64_t ldk = ((m + VAR_BN - 1) / VAR_BN) * VAR_BN;   // as gp_score_impl
-  int rc;
   if ((rc = ensure(c, c->cnorm, (size_t)ldk))) return rc;
   if (c->cat_on) {   // numeric U', norms and the one-hot codes (categorical K*)
     const int32_t dpn = cat_dpad(c);
@@ -1307,6 +1345,7 @@ int gp_score_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, const ut
   UT_CHECK(c, c->gp_ready, UT_EINVAL, "gp_score: call ut_gp_fit first");
   UT_CHECK(c, acq != nullptr, UT_EINVAL, "gp_score: acq is NULL");
   if (m <= 0) return 0;
+  if (int rc0 = gp_fit_flush(c)) return rc0;
   const int prec = c->gp_fit_prec;
   const bool fp32 = prec != 64;  // fp32, h3 (f16x3) and i8: K* stores a reduced-precision K*
   const bool i8 = prec == 8;
@@ -1353,10 +1392,14 @@ int gp_score_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, const ut
     return rc;
   mark(c, "kstar");
   if (c->fit_pending && !kmu) UT_HIP(c, hipStreamWaitEvent(c->stream, c->ev_fit, 0));
-  // the variance GEMM runs alone: the side stream's hash + dedup share the CUs
-  // with K* only (C2: 27.95 -> 28.2 ms per round when they spilled into it, the
-  // GEMM at 0.74 instead of 0.80 of peak; round 1)
-  if (dup_ready) UT_HIP(c, hipStreamWaitEvent(c->stream, dup_ready, 0));
+  // fp64 / fp32 / h3: the variance GEMM runs alone, the side stream's hash +
+  // dedup share the CUs with K* only (C2: 27.95 -> 28.2 ms per round when they
+  // spilled into it, the GEMM at 0.74 instead of 0.80 of peak; round 1).  i8:
+  // it starts when K* ends and the hash's tail runs beside it (only the
+  // finalize needs the dup mask): C2 16.60 -> 16.40 ms at ell 0.2, 19.62 ->
+  // 19.36 at ell 2, C3 / C4 unchanged (their hash ends before K*;
+  // scripts/ab/r06_varjoin*.sh, r06_sched.sh)
+  if (dup_ready && !i8) UT_HIP(c, hipStreamWaitEvent(c->stream, dup_ready, 0));
   mark(c, "");  // the wait for the fit is not variance time
   if (i8) {
     if ((rc = launch_gemm_var_i8(c, npad, reinterpret_cast<const int8_t*>(c->kst.p), ldk, m, c->var_part.p,
@@ -1736,6 +1779,7 @@ int gp_topk_pruned_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, co
   UT_CHECK(c, acq->kind == UT_ACQ_EI || (acq->kind == UT_ACQ_UCB && acq->kappa >= 0.0), UT_EINVAL,
            "gp_topk_pruned: the score must increase with sigma (EI, or UCB with kappa >= 0)");
   UT_CHECK(c, k >= 1 && k <= 1024, UT_EINVAL, "gp_topk_pruned: k must be in [1, 1024]");
+  if (int rc0 = gp_fit_flush(c)) return rc0;
   // the candidates' K* operands need only the fit's scaled inputs (1/ell):
   // they are prepared while the factorisation still runs, and K* then waits
   // for the whole fit (C3 pruned: the 2.8-ms categorical prep came off the

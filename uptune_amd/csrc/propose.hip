@@ -1032,7 +1032,11 @@ extern "C" int ut_propose_pso(ut_ctx* c, const ut_pso_params* a, const double* g
            "propose_pso: bad arguments");
   UT_CHECK(c, a->crossover >= UT_X_NONE && a->crossover <= UT_X_PMX, UT_EINVAL, "propose_pso: bad crossover");
   if (m == 0) return 0;
-  return ut::launch_pso(c, a, gbest, round_, cand_base, m, out_values, out_vel, ld);
+  // a staged fit is issued after the proposal (api.hip score_round_de_impl)
+  int rc;
+  if ((rc = ut::gp_fit_prefit(c))) return rc;
+  if ((rc = ut::launch_pso(c, a, gbest, round_, cand_base, m, out_values, out_vel, ld))) return rc;
+  return ut::gp_fit_flush(c);
 }
 
 extern "C" int ut_pso_commit(ut_ctx* c, const double* values, const double* vel, int64_t ld, int64_t cand_base,
@@ -1073,5 +1077,8 @@ extern "C" int ut_propose_ga(ut_ctx* c, const ut_ga_params* a, const double* par
   UT_CHECK(c, a->op >= 0 && a->op < 256, UT_EINVAL, "propose_ga: op must fit 8 bits");
   UT_CHECK(c, a->crossover >= UT_X_NONE && a->crossover <= UT_X_PMX, UT_EINVAL, "propose_ga: bad crossover");
   if (m == 0) return 0;
-  return ut::launch_ga(c, a, parent1, parent2, round_, cand_base, m, out_values, ld, out_invalid);
+  int rc;
+  if ((rc = ut::gp_fit_prefit(c))) return rc;
+  if ((rc = ut::launch_ga(c, a, parent1, parent2, round_, cand_base, m, out_values, ld, out_invalid))) return rc;
+  return ut::gp_fit_flush(c);
 }

@@ -143,6 +143,19 @@ struct ut_ctx {
   int32_t var_split = 1;
   double* fit_host = nullptr;        // pinned staging of X, y, 1/ell for the asynchronous fit
   size_t fit_host_n = 0;
+  // a staged fit whose device work is not enqueued yet: gp_fit_enqueue stages
+  // X, y and the host-side decisions, gp_fit_flush issues the launches.  A
+  // proposal (and so every scoring round) is enqueued before the staged fit,
+  // so the caller's stream is not idle while the host issues the fit's ~50
+  // launches; anything that reads GP state flushes first.
+  struct FitJob {
+    bool on = false;
+    int32_t n = 0, n0 = 0, d = 0, npad = 0, dpn = 0, xr0 = 0;
+    bool app = false;
+    double diag = 0.0, sf2 = 1.0;
+  } fit_job;
+  bool fit_prefit_set = false;   // ev_prefit already recorded for fit_job (gp_fit_prefit)
+  int32_t fit_defer = 1;         // UT_FIT_DEFER=0: gp_fit_enqueue issues the launches itself
   std::string err;
   ut::Space space;
   bool has_space = false;
@@ -439,6 +452,8 @@ int ensure(ut_ctx* c, DevBuf<T>& b, size_t n) {
 void mark(ut_ctx* c, const char* name);
 int gp_fit_enqueue(ut_ctx* c, const double* X, const double* y, int32_t n, int32_t d, const ut_gp_hyper* h);
 int gp_wait_fit(ut_ctx* c);
+int gp_fit_flush(ut_ctx* c);
+int gp_fit_prefit(ut_ctx* c);
 
 // kernel launchers implemented in the .hip translation units
 int launch_population_init(ut_ctx* c, uint32_t round_);
