@@ -248,9 +248,12 @@ int ut_gp_fit(ut_ctx* ctx, const double* X_host, const double* y_host, int32_t n
 /* The same fit, enqueued on the context's internal fit stream without a host
  * wait: it runs beside whatever is enqueued next (e.g. the proposal and hash
  * stages of the next round), and every later scoring call waits for it on the
- * device.  X_host / y_host may be reused on return.  A failed fit (not
- * positive definite) is reported by ut_gp_stats / ut_gp_fit, and makes every
- * score NaN (nothing is selected). */
+ * device.  X_host / y_host may be reused on return (they are staged in
+ * pinned memory); the fit's launches are issued by the next call that needs
+ * them -- after the proposal of ut_score_round_* / ut_propose_* (ordered
+ * before it on the device), or on entry to any call that reads GP state.
+ * A failed fit (not positive definite) is reported by ut_gp_stats /
+ * ut_gp_fit_status, and makes every score NaN (nothing is selected). */
 int ut_gp_fit_async(ut_ctx* ctx, const double* X_host, const double* y_host, int32_t n, int32_t d,
                     const ut_gp_hyper* hyper);
 /* Incremental fits (default on; UT_FIT_APPEND=0 or enable=0 turns them off):
