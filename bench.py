@@ -187,8 +187,11 @@ def kernel_table(m, n, d, outer_blocks, prec=64, suffix=""):
     (SURVEY.md §8(d)):
       k_de: 40 d B per candidate (target, 3 donors, trial); k_hash (outer):
       outer_blocks compressions per candidate; K*: 2 n dpad flops; encode: 16 F B.
-    prec 8: K* is k_gp_kstar<int8_t> (the mean k* . alpha and six digit planes
-    in its epilogue; record key kstar8).  suffix "_l2": the ell = 2 records."""
+    prec 8: K* is k_gp_kstar_q (gp_kq.hip: the distance contraction on the int8
+    MFMA, 21 digit products per multiply-add, the exp and six digit planes in its
+    epilogue; record key kstar8; its peak = int8 peak / 21, as the variance's;
+    UT_KSTAR_Q=0: k_gp_kstar<int8_t> on the fp64 MFMA).  suffix "_l2": the ell =
+    2 records."""
     out = {}
     try:
         with open(os.path.join(ROOT, "profiles", "pmc_summary.json")) as f:
@@ -221,16 +224,18 @@ def kernel_table(m, n, d, outer_blocks, prec=64, suffix=""):
                     "frac": alg_bytes / t / 1e9 / PEAK_HBM_GBS, "algorithmic_bytes": alg_bytes,
                     "traffic_bytes": traffic, "traffic_GBps": (traffic / t / 1e9) if traffic else None}
 
-    def mfma(key, flops):
+    def mfma(key, flops, peak=PEAK_FP64_TFLOPS):
         t, traffic = rec(key)
         if t <= 0:
             return
         out[key] = {"bound": "mfma", "ms": t * 1e3, "achieved_TFps": flops / t / 1e12,
-                    "frac": flops / t / 1e12 / PEAK_FP64_TFLOPS, "flops": flops, "traffic_bytes": traffic}
+                    "frac": flops / t / 1e12 / peak, "peak_TFps": peak, "flops": flops, "traffic_bytes": traffic}
 
     hbm("propose", 40.0 * d * m)
     hbm("encode", 16.0 * d * m)
-    mfma("kstar8" if prec == 8 else "kstar", 2.0 * n * (d + (-d) % 16) * m)   # the variance GEMM is `roofline`
+    kq = prec == 8 and os.environ.get("UT_KSTAR_Q", "1") != "0"
+    mfma("kstar8" if prec == 8 else "kstar", 2.0 * n * (d + (-d) % 16) * m,   # the variance GEMM is `roofline`
+         PEAK_I8_TOPS / I8_PRODUCTS if kq else PEAK_FP64_TFLOPS)
     t, traffic = rec("hash")
     if t > 0:
         c = float(outer_blocks) * m
@@ -589,7 +594,7 @@ def main():
         # library's streams during the rounds, read once here)
         st_ms = {}
         for st in ("propose", "hash", "dedup", "encode", "prep", "fit_wait", "kstar", "bound", "prune", "var",
-                   "finalize", "recompute", "topk", "outputs", "between"):
+                   "var_wait", "finalize", "recompute", "topk", "outputs", "between"):
             try:
                 st_ms[st] = eng.stage_time(st)
             except Exception:

@@ -18,7 +18,8 @@ import sys
 from collections import defaultdict
 
 KERNELS = {"var": ("void ut::k_gp_var_pp<false>(", "ut::k_gp_var_pp(", "void ut::k_gp_var<double>"),
-           "var8": ("ut::k_gp_var_i8(",), "kstar8": ("void ut::k_gp_kstar<signed char, false, false>", "void ut::k_gp_kstar<signed char, true, false>"),
+           "var8": ("ut::k_gp_var_i8(",), "kstar8": ("void ut::k_gp_kstar_q<signed char, false", "void ut::k_gp_kstar<signed char, false, false>",
+                     "void ut::k_gp_kstar<signed char, true, false>"), "split_u8": ("ut::k_q_split_u(",),
            "kstar": ("void ut::k_gp_kstar<double, false, false>", "void ut::k_gp_kstar<double, false>"), "inner_pairs": ("ut::k_inner_pairs",),
            "encode": ("ut::k_encode_scaled",),
            "hash": ("void ut::k_hash<true", "void ut::k_hash<", "ut::k_hash("), "propose": ("void ut::k_de<", "ut::k_de("),

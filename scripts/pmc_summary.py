@@ -33,14 +33,16 @@ STAGES = {  # stage key -> kernel-name prefixes (the first match wins)
     # rocprofv3 leaves the _Float16 instantiations mangled
     "var16": ("_ZN2ut11k_gp_var_h3",), "kstar16": ("_ZN2ut10k_gp_kstarIDF16_",),
     # precision 8 (int8 slices)
-    "var8": ("ut::k_gp_var_i8(",), "kstar8": ("void ut::k_gp_kstar<signed char, false, false>", "void ut::k_gp_kstar<signed char, true, false>"),
+    "var8": ("ut::k_gp_var_i8(",), "kstar8": ("void ut::k_gp_kstar_q<signed char, false", "void ut::k_gp_kstar<signed char, false, false>",
+                     "void ut::k_gp_kstar<signed char, true, false>"), "split_u8": ("ut::k_q_split_u(",),
     "split8": ("ut::k_split_i8(",), "finalize8": ("ut::k_gp_finalize_i8(",),
     "inner_pairs": ("ut::k_inner_pairs",), "de_diff": ("ut::k_de_diff",), "pop_digests": ("ut::k_pop_digests",),
 }
 # stages of the default C2 round that a refreshed C2 profile replaces (a key
 # absent from the new profile -- e.g. de_diff, now folded into k_de -- is dropped)
 C2_ROUND = ("var", "var_1wg", "kstar", "hash", "propose", "encode", "prep_cand", "finalize", "dedup_insert",
-            "dedup_mark", "topk0", "topk1", "inner_pairs", "de_diff", "pop_digests", "var8", "kstar8", "split8", "finalize8")
+            "dedup_mark", "topk0", "topk1", "inner_pairs", "de_diff", "pop_digests", "var8", "kstar8", "split8", "finalize8",
+            "split_u8")
 
 
 

@@ -26,7 +26,7 @@ HOSTLIB = os.path.join(HERE, "libuthot_hostcheck.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("UT_OFFLOAD_ARCH", "gfx950")
 
-SOURCES = ["api.hip", "propose.hip", "hash.hip", "dedup.hip", "gp.hip", "gp_gemm.hip", "gp_i8.hip", "topk.hip", "forest.hip", "comm.hip"]
+SOURCES = ["api.hip", "propose.hip", "hash.hip", "dedup.hip", "gp.hip", "gp_gemm.hip", "gp_i8.hip", "gp_kq.hip", "topk.hip", "forest.hip", "comm.hip"]
 HEADERS = ["ut_core.h", "ut_internal.h", "ut_param.h", "ut_perm.h", "ryu_tables.h", "libm_log_data.h", os.path.join("..", "..", "include", "uthot.h")]
 
 # RCCL for the multi-GPU exchange (comm.hip); the soname (librccl.so.1) is the

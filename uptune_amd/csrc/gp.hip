@@ -1035,6 +1035,11 @@ static int fit_device(ut_ctx* c, int part, int32_t n, int32_t n0, int32_t d, int
                          dX, n, d, npad, c->gp_acat.p);
       UT_LAUNCH_CHECK(c);
     }
+    // precision 8: K*'s training operand as int8 digit planes (gp_kq.hip)
+    if (c->gp_prec == 8 && c->kstar_q) {
+      if ((rc = launch_split_x8(c, c->gp_XsT, kstar_dpad(d), npad, false))) return rc;
+      if (c->cat_on && (rc = launch_split_x8(c, c->gp_XsT_num.p, dpn, npad, true))) return rc;
+    }
     return 0;
   }
   if (app) {
@@ -1235,6 +1240,10 @@ int gp_fit_enqueue(ut_ctx* c, const double* X, const double* y, int32_t n, int32
   if (c->gp_prec == 8) {
     if ((rc = alloc_split_i8(c, npad))) return rc;
     c->gp_i8_eb = i8_kstar_exp(h->sigma_f2);
+    if (c->kstar_q) {
+      if ((rc = alloc_split_x8(c, npad, kstar_dpad(d), false))) return rc;
+      if (c->cat_on && (rc = alloc_split_x8(c, npad, dpn, true))) return rc;
+    }
   }
   c->gp_n = n;
   c->gp_sf2 = h->sigma_f2;
@@ -1386,10 +1395,18 @@ int gp_score_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, const ut
     c->ucand_cat = false;
     mark(c, "cnorm");
   }
-  if ((rc = launch_gemm_kstar(c, prec, cat ? c->gp_XsT_num.p : c->gp_XsT, npad, c->ucand.p, dpad, m, c->kst.p, ldk,
-                              kmu ? c->mu_part.p : nullptr, -1, nullptr, nullptr,
-                              cat ? kstar_cat(c, c->bcat.p) : KstarCat(), cat ? c->gp_xnorm_num.p : nullptr)))
+  if (i8 && c->kstar_q && c->gp_x8.p) {
+    // the distance contraction on the int8 MFMA (gp_kq.hip): beside the round's
+    // hash its MFMAs issue under the hash's integer VALU work
+    if ((rc = launch_gemm_kstar_q(c, true, cat ? c->gp_XsT_num.p : c->gp_XsT, npad, c->ucand.p, dpad, m, c->kst.p,
+                                  ldk, nullptr, -1, nullptr, nullptr, cat ? kstar_cat(c, c->bcat.p) : KstarCat(),
+                                  cat ? c->gp_xnorm_num.p : nullptr, c->u8, c->scol)))
+      return rc;
+  } else if ((rc = launch_gemm_kstar(c, prec, cat ? c->gp_XsT_num.p : c->gp_XsT, npad, c->ucand.p, dpad, m, c->kst.p,
+                                     ldk, kmu ? c->mu_part.p : nullptr, -1, nullptr, nullptr,
+                                     cat ? kstar_cat(c, c->bcat.p) : KstarCat(), cat ? c->gp_xnorm_num.p : nullptr))) {
     return rc;
+  }
   mark(c, "kstar");
   if (c->fit_pending && !kmu) UT_HIP(c, hipStreamWaitEvent(c->stream, c->ev_fit, 0));
   // fp64 / fp32 / h3: the variance GEMM runs alone, the side stream's hash +
@@ -1400,7 +1417,7 @@ int gp_score_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, const ut
   // 19.36 at ell 2, C3 / C4 unchanged (their hash ends before K*;
   // scripts/ab/r06_varjoin*.sh, r06_sched.sh)
   if (dup_ready && !i8) UT_HIP(c, hipStreamWaitEvent(c->stream, dup_ready, 0));
-  mark(c, "");  // the wait for the fit is not variance time
+  mark(c, "var_wait");  // the wait for the fit (and the dup mask) is not variance time
   if (i8) {
     if ((rc = launch_gemm_var_i8(c, npad, reinterpret_cast<const int8_t*>(c->kst.p), ldk, m, c->var_part.p,
                                  c->mu_part.p)))

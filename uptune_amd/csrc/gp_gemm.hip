@@ -60,35 +60,7 @@ __device__ __forceinline__ int64_t h3_blk_off(int64_t r, int32_t k, int32_t K) {
 }
   // CUs left to an in-flight GP fit (launch_gemm_kstar)
 
-// sf2 * exp(x) for x <= 0, table-driven: etab[j] = sf2 * 2^(j/256) built in LDS by
-// each workgroup (2 KiB); about 12 VALU ops against ~32 for the library exp with
-// its range checks (the epilogue shares the SIMDs with the f64 MFMAs, so every
-// op counts; a 32-entry table with a degree-6 polynomial took two more FMAs).
-// Max error ~2 ulp; 2^k' underflows to exactly 0 at x = -1000.
-constexpr int EXP_TAB = 256;
-
-// The K* contraction works in units of 2^(1/256): its training operand is
-// Xs^T * (256 / ln 2) (KSTAR_T_SCALE, applied where Xs^T is built, k_gp_xs_t /
-// k_gp_num_train), the epilogue's norms and categorical coefficients carry the
-// same factor, so the accumulator is t = -|x - u|^2 / 2 * 256 / ln 2 directly
-// and the exp needs no multiply and no two-step reduction: t = 256 k' + j + f
-// with kf = rint(t), f = t - kf exact (|f| <= 1/2), and
-// exp = 2^k' * 2^(j/256) * e^(f ln2/256) with the same degree-4 polynomial
-// (|f ln2/256| <= 1.36e-3: truncation < 4e-17).  Two DP ops fewer per k*
-// than sf2_exp_nonpos, whose rounding it shares to ~1 ulp.
-__device__ __forceinline__ double sf2_exp2t_nonpos(double t, const double* etab) {
-  constexpr double L = 0.6931471805599453 / 256.0;    // ln 2 / 256 (exact: a power-of-two division)
-  constexpr double C2 = L * L / 2.0, C3 = L * L * L / 6.0, C4 = L * L * L * L / 24.0;
-  const double kf = __builtin_rint(t);
-  const double f = t - kf;
-  double p = __builtin_fma(C4, f, C3);
-  p = __builtin_fma(p, f, C2);
-  p = __builtin_fma(p, f, L);
-  p = __builtin_fma(p, f, 1.0);
-  const int k = (int)kf;
-  return __builtin_ldexp(p * etab[k & (EXP_TAB - 1)], k >> 8);
-}
-constexpr double KSTAR_T_MIN = -1000.0 * KSTAR_T_SCALE;   // exp(-1000): the table's 2^k' underflows to 0
+// (sf2_exp2t_nonpos, EXP_TAB, KSTAR_T_MIN: ut_internal.h)
 
 constexpr int K_SA = K_BK * K_BM, K_SB = K_BK * K_BN, K_STAGE = K_SA + K_SB;
 

@@ -38,9 +38,6 @@
 
 namespace ut {
 
-typedef int32_t i8v4 __attribute__((ext_vector_type(4)));
-typedef int32_t i8v16 __attribute__((ext_vector_type(16)));
-
 constexpr int I8_PL = I8_BM * I8_BK;   // one plane's piece of a stage: 64 rows x 32 k = 2 KiB
 constexpr double I8_C = 3.5 * 0x1p-49;
 

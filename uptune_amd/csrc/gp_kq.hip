@@ -1,13 +1,9 @@
-// MEASURED, NOT KEPT (round 5): K* of a precision-8 fit with the distance
-// contraction on the int8 MFMA.  This is the last version measured (it was
-// wired into libuthot through launch_gemm_kstar for precision-8 fits; the first
-// version is in git history, commit 01cd36a); it is kept here as the record of
-// the experiment ("Round 5: an int8 distance contraction for
-// K*") and is not built.  C2: K* 2.6-2.7 ms + 0.33 ms candidate split against
-// 3.1-3.3 ms for k_gp_kstar<int8_t>; the round did not move (17.1-17.2 ms
-// against 17.0); C3 pruned K* 25.6 ms against 20.1 (fp64 MFMA).
 // gp_kq.hip -- K* for precision-8 fits: the distance contraction on the int8
 // MFMA ("Ozaki" digits, exact int32 sums), the exp epilogue on the VALU beside it.
+// (Round 5 measured it alone: 2.6-2.7 + 0.33 ms against 3.1-3.3 for
+// k_gp_kstar<int8_t>, and did not keep it; round 6 runs it beside the round's
+// hash, which is integer VALU work the int8 MFMA issues beside, where the f64
+// MFMA does not.  UT_KSTAR_Q=0 keeps k_gp_kstar<int8_t>.)
 //
 // k_gp_kstar (gp_gemm.hip) contracts C = Xs U' on the fp64 MFMA, and on gfx950
 // an f64 MFMA holds its SIMD's VALU issue for its whole duration: the exp
@@ -497,7 +493,6 @@ int launch_gemm_kstar_q(ut_ctx* c, bool planes, const double* XsT, int32_t npad,
   UT_CHECK(c, xd.p && xd.n >= (size_t)I8_S * K32 * 32 * npad, UT_EINVAL,
            "gemm_kstar_q: the fit has no training digit planes");
   UT_CHECK(c, !has_cat || (cat.acat && cat.bcat), UT_EINVAL, "gemm_kstar_q: categorical operands missing");
-  UT_CHECK(c, part != nullptr || !planes, UT_EINVAL, "gemm_kstar_q: the digit planes come with the mean partial");
   UT_CHECK(c, K32 + cat.nkc >= 1, UT_EINVAL, "gemm_kstar_q: no features");
   int rc;
   if ((rc = ensure(c, u8, (size_t)I8_S * (K32 > 0 ? K32 : 1) * 32 * ldk))) return rc;
@@ -531,7 +526,9 @@ int launch_gemm_kstar_q(ut_ctx* c, bool planes, const double* XsT, int32_t npad,
     if (pair) UT_KQ_CAT(TS, MU, true, PART); \
     else UT_KQ_CAT(TS, MU, false, PART);     \
   } while (0)
-  if (planes) UT_KQ_PAIR(int8_t, true, part);
+  // (precision 8 takes the mean from the variance epilogue: planes without it)
+  if (planes && part) UT_KQ_PAIR(int8_t, true, part);
+  else if (planes) UT_KQ_PAIR(int8_t, false, nullptr);
   else if (part) UT_KQ_PAIR(double, true, part);
   else UT_KQ_PAIR(double, false, nullptr);
 #undef UT_KQ_PAIR

@@ -286,6 +286,13 @@ struct ut_ctx {
   // per-row scales 2^(ea_i + eb) [npad] | e_i^2 [npad] | the bound E [1]
   ut::DevBuf<int8_t> gp_i8a;
   ut::DevBuf<double> gp_i8rs;
+  // precision 8's K* on the int8 MFMA (gp_kq.hip): digit planes of the training
+  // operand (all features / the numeric ones of a categorical fit) and
+  // [amax, ea] of each; the round's candidate planes and column scales
+  ut::DevBuf<int8_t> gp_x8, gp_x8n, u8;
+  ut::DevBuf<int64_t> gp_q8;
+  ut::DevBuf<double> scol;
+  int32_t kstar_q = 1;   // UT_KSTAR_Q=0: precision-8 K* on k_gp_kstar<int8_t> (the fp64 MFMA)
   int32_t gp_i8_eb = 0;          // K* digit scale: y = k* 2^-eb <= 0.49
   double i8_tol = 0x1p-20;       // accepted relative variance error (ut_gp_set_i8_tol)
   int64_t i8_recomputed = 0;     // candidates of the last score recomputed in fp64 (-1: all, dense)
@@ -520,8 +527,37 @@ constexpr int H3_KSCALE_EXP = 14;  // K* (<= sf2) is scaled by 2^(14 - ceil(log2
 int h3_kstar_exp(double sf2);
 // K*'s training operand (Xs^T, the numeric part in categorical mode) is stored
 // times 256 / ln 2: the contraction then yields the exponent in 2^(1/256) units
-// (gp_gemm.hip sf2_exp2t_nonpos)
+// (sf2_exp2t_nonpos below)
 constexpr double KSTAR_T_SCALE = 369.3299304675746;   // 256 / ln 2
+// sf2 * exp(x) for x <= 0, table-driven: etab[j] = sf2 * 2^(j/256) built in LDS by
+// each workgroup (2 KiB); about 12 VALU ops against ~32 for the library exp with
+// its range checks (the epilogue shares the SIMDs with the f64 MFMAs, so every
+// op counts; a 32-entry table with a degree-6 polynomial took two more FMAs).
+// Max error ~2 ulp; 2^k' underflows to exactly 0 at x = -1000.
+constexpr int EXP_TAB = 256;
+
+// The K* contraction works in units of 2^(1/256): its training operand is
+// Xs^T * (256 / ln 2) (KSTAR_T_SCALE, applied where Xs^T is built, k_gp_xs_t /
+// k_gp_num_train), the epilogue's norms and categorical coefficients carry the
+// same factor, so the accumulator is t = -|x - u|^2 / 2 * 256 / ln 2 directly
+// and the exp needs no multiply and no two-step reduction: t = 256 k' + j + f
+// with kf = rint(t), f = t - kf exact (|f| <= 1/2), and
+// exp = 2^k' * 2^(j/256) * e^(f ln2/256) with the same degree-4 polynomial
+// (|f ln2/256| <= 1.36e-3: truncation < 4e-17).  Two DP ops fewer per k*
+// than sf2_exp_nonpos, whose rounding it shares to ~1 ulp.
+__device__ __forceinline__ double sf2_exp2t_nonpos(double t, const double* etab) {
+  constexpr double L = 0.6931471805599453 / 256.0;    // ln 2 / 256 (exact: a power-of-two division)
+  constexpr double C2 = L * L / 2.0, C3 = L * L * L / 6.0, C4 = L * L * L * L / 24.0;
+  const double kf = __builtin_rint(t);
+  const double f = t - kf;
+  double p = __builtin_fma(C4, f, C3);
+  p = __builtin_fma(p, f, C2);
+  p = __builtin_fma(p, f, L);
+  p = __builtin_fma(p, f, 1.0);
+  const int k = (int)kf;
+  return __builtin_ldexp(p * etab[k & (EXP_TAB - 1)], k >> 8);
+}
+constexpr double KSTAR_T_MIN = -1000.0 * KSTAR_T_SCALE;   // exp(-1000): the table's 2^k' underflows to 0
 // the K* contraction's categorical operands (nkc = cat_k / 128 int8 stages; 0 = none)
 struct KstarCat {
   const int8_t* acat = nullptr;
@@ -536,6 +572,17 @@ int launch_gemm_kstar(ut_ctx* c, int prec, const double* XsT, int32_t npad, cons
                       const KstarCat& cat = KstarCat(),
                       const double* xn = nullptr,    // training norms (nullptr: c->gp_xnorm)
                       int32_t row_tiles = -1);       // > 0: only the first row_tiles 128-row tiles
+// gp_kq.hip: K* of a precision-8 fit as the distance contraction on the int8
+// MFMA (digit planes of the training operand from the fit, of the candidates'
+// operand per call into u8 / scol); planes = true: K* as six digit planes for
+// the int8 variance (with the mean partial if part), else fp64 rows.  Mean
+// partials come per 64-row tile (npad / 64 of them).
+int alloc_split_x8(ut_ctx* c, int32_t npad, int32_t K, bool num);
+int launch_split_x8(ut_ctx* c, const double* XsT, int32_t K, int32_t npad, bool num);
+int launch_gemm_kstar_q(ut_ctx* c, bool planes, const double* XsT, int32_t npad, const double* ucand, int32_t dpad,
+                        int64_t m, void* kst, int64_t ldk, double* part, int32_t store_rows, const double* cn,
+                        double* part2, const KstarCat& cat, const double* xn, DevBuf<int8_t>& u8,
+                        DevBuf<double>& scol);
 int launch_gemm_kstar_f32c(ut_ctx* c, const float* XsT_f, int32_t npad, const float* ucand_f, int32_t dpad,
                            int64_t m, int64_t ldk, int32_t rt0, double* part, double* part2, double* part3,
                            const KstarCat& cat, const double* xn, const double* cn);
@@ -606,6 +653,8 @@ __device__ __forceinline__ uint64_t i8_biased(double x) {
 // (byte u of plane p's dword = digit p of value u; plane 0 = most significant):
 // a 4 x 4 byte transpose by v_perm_b32 (byte j of perm(a, b, s) is byte
 // s_j of the pair, 0..3 = b, 4..7 = a)
+typedef int32_t i8v4 __attribute__((ext_vector_type(4)));
+typedef int32_t i8v16 __attribute__((ext_vector_type(16)));
 __device__ __forceinline__ void i8_planes(const uint32_t (&lo)[4], const uint32_t (&hi)[4], uint32_t (&pl)[I8_S]) {
   const uint32_t t0 = __builtin_amdgcn_perm(lo[1], lo[0], 0x05010400u);   // w0.b0 w1.b0 w0.b1 w1.b1
   const uint32_t t1 = __builtin_amdgcn_perm(lo[1], lo[0], 0x07030602u);   // w0.b2 w1.b2 w0.b3 w1.b3
