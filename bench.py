@@ -229,7 +229,9 @@ def kernel_table(m, n, d, outer_blocks, prec=64, suffix=""):
         if t <= 0:
             return
         out[key] = {"bound": "mfma", "ms": t * 1e3, "achieved_TFps": flops / t / 1e12,
-                    "frac": flops / t / 1e12 / peak, "peak_TFps": peak, "flops": flops, "traffic_bytes": traffic}
+                    "frac": flops / t / 1e12 / peak, "peak_TFps": peak, "flops": flops, "traffic_bytes": traffic,
+                    # (K* at precision 8 stores six digit planes per k*: 6 n B per candidate)
+                    "traffic_frac_of_hbm_peak": (traffic / t / 1e9 / PEAK_HBM_GBS) if traffic else None}
 
     hbm("propose", 40.0 * d * m)
     hbm("encode", 16.0 * d * m)
