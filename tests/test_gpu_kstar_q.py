@@ -2,9 +2,10 @@
 the default) against k_gp_kstar<int8_t> on the fp64 MFMA (UT_KSTAR_Q=0): both
 are the fp64 tier (the int8 contraction's digit rounding is below the fp64
 contraction's own, gp_kq.hip), so every candidate's mean and variance agree to
-1e-9 relative (1e-10 absolute) and the dense rounds select the same candidates, over a numeric
-and a categorical space and the padded sizes 1024 / 2048 (sf2 far from 1 too:
-the round-5 fault case, npad 2048 and sf2 1e-3).  Both are held to
+1e-9 relative (1e-10 absolute) and the dense rounds select the same
+candidates, at the padded sizes 1024 / 2048 (sf2 far from 1 too: the round-5
+fault case, npad 2048 and sf2 1e-3).  A categorical fit keeps the fp64-MFMA K*
+(bit-identical with and without UT_KSTAR_Q).  Both are held to
 oracle/gp.py by test_gpu_i8.py / test_gpu_parity.py."""
 import ctypes
 import os
@@ -70,6 +71,11 @@ def test_kstar_q_equals_fp64_kstar(monkeypatch, which, n, sf2, ell):
     a = _round(monkeypatch, space, True, n, sf2, ell)
     b = _round(monkeypatch, space, False, n, sf2, ell)
     assert a[5] == b[5] == ("dense" if which == "r64" else "categorical")
+    if which == "cat":
+        # categorical fits keep the fp64-MFMA K* (gp.hip gp_score_impl): the same kernels
+        for x, y in zip(a[:5], b[:5]):
+            np.testing.assert_array_equal(x, y)
+        return
     # (the two contractions round differently at ~1e-12 of the operands' scale;
     # the tier's bound on the mean is E_mu ~1e-7, on the variance tau = 2^-20)
     np.testing.assert_allclose(a[2], b[2], rtol=1e-9, atol=1e-10)          # mean

@@ -300,7 +300,7 @@ int ut_ctx_destroy(ut_ctx* c) {
   fr(c->gp_LinvT); fr(c->gp_LinvT_f); fr(c->gp_ctr); fr(c->gp_XsT); fr(c->ucand.p);
   fr(c->gp_XsT_num.p); fr(c->gp_xnorm_num.p); fr(c->gp_acat.p); fr(c->bcat.p); fr(c->pr_bcat.p);
   fr(c->gp_i8a.p); fr(c->gp_i8rs.p);
-  fr(c->gp_x8.p); fr(c->gp_x8n.p); fr(c->u8.p); fr(c->gp_q8.p); fr(c->scol.p);
+  fr(c->gp_x8.p); fr(c->u8.p); fr(c->gp_q8.p); fr(c->scol.p);
   fr(c->kst.p); fr(c->mu_part.p); fr(c->var_part.p); fr(c->cnorm.p);
   fr(c->r_values.p); fr(c->r_feat.p); fr(c->r_mu.p); fr(c->r_var.p); fr(c->r_score.p); fr(c->r_digest.p);
   fr(c->r_dup.p); fr(c->tk_score[0].p); fr(c->tk_score[1].p); fr(c->tk_idx[0].p); fr(c->tk_idx[1].p);

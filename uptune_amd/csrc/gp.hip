@@ -1035,11 +1035,11 @@ static int fit_device(ut_ctx* c, int part, int32_t n, int32_t n0, int32_t d, int
                          dX, n, d, npad, c->gp_acat.p);
       UT_LAUNCH_CHECK(c);
     }
-    // precision 8: K*'s training operand as int8 digit planes (gp_kq.hip)
-    if (c->gp_prec == 8 && c->kstar_q) {
-      if ((rc = launch_split_x8(c, c->gp_XsT, kstar_dpad(d), npad, false))) return rc;
-      if (c->cat_on && (rc = launch_split_x8(c, c->gp_XsT_num.p, dpn, npad, true))) return rc;
-    }
+    // precision 8: K*'s training operand as int8 digit planes (gp_kq.hip;
+    // numeric fits only, gp_score_impl)
+    if (c->gp_prec == 8 && c->kstar_q && !c->cat_on &&
+        (rc = launch_split_x8(c, c->gp_XsT, kstar_dpad(d), npad)))
+      return rc;
     return 0;
   }
   if (app) {
@@ -1240,10 +1240,7 @@ int gp_fit_enqueue(ut_ctx* c, const double* X, const double* y, int32_t n, int32
   if (c->gp_prec == 8) {
     if ((rc = alloc_split_i8(c, npad))) return rc;
     c->gp_i8_eb = i8_kstar_exp(h->sigma_f2);
-    if (c->kstar_q) {
-      if ((rc = alloc_split_x8(c, npad, kstar_dpad(d), false))) return rc;
-      if (c->cat_on && (rc = alloc_split_x8(c, npad, dpn, true))) return rc;
-    }
+    if (c->kstar_q && !c->cat_on && (rc = alloc_split_x8(c, npad, kstar_dpad(d)))) return rc;
   }
   c->gp_n = n;
   c->gp_sf2 = h->sigma_f2;
@@ -1395,12 +1392,13 @@ int gp_score_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, const ut
     c->ucand_cat = false;
     mark(c, "cnorm");
   }
-  if (i8 && c->kstar_q && c->gp_x8.p) {
+  if (i8 && c->kstar_q && !c->cat_on && c->gp_x8.p) {
     // the distance contraction on the int8 MFMA (gp_kq.hip): beside the round's
-    // hash its MFMAs issue under the hash's integer VALU work
-    if ((rc = launch_gemm_kstar_q(c, true, cat ? c->gp_XsT_num.p : c->gp_XsT, npad, c->ucand.p, dpad, m, c->kst.p,
-                                  ldk, nullptr, -1, nullptr, nullptr, cat ? kstar_cat(c, c->bcat.p) : KstarCat(),
-                                  cat ? c->gp_xnorm_num.p : nullptr, c->u8, c->scol)))
+    // hash its MFMAs issue under the hash's integer VALU work (C2 ~1 % per
+    // round).  Categorical fits keep the fp64-MFMA K* (C3 HPL-64: K* 43 against
+    // 28.5 ms, the round 288 against 270; C4 no better; scripts/r06_lines.sh)
+    if ((rc = launch_gemm_kstar_q(c, true, c->gp_XsT, npad, c->ucand.p, dpad, m, c->kst.p, ldk, nullptr, -1, nullptr,
+                                  nullptr, KstarCat(), nullptr, c->u8, c->scol)))
       return rc;
   } else if ((rc = launch_gemm_kstar(c, prec, cat ? c->gp_XsT_num.p : c->gp_XsT, npad, c->ucand.p, dpad, m, c->kst.p,
                                      ldk, kmu ? c->mu_part.p : nullptr, -1, nullptr, nullptr,

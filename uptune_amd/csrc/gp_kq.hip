@@ -3,7 +3,10 @@
 // (Round 5 measured it alone: 2.6-2.7 + 0.33 ms against 3.1-3.3 for
 // k_gp_kstar<int8_t>, and did not keep it; round 6 runs it beside the round's
 // hash, which is integer VALU work the int8 MFMA issues beside, where the f64
-// MFMA does not.  UT_KSTAR_Q=0 keeps k_gp_kstar<int8_t>.)
+// MFMA does not: C2 ~1 % per round.  Numeric fits only -- at C3's categorical
+// HPL-64 fit it was 43 against 28.5 ms of K* -- and only the digit-plane
+// variant without the mean (the variance epilogue has it) is instantiated.
+// UT_KSTAR_Q=0 keeps k_gp_kstar<int8_t>.)
 //
 // k_gp_kstar (gp_gemm.hip) contracts C = Xs U' on the fp64 MFMA, and on gfx950
 // an f64 MFMA holds its SIMD's VALU issue for its whole duration: the exp
@@ -26,15 +29,16 @@
 // operand's scale) and the dropped pairs p + q >= 8 leave |C - C^| below
 // 2^-46 K 2^(ea + eb_c) -- the size of the fp64 contraction's own rounding
 // (K 2^-53 |x| |u|), so k* = sf2 exp2((C - |x|^2/2 - |u|^2/2) / 256) keeps the
-// fp64 tier's accuracy.  The epilogue is k_gp_kstar's: exp, mean partial
-// sum_r alpha_r k*_r, and K* as six digit planes for the int8 variance (TS =
-// int8_t) or fp64 rows (TS = double: the fp64 recompute and pruned scoring of a
-// precision-8 fit); the categorical codes (ENUM / BOOL one-hot blocks) go
-// through the same MFMA as an int32 match count.
+// fp64 tier's accuracy.  The epilogue is k_gp_kstar's: exp and K* as six
+// digit planes for the int8 variance (TS = int8_t).  The template also holds
+// the round-5 variants (MU: the mean partial sum_r alpha_r k*_r; TS = double:
+// fp64 rows; CAT: the ENUM / BOOL one-hot blocks through the same MFMA as an
+// int32 match count), which the library no longer instantiates.
 //
 // Tiles: 64 training rows x 64 candidates per 256-thread workgroup, two per
 // CU; waves 2 x 2 of 32 x 32 (one MFMA output tile, six group accumulators);
-// stages of 32 k: 6 A + 6 B planes of 2 KiB each, a 2-stage glds ring.
+// stages of 32 k: 6 A + 6 B planes of 2 KiB each in a 3-slot glds ring; each
+// XCD's items dealt round-robin to its workgroups (no ticket atomics).
 #include "ut_internal.h"
 
 namespace ut {
@@ -456,24 +460,24 @@ __global__ __launch_bounds__(Q_NT, 2) void k_gp_kstar_q(
 }
 
 // ---------------------------------------------------------------------------
-int alloc_split_x8(ut_ctx* c, int32_t npad, int32_t K, bool num) {
+int alloc_split_x8(ut_ctx* c, int32_t npad, int32_t K) {
   int rc;
   const int32_t K32 = (K + 31) / 32;
-  if ((rc = ensure(c, num ? c->gp_x8n : c->gp_x8, (size_t)I8_S * (K32 > 0 ? K32 : 1) * 32 * npad))) return rc;
-  return ensure(c, c->gp_q8, 4);
+  if ((rc = ensure(c, c->gp_x8, (size_t)I8_S * (K32 > 0 ? K32 : 1) * 32 * npad))) return rc;
+  return ensure(c, c->gp_q8, 2);
 }
 
-int launch_split_x8(ut_ctx* c, const double* XsT, int32_t K, int32_t npad, bool num) {
+int launch_split_x8(ut_ctx* c, const double* XsT, int32_t K, int32_t npad) {
   const int32_t K32 = (K + 31) / 32;
-  DevBuf<int8_t>& xd = num ? c->gp_x8n : c->gp_x8;
-  UT_CHECK(c, xd.n >= (size_t)I8_S * K32 * 32 * npad && c->gp_q8.n >= 4, UT_EINVAL,
+  DevBuf<int8_t>& xd = c->gp_x8;
+  UT_CHECK(c, xd.n >= (size_t)I8_S * K32 * 32 * npad && c->gp_q8.n >= 2, UT_EINVAL,
            "split_x8: planes not allocated (alloc_split_x8)");
-  unsigned long long* amax = reinterpret_cast<unsigned long long*>(c->gp_q8.p + (num ? 2 : 0));
+  unsigned long long* amax = reinterpret_cast<unsigned long long*>(c->gp_q8.p);
   UT_HIP(c, hipMemsetAsync(amax, 0, sizeof(unsigned long long), c->stream));
   if (K > 0)
     hipLaunchKernelGGL(k_q_absmax, dim3(256), dim3(256), 0, c->stream, XsT, (int64_t)K * npad, amax);
   hipLaunchKernelGGL(k_q_split_x, dim3(grid1(npad, 256)), dim3(256), 0, c->stream, XsT, K, npad, K32, amax, xd.p,
-                     c->gp_q8.p + (num ? 3 : 1));
+                     c->gp_q8.p + 1);
   UT_LAUNCH_CHECK(c);
   return 0;
 }
@@ -482,8 +486,7 @@ int launch_gemm_kstar_q(ut_ctx* c, bool planes, const double* XsT, int32_t npad,
                         int64_t m, void* kst, int64_t ldk, double* part, int32_t store_rows, const double* cn,
                         double* part2, const KstarCat& cat, const double* xn, DevBuf<int8_t>& u8,
                         DevBuf<double>& scol) {
-  const bool num = XsT == c->gp_XsT_num.p && XsT != nullptr;
-  const DevBuf<int8_t>& xd = num ? c->gp_x8n : c->gp_x8;
+  const DevBuf<int8_t>& xd = c->gp_x8;
   const int32_t K32 = (dpad + 31) / 32;
   const bool pair = K32 * 32 <= Q_PAIR_MAX_K;
   const bool has_cat = cat.nkc > 0;
@@ -494,11 +497,15 @@ int launch_gemm_kstar_q(ut_ctx* c, bool planes, const double* XsT, int32_t npad,
            "gemm_kstar_q: the fit has no training digit planes");
   UT_CHECK(c, !has_cat || (cat.acat && cat.bcat), UT_EINVAL, "gemm_kstar_q: categorical operands missing");
   UT_CHECK(c, K32 + cat.nkc >= 1, UT_EINVAL, "gemm_kstar_q: no features");
+  // the library runs it for the variance's digit planes of numeric fits (the
+  // mean from the variance epilogue, no one-hot codes: gp.hip gp_score_impl)
+  UT_CHECK(c, planes && !part && !part2 && !has_cat && XsT == c->gp_XsT, UT_EINVAL,
+           "gemm_kstar_q: digit planes of a numeric fit only");
   int rc;
   if ((rc = ensure(c, u8, (size_t)I8_S * (K32 > 0 ? K32 : 1) * 32 * ldk))) return rc;
   if ((rc = ensure(c, scol, (size_t)ldk))) return rc;
   hipLaunchKernelGGL(k_q_split_u, dim3(grid1(ldk, 256)), dim3(256), 0, c->stream, ucand, dpad, ldk, K32,
-                     c->gp_q8.p + (num ? 3 : 1), pair ? -24 : -16, u8.p, scol.p);
+                     c->gp_q8.p + 1, pair ? -24 : -16, u8.p, scol.p);
   UT_LAUNCH_CHECK(c);
   const int32_t RT = npad / Q_BM;
   const int32_t CT = (int32_t)(ldk / Q_BN);
@@ -511,28 +518,13 @@ int launch_gemm_kstar_q(ut_ctx* c, bool planes, const double* XsT, int32_t npad,
   const double* xnorm = xn ? xn : c->gp_xnorm;
   const double* cnorm = cn ? cn : c->cnorm.p;
   const double kscale = planes ? ldexp(1.0, -i8_kstar_exp(c->gp_sf2)) : 1.0;
-#define UT_KQ_LAUNCH(TS, MU, CAT, PAIR, PART)                                                                     \
-  hipLaunchKernelGGL((k_gp_kstar_q<TS, MU, CAT, PAIR>), dim3(nb), dim3(Q_NT), 0, c->stream, xd.p, npad, u8.p, ldk, \
-                     K32, scol.p, RT, CT, xnorm, cnorm, c->gp_alpha, c->gp_sf2, c->gp_n, m, (TS*)kst, PART,         \
-                     kscale, (int64_t)npad * ldk, store_rt, part2, cat.acat, cat.bcat, cat.nkc,    \
+#define UT_KQ_LAUNCH(PAIR)                                                                                     \
+  hipLaunchKernelGGL((k_gp_kstar_q<int8_t, false, false, PAIR>), dim3(nb), dim3(Q_NT), 0, c->stream, xd.p, npad,    \
+                     u8.p, ldk, K32, scol.p, RT, CT, xnorm, cnorm, c->gp_alpha, c->gp_sf2, c->gp_n, m, (int8_t*)kst, \
+                     nullptr, kscale, (int64_t)npad * ldk, store_rt, nullptr, cat.acat, cat.bcat, cat.nkc,         \
                      cat.c0 * KSTAR_T_SCALE, cat.c1 * KSTAR_T_SCALE)
-#define UT_KQ_CAT(TS, MU, PAIR, PART)                    \
-  do {                                                   \
-    if (has_cat) UT_KQ_LAUNCH(TS, MU, true, PAIR, PART); \
-    else UT_KQ_LAUNCH(TS, MU, false, PAIR, PART);        \
-  } while (0)
-#define UT_KQ_PAIR(TS, MU, PART)             \
-  do {                                       \
-    if (pair) UT_KQ_CAT(TS, MU, true, PART); \
-    else UT_KQ_CAT(TS, MU, false, PART);     \
-  } while (0)
-  // (precision 8 takes the mean from the variance epilogue: planes without it)
-  if (planes && part) UT_KQ_PAIR(int8_t, true, part);
-  else if (planes) UT_KQ_PAIR(int8_t, false, nullptr);
-  else if (part) UT_KQ_PAIR(double, true, part);
-  else UT_KQ_PAIR(double, false, nullptr);
-#undef UT_KQ_PAIR
-#undef UT_KQ_CAT
+  if (pair) UT_KQ_LAUNCH(true);
+  else UT_KQ_LAUNCH(false);
 #undef UT_KQ_LAUNCH
   UT_LAUNCH_CHECK(c);
   return 0;

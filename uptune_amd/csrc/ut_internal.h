@@ -286,10 +286,10 @@ struct ut_ctx {
   // per-row scales 2^(ea_i + eb) [npad] | e_i^2 [npad] | the bound E [1]
   ut::DevBuf<int8_t> gp_i8a;
   ut::DevBuf<double> gp_i8rs;
-  // precision 8's K* on the int8 MFMA (gp_kq.hip): digit planes of the training
-  // operand (all features / the numeric ones of a categorical fit) and
-  // [amax, ea] of each; the round's candidate planes and column scales
-  ut::DevBuf<int8_t> gp_x8, gp_x8n, u8;
+  // precision 8's K* on the int8 MFMA (gp_kq.hip, numeric fits): digit planes
+  // of the training operand and its [amax, ea]; the round's candidate planes
+  // and column scales
+  ut::DevBuf<int8_t> gp_x8, u8;
   ut::DevBuf<int64_t> gp_q8;
   ut::DevBuf<double> scol;
   int32_t kstar_q = 1;   // UT_KSTAR_Q=0: precision-8 K* on k_gp_kstar<int8_t> (the fp64 MFMA)
@@ -572,13 +572,12 @@ int launch_gemm_kstar(ut_ctx* c, int prec, const double* XsT, int32_t npad, cons
                       const KstarCat& cat = KstarCat(),
                       const double* xn = nullptr,    // training norms (nullptr: c->gp_xnorm)
                       int32_t row_tiles = -1);       // > 0: only the first row_tiles 128-row tiles
-// gp_kq.hip: K* of a precision-8 fit as the distance contraction on the int8
-// MFMA (digit planes of the training operand from the fit, of the candidates'
-// operand per call into u8 / scol); planes = true: K* as six digit planes for
-// the int8 variance (with the mean partial if part), else fp64 rows.  Mean
-// partials come per 64-row tile (npad / 64 of them).
-int alloc_split_x8(ut_ctx* c, int32_t npad, int32_t K, bool num);
-int launch_split_x8(ut_ctx* c, const double* XsT, int32_t K, int32_t npad, bool num);
+// gp_kq.hip: K* of a numeric precision-8 fit as the distance contraction on
+// the int8 MFMA (digit planes of the training operand from the fit, of the
+// candidates' operand per call into u8 / scol), stored as the six digit planes
+// the int8 variance reads (planes = true; no mean partial, no one-hot codes).
+int alloc_split_x8(ut_ctx* c, int32_t npad, int32_t K);
+int launch_split_x8(ut_ctx* c, const double* XsT, int32_t K, int32_t npad);
 int launch_gemm_kstar_q(ut_ctx* c, bool planes, const double* XsT, int32_t npad, const double* ucand, int32_t dpad,
                         int64_t m, void* kst, int64_t ldk, double* part, int32_t store_rows, const double* cn,
                         double* part2, const KstarCat& cat, const double* xn, DevBuf<int8_t>& u8,
