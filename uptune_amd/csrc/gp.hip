@@ -1043,6 +1043,8 @@ static int fit_device(ut_ctx* c, int part, int32_t n, int32_t n0, int32_t d, int
     return 0;
   }
   if (app) {
+    // (the previous precision-8 refit left (L^-1)^T to its readers)
+    if ((rc = gp_ensure_linvt(c))) return rc;
     // block rows b0 .. b1 hold the new rows (b0 may also hold old ones: it is
     // recomputed whole)
     const int32_t b0 = n0 / NB, b1 = (n - 1) / NB;
@@ -1118,6 +1120,15 @@ static int fit_device(ut_ctx* c, int part, int32_t n, int32_t n0, int32_t d, int
                      c->gp_beta);
   UT_LAUNCH_CHECK(c);
   if (c->gp_prec == 32 && (rc = launch_to_f32(c, c->gp_Xs, c->gp_Xs_f, (int64_t)npad * d))) return rc;
+  // precision 8 scores from the digit planes of L^-1 and beta alone: a refit
+  // leaves (L^-1)^T and alpha = L^-T beta to the paths that read them (the fp64
+  // recompute, the next append: gp_ensure_linvt), off the chain the variance
+  // GEMM waits for
+  if (c->gp_prec == 8 && !app) {
+    if ((rc = launch_split_i8(c, n, npad))) return rc;
+    c->gp_linvt_stale = true;
+    return 0;
+  }
   // (an append wrote its rows of LinvT itself)
   if ((!app || c->gp_prec == 32) &&
       (rc = launch_transpose(c, c->gp_Linv, npad, c->gp_LinvT, c->gp_prec == 32 ? c->gp_LinvT_f : nullptr)))
@@ -1125,9 +1136,23 @@ static int fit_device(ut_ctx* c, int part, int32_t n, int32_t n0, int32_t d, int
   hipLaunchKernelGGL(k_upper_mv, dim3(grid1(npad, 4)), dim3(256), 0, c->stream, c->gp_LinvT, npad, c->gp_beta,
                      c->gp_alpha);
   UT_LAUNCH_CHECK(c);
+  c->gp_linvt_stale = false;
   if (c->gp_prec == 16 && (rc = launch_split_h3(c, c->gp_Linv, npad, reinterpret_cast<_Float16*>(c->gp_LinvT_f))))
     return rc;
   if (c->gp_prec == 8 && (rc = launch_split_i8(c, n, npad))) return rc;
+  return 0;
+}
+
+// (L^-1)^T and alpha of a precision-8 refit, on c->stream, once (fit_device)
+int gp_ensure_linvt(ut_ctx* c) {
+  if (!c->gp_linvt_stale) return 0;
+  const int32_t npad = c->gp_npad_fit;
+  int rc;
+  if ((rc = launch_transpose(c, c->gp_Linv, npad, c->gp_LinvT, nullptr))) return rc;
+  hipLaunchKernelGGL(k_upper_mv, dim3(grid1(npad, 4)), dim3(256), 0, c->stream, c->gp_LinvT, npad, c->gp_beta,
+                     c->gp_alpha);
+  UT_LAUNCH_CHECK(c);
+  c->gp_linvt_stale = false;
   return 0;
 }
 
@@ -1440,6 +1465,7 @@ int gp_score_impl(ut_ctx* c, const double* feat, int64_t ld, int64_t m, const ut
     UT_HIP(c, hipMemcpyAsync(&nf, c->pr_count.p, sizeof(int64_t), hipMemcpyDeviceToHost, c->stream));
     UT_HIP(c, hipStreamSynchronize(c->stream));
     c->i8_recomputed = nf;
+    if (nf > 0 && (rc = gp_ensure_linvt(c))) return rc;   // (the fp64 contraction reads (L^-1)^T)
     if (nf * 2 > m) {
       // most candidates need fp64: the whole K* (fp64, over the planes) and the
       // fp64 contraction, with the mean from its epilogue

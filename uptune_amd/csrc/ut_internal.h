@@ -264,6 +264,7 @@ struct ut_ctx {
   int32_t gp_npad_fit = 0;     // padded size of the current factor
   double gp_diag_fit = 0.0;    // its sigma_n2 + jitter
   int32_t gp_fit_kind = 0;     // 0 = the last fit refactored, 1 = it appended rows
+  bool gp_linvt_stale = false; // gp_LinvT / gp_alpha not yet written for the current factor (gp_ensure_linvt)
   int32_t* flag_host = nullptr;  // pinned readback of the previous fit's flag
   float* gp_Xs_f = nullptr;    // fp32 copies for the fp32 MFMA path
   double* gp_LinvT = nullptr;  // (L^-1)^T [k][row]: the A operand of the variance contraction
@@ -460,6 +461,7 @@ void mark(ut_ctx* c, const char* name);
 int gp_fit_enqueue(ut_ctx* c, const double* X, const double* y, int32_t n, int32_t d, const ut_gp_hyper* h);
 int gp_wait_fit(ut_ctx* c);
 int gp_fit_flush(ut_ctx* c);
+int gp_ensure_linvt(ut_ctx* c);
 int gp_fit_prefit(ut_ctx* c);
 
 // kernel launchers implemented in the .hip translation units
